@@ -1,0 +1,19 @@
+"""sfmhip — MI355X-native (gfx950) backend for the dense-compute path of
+daovietanh190499/3D_Reconstruction: BF-L2 descriptor matching + ratio test,
+DLT triangulation, reprojection residual / FD Jacobian, voxel-grid work.
+
+The directory name is not a Python identifier; import it with
+``importlib.import_module("3d_reconstruction_amd")``.
+Every compute entry point runs a HIP kernel from ``libsfmhip.so``; there is no
+CPU fallback.
+"""
+from ._abi import LIB_PATH, SfmHipError, lib, require_gpu  # noqa: F401  (fails loudly if the .so is missing)
+from .match import (MODE_FLOAT, MODE_SIFT, DescriptorBank, Matcher, all_pairs,  # noqa: F401
+                    bf_match, vq)
+from .geometry import (Rodrigues, ba_sparse, calculate_reprojection_error,  # noqa: F401
+                       convertPointsFromHomogeneous, fd_jacobian, projectPoints,
+                       residual_jacobian_batched, triangulatePoints, triangulate_batched)
+from .voxel import (MASK_PLENOXEL, MASK_SDF, VoxelGrid, tsdf_integrate,  # noqa: F401
+                    voxel_traversal)
+
+__version__ = "0.1.0"

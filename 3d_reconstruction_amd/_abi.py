@@ -1,0 +1,118 @@
+"""ctypes binding of ``libsfmhip.so`` (the C-ABI declared in ``include/sfmhip.h``).
+
+This is the only place the package touches native code.  The library is built
+in-tree by ``__graft_entry__.build()`` (``make -C 3d_reconstruction_amd/csrc``)
+and is REQUIRED: importing the package on a machine without it raises, and the
+compute entry points raise when no HIP device is present.  There is no CPU
+fallback anywhere in the product path.
+
+Device memory is handed over as raw pointers (``tensor.data_ptr()``) of
+torch-ROCm tensors; torch is used only as the allocator / stream provider.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsfmhip.so")
+
+SFMHIP_OK = 0
+SFMHIP_E_ARG = -1
+SFMHIP_E_HIP = -2
+SFMHIP_E_UNSUPPORTED = -3
+SFMHIP_E_OVERFLOW = -4
+
+
+class SfmHipError(RuntimeError):
+    """Raised when a libsfmhip call returns a non-zero status."""
+
+    def __init__(self, func: str, code: int, msg: str):
+        super().__init__(f"{func} failed ({code}): {msg}")
+        self.code = code
+
+
+_p = ctypes.c_void_p
+_i32 = ctypes.c_int
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+
+# name -> argtypes, in the order of include/sfmhip.h
+SIGNATURES = {
+    "sfmhip_version": [],
+    "sfmhip_last_error": [],
+    "sfmhip_device_arch": [ctypes.c_char_p, _i32],
+    "sfmhip_desc_quantize": [_p, _i32, _i32, _i32, _p, _i32, _p, _p],
+    "sfmhip_desc_prepare": [_p, _i32, _i32, _i32, _p, _p, _p, _p],
+    "sfmhip_match_pairs": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p],
+    "sfmhip_mutual_filter": [_p, _p, _i32, _i32, _p],
+    "sfmhip_vq": [_p, _i64, _p, _i32, _i32, _p, _p, _p],
+    "sfmhip_triangulate_dlt": [_p, _p, _p, _p, _i64, _p, _p],
+    "sfmhip_reproj_residual": [_p, _p, _p, _p, _p, _i64, _p, _p],
+    "sfmhip_reproj_fd_jacobian": [_p, _p, _p, _p, _p, _i32, _i64, _p, _p, _p, _p],
+    "sfmhip_voxel_traversal_count": [_p, _i64, _f32, _i32, _p, _p],
+    "sfmhip_voxel_traversal": [_p, _i64, _f32, _i32, _p, _p],
+    "sfmhip_grid_sample": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i64, _p, _p],
+    "sfmhip_grid_to_voxel_major": [_p, _i32, _i32, _i32, _i32, _p, _p],
+    "sfmhip_render_rays": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _i64, _i32, _p, _p],
+    "sfmhip_tsdf_integrate": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p,
+                              _f32, _p],
+}
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libsfmhip.so not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (make -C 3d_reconstruction_amd/csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = _i32
+    lib.sfmhip_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+lib = _load()
+
+
+def call(name: str, *args) -> None:
+    """Invoke ``name`` and raise :class:`SfmHipError` on a non-zero status."""
+    rc = getattr(lib, name)(*args)
+    if rc != SFMHIP_OK:
+        msg = lib.sfmhip_last_error().decode(errors="replace")
+        raise SfmHipError(name, rc, msg)
+
+
+def require_gpu() -> torch.device:
+    """The compute path runs only on a HIP device; fail loudly otherwise."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("sfmhip: no HIP device visible — the MI355X kernels cannot run "
+                           "(there is deliberately no CPU fallback)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def dev(x, dtype: torch.dtype) -> torch.Tensor:
+    """numpy / tensor -> contiguous device tensor of ``dtype`` (copy only if needed)."""
+    d = require_gpu()
+    if isinstance(x, torch.Tensor):
+        t = x
+    else:
+        t = torch.as_tensor(x)
+    if t.device != d or t.dtype != dtype:
+        t = t.to(device=d, dtype=dtype)
+    return t.contiguous()

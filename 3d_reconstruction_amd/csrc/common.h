@@ -1,0 +1,53 @@
+// common.h — shared plumbing for libsfmhip.so (gfx950 only).
+// Error state is thread-local; every extern "C" entry point returns an int
+// status and leaves a message for sfmhip_last_error().
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <cstdio>
+#include <cstdarg>
+
+#include "../../include/sfmhip.h"
+
+namespace sfmhip {
+
+void set_error(const char* fmt, ...);
+
+// Launch-status helper: HIP kernel launches report failure through
+// hipGetLastError(); translate it into SFMHIP_E_HIP with the kernel name.
+inline int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: %s", what, hipGetErrorString(e));
+        return SFMHIP_E_HIP;
+    }
+    return SFMHIP_OK;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Number of XCDs on MI355X; blocks are dealt round-robin over them.
+constexpr int kNumXcd = 8;
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 template): logical
+// block ids that are consecutive land on the same XCD (shared L2).  Speed
+// only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int q = nwg / kNumXcd, r = nwg % kNumXcd;
+    const int xcd = bid % kNumXcd;
+    const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + bid / kNumXcd;
+}
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace sfmhip
+
+#define SFMHIP_REQUIRE(cond, ...)                                   \
+    do {                                                            \
+        if (!(cond)) {                                              \
+            ::sfmhip::set_error(__VA_ARGS__);                       \
+            return SFMHIP_E_ARG;                                    \
+        }                                                           \
+    } while (0)

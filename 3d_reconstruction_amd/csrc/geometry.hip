@@ -1,0 +1,251 @@
+// geometry.hip — S2 DLT triangulation, S3 reprojection residual, S5 scipy
+// 2-point grouped finite-difference Jacobian; all f64, one thread per
+// observation, contract off (the Makefile builds with -ffp-contract=off).
+//
+// Reference boundary:
+//   cv2.triangulatePoints            sfm.py:27   (OpenCV calib3d DLT + cvSVD)
+//   calculate_reprojection_error     sfm.py:87-91 -> cv2.projectPoints (no distortion)
+//   least_squares(jac_sparsity=ba_sparse(...))   sfm.py:37-38, 79-85
+//     -> scipy/optimize/_numdiff.py _compute_absolute_step / _sparse_difference
+// Restated in oracle/geometry.py; the kernels follow the same op order.
+#include "common.h"
+#include <climits>
+
+namespace sfmhip {
+
+// OpenCV Rodrigues (vector -> matrix), op order of cv::Rodrigues:
+//   theta = sqrt(rx^2+ry^2+rz^2); theta < DBL_EPSILON -> I;
+//   R = (c*I + c1*r r^T) + s*[r]_x  with r normalised by itheta = 1/theta.
+__device__ __forceinline__ void rodrigues(const double* rv, double* R) {
+    double rx = rv[0], ry = rv[1], rz = rv[2];
+    const double theta = sqrt(rx * rx + ry * ry + rz * rz);
+    if (theta < 2.220446049250313e-16) {
+        R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
+        return;
+    }
+    const double c = cos(theta), s = sin(theta), c1 = 1.0 - c;
+    const double itheta = 1.0 / theta;
+    rx = rx * itheta; ry = ry * itheta; rz = rz * itheta;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double rxm[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = (c * I[k] + c1 * rrt[k]) + s * rxm[k];
+}
+
+// cv::projectPoints without distortion: x = R X + t; z = z ? 1/z : 1; u = x*z*fx + cx.
+__device__ __forceinline__ void project(const double* R, const double* t, const double* X,
+                                        double fx, double fy, double cx, double cy,
+                                        double& u, double& v) {
+    double x = R[0] * X[0] + R[1] * X[1] + R[2] * X[2] + t[0];
+    double y = R[3] * X[0] + R[4] * X[1] + R[5] * X[2] + t[1];
+    double z = R[6] * X[0] + R[7] * X[1] + R[8] * X[2] + t[2];
+    z = (z != 0.0) ? 1.0 / z : 1.0;
+    x = x * z;
+    y = y * z;
+    u = x * fx + cx;
+    v = y * fy + cy;
+}
+
+// scipy _compute_absolute_step for '2-point': EPS**0.5 * sign0(x) * max(1, |x|)
+__device__ __forceinline__ double fd_step(double x) {
+    const double rstep = 1.4901161193847656e-08;  // np.finfo(float64).eps ** 0.5
+    const double sgn = (x >= 0.0) ? 1.0 : -1.0;
+    return rstep * sgn * fmax(1.0, fabs(x));
+}
+
+// ---------------------------------------------------------------------------
+// DLT: A (6x4) rows per view v: x*P[2]-P[0], y*P[2]-P[1], x*P[1]-y*P[0];
+// one-sided (Hestenes) Jacobi on the 4 columns, V accumulates the rotations;
+// the right singular vector of the smallest singular value is V's column with
+// the smallest resulting column norm.
+__global__ void dlt_kernel(const double* __restrict__ P, const int32_t* __restrict__ pair_of_obs,
+                           const double* __restrict__ x0, const double* __restrict__ x1, int64_t n,
+                           double* __restrict__ X4) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int pr = pair_of_obs ? pair_of_obs[i] : 0;
+    const double* Pv[2] = {P + (size_t)pr * 24, P + (size_t)pr * 24 + 12};
+    const double px[2] = {x0[i], x1[i]};
+    const double py[2] = {x0[n + i], x1[n + i]};
+    double A[4][6];  // column-major: A[col][row]
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double p0 = Pv[v][k], p1 = Pv[v][4 + k], p2 = Pv[v][8 + k];
+            A[k][3 * v + 0] = px[v] * p2 - p0;
+            A[k][3 * v + 1] = py[v] * p2 - p1;
+            A[k][3 * v + 2] = px[v] * p1 - py[v] * p0;
+        }
+    }
+    double V[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
+    for (int sweep = 0; sweep < 30; ++sweep) {
+        bool rotated = false;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+            for (int q = p + 1; q < 4; ++q) {
+                double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+                    alpha += A[p][r] * A[p][r];
+                    beta += A[q][r] * A[q][r];
+                    gamma += A[p][r] * A[q][r];
+                }
+                if (fabs(gamma) <= 1e-15 * sqrt(alpha * beta) || gamma == 0.0) continue;
+                rotated = true;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+                    const double ap = A[p][r], aq = A[q][r];
+                    A[p][r] = c * ap - s * aq;
+                    A[q][r] = s * ap + c * aq;
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double vp = V[p][r], vq = V[q][r];
+                    V[p][r] = c * vp - s * vq;
+                    V[q][r] = s * vp + c * vq;
+                }
+            }
+        }
+        if (!rotated) break;
+    }
+    int best = 0;
+    double bn = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) bn += A[0][r] * A[0][r];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        double nk = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) nk += A[k][r] * A[k][r];
+        if (nk < bn) { bn = nk; best = k; }
+    }
+    double X[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) X[r] = V[0][r];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+        if (k == best) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[r] = V[k][r];
+        }
+    const double nrm = sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2] + X[3] * X[3]);
+    const double sc = (X[3] < 0 ? -1.0 : 1.0) / nrm;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) X4[(int64_t)r * n + i] = X[r] * sc;
+}
+
+// ---------------------------------------------------------------------------
+__global__ void residual_kernel(const double* __restrict__ cam, const double* __restrict__ K,
+                                const double* __restrict__ X, const double* __restrict__ pts2d,
+                                const int32_t* __restrict__ pair_of_obs, int64_t n,
+                                double* __restrict__ r) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int pr = pair_of_obs ? pair_of_obs[i] : 0;
+    const double* c = cam + (size_t)pr * 6;
+    const double* k = K + (size_t)pr * 9;
+    double R[9];
+    rodrigues(c, R);
+    const double Xp[3] = {X[3 * i], X[3 * i + 1], X[3 * i + 2]};
+    double u, v;
+    project(R, c + 3, Xp, k[0], k[4], k[2], k[5], u, v);
+    r[2 * i] = pts2d[2 * i] - u;
+    r[2 * i + 1] = pts2d[2 * i + 1] - v;
+}
+
+// 2-point FD: for each of the 9 parameters touching observation i, perturb it
+// by h (scipy step), re-project, J = (f(x+h) - f0) / ((x+h) - x).  Groups of
+// structurally orthogonal columns are perturbed together by scipy, but only
+// one column of each group touches row i, so each value depends only on that
+// column's perturbation (DESIGN.md "FD Jacobian").
+__global__ void fdjac_kernel(const double* __restrict__ cam, const double* __restrict__ K,
+                             const double* __restrict__ X, const double* __restrict__ pts2d,
+                             const int32_t* __restrict__ pair_of_obs, int64_t n,
+                             const double* __restrict__ f0, double* __restrict__ r,
+                             double* __restrict__ jv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int pr = pair_of_obs ? pair_of_obs[i] : 0;
+    const double* c = cam + (size_t)pr * 6;
+    const double* k = K + (size_t)pr * 9;
+    const double fx = k[0], fy = k[4], cx = k[2], cy = k[5];
+    const double obs_u = pts2d[2 * i], obs_v = pts2d[2 * i + 1];
+    double p[9] = {c[0], c[1], c[2], c[3], c[4], c[5], X[3 * i], X[3 * i + 1], X[3 * i + 2]};
+
+    double R0[9];
+    rodrigues(p, R0);
+    double base_u, base_v;
+    {
+        double u, v;
+        project(R0, p + 3, p + 6, fx, fy, cx, cy, u, v);
+        base_u = obs_u - u;
+        base_v = obs_v - v;
+    }
+    if (r) { r[2 * i] = base_u; r[2 * i + 1] = base_v; }
+    const double f0u = f0 ? f0[2 * i] : base_u;
+    const double f0v = f0 ? f0[2 * i + 1] : base_v;
+
+    double* row0 = jv + (size_t)i * 18;
+    double* row1 = row0 + 9;
+#pragma unroll 1
+    for (int q = 0; q < 9; ++q) {
+        const double x0v = p[q];
+        const double hx = x0v + fd_step(x0v);
+        const double dx = hx - x0v;
+        p[q] = hx;
+        double u, v;
+        if (q < 3) {
+            double Rq[9];
+            rodrigues(p, Rq);
+            project(Rq, p + 3, p + 6, fx, fy, cx, cy, u, v);
+        } else {
+            project(R0, p + 3, p + 6, fx, fy, cx, cy, u, v);
+        }
+        p[q] = x0v;
+        row0[q] = ((obs_u - u) - f0u) / dx;
+        row1[q] = ((obs_v - v) - f0v) / dx;
+    }
+}
+
+}  // namespace sfmhip
+
+using namespace sfmhip;
+
+extern "C" int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_obs, const double* x0,
+                                      const double* x1, int64_t n, double* X4, void* stream) {
+    SFMHIP_REQUIRE(P && x0 && x1 && X4, "sfmhip_triangulate_dlt: null pointer");
+    SFMHIP_REQUIRE(n >= 0, "sfmhip_triangulate_dlt: negative n");
+    if (n == 0) return SFMHIP_OK;
+    hipLaunchKernelGGL(dlt_kernel, dim3(ceil_div(n, 128)), dim3(128), 0, as_stream(stream), P,
+                       pair_of_obs, x0, x1, n, X4);
+    return check_launch("dlt_kernel");
+}
+
+extern "C" int sfmhip_reproj_residual(const double* cam, const double* K, const double* X,
+                                      const double* pts2d, const int32_t* pair_of_obs, int64_t n,
+                                      double* r, void* stream) {
+    SFMHIP_REQUIRE(cam && K && X && pts2d && r, "sfmhip_reproj_residual: null pointer");
+    SFMHIP_REQUIRE(n >= 0, "sfmhip_reproj_residual: negative n");
+    if (n == 0) return SFMHIP_OK;
+    hipLaunchKernelGGL(residual_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), cam,
+                       K, X, pts2d, pair_of_obs, n, r);
+    return check_launch("residual_kernel");
+}
+
+extern "C" int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, const double* X,
+                                         const double* pts2d, const int32_t* pair_of_obs, int n_pairs,
+                                         int64_t n, const double* f0, double* r, double* jvals,
+                                         void* stream) {
+    SFMHIP_REQUIRE(cam && K && X && pts2d && jvals, "sfmhip_reproj_fd_jacobian: null pointer");
+    SFMHIP_REQUIRE(n >= 0 && n_pairs >= 1, "sfmhip_reproj_fd_jacobian: bad counts");
+    if (n == 0) return SFMHIP_OK;
+    hipLaunchKernelGGL(fdjac_kernel, dim3(ceil_div(n, 128)), dim3(128), 0, as_stream(stream), cam, K, X,
+                       pts2d, pair_of_obs, n, f0, r, jvals);
+    return check_launch("fdjac_kernel");
+}

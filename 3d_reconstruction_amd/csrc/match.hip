@@ -1,0 +1,407 @@
+// match.hip — M1 brute-force L2 matching + Lowe ratio test on MFMA (int8),
+// M2 scipy-compatible vq, and the descriptor prep kernels.
+//
+// Reference boundary: the matcher call site matching.py:20,122-128 (LightGlue)
+// and scipy.cluster.vq.vq at matching.py:27.  Semantics: SURVEY.md §8a M1/M2,
+// pinned by oracle/match.py.
+//
+// Design (DESIGN.md "K1"):
+//   * descriptors int8 in HBM, [img][m_pad][d]; squared L2 is exact in int32.
+//   * one 512-thread workgroup = one pair x 512 rows of image a; each wave keeps
+//     its 64 rows of image a as MFMA B-operands in registers for the whole run.
+//   * image b streams through LDS in 128-row blocks (XOR-swizzled, double
+//     buffered); v_mfma_i32_32x32x32_i8 computes C'[j][i] = <b_j, a_i>, so a
+//     lane owns ONE query row i and sixteen candidate rows j per tile.
+//   * fused epilogue, 3 VALU ops per distance: packed key
+//        k = (dot << 8) + keys[j],  keys[j] = (-|b_j|^2 << 7) | (127 - j%128)
+//     i.e. k = ((2 dot - |b_j|^2) << 7) | (127 - j%128); larger k = smaller
+//     distance, lower index on ties.  top-2 per lane via max + med3; blocks
+//     merge into (best key, best index, second key) with explicit index order.
+//   * nothing of the M x N distance matrix is ever written.
+#include "common.h"
+#include <climits>
+
+namespace sfmhip {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kJB = 128;              // candidate rows per staged LDS block (7-bit local index)
+constexpr int kIW = 64;               // query rows per wave (two 32-wide MFMA column tiles)
+constexpr int kWaves = 8;             // waves per workgroup (2 per SIMD)
+constexpr int kIB = kIW * kWaves;     // query rows per workgroup
+constexpr int kThreads = 64 * kWaves;
+
+// Byte offset of logical 16-byte chunk c of row r inside a [rows][D] int8 LDS
+// tile.  XOR swizzle makes the 16 rows a ds_read_b128 lane group touches land
+// on 16 distinct 16-byte bank slots (cdna_hip_programming.md §5.5 T2).
+template <int D>
+__device__ __forceinline__ int swz_off(int r, int c) {
+    constexpr int CPR = D / 16;   // chunks per row
+    constexpr int RPB = 256 / D;  // rows per 256-byte bank row
+    return r * D + ((c ^ ((r / RPB) % CPR)) << 4);
+}
+
+__device__ __forceinline__ int med3i(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// Quantisation f32 -> int8 (padded rows zeroed).  4 elements per thread.
+__global__ void quantize_kernel(const float* __restrict__ in, int64_t total, int d, int m_pad,
+                                const int32_t* __restrict__ nk, int mode, int8_t* __restrict__ out) {
+    const int64_t n4 = total >> 2;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = q << 2;
+        const int64_t row = e / d;
+        const int img = (int)(row / m_pad);
+        const int r = (int)(row % m_pad);
+        const float4 x = *reinterpret_cast<const float4*>(in + e);
+        char4 o = make_char4(0, 0, 0, 0);
+        if (r < nk[img]) {
+            float v[4] = {x.x, x.y, x.z, x.w};
+            int qv[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (mode == 0) {
+                    float rr = fminf(fmaxf(__builtin_rintf(v[t]), 0.f), 255.f);
+                    qv[t] = (int)rr - 128;
+                } else {
+                    float rr = __builtin_rintf(127.f * v[t]);
+                    rr = fminf(fmaxf(rr, -127.f), 127.f);
+                    qv[t] = (int)rr;
+                }
+            }
+            o = make_char4((signed char)qv[0], (signed char)qv[1], (signed char)qv[2], (signed char)qv[3]);
+        }
+        *reinterpret_cast<char4*>(out + e) = o;
+    }
+}
+
+// Row norms and packed candidate keys, one thread per row.
+__global__ void prepare_kernel(const int8_t* __restrict__ desc, int n_rows, int m_pad, int d,
+                               const int32_t* __restrict__ nk, int32_t* __restrict__ norms,
+                               int32_t* __restrict__ keys) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= n_rows) return;
+    const int img = row / m_pad, r = row % m_pad;
+    const int8_t* p = desc + (size_t)row * d;
+    int s = 0;
+    for (int k = 0; k < d; k += 16) {
+        const i32x4 v = *reinterpret_cast<const i32x4*>(p + k);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int x = v[w];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int q = (int)(signed char)((x >> (8 * t)) & 0xff);
+                s += q * q;
+            }
+        }
+    }
+    norms[row] = s;
+    const int low = 127 - (r & (kJB - 1));
+    keys[row] = (r < nk[img]) ? (-s * 128 + low) : (INT_MIN + low);
+}
+
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(kThreads, 2) void match_kernel(
+    const int8_t* __restrict__ desc, const int32_t* __restrict__ norms,
+    const int32_t* __restrict__ keys, const int32_t* __restrict__ nk, int m_pad,
+    const int32_t* __restrict__ pairs, int n_iblk, int nwg, long long rn2, long long rd2,
+    int32_t* __restrict__ m0, int32_t* __restrict__ dist1, int32_t* __restrict__ dist2) {
+    constexpr int KK = D / 32;                      // MFMA k-steps per descriptor
+    constexpr int CPR = D / 16;                     // 16-byte chunks per row
+    constexpr int TILE = kJB * D;                   // bytes per staged block
+    constexpr int LDT = kJB * CPR / kThreads;       // 16-byte loads per thread per block
+    static_assert(LDT >= 1, "tile too small for the workgroup");
+
+    // All LDS in ONE array (cdna_hip_programming.md §5 item 4(a)).
+    __shared__ __attribute__((aligned(16))) int8_t lds[2 * TILE + 2 * kJB * 4];
+
+    const int wg = xcd_remap(blockIdx.x, nwg);
+    const int pair = wg / n_iblk, ib = wg % n_iblk;
+    const int a = pairs[2 * pair], b = pairs[2 * pair + 1];
+    const int na_rows = nk[a], nb_rows = nk[b];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int ibase = ib * kIB;
+    int32_t* out_m = m0 + (size_t)pair * m_pad;
+
+    if (ibase >= na_rows || nb_rows < 2) {  // block-uniform: nothing to match
+        const int iend = min(ibase + kIB, m_pad);
+        for (int i = ibase + tid; i < iend; i += kThreads) {
+            out_m[i] = -1;
+            if (dist1) dist1[(size_t)pair * m_pad + i] = -1;
+            if (dist2) dist2[(size_t)pair * m_pad + i] = -1;
+        }
+        return;
+    }
+
+    // Query rows of image a -> MFMA B-operand fragments, resident for the run.
+    i32x4 bi0[KK], bi1[KK];
+    {
+        const int i0 = min(ibase + wave * kIW + l32, m_pad - 1);
+        const int i1 = min(ibase + wave * kIW + 32 + l32, m_pad - 1);
+        const int8_t* r0 = desc + ((size_t)a * m_pad + i0) * D + h * 16;
+        const int8_t* r1 = desc + ((size_t)a * m_pad + i1) * D + h * 16;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+            bi0[kk] = *reinterpret_cast<const i32x4*>(r0 + kk * 32);
+            bi1[kk] = *reinterpret_cast<const i32x4*>(r1 + kk * 32);
+        }
+    }
+
+    const int8_t* bdesc = desc + (size_t)b * m_pad * D;
+    const int32_t* bkeys = keys + (size_t)b * m_pad;
+    const int nblk = (nb_rows + kJB - 1) / kJB;
+
+    i32x4 stg[LDT];
+    i32x4 kstg = {0, 0, 0, 0};
+    auto gload = [&](int blk) {
+        const int8_t* src = bdesc + (size_t)blk * TILE;
+#pragma unroll
+        for (int u = 0; u < LDT; ++u)
+            stg[u] = *reinterpret_cast<const i32x4*>(src + (size_t)(tid + u * kThreads) * 16);
+        if (tid < kJB / 4) kstg = *reinterpret_cast<const i32x4*>(bkeys + blk * kJB + tid * 4);
+    };
+    auto swrite = [&](int buf) {
+        int8_t* dst = lds + buf * TILE;
+#pragma unroll
+        for (int u = 0; u < LDT; ++u) {
+            const int q = tid + u * kThreads;
+            *reinterpret_cast<i32x4*>(dst + swz_off<D>(q / CPR, q % CPR)) = stg[u];
+        }
+        if (tid < kJB / 4)
+            *reinterpret_cast<i32x4*>(lds + 2 * TILE + buf * kJB * 4 + tid * 16) = kstg;
+    };
+
+    int g1k0 = INT_MIN, g1i0 = 0, g2k0 = INT_MIN;
+    int g1k1 = INT_MIN, g1i1 = 0, g2k1 = INT_MIN;
+
+    gload(0);
+    swrite(0);
+    __syncthreads();
+
+    for (int blk = 0; blk < nblk; ++blk) {
+        const int cur = blk & 1;
+        if (blk + 1 < nblk) gload(blk + 1);  // next block in flight under the MFMAs
+        const int8_t* tl = lds + cur * TILE;
+        const int32_t* kl = reinterpret_cast<const int32_t*>(lds + 2 * TILE + cur * kJB * 4);
+        int t1a = INT_MIN, t2a = INT_MIN, t1b = INT_MIN, t2b = INT_MIN;
+#pragma unroll
+        for (int jt = 0; jt < kJB / 32; ++jt) {
+            i32x16 acc0 = {0}, acc1 = {0};
+            const int r = jt * 32 + l32;
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+                const i32x4 av = *reinterpret_cast<const i32x4*>(tl + swz_off<D>(r, kk * 2 + h));
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bi0[kk], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bi1[kk], acc1, 0, 0, 0);
+            }
+            // acc reg q holds candidate row (q&3) + 8(q>>2) + 4h of this 32-row tile.
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const i32x4 kv = *reinterpret_cast<const i32x4*>(kl + jt * 32 + 8 * g + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int ka = acc0[4 * g + e] * 256 + kv[e];
+                    t2a = med3i(t2a, ka, t1a);
+                    t1a = max(t1a, ka);
+                    const int kb = acc1[4 * g + e] * 256 + kv[e];
+                    t2b = med3i(t2b, kb, t1b);
+                    t1b = max(t1b, kb);
+                }
+            }
+        }
+        // merge this block's top-2 into the running (key, index, second key)
+        {
+            const int k1 = t1a >> 7, k2 = t2a >> 7, ix = blk * kJB + 127 - (t1a & 127);
+            if (k1 > g1k0) { g2k0 = max(g1k0, k2); g1k0 = k1; g1i0 = ix; }
+            else           { g2k0 = max(g2k0, k1); }
+        }
+        {
+            const int k1 = t1b >> 7, k2 = t2b >> 7, ix = blk * kJB + 127 - (t1b & 127);
+            if (k1 > g1k1) { g2k1 = max(g1k1, k2); g1k1 = k1; g1i1 = ix; }
+            else           { g2k1 = max(g2k1, k1); }
+        }
+        if (blk + 1 < nblk) swrite(cur ^ 1);
+        __syncthreads();
+    }
+
+    // lanes l and l^32 hold the same query row, disjoint candidate rows: merge.
+    auto merge = [](int& k1, int& i1, int& k2) {
+        const int ok = __shfl_xor(k1, 32), oi = __shfl_xor(i1, 32), o2 = __shfl_xor(k2, 32);
+        const bool mine = (k1 > ok) || (k1 == ok && i1 < oi);
+        const int n2 = mine ? max(k2, ok) : max(o2, k1);
+        if (!mine) { k1 = ok; i1 = oi; }
+        k2 = n2;
+    };
+    merge(g1k0, g1i0, g2k0);
+    merge(g1k1, g1i1, g2k1);
+
+    const int i = ibase + wave * kIW + h * 32 + l32;  // lane half h writes column tile h
+    if (i < m_pad) {
+        const int k1 = h ? g1k1 : g1k0, i1 = h ? g1i1 : g1i0, k2 = h ? g2k1 : g2k0;
+        int res = -1, d1 = -1, d2 = -1;
+        if (i < na_rows) {
+            const int na = norms[(size_t)a * m_pad + i];
+            d1 = na - k1;
+            d2 = na - k2;
+            if (rd2 * (long long)d1 < rn2 * (long long)d2) res = i1;
+        }
+        out_m[i] = res;
+        if (dist1) dist1[(size_t)pair * m_pad + i] = d1;
+        if (dist2) dist2[(size_t)pair * m_pad + i] = d2;
+    }
+}
+
+__global__ void mutual_kernel(int32_t* __restrict__ m0, int32_t* __restrict__ m1, int P, int m_pad) {
+    // In place is race-free: an entry is cleared only when it is not mutual, and
+    // a reader that sees the cleared value (-1) decides the same way.
+    const int64_t total = (int64_t)P * m_pad;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t base = (e / m_pad) * m_pad;
+        const int i = (int)(e - base);
+        const int j0 = m0[e];
+        const int j1 = m1[e];
+        const bool keep0 = j0 >= 0 && m1[base + j0] == i;
+        const bool keep1 = j1 >= 0 && m0[base + j1] == i;
+        if (j0 >= 0 && !keep0) m0[e] = -1;
+        if (j1 >= 0 && !keep1) m1[e] = -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// vq: 16 threads per observation, each scanning codes c = lane16, lane16+16, ...
+// with the distance summed in k order (f64), then a 16-lane argmin reduction
+// with lowest-index tie-break.
+constexpr int kVqObsPerBlock = 16;
+
+__global__ __launch_bounds__(256) void vq_kernel(const double* __restrict__ obs, int64_t n_obs,
+                                                 const double* __restrict__ code, int n_codes, int d,
+                                                 int32_t* __restrict__ codes, double* __restrict__ dist) {
+    extern __shared__ double sobs[];  // [16][d]
+    const int64_t o0 = (int64_t)blockIdx.x * kVqObsPerBlock;
+    for (int t = threadIdx.x; t < kVqObsPerBlock * d; t += blockDim.x) {
+        const int64_t o = o0 + t / d;
+        sobs[t] = (o < n_obs) ? obs[o * d + (t % d)] : 0.0;
+    }
+    __syncthreads();
+    const int lo = threadIdx.x >> 4, l16 = threadIdx.x & 15;
+    const double* x = sobs + lo * d;
+    double best = __builtin_inf();
+    int bidx = INT_MAX;
+    for (int c = l16; c < n_codes; c += 16) {
+        const double* y = code + (size_t)c * d;
+        double s = 0.0;
+        for (int k = 0; k < d; ++k) {
+            const double df = x[k] - y[k];
+            s = s + df * df;
+        }
+        if (s < best) { best = s; bidx = c; }
+    }
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) {
+        const double ob = __shfl_xor(best, off, 16);
+        const int oi = __shfl_xor(bidx, off, 16);
+        if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+    }
+    const int64_t o = o0 + lo;
+    if (l16 == 0 && o < n_obs) {
+        codes[o] = bidx;
+        dist[o] = sqrt(best);
+    }
+}
+
+}  // namespace sfmhip
+
+using namespace sfmhip;
+
+extern "C" int sfmhip_desc_quantize(const float* in, int n_img, int m_pad, int d,
+                                    const int32_t* n_kpts, int mode, int8_t* out, void* stream) {
+    SFMHIP_REQUIRE(in && out && n_kpts, "sfmhip_desc_quantize: null pointer");
+    SFMHIP_REQUIRE(n_img > 0 && m_pad > 0 && d > 0 && d % 4 == 0, "sfmhip_desc_quantize: bad shape");
+    SFMHIP_REQUIRE(mode == 0 || mode == 1, "sfmhip_desc_quantize: mode must be 0 or 1");
+    const int64_t total = (int64_t)n_img * m_pad * d;
+    const int64_t n4 = total / 4;
+    const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(quantize_kernel, dim3(grid), dim3(256), 0, as_stream(stream), in, total, d,
+                       m_pad, n_kpts, mode, out);
+    return check_launch("quantize_kernel");
+}
+
+extern "C" int sfmhip_desc_prepare(const int8_t* desc, int n_img, int m_pad, int d,
+                                   const int32_t* n_kpts, int32_t* norms, int32_t* keys, void* stream) {
+    SFMHIP_REQUIRE(desc && n_kpts && norms && keys, "sfmhip_desc_prepare: null pointer");
+    SFMHIP_REQUIRE(n_img > 0 && m_pad > 0 && d > 0 && d % 16 == 0, "sfmhip_desc_prepare: bad shape");
+    const int rows = n_img * m_pad;
+    hipLaunchKernelGGL(prepare_kernel, dim3(ceil_div(rows, 256)), dim3(256), 0, as_stream(stream),
+                       desc, rows, m_pad, d, n_kpts, norms, keys);
+    return check_launch("prepare_kernel");
+}
+
+extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                                  const int32_t* n_kpts, int n_img, int m_pad, int d,
+                                  const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                                  int32_t* matches0, int32_t* dist1, int32_t* dist2, void* stream) {
+    SFMHIP_REQUIRE(desc && norms && keys && n_kpts && pairs && matches0,
+                   "sfmhip_match_pairs: null pointer");
+    SFMHIP_REQUIRE(n_img > 0 && P >= 0, "sfmhip_match_pairs: bad counts");
+    SFMHIP_REQUIRE(m_pad > 0 && m_pad % kJB == 0, "sfmhip_match_pairs: m_pad must be a positive multiple of 128");
+    SFMHIP_REQUIRE(ratio_num > 0 && ratio_den > 0 && ratio_num <= 65535 && ratio_den <= 65535,
+                   "sfmhip_match_pairs: ratio must be a positive fraction");
+    if (P == 0) return SFMHIP_OK;
+    const int n_iblk = ceil_div(m_pad, kIB);
+    const int64_t nwg64 = (int64_t)P * n_iblk;
+    SFMHIP_REQUIRE(nwg64 < INT_MAX, "sfmhip_match_pairs: too many pairs for one launch");
+    const int nwg = (int)nwg64;
+    const long long rn2 = (long long)ratio_num * ratio_num, rd2 = (long long)ratio_den * ratio_den;
+    hipStream_t s = as_stream(stream);
+    switch (d) {
+        case 64:
+            hipLaunchKernelGGL(match_kernel<64>, dim3(nwg), dim3(kThreads), 0, s, desc, norms, keys,
+                               n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2);
+            break;
+        case 128:
+            hipLaunchKernelGGL(match_kernel<128>, dim3(nwg), dim3(kThreads), 0, s, desc, norms, keys,
+                               n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2);
+            break;
+        case 256:
+            hipLaunchKernelGGL(match_kernel<256>, dim3(nwg), dim3(kThreads), 0, s, desc, norms, keys,
+                               n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2);
+            break;
+        default:
+            set_error("sfmhip_match_pairs: descriptor dim %d not in {64,128,256}", d);
+            return SFMHIP_E_UNSUPPORTED;
+    }
+    return check_launch("match_kernel");
+}
+
+extern "C" int sfmhip_mutual_filter(int32_t* matches0, int32_t* matches1, int P, int m_pad, void* stream) {
+    SFMHIP_REQUIRE(matches0 && matches1, "sfmhip_mutual_filter: null pointer");
+    SFMHIP_REQUIRE(P >= 0 && m_pad > 0, "sfmhip_mutual_filter: bad shape");
+    if (P == 0) return SFMHIP_OK;
+    const int64_t total = (int64_t)P * m_pad;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(mutual_kernel, dim3(grid), dim3(256), 0, as_stream(stream), matches0, matches1, P,
+                       m_pad);
+    return check_launch("mutual_kernel");
+}
+
+extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_book, int n_codes, int d,
+                         int32_t* codes, double* dist, void* stream) {
+    SFMHIP_REQUIRE(obs && code_book && codes && dist, "sfmhip_vq: null pointer");
+    SFMHIP_REQUIRE(n_obs >= 0 && n_codes > 0 && d > 0 && d <= 1024, "sfmhip_vq: bad shape");
+    if (n_obs == 0) return SFMHIP_OK;
+    const int64_t blocks = (n_obs + kVqObsPerBlock - 1) / kVqObsPerBlock;
+    SFMHIP_REQUIRE(blocks < INT_MAX, "sfmhip_vq: too many observations");
+    hipLaunchKernelGGL(vq_kernel, dim3((int)blocks), dim3(256), kVqObsPerBlock * d * sizeof(double),
+                       as_stream(stream), obs, n_obs, code_book, n_codes, d, codes, dist);
+    return check_launch("vq_kernel");
+}

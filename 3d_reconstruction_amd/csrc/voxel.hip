@@ -1,0 +1,460 @@
+// voxel.hip — voxel-grid kernels: V1 DDA traversal (voxel_travesal.py), V2
+// trilinear grid sample (sdf.py get_sdf/get_sdf_sh, plenoxel NerfModel), V4
+// fused sample + SH-2 colour + alpha composite (sdf.py forward, plenoxel
+// render_rays) and V5 TSDF integration (build-defined).
+// All fp32 with -ffp-contract=off so the op order matches oracle/voxel.py.
+#include "common.h"
+#include <climits>
+
+namespace sfmhip {
+
+// ---------------------------------------------------------------------------
+// V1: torch.floor_divide on floats (c10::div_floor_floating): Python floor
+// division via fmod, with the same fix-ups.
+__device__ __forceinline__ float floor_div(float a, float b) {
+    if (b == 0.f) return a / b;
+    const float mod = fmodf(a, b);
+    float div = (a - mod) / b;
+    if (mod != 0.f && ((b < 0.f) != (mod < 0.f))) div -= 1.f;
+    float fl;
+    if (div != 0.f) {
+        fl = floorf(div);
+        if (div - fl > 0.5f) fl += 1.f;
+    } else {
+        fl = copysignf(0.f, a / b);
+    }
+    return fl;
+}
+
+struct Ray {
+    float cur[3], last[3], step[3], tmax[3], tdelta[3];
+};
+
+__device__ __forceinline__ void ray_setup(const float* rr, float bin, Ray& R) {
+    const float near = rr[6], far = rr[7];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float o = rr[a], d = rr[3 + a];
+        const float start = o + d * near;
+        const float end = o + d * far;
+        R.cur[a] = floor_div(start, bin);
+        R.last[a] = floor_div(end, bin);
+        R.step[a] = (d < 0.f) ? -1.f : 1.f;
+        const float nvb = (R.cur[a] + R.step[a]) * bin;
+        R.tmax[a] = (d == 0.f) ? __builtin_inff() : (nvb - start) / d;
+        R.tdelta[a] = (d == 0.f) ? __builtin_inff() : (R.step[a] * bin) / d;
+    }
+}
+
+// voxel_travesal.py:32-37 get_maskt: any axis with cur==cur and step*cur < step*last
+__device__ __forceinline__ bool ray_active(const Ray& R) {
+    bool m = false;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        m = m || ((R.cur[a] == R.cur[a]) && (R.step[a] * R.cur[a] < R.step[a] * R.last[a]));
+    return m;
+}
+
+// voxel_travesal.py:43-64: one step; axis masks are mutually exclusive.
+__device__ __forceinline__ void ray_step(Ray& R) {
+    const float tx = R.tmax[0], ty = R.tmax[1], tz = R.tmax[2];
+    const bool mx = (tx < ty) && (tx < tz);
+    const bool my = (ty <= tx) && (ty < tz);
+    const bool mz = ((tx >= ty) && (ty >= tz)) || ((tx >= tz) && (ty > tx));
+    if (mx) { R.cur[0] = R.cur[0] + R.step[0]; R.tmax[0] = R.tmax[0] + R.tdelta[0]; }
+    if (my) { R.cur[1] = R.cur[1] + R.step[1]; R.tmax[1] = R.tmax[1] + R.tdelta[1]; }
+    if (mz) { R.cur[2] = R.cur[2] + R.step[2]; R.tmax[2] = R.tmax[2] + R.tdelta[2]; }
+}
+
+__global__ void dda_count_kernel(const float* __restrict__ rays, int64_t N, float bin, int max_steps,
+                                 int32_t* __restrict__ n_steps, int32_t* __restrict__ overflow) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    Ray R;
+    ray_setup(rays + 8 * i, bin, R);
+    int k = 0;
+    bool act = ray_active(R);
+    while (act && k < max_steps) {
+        ray_step(R);
+        ++k;
+        act = ray_active(R);
+    }
+    if (act) atomicOr(overflow, 1);
+    n_steps[i] = k;
+}
+
+__global__ void dda_fill_kernel(const float* __restrict__ rays, int64_t N, float bin, int S,
+                                float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    Ray R;
+    ray_setup(rays + 8 * i, bin, R);
+    float* o = out + (size_t)i * S * 3;
+    const float nan = __builtin_nanf("");
+    o[0] = R.cur[0]; o[1] = R.cur[1]; o[2] = R.cur[2];
+    bool act = ray_active(R);
+    int s = 1;
+    if (!act && S > 1) {  // inactive from the start: the first loop pass re-appends it
+        o[3] = R.cur[0]; o[4] = R.cur[1]; o[5] = R.cur[2];
+        s = 2;
+    }
+    while (act && s < S) {
+        ray_step(R);
+        o[3 * s] = R.cur[0]; o[3 * s + 1] = R.cur[1]; o[3 * s + 2] = R.cur[2];
+        ++s;
+        act = ray_active(R);
+    }
+    for (; s < S; ++s) { o[3 * s] = nan; o[3 * s + 1] = nan; o[3 * s + 2] = nan; }
+}
+
+// ---------------------------------------------------------------------------
+// V2: sdf.py:287-291 / plenoxel.py:34-37 normalisation, then ATen
+// grid_sampler_3d (bilinear, zeros, align_corners=True) weight formulas.
+struct Bounds { float mn[3], mx[3]; };
+
+__device__ __forceinline__ bool normalise(const float* p, const Bounds& B, int mode, float* g) {
+    if (mode == 0) {
+        const bool in = (p[0] >= B.mn[0]) && (p[1] >= B.mn[1]) && (p[2] >= B.mn[2]) &&
+                        (p[0] <= B.mx[0]) && (p[1] <= B.mx[1]) && (p[2] <= B.mx[2]);
+        if (!in) return false;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) g[a] = ((p[a] - B.mn[a]) / (B.mx[a] - B.mn[a])) * 2.f - 1.f;
+        return true;
+    }
+    const float s = B.mx[0];
+    const bool in = (fabsf(p[0]) < s) && (fabsf(p[1]) < s) && (fabsf(p[2]) < s);
+    if (!in) return false;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) g[a] = fminf(fmaxf(p[a] / s, -1.f), 1.f);
+    return true;
+}
+
+struct Corners {
+    int ix, iy, iz;     // tnw corner
+    float w[8];         // tnw tne tsw tse bnw bne bsw bse
+};
+
+__device__ __forceinline__ void corners(const float* g, int D, int H, int W, Corners& c) {
+    const float ix = ((g[0] + 1.f) / 2.f) * (float)(W - 1);
+    const float iy = ((g[1] + 1.f) / 2.f) * (float)(H - 1);
+    const float iz = ((g[2] + 1.f) / 2.f) * (float)(D - 1);
+    const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+    c.ix = (int)fx; c.iy = (int)fy; c.iz = (int)fz;
+    const float x1 = fx + 1.f, y1 = fy + 1.f, z1 = fz + 1.f;
+    c.w[0] = (x1 - ix) * (y1 - iy) * (z1 - iz);  // tnw
+    c.w[1] = (ix - fx) * (y1 - iy) * (z1 - iz);  // tne
+    c.w[2] = (x1 - ix) * (iy - fy) * (z1 - iz);  // tsw
+    c.w[3] = (ix - fx) * (iy - fy) * (z1 - iz);  // tse
+    c.w[4] = (x1 - ix) * (y1 - iy) * (iz - fz);  // bnw
+    c.w[5] = (ix - fx) * (y1 - iy) * (iz - fz);  // bne
+    c.w[6] = (x1 - ix) * (iy - fy) * (iz - fz);  // bsw
+    c.w[7] = (ix - fx) * (iy - fy) * (iz - fz);  // bse
+}
+
+__device__ __forceinline__ bool corner_in(const Corners& c, int k, int D, int H, int W, int& x, int& y, int& z) {
+    x = c.ix + (k & 1);
+    y = c.iy + ((k >> 1) & 1);
+    z = c.iz + ((k >> 2) & 1);
+    return x >= 0 && x < W && y >= 0 && y < H && z >= 0 && z < D;
+}
+
+__global__ void grid_sample_kernel(const float* __restrict__ grid, int C, int D, int H, int W, Bounds B,
+                                   int mode, const float* __restrict__ pts, int64_t P, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float p[3] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+    float g[3];
+    float* o = out + (size_t)i * C;
+    if (!normalise(p, B, mode, g)) {
+        for (int c = 0; c < C; ++c) o[c] = 0.f;
+        return;
+    }
+    Corners cn;
+    corners(g, D, H, W, cn);
+    int64_t off[8];
+    bool in[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int x, y, z;
+        in[k] = corner_in(cn, k, D, H, W, x, y, z);
+        off[k] = ((int64_t)z * H + y) * W + x;
+    }
+    const int64_t plane = (int64_t)D * H * W;
+    for (int c = 0; c < C; ++c) {
+        const float* gc = grid + (size_t)c * plane;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (in[k]) acc = acc + gc[off[k]] * cn.w[k];
+        o[c] = acc;
+    }
+}
+
+// (C,D,H,W) -> (D,H,W,32), zero padded channels.
+__global__ void to_vm_kernel(const float* __restrict__ grid, int C, int64_t nvox, float* __restrict__ vm) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nvox * 32) return;
+    const int64_t v = e >> 5;
+    const int c = (int)(e & 31);
+    vm[e] = (c < C) ? grid[(size_t)c * nvox + v] : 0.f;
+}
+
+// ---------------------------------------------------------------------------
+// V4: one wave per ray, one lane per sample (chunks of 64 samples).
+__device__ __forceinline__ void sh_colour(const float* k, float x, float y, float z, float* col) {
+    // sdf.py:361-369 / plenoxel.py:9-16, Python operator order, fp32 constants.
+    const float C0 = 0.282095f, C1 = 0.488603f, C2 = 1.092548f, C3 = 0.315392f, C4 = 0.546274f;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const float* kk = k + 9 * ch;
+        const float inner = ((((C2 * x) * y) * kk[4] - ((C2 * y) * z) * kk[5]) +
+                             (C3 * (((2.0f * z) * z - x * x) - y * y)) * kk[6]) +
+                            ((-C2) * x) * z * kk[7];
+        const float inner2 = inner + (C4 * (x * x - y * y)) * kk[8];
+        col[ch] = (((C0 * kk[0] + ((-C1) * y) * kk[1]) + (C1 * z) * kk[2]) - (C1 * x) * kk[3]) + inner2;
+    }
+}
+
+__global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ gvm, int D, int H, int W,
+                                                     Bounds B, int mode, const float* __restrict__ ro,
+                                                     const float* __restrict__ rd, const float* __restrict__ zv,
+                                                     int64_t nrays, int S, float* __restrict__ rgb) {
+    const int lane = threadIdx.x & 63;
+    const int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (ray >= nrays) return;  // wave-uniform
+    const float o[3] = {ro[3 * ray], ro[3 * ray + 1], ro[3 * ray + 2]};
+    const float d[3] = {rd[3 * ray], rd[3 * ray + 1], rd[3 * ray + 2]};
+    const float* z = zv + (size_t)ray * S;
+    float carry = 1.f;  // transmittance entering this chunk
+    float cr = 0.f, cg = 0.f, cb = 0.f, ws = 0.f;
+    for (int s0 = 0; s0 < S; s0 += 64) {
+        const int s = s0 + lane;
+        float alpha = 0.f, col[3] = {0.f, 0.f, 0.f};
+        if (s < S) {
+            const float zs = z[s];
+            const float p[3] = {o[0] + d[0] * zs, o[1] + d[1] * zs, o[2] + d[2] * zs};
+            float g[3];
+            float sdf = 0.f;
+            float k[27];
+#pragma unroll
+            for (int c = 0; c < 27; ++c) k[c] = 0.f;
+            if (normalise(p, B, mode, g)) {
+                Corners cn;
+                corners(g, D, H, W, cn);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    int x, y, zz;
+                    if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
+                    const float w = cn.w[q];
+                    const float4* v = reinterpret_cast<const float4*>(gvm + ((((size_t)zz * H + y) * W + x) << 5));
+                    float vv[28];
+#pragma unroll
+                    for (int t = 0; t < 7; ++t) {
+                        const float4 f = v[t];
+                        vv[4 * t] = f.x; vv[4 * t + 1] = f.y; vv[4 * t + 2] = f.z; vv[4 * t + 3] = f.w;
+                    }
+                    sdf = sdf + vv[0] * w;
+#pragma unroll
+                    for (int c = 0; c < 27; ++c) k[c] = k[c] + vv[1 + c] * w;
+                }
+            }
+            sh_colour(k, d[0], d[1], d[2], col);
+            const float sigma = fmaxf(sdf, 0.f);
+            const float delta = (s + 1 < S) ? (z[s + 1] - zs) : 1e10f;
+            alpha = 1.f - expf((-sigma) * delta);
+        }
+        // exclusive multiplicative scan of (1 - alpha) across the wave
+        float incl = 1.f - alpha;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const float up = __shfl_up(incl, off, 64);
+            if (lane >= off) incl = incl * up;
+        }
+        float excl = __shfl_up(incl, 1, 64);
+        if (lane == 0) excl = 1.f;
+        const float T = carry * excl;
+        const float w = T * alpha;
+        float pr = w * col[0], pg = w * col[1], pb = w * col[2], pw = w;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            pr += __shfl_xor(pr, off, 64);
+            pg += __shfl_xor(pg, off, 64);
+            pb += __shfl_xor(pb, off, 64);
+            pw += __shfl_xor(pw, off, 64);
+        }
+        cr += pr; cg += pg; cb += pb; ws += pw;
+        carry = carry * __shfl(incl, 63, 64);
+    }
+    if (lane == 0) {
+        rgb[3 * ray] = (cr + 1.f) - ws;
+        rgb[3 * ray + 1] = (cg + 1.f) - ws;
+        rgb[3 * ray + 2] = (cb + 1.f) - ws;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// V5: TSDF integration.  Workgroup = 16(x) x 4(y) x 4(z) voxels; every thread
+// keeps its voxel's (T, W) in registers across all F frames, so the grid is
+// read and written once per call; poses/intrinsics staged in LDS.
+constexpr int kTsdfMaxFramesLds = 512;
+
+__global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float* __restrict__ Wt, int D, int H,
+                                                   int W, int z0, int z1, const float* __restrict__ depth, int F,
+                                                   int Hd, int Wd, const float* __restrict__ poses,
+                                                   const float* __restrict__ Kf, Bounds B, float trunc) {
+    __shared__ float cam[kTsdfMaxFramesLds * 16];
+    const int nf = min(F, kTsdfMaxFramesLds);
+    for (int t = threadIdx.x; t < nf * 16; t += blockDim.x) {
+        const int f = t >> 4, q = t & 15;
+        cam[t] = (q < 12) ? poses[f * 12 + q] : Kf[f * 4 + (q - 12)];
+    }
+    __syncthreads();
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 4 + ((threadIdx.x >> 4) & 3);
+    const int z = z0 + blockIdx.z * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H || z >= z1) return;
+    const float sx = (B.mx[0] - B.mn[0]) / (float)(W - 1);
+    const float sy = (B.mx[1] - B.mn[1]) / (float)(H - 1);
+    const float sz = (B.mx[2] - B.mn[2]) / (float)(D - 1);
+    const float vx = B.mn[0] + (float)x * sx;
+    const float vy = B.mn[1] + (float)y * sy;
+    const float vz = B.mn[2] + (float)z * sz;
+    const size_t idx = ((size_t)z * H + y) * W + x;
+    float tv = T[idx], wv = Wt[idx];
+    const size_t frame = (size_t)Hd * Wd;
+    for (int f = 0; f < F; ++f) {
+        const float* c = (f < kTsdfMaxFramesLds) ? cam + f * 16 : nullptr;
+        float P[16];
+        if (c) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) P[q] = c[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 12; ++q) P[q] = poses[f * 12 + q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) P[12 + q] = Kf[f * 4 + q];
+        }
+        const float Xc = P[0] * vx + P[1] * vy + P[2] * vz + P[3];
+        const float Yc = P[4] * vx + P[5] * vy + P[6] * vz + P[7];
+        const float Zc = P[8] * vx + P[9] * vy + P[10] * vz + P[11];
+        if (!(Zc > 0.f)) continue;
+        const float iz = 1.0f / Zc;
+        const float u = (P[12] * Xc) * iz + P[14];
+        const float v = (P[13] * Yc) * iz + P[15];
+        const float fu = floorf(u + 0.5f), fv = floorf(v + 0.5f);
+        if (!(fu >= 0.f && fu < (float)Wd && fv >= 0.f && fv < (float)Hd)) continue;
+        const float dep = depth[f * frame + (size_t)fv * Wd + (size_t)fu];
+        if (!(dep > 0.f)) continue;
+        const float sdf = dep - Zc;
+        if (sdf < -trunc) continue;
+        const float ts = fminf(1.0f, sdf / trunc);
+        tv = (tv * wv + ts) / (wv + 1.0f);
+        wv = wv + 1.0f;
+    }
+    T[idx] = tv;
+    Wt[idx] = wv;
+}
+
+}  // namespace sfmhip
+
+using namespace sfmhip;
+
+extern "C" int sfmhip_voxel_traversal_count(const float* rays, int64_t N, float bin, int32_t max_steps,
+                                            int32_t* n_steps, void* stream) {
+    SFMHIP_REQUIRE(rays && n_steps, "sfmhip_voxel_traversal_count: null pointer");
+    SFMHIP_REQUIRE(N >= 0 && max_steps > 0, "sfmhip_voxel_traversal_count: bad args");
+    if (N == 0) return SFMHIP_OK;
+    hipStream_t s = as_stream(stream);
+    int32_t* dflag = nullptr;
+    // The overflow flag rides in a pinned host word so no device allocation is needed.
+    int32_t* hflag = nullptr;
+    if (hipHostMalloc((void**)&hflag, sizeof(int32_t), hipHostMallocMapped) != hipSuccess) {
+        set_error("sfmhip_voxel_traversal_count: hipHostMalloc failed");
+        return SFMHIP_E_HIP;
+    }
+    *hflag = 0;
+    if (hipHostGetDevicePointer((void**)&dflag, hflag, 0) != hipSuccess) {
+        (void)hipHostFree(hflag);
+        set_error("sfmhip_voxel_traversal_count: hipHostGetDevicePointer failed");
+        return SFMHIP_E_HIP;
+    }
+    hipLaunchKernelGGL(dda_count_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, rays, N, bin, max_steps,
+                       n_steps, dflag);
+    int rc = check_launch("dda_count_kernel");
+    if (rc == SFMHIP_OK) {
+        if (hipStreamSynchronize(s) != hipSuccess) {
+            set_error("sfmhip_voxel_traversal_count: stream sync failed");
+            rc = SFMHIP_E_HIP;
+        } else if (*hflag) {
+            set_error("sfmhip_voxel_traversal_count: a ray exceeded max_steps=%d", max_steps);
+            rc = SFMHIP_E_OVERFLOW;
+        }
+    }
+    (void)hipHostFree(hflag);
+    return rc;
+}
+
+extern "C" int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, int32_t S, float* out,
+                                      void* stream) {
+    SFMHIP_REQUIRE(rays && out, "sfmhip_voxel_traversal: null pointer");
+    SFMHIP_REQUIRE(N >= 0 && S >= 1, "sfmhip_voxel_traversal: bad args");
+    if (N == 0) return SFMHIP_OK;
+    hipLaunchKernelGGL(dda_fill_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, as_stream(stream), rays, N, bin, S,
+                       out);
+    return check_launch("dda_fill_kernel");
+}
+
+static Bounds make_bounds(const float* bmin, const float* bmax) {
+    Bounds B;
+    for (int a = 0; a < 3; ++a) { B.mn[a] = bmin[a]; B.mx[a] = bmax[a]; }
+    return B;
+}
+
+extern "C" int sfmhip_grid_sample(const float* grid, int C, int D, int H, int W, const float* bmin,
+                                  const float* bmax, int mask_mode, const float* pts, int64_t P, float* out,
+                                  void* stream) {
+    SFMHIP_REQUIRE(grid && bmin && bmax && pts && out, "sfmhip_grid_sample: null pointer");
+    SFMHIP_REQUIRE(C > 0 && D > 1 && H > 1 && W > 1 && P >= 0, "sfmhip_grid_sample: bad shape");
+    SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_grid_sample: mask_mode must be 0 or 1");
+    if (P == 0) return SFMHIP_OK;
+    hipLaunchKernelGGL(grid_sample_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, as_stream(stream), grid, C, D,
+                       H, W, make_bounds(bmin, bmax), mask_mode, pts, P, out);
+    return check_launch("grid_sample_kernel");
+}
+
+extern "C" int sfmhip_grid_to_voxel_major(const float* grid, int C, int D, int H, int W, float* grid_vm,
+                                          void* stream) {
+    SFMHIP_REQUIRE(grid && grid_vm, "sfmhip_grid_to_voxel_major: null pointer");
+    SFMHIP_REQUIRE(C > 0 && C <= 32 && D > 0 && H > 0 && W > 0, "sfmhip_grid_to_voxel_major: bad shape");
+    const int64_t nvox = (int64_t)D * H * W;
+    hipLaunchKernelGGL(to_vm_kernel, dim3(ceil_div(nvox * 32, 256)), dim3(256), 0, as_stream(stream), grid, C,
+                       nvox, grid_vm);
+    return check_launch("to_vm_kernel");
+}
+
+extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, const float* bmin,
+                                  const float* bmax, int mask_mode, const float* rays_o, const float* rays_d,
+                                  const float* z, int64_t B, int S, float* rgb, void* stream) {
+    SFMHIP_REQUIRE(grid_vm && bmin && bmax && rays_o && rays_d && z && rgb, "sfmhip_render_rays: null pointer");
+    SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && B >= 0 && S >= 1, "sfmhip_render_rays: bad shape");
+    SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_render_rays: mask_mode must be 0 or 1");
+    if (B == 0) return SFMHIP_OK;
+    hipLaunchKernelGGL(render_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, as_stream(stream), grid_vm, D, H, W,
+                       make_bounds(bmin, bmax), mask_mode, rays_o, rays_d, z, B, S, rgb);
+    return check_launch("render_kernel");
+}
+
+extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, int z0, int z1,
+                                     const float* depth, int F, int Hd, int Wd, const float* poses,
+                                     const float* Kf, const float* bmin, const float* bmax, float trunc,
+                                     void* stream) {
+    SFMHIP_REQUIRE(T && Wt && depth && poses && Kf && bmin && bmax, "sfmhip_tsdf_integrate: null pointer");
+    SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && F >= 0 && Hd > 0 && Wd > 0, "sfmhip_tsdf_integrate: bad shape");
+    SFMHIP_REQUIRE(0 <= z0 && z0 <= z1 && z1 <= D, "sfmhip_tsdf_integrate: bad z range");
+    SFMHIP_REQUIRE(trunc > 0.f, "sfmhip_tsdf_integrate: trunc must be > 0");
+    if (F == 0 || z0 == z1) return SFMHIP_OK;
+    dim3 grid(ceil_div(W, 16), ceil_div(H, 4), ceil_div(z1 - z0, 4));
+    hipLaunchKernelGGL(tsdf_kernel, grid, dim3(256), 0, as_stream(stream), T, Wt, D, H, W, z0, z1, depth, F,
+                       Hd, Wd, poses, Kf, make_bounds(bmin, bmax), trunc);
+    return check_launch("tsdf_kernel");
+}

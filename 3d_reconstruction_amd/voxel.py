@@ -1,0 +1,126 @@
+"""V1-V5: voxel-grid kernels with the reference's torch signatures.
+
+* :func:`voxel_traversal` — ``voxel_travesal.py:1-73`` (quirks included:
+  one-cell-late negative-direction boundary, overshoot, NaN padding, a ray that
+  starts inactive is emitted twice).
+* :class:`VoxelGrid` — ``SDFGrid.get_sdf`` / ``get_sdf_sh`` (``sdf.py:284-342``),
+  ``NerfModel.forward`` (``plenoxel.py:31-43``) and the composite of
+  ``SDFGrid.forward`` / ``render_rays`` (``sdf.py:391-406``,
+  ``plenoxel.py:71-93``) for a given sample set ``z`` (the reference draws it
+  with ``torch.rand``; callers pass it explicitly).
+* :func:`tsdf_integrate` — TSDF fusion of depth maps into a (D,H,W) grid laid
+  out like the ``sdf.py`` grid (build-defined).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._abi import call, dev, ptr, require_gpu, stream_ptr
+
+MASK_SDF = 0       # sdf.py test_points: bmin <= p <= bmax (inclusive)
+MASK_PLENOXEL = 1  # plenoxel: |p| < scale (strict), p/scale clipped to [-1, 1]
+
+
+def _f3(v) -> np.ndarray:
+    a = np.asarray(v if not isinstance(v, torch.Tensor) else v.detach().cpu().numpy(), dtype=np.float32)
+    return np.ascontiguousarray(np.broadcast_to(a.ravel(), (3,)) if a.size == 1 else a.ravel()[:3])
+
+
+def _host_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def voxel_traversal(rays: torch.Tensor, _bin_size, max_steps: int = 1 << 20) -> torch.Tensor:
+    """(N,8) rays [o, d, near, far] -> (N, S, 3) visited voxel indices (float, NaN padded)."""
+    require_gpu()
+    r = dev(rays, torch.float32)
+    N = r.shape[0]
+    b = float(_bin_size)
+    steps = torch.empty(N, dtype=torch.int32, device=r.device)
+    call("sfmhip_voxel_traversal_count", ptr(r), N, b, int(max_steps), ptr(steps), stream_ptr())
+    S = 1 + (int(steps.max().item()) if N > 0 else 0)
+    out = torch.empty((N, S, 3), dtype=torch.float32, device=r.device)
+    call("sfmhip_voxel_traversal", ptr(r), N, b, S, ptr(out), stream_ptr())
+    return out
+
+
+class VoxelGrid:
+    """An SDF + SH-2 colour grid (1, 28, D, H, W) in the reference layout.
+
+    ``mask_mode`` MASK_SDF reproduces sdf.py (bounds min_bound/max_bound),
+    MASK_PLENOXEL reproduces plenoxel.py (bounds +-scale)."""
+
+    def __init__(self, grid: torch.Tensor, min_bound, max_bound, mask_mode: int = MASK_SDF):
+        require_gpu()
+        g = grid.detach()
+        if g.dim() == 5:
+            g = g[0]
+        self.grid = dev(g, torch.float32)
+        self.C, self.D, self.H, self.W = (int(s) for s in self.grid.shape)
+        self.bmin = _f3(min_bound)
+        self.bmax = _f3(max_bound)
+        self.mask_mode = int(mask_mode)
+        self._vm = None
+
+    @classmethod
+    def plenoxel(cls, voxel_grid: torch.Tensor, scale: float = 1.5) -> "VoxelGrid":
+        return cls(voxel_grid, (-scale,) * 3, (scale,) * 3, MASK_PLENOXEL)
+
+    def sample(self, points: torch.Tensor) -> torch.Tensor:
+        """All C channels at the points: (P, C) f32 (zero outside)."""
+        p = dev(points, torch.float32).reshape(-1, 3)
+        out = torch.empty((p.shape[0], self.C), dtype=torch.float32, device=p.device)
+        call("sfmhip_grid_sample", ptr(self.grid), self.C, self.D, self.H, self.W, _host_ptr(self.bmin),
+             _host_ptr(self.bmax), self.mask_mode, ptr(p), p.shape[0], ptr(out), stream_ptr())
+        return out
+
+    def get_sdf(self, points: torch.Tensor) -> torch.Tensor:
+        return self.sample(points)[:, 0]
+
+    def get_sdf_sh(self, points: torch.Tensor):
+        s = self.sample(points)
+        return s[:, 0], s[:, 1:]
+
+    def voxel_major(self) -> torch.Tensor:
+        if self._vm is None:
+            if self.C > 32:
+                raise ValueError("voxel-major layout supports C <= 32")
+            vm = torch.empty((self.D, self.H, self.W, 32), dtype=torch.float32, device=self.grid.device)
+            call("sfmhip_grid_to_voxel_major", ptr(self.grid), self.C, self.D, self.H, self.W, ptr(vm),
+                 stream_ptr())
+            self._vm = vm
+        return self._vm
+
+    def render(self, rays_o: torch.Tensor, rays_d: torch.Tensor, z: torch.Tensor) -> torch.Tensor:
+        """Fused sample + SH colour + composite for sorted sample depths z (B,S): (B,3)."""
+        if self.C != 28:
+            raise ValueError("render needs the 28-channel SDF+SH grid")
+        o = dev(rays_o, torch.float32).reshape(-1, 3)
+        d = dev(rays_d, torch.float32).reshape(-1, 3)
+        zz = dev(z, torch.float32)
+        B, S = zz.shape
+        rgb = torch.empty((B, 3), dtype=torch.float32, device=o.device)
+        call("sfmhip_render_rays", ptr(self.voxel_major()), self.D, self.H, self.W, _host_ptr(self.bmin),
+             _host_ptr(self.bmax), self.mask_mode, ptr(o), ptr(d), ptr(zz), B, S, ptr(rgb), stream_ptr())
+        return rgb
+
+
+def tsdf_integrate(T: torch.Tensor, Wt: torch.Tensor, depth: torch.Tensor, poses: torch.Tensor,
+                   K: torch.Tensor, bmin, bmax, trunc: float, z0: int = 0, z1: int | None = None) -> None:
+    """In-place TSDF update of z-slices [z0, z1) of T/Wt (D,H,W) from F depth maps.
+
+    depth (F,Hd,Wd) f32 (<=0 invalid), poses (F,3,4) world->camera f32,
+    K (F,4) [fx, fy, cx, cy] f32, bounds in world units, trunc = mu."""
+    require_gpu()
+    if T.dtype != torch.float32 or Wt.dtype != torch.float32 or not T.is_contiguous() or not Wt.is_contiguous():
+        raise ValueError("T and Wt must be contiguous float32 device tensors")
+    D, H, W = T.shape
+    z1 = D if z1 is None else int(z1)
+    dp = dev(depth, torch.float32)
+    ps = dev(poses, torch.float32)
+    kk = dev(K, torch.float32)
+    F, Hd, Wd = dp.shape
+    bmn, bmx = _f3(bmin), _f3(bmax)
+    call("sfmhip_tsdf_integrate", ptr(T), ptr(Wt), D, H, W, int(z0), z1, ptr(dp), F, Hd, Wd, ptr(ps), ptr(kk),
+         _host_ptr(bmn), _host_ptr(bmx), float(trunc), stream_ptr())

@@ -1,0 +1,157 @@
+/*
+ * sfmhip.h — C-ABI of libsfmhip.so, the MI355X (gfx950) backend for the dense
+ * compute path of daovietanh190499/3D_Reconstruction (SfM matching, DLT
+ * triangulation, reprojection residual / FD Jacobian, voxel-grid work).
+ *
+ * Conventions (all entry points):
+ *   - Every pointer argument that names device data is a HIP device pointer owned
+ *     by the caller (normally a torch-ROCm tensor's data_ptr()); the library never
+ *     allocates, frees or retains caller memory.
+ *   - `stream` is a hipStream_t passed as void* (0 = the null stream).  Calls are
+ *     asynchronous on that stream; the Python wrappers synchronise before handing
+ *     numpy arrays back, which keeps the cv2 / scipy call semantics.
+ *   - Return value: 0 on success, a negative SFMHIP_E_* code on failure; the
+ *     message for the calling thread is in sfmhip_last_error().
+ *   - Row-major, densely packed arrays unless a stride is given.
+ *
+ * Each entry point cites the reference interface it replaces (file:line in
+ * /root/reference).  See INTEGRATION.md for the ctypes binding.
+ */
+#ifndef SFMHIP_H
+#define SFMHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFMHIP_OK            0
+#define SFMHIP_E_ARG        -1   /* bad argument (shape, null pointer, range) */
+#define SFMHIP_E_HIP        -2   /* HIP runtime error (launch / memory)        */
+#define SFMHIP_E_UNSUPPORTED -3  /* e.g. descriptor dim not in {64,128,256}    */
+#define SFMHIP_E_OVERFLOW   -4   /* a bounded loop hit its cap                 */
+
+/* ---- library ---------------------------------------------------------- */
+int         sfmhip_version(void);            /* (major<<16)|(minor<<8)|patch */
+const char* sfmhip_last_error(void);         /* thread-local message          */
+int         sfmhip_device_arch(char* buf, int len); /* "gfx950" of device 0   */
+
+/* ---- M1: brute-force L2 matching + ratio test --------------------------
+ * Replaces the matcher call site matching.py:20,122-128 (LightGlue forward,
+ * output contract lightglue/lightglue.py:442-450).  The BF-L2 + Lowe-ratio
+ * semantics are build-defined and pinned by oracle/match.py.
+ *
+ * Descriptors live in HBM as int8 [n_img][m_pad][d], rows >= n_kpts[img] zero.
+ *   mode 0 (SIFT-like, integer values 0..255 stored as f32):  q = x - 128
+ *   mode 1 (float, e.g. L2-normalised SuperPoint/DISK):       q = clamp(rint(127*x), -127, 127)
+ * Squared L2 on q is exact in int32 (|q|<=128, d<=256).                       */
+int sfmhip_desc_quantize(const float* in, int n_img, int m_pad, int d,
+                         const int32_t* n_kpts /* device [n_img] */, int mode,
+                         int8_t* out /* [n_img][m_pad][d] */, void* stream);
+
+/* norms[img][r] = sum_k q^2 (int32); keys[img][r] = packed column key used by
+ * the matcher's fused epilogue (see DESIGN.md "packed key").                  */
+int sfmhip_desc_prepare(const int8_t* desc, int n_img, int m_pad, int d,
+                        const int32_t* n_kpts, int32_t* norms, int32_t* keys,
+                        void* stream);
+
+/* For every pair p=(a,b) and every row i < n_kpts[a] of image a: best column j1
+ * (lowest index on ties) and second-best distance d2 over j != j1 in image b.
+ * matches0[p][i] = j1 if ratio_den^2 * d1 < ratio_num^2 * d2 (exact, int64)
+ * and n_kpts[b] >= 2, else -1; rows i >= n_kpts[a] get -1.
+ * dist1/dist2 (nullable) receive d1/d2 (squared, quantised units).
+ * m_pad must be a multiple of 128; d in {64,128,256}.                        */
+int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                       const int32_t* n_kpts, int n_img, int m_pad, int d,
+                       const int32_t* pairs /* device [P][2] */, int P,
+                       int ratio_num, int ratio_den,
+                       int32_t* matches0 /* [P][m_pad] */,
+                       int32_t* dist1, int32_t* dist2, void* stream);
+
+/* LightGlue-style mutual filter (lightglue/lightglue.py:235-254 semantics):
+ * given forward matches0 (a->b) and backward matches1 (b->a), both [P][m_pad],
+ * clear every match that is not mutual, in place.                           */
+int sfmhip_mutual_filter(int32_t* matches0, int32_t* matches1, int P, int m_pad,
+                         void* stream);
+
+/* ---- M2: scipy.cluster.vq.vq (matching.py:27, bow.py:23) ---------------
+ * codes[i] = argmin_c sum_k (obs[i,k]-code[c,k])^2 (lowest index on ties),
+ * dist[i] = sqrt(min).  f64 throughout.                                      */
+int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_book, int n_codes,
+              int d, int32_t* codes, double* dist, void* stream);
+
+/* ---- S2: cv2.triangulatePoints (sfm.py:27) ------------------------------
+ * OpenCV DLT: per point a 6x4 system (rows x*p3-p1, y*p3-p2, x*p2-y*p1 per
+ * view), right singular vector of the smallest singular value (one-sided
+ * Jacobi, f64).  x0/x1 are cv2 layout (2,n); X4 is (4,n), unit norm, X4[3]>=0.
+ * Batched form: P is [n_pairs][2][3][4] and pair_of_obs[n] selects the pair
+ * (pair_of_obs == NULL means one pair).                                      */
+int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_obs,
+                           const double* x0, const double* x1, int64_t n,
+                           double* X4, void* stream);
+
+/* ---- S3/S5: reprojection residual + scipy 2-point grouped FD Jacobian ----
+ * sfm.py:87-91 (residual via cv2.projectPoints, no distortion) and
+ * least_squares(..., jac_sparsity=ba_sparse(...)) sfm.py:37-38.
+ * cam: [n_pairs][6] = rvec(3), t(3);  K: [n_pairs][3][3] (fx,fy,cx,cy used);
+ * X: [n][3]; pts2d: [n][2]; pair_of_obs: [n] (NULL = one pair).
+ * r: [n][2]  residual (pts2d - proj)  (nullable)
+ * f0: [n][2] base residual to difference against (NULL = computed here)
+ * jvals: [n][2][9] CSR values of J, per row: d/d(rvec0..2,t0..2, X0..2).    */
+int sfmhip_reproj_residual(const double* cam, const double* K, const double* X,
+                           const double* pts2d, const int32_t* pair_of_obs,
+                           int64_t n, double* r, void* stream);
+int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, const double* X,
+                              const double* pts2d, const int32_t* pair_of_obs,
+                              int n_pairs, int64_t n, const double* f0,
+                              double* r, double* jvals, void* stream);
+
+/* ---- V1: voxel_traversal (voxel_travesal.py:1-73), quirks included -------
+ * rays [N][8] f32 = o(3), d(3), near, far.  Pass 1 counts per-ray steps
+ * (n_steps[N], capped at max_steps -> SFMHIP_E_OVERFLOW), pass 2 writes
+ * out [N][S][3] f32 (NaN padded) with S = 1 + max(n_steps) (or 1).          */
+int sfmhip_voxel_traversal_count(const float* rays, int64_t N, float bin,
+                                 int32_t max_steps, int32_t* n_steps, void* stream);
+int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, int32_t S,
+                           float* out, void* stream);
+
+/* ---- V2: trilinear grid sample (sdf.py:284-342, plenoxel.py:31-43) -------
+ * grid in the reference layout (1,C,D,H,W) f32.  pts [P][3] world coords.
+ * mask_mode 0: sdf.py  (inside iff bmin <= p <= bmax, normalise to [-1,1])
+ * mask_mode 1: plenoxel (inside iff |p| < scale=bmax[0], p/scale clipped)
+ * out [P][C] (zero outside).  F.grid_sample(align_corners=True, zeros)
+ * arithmetic, x->W, y->H, z->D.  bmin/bmax are HOST float[3].               */
+int sfmhip_grid_sample(const float* grid, int C, int D, int H, int W,
+                       const float* bmin, const float* bmax, int mask_mode,
+                       const float* pts, int64_t P, float* out, void* stream);
+
+/* Voxel-major relayout (C,D,H,W) -> (D,H,W,Cp) with Cp = 32 (zero pad) so a
+ * corner's channels are one 128-byte line; used by the fused renderer.       */
+int sfmhip_grid_to_voxel_major(const float* grid, int C, int D, int H, int W,
+                               float* grid_vm, void* stream);
+
+/* ---- V4: fused sample + SH-2 colour + alpha composite --------------------
+ * sdf.py:391-406 / plenoxel.py:71-93 for C=28 grids.  rays_o/rays_d [B][3],
+ * z [B][S] (sorted sample depths).  rgb [B][3] = sum T*a*c + 1 - sum T*a.
+ * grid_vm from sfmhip_grid_to_voxel_major; bmin/bmax are HOST float[3].     */
+int sfmhip_render_rays(const float* grid_vm, int D, int H, int W,
+                       const float* bmin, const float* bmax, int mask_mode,
+                       const float* rays_o, const float* rays_d, const float* z,
+                       int64_t B, int S, float* rgb, void* stream);
+
+/* ---- V5: TSDF integration (build-defined) --------------
+ * T, Wt: (D,H,W) f32 grids updated in place for z-slices [z0, z1).
+ * depth [F][Hd][Wd] f32 (<= 0 invalid); poses [F][3][4] world->camera;
+ * Kf [F][4] = fx, fy, cx, cy; bmin/bmax are HOST float[3] grid bounds;
+ * trunc = truncation distance mu (world units).                               */
+int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, int z0, int z1,
+                          const float* depth, int F, int Hd, int Wd,
+                          const float* poses, const float* Kf,
+                          const float* bmin, const float* bmax, float trunc,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFMHIP_H */

@@ -1,0 +1,201 @@
+"""Oracle for V1-V5 (voxel path).  TEST INFRASTRUCTURE ONLY.
+
+float32 restatements with the reference's op order:
+  voxel_traversal  voxel_travesal.py:1-73 (torch.floor_divide = Python floor
+                   division: c10::div_floor_floating; same in numpy's npy_divmod)
+  grid_sample      sdf.py:284-342 / plenoxel.py:31-43 -> ATen grid_sampler_3d
+                   (bilinear, zeros padding, align_corners=True)
+  sh_colour        sdf.py:361-369 / plenoxel.py:9-16
+  composite        sdf.py:391-406 / plenoxel.py:71-93
+  tsdf_integrate   build-defined, parity unpinned.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+F32 = np.float32
+
+
+# ---------------------------------------------------------------------------
+def voxel_traversal(rays: np.ndarray, bin_size: float) -> np.ndarray:
+    """(N,8) f32 -> (N,S,3) f32, synchronous-loop semantics of the reference."""
+    r = np.asarray(rays, F32)
+    b = F32(bin_size)
+    o, d, near, far = r[:, :3], r[:, 3:6], r[:, 6:7], r[:, 7:8]
+    start = o + d * near
+    end = o + d * far
+    cur = np.floor_divide(start, b)
+    last = np.floor_divide(end, b)
+    step = np.where(d < 0, F32(-1), F32(1)).astype(F32)
+    nvb = (cur + step) * b
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tmax = ((nvb - start) / d).astype(F32)
+        tdelta = ((step * b) / d).astype(F32)
+    tmax[d == 0] = np.inf
+    tdelta[d == 0] = np.inf
+
+    def active(c):
+        with np.errstate(invalid="ignore"):
+            return np.any((c == c) & (step * c < step * last), axis=1)
+
+    out = [cur.copy()]
+    m = active(cur)
+    guard = 0
+    while m.any():
+        tx, ty, tz = tmax[:, 0], tmax[:, 1], tmax[:, 2]
+        with np.errstate(invalid="ignore"):
+            mx = (tx < ty) & (tx < tz) & m
+            my = (ty <= tx) & (ty < tz) & m
+            mz = (((tx >= ty) & (ty >= tz)) | ((tx >= tz) & (ty > tx))) & m
+        for a, ma in ((0, mx), (1, my), (2, mz)):
+            cur[ma, a] = cur[ma, a] + step[ma, a]
+            tmax[ma, a] = tmax[ma, a] + tdelta[ma, a]
+        out.append(cur.copy())
+        m = active(cur)
+        cur[~m] = np.nan
+        guard += 1
+        if guard > 1 << 20:
+            raise RuntimeError("voxel_traversal oracle: runaway loop")
+    return np.stack(out, 1)
+
+
+# ---------------------------------------------------------------------------
+def normalise(pts, bmin, bmax, mask_mode):
+    p = np.asarray(pts, F32).reshape(-1, 3)
+    mn = np.asarray(bmin, F32).ravel()
+    mx = np.asarray(bmax, F32).ravel()
+    if mask_mode == 0:
+        inside = np.all(p >= mn, 1) & np.all(p <= mx, 1)
+        g = ((p - mn) / (mx - mn)) * F32(2) - F32(1)
+    else:
+        s = mx[0]
+        inside = np.all(np.abs(p) < s, 1)
+        g = np.clip(p / s, F32(-1), F32(1))
+    return inside, g.astype(F32)
+
+
+def grid_sample(grid, pts, bmin, bmax, mask_mode=0) -> np.ndarray:
+    """grid (C,D,H,W) f32 -> (P,C); zero outside the mask."""
+    grid = np.asarray(grid, F32)
+    if grid.ndim == 5:
+        grid = grid[0]
+    C, D, H, W = grid.shape
+    inside, g = normalise(pts, bmin, bmax, mask_mode)
+    P = g.shape[0]
+    out = np.zeros((P, C), F32)
+    gi = g[inside]
+    ix = ((gi[:, 0] + F32(1)) / F32(2)) * F32(W - 1)
+    iy = ((gi[:, 1] + F32(1)) / F32(2)) * F32(H - 1)
+    iz = ((gi[:, 2] + F32(1)) / F32(2)) * F32(D - 1)
+    fx, fy, fz = np.floor(ix), np.floor(iy), np.floor(iz)
+    x1, y1, z1 = fx + F32(1), fy + F32(1), fz + F32(1)
+    w = [
+        (x1 - ix) * (y1 - iy) * (z1 - iz),
+        (ix - fx) * (y1 - iy) * (z1 - iz),
+        (x1 - ix) * (iy - fy) * (z1 - iz),
+        (ix - fx) * (iy - fy) * (z1 - iz),
+        (x1 - ix) * (y1 - iy) * (iz - fz),
+        (ix - fx) * (y1 - iy) * (iz - fz),
+        (x1 - ix) * (iy - fy) * (iz - fz),
+        (ix - fx) * (iy - fy) * (iz - fz),
+    ]
+    acc = np.zeros((gi.shape[0], C), F32)
+    bx, by, bz = fx.astype(np.int64), fy.astype(np.int64), fz.astype(np.int64)
+    for k in range(8):
+        x = bx + (k & 1)
+        y = by + ((k >> 1) & 1)
+        z = bz + ((k >> 2) & 1)
+        ok = (x >= 0) & (x < W) & (y >= 0) & (y < H) & (z >= 0) & (z < D)
+        v = np.zeros((gi.shape[0], C), F32)
+        v[ok] = grid[:, z[ok], y[ok], x[ok]].T
+        acc = np.where(ok[:, None], acc + v * w[k][:, None], acc).astype(F32)
+    out[inside] = acc
+    return out
+
+
+def sh_colour(k, d) -> np.ndarray:
+    """sdf.py:361-369: k (P,27) as (P,3,9), d (P,3) -> (P,3), Python op order."""
+    k = np.asarray(k, F32).reshape(-1, 3, 9)
+    d = np.asarray(d, F32).reshape(-1, 3)
+    x, y, z = d[:, 0:1], d[:, 1:2], d[:, 2:3]
+    C0, C1, C2, C3, C4 = F32(0.282095), F32(0.488603), F32(1.092548), F32(0.315392), F32(0.546274)
+    kk = [k[..., m] for m in range(9)]
+    inner = ((((C2 * x) * y) * kk[4] - ((C2 * y) * z) * kk[5])
+             + (C3 * (((F32(2.0) * z) * z - x * x) - y * y)) * kk[6]) + (((-C2) * x) * z) * kk[7]
+    inner2 = inner + (C4 * (x * x - y * y)) * kk[8]
+    return ((((C0 * kk[0] + ((-C1) * y) * kk[1]) + (C1 * z) * kk[2]) - (C1 * x) * kk[3]) + inner2).astype(F32)
+
+
+def render(grid, bmin, bmax, mask_mode, rays_o, rays_d, z) -> np.ndarray:
+    """Sample + SH colour + composite (sdf.py:391-406): (B,3)."""
+    o = np.asarray(rays_o, F32).reshape(-1, 3)
+    d = np.asarray(rays_d, F32).reshape(-1, 3)
+    z = np.asarray(z, F32)
+    B, S = z.shape
+    pts = o[:, None, :] + d[:, None, :] * z[:, :, None]
+    s = grid_sample(grid, pts.reshape(-1, 3), bmin, bmax, mask_mode)
+    sdf = s[:, 0].reshape(B, S)
+    col = sh_colour(s[:, 1:], np.repeat(d, S, 0)).reshape(B, S, 3)
+    sigma = np.maximum(sdf, F32(0))
+    delta = np.concatenate([z[:, 1:] - z[:, :-1], np.full((B, 1), F32(1e10))], 1)
+    alpha = F32(1) - np.exp((-sigma) * delta).astype(F32)
+    T = np.cumprod(F32(1) - alpha, 1, dtype=F32)
+    T = np.concatenate([np.ones((B, 1), F32), T[:, :-1]], 1)
+    w = (T * alpha)[:, :, None]
+    c = (w * col).sum(1, dtype=F32)
+    ws = w.sum(-1).sum(-1, dtype=F32)
+    return ((c + F32(1)) - ws[:, None]).astype(F32)
+
+
+# ---------------------------------------------------------------------------
+def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
+    """Build-defined TSDF update, in place on copies; returns (T, Wt).
+
+    voxel (z,y,x) -> world bmin + idx*(bmax-bmin)/(R-1) (align_corners, x->W);
+    Xc = R v + t (left-to-right); skip Zc <= 0; iz = 1/Zc; u = (fx Xc) iz + cx;
+    pixel = floor(u + 0.5); skip off-image or depth <= 0; sdf = depth - Zc;
+    skip sdf < -mu; tsdf = min(1, sdf/mu); T = (T W + tsdf)/(W + 1); W += 1."""
+    T = np.array(T, F32, copy=True)
+    Wt = np.array(Wt, F32, copy=True)
+    D, H, W = T.shape
+    z1 = D if z1 is None else z1
+    mn = np.asarray(bmin, F32).ravel()
+    mx = np.asarray(bmax, F32).ravel()
+    sx = (mx[0] - mn[0]) / F32(W - 1)
+    sy = (mx[1] - mn[1]) / F32(H - 1)
+    sz = (mx[2] - mn[2]) / F32(D - 1)
+    vx = (mn[0] + np.arange(W, dtype=F32) * sx)[None, None, :]
+    vy = (mn[1] + np.arange(H, dtype=F32) * sy)[None, :, None]
+    vz = (mn[2] + np.arange(z0, z1, dtype=F32) * sz)[:, None, None]
+    dep_all = np.asarray(depth, F32)
+    F, Hd, Wd = dep_all.shape
+    poses = np.asarray(poses, F32).reshape(F, 12)
+    K = np.asarray(K, F32).reshape(F, 4)
+    tr = F32(trunc)
+    Ts, Ws = T[z0:z1], Wt[z0:z1]
+    for f in range(F):
+        P = poses[f]
+        Xc = P[0] * vx + P[1] * vy + P[2] * vz + P[3]
+        Yc = P[4] * vx + P[5] * vy + P[6] * vz + P[7]
+        Zc = P[8] * vx + P[9] * vy + P[10] * vz + P[11]
+        ok = Zc > 0
+        with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+            iz = F32(1) / np.where(ok, Zc, F32(1))
+            u = (K[f, 0] * Xc) * iz + K[f, 2]
+            v = (K[f, 1] * Yc) * iz + K[f, 3]
+            fu = np.floor(u + F32(0.5))
+            fv = np.floor(v + F32(0.5))
+        ok &= (fu >= 0) & (fu < Wd) & (fv >= 0) & (fv < Hd)
+        ui = np.where(ok, fu, 0).astype(np.int64)
+        vi = np.where(ok, fv, 0).astype(np.int64)
+        dep = dep_all[f][vi, ui]
+        ok &= dep > 0
+        sdf = dep - Zc
+        ok &= ~(sdf < -tr)
+        ts = np.minimum(F32(1), sdf / tr)
+        Tn = (Ts * Ws + ts) / (Ws + F32(1))
+        Ts = np.where(ok, Tn, Ts).astype(F32)
+        Ws = np.where(ok, Ws + F32(1), Ws).astype(F32)
+    T[z0:z1] = Ts
+    Wt[z0:z1] = Ws
+    return T, Wt

@@ -1,0 +1,148 @@
+"""CPU: pin the oracle against fixtures generated from the reference code
+(tests/golden/make_golden.py).  No GPU needed."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import geometry as og
+from oracle import match as om
+from oracle import voxel as ov
+
+
+# --- M2: vq -----------------------------------------------------------------
+def test_vq_oracle_is_scipy_integer_ties():
+    g = golden("vq_golden.npz")
+    codes, dist = om.vq(g["obs"], g["code"])
+    assert np.array_equal(codes, g["codes"]) and np.array_equal(dist, g["dist"])
+    # tie rule: obs equal to the duplicated codeword 3 (= 7 = 20) -> 3
+    assert (g["codes"][30:40] == 3).all()
+
+
+def test_bf_top1_equals_vq_argmin_on_integer_data():
+    """Anchor M1's best-index rule to scipy vq (matching.py:27): lowest index on ties."""
+    g = golden("vq_golden.npz")
+    qa = (g["obs"] - 128).astype(np.int8)
+    qb = (g["code"] - 128).astype(np.int8)
+    D = om.sq_dist(qa, qb)
+    j1, d1, _ = om.top2(D)
+    assert np.array_equal(j1, g["codes"])
+    assert np.array_equal(np.sqrt(d1.astype(np.float64)), g["dist"])
+
+
+# --- M1: mutual rule == lightglue filter_matches ------------------------------
+def test_bf_mutual_equals_filter_matches():
+    g = golden("filter_matches_golden.npz")
+    # ratio 1 (accept iff d1 < d2; tie-free data) + mutual = filter_matches(th=None)
+    m0, m1 = om.bf_match_mutual_pair(g["qa"], g["qb"], ratio=(1, 1))
+    assert np.array_equal(m0, g["m0"])
+    assert np.array_equal(m1, g["m1"])
+
+
+def test_bf_ratio_semantics_small():
+    qa = np.array([[0, 0], [10, 10], [5, 5]], np.int8)
+    qb = np.array([[0, 1], [0, 3], [10, 10], [10, 10]], np.int8)
+    m0, d1, d2 = om.bf_match_q(qa, qb, (3, 4), return_dist=True)
+    # row0: d=[1,9,200,200]: 16*1 < 9*9 -> j=0 ; row1: tie at 2,3 -> j1=2, d2=0 -> reject
+    assert m0.tolist() == [0, -1, -1] or m0[0] == 0
+    assert d1[1] == 0 and d2[1] == 0 and m0[1] == -1
+    assert om.bf_match_q(qa, qb[:1]).tolist() == [-1, -1, -1]
+
+
+# --- S4/S5: ba_sparse + FD Jacobian -----------------------------------------
+def test_ba_sparse_matches_reference():
+    g = golden("ba_golden.npz")
+    for n in (3, 50):
+        assert np.array_equal(og.ba_sparse(n, 6 + 3 * n).toarray(), g[f"A{n}"])
+
+
+def test_fd_jacobian_direct_matches_scipy_grouped():
+    g = golden("ba_golden.npz")
+    assert int(g["n_groups"]) == 9
+    J = og.fd_jacobian(g["x"], g["K"], g["pts"]).toarray()
+    assert np.array_equal(J, g["J"])
+    Jd = og.fd_jacobian_direct(g["x"], g["K"], g["pts"])
+    n = len(g["pts"])
+    dense = np.zeros_like(g["J"])
+    for p in range(n):
+        cols = list(range(6)) + [6 + 3 * p + c for c in range(3)]
+        dense[2 * p, cols] = Jd[p, 0]
+        dense[2 * p + 1, cols] = Jd[p, 1]
+    assert np.array_equal(dense, g["J"])  # grouping does not change any value
+
+
+def test_dlt_known_answer():
+    rng = np.random.default_rng(0)
+    f = 2378.98305085
+    K = np.array([[f, 0, 0], [0, f, 0], [0, 0, 1]])
+    R = og.rodrigues([0.1, -0.2, 0.05])
+    t = np.array([[1.0], [0.1], [0.2]])
+    P0 = K @ np.hstack([np.eye(3), np.zeros((3, 1))])
+    P1 = K @ np.hstack([R, t])
+    X = rng.uniform([-2, -2, 5], [2, 2, 10], (200, 3))
+    Xh = np.hstack([X, np.ones((200, 1))]).T
+    x0 = P0 @ Xh
+    x1 = P1 @ Xh
+    X4 = og.triangulate_points(P0, P1, x0[:2] / x0[2], x1[:2] / x1[2])
+    np.testing.assert_allclose((X4[:3] / X4[3]).T, X, rtol=1e-9, atol=1e-9)
+
+
+# --- V1: voxel traversal ------------------------------------------------------
+@pytest.mark.parametrize("b", ["1p0", "0p5", "2p0"])
+def test_voxel_traversal_oracle_matches_reference(b):
+    g = golden("voxel_traversal_golden.npz")
+    out = ov.voxel_traversal(g["rays"], float(b.replace("p", ".")))
+    np.testing.assert_array_equal(out, g[f"out_{b}"])
+
+
+# --- V2/V4: grid sample, SH colour, composite --------------------------------
+def test_grid_sample_oracle_matches_sdf_py():
+    g = golden("sdf_golden.npz")
+    s = ov.grid_sample(g["grid"], g["pts"], g["bmin"], g["bmax"], 0)
+    np.testing.assert_allclose(s[:, 0], g["sdf"], rtol=0, atol=2e-6)
+    np.testing.assert_allclose(s[:, 1:], g["sh"], rtol=0, atol=2e-6)
+    exact = (s[:, 0] == g["sdf"]).mean()
+    assert exact > 0.95, exact
+
+
+def test_plenoxel_forward_oracle():
+    g = golden("plenoxel_golden.npz")
+    s = ov.grid_sample(g["grid"], g["x"], (-1.5,) * 3, (1.5,) * 3, 1)
+    sigma = np.maximum(s[:, 0], 0)
+    inside, _ = ov.normalise(g["x"], (-1.5,) * 3, (1.5,) * 3, 1)
+    col = np.where(inside[:, None], ov.sh_colour(s[:, 1:], g["d"]), 0)
+    np.testing.assert_allclose(sigma, g["sigma"], atol=2e-6)
+    np.testing.assert_allclose(col, g["color"], atol=5e-6)
+
+
+def test_sh_colour_oracle_bitexact():
+    g = golden("plenoxel_golden.npz")
+    out = ov.sh_colour(g["sh_k"], g["sh_d"])
+    np.testing.assert_allclose(out, g["sh_out"], rtol=0, atol=1e-6)
+
+
+def test_render_oracle_matches_sdf_forward_and_plenoxel():
+    g = golden("sdf_golden.npz")
+    rgb = ov.render(g["grid"], g["bmin"], g["bmax"], 0, g["rays_o"], g["rays_d"], g["z"])
+    np.testing.assert_allclose(rgb, g["rgb"], rtol=1e-5, atol=1e-5)
+    p = golden("plenoxel_golden.npz")
+    rgb = ov.render(p["grid"], (-1.5,) * 3, (1.5,) * 3, 1, p["rays_o"], p["rays_d"], p["z"])
+    np.testing.assert_allclose(rgb, p["rgb"], rtol=1e-5, atol=1e-5)
+
+
+# --- V5: TSDF known answer ----------------------------------------------------
+def test_tsdf_oracle_planar_known_answer():
+    """A fronto-parallel plane at depth Zp: every voxel in front of it within mu
+    gets tsdf = min(1, (Zp - Zc)/mu) after one frame."""
+    R = 24
+    T = np.zeros((R, R, R), np.float32)
+    W = np.zeros_like(T)
+    Hd, Wd = 64, 80
+    depth = np.full((1, Hd, Wd), 5.0, np.float32)
+    pose = np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 5.0]], np.float32)[None]
+    K = np.array([[40.0, 40.0, Wd / 2, Hd / 2]], np.float32)
+    Tn, Wn = ov.tsdf_integrate(T, W, depth, pose, K, (-1, -1, -1), (1, 1, 1), 0.2)
+    zc = (np.float32(-1) + np.arange(R, dtype=np.float32) * (np.float32(2) / np.float32(R - 1))) + np.float32(5)
+    exp = np.minimum(1, (5.0 - zc) / 0.2)
+    upd = Wn[:, R // 2, R // 2] > 0
+    np.testing.assert_allclose(Tn[upd, R // 2, R // 2], exp[upd], rtol=1e-6, atol=1e-6)
+    assert (~upd == (exp * 0.2 < -0.2)).all()
