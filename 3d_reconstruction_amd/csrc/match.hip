@@ -20,6 +20,7 @@
 //   * nothing of the M x N distance matrix is ever written.
 #include "common.h"
 #include <climits>
+#include <cstdlib>
 
 namespace sfmhip {
 
@@ -27,10 +28,6 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kJB = 128;              // candidate rows per staged LDS block (7-bit local index)
-constexpr int kIW = 64;               // query rows per wave (two 32-wide MFMA column tiles)
-constexpr int kWaves = 8;             // waves per workgroup (2 per SIMD)
-constexpr int kIB = kIW * kWaves;     // query rows per workgroup
-constexpr int kThreads = 64 * kWaves;
 
 // Byte offset of logical 16-byte chunk c of row r inside a [rows][D] int8 LDS
 // tile.  XOR swizzle makes the 16 rows a ds_read_b128 lane group touches land
@@ -108,19 +105,91 @@ __global__ void prepare_kernel(const int8_t* __restrict__ desc, int n_rows, int 
 }
 
 // ---------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(kThreads, 2) void match_kernel(
+// Stage candidate block `blk` of image b into LDS buffer `dst` (XOR-swizzled
+// rows) and its 128 packed keys into `kdst`.
+//   GLDS=true : LDS-DMA (global_load_lds_dwordx4): the LDS image is lane-linear
+//               per wave-instruction, so the swizzle moves to the per-lane SOURCE
+//               chunk (cdna_hip_programming.md §5.4 rule 21).  No VGPRs.
+//   GLDS=false: register staging (load now, ds_write later).
+template <int D, int WAVES>
+struct Stager {
+    static constexpr int CPR = D / 16;                 // 16-B chunks per row
+    static constexpr int RPB = 256 / D;                // rows per 256-B bank row
+    static constexpr int TILE = kJB * D;               // bytes per block
+    static constexpr int NI = TILE / 1024;             // 1-KiB wave-instructions per block
+    static constexpr int PER_WAVE = NI / WAVES;        // per wave
+    static constexpr int LDT = TILE / 16 / (64 * WAVES);  // 16-B register loads per thread
+    static_assert(NI % WAVES == 0 && LDT >= 1, "block / workgroup mismatch");
+
+    __device__ static void dma(const int8_t* src, const int32_t* ksrc, int8_t* dst, int32_t* kdst, int wave,
+                               int lane) {
+#pragma unroll
+        for (int u = 0; u < PER_WAVE; ++u) {
+            const int ins = wave * PER_WAVE + u;
+            const int rows_per_ins = 1024 / D;
+            const int r0 = ins * rows_per_ins;
+            const int r = r0 + lane / CPR;
+            const int c = (lane % CPR) ^ ((r / RPB) % CPR);
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void*)(src + (size_t)r * D + c * 16),
+                (__attribute__((address_space(3))) void*)(dst + r0 * D), 16, 0, 0);
+        }
+        if (wave == WAVES - 1) {  // 128 keys = 2 x (64 lanes x 4 B)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                __builtin_amdgcn_global_load_lds(
+                    (__attribute__((address_space(1))) void*)(ksrc + u * 64 + lane),
+                    (__attribute__((address_space(3))) void*)(kdst + u * 64), 4, 0, 0);
+        }
+    }
+};
+
+// MFMA shape traits.  MF = output tile edge (32: v_mfma_i32_32x32x32_i8,
+// 16: v_mfma_i32_16x16x64_i8).  Both give lane l the 16 bytes of tile row
+// (l % MF) for k-chunk group (l / MF), and D/C layouts
+//   32x32: col = l % 32, row = (q & 3) + 8 (q >> 2) + 4 (l / 32)   (q < 16)
+//   16x16: col = l % 16, row = 4 (l / 16) + q                      (q < 4)
+// The k order inside an MFMA is irrelevant here: A and B use the same map.
+template <int MF> struct Mfma;
+template <> struct Mfma<32> {
+    using acc_t = i32x16;
+    static constexpr int NREG = 16, KB = 32;   // accumulators per lane, k bytes per MFMA
+    __device__ static acc_t run(i32x4 a, i32x4 b, acc_t c) {
+        return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+    }
+    __device__ static int row(int q, int grp) { return (q & 3) + 8 * (q >> 2) + 4 * grp; }
+};
+template <> struct Mfma<16> {
+    using acc_t = i32x4;
+    static constexpr int NREG = 4, KB = 64;
+    __device__ static acc_t run(i32x4 a, i32x4 b, acc_t c) {
+        return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+    }
+    __device__ static int row(int q, int grp) { return 4 * grp + q; }
+};
+
+// One workgroup = one pair x (WAVES * NS * MF) query rows of image a.  Each
+// wave owns NS column tiles of MF query rows as resident B-operand fragments
+// and streams image b's 128-row blocks from the LDS ring (LDS-DMA filled).
+template <int D, int MF, int NS, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
     const int8_t* __restrict__ desc, const int32_t* __restrict__ norms,
     const int32_t* __restrict__ keys, const int32_t* __restrict__ nk, int m_pad,
     const int32_t* __restrict__ pairs, int n_iblk, int nwg, long long rn2, long long rd2,
     int32_t* __restrict__ m0, int32_t* __restrict__ dist1, int32_t* __restrict__ dist2) {
-    constexpr int KK = D / 32;                      // MFMA k-steps per descriptor
-    constexpr int CPR = D / 16;                     // 16-byte chunks per row
-    constexpr int TILE = kJB * D;                   // bytes per staged block
-    constexpr int LDT = kJB * CPR / kThreads;       // 16-byte loads per thread per block
-    static_assert(LDT >= 1, "tile too small for the workgroup");
+    using S = Stager<D, WAVES>;
+    using M = Mfma<MF>;
+    using acc_t = typename M::acc_t;
+    constexpr int KK = D / M::KB;                   // MFMAs per output tile
+    constexpr int CPK = M::KB / 16;                 // 16-B chunks per MFMA k-step
+    constexpr int NG = 64 / MF;                     // lane groups sharing a query row
+    constexpr int TILE = S::TILE;
+    constexpr int NT = 64 * WAVES;
+    constexpr int IW = MF * NS;                     // query rows per wave
+    constexpr int IB = IW * WAVES;                  // query rows per workgroup
+    constexpr int JT = kJB / MF;                    // candidate tiles per block
+    static_assert(NS % NG == 0 || NG % NS == 0, "output lane mapping");
 
-    // All LDS in ONE array (cdna_hip_programming.md §5 item 4(a)).
     __shared__ __attribute__((aligned(16))) int8_t lds[2 * TILE + 2 * kJB * 4];
 
     const int wg = xcd_remap(blockIdx.x, nwg);
@@ -128,13 +197,13 @@ __global__ __launch_bounds__(kThreads, 2) void match_kernel(
     const int a = pairs[2 * pair], b = pairs[2 * pair + 1];
     const int na_rows = nk[a], nb_rows = nk[b];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int h = lane >> 5, l32 = lane & 31;
-    const int ibase = ib * kIB;
+    const int grp = lane / MF, lr = lane % MF;
+    const int ibase = ib * IB + wave * IW;
     int32_t* out_m = m0 + (size_t)pair * m_pad;
 
-    if (ibase >= na_rows || nb_rows < 2) {  // block-uniform: nothing to match
-        const int iend = min(ibase + kIB, m_pad);
-        for (int i = ibase + tid; i < iend; i += kThreads) {
+    if (ib * IB >= na_rows || nb_rows < 2) {  // block-uniform: nothing to match
+        const int iend = min(ib * IB + IB, m_pad);
+        for (int i = ib * IB + tid; i < iend; i += NT) {
             out_m[i] = -1;
             if (dist1) dist1[(size_t)pair * m_pad + i] = -1;
             if (dist2) dist2[(size_t)pair * m_pad + i] = -1;
@@ -142,117 +211,98 @@ __global__ __launch_bounds__(kThreads, 2) void match_kernel(
         return;
     }
 
-    // Query rows of image a -> MFMA B-operand fragments, resident for the run.
-    i32x4 bi0[KK], bi1[KK];
-    {
-        const int i0 = min(ibase + wave * kIW + l32, m_pad - 1);
-        const int i1 = min(ibase + wave * kIW + 32 + l32, m_pad - 1);
-        const int8_t* r0 = desc + ((size_t)a * m_pad + i0) * D + h * 16;
-        const int8_t* r1 = desc + ((size_t)a * m_pad + i1) * D + h * 16;
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-            bi0[kk] = *reinterpret_cast<const i32x4*>(r0 + kk * 32);
-            bi1[kk] = *reinterpret_cast<const i32x4*>(r1 + kk * 32);
-        }
-    }
-
     const int8_t* bdesc = desc + (size_t)b * m_pad * D;
     const int32_t* bkeys = keys + (size_t)b * m_pad;
     const int nblk = (nb_rows + kJB - 1) / kJB;
+    int32_t* kbase = reinterpret_cast<int32_t*>(lds + 2 * TILE);
 
-    i32x4 stg[LDT];
-    i32x4 kstg = {0, 0, 0, 0};
-    auto gload = [&](int blk) {
-        const int8_t* src = bdesc + (size_t)blk * TILE;
+    S::dma(bdesc, bkeys, lds, kbase, wave, lane);  // block 0 in flight
+
+    // Query rows of image a -> MFMA B-operand fragments, resident for the run.
+    i32x4 bq[NS][KK];
 #pragma unroll
-        for (int u = 0; u < LDT; ++u)
-            stg[u] = *reinterpret_cast<const i32x4*>(src + (size_t)(tid + u * kThreads) * 16);
-        if (tid < kJB / 4) kstg = *reinterpret_cast<const i32x4*>(bkeys + blk * kJB + tid * 4);
-    };
-    auto swrite = [&](int buf) {
-        int8_t* dst = lds + buf * TILE;
+    for (int s = 0; s < NS; ++s) {
+        const int i = min(ibase + s * MF + lr, m_pad - 1);
+        const int8_t* rp = desc + ((size_t)a * m_pad + i) * D + grp * 16;
 #pragma unroll
-        for (int u = 0; u < LDT; ++u) {
-            const int q = tid + u * kThreads;
-            *reinterpret_cast<i32x4*>(dst + swz_off<D>(q / CPR, q % CPR)) = stg[u];
-        }
-        if (tid < kJB / 4)
-            *reinterpret_cast<i32x4*>(lds + 2 * TILE + buf * kJB * 4 + tid * 16) = kstg;
-    };
+        for (int kk = 0; kk < KK; ++kk) bq[s][kk] = *reinterpret_cast<const i32x4*>(rp + kk * M::KB);
+    }
 
-    int g1k0 = INT_MIN, g1i0 = 0, g2k0 = INT_MIN;
-    int g1k1 = INT_MIN, g1i1 = 0, g2k1 = INT_MIN;
+    int g1k[NS], g1i[NS], g2k[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) { g1k[s] = INT_MIN; g1i[s] = 0; g2k[s] = INT_MIN; }
 
-    gload(0);
-    swrite(0);
     __syncthreads();
 
     for (int blk = 0; blk < nblk; ++blk) {
         const int cur = blk & 1;
-        if (blk + 1 < nblk) gload(blk + 1);  // next block in flight under the MFMAs
+        if (blk + 1 < nblk)  // next block in flight under the MFMAs
+            S::dma(bdesc + (size_t)(blk + 1) * TILE, bkeys + (blk + 1) * kJB, lds + (cur ^ 1) * TILE,
+                   kbase + (cur ^ 1) * kJB, wave, lane);
         const int8_t* tl = lds + cur * TILE;
-        const int32_t* kl = reinterpret_cast<const int32_t*>(lds + 2 * TILE + cur * kJB * 4);
-        int t1a = INT_MIN, t2a = INT_MIN, t1b = INT_MIN, t2b = INT_MIN;
+        const int32_t* kl = kbase + cur * kJB;
+        int t1[NS], t2[NS];
 #pragma unroll
-        for (int jt = 0; jt < kJB / 32; ++jt) {
-            i32x16 acc0 = {0}, acc1 = {0};
-            const int r = jt * 32 + l32;
+        for (int s = 0; s < NS; ++s) { t1[s] = INT_MIN; t2[s] = INT_MIN; }
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) {
+            acc_t acc[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) acc[s] = acc_t{0};
+            const int r = jt * MF + lr;
 #pragma unroll
             for (int kk = 0; kk < KK; ++kk) {
-                const i32x4 av = *reinterpret_cast<const i32x4*>(tl + swz_off<D>(r, kk * 2 + h));
-                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bi0[kk], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bi1[kk], acc1, 0, 0, 0);
-            }
-            // acc reg q holds candidate row (q&3) + 8(q>>2) + 4h of this 32-row tile.
+                const i32x4 av = *reinterpret_cast<const i32x4*>(tl + swz_off<D>(r, kk * CPK + grp));
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const i32x4 kv = *reinterpret_cast<const i32x4*>(kl + jt * 32 + 8 * g + 4 * h);
+                for (int s = 0; s < NS; ++s) acc[s] = M::run(av, bq[s][kk], acc[s]);
+            }
+#pragma unroll
+            for (int g = 0; g < M::NREG / 4; ++g) {
+                const i32x4 kv = *reinterpret_cast<const i32x4*>(kl + jt * MF + M::row(4 * g, grp));
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int ka = acc0[4 * g + e] * 256 + kv[e];
-                    t2a = med3i(t2a, ka, t1a);
-                    t1a = max(t1a, ka);
-                    const int kb = acc1[4 * g + e] * 256 + kv[e];
-                    t2b = med3i(t2b, kb, t1b);
-                    t1b = max(t1b, kb);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) {
+                        const int kx = acc[s][4 * g + e] * 256 + kv[e];
+                        t2[s] = med3i(t2[s], kx, t1[s]);
+                        t1[s] = max(t1[s], kx);
+                    }
                 }
             }
         }
         // merge this block's top-2 into the running (key, index, second key)
-        {
-            const int k1 = t1a >> 7, k2 = t2a >> 7, ix = blk * kJB + 127 - (t1a & 127);
-            if (k1 > g1k0) { g2k0 = max(g1k0, k2); g1k0 = k1; g1i0 = ix; }
-            else           { g2k0 = max(g2k0, k1); }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int k1 = t1[s] >> 7, k2 = t2[s] >> 7, ix = blk * kJB + 127 - (t1[s] & 127);
+            if (k1 > g1k[s]) { g2k[s] = max(g1k[s], k2); g1k[s] = k1; g1i[s] = ix; }
+            else             { g2k[s] = max(g2k[s], k1); }
         }
-        {
-            const int k1 = t1b >> 7, k2 = t2b >> 7, ix = blk * kJB + 127 - (t1b & 127);
-            if (k1 > g1k1) { g2k1 = max(g1k1, k2); g1k1 = k1; g1i1 = ix; }
-            else           { g2k1 = max(g2k1, k1); }
-        }
-        if (blk + 1 < nblk) swrite(cur ^ 1);
-        __syncthreads();
+        __syncthreads();  // drains this wave's DMA; next block visible to all waves
     }
 
-    // lanes l and l^32 hold the same query row, disjoint candidate rows: merge.
-    auto merge = [](int& k1, int& i1, int& k2) {
-        const int ok = __shfl_xor(k1, 32), oi = __shfl_xor(i1, 32), o2 = __shfl_xor(k2, 32);
-        const bool mine = (k1 > ok) || (k1 == ok && i1 < oi);
-        const int n2 = mine ? max(k2, ok) : max(o2, k1);
-        if (!mine) { k1 = ok; i1 = oi; }
-        k2 = n2;
-    };
-    merge(g1k0, g1i0, g2k0);
-    merge(g1k1, g1i1, g2k1);
-
-    const int i = ibase + wave * kIW + h * 32 + l32;  // lane half h writes column tile h
-    if (i < m_pad) {
-        const int k1 = h ? g1k1 : g1k0, i1 = h ? g1i1 : g1i0, k2 = h ? g2k1 : g2k0;
+    // lanes of the NG groups hold the same query row, disjoint candidate rows.
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+#pragma unroll
+        for (int off = MF; off < 64; off <<= 1) {
+            const int ok = __shfl_xor(g1k[s], off), oi = __shfl_xor(g1i[s], off), o2 = __shfl_xor(g2k[s], off);
+            const bool mine = (g1k[s] > ok) || (g1k[s] == ok && g1i[s] < oi);
+            const int n2 = mine ? max(g2k[s], ok) : max(o2, g1k[s]);
+            if (!mine) { g1k[s] = ok; g1i[s] = oi; }
+            g2k[s] = n2;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (s % NG != grp % NS) continue;   // one lane group writes each tile
+        const int i = ibase + s * MF + lr;
+        if (i >= m_pad) continue;
         int res = -1, d1 = -1, d2 = -1;
         if (i < na_rows) {
             const int na = norms[(size_t)a * m_pad + i];
-            d1 = na - k1;
-            d2 = na - k2;
-            if (rd2 * (long long)d1 < rn2 * (long long)d2) res = i1;
+            d1 = na - g1k[s];
+            d2 = na - g2k[s];
+            if (rd2 * (long long)d1 < rn2 * (long long)d2) res = g1i[s];
         }
         out_m[i] = res;
         if (dist1) dist1[(size_t)pair * m_pad + i] = d1;
@@ -357,29 +407,39 @@ extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, cons
     SFMHIP_REQUIRE(ratio_num > 0 && ratio_den > 0 && ratio_num <= 65535 && ratio_den <= 65535,
                    "sfmhip_match_pairs: ratio must be a positive fraction");
     if (P == 0) return SFMHIP_OK;
-    const int n_iblk = ceil_div(m_pad, kIB);
+    // Variant (SFMHIP_MATCH_VARIANT, for A/B runs): {MFMA tile, tiles/wave, waves/WG}
+    //   0: 16x16, 4, 4 (default; fastest measured)   1: 32x32, 2, 4   2: 16x16, 8, 4   3: 32x32, 4, 4   4: 16x16, 4, 8
+    const char* venv = std::getenv("SFMHIP_MATCH_VARIANT");
+    const int variant = venv ? std::atoi(venv) : 0;
+    static const int kIBv[5] = {256, 256, 512, 512, 512};
+    const int iblk = kIBv[(variant >= 0 && variant < 5) ? variant : 0];
+    const int n_iblk = ceil_div(m_pad, iblk);
     const int64_t nwg64 = (int64_t)P * n_iblk;
     SFMHIP_REQUIRE(nwg64 < INT_MAX, "sfmhip_match_pairs: too many pairs for one launch");
     const int nwg = (int)nwg64;
     const long long rn2 = (long long)ratio_num * ratio_num, rd2 = (long long)ratio_den * ratio_den;
     hipStream_t s = as_stream(stream);
+#define SFMHIP_LAUNCH_MATCH(DD, MF, NS, WW)                                                              \
+    hipLaunchKernelGGL((match_kernel<DD, MF, NS, WW>), dim3(nwg), dim3(64 * WW), 0, s, desc, norms, keys, \
+                       n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2)
+#define SFMHIP_LAUNCH_D(DD)                                        \
+    switch (variant) {                                             \
+        case 1: SFMHIP_LAUNCH_MATCH(DD, 32, 2, 4); break;          \
+        case 2: SFMHIP_LAUNCH_MATCH(DD, 16, 8, 4); break;          \
+        case 3: SFMHIP_LAUNCH_MATCH(DD, 32, 4, 4); break;          \
+        case 4: SFMHIP_LAUNCH_MATCH(DD, 16, 4, 8); break;          \
+        default: SFMHIP_LAUNCH_MATCH(DD, 16, 4, 4); break;         \
+    }
     switch (d) {
-        case 64:
-            hipLaunchKernelGGL(match_kernel<64>, dim3(nwg), dim3(kThreads), 0, s, desc, norms, keys,
-                               n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2);
-            break;
-        case 128:
-            hipLaunchKernelGGL(match_kernel<128>, dim3(nwg), dim3(kThreads), 0, s, desc, norms, keys,
-                               n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2);
-            break;
-        case 256:
-            hipLaunchKernelGGL(match_kernel<256>, dim3(nwg), dim3(kThreads), 0, s, desc, norms, keys,
-                               n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2);
-            break;
+        case 64: SFMHIP_LAUNCH_D(64); break;
+        case 128: SFMHIP_LAUNCH_D(128); break;
+        case 256: SFMHIP_LAUNCH_D(256); break;
         default:
             set_error("sfmhip_match_pairs: descriptor dim %d not in {64,128,256}", d);
             return SFMHIP_E_UNSUPPORTED;
     }
+#undef SFMHIP_LAUNCH_D
+#undef SFMHIP_LAUNCH_MATCH
     return check_launch("match_kernel");
 }
 

@@ -5,6 +5,8 @@
 // All fp32 with -ffp-contract=off so the op order matches oracle/voxel.py.
 #include "common.h"
 #include <climits>
+#include <cstdlib>
+#include <algorithm>
 
 namespace sfmhip {
 
@@ -293,66 +295,116 @@ __global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ g
 }
 
 // ---------------------------------------------------------------------------
-// V5: TSDF integration.  Workgroup = 16(x) x 4(y) x 4(z) voxels; every thread
-// keeps its voxel's (T, W) in registers across all F frames, so the grid is
-// read and written once per call; poses/intrinsics staged in LDS.
-constexpr int kTsdfMaxFramesLds = 512;
+// V5: TSDF integration.  Every thread keeps ONE voxel's (T, W) in registers
+// across all frames of the launch, so the grid is read and written once per
+// launch; poses/intrinsics are staged in LDS.  The kernel is bound by the
+// depth gathers: the thread->voxel map decides how many cache lines a wave's
+// 64 gathers touch (MAP 0: a wave = 16 x by 4 z at one y, i.e. one image-row
+// band for orbiting cameras; MAP 1: 16 x by 4 y; MAP 2: 8 x by 8 z; MAP 3: 64 x).
+// U frames' projections + gathers are issued before their (ordered) updates.
+constexpr int kTsdfMaxFrames = 512;   // frames per launch (host splits longer runs)
 
+template <int MAP>
+__device__ __forceinline__ void tsdf_map(int t, int& x, int& y, int& z) {
+    // tile of 256 threads: returns offsets inside the tile (extents in tsdf_tile)
+    if (MAP == 0) { x = t & 15; z = (t >> 4) & 3; y = t >> 6; }            // 16 x 4(y) x 4(z), wave = x*z
+    else if (MAP == 1) { x = t & 15; y = (t >> 4) & 3; z = t >> 6; }       // wave = x*y
+    else if (MAP == 2) { x = t & 7; z = (t >> 3) & 7; y = t >> 6; }        // 8 x 4(y) x 8(z), wave = x*z
+    else { x = t & 63; y = 0; z = t >> 6; }                                // 64 x 1 x 4
+}
+template <int MAP> struct TsdfTile;
+template <> struct TsdfTile<0> { static constexpr int X = 16, Y = 4, Z = 4; };
+template <> struct TsdfTile<1> { static constexpr int X = 16, Y = 4, Z = 4; };
+template <> struct TsdfTile<2> { static constexpr int X = 8, Y = 4, Z = 8; };
+template <> struct TsdfTile<3> { static constexpr int X = 64, Y = 1, Z = 4; };
+
+// Spatially compact brick order: the 1-D grid is dealt round-robin over the 8
+// XCDs, so xcd_remap gives each XCD a contiguous range of logical bricks, and
+// logical bricks are ordered by "super-bricks" of SB_X x SB_Y x SB_Z bricks
+// (64 x 64 x 16 voxels for MAP 0).  Workgroups resident on one XCD at the same
+// time then project onto one compact image region per frame, so the depth
+// lines they gather stay in that XCD's L2 (speed only, never correctness).
+constexpr int kSbX = 4, kSbY = 16, kSbZ = 4;
+
+template <int MAP, int U, bool SWZ>
 __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float* __restrict__ Wt, int D, int H,
                                                    int W, int z0, int z1, const float* __restrict__ depth, int F,
                                                    int Hd, int Wd, const float* __restrict__ poses,
                                                    const float* __restrict__ Kf, Bounds B, float trunc) {
-    __shared__ float cam[kTsdfMaxFramesLds * 16];
-    const int nf = min(F, kTsdfMaxFramesLds);
-    for (int t = threadIdx.x; t < nf * 16; t += blockDim.x) {
+    using TT = TsdfTile<MAP>;
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (SWZ) {
+        const int nbx = (W + TT::X - 1) / TT::X, nby = (H + TT::Y - 1) / TT::Y;
+        const int nsx = (nbx + kSbX - 1) / kSbX, nsy = (nby + kSbY - 1) / kSbY;
+        const int L = xcd_remap(blockIdx.x, gridDim.x);
+        const int sb = L / (kSbX * kSbY * kSbZ), in = L % (kSbX * kSbY * kSbZ);
+        const int sx = sb % nsx, sy = (sb / nsx) % nsy, sz = sb / (nsx * nsy);
+        bx = sx * kSbX + in % kSbX;
+        by = sy * kSbY + (in / kSbX) % kSbY;
+        bz = sz * kSbZ + in / (kSbX * kSbY);
+    }
+    __shared__ float cam[kTsdfMaxFrames * 16];
+    for (int t = threadIdx.x; t < F * 16; t += blockDim.x) {
         const int f = t >> 4, q = t & 15;
         cam[t] = (q < 12) ? poses[f * 12 + q] : Kf[f * 4 + (q - 12)];
     }
     __syncthreads();
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const int y = blockIdx.y * 4 + ((threadIdx.x >> 4) & 3);
-    const int z = z0 + blockIdx.z * 4 + (threadIdx.x >> 6);
-    if (x >= W || y >= H || z >= z1) return;
+    int ox, oy, oz;
+    tsdf_map<MAP>(threadIdx.x, ox, oy, oz);
+    const int x = bx * TT::X + ox;
+    const int y = by * TT::Y + oy;
+    const int z = z0 + bz * TT::Z + oz;
+    if (x >= W || y >= H || z >= z1) return;  // (after the only barrier)
     const float sx = (B.mx[0] - B.mn[0]) / (float)(W - 1);
     const float sy = (B.mx[1] - B.mn[1]) / (float)(H - 1);
     const float sz = (B.mx[2] - B.mn[2]) / (float)(D - 1);
     const float vx = B.mn[0] + (float)x * sx;
     const float vy = B.mn[1] + (float)y * sy;
     const float vz = B.mn[2] + (float)z * sz;
+    const float inv_trunc = 1.0f / trunc;
     const size_t idx = ((size_t)z * H + y) * W + x;
     float tv = T[idx], wv = Wt[idx];
     const size_t frame = (size_t)Hd * Wd;
-    for (int f = 0; f < F; ++f) {
-        const float* c = (f < kTsdfMaxFramesLds) ? cam + f * 16 : nullptr;
-        float P[16];
-        if (c) {
+    for (int f0 = 0; f0 < F; f0 += U) {
+        size_t at[U];
+        float zc[U];
+        bool ok[U];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) P[q] = c[q];
-        } else {
-#pragma unroll
-            for (int q = 0; q < 12; ++q) P[q] = poses[f * 12 + q];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) P[12 + q] = Kf[f * 4 + q];
+        for (int u = 0; u < U; ++u) {
+            const int f = f0 + u;
+            const float* P = cam + min(f, F - 1) * 16;
+            const float Xc = P[0] * vx + P[1] * vy + P[2] * vz + P[3];
+            const float Yc = P[4] * vx + P[5] * vy + P[6] * vz + P[7];
+            const float Zc = P[8] * vx + P[9] * vy + P[10] * vz + P[11];
+            const float iz = 1.0f / Zc;
+            const float uu = (P[12] * Xc) * iz + P[14];
+            const float vv = (P[13] * Yc) * iz + P[15];
+            const float fu = floorf(uu + 0.5f), fv = floorf(vv + 0.5f);
+            const bool good = (f < F) && (Zc > 0.f) && fu >= 0.f && fu < (float)Wd && fv >= 0.f && fv < (float)Hd;
+            ok[u] = good;
+            zc[u] = Zc;
+            at[u] = good ? (size_t)f * frame + (size_t)fv * Wd + (size_t)fu : 0;
         }
-        const float Xc = P[0] * vx + P[1] * vy + P[2] * vz + P[3];
-        const float Yc = P[4] * vx + P[5] * vy + P[6] * vz + P[7];
-        const float Zc = P[8] * vx + P[9] * vy + P[10] * vz + P[11];
-        if (!(Zc > 0.f)) continue;
-        const float iz = 1.0f / Zc;
-        const float u = (P[12] * Xc) * iz + P[14];
-        const float v = (P[13] * Yc) * iz + P[15];
-        const float fu = floorf(u + 0.5f), fv = floorf(v + 0.5f);
-        if (!(fu >= 0.f && fu < (float)Wd && fv >= 0.f && fv < (float)Hd)) continue;
-        const float dep = depth[f * frame + (size_t)fv * Wd + (size_t)fu];
-        if (!(dep > 0.f)) continue;
-        const float sdf = dep - Zc;
-        if (sdf < -trunc) continue;
-        const float ts = fminf(1.0f, sdf / trunc);
-        tv = (tv * wv + ts) / (wv + 1.0f);
-        wv = wv + 1.0f;
+        float dep[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) dep[u] = depth[at[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float sdf = dep[u] - zc[u];
+            if (ok[u] && dep[u] > 0.f && !(sdf < -trunc)) {
+                const float ts = fminf(1.0f, sdf * inv_trunc);
+                tv = (tv * wv + ts) / (wv + 1.0f);
+                wv = wv + 1.0f;
+            }
+        }
     }
     T[idx] = tv;
     Wt[idx] = wv;
+}
+
+static int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
 }
 
 }  // namespace sfmhip
@@ -453,8 +505,57 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     SFMHIP_REQUIRE(0 <= z0 && z0 <= z1 && z1 <= D, "sfmhip_tsdf_integrate: bad z range");
     SFMHIP_REQUIRE(trunc > 0.f, "sfmhip_tsdf_integrate: trunc must be > 0");
     if (F == 0 || z0 == z1) return SFMHIP_OK;
-    dim3 grid(ceil_div(W, 16), ceil_div(H, 4), ceil_div(z1 - z0, 4));
-    hipLaunchKernelGGL(tsdf_kernel, grid, dim3(256), 0, as_stream(stream), T, Wt, D, H, W, z0, z1, depth, F,
-                       Hd, Wd, poses, Kf, make_bounds(bmin, bmax), trunc);
-    return check_launch("tsdf_kernel");
+    // Tuning knobs (A/B runs only): SFMHIP_TSDF_MAP, SFMHIP_TSDF_U, SFMHIP_TSDF_CHUNK
+    // (frames per launch: a shorter chunk bounds how many frames the resident
+    // workgroups touch at once, i.e. the depth working set in L2 / MALL).
+    const int map = env_int("SFMHIP_TSDF_MAP", 0);
+    const int unroll = env_int("SFMHIP_TSDF_U", 4);
+    const int swz = env_int("SFMHIP_TSDF_SWZ", 1);
+    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", 32)));
+    static const int tx[4] = {16, 16, 8, 64}, ty[4] = {4, 4, 4, 1}, tz[4] = {4, 4, 8, 4};
+    const int mi = swz ? 0 : ((map >= 0 && map < 4) ? map : 0);
+    const int nbx = ceil_div(W, tx[mi]), nby = ceil_div(H, ty[mi]), nbz = ceil_div(z1 - z0, tz[mi]);
+    dim3 grid(nbx, nby, nbz);
+    if (swz) {
+        const int64_t slots = (int64_t)ceil_div(nbx, kSbX) * ceil_div(nby, kSbY) * ceil_div(nbz, kSbZ) *
+                              (kSbX * kSbY * kSbZ);
+        SFMHIP_REQUIRE(slots < INT_MAX, "sfmhip_tsdf_integrate: grid too large");
+        grid = dim3((unsigned)slots, 1, 1);
+    }
+    // frame chunks run in order on the stream, so per-voxel update order is kept
+    for (int f0 = 0; f0 < F; f0 += chunk) {
+        const int nf = std::min(chunk, F - f0);
+        const float* dp = depth + (size_t)f0 * Hd * Wd;
+        const float* pp = poses + (size_t)f0 * 12;
+        const float* kp = Kf + (size_t)f0 * 4;
+        const Bounds bb = make_bounds(bmin, bmax);
+#define SFMHIP_TSDF(MM, UU, SS)                                                                              \
+    hipLaunchKernelGGL((tsdf_kernel<MM, UU, SS>), grid, dim3(256), 0, as_stream(stream), T, Wt, D, H, W, z0, \
+                       z1, dp, nf, Hd, Wd, pp, kp, bb, trunc)
+#define SFMHIP_TSDF_M(MM)                          \
+    switch (unroll) {                              \
+        case 1: SFMHIP_TSDF(MM, 1, false); break;  \
+        case 8: SFMHIP_TSDF(MM, 8, false); break;  \
+        default: SFMHIP_TSDF(MM, 4, false); break; \
+    }
+        if (swz) {
+            switch (unroll) {
+                case 1: SFMHIP_TSDF(0, 1, true); break;
+                case 8: SFMHIP_TSDF(0, 8, true); break;
+                default: SFMHIP_TSDF(0, 4, true); break;
+            }
+        } else {
+            switch (mi) {
+                case 1: SFMHIP_TSDF_M(1); break;
+                case 2: SFMHIP_TSDF_M(2); break;
+                case 3: SFMHIP_TSDF_M(3); break;
+                default: SFMHIP_TSDF_M(0); break;
+            }
+        }
+#undef SFMHIP_TSDF_M
+#undef SFMHIP_TSDF
+        const int rc = check_launch("tsdf_kernel");
+        if (rc != SFMHIP_OK) return rc;
+    }
+    return SFMHIP_OK;
 }

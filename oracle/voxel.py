@@ -154,7 +154,7 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
     voxel (z,y,x) -> world bmin + idx*(bmax-bmin)/(R-1) (align_corners, x->W);
     Xc = R v + t (left-to-right); skip Zc <= 0; iz = 1/Zc; u = (fx Xc) iz + cx;
     pixel = floor(u + 0.5); skip off-image or depth <= 0; sdf = depth - Zc;
-    skip sdf < -mu; tsdf = min(1, sdf/mu); T = (T W + tsdf)/(W + 1); W += 1."""
+    skip sdf < -mu; tsdf = min(1, sdf * (1/mu)); T = (T W + tsdf)/(W + 1); W += 1."""
     T = np.array(T, F32, copy=True)
     Wt = np.array(Wt, F32, copy=True)
     D, H, W = T.shape
@@ -172,6 +172,7 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
     poses = np.asarray(poses, F32).reshape(F, 12)
     K = np.asarray(K, F32).reshape(F, 4)
     tr = F32(trunc)
+    inv_tr = F32(1) / tr
     Ts, Ws = T[z0:z1], Wt[z0:z1]
     for f in range(F):
         P = poses[f]
@@ -192,7 +193,7 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
         ok &= dep > 0
         sdf = dep - Zc
         ok &= ~(sdf < -tr)
-        ts = np.minimum(F32(1), sdf / tr)
+        ts = np.minimum(F32(1), sdf * inv_tr)
         Tn = (Ts * Ws + ts) / (Ws + F32(1))
         Ts = np.where(ok, Tn, Ts).astype(F32)
         Ws = np.where(ok, Ws + F32(1), Ws).astype(F32)

@@ -1,0 +1,87 @@
+// mfma_peak.hip — diagnostic: the int8 MFMA rate this MI355X sustains on
+// random register operands, with and without the matcher's 3-op epilogue per
+// output element (no LDS, no global traffic in the loop).  Gives the practical
+// ceiling (clock under load) the match kernel is compared against.
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/mfma_peak tools/mfma_peak.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int med3i(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+template <bool EPI>
+__global__ __launch_bounds__(256, 2) void kern(const int* __restrict__ seed, int iters, int* out) {
+    const int lane = threadIdx.x & 63;
+    i32x4 a[8], b[2][8];
+    for (int k = 0; k < 8; ++k)
+        for (int e = 0; e < 4; ++e) {
+            a[k][e] = seed[(blockIdx.x * 97 + lane * 13 + k * 7 + e) & 4095];
+            b[0][k][e] = seed[(blockIdx.x * 31 + lane * 5 + k * 11 + e * 3) & 4095];
+            b[1][k][e] = seed[(blockIdx.x * 17 + lane * 7 + k * 3 + e * 5) & 4095];
+        }
+    int t1a = INT_MIN, t2a = INT_MIN, t1b = INT_MIN, t2b = INT_MIN;
+    int kv = seed[lane];
+    for (int it = 0; it < iters; ++it) {
+        i32x16 acc0 = {0}, acc1 = {0};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[k], b[0][k], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[k], b[1][k], acc1, 0, 0, 0);
+        }
+        if (EPI) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int ka = acc0[q] * 256 + kv;
+                t2a = med3i(t2a, ka, t1a);
+                t1a = max(t1a, ka);
+                const int kb = acc1[q] * 256 + kv;
+                t2b = med3i(t2b, kb, t1b);
+                t1b = max(t1b, kb);
+            }
+        } else {
+            t1a ^= acc0[lane & 15];
+            t1b ^= acc1[(lane + 3) & 15];
+        }
+        kv += 1;
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = t1a + t2a + t1b + t2b;
+}
+
+int main(int argc, char** argv) {
+    const int blocks = 256 * 2 * 8, iters = argc > 1 ? atoi(argv[1]) : 2000;
+    int *seed, *out;
+    hipMalloc(&seed, 4096 * 4);
+    hipMalloc(&out, blocks * 256 * 4);
+    int h[4096];
+    for (int zero = 0; zero < 2; ++zero) {
+        unsigned x = 12345;
+        for (int i = 0; i < 4096; ++i) { x = x * 1664525u + 1013904223u; h[i] = zero ? 0 : (int)x; }
+        hipMemcpy(seed, h, sizeof(h), hipMemcpyHostToDevice);
+        for (int epi = 0; epi < 2; ++epi) {
+            hipEvent_t e0, e1;
+            hipEventCreate(&e0);
+            hipEventCreate(&e1);
+            for (int rep = 0; rep < 3; ++rep) {
+                hipEventRecord(e0);
+                if (epi) hipLaunchKernelGGL(kern<true>, dim3(blocks), dim3(256), 0, 0, seed, iters, out);
+                else hipLaunchKernelGGL(kern<false>, dim3(blocks), dim3(256), 0, 0, seed, iters, out);
+                hipEventRecord(e1);
+                hipEventSynchronize(e1);
+                float ms;
+                hipEventElapsedTime(&ms, e0, e1);
+                const double ops = (double)blocks * 4 * iters * 16 * 65536.0;
+                if (rep == 2)
+                    printf("%s operands, %s epilogue: %.2f ms  %.0f TOPS (%.1f%% of 5000)\n", zero ? "zero" : "random",
+                           epi ? "with" : "no", ms, ops / ms / 1e9, ops / ms / 1e9 / 50.0);
+            }
+        }
+    }
+    return 0;
+}

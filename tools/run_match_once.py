@@ -1,0 +1,21 @@
+"""Launch the C3 match kernel a few times (for rocprofv3 --pmc passes)."""
+import importlib
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sfm = importlib.import_module("3d_reconstruction_amd")
+syn = importlib.import_module("3d_reconstruction_amd.synthetic")
+n_img = int(os.environ.get("N_IMG", "257"))
+dev = torch.device("cuda", 0)
+x = syn.superpoint_like(n_img, 4096, 256, seed=1, device=dev)
+bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_FLOAT)
+del x
+pairs = torch.from_numpy(sfm.all_pairs(n_img)).to(dev)
+out = torch.empty((pairs.shape[0], bank.m_pad), dtype=torch.int32, device=dev)
+for _ in range(int(os.environ.get("REPS", "2"))):
+    bank._launch(pairs, 3, 4, out, None, None)
+torch.cuda.synchronize()
+print("matches", int((out >= 0).sum().item()))
