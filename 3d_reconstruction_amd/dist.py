@@ -39,8 +39,17 @@ def allgather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tenso
     if local.shape[0] < per:
         send = torch.empty((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         send[: local.shape[0]] = local
-    recv = torch.empty((per * world,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(recv, send.contiguous(), group=group)
+    stage = local.is_cuda and dist.get_backend(group) == "gloo"   # gloo: host staging (tests only)
+    if stage:
+        send = send.cpu()
+    recv = torch.empty((per * world,) + tuple(local.shape[1:]), dtype=local.dtype, device=send.device)
+    # byte view: one collective for any dtype on any backend (gloo has no int16)
+    dist.all_gather_into_tensor(recv.view(-1).view(torch.uint8), send.contiguous().view(-1).view(torch.uint8),
+                                group=group)
+    if stage:
+        recv = recv.to(local.device)
+    if n_total == per * world:
+        return recv
     parts = []
     for r in range(world):
         rl, rh = shard_range(n_total, r, world)

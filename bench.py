@@ -67,7 +67,8 @@ def timed(fn, steps, warmup, barrier):
 def max_over_ranks(x: float, world: int, device) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64,
+                     device=device if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -109,15 +110,21 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--skip-secondary", action="store_true")
     ap.add_argument("--n-img", type=int, default=N_IMG)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for rehearsal")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SFMHIP_BENCH_SAME_DEVICE"):  # rehearsal: every rank on device 0
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
         barrier = lambda: dist.barrier()  # noqa: E731
     else:
         barrier = lambda: None  # noqa: E731

@@ -1,0 +1,76 @@
+"""CPU: the multi-GPU sharding path (pair ranges / z-slabs + one all-gather of
+the match graph) exercised with the gloo backend, world_size 2 (and 3)."""
+import importlib
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+sdist = importlib.import_module("3d_reconstruction_amd.dist")
+
+
+@pytest.mark.parametrize("n,world", [(32896, 8), (7, 3), (5, 8), (0, 2), (256, 4)])
+def test_shard_range_partitions(n, world):
+    seen = []
+    sizes = []
+    for r in range(world):
+        lo, hi = sdist.shard_range(n, r, world)
+        seen.extend(range(lo, hi))
+        sizes.append(hi - lo)
+    assert seen == list(range(n))
+    assert max(sizes) - min(sizes) <= 1
+    assert max(sizes) <= sdist.padded_shard(n, world)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        lo, hi = sdist.shard_range(n_total, rank, world)
+        # rank r "matches" its pair range: rows filled with a function of the global pair id
+        local = (torch.arange(lo, hi, dtype=torch.int32)[:, None] * 10 +
+                 torch.arange(6, dtype=torch.int32)[None, :]).to(torch.int16)
+        full = sdist.allgather_rows(local, n_total)
+        exp = (torch.arange(n_total, dtype=torch.int32)[:, None] * 10 +
+               torch.arange(6, dtype=torch.int32)[None, :]).to(torch.int16)
+        q.put((rank, bool(torch.equal(full, exp))))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 11), (3, 10)])
+def test_allgather_match_graph_gloo(world, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v is True for v in res.values()), res
+
+
+def test_zslab_shards_cover_grid():
+    R = 256
+    for world in (1, 2, 4, 8):
+        slabs = [sdist.shard_range(R, r, world) for r in range(world)]
+        assert slabs[0][0] == 0 and slabs[-1][1] == R
+        assert all(slabs[i][1] == slabs[i + 1][0] for i in range(world - 1))
