@@ -402,6 +402,101 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
     Wt[idx] = wv;
 }
 
+// Persistent-band TSDF (SFMHIP_TSDF_KIND=1): the 8 XCD labels (blockIdx % 8)
+// each own a band of kBandRows voxel rows (y), so for cameras orbiting the y
+// axis an XCD's voxels project onto one horizontal image band that stays in
+// its L2 while all of that XCD's workgroups fuse the same frame (they start
+// together and do equal work per frame).  Workgroup = one z-slice of the band:
+// thread t owns voxel column x = x0 + t and the kBandRows voxels above it,
+// with their (T, W) in registers for all F frames (grid read/written once).
+// Gathers are issued kBandGroup at a time before their ordered updates.
+constexpr int kBandGroup = 8;
+
+template <int kBandRows, int OCC>
+__global__ __launch_bounds__(256, OCC) void tsdf_band_kernel(
+    float* __restrict__ T, float* __restrict__ Wt, int D, int H, int W, int x0, int y0, int zs, int nz,
+    const float* __restrict__ depth, int F, int Hd, int Wd, const float* __restrict__ poses,
+    const float* __restrict__ Kf, Bounds B, float trunc) {
+    __shared__ float cam[kTsdfMaxFrames * 16];
+    for (int t = threadIdx.x; t < F * 16; t += blockDim.x) {
+        const int f = t >> 4, q = t & 15;
+        cam[t] = (q < 12) ? poses[f * 12 + q] : Kf[f * 4 + (q - 12)];
+    }
+    __syncthreads();
+    const int label = blockIdx.x % kNumXcd;          // shares an XCD (speed only)
+    const int zi = blockIdx.x / kNumXcd;
+    if (zi >= nz) return;
+    const int x = x0 + threadIdx.x;
+    const int ya = y0 + label * kBandRows;
+    const int z = zs + zi;
+    if (x >= W || ya >= H || z >= D) return;
+    const int ny = min(kBandRows, H - ya);
+    const float sx = (B.mx[0] - B.mn[0]) / (float)(W - 1);
+    const float sy = (B.mx[1] - B.mn[1]) / (float)(H - 1);
+    const float sz = (B.mx[2] - B.mn[2]) / (float)(D - 1);
+    const float vx = B.mn[0] + (float)x * sx;
+    const float vz = B.mn[2] + (float)z * sz;
+    const float inv_trunc = 1.0f / trunc;
+    float tv[kBandRows], wv[kBandRows];
+    const size_t plane = (size_t)H * W;
+    const size_t base = (size_t)z * plane + (size_t)ya * W + x;
+#pragma unroll
+    for (int v = 0; v < kBandRows; ++v) {
+        tv[v] = (v < ny) ? T[base + (size_t)v * W] : 0.f;
+        wv[v] = (v < ny) ? Wt[base + (size_t)v * W] : 0.f;
+    }
+    const size_t frame = (size_t)Hd * Wd;
+    for (int f = 0; f < F; ++f) {
+        const float* P = cam + f * 16;
+        const float* dp = depth + (size_t)f * frame;
+        // per-thread partial products (exactly the first terms of the left-to-right sums)
+        const float ax = P[0] * vx, ay = P[4] * vx, az = P[8] * vx;
+        const float cx = P[2] * vz, cy = P[6] * vz, cz = P[10] * vz;
+#pragma unroll
+        for (int g = 0; g < kBandRows; g += kBandGroup) {
+            int off[kBandGroup];
+            float zc[kBandGroup];
+            bool ok[kBandGroup];
+#pragma unroll
+            for (int u = 0; u < kBandGroup; ++u) {
+                const int v = g + u;
+                const float vyv = B.mn[1] + (float)(ya + v) * sy;
+                const float Xc = ((ax + P[1] * vyv) + cx) + P[3];
+                const float Yc = ((ay + P[5] * vyv) + cy) + P[7];
+                const float Zc = ((az + P[9] * vyv) + cz) + P[11];
+                const float iz = 1.0f / Zc;
+                const float uu = (P[12] * Xc) * iz + P[14];
+                const float vv = (P[13] * Yc) * iz + P[15];
+                const float fu = floorf(uu + 0.5f), fv = floorf(vv + 0.5f);
+                const bool good = (v < ny) && (Zc > 0.f) && fu >= 0.f && fu < (float)Wd && fv >= 0.f &&
+                                  fv < (float)Hd;
+                ok[u] = good;
+                zc[u] = Zc;
+                off[u] = good ? (int)fv * Wd + (int)fu : 0;
+            }
+            float dep[kBandGroup];
+#pragma unroll
+            for (int u = 0; u < kBandGroup; ++u) dep[u] = dp[off[u]];
+#pragma unroll
+            for (int u = 0; u < kBandGroup; ++u) {
+                const int v = g + u;
+                const float sdf = dep[u] - zc[u];
+                if (ok[u] && dep[u] > 0.f && !(sdf < -trunc)) {
+                    const float ts = fminf(1.0f, sdf * inv_trunc);
+                    tv[v] = (tv[v] * wv[v] + ts) / (wv[v] + 1.0f);
+                    wv[v] = wv[v] + 1.0f;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < kBandRows; ++v)
+        if (v < ny) {
+            T[base + (size_t)v * W] = tv[v];
+            Wt[base + (size_t)v * W] = wv[v];
+        }
+}
+
 static int env_int(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return e ? std::atoi(e) : dflt;
@@ -508,6 +603,35 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     // Tuning knobs (A/B runs only): SFMHIP_TSDF_MAP, SFMHIP_TSDF_U, SFMHIP_TSDF_CHUNK
     // (frames per launch: a shorter chunk bounds how many frames the resident
     // workgroups touch at once, i.e. the depth working set in L2 / MALL).
+    if (env_int("SFMHIP_TSDF_KIND", 0) == 1 && (size_t)Hd * Wd < (size_t)INT_MAX) {
+        // persistent-band kernel; launches tile x (256 per WG), y (8 bands of
+        // `rows` rows), z (chunks sized to stay resident) and frames (<= 512).
+        const int rows = env_int("SFMHIP_TSDF_ROWS", 16) == 32 ? 32 : 16;
+        const int zchunk = std::max(1, env_int("SFMHIP_TSDF_ZCHUNK", rows == 16 ? 128 : 96));
+        const Bounds bb = make_bounds(bmin, bmax);
+        for (int f0 = 0; f0 < F; f0 += kTsdfMaxFrames) {
+            const int nf = std::min(kTsdfMaxFrames, F - f0);
+            for (int y0 = 0; y0 < H; y0 += kNumXcd * rows)
+                for (int x0 = 0; x0 < W; x0 += 256)
+                    for (int zs = z0; zs < z1; zs += zchunk) {
+                        const int nz = std::min(zchunk, z1 - zs);
+                        const float* dp = depth + (size_t)f0 * Hd * Wd;
+                        const float* pp = poses + (size_t)f0 * 12;
+                        const float* kp = Kf + (size_t)f0 * 4;
+                        if (rows == 32)
+                            hipLaunchKernelGGL((tsdf_band_kernel<32, 3>), dim3(kNumXcd * nz), dim3(256), 0,
+                                               as_stream(stream), T, Wt, D, H, W, x0, y0, zs, nz, dp, nf, Hd, Wd, pp,
+                                               kp, bb, trunc);
+                        else
+                            hipLaunchKernelGGL((tsdf_band_kernel<16, 4>), dim3(kNumXcd * nz), dim3(256), 0,
+                                               as_stream(stream), T, Wt, D, H, W, x0, y0, zs, nz, dp, nf, Hd, Wd, pp,
+                                               kp, bb, trunc);
+                        const int rc = check_launch("tsdf_band_kernel");
+                        if (rc != SFMHIP_OK) return rc;
+                    }
+        }
+        return SFMHIP_OK;
+    }
     const int map = env_int("SFMHIP_TSDF_MAP", 0);
     const int unroll = env_int("SFMHIP_TSDF_U", 4);
     const int swz = env_int("SFMHIP_TSDF_SWZ", 1);

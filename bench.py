@@ -40,6 +40,18 @@ PEAK_INT8_TOPS = 5000.0       # MI355X dense int8 MFMA (MI355X_MICROARCH.md: 2x 
 PEAK_HBM_GBS = 8000.0         # HBM3E spec
 PEAK_FP32_TFLOPS = 157.3      # vector fp32
 PEAK_FP64_TFLOPS = 78.6       # vector fp64
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1", "traffic.json")
+
+
+def pmc_traffic(kind: str, frac: float = 1.0):
+    """HBM bytes per step of the dominant kernel from the committed PMC passes
+    (counters need their own rocprofv3 runs), scaled to this rank's share."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+        return t[kind]["bytes_per_step"] * frac
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def log(*a):
@@ -190,7 +202,9 @@ def main():
         "config": {"workload": f"C3/C4 all-pairs BF-L2 + ratio 0.75: {n_img} imgs x {M_KPT} kpts x {DIM}-d",
                    "pairs": P, "parallelism": f"pairs/{world}" + (" + 1 RCCL all-gather (int16)" if world > 1 else "")},
         "roofline": {"bound": "mfma", "achieved": achieved_tops, "peak": PEAK_INT8_TOPS, "unit": "TOPS",
-                     "frac": achieved_tops / PEAK_INT8_TOPS, "traffic": None,
+                     "frac": achieved_tops / PEAK_INT8_TOPS,
+                     "traffic": pmc_traffic("match", pairs_per_launch / P) if n_img == N_IMG else None,
+                     "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r1/traffic.json)",
                      "kernel": "match_kernel<256>", "kernel_ms": kern_ms,
                      "algorithmic": "2*M*N*d int8 ops per pair x pairs per launch"},
     }
@@ -245,7 +259,9 @@ def main():
                          "achieved_hbm_gbs": comp_bytes / (tk_ms * 1e-3) / 1e9, "peak_hbm_gbs": PEAK_HBM_GBS,
                          "achieved_tflops": 32.0 * local_upd / (tk_ms * 1e-3) / 1e12,
                          "peak_tflops": PEAK_FP32_TFLOPS,
-                         "frac": (32.0 * local_upd / (tk_ms * 1e-3) / 1e12) / PEAK_FP32_TFLOPS},
+                         "frac": (32.0 * local_upd / (tk_ms * 1e-3) / 1e12) / PEAK_FP32_TFLOPS,
+                         "traffic": pmc_traffic("tsdf", (z1 - z0) / R),
+                         "traffic_unit": "bytes per step (all frame-chunk launches, profiles/r1/traffic.json)"},
             "updated_voxel_frac": float((Wt[z0:z1] > 0).float().mean().item()),
         }]
         del depth, T, Wt
