@@ -81,6 +81,19 @@ int sfmhip_mutual_filter(int32_t* matches0, int32_t* matches1, int P, int m_pad,
 int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_book, int n_codes,
               int d, int32_t* codes, double* dist, void* stream);
 
+/* ---- BoW retrieval ---------------------------------
+ * Per-image visual-word histograms (matching.py:30-35): codes of all images
+ * concatenated, image i owns codes[offsets[i] : offsets[i+1]];
+ * hist [n_img][k] int32.                                                      */
+int sfmhip_word_histogram(const int32_t* codes, const int64_t* offsets, int n_img, int k,
+                          int32_t* hist, void* stream);
+
+/* scipy.cluster.vq.kmeans centroid update (bow.py:23 -> _vq.update_cluster_means):
+ * per cluster, the f64 sum of its observations in index order, / count.
+ * book [k][d] rows of empty clusters are left untouched; counts [k].          */
+int sfmhip_kmeans_update(const double* obs, int64_t n, int d, const int32_t* codes, int k,
+                         double* book, int32_t* counts, void* stream);
+
 /* ---- S2: cv2.triangulatePoints (sfm.py:27) ------------------------------
  * OpenCV DLT: per point a 6x4 system (rows x*p3-p1, y*p3-p2, x*p2-y*p1 per
  * view), right singular vector of the smallest singular value (one-sided

@@ -204,6 +204,54 @@ def gen_ba_sparse_and_jacobian():
     save("ba_golden.npz", **out)
 
 
+def _stmts(path, first, last):
+    """Module-level statements of a reference script whose lines lie in [first, last]."""
+    tree = ast.parse(open(path).read())
+    body = [n for n in tree.body if first <= n.lineno and n.end_lineno <= last]
+    return compile(ast.Module(body=body, type_ignores=[]), f"{os.path.basename(path)}:{first}-{last}", "exec")
+
+
+def gen_bow():
+    """bow.py:14-23 (stack + kmeans k=200, iter=1) and matching.py:24-82 (vq ->
+    histograms -> tf-idf -> cosine top-k -> connection graph -> start node),
+    executed from the reference files on synthetic DISK-like descriptors."""
+    from numpy.linalg import norm
+    from scipy.cluster.vq import kmeans, vq
+    rng = np.random.default_rng(17)
+    n_img, m, d = 10, 200, 128
+    groups = [rng.standard_normal((m, d)) for _ in range(4)]   # images 3g..3g+2 view "scene part" g
+    descs = []
+    for i in range(n_img):
+        own = rng.standard_normal((m, d))
+        share = rng.random(m) < (0.9 if i % 3 else 0.6)
+        own[share] = groups[(i // 3) % 4][share] + 0.02 * rng.standard_normal((share.sum(), d))
+        own /= np.linalg.norm(own, axis=1, keepdims=True)
+        descs.append(own.astype(np.float32))
+    all_descriptors = np.empty(n_img, dtype=object)
+    for i in range(n_img):
+        all_descriptors[i] = descs[i]
+    ns = {"np": np, "kmeans": kmeans, "vq": vq, "norm": norm, "print": lambda *a, **k: None,
+          "all_descriptors": all_descriptors}
+    ns_bow = dict(ns)
+    ns_bow.update(k=200, iters=1)
+    np.random.seed(123)
+    exec(_stmts(os.path.join(REF, "bow.py"), 14, 23), ns_bow)
+    codebook, variance = ns_bow["codebook"], ns_bow["variance"]
+    np.random.seed(123)
+    stacked = ns_bow["all_descriptors_"]
+    init_idx = np.random.choice(stacked.shape[0], size=200, replace=False)
+    ns_m = dict(ns)
+    ns_m.update(k=len(codebook), codebook=codebook)
+    exec(_stmts(os.path.join(REF, "matching.py"), 24, 82), ns_m)
+    conn = ns_m["connection"]
+    save("bow_golden.npz", desc=np.stack(descs), stacked=stacked, init_idx=init_idx, codebook=codebook,
+         variance=np.array(variance), words=np.stack(ns_m["visual_words"]),
+         freq=ns_m["frequency_vectors"], tfidf=ns_m["tfidf"], all_idx=np.stack(ns_m["all_idx"]),
+         all_score=np.stack(ns_m["all_score"]),
+         conn_flat=np.array([j for c in conn for j in c], dtype=np.int64),
+         conn_len=np.array([len(c) for c in conn], dtype=np.int64), start=np.array(ns_m["start"]))
+
+
 if __name__ == "__main__":
     gen_vq()
     gen_filter_matches()
@@ -211,3 +259,4 @@ if __name__ == "__main__":
     gen_sdf()
     gen_plenoxel()
     gen_ba_sparse_and_jacobian()
+    gen_bow()

@@ -146,3 +146,20 @@ def test_tsdf_oracle_planar_known_answer():
     upd = Wn[:, R // 2, R // 2] > 0
     np.testing.assert_allclose(Tn[upd, R // 2, R // 2], exp[upd], rtol=1e-6, atol=1e-6)
     assert (~upd == (exp * 0.2 < -0.2)).all()
+
+
+# --- BoW retrieval (§8f row 3) -------------------------------------------------
+def test_bow_oracle_matches_reference():
+    from oracle import bow as ob
+    g = golden("bow_golden.npz")
+    desc = list(g["desc"])
+    assert np.array_equal(ob.stack_descriptors(desc), g["stacked"])
+    book, dist = ob.codebook(desc, 200, 1, seed=123)
+    assert np.array_equal(book, g["codebook"]) and dist == float(g["variance"])
+    r = ob.retrieval(desc, g["codebook"])
+    assert np.array_equal(np.stack(r["words"]), g["words"])
+    assert np.array_equal(r["freq"], g["freq"]) and np.array_equal(r["tfidf"], g["tfidf"])
+    assert np.array_equal(np.stack(r["idx"]), g["all_idx"])
+    flat = [j for c in r["conn"] for j in c]
+    assert flat == g["conn_flat"].tolist() and [len(c) for c in r["conn"]] == g["conn_len"].tolist()
+    assert r["start"] == int(g["start"])
