@@ -51,6 +51,8 @@ SIGNATURES = {
     "sfmhip_vq": [_p, _i64, _p, _i32, _i32, _p, _p, _p],
     "sfmhip_word_histogram": [_p, _p, _i32, _i32, _p, _p],
     "sfmhip_kmeans_update": [_p, _i64, _i32, _p, _i32, _p, _p, _p],
+    "sfmhip_track_interlace": [_p, _i64, _p, _i64, _p, _p, _i64, _p],
+    "sfmhip_track_merge": [_p, _i64, _p, _i64, _p, _p, _i64, _p, _p],
     "sfmhip_triangulate_dlt": [_p, _p, _p, _p, _i64, _p, _p],
     "sfmhip_reproj_residual": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "sfmhip_reproj_fd_jacobian": [_p, _p, _p, _p, _p, _i32, _i64, _p, _p, _p, _p],

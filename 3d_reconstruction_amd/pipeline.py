@@ -1,0 +1,28 @@
+"""The matching stage of the reference (matching.py) on the sfmhip path:
+BoW retrieval graph (GPU vq) -> exhaustive all-pairs BF matching (GPU, mutual
++ ratio) -> BFS pair selection + track building on the match graph (host C++)
+-> the img_pairs / all_matches that sfm.py reads (matching.py:188-189)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import bow, tracks
+from .match import MODE_FLOAT, DescriptorBank, all_pairs
+
+
+def matching_stage(all_descriptors, codebook, ratio=0.75, mode: int = MODE_FLOAT, top_k: int = 10,
+                   verify=None, min_matches: int = 500):
+    """Returns dict(img_pairs, all_matches, connection, start, matches0, matches1)."""
+    descs = [np.asarray(d, np.float32) for d in all_descriptors]
+    _, conn, start = bow.retrieval_graph(descs, codebook, top_k=top_k)
+    bank = DescriptorBank.from_float(descs, mode=mode)
+    pairs = all_pairs(len(descs))
+    m0, m1 = bank.match(pairs, ratio=ratio, mutual=True)
+    torch.cuda.synchronize()
+    n_kpts = [d.shape[0] for d in descs]
+    graph = tracks.MatchGraph(pairs, m0, m1, n_kpts)
+    img_pairs, all_matches = tracks.bfs_tracks(conn, start, n_kpts, graph, verify=verify,
+                                               min_matches=min_matches)
+    return dict(img_pairs=img_pairs, all_matches=all_matches, connection=conn, start=start,
+                matches0=m0, matches1=m1)

@@ -94,6 +94,18 @@ int sfmhip_word_histogram(const int32_t* codes, const int64_t* offsets, int n_im
 int sfmhip_kmeans_update(const double* obs, int64_t n, int d, const int32_t* codes, int k,
                          double* book, int32_t* counts, void* stream);
 
+/* ---- match-graph consumer, HOST memory ------------
+ * Track bookkeeping of matching.py:146-176 for one candidate pair (ref, id):
+ * tracks_* are the per-keypoint 3D-point ids of the two images (-1 = none);
+ * idx0/idx1 the pair's matches.  interlace = the count of matching.py:146-158;
+ * merge = matching.py:161-176 (updates tracks in place, point_ids[n] out,
+ * *next_id advanced).  The reference's p1/p2 index quirks are kept.          */
+int sfmhip_track_interlace(const int32_t* tracks_ref, int64_t n_ref, const int32_t* tracks_id, int64_t n_id,
+                           const int64_t* idx0, const int64_t* idx1, int64_t n, int64_t* interlaced);
+int sfmhip_track_merge(int32_t* tracks_ref, int64_t n_ref, int32_t* tracks_id, int64_t n_id,
+                       const int64_t* idx0, const int64_t* idx1, int64_t n, int64_t* next_id,
+                       int64_t* point_ids);
+
 /* ---- S2: cv2.triangulatePoints (sfm.py:27) ------------------------------
  * OpenCV DLT: per point a 6x4 system (rows x*p3-p1, y*p3-p2, x*p2-y*p1 per
  * view), right singular vector of the smallest singular value (one-sided

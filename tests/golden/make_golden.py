@@ -11,6 +11,9 @@ loaded by file path at run time:
   * lightglue/lightglue.py  (loaded standalone; filter_matches only — no weights)
   * sfm.py              ba_sparse extracted with `ast` (the module body needs cv2
                         and output/*.npy)
+  * bow.py:14-23, matching.py:24-82 and matching.py:84-185 executed with `ast`
+                        from the reference files (cv2 / matcher / tqdm stubbed
+                        where the BFS calls them; see gen_bfs)
 and scipy.cluster.vq.vq / scipy.optimize._numdiff.approx_derivative, the
 third-party functions the reference calls (matching.py:27, sfm.py:38).
 """
@@ -252,6 +255,91 @@ def gen_bow():
          conn_len=np.array([len(c) for c in conn], dtype=np.int64), start=np.array(ns_m["start"]))
 
 
+def bfs_scene(n_img=12, k=800, stride=150, seed=18):
+    """Synthetic tracks: image i sees global points [i*stride, i*stride + k) under a
+    random keypoint permutation; matches of (ref, id) = shared points (ordered by
+    ref keypoint) plus a few spurious pairs."""
+    rng = np.random.default_rng(seed)
+    perm = [rng.permutation(k) for _ in range(n_img)]          # global local-slot -> keypoint idx
+    def kp_of(img, g):
+        return perm[img][g - img * stride]
+    table = {}
+    for a in range(n_img):
+        for b in range(n_img):
+            if a == b:
+                continue
+            lo, hi = max(a, b) * stride, min(a, b) * stride + k
+            g = np.arange(lo, hi) if hi > lo else np.zeros(0, np.int64)
+            i0 = np.array([kp_of(a, x) for x in g], np.int64)
+            i1 = np.array([kp_of(b, x) for x in g], np.int64)
+            if len(i0):
+                extra = rng.integers(0, k, (5, 2))
+                i0 = np.concatenate([i0, extra[:, 0]])
+                i1 = np.concatenate([i1, extra[:, 1]])
+                _, first = np.unique(i0, return_index=True)   # one match per ref keypoint
+                i0, i1 = i0[first], i1[first]
+            table[(a, b)] = (i0, i1)
+    conn = [[] for _ in range(n_img)]
+    for a in range(n_img):
+        for b in (a + 1, a + 2, a + 4):
+            if b < n_img:
+                conn[a].append(b)
+                conn[b].append(a)
+    return table, conn
+
+
+def gen_bfs():
+    """matching.py:84-185 (BFS pair selection + track merge) executed from the
+    reference file with stubs: a table-driven matcher (LightGlue's output dict),
+    cv2 RANSAC stubs that accept every match, rbd, tqdm."""
+    n_img, k = 12, 800
+    table, conn = bfs_scene(n_img, k)
+    all_points = np.empty(n_img, dtype=object)
+    img_size = np.empty(n_img, dtype=object)
+    for i in range(n_img):
+        all_points[i] = np.random.default_rng(i).uniform(-500, 500, (k, 2)).astype(np.float32)
+        img_size[i] = np.array([1936.0, 1296.0], np.float32)
+    ns = {}
+
+    def matcher(data):
+        i0, i1 = table[(ns["reference_id"], ns["id"])]
+        return {"matches": [torch.from_numpy(np.stack([i0, i1], 1)).long()]}
+
+    def rbd(d):
+        return {kk: v[0] if isinstance(v, (torch.Tensor, np.ndarray, list)) else v for kk, v in d.items()}
+
+    cv2 = types.SimpleNamespace(
+        RANSAC=8,
+        findEssentialMat=lambda p0, p1, K, method=None, prob=None, threshold=None: (np.eye(3), np.ones((len(p0), 1), np.uint8)),
+        recoverPose=lambda E, p0, p1, K: (len(p0), np.eye(3), np.zeros((3, 1)), np.ones((len(p0), 1), np.uint8)))
+
+    class _Bar:
+        def __init__(self, total=None): pass
+        def __enter__(self): return self
+        def __exit__(self, *a): return False
+        def update(self, n=1): pass
+
+    degrees = [len(c) for c in conn]
+    start = int(np.argmax(degrees))
+    ns.update(np=np, torch=torch, cv2=cv2, rbd=rbd, matcher=matcher, tqdm=_Bar, print=lambda *a, **kw: None,
+              all_points=all_points, img_size=img_size, all_descriptors=all_points, connection=conn,
+              start=start, N=n_img, device=torch.device("cpu"))
+    exec(_stmts(os.path.join(REF, "matching.py"), 84, 185), ns)
+    queue, all_matches = ns["queue"], ns["all_matches"]
+    tab_keys = np.array(sorted(table), np.int64)
+    save("bfs_golden.npz", conn_flat=np.array([j for c in conn for j in c], np.int64),
+         conn_len=np.array([len(c) for c in conn], np.int64), start=np.array(start), k=np.array(k),
+         tab_keys=tab_keys,
+         tab_len=np.array([len(table[tuple(t)][0]) for t in tab_keys], np.int64),
+         tab_i0=np.concatenate([table[tuple(t)][0] for t in tab_keys]),
+         tab_i1=np.concatenate([table[tuple(t)][1] for t in tab_keys]),
+         img_pairs=np.array(queue[1:], np.int64),
+         m_len=np.array([len(m[0]) for m in all_matches], np.int64),
+         m_idx0=np.concatenate([m[0] for m in all_matches]),
+         m_idx1=np.concatenate([m[1] for m in all_matches]),
+         m_tracks=np.concatenate([m[2] for m in all_matches]).astype(np.int64))
+
+
 if __name__ == "__main__":
     gen_vq()
     gen_filter_matches()
@@ -260,3 +348,4 @@ if __name__ == "__main__":
     gen_plenoxel()
     gen_ba_sparse_and_jacobian()
     gen_bow()
+    gen_bfs()
