@@ -247,7 +247,7 @@ def gen_bow():
     ns_m.update(k=len(codebook), codebook=codebook)
     exec(_stmts(os.path.join(REF, "matching.py"), 24, 82), ns_m)
     conn = ns_m["connection"]
-    save("bow_golden.npz", desc=np.stack(descs), stacked=stacked, init_idx=init_idx, codebook=codebook,
+    save("bow_golden.npz", desc=np.stack(descs), stacked_rowsum=stacked.sum(1), init_idx=init_idx, codebook=codebook,
          variance=np.array(variance), words=np.stack(ns_m["visual_words"]),
          freq=ns_m["frequency_vectors"], tfidf=ns_m["tfidf"], all_idx=np.stack(ns_m["all_idx"]),
          all_score=np.stack(ns_m["all_score"]),
