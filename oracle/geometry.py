@@ -68,6 +68,34 @@ def rodrigues(rvec) -> np.ndarray:
     return np.array([(c * eye[k] + c1 * rrt[k]) + s * rxm[k] for k in range(9)]).reshape(3, 3)
 
 
+def rodrigues_inverse(R) -> np.ndarray:
+    """cv::Rodrigues matrix->vector (OpenCV 4.x calibration.cpp): project R onto
+    SO(3) by SVD, then the axis-angle from the skew part (small- and
+    pi-angle branches as in OpenCV).  Returns (3,1)."""
+    u, _, vt = np.linalg.svd(np.asarray(R, np.float64))
+    R = u @ vt
+    rx, ry, rz = R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]
+    s = math.sqrt((rx * rx + ry * ry + rz * rz) * 0.25)
+    c = (R[0, 0] + R[1, 1] + R[2, 2] - 1) * 0.5
+    c = 1.0 if c > 1.0 else (-1.0 if c < -1.0 else c)
+    theta = math.acos(c)
+    if s < 1e-5:
+        if c > 0:
+            return np.zeros((3, 1))
+        t = (R[0, 0] + 1) * 0.5
+        rx = math.sqrt(max(t, 0.0))
+        t = (R[1, 1] + 1) * 0.5
+        ry = math.sqrt(max(t, 0.0)) * (-1.0 if R[0, 1] < 0 else 1.0)
+        t = (R[2, 2] + 1) * 0.5
+        rz = math.sqrt(max(t, 0.0)) * (-1.0 if R[0, 2] < 0 else 1.0)
+        if abs(rx) < abs(ry) and abs(rx) < abs(rz) and (R[1, 2] > 0) != (ry * rz > 0):
+            rz = -rz
+        theta /= math.sqrt(rx * rx + ry * ry + rz * rz)
+        return np.array([[rx * theta], [ry * theta], [rz * theta]])
+    vth = 1.0 / (2 * s) * theta
+    return np.array([[rx * vth], [ry * vth], [rz * vth]])
+
+
 def project_points(X, rvec, tvec, K) -> np.ndarray:
     """cvProjectPoints2Internal with zero distortion: (n,2).
 

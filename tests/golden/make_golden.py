@@ -340,6 +340,64 @@ def gen_bfs():
          m_tracks=np.concatenate([m[2] for m in all_matches]).astype(np.int64))
 
 
+def gen_sfm_triangulate():
+    """sfm.py:26-52 triangulate() + ba_sparse + calculate_reprojection_error
+    executed from the reference file, with cv2 replaced by the oracle's numpy
+    restatements of triangulatePoints / convertPointsFromHomogeneous /
+    Rodrigues / projectPoints (cv2 is not installed; parity at the OpenCV
+    boundary is unpinned, the wrapper logic around it is what this pins)."""
+    from scipy.optimize import least_squares
+    from scipy.sparse import lil_matrix
+    from oracle import geometry as og
+    tree = ast.parse(open(os.path.join(REF, "sfm.py")).read())
+    fns = [n for n in tree.body if isinstance(n, ast.FunctionDef)
+           and n.name in ("triangulate", "ba_sparse", "calculate_reprojection_error")]
+
+    def _rod(src):
+        a = np.asarray(src, np.float64)
+        return (og.rodrigues(a), None) if a.size == 3 else (og.rodrigues_inverse(a), None)
+
+    cv2 = types.SimpleNamespace(
+        triangulatePoints=lambda P0, P1, x0, x1: og.triangulate_points(P0, P1, x0, x1),
+        convertPointsFromHomogeneous=lambda X: (X[:, :3] / X[:, 3:4])[:, None, :],
+        Rodrigues=_rod,
+        projectPoints=lambda X, r, t, K, distCoeffs=None: (og.project_points(X, r, t, K)[:, None, :], None))
+    rng = np.random.default_rng(19)
+    n_pts, n_img = 120, 3
+    f = 2378.98305085
+    K = np.array([[f, 0, 0], [0, f, 0], [0, 0, 1.0]])
+    R1 = og.rodrigues([0.02, -0.15, 0.01])
+    cameras = [np.hstack([np.eye(3), np.zeros((3, 1))]), np.hstack([R1, np.array([[0.8], [0.05], [0.1]])]), None]
+    X = rng.uniform([-1, -1, 4], [1, 1, 7], (n_pts, 3))
+    Xh = np.hstack([X, np.ones((n_pts, 1))]).T
+    p0 = (K @ cameras[0] @ Xh)
+    p1 = (K @ cameras[1] @ Xh)
+    pts0 = (p0[:2] / p0[2]).T + rng.normal(0, 0.5, (n_pts, 2))
+    pts1 = (p1[:2] / p1[2]).T + rng.normal(0, 0.5, (n_pts, 2))
+    cam_in = [c.copy() if c is not None else None for c in cameras]
+    # BA init pose of camera j is perturbed (as after PnP): the solve has work to do
+    cameras[1] = np.hstack([og.rodrigues([0.025, -0.14, 0.012]), np.array([[0.78], [0.06], [0.11]])])
+    cam_in[1] = cameras[1].copy()
+    idx0 = rng.permutation(400)[:n_pts]
+    idx1 = rng.permutation(400)[:n_pts]
+    idx3d = np.arange(n_pts) * 2 + 1
+    idx3d[5] = idx3d[4]           # a duplicated track id (possible in the reference's merge)
+    n_tracks = 2 * n_pts + 5
+    all_point3ds = [[None] * n_tracks, [None] * n_tracks]
+    all_colors = np.empty(n_img, dtype=object)
+    for i in range(n_img):
+        all_colors[i] = rng.integers(0, 256, (400, 3)).astype(np.uint8)
+    ns = {"np": np, "cv2": cv2, "least_squares": least_squares, "lil_matrix": lil_matrix,
+          "cameras": cameras, "all_point3ds": all_point3ds, "all_colors": all_colors}
+    exec(compile(ast.Module(body=fns, type_ignores=[]), "sfm.py:functions", "exec"), ns)
+    focal = ns["triangulate"](0, 1, pts0, pts1, idx0, idx1, idx3d, K)
+    P3 = np.array([p if p is not None else np.full(3, np.nan) for p in all_point3ds[0]])
+    C3 = np.array([c if c is not None else np.full(3, -1) for c in all_point3ds[1]]).astype(np.int64)
+    save("sfm_triangulate_golden.npz", K=K, cam0=cam_in[0], cam1=cam_in[1], pts0=pts0, pts1=pts1, idx0=idx0,
+         idx1=idx1, idx3d=idx3d, n_tracks=np.array(n_tracks), colors=np.stack(list(all_colors)),
+         focal=np.array(focal), cam1_out=cameras[1], points=P3, point_colors=C3)
+
+
 if __name__ == "__main__":
     gen_vq()
     gen_filter_matches()
@@ -349,3 +407,4 @@ if __name__ == "__main__":
     gen_ba_sparse_and_jacobian()
     gen_bow()
     gen_bfs()
+    gen_sfm_triangulate()
