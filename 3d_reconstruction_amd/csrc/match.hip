@@ -328,33 +328,55 @@ __global__ void mutual_kernel(int32_t* __restrict__ m0, int32_t* __restrict__ m1
 }
 
 // ---------------------------------------------------------------------------
-// vq: 16 threads per observation, each scanning codes c = lane16, lane16+16, ...
-// with the distance summed in k order (f64), then a 16-lane argmin reduction
+// vq: 16 lanes per observation (16 observations per workgroup); the code book
+// streams through LDS in chunks of 32 codewords (row stride padded by one f64
+// so the 16 codewords a wave reads at one k sit in distinct banks); each lane
+// accumulates 2 codewords of the chunk (sum of squared differences in k order,
+// one fused multiply-add per term: exact for integer-valued data, within
+// rounding of scipy's BLAS-form distance otherwise), then a 16-lane argmin
 // with lowest-index tie-break.
 constexpr int kVqObsPerBlock = 16;
+constexpr int kVqCodesPerChunk = 32;
 
 __global__ __launch_bounds__(256) void vq_kernel(const double* __restrict__ obs, int64_t n_obs,
                                                  const double* __restrict__ code, int n_codes, int d,
                                                  int32_t* __restrict__ codes, double* __restrict__ dist) {
-    extern __shared__ double sobs[];  // [16][d]
+    extern __shared__ double smem[];
+    double* sobs = smem;                                   // [16][d]
+    double* scode = smem + kVqObsPerBlock * d;             // [64][d + 1]
+    const int ld = d + 1;
     const int64_t o0 = (int64_t)blockIdx.x * kVqObsPerBlock;
     for (int t = threadIdx.x; t < kVqObsPerBlock * d; t += blockDim.x) {
         const int64_t o = o0 + t / d;
         sobs[t] = (o < n_obs) ? obs[o * d + (t % d)] : 0.0;
     }
-    __syncthreads();
     const int lo = threadIdx.x >> 4, l16 = threadIdx.x & 15;
     const double* x = sobs + lo * d;
     double best = __builtin_inf();
     int bidx = INT_MAX;
-    for (int c = l16; c < n_codes; c += 16) {
-        const double* y = code + (size_t)c * d;
-        double s = 0.0;
-        for (int k = 0; k < d; ++k) {
-            const double df = x[k] - y[k];
-            s = s + df * df;
+    for (int c0 = 0; c0 < n_codes; c0 += kVqCodesPerChunk) {
+        const int nc = min(kVqCodesPerChunk, n_codes - c0);
+        __syncthreads();
+        for (int t = threadIdx.x; t < nc * d; t += blockDim.x) {
+            const int r = t / d;
+            scode[r * ld + (t - r * d)] = code[(size_t)(c0 + r) * d + (t - r * d)];
         }
-        if (s < best) { best = s; bidx = c; }
+        __syncthreads();
+        double acc[2] = {0.0, 0.0};
+        for (int k = 0; k < d; ++k) {
+            const double xv = x[k];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = l16 + 16 * j;
+                const double df = xv - scode[r * ld + k];
+                acc[j] = __builtin_fma(df, df, acc[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {   // codewords ascend with j -> strict < keeps the lowest index
+            const int r = l16 + 16 * j;
+            if (r < nc && acc[j] < best) { best = acc[j]; bidx = c0 + r; }
+        }
     }
 #pragma unroll
     for (int off = 8; off >= 1; off >>= 1) {
@@ -457,11 +479,13 @@ extern "C" int sfmhip_mutual_filter(int32_t* matches0, int32_t* matches1, int P,
 extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_book, int n_codes, int d,
                          int32_t* codes, double* dist, void* stream) {
     SFMHIP_REQUIRE(obs && code_book && codes && dist, "sfmhip_vq: null pointer");
-    SFMHIP_REQUIRE(n_obs >= 0 && n_codes > 0 && d > 0 && d <= 1024, "sfmhip_vq: bad shape");
+    SFMHIP_REQUIRE(n_obs >= 0 && n_codes > 0 && d > 0 && d <= 256, "sfmhip_vq: bad shape (d <= 256)");
     if (n_obs == 0) return SFMHIP_OK;
     const int64_t blocks = (n_obs + kVqObsPerBlock - 1) / kVqObsPerBlock;
     SFMHIP_REQUIRE(blocks < INT_MAX, "sfmhip_vq: too many observations");
-    hipLaunchKernelGGL(vq_kernel, dim3((int)blocks), dim3(256), kVqObsPerBlock * d * sizeof(double),
-                       as_stream(stream), obs, n_obs, code_book, n_codes, d, codes, dist);
+    const size_t shm = (size_t)(kVqObsPerBlock * d + kVqCodesPerChunk * (d + 1)) * sizeof(double);
+    SFMHIP_REQUIRE(shm <= 160 * 1024, "sfmhip_vq: descriptor dim too large for the LDS tiles");
+    hipLaunchKernelGGL(vq_kernel, dim3((int)blocks), dim3(256), shm, as_stream(stream), obs, n_obs, code_book,
+                       n_codes, d, codes, dist);
     return check_launch("vq_kernel");
 }

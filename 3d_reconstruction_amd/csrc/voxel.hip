@@ -69,7 +69,7 @@ __device__ __forceinline__ void ray_step(Ray& R) {
 }
 
 __global__ void dda_count_kernel(const float* __restrict__ rays, int64_t N, float bin, int max_steps,
-                                 int32_t* __restrict__ n_steps, int32_t* __restrict__ overflow) {
+                                 int32_t* __restrict__ n_steps) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     Ray R;
@@ -81,32 +81,60 @@ __global__ void dda_count_kernel(const float* __restrict__ rays, int64_t N, floa
         ++k;
         act = ray_active(R);
     }
-    if (act) atomicOr(overflow, 1);
-    n_steps[i] = k;
+    n_steps[i] = act ? max_steps + 1 : k;   // max_steps + 1 = still active at the cap
 }
 
-__global__ void dda_fill_kernel(const float* __restrict__ rays, int64_t N, float bin, int S,
-                                float* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N) return;
-    Ray R;
-    ray_setup(rays + 8 * i, bin, R);
-    float* o = out + (size_t)i * S * 3;
+// Pass 2: every lane walks its ray; rows are produced kDdaCh steps at a time
+// into an LDS tile [64 rays][kDdaCh*3] and written back cooperatively by the
+// wave (consecutive lanes -> consecutive floats of one ray's row), instead of
+// 64 lanes each storing to its own far-apart row.
+constexpr int kDdaCh = 16;
+
+__global__ __launch_bounds__(256) void dda_fill_kernel(const float* __restrict__ rays, int64_t N, float bin, int S,
+                                                       float* __restrict__ out) {
+    __shared__ float tile[4][64 * kDdaCh * 3];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t ray0 = ((int64_t)blockIdx.x * 4 + w) * 64;   // first ray of this wave
+    if (ray0 >= N) return;                                     // wave-uniform
+    const int64_t i = ray0 + lane;
     const float nan = __builtin_nanf("");
-    o[0] = R.cur[0]; o[1] = R.cur[1]; o[2] = R.cur[2];
-    bool act = ray_active(R);
-    int s = 1;
-    if (!act && S > 1) {  // inactive from the start: the first loop pass re-appends it
-        o[3] = R.cur[0]; o[4] = R.cur[1]; o[5] = R.cur[2];
-        s = 2;
-    }
-    while (act && s < S) {
-        ray_step(R);
-        o[3 * s] = R.cur[0]; o[3 * s + 1] = R.cur[1]; o[3 * s + 2] = R.cur[2];
-        ++s;
+    Ray R;
+    bool act = false, dup = false;
+    if (i < N) {
+        ray_setup(rays + 8 * i, bin, R);
         act = ray_active(R);
+        dup = !act;   // inactive from the start: the reference's first loop pass re-appends it
     }
-    for (; s < S; ++s) { o[3 * s] = nan; o[3 * s + 1] = nan; o[3 * s + 2] = nan; }
+    float* t = tile[w];
+    const int nrows = (int)min((int64_t)64, N - ray0);
+    for (int s0 = 0; s0 < S; s0 += kDdaCh) {
+        const int cnt = min(kDdaCh, S - s0);
+        for (int q = 0; q < cnt; ++q) {
+            const int s = s0 + q;
+            float v0 = nan, v1 = nan, v2 = nan;
+            if (i < N) {
+                if (s == 0 || (s == 1 && dup)) {
+                    v0 = R.cur[0]; v1 = R.cur[1]; v2 = R.cur[2];
+                } else if (act) {
+                    ray_step(R);
+                    v0 = R.cur[0]; v1 = R.cur[1]; v2 = R.cur[2];
+                    act = ray_active(R);
+                }
+            }
+            t[(lane * kDdaCh + q) * 3 + 0] = v0;
+            t[(lane * kDdaCh + q) * 3 + 1] = v1;
+            t[(lane * kDdaCh + q) * 3 + 2] = v2;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        const int per_row = cnt * 3;
+        for (int f = lane; f < nrows * per_row; f += 64) {
+            const int r = f / per_row, c = f - r * per_row;
+            out[((size_t)(ray0 + r) * S + s0) * 3 + c] = t[r * kDdaCh * 3 + c];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -509,36 +537,11 @@ using namespace sfmhip;
 extern "C" int sfmhip_voxel_traversal_count(const float* rays, int64_t N, float bin, int32_t max_steps,
                                             int32_t* n_steps, void* stream) {
     SFMHIP_REQUIRE(rays && n_steps, "sfmhip_voxel_traversal_count: null pointer");
-    SFMHIP_REQUIRE(N >= 0 && max_steps > 0, "sfmhip_voxel_traversal_count: bad args");
+    SFMHIP_REQUIRE(N >= 0 && max_steps > 0 && max_steps < INT_MAX, "sfmhip_voxel_traversal_count: bad args");
     if (N == 0) return SFMHIP_OK;
-    hipStream_t s = as_stream(stream);
-    int32_t* dflag = nullptr;
-    // The overflow flag rides in a pinned host word so no device allocation is needed.
-    int32_t* hflag = nullptr;
-    if (hipHostMalloc((void**)&hflag, sizeof(int32_t), hipHostMallocMapped) != hipSuccess) {
-        set_error("sfmhip_voxel_traversal_count: hipHostMalloc failed");
-        return SFMHIP_E_HIP;
-    }
-    *hflag = 0;
-    if (hipHostGetDevicePointer((void**)&dflag, hflag, 0) != hipSuccess) {
-        (void)hipHostFree(hflag);
-        set_error("sfmhip_voxel_traversal_count: hipHostGetDevicePointer failed");
-        return SFMHIP_E_HIP;
-    }
-    hipLaunchKernelGGL(dda_count_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, s, rays, N, bin, max_steps,
-                       n_steps, dflag);
-    int rc = check_launch("dda_count_kernel");
-    if (rc == SFMHIP_OK) {
-        if (hipStreamSynchronize(s) != hipSuccess) {
-            set_error("sfmhip_voxel_traversal_count: stream sync failed");
-            rc = SFMHIP_E_HIP;
-        } else if (*hflag) {
-            set_error("sfmhip_voxel_traversal_count: a ray exceeded max_steps=%d", max_steps);
-            rc = SFMHIP_E_OVERFLOW;
-        }
-    }
-    (void)hipHostFree(hflag);
-    return rc;
+    hipLaunchKernelGGL(dda_count_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, as_stream(stream), rays, N, bin,
+                       max_steps, n_steps);
+    return check_launch("dda_count_kernel");
 }
 
 extern "C" int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, int32_t S, float* out,
@@ -547,7 +550,7 @@ extern "C" int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, i
     SFMHIP_REQUIRE(N >= 0 && S >= 1, "sfmhip_voxel_traversal: bad args");
     if (N == 0) return SFMHIP_OK;
     hipLaunchKernelGGL(dda_fill_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, as_stream(stream), rays, N, bin, S,
-                       out);
+                       out);  // 4 waves x 64 rays per workgroup
     return check_launch("dda_fill_kernel");
 }
 

@@ -39,7 +39,11 @@ def voxel_traversal(rays: torch.Tensor, _bin_size, max_steps: int = 1 << 20) -> 
     b = float(_bin_size)
     steps = torch.empty(N, dtype=torch.int32, device=r.device)
     call("sfmhip_voxel_traversal_count", ptr(r), N, b, int(max_steps), ptr(steps), stream_ptr())
-    S = 1 + (int(steps.max().item()) if N > 0 else 0)
+    longest = int(steps.max().item()) if N > 0 else 0
+    if longest > max_steps:
+        raise RuntimeError(f"voxel_traversal: a ray is still active after max_steps={max_steps} "
+                           "(the reference loop would not terminate)")
+    S = 1 + longest
     out = torch.empty((N, S, 3), dtype=torch.float32, device=r.device)
     call("sfmhip_voxel_traversal", ptr(r), N, b, S, ptr(out), stream_ptr())
     return out

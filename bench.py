@@ -114,6 +114,128 @@ def cpu_baseline_match(qcpu, pairs, sample, budget_s=12.0):
     return n_done / t_used, n_done, t_used
 
 
+def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
+    """V1 DDA traversal, V2+V4 fused sample/SH/composite at the plenoxel config
+    (28 x 256^3 grid, 2048 rays x 192 bins per batch) and M2 vq (C3 descriptors
+    as f64 vs a 200-word codebook), each with an oracle CPU baseline sample."""
+    out = []
+    g = torch.Generator(device=device)
+    g.manual_seed(7)
+    # V1: the survey's probe geometry (4096 rays, bin 1, far <= 64).  The output is
+    # the reference's (N, S_max, 3) NaN-padded tensor, so its size grows with the
+    # longest ray; at 1M rays it is ~89 GB of mostly padding (tools/dda_probe.py).
+    nr = 4096
+    o = torch.rand((nr, 3), generator=g, device=device) * 64 - 32
+    dvec = torch.randn((nr, 3), generator=g, device=device)
+    far = torch.rand((nr, 1), generator=g, device=device) * 64
+    rays = torch.cat([o, dvec / dvec.norm(dim=1, keepdim=True), torch.zeros_like(far), far], 1).contiguous()
+
+    def dda_step(record):
+        e0 = e1 = None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        vt = sfm.voxel_traversal(rays, 1.0)
+        if record:
+            e1.record()
+        return (e0, e1)
+
+    wall, _ = timed(dda_step, args.steps, 1, barrier)
+    ms = wall / args.steps * 1e3
+    line = {"metric": "voxel_traversal rays/sec", "value": nr / (ms * 1e-3), "unit": "rays/s", "ms_per_step": ms,
+            "config": {"workload": "V1 DDA (voxel_travesal.py semantics): 4096 rays, bin 1, far U(0,64) "
+                                   "(count pass + host S_max + fill pass)"}}
+    if cpu:
+        from oracle import voxel as ov
+        rr = rays.cpu().numpy()
+        t0 = time.perf_counter()
+        ov.voxel_traversal(rr, 1.0)
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": nr / dt, "unit": "rays/s", "cores": 1, "kind": "port",
+                                "sample": f"the same {nr} rays through oracle.voxel.voxel_traversal (numpy), {dt:.2f}s"}
+    out.append(line)
+    # V2+V4: plenoxel N=256 grid, 16 batches of 2048 rays x 192 bins
+    N, B, S, NB = 256, 2048, 192, 16
+    grid = (torch.randn((28, N, N, N), generator=g, device=device) * 0.1)
+    vg = sfm.VoxelGrid.plenoxel(grid, 1.5)
+    vg.voxel_major()
+    del grid
+    ro = torch.randn((NB * B, 3), generator=g, device=device) * 0.2 + torch.tensor([0.0, 0.0, -3.0], device=device)
+    rd = torch.randn((NB * B, 3), generator=g, device=device) * 0.2 + torch.tensor([0.0, 0.0, 1.0], device=device)
+    rd = rd / rd.norm(dim=1, keepdim=True)
+    t = torch.linspace(2.0, 6.0, S, device=device).expand(NB * B, S)
+    mid = (t[:, :-1] + t[:, 1:]) / 2
+    u = torch.rand((NB * B, S), generator=g, device=device)
+    z = (torch.cat([t[:, :1], mid], 1) + (torch.cat([mid, t[:, -1:]], 1) - torch.cat([t[:, :1], mid], 1)) * u)
+    z = z.contiguous()
+
+    def render_step(record):
+        e0 = e1 = None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        vg.render(ro, rd, z)
+        if record:
+            e1.record()
+        return (e0, e1)
+
+    wall, kms = timed(render_step, args.steps, 1, barrier)
+    ms = wall / args.steps * 1e3
+    line = {"metric": "render_rays rays/sec", "value": NB * B / (ms * 1e-3), "unit": "rays/s", "ms_per_step": ms,
+            "config": {"workload": "V2+V4 plenoxel render_rays: 28x256^3 grid, 16 x (2048 rays x 192 bins)"},
+            "roofline": {"bound": "hbm", "kernel": "render_kernel", "kernel_ms": float(np.mean(kms)),
+                         "algorithmic_bytes_per_sample": 8 * 112}}
+    if cpu:
+        from oracle import voxel as ov
+        gsmall = vg.grid.cpu().numpy()
+        t0 = time.perf_counter()
+        ov.render(gsmall, (-1.5,) * 3, (1.5,) * 3, 1, ro[:64].cpu().numpy(), rd[:64].cpu().numpy(),
+                  z[:64].cpu().numpy())
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": 64 / dt, "unit": "rays/s", "cores": 1, "kind": "port",
+                                "sample": f"64 rays x 192 bins through oracle.voxel.render (numpy f32), {dt:.2f}s"}
+        del gsmall
+    out.append(line)
+    del vg
+    torch.cuda.empty_cache()
+    # M2: vq of all C3 descriptors (f64) against a 200-word codebook
+    obs = syn.superpoint_like(N_IMG, M_KPT, 128, seed=3, device=device).reshape(-1, 128).double().contiguous()
+    book = obs[torch.randperm(obs.shape[0], generator=g, device=device)[:200]].contiguous()
+    codes = torch.empty(obs.shape[0], dtype=torch.int32, device=device)
+    dist = torch.empty(obs.shape[0], dtype=torch.float64, device=device)
+    from importlib import import_module
+    abi = import_module("3d_reconstruction_amd._abi")
+
+    def vq_step(record):
+        e0 = e1 = None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        abi.call("sfmhip_vq", obs.data_ptr(), obs.shape[0], book.data_ptr(), 200, 128, codes.data_ptr(),
+                 dist.data_ptr(), abi.stream_ptr())
+        if record:
+            e1.record()
+        return (e0, e1)
+
+    wall, kms = timed(vq_step, args.steps, 1, barrier)
+    ms = wall / args.steps * 1e3
+    line = {"metric": "vq obs/sec", "value": obs.shape[0] / (ms * 1e-3), "unit": "obs/s", "ms_per_step": ms,
+            "config": {"workload": "M2 vq (matching.py:27): 257x4096 obs x 200 codes x 128-d, f64"},
+            "roofline": {"bound": "fp64", "kernel": "vq_kernel", "kernel_ms": float(np.mean(kms)),
+                         "achieved_tflops": 3 * obs.shape[0] * 200 * 128 / (np.mean(kms) * 1e-3) / 1e12,
+                         "peak_tflops": PEAK_FP64_TFLOPS}}
+    if cpu:
+        from scipy.cluster.vq import vq as scipy_vq
+        oo, bb = obs[:4096].cpu().numpy(), book.cpu().numpy()
+        t0 = time.perf_counter()
+        scipy_vq(oo, bb)
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": 4096 / dt, "unit": "obs/s", "cores": blas_threads(), "kind": "reference",
+                                "sample": f"scipy.cluster.vq.vq (the reference's own call) on 4096 obs, {dt:.3f}s"}
+    out.append(line)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -301,6 +423,11 @@ def main():
                          "kernel_ms": max_over_ranks(float(np.mean(kms_b)), world, device),
                          "algorithmic_bytes_per_obs": 64 + 200},
         })
+
+    # ---------------- voxel anchors + vq (N=1 only; rays / obs are independent) --
+    if not args.skip_secondary and world == 1:
+        result["secondary"].extend(voxel_and_vq_lines(sfm, syn, device, args, barrier,
+                                                      cpu=(not args.no_cpu_baseline)))
 
     # ---------------- CPU baseline (rank 0, N=1 only) ------------------------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -134,8 +134,8 @@ int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, const double* 
 
 /* ---- V1: voxel_traversal (voxel_travesal.py:1-73), quirks included -------
  * rays [N][8] f32 = o(3), d(3), near, far.  Pass 1 counts per-ray steps
- * (n_steps[N], capped at max_steps -> SFMHIP_E_OVERFLOW), pass 2 writes
- * out [N][S][3] f32 (NaN padded) with S = 1 + max(n_steps) (or 1).          */
+ * (n_steps[N]; a ray still active after max_steps reports max_steps + 1),
+ * pass 2 writes out [N][S][3] f32 (NaN padded) with S = 1 + max(n_steps).   */
 int sfmhip_voxel_traversal_count(const float* rays, int64_t N, float bin,
                                  int32_t max_steps, int32_t* n_steps, void* stream);
 int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, int32_t S,
