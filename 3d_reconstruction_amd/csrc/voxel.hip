@@ -352,13 +352,15 @@ template <> struct TsdfTile<3> { static constexpr int X = 64, Y = 1, Z = 4; };
 // (64 x 64 x 16 voxels for MAP 0).  Workgroups resident on one XCD at the same
 // time then project onto one compact image region per frame, so the depth
 // lines they gather stay in that XCD's L2 (speed only, never correctness).
-constexpr int kSbX = 4, kSbY = 16, kSbZ = 4;
+struct SuperBrick { int x, y, z; };   // super-brick extent in bricks (default 4 x 4 x 16: 64 x 16 x 64 voxels, measured best)
 
 template <int MAP, int U, bool SWZ>
 __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float* __restrict__ Wt, int D, int H,
                                                    int W, int z0, int z1, const float* __restrict__ depth, int F,
                                                    int Hd, int Wd, const float* __restrict__ poses,
-                                                   const float* __restrict__ Kf, Bounds B, float trunc) {
+                                                   const float* __restrict__ Kf, Bounds B, float trunc,
+                                                   SuperBrick SB) {
+    const int kSbX = SB.x, kSbY = SB.y, kSbZ = SB.z;
     using TT = TsdfTile<MAP>;
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (SWZ) {
@@ -638,14 +640,16 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     const int map = env_int("SFMHIP_TSDF_MAP", 0);
     const int unroll = env_int("SFMHIP_TSDF_U", 4);
     const int swz = env_int("SFMHIP_TSDF_SWZ", 1);
+    const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 4)), std::max(1, env_int("SFMHIP_TSDF_SBY", 4)),
+                        std::max(1, env_int("SFMHIP_TSDF_SBZ", 16))};
     const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", 32)));
     static const int tx[4] = {16, 16, 8, 64}, ty[4] = {4, 4, 4, 1}, tz[4] = {4, 4, 8, 4};
     const int mi = swz ? 0 : ((map >= 0 && map < 4) ? map : 0);
     const int nbx = ceil_div(W, tx[mi]), nby = ceil_div(H, ty[mi]), nbz = ceil_div(z1 - z0, tz[mi]);
     dim3 grid(nbx, nby, nbz);
     if (swz) {
-        const int64_t slots = (int64_t)ceil_div(nbx, kSbX) * ceil_div(nby, kSbY) * ceil_div(nbz, kSbZ) *
-                              (kSbX * kSbY * kSbZ);
+        const int64_t slots = (int64_t)ceil_div(nbx, sb.x) * ceil_div(nby, sb.y) * ceil_div(nbz, sb.z) *
+                              (sb.x * sb.y * sb.z);
         SFMHIP_REQUIRE(slots < INT_MAX, "sfmhip_tsdf_integrate: grid too large");
         grid = dim3((unsigned)slots, 1, 1);
     }
@@ -658,7 +662,7 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
         const Bounds bb = make_bounds(bmin, bmax);
 #define SFMHIP_TSDF(MM, UU, SS)                                                                              \
     hipLaunchKernelGGL((tsdf_kernel<MM, UU, SS>), grid, dim3(256), 0, as_stream(stream), T, Wt, D, H, W, z0, \
-                       z1, dp, nf, Hd, Wd, pp, kp, bb, trunc)
+                       z1, dp, nf, Hd, Wd, pp, kp, bb, trunc, sb)
 #define SFMHIP_TSDF_M(MM)                          \
     switch (unroll) {                              \
         case 1: SFMHIP_TSDF(MM, 1, false); break;  \
