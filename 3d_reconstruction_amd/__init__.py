@@ -15,9 +15,10 @@ from .geometry import (Rodrigues, ba_sparse, calculate_reprojection_error,  # no
                        residual_jacobian_batched, triangulatePoints, triangulate_batched)
 from .voxel import (MASK_PLENOXEL, MASK_SDF, VoxelGrid, tsdf_integrate,  # noqa: F401
                     voxel_traversal)
-from . import bow, pipeline, reconstruct, tracks  # noqa: F401,E402
+from . import bow, pipeline, reconstruct, tracks, verify  # noqa: F401,E402
 from .bow import kmeans  # noqa: F401
 from .reconstruct import triangulate  # noqa: F401
 from .tracks import MatchGraph, bfs_tracks  # noqa: F401
+from .verify import findEssentialMat, recoverPose  # noqa: F401
 
 __version__ = "0.1.0"

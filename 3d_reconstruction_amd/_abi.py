@@ -38,6 +38,7 @@ _p = ctypes.c_void_p
 _i32 = ctypes.c_int
 _i64 = ctypes.c_int64
 _f32 = ctypes.c_float
+_f64 = ctypes.c_double
 
 # name -> argtypes, in the order of include/sfmhip.h
 SIGNATURES = {
@@ -63,6 +64,8 @@ SIGNATURES = {
     "sfmhip_render_rays": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _i64, _i32, _p, _p],
     "sfmhip_tsdf_integrate": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p,
                               _f32, _p],
+    "sfmhip_find_essential": [_p, _p, _p, _i32, _p, _f64, _f64, _i32, _p, _p, _p, _p, _p, _p, _p],
+    "sfmhip_recover_pose": [_p, _i64, _p, _p, _p, _i32, _p, _p, _f64, _p, _p, _p, _p, _p],
 }
 
 

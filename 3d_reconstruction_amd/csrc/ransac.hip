@@ -1,0 +1,882 @@
+// ransac.hip — SURVEY.md §8f row 2: batched geometric verification, f64.
+//
+// Reference call sites:
+//   cv2.findEssentialMat(pts0, pts1, K, method=cv2.RANSAC, prob=0.999, threshold=1)
+//        matching.py:134, sfm.py:108
+//   cv2.recoverPose(E, pts0, pts1, K)                 matching.py:139, sfm.py:117,119
+// Restated from OpenCV 4.x (calib3d: ptsetreg.cpp RANSACPointSetRegistrator,
+// five-point.cpp EMEstimatorCallback, decomposeEssentialMat, recoverPose);
+// the CPU restatement is oracle/ransac.py.  Parity at the OpenCV boundary is
+// unpinned (cv2 absent).
+//
+// One workgroup (8 waves) per image pair.  Hypotheses are processed kRH = 32
+// at a time:
+//   1. lane 0 draws the 32 five-point samples from cv::RNG(-1) (sequential by
+//      definition — a sample depends only on the draw order, never on the
+//      models, so the draws can run ahead of the scoring);
+//   2. each sample is solved by a 16-lane group (Nister's method): the 10x20
+//      constraint matrix is held column-per-lane in registers and reduced by
+//      Gauss-Jordan with shuffles; the real roots of the degree-10 polynomial
+//      are isolated level by level between the roots of its derivatives, one
+//      interval per lane; one lane per root back-substitutes;
+//   3. all 512 lanes score every model of the chunk (points in registers,
+//      Sampson error as float with an exact division only near the
+//      threshold, wave reductions, LDS atomics);
+//   4. lane 0 replays the chunk in OpenCV's sequential order: a model
+//      replaces the best iff count > max(best, 4), niters shrinks by
+//      RANSACUpdateNumIters — so the chosen model and the iteration count are
+//      exactly those of the sequential loop over the same models.
+#include "common.h"
+#include "geom_dev.h"
+
+namespace sfmhip {
+namespace {
+
+constexpr int kRThreads = 512;          // essential kernel: 8 waves
+constexpr int kGL = 16;                 // lanes per hypothesis group
+constexpr int kRH = kRThreads / kGL;    // hypotheses per chunk (32)
+constexpr int kMaxModels = 10;
+constexpr int kGS = 224;                // LDS doubles per group
+constexpr int kPB = 4;                  // points per lane per scoring block
+constexpr int kPThreads = 256;          // recover_pose kernel
+constexpr double kDblEps = 2.220446049250313e-16;
+constexpr double kDblMin = 2.2250738585072014e-308;
+
+// cv::RNG: multiply-with-carry, uniform(a, b) = a + next() % (b - a).
+struct CvRng {
+    uint64_t s;
+    __device__ unsigned next() {
+        s = (uint64_t)(unsigned)s * 4164903690ULL + (unsigned)(s >> 32);
+        return (unsigned)s;
+    }
+    __device__ int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + (unsigned)a); }
+    // uniform(0, n) with x % n computed from a double reciprocal (exact after
+    // one correction: x < 2^32, so the quotient estimate is off by at most 1)
+    __device__ int uniform0(unsigned n, double inv_n) {
+        const unsigned x = next();
+        unsigned qd = (unsigned)((double)x * inv_n);
+        long long r = (long long)x - (long long)qd * n;
+        if (r < 0) r += n;
+        else if (r >= (long long)n) r -= n;
+        return (int)r;
+    }
+};
+
+// RANSACUpdateNumIters (ptsetreg.cpp).
+__device__ int update_num_iters(double p, double ep, int m, int max_iters) {
+    p = fmax(p, 0.0);
+    p = fmin(p, 1.0);
+    ep = fmax(ep, 0.0);
+    ep = fmin(ep, 1.0);
+    double num = fmax(1.0 - p, kDblMin);
+    double denom = 1.0 - pow(1.0 - ep, (double)m);
+    if (denom < kDblMin) return 0;
+    num = log(num);
+    denom = log(denom);
+    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
+}
+
+// Monomial tables.  Linear: x y z 1.  Quadratic: x2 xy xz x y2 yz y z2 z 1.
+// Cubic (Nister / OpenCV order): x3 y3 x2y xy2 x2z x2 y2z y2 xyz xy | xz2 xz x yz2 yz y z3 z2 z 1.
+constexpr int kLL[4][4] = {{0, 1, 2, 3}, {1, 4, 5, 6}, {2, 5, 7, 8}, {3, 6, 8, 9}};
+constexpr int kQL[10][4] = {{0, 2, 4, 5},    {2, 3, 8, 9},     {4, 8, 10, 11},   {5, 9, 11, 12},
+                            {3, 1, 6, 7},    {8, 6, 13, 14},   {9, 7, 14, 15},   {10, 13, 16, 17},
+                            {11, 14, 17, 18}, {12, 15, 18, 19}};
+__device__ __forceinline__ void mul_ll(const double* a, const double* b, double sgn, double* q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[kLL[i][j]] += sgn * (a[i] * b[j]);
+}
+__device__ __forceinline__ void mul_ql(const double* q, const double* l, double sgn, double* c) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[kQL[i][j]] += sgn * (q[i] * l[j]);
+}
+
+template <int NA, int NB>
+__device__ __forceinline__ void pmul(const double* a, const double* b, double* o) {
+#pragma unroll
+    for (int i = 0; i < NA + NB - 1; ++i) o[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) o[i + j] += a[i] * b[j];
+}
+
+__device__ __forceinline__ void wave_sync_lds() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
+// Phase timers for tools/prof_ransac.py: build with -DSFMHIP_RANSAC_PROF
+// (make EXTRA=-DSFMHIP_RANSAC_PROF); compiled out otherwise.
+__device__ unsigned long long g_rprof[16];
+#ifdef SFMHIP_RANSAC_PROF
+#define SPROF(i) do { if (threadIdx.x == 0) { const unsigned long long t1 = wall_clock64(); atomicAdd(&g_rprof[i], t1 - st); st = t1; } } while (0)
+#define SPROF_INIT unsigned long long st = wall_clock64()
+#define RPROF(i, t0) do { if (tid == 0) { const unsigned long long t1 = wall_clock64(); atomicAdd(&g_rprof[i], t1 - t0); t0 = t1; } } while (0)
+#define RPROF_INIT unsigned long long tp = wall_clock64()
+#define PROF_COUNT(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_rprof[i], (unsigned long long)(v)); } while (0)
+#else
+#define SPROF(i) do {} while (0)
+#define SPROF_INIT do {} while (0)
+#define RPROF(i, t0) do {} while (0)
+#define RPROF_INIT do {} while (0)
+#define PROF_COUNT(i, v) do {} while (0)
+#endif
+
+// EMEstimatorCallback::runKernel for one sample, by a 16-lane group (gl =
+// lane in group, gsh = bit offset of the group in the wave's ballot).  G is
+// the group's LDS area; up to 10 unit-norm E (row-major) go to models.
+__device__ int five_point_group(const double (&q)[5][4], int gl, int gsh, double* G, double* models) {
+    SPROF_INIT;
+    // 1. orthonormal null-space basis of the 5x9 system (Householder QR of
+    //    Q^T, reflectors stored in place; every lane computes it in registers).
+    double A[9][5], beta[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const double x1 = q[j][0], y1 = q[j][1], x2 = q[j][2], y2 = q[j][3];
+        A[0][j] = x1 * x2; A[1][j] = y1 * x2; A[2][j] = x2;
+        A[3][j] = x1 * y2; A[4][j] = y1 * y2; A[5][j] = y2;
+        A[6][j] = x1;      A[7][j] = y1;      A[8][j] = 1.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        double nrm2 = 0;
+#pragma unroll
+        for (int r = k; r < 9; ++r) nrm2 += A[r][k] * A[r][k];
+        const double nrm = sqrt(nrm2);
+        const double alpha = (A[k][k] >= 0) ? -nrm : nrm;
+        A[k][k] -= alpha;  // column k below the diagonal is now the reflector v_k
+        double vn2 = 0;
+#pragma unroll
+        for (int r = k; r < 9; ++r) vn2 += A[r][k] * A[r][k];
+        beta[k] = (vn2 > 0) ? 2.0 / vn2 : 0.0;
+#pragma unroll
+        for (int c = k + 1; c < 5; ++c) {
+            double s = 0;
+#pragma unroll
+            for (int r = k; r < 9; ++r) s += A[r][k] * A[r][c];
+            s *= beta[k];
+#pragma unroll
+            for (int r = k; r < 9; ++r) A[r][c] -= s * A[r][k];
+        }
+    }
+    double basis[4][9];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) basis[j][r] = (r == 5 + j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 4; k >= 0; --k) {
+            double s = 0;
+#pragma unroll
+            for (int r = k; r < 9; ++r) s += A[r][k] * basis[j][r];
+            s *= beta[k];
+#pragma unroll
+            for (int r = k; r < 9; ++r) basis[j][r] -= s * A[r][k];
+        }
+    }
+    SPROF(3);
+    // E entries as linear polys in (x, y, z, 1): E = x b0 + y b1 + z b2 + b3.
+    double E[9][4];
+#pragma unroll
+    for (int e = 0; e < 9; ++e)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) E[e][j] = basis[j][e];
+
+    // 2. constraint rows: lane 0 -> det E, lane r = 1..9 -> (2 E E^T E - tr(E E^T) E)_{ij}
+    //    with i = (r-1)/3, j = (r-1)%3.  Rows go through LDS to become columns.
+    if (gl < 10) {
+        double c[20];
+#pragma unroll
+        for (int m = 0; m < 20; ++m) c[m] = 0.0;
+        if (gl == 0) {
+            double t1[10], t2[10], t3[10];
+#pragma unroll
+            for (int m = 0; m < 10; ++m) t1[m] = t2[m] = t3[m] = 0.0;
+            mul_ll(E[4], E[8], 1.0, t1); mul_ll(E[5], E[7], -1.0, t1);
+            mul_ll(E[3], E[8], 1.0, t2); mul_ll(E[5], E[6], -1.0, t2);
+            mul_ll(E[3], E[7], 1.0, t3); mul_ll(E[4], E[6], -1.0, t3);
+            mul_ql(t1, E[0], 1.0, c);
+            mul_ql(t2, E[1], -1.0, c);
+            mul_ql(t3, E[2], 1.0, c);
+        } else {
+            const int i = (gl - 1) / 3, j = (gl - 1) % 3;
+            double Ei[3][4], Ej[3][4], Eij[4];
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    Ei[k][m] = (i == 0) ? E[k][m] : (i == 1) ? E[3 + k][m] : E[6 + k][m];
+                    Ej[k][m] = (j == 0) ? E[3 * k][m] : (j == 1) ? E[3 * k + 1][m] : E[3 * k + 2][m];
+                }
+#pragma unroll
+            for (int m = 0; m < 4; ++m) Eij[m] = (j == 0) ? Ei[0][m] : (j == 1) ? Ei[1][m] : Ei[2][m];
+            double tr[10];
+#pragma unroll
+            for (int m = 0; m < 10; ++m) tr[m] = 0.0;
+#pragma unroll
+            for (int e = 0; e < 9; ++e) mul_ll(E[e], E[e], 1.0, tr);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                double eet[10];
+#pragma unroll
+                for (int m = 0; m < 10; ++m) eet[m] = 0.0;
+#pragma unroll
+                for (int l = 0; l < 3; ++l) mul_ll(Ei[l], E[3 * k + l], 1.0, eet);
+                mul_ql(eet, Ej[k], 2.0, c);
+            }
+            mul_ql(tr, Eij, -1.0, c);
+        }
+#pragma unroll
+        for (int m = 0; m < 20; ++m) G[gl * 20 + m] = c[m];
+    }
+    wave_sync_lds();
+    double col[10], col2[10];
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        col[r] = G[r * 20 + gl];
+        col2[r] = (gl < 4) ? G[r * 20 + 16 + gl] : 0.0;
+    }
+    wave_sync_lds();
+    double* GE = G + 128;   // E polys, kept for the back-substitution
+    double* GB = G + 64;    // B(z) polys
+    if (gl == 0)
+#pragma unroll
+        for (int e = 0; e < 9; ++e)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) GE[e * 4 + j] = E[e][j];
+    SPROF(4);
+    // 3. Gauss-Jordan on the left 10x10 block (partial pivoting; OpenCV's LU
+    //    calls a pivot below 100*DBL_EPSILON singular).  Column k lives in lane k.
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        int pl = k;
+        double pv = fabs(col[k]);
+#pragma unroll
+        for (int r = k + 1; r < 10; ++r)
+            if (fabs(col[r]) > pv) { pv = fabs(col[r]); pl = r; }
+        const int p = __shfl(pl, k, kGL);
+#pragma unroll
+        for (int r = k + 1; r < 10; ++r)
+            if (r == p) {
+                double t = col[k]; col[k] = col[r]; col[r] = t;
+                t = col2[k]; col2[k] = col2[r]; col2[r] = t;
+            }
+        double f[10];
+#pragma unroll
+        for (int r = 0; r < 10; ++r) f[r] = __shfl(col[r], k, kGL);
+        if (fabs(f[k]) < 100 * kDblEps) return 0;
+        const double inv = 1.0 / f[k];
+        const double xk = col[k] * inv, xk2 = col2[k] * inv;
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            if (r == k) continue;
+            col[r] -= f[r] * xk;
+            col2[r] -= f[r] * xk2;
+        }
+        col[k] = xk;
+        col2[k] = xk2;
+    }
+    SPROF(5);
+    // 4. rows 4..9 of A[:, :10]^-1 A[:, 10:] -> B(z) = e_row - z f_row (ascending in z).
+    if (gl >= 10) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) G[r * 10 + gl - 10] = col[4 + r];
+    } else if (gl < 4) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) G[r * 10 + 6 + gl] = col2[4 + r];
+    }
+    wave_sync_lds();
+    double bx[3][4], by[3][4], bc[3][5];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        double e[10], f[10];
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            e[c] = G[(2 * r) * 10 + c];
+            f[c] = G[(2 * r + 1) * 10 + c];
+        }
+        bx[r][0] = e[2]; bx[r][1] = e[1] - f[2]; bx[r][2] = e[0] - f[1]; bx[r][3] = -f[0];
+        by[r][0] = e[5]; by[r][1] = e[4] - f[5]; by[r][2] = e[3] - f[4]; by[r][3] = -f[3];
+        bc[r][0] = e[9]; bc[r][1] = e[8] - f[9]; bc[r][2] = e[7] - f[8]; bc[r][3] = e[6] - f[7]; bc[r][4] = -f[6];
+    }
+    wave_sync_lds();
+    if (gl == 0)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) { GB[r * 13 + m] = bx[r][m]; GB[r * 13 + 4 + m] = by[r][m]; }
+#pragma unroll
+            for (int m = 0; m < 5; ++m) GB[r * 13 + 8 + m] = bc[r][m];
+        }
+    // 5. det B(z), degree 10 (every lane).
+    double c[11];
+    {
+        double a7[8], b7[8], m7[8], a6[7], b6[7], m6[7], t[11];
+        pmul<4, 5>(by[1], bc[2], a7); pmul<4, 5>(by[2], bc[1], b7);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m7[i] = a7[i] - b7[i];
+        pmul<4, 8>(bx[0], m7, t);
+#pragma unroll
+        for (int i = 0; i < 11; ++i) c[i] = t[i];
+        pmul<4, 5>(bx[1], bc[2], a7); pmul<4, 5>(bx[2], bc[1], b7);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m7[i] = a7[i] - b7[i];
+        pmul<4, 8>(by[0], m7, t);
+#pragma unroll
+        for (int i = 0; i < 11; ++i) c[i] -= t[i];
+        pmul<4, 4>(bx[1], by[2], a6); pmul<4, 4>(bx[2], by[1], b6);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) m6[i] = a6[i] - b6[i];
+        pmul<5, 7>(bc[0], m6, t);
+#pragma unroll
+        for (int i = 0; i < 11; ++i) c[i] += t[i];
+    }
+    SPROF(6);
+    // 6. roots of det B(z) by Aberth-Ehrlich simultaneous iteration, one root
+    //    per lane (OpenCV's solvePoly iterates all roots simultaneously too,
+    //    Durand-Kerner); real roots = |imag| <= 1e-10 (five-point.cpp's
+    //    test), polished by two real Newton steps, visited in ascending order.
+    double cmax = 0;
+#pragma unroll
+    for (int i = 0; i < 11; ++i) cmax = fmax(cmax, fabs(c[i]));
+    if (cmax == 0.0) return 0;
+    int n = 10;
+#pragma unroll
+    for (int i = 10; i >= 1; --i)
+        if (n == i && fabs(c[i]) <= kDblEps * cmax) n = i - 1;
+    if (n == 0) return 0;
+    double lead = 0;
+#pragma unroll
+    for (int i = 0; i < 11; ++i)
+        if (i == n) lead = c[i];
+    double a[10];  // monic: z^n + a[n-1] z^(n-1) + ... + a[0]
+#pragma unroll
+    for (int i = 0; i < 10; ++i) a[i] = (i < n) ? c[i] / lead : 0.0;
+    const bool act = gl < n;
+    double zr = 0, zi = 0;
+    {
+        const double R = fmax(exp(log(fmax(fabs(a[0]), 1e-300)) / n), 1e-8);
+        const double ang = 6.283185307179586 * gl / n + 0.4;
+        zr = R * cos(ang);
+        zi = R * sin(ang);
+    }
+    double* Z = G;
+    bool conv = !act;
+    for (int it = 0; it < 80; ++it) {
+        if (act) { Z[2 * gl] = zr; Z[2 * gl + 1] = zi; }
+        wave_sync_lds();
+        if (!conv) {
+            double pr = 1.0, pim = 0.0, dr = 0.0, di = 0.0, pabs = 1.0;
+            const double az = sqrt(zr * zr + zi * zi);
+#pragma unroll
+            for (int j = 9; j >= 0; --j)
+                if (j < n) {
+                    pabs = __builtin_fma(pabs, az, fabs(a[j]));
+                    const double ndr = __builtin_fma(dr, zr, __builtin_fma(-di, zi, pr));
+                    const double ndi = __builtin_fma(dr, zi, __builtin_fma(di, zr, pim));
+                    const double npr = __builtin_fma(pr, zr, __builtin_fma(-pim, zi, a[j]));
+                    const double npi = __builtin_fma(pr, zi, pim * zr);
+                    dr = ndr; di = ndi; pr = npr; pim = npi;
+                }
+            // N = p / p'
+            const double dd = dr * dr + di * di;
+            double nr_ = 0, ni_ = 0;
+            if (dd > 0) {
+                nr_ = (pr * dr + pim * di) / dd;
+                ni_ = (pim * dr - pr * di) / dd;
+            }
+            double sr = 0, si = 0;  // S = sum_{j != i} 1 / (z - z_j)
+#pragma unroll
+            for (int j = 0; j < 10; ++j)
+                if (j < n && j != gl) {
+                    const double xr = zr - Z[2 * j], xi = zi - Z[2 * j + 1];
+                    const double m = xr * xr + xi * xi;
+                    if (m > 0) { sr += xr / m; si -= xi / m; }
+                }
+            // w = N / (1 - N S)
+            const double qr = 1.0 - (nr_ * sr - ni_ * si), qi = -(nr_ * si + ni_ * sr);
+            const double qq = qr * qr + qi * qi;
+            double wr = nr_, wi = ni_;
+            if (qq > 0) {
+                wr = (nr_ * qr + ni_ * qi) / qq;
+                wi = (ni_ * qr - nr_ * qi) / qq;
+            }
+            zr -= wr;
+            zi -= wi;
+            // converged: step at rounding level, or |p(z)| within the rounding noise of Horner
+            conv = sqrt(wr * wr + wi * wi) <= 4 * kDblEps * sqrt(zr * zr + zi * zi) ||
+                   sqrt(pr * pr + pim * pim) <= 16 * kDblEps * pabs;
+        }
+        wave_sync_lds();
+        if ((((unsigned)(__ballot(!conv) >> gsh)) & 0xFFFFu) == 0u) {
+            PROF_COUNT(12, it);
+            PROF_COUNT(13, 1);
+            break;
+        }
+    }
+    bool real = act && fabs(zi) <= 1e-10;
+    double xr = zr;
+    if (real) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            double f = 1.0, df = 0.0;
+#pragma unroll
+            for (int j = 9; j >= 0; --j)
+                if (j < n) {
+                    df = __builtin_fma(df, xr, f);
+                    f = __builtin_fma(f, xr, a[j]);
+                }
+            if (df != 0.0 && f != 0.0) xr -= f / df;
+        }
+    }
+    if (act) { Z[2 * gl] = real ? xr : 0.0; Z[2 * gl + 1] = real ? 1.0 : 0.0; }
+    wave_sync_lds();
+    const unsigned rm = ((unsigned)(__ballot(real) >> gsh)) & 0xFFFFu;
+    int rank = 0;
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+        if (j < n && j != gl && Z[2 * j + 1] != 0.0) {
+            const double xj = Z[2 * j];
+            rank += (xj < xr || (xj == xr && j < gl)) ? 1 : 0;
+        }
+    wave_sync_lds();
+    double* prev = G + 32;
+    if (real) prev[rank] = xr;
+    wave_sync_lds();
+    const int np = __popc(rm);
+    const int nr = np;
+    SPROF(7);
+    // 7. back-substitution, one root per lane: null vector of B(z) -> (x, y),
+    //    E = x E0 + y E1 + z E2 + E3, normalised.
+    bool ok = false;
+    double ev[9];
+    if (gl < nr) {
+        const double z = prev[gl];
+        double row[3][3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const double* b = GB + r * 13;
+            row[r][0] = ((b[3] * z + b[2]) * z + b[1]) * z + b[0];
+            row[r][1] = ((b[7] * z + b[6]) * z + b[5]) * z + b[4];
+            row[r][2] = (((b[12] * z + b[11]) * z + b[10]) * z + b[9]) * z + b[8];
+        }
+        double best[3] = {0, 0, 0}, bn = -1;
+#pragma unroll
+        for (int pi = 0; pi < 3; ++pi) {
+            const int a = (pi == 2) ? 1 : 0, b = (pi == 0) ? 1 : 2;
+            const double cx = row[a][1] * row[b][2] - row[a][2] * row[b][1];
+            const double cy = row[a][2] * row[b][0] - row[a][0] * row[b][2];
+            const double cz = row[a][0] * row[b][1] - row[a][1] * row[b][0];
+            const double n2 = cx * cx + cy * cy + cz * cz;
+            if (n2 > bn) { bn = n2; best[0] = cx; best[1] = cy; best[2] = cz; }
+        }
+        if (bn > 0) {
+            const double inv = 1.0 / sqrt(bn);
+            const double v0 = best[0] * inv, v1 = best[1] * inv, v2 = best[2] * inv;
+            if (fabs(v2) >= 1e-10) {
+                const double x = v0 / v2, y = v1 / v2;
+                double n2 = 0;
+#pragma unroll
+                for (int e = 0; e < 9; ++e) {
+                    ev[e] = GE[4 * e] * x + GE[4 * e + 1] * y + GE[4 * e + 2] * z + GE[4 * e + 3];
+                    n2 += ev[e] * ev[e];
+                }
+                const double s = 1.0 / sqrt(n2);
+#pragma unroll
+                for (int e = 0; e < 9; ++e) ev[e] *= s;
+                ok = true;
+            }
+        }
+    }
+    const unsigned gm = (unsigned)(__ballot(ok) >> gsh) & 0xFFFFu;
+    if (ok) {
+        const int slot = __popc(gm & ((1u << gl) - 1u));
+#pragma unroll
+        for (int e = 0; e < 9; ++e) models[slot * 9 + e] = ev[e];
+    }
+    SPROF(8);
+    return __popc(gm);
+}
+
+// EMEstimatorCallback::computeError (Matx op order) <= t, where the stored
+// error is (float)(num / den).  T = the largest double that rounds to a float
+// <= t; num/den is compared against T with a 2^-40 relative margin and only
+// the undecided points take the exact division.
+__device__ __forceinline__ bool sampson_in(const double* E, double x1, double y1, double x2, double y2, float tf,
+                                           double tlo, double thi) {
+    const double ex0 = (E[0] * x1 + E[1] * y1) + E[2];
+    const double ex1 = (E[3] * x1 + E[4] * y1) + E[5];
+    const double ex2 = (E[6] * x1 + E[7] * y1) + E[8];
+    const double et0 = (E[0] * x2 + E[3] * y2) + E[6];
+    const double et1 = (E[1] * x2 + E[4] * y2) + E[7];
+    const double d = (x2 * ex0 + y2 * ex1) + ex2;
+    const double num = d * d;
+    const double den = ((ex0 * ex0 + ex1 * ex1) + et0 * et0) + et1 * et1;
+    if (den > 0) {
+        if (num <= den * tlo) return true;
+        if (num > den * thi) return false;
+    }
+    return (float)(num / den) <= tf;
+}
+
+__device__ __forceinline__ float sampson(const double* E, double x1, double y1, double x2, double y2) {
+    const double ex0 = (E[0] * x1 + E[1] * y1) + E[2];
+    const double ex1 = (E[3] * x1 + E[4] * y1) + E[5];
+    const double ex2 = (E[6] * x1 + E[7] * y1) + E[8];
+    const double et0 = (E[0] * x2 + E[3] * y2) + E[6];
+    const double et1 = (E[1] * x2 + E[4] * y2) + E[7];
+    const double d = (x2 * ex0 + y2 * ex1) + ex2;
+    return (float)(d * d / (((ex0 * ex0 + ex1 * ex1) + et0 * et0) + et1 * et1));
+}
+
+__device__ __forceinline__ int wave_count(bool pred) { return __popcll(__ballot(pred)); }
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+
+__global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
+    const double* __restrict__ pts0, const double* __restrict__ pts1, const int64_t* __restrict__ offs,
+    const double* __restrict__ cam, double prob, double threshold, int max_iters, double* __restrict__ qn,
+    double* __restrict__ E_out, int32_t* __restrict__ nmodels_out, uint8_t* __restrict__ mask,
+    int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out) {
+    __shared__ double s_grp[kRH * kGS];
+    __shared__ double s_models[kRH * kMaxModels * 9];
+    __shared__ int s_nmod[kRH];
+    __shared__ int s_cnt[kRH * kMaxModels];
+    __shared__ int s_sub[kRH * 5];
+    __shared__ double s_best[9];
+    __shared__ int s_niters, s_maxgood, s_k0, s_last;
+
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int h = tid / kGL, gl = tid % kGL, gsh = (lane / kGL) * kGL;
+    const int64_t off = offs[p];
+    const int n = (int)(offs[p + 1] - off);
+    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
+    const double thresh = threshold / ((fx + fy) / 2);
+    const float tf = (float)(thresh * thresh);
+    // largest double that rounds to a float <= tf (round to nearest even)
+    const float tfu = nextafterf(tf, INFINITY);
+    const double mid = 0.5 * ((double)tf + (double)tfu);
+    const double Tmax = ((__float_as_uint(tf) & 1u) == 0u) ? mid : nextafter(mid, 0.0);
+    const double tlo = Tmax * (1.0 - 0x1p-40), thi = Tmax * (1.0 + 0x1p-40);
+    double* q = qn + off * 4;
+    for (int i = tid; i < n; i += kRThreads) {
+        q[4 * i + 0] = (pts0[2 * (off + i)] - cx) / fx;
+        q[4 * i + 1] = (pts0[2 * (off + i) + 1] - cy) / fy;
+        q[4 * i + 2] = (pts1[2 * (off + i)] - cx) / fx;
+        q[4 * i + 3] = (pts1[2 * (off + i) + 1] - cy) / fy;
+        mask[off + i] = 0;
+    }
+    if (tid == 0) {
+        s_niters = max(max_iters, 1);
+        s_maxgood = 0;
+        s_k0 = 0;
+        s_last = -1;
+    }
+    __syncthreads();
+    double* Eo = E_out + (int64_t)p * kMaxModels * 9;
+    if (n < 5) {
+        if (tid == 0) { nmodels_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
+        return;
+    }
+    if (n == 5) {  // count == modelPoints: one kernel call on all points, mask all ones
+        if (h == 0) {
+            double qq[5][4];
+#pragma unroll
+            for (int j = 0; j < 5; ++j)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) qq[j][c] = q[4 * j + c];
+            const int nm = five_point_group(qq, gl, gsh, s_grp, s_models);
+            if (gl == 0) {
+                for (int e = 0; e < nm * 9; ++e) Eo[e] = s_models[e];
+                nmodels_out[p] = nm;
+                ninl_out[p] = nm > 0 ? 5 : 0;
+                iters_out[p] = 1;
+                for (int i = 0; i < 5; ++i) mask[off + i] = nm > 0 ? 1 : 0;
+            }
+        }
+        return;
+    }
+    CvRng rng{~0ULL};
+    const double inv_n = 1.0 / (double)n;
+    RPROF_INIT;
+    for (;;) {
+        const int k0 = s_k0, niters = s_niters;
+        if (tid == 0) {
+            const int nh = min(kRH, niters - k0);
+            for (int hh = 0; hh < nh; ++hh)
+                for (int i = 0; i < 5; ++i) {
+                    int idx;
+                    for (;;) {
+                        idx = rng.uniform0((unsigned)n, inv_n);
+                        int j = 0;
+                        while (j < i && s_sub[hh * 5 + j] != idx) ++j;
+                        if (j == i) break;
+                    }
+                    s_sub[hh * 5 + i] = idx;
+                }
+        }
+        for (int i = tid; i < kRH * kMaxModels; i += kRThreads) s_cnt[i] = 0;
+        __syncthreads();
+        RPROF(0, tp);
+        {
+            int nm = 0;
+            if (k0 + h < niters) {
+                double qq[5][4];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const int idx = s_sub[h * 5 + j];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) qq[j][c] = q[4 * idx + c];
+                }
+                nm = five_point_group(qq, gl, gsh, s_grp + h * kGS, s_models + h * kMaxModels * 9);
+            }
+            if (gl == 0) s_nmod[h] = nm;
+        }
+        __syncthreads();
+        RPROF(1, tp);
+        for (int b0 = 0; b0 < n; b0 += kRThreads * kPB) {
+            double pt[kPB][4];
+            bool val[kPB];
+#pragma unroll
+            for (int u = 0; u < kPB; ++u) {
+                const int i = b0 + u * kRThreads + tid;
+                val[u] = i < n;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) pt[u][c] = val[u] ? q[4 * i + c] : 0.0;
+            }
+            for (int hh = 0; hh < kRH; ++hh) {
+                const int nm = s_nmod[hh];
+                for (int m = 0; m < nm; ++m) {
+                    const double* Em = s_models + (hh * kMaxModels + m) * 9;
+                    double Er[9];
+#pragma unroll
+                    for (int e = 0; e < 9; ++e) Er[e] = Em[e];
+                    int cnt = 0;  // wave-uniform: ballots + scalar popcounts
+#pragma unroll
+                    for (int u = 0; u < kPB; ++u)
+                        cnt += wave_count(val[u] && sampson_in(Er, pt[u][0], pt[u][1], pt[u][2], pt[u][3], tf, tlo, thi));
+                    if (lane == 0 && cnt) atomicAdd(&s_cnt[hh * kMaxModels + m], cnt);
+                }
+            }
+        }
+        __syncthreads();
+        RPROF(2, tp);
+        if (tid == 0) {
+            int nit = niters, maxgood = s_maxgood, last = s_last;
+            for (int hh = 0; hh < kRH; ++hh) {
+                const int k = k0 + hh;
+                if (k >= nit) break;
+                for (int m = 0; m < s_nmod[hh]; ++m) {
+                    const int good = s_cnt[hh * kMaxModels + m];
+                    if (good > max(maxgood, 4)) {
+                        for (int e = 0; e < 9; ++e) s_best[e] = s_models[(hh * kMaxModels + m) * 9 + e];
+                        maxgood = good;
+                        nit = update_num_iters(prob, (double)(n - good) / n, 5, nit);
+                    }
+                }
+                last = k;
+            }
+            s_niters = nit;
+            s_maxgood = maxgood;
+            s_last = last;
+            s_k0 = k0 + kRH;
+        }
+        __syncthreads();
+        if (s_k0 >= s_niters) break;
+    }
+    const int maxgood = s_maxgood;
+    if (tid == 0) {
+        nmodels_out[p] = maxgood > 0 ? 1 : 0;
+        ninl_out[p] = maxgood;
+        iters_out[p] = s_last + 1;
+        if (maxgood > 0)
+            for (int e = 0; e < 9; ++e) Eo[e] = s_best[e];
+    }
+    if (maxgood > 0)
+        for (int i = tid; i < n; i += kRThreads)
+            mask[off + i] = sampson(s_best, q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]) <= tf ? 1 : 0;
+}
+
+// cv::decomposeEssentialMat: SVD by one-sided Jacobi on E's columns, U's third
+// column = u1 x u2 (det U = +1); Vt negated when det(Vt) < 0.
+__device__ void decompose_essential(const double* E, double* R1, double* R2, double* t) {
+    double A[3][3], V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};  // A[col][row], V[col][row]
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) A[c][r] = E[3 * r + c];
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        bool rotated = false;
+        for (int pc = 0; pc < 2; ++pc)
+            for (int qc = pc + 1; qc < 3; ++qc) {
+                double al = 0, be = 0, ga = 0;
+                for (int r = 0; r < 3; ++r) {
+                    al += A[pc][r] * A[pc][r];
+                    be += A[qc][r] * A[qc][r];
+                    ga += A[pc][r] * A[qc][r];
+                }
+                if (ga == 0.0 || fabs(ga) <= 1e-15 * sqrt(al * be)) continue;
+                rotated = true;
+                const double zeta = (be - al) / (2.0 * ga);
+                const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + tt * tt), s = c * tt;
+                for (int r = 0; r < 3; ++r) {
+                    const double ap = A[pc][r], aq = A[qc][r];
+                    A[pc][r] = c * ap - s * aq;
+                    A[qc][r] = s * ap + c * aq;
+                    const double vp = V[pc][r], vq = V[qc][r];
+                    V[pc][r] = c * vp - s * vq;
+                    V[qc][r] = s * vp + c * vq;
+                }
+            }
+        if (!rotated) break;
+    }
+    double sg[3];
+    int ord[3] = {0, 1, 2};
+    for (int c = 0; c < 3; ++c) sg[c] = sqrt(A[c][0] * A[c][0] + A[c][1] * A[c][1] + A[c][2] * A[c][2]);
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2 - i; ++j)
+            if (sg[ord[j]] < sg[ord[j + 1]]) { const int t2 = ord[j]; ord[j] = ord[j + 1]; ord[j + 1] = t2; }
+    double U[3][3], Vs[3][3];  // [col][row]
+    for (int c = 0; c < 2; ++c)
+        for (int r = 0; r < 3; ++r) U[c][r] = A[ord[c]][r] / sg[ord[c]];
+    U[2][0] = U[0][1] * U[1][2] - U[0][2] * U[1][1];
+    U[2][1] = U[0][2] * U[1][0] - U[0][0] * U[1][2];
+    U[2][2] = U[0][0] * U[1][1] - U[0][1] * U[1][0];
+    const double un = sqrt(U[2][0] * U[2][0] + U[2][1] * U[2][1] + U[2][2] * U[2][2]);
+    for (int r = 0; r < 3; ++r) U[2][r] /= un;
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) Vs[c][r] = V[ord[c]][r];
+    const double detV = Vs[0][0] * (Vs[1][1] * Vs[2][2] - Vs[1][2] * Vs[2][1]) -
+                        Vs[1][0] * (Vs[0][1] * Vs[2][2] - Vs[0][2] * Vs[2][1]) +
+                        Vs[2][0] * (Vs[0][1] * Vs[1][2] - Vs[0][2] * Vs[1][1]);
+    if (detV < 0)
+        for (int c = 0; c < 3; ++c)
+            for (int r = 0; r < 3; ++r) Vs[c][r] = -Vs[c][r];
+    // R1 = U W Vt, R2 = U W^T Vt with W = [[0,1,0],[-1,0,0],[0,0,1]]:
+    // U W = [-u2, u1, u3], U W^T = [u2, -u1, u3]; (X Vt)[r][c] = sum_k X[k][r] * V[k][c]
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            R1[3 * r + c] = (-U[1][r] * Vs[0][c] + U[0][r] * Vs[1][c]) + U[2][r] * Vs[2][c];
+            R2[3 * r + c] = (U[1][r] * Vs[0][c] - U[0][r] * Vs[1][c]) + U[2][r] * Vs[2][c];
+        }
+    for (int r = 0; r < 3; ++r) t[r] = U[2][r];
+}
+
+// cv::recoverPose (distanceThresh variant): cheirality of the DLT
+// triangulation for the 4 candidate poses; best count wins, ties in the
+// order (R1,t), (R2,t), (R1,-t), (R2,-t).
+__global__ __launch_bounds__(kPThreads) void recover_pose_kernel(
+    const double* __restrict__ Ein, int64_t e_stride, const double* __restrict__ pts0,
+    const double* __restrict__ pts1, const int64_t* __restrict__ offs, const double* __restrict__ cam,
+    const uint8_t* __restrict__ mask_in, double dist, double* __restrict__ R_out, double* __restrict__ t_out,
+    uint8_t* __restrict__ mask_out, int32_t* __restrict__ good_out) {
+    __shared__ double sP[4][12];
+    __shared__ int s_cnt[4];
+    __shared__ int s_sel;
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int64_t off = offs[p];
+    const int n = (int)(offs[p + 1] - off);
+    if (tid == 0) {
+        double R1[9], R2[9], t[3];
+        decompose_essential(Ein + (int64_t)p * e_stride, R1, R2, t);
+        for (int k = 0; k < 4; ++k) {
+            const double* R = (k & 1) ? R2 : R1;
+            const double sg = (k & 2) ? -1.0 : 1.0;
+            for (int r = 0; r < 3; ++r) {
+                for (int c = 0; c < 3; ++c) sP[k][4 * r + c] = R[3 * r + c];
+                sP[k][4 * r + 3] = sg * t[r];
+            }
+            s_cnt[k] = 0;
+        }
+    }
+    __syncthreads();
+    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
+    const double P0[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    for (int i0 = 0; i0 < n; i0 += kPThreads) {
+        const int i = i0 + tid;
+        int code = 0;
+        if (i < n && (!mask_in || mask_in[off + i])) {
+            const double x1 = (pts0[2 * (off + i)] - cx) / fx, y1 = (pts0[2 * (off + i) + 1] - cy) / fy;
+            const double x2 = (pts1[2 * (off + i)] - cx) / fx, y2 = (pts1[2 * (off + i) + 1] - cy) / fy;
+            for (int k = 0; k < 4; ++k) {
+                double Q[4];
+                dlt_point(P0, sP[k], x1, y1, x2, y2, Q);
+                bool ok = Q[2] * Q[3] > 0;
+                const double X = Q[0] / Q[3], Y = Q[1] / Q[3], Z = Q[2] / Q[3], W = Q[3] / Q[3];
+                ok = ok && Z < dist;
+                const double* P = sP[k];
+                const double z2 = ((P[8] * X + P[9] * Y) + P[10] * Z) + P[11] * W;
+                ok = ok && z2 > 0 && z2 < dist;
+                code |= ok ? (1 << k) : 0;
+            }
+        }
+        for (int k = 0; k < 4; ++k) {
+            const int c = wave_count((code >> k) & 1);
+            if (lane == 0 && c) atomicAdd(&s_cnt[k], c);
+        }
+        if (i < n) mask_out[off + i] = (uint8_t)code;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int sel = 3;
+        for (int k = 0; k < 4; ++k) {
+            bool best = true;
+            for (int o = 0; o < 4; ++o) best = best && s_cnt[k] >= s_cnt[o];
+            if (best) { sel = k; break; }
+        }
+        s_sel = sel;
+        good_out[p] = s_cnt[sel];
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) R_out[9 * p + 3 * r + c] = sP[sel][4 * r + c];
+            t_out[3 * p + r] = sP[sel][4 * r + 3];
+        }
+    }
+    __syncthreads();
+    const int sel = s_sel;
+    for (int i = tid; i < n; i += kPThreads) mask_out[off + i] = ((mask_out[off + i] >> sel) & 1) ? 255 : 0;
+}
+
+}  // namespace
+}  // namespace sfmhip
+
+using namespace sfmhip;
+
+extern "C" int sfmhip_debug_ransac_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rprof), sizeof(unsigned long long) * 16) != hipSuccess) return -2;
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), z, sizeof(z)) != hipSuccess) return -2;
+    return 0;
+}
+
+extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, const int64_t* offsets,
+                                     int n_pairs, const double* cam, double prob, double threshold,
+                                     int max_iters, double* work, double* E, int32_t* n_models,
+                                     uint8_t* mask, int32_t* n_inliers, int32_t* iters, void* stream) {
+    SFMHIP_REQUIRE(n_pairs >= 0, "find_essential: n_pairs < 0");
+    if (n_pairs == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(pts0 && pts1 && offsets && cam && work && E && n_models && mask && n_inliers && iters,
+                   "find_essential: null pointer");
+    SFMHIP_REQUIRE(prob >= 0 && prob <= 1 && threshold > 0, "find_essential: prob in [0,1], threshold > 0");
+    hipLaunchKernelGGL(essential_ransac_kernel, dim3(n_pairs), dim3(kRThreads), 0, as_stream(stream), pts0, pts1,
+                       offsets, cam, prob, threshold, max_iters, work, E, n_models, mask, n_inliers, iters);
+    return check_launch("essential_ransac_kernel");
+}
+
+extern "C" int sfmhip_recover_pose(const double* E, int64_t e_stride, const double* pts0, const double* pts1,
+                                   const int64_t* offsets, int n_pairs, const double* cam, const uint8_t* mask_in,
+                                   double distance_thresh, double* R, double* t, uint8_t* mask_out,
+                                   int32_t* n_good, void* stream) {
+    SFMHIP_REQUIRE(n_pairs >= 0, "recover_pose: n_pairs < 0");
+    if (n_pairs == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(E && pts0 && pts1 && offsets && cam && R && t && mask_out && n_good,
+                   "recover_pose: null pointer");
+    SFMHIP_REQUIRE(e_stride >= 9, "recover_pose: e_stride >= 9");
+    hipLaunchKernelGGL(recover_pose_kernel, dim3(n_pairs), dim3(kPThreads), 0, as_stream(stream), E, e_stride,
+                       pts0, pts1, offsets, cam, mask_in, distance_thresh, R, t, mask_out, n_good);
+    return check_launch("recover_pose_kernel");
+}

@@ -128,6 +128,36 @@ def ba_scene(n_pairs=256, n_obs=4096, seed=4, noise_px=0.5):
     return dict(P=P, x0=x0, x1=x1, cam=cam, K=Kb, X=Xinit, pts2d=x1.T.copy(), pair_of_obs=pair_of_obs)
 
 
+def two_view_pairs(n_pairs=256, n_pts=2048, outlier_frac=0.3, noise_px=0.5, seed=6, step=1):
+    """Matched keypoints for pairs (i, i+step) of an orbit, in the reference's
+    centred pixel convention (K = diag(f, f, 1), matching.py:133): pts0/pts1
+    lists of (n, 2) f32 (like m_kpts0/1, matching.py:126-127), a fraction
+    ``outlier_frac`` replaced by random image points; also the true R, t
+    (camera i -> camera i+step) and the inlier flags.  ``n_pts`` may be a
+    per-pair sequence."""
+    rng = np.random.default_rng(seed)
+    Rs, ts = orbit_cameras(n_pairs + step, seed=seed)
+    K = np.array([[FOCAL, 0, 0], [0, FOCAL, 0], [0, 0, 1.0]])
+    sizes = np.broadcast_to(np.asarray(n_pts), (n_pairs,))
+    out = dict(pts0=[], pts1=[], R=[], t=[], inlier=[], K=K)
+    for p in range(n_pairs):
+        n = int(sizes[p])
+        X = rng.uniform(-1, 1, (n, 3))
+        uv = []
+        for c in (p, p + step):
+            Xc = X @ Rs[c].T + ts[c]
+            uv.append(Xc[:, :2] / Xc[:, 2:] * FOCAL + rng.normal(0, noise_px, (n, 2)))
+        bad = rng.random(n) < outlier_frac
+        uv[1][bad] = rng.uniform([-IMG_W / 2, -IMG_H / 2], [IMG_W / 2, IMG_H / 2], (int(bad.sum()), 2))
+        out["pts0"].append(uv[0].astype(np.float32))
+        out["pts1"].append(uv[1].astype(np.float32))
+        R = Rs[p + step] @ Rs[p].T
+        out["R"].append(R)
+        out["t"].append(ts[p + step] - R @ ts[p])
+        out["inlier"].append(~bad)
+    return out
+
+
 # ---------------------------------------------------------------------------
 SPHERES = ((0.0, -0.2, 0.0, 0.45), (0.5, 0.1, 0.3, 0.25), (-0.45, 0.0, -0.35, 0.3))
 FLOOR_Y = -0.6

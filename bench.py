@@ -236,6 +236,52 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
     return out
 
 
+def verify_line(sfm, syn, device, args, barrier, cpu=True):
+    """§8f row 2: findEssentialMat (RANSAC, prob 0.999, 1 px) + recoverPose for
+    256 BFS-candidate pairs x 2048 matches (30 % outliers, 0.5 px noise), one
+    batched launch each; CPU baseline = the oracle restatement on 2 pairs."""
+    v = sfm.verify
+    s = syn.two_view_pairs(256, 2048, outlier_frac=0.3, noise_px=0.5, seed=6)
+    a, b, of = v.pack_pairs(s["pts0"], s["pts1"])
+    cam = torch.tensor(v._cam(s["K"]), dtype=torch.float64, device=device).expand(256, 4).contiguous()
+    holder = {}
+
+    def step(record):
+        e0 = e1 = None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        r = v.find_essential_batched(a, b, of, cam)
+        holder["rp"] = v.recover_pose_batched(r["E"], a, b, of, cam, mask=r["mask"])
+        holder["r"] = r
+        if record:
+            e1.record()
+        return (e0, e1)
+
+    wall, kms = timed(step, args.steps, 1, barrier)
+    ms = wall / args.steps * 1e3
+    iters = holder["r"]["iters"].float().mean().item()
+    line = {"metric": "geometric verification pairs/sec", "value": 256 / (ms * 1e-3), "unit": "pairs/s",
+            "ms_per_step": ms,
+            "config": {"workload": "findEssentialMat(RANSAC, 0.999, 1px) + recoverPose: 256 pairs x 2048 matches, "
+                                   "30% outliers, 0.5 px noise (matching.py:134-139 / sfm.py:108-119)",
+                       "mean_ransac_iters": iters},
+            "roofline": {"bound": "fp64", "kernel": "essential_ransac_kernel+recover_pose_kernel",
+                         "kernel_ms": float(np.mean(kms))}}
+    if cpu:
+        from oracle import ransac as orc
+        t0 = time.perf_counter()
+        for p in range(2):
+            E, m = orc.find_essential_mat(s["pts0"][p], s["pts1"][p], s["K"])
+            keep = m.ravel() > 0
+            orc.recover_pose(E, s["pts0"][p][keep], s["pts1"][p][keep], s["K"])
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": 2 / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+                                "sample": f"2 of the 256 pairs through oracle.ransac (numpy restatement of "
+                                          f"OpenCV's findEssentialMat + recoverPose), {dt:.2f}s"}
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -428,6 +474,7 @@ def main():
     if not args.skip_secondary and world == 1:
         result["secondary"].extend(voxel_and_vq_lines(sfm, syn, device, args, barrier,
                                                       cpu=(not args.no_cpu_baseline)))
+        result["secondary"].append(verify_line(sfm, syn, device, args, barrier, cpu=(not args.no_cpu_baseline)))
 
     # ---------------- CPU baseline (rank 0, N=1 only) ------------------------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

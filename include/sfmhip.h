@@ -176,6 +176,34 @@ int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, int z0, int 
                           const float* bmin, const float* bmax, float trunc,
                           void* stream);
 
+/* ---- §8f row 2: geometric verification (batched over image pairs) --------
+ * cv2.findEssentialMat(pts0, pts1, K, method=cv2.RANSAC, prob=0.999,
+ * threshold=1) at matching.py:134 and sfm.py:108 (OpenCV five-point.cpp +
+ * ptsetreg.cpp, maxIters 1000 by default): cv::RNG(-1) 5-point samples,
+ * Nister solver, Sampson error (float) <= (thresh/((fx+fy)/2))^2, a model
+ * replaces the best iff count > max(best, 4), RANSACUpdateNumIters.
+ * Pair p owns rows [offsets[p], offsets[p+1]) of pts0/pts1 ([N][2] f64
+ * pixels); cam [n_pairs][4] = fx, fy, cx, cy.  work [N][4] f64 scratch.
+ * Out: E [n_pairs][10][9] (row-major; model 0 is the RANSAC result, all
+ * models only when a pair has exactly 5 points), n_models (0 = no model,
+ * cv2 returns None), mask [N] u8 0/1, n_inliers, iters (hypotheses drawn).
+ * All pointers are device memory.                                            */
+int sfmhip_find_essential(const double* pts0, const double* pts1, const int64_t* offsets,
+                          int n_pairs, const double* cam, double prob, double threshold,
+                          int max_iters, double* work, double* E, int32_t* n_models,
+                          uint8_t* mask, int32_t* n_inliers, int32_t* iters, void* stream);
+
+/* cv2.recoverPose(E, pts0, pts1, K) at matching.py:139, sfm.py:117,119
+ * (distanceThresh = 50): decomposeEssentialMat + DLT cheirality of the 4
+ * candidate poses.  E for pair p at E + p*e_stride (e_stride >= 9, 90 for
+ * sfmhip_find_essential's output); mask_in [N] u8 or NULL (rows with 0 are
+ * excluded, == recoverPose on the compacted points).  Out: R [n_pairs][9],
+ * t [n_pairs][3], mask_out [N] u8 0/255, n_good [n_pairs].                   */
+int sfmhip_recover_pose(const double* E, int64_t e_stride, const double* pts0, const double* pts1,
+                        const int64_t* offsets, int n_pairs, const double* cam,
+                        const uint8_t* mask_in, double distance_thresh, double* R, double* t,
+                        uint8_t* mask_out, int32_t* n_good, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
