@@ -532,6 +532,250 @@ static int env_int(const char* name, int dflt) {
     return e ? std::atoi(e) : dflt;
 }
 
+// ---------------------------------------------------------------------------
+// §8f row 4: one training step of the grid (plenoxel.py:100-111, sdf.py:427-438):
+// fused render forward + mse gradient + analytic backward + trilinear scatter
+// (ATen grid_sampler_3d backward) into a voxel-major gradient, then Adam.
+// One wave per ray, one lane per sample, up to kTrainChunks x 64 samples kept
+// in registers between the forward and the reverse (suffix) pass.
+constexpr int kTrainChunks = 4;
+
+// coefficient of k[ch*9 + m] in eval_spherical_function (oracle/train.py sh_basis)
+__device__ __forceinline__ void sh_basis(float x, float y, float z, float* b) {
+    const float C0 = 0.282095f, C1 = 0.488603f, C2 = 1.092548f, C3 = 0.315392f, C4 = 0.546274f;
+    b[0] = C0;
+    b[1] = (-C1) * y;
+    b[2] = C1 * z;
+    b[3] = -(C1 * x);
+    b[4] = (C2 * x) * y;
+    b[5] = -((C2 * y) * z);
+    b[6] = C3 * (((2.0f * z) * z - x * x) - y * y);
+    b[7] = ((-C2) * x) * z;
+    b[8] = C4 * (x * x - y * y);
+}
+
+__global__ __launch_bounds__(256) void render_train_kernel(
+    const float* __restrict__ gvm, int D, int H, int W, Bounds B, int mode, const float* __restrict__ ro,
+    const float* __restrict__ rd, const float* __restrict__ zv, const float* __restrict__ gt, int64_t nrays, int S,
+    float gscale, float* __restrict__ rgb, float* __restrict__ sqerr, float* __restrict__ grad) {
+    // per-wave LDS staging of the scatter: sample -> (28 channel grads, 8 corners)
+    __shared__ float s_dt[4][64 * 29];
+    __shared__ int s_cv[4][64 * 8];
+    __shared__ float s_cw[4][64 * 8];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (ray >= nrays) return;  // wave-uniform
+    const float o[3] = {ro[3 * ray], ro[3 * ray + 1], ro[3 * ray + 2]};
+    const float d[3] = {rd[3 * ray], rd[3 * ray + 1], rd[3 * ray + 2]};
+    const float* z = zv + (size_t)ray * S;
+    float* dt = s_dt[wv];
+    int* cvx = s_cv[wv];
+    float* cwt = s_cw[wv];
+    float sA[kTrainChunks], sE[kTrainChunks], sDel[kTrainChunks], sT[kTrainChunks], sC[kTrainChunks][3];
+    bool sRelu[kTrainChunks];
+    float carry = 1.f;
+    float cr = 0.f, cg = 0.f, cb = 0.f, ws = 0.f;
+#pragma unroll
+    for (int c = 0; c < kTrainChunks; ++c) {
+        sA[c] = 0.f; sE[c] = 1.f; sDel[c] = 0.f; sT[c] = 0.f; sC[c][0] = sC[c][1] = sC[c][2] = 0.f; sRelu[c] = false;
+        if (c * 64 >= S) continue;  // wave-uniform
+        const int s = c * 64 + lane;
+        float alpha = 0.f;
+        if (s < S) {
+            const float zs = z[s];
+            const float p[3] = {o[0] + d[0] * zs, o[1] + d[1] * zs, o[2] + d[2] * zs};
+            float g[3], sdf = 0.f, k[27];
+#pragma unroll
+            for (int q = 0; q < 27; ++q) k[q] = 0.f;
+            if (normalise(p, B, mode, g)) {
+                Corners cn;
+                corners(g, D, H, W, cn);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    int x, y, zz;
+                    if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
+                    const float w = cn.w[q];
+                    const float4* v = reinterpret_cast<const float4*>(gvm + ((((size_t)zz * H + y) * W + x) << 5));
+                    float vv[28];
+#pragma unroll
+                    for (int t = 0; t < 7; ++t) {
+                        const float4 f = v[t];
+                        vv[4 * t] = f.x; vv[4 * t + 1] = f.y; vv[4 * t + 2] = f.z; vv[4 * t + 3] = f.w;
+                    }
+                    sdf = sdf + vv[0] * w;
+#pragma unroll
+                    for (int q2 = 0; q2 < 27; ++q2) k[q2] = k[q2] + vv[1 + q2] * w;
+                }
+            }
+            sh_colour(k, d[0], d[1], d[2], sC[c]);
+            const float sigma = fmaxf(sdf, 0.f);
+            sRelu[c] = sdf > 0.f;
+            sDel[c] = (s + 1 < S) ? (z[s + 1] - zs) : 1e10f;
+            sE[c] = expf((-sigma) * sDel[c]);
+            alpha = 1.f - sE[c];
+        }
+        sA[c] = alpha;
+        float incl = 1.f - alpha;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const float up = __shfl_up(incl, off, 64);
+            if (lane >= off) incl = incl * up;
+        }
+        float excl = __shfl_up(incl, 1, 64);
+        if (lane == 0) excl = 1.f;
+        sT[c] = carry * excl;
+        const float w = sT[c] * alpha;
+        float pr = w * sC[c][0], pg = w * sC[c][1], pb = w * sC[c][2], pw = w;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            pr += __shfl_xor(pr, off, 64);
+            pg += __shfl_xor(pg, off, 64);
+            pb += __shfl_xor(pb, off, 64);
+            pw += __shfl_xor(pw, off, 64);
+        }
+        cr += pr; cg += pg; cb += pb; ws += pw;
+        carry = carry * __shfl(incl, 63, 64);
+    }
+    const float out[3] = {(cr + 1.f) - ws, (cg + 1.f) - ws, (cb + 1.f) - ws};
+    float gch[3], se = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const float df = out[ch] - gt[3 * ray + ch];
+        se += df * df;
+        gch[ch] = gscale * df;  // d mse / d rgb
+    }
+    if (lane == 0) {
+        rgb[3 * ray] = out[0]; rgb[3 * ray + 1] = out[1]; rgb[3 * ray + 2] = out[2];
+        sqerr[ray] = se;
+    }
+    float bas[9];
+    sh_basis(d[0], d[1], d[2], bas);
+    float vcarry = 0.f;  // V after the last sample
+#pragma unroll
+    for (int c = kTrainChunks - 1; c >= 0; --c) {
+        if (c * 64 >= S) continue;  // wave-uniform
+        const int s = c * 64 + lane;
+        const bool live = s < S;
+        const float e = live ? ((gch[0] * (sC[c][0] - 1.f) + gch[1] * (sC[c][1] - 1.f)) + gch[2] * (sC[c][2] - 1.f))
+                             : 0.f;
+        // f_k(V) = a_k e_k + (1 - a_k) V ; suffix composition F_k = f_k o ... o f_63
+        float fa = live ? 1.f - sA[c] : 1.f, fb = live ? sA[c] * e : 0.f;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const float na = __shfl_down(fa, off, 64), nb = __shfl_down(fb, off, 64);
+            if (lane + off < 64) { fb = fb + fa * nb; fa = fa * na; }
+        }
+        float nxa = __shfl_down(fa, 1, 64), nxb = __shfl_down(fb, 1, 64);
+        if (lane == 63) { nxa = 1.f; nxb = 0.f; }
+        const float V = nxb + nxa * vcarry;
+        vcarry = __shfl(fb, 0, 64) + __shfl(fa, 0, 64) * vcarry;
+        bool has = false;
+        if (live) {
+            const float zs = z[s];
+            const float p[3] = {o[0] + d[0] * zs, o[1] + d[1] * zs, o[2] + d[2] * zs};
+            float g[3];
+            if (normalise(p, B, mode, g)) {
+                has = true;
+                const float dalpha = sT[c] * (e - V);
+                const float dsig = (dalpha * sE[c]) * sDel[c];
+                dt[lane * 29] = sRelu[c] ? dsig : 0.f;
+                const float w = sT[c] * sA[c];
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    const float dc = w * gch[ch];
+#pragma unroll
+                    for (int m = 0; m < 9; ++m) dt[lane * 29 + 1 + 9 * ch + m] = dc * bas[m];
+                }
+                Corners cn;
+                corners(g, D, H, W, cn);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    int x, y, zz;
+                    cvx[lane * 8 + q] = corner_in(cn, q, D, H, W, x, y, zz) ? (zz * H + y) * W + x : -1;
+                    cwt[lane * 8 + q] = cn.w[q];
+                }
+            }
+        }
+        if (!has)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cvx[lane * 8 + q] = -1;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        // scatter: each wave-instruction adds the 28 channels of two (sample, corner)
+        // pairs, lanes 0..27 and 32..59 -> two contiguous 112-B runs (full-rate
+        // atomics; one voxel per lane would be ~17x slower, MI355X_MICROARCH.md)
+        const unsigned long long any = __ballot(has);
+        if (any) {
+            const int ch = lane & 31, half = lane >> 5;
+            const int first = __ffsll((long long)any) - 1, last = 63 - __clzll((long long)any);
+            for (int pr = first * 4; pr < (last + 1) * 4; ++pr) {
+                const int idx = 2 * pr + half, smp = idx >> 3;
+                const int vox = cvx[idx];
+                if (ch < 28 && vox >= 0)
+                    unsafeAtomicAdd(grad + ((size_t)vox << 5) + ch, cwt[idx] * dt[smp * 29 + ch]);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+}
+
+// torch.optim.Adam single-tensor step (torch/optim/adam.py, CPU kernels):
+//   m = fma(1-b1, g - m, m)            (vectorised lerp_)
+//   v = fma((1-b2) * g, g, v * b2)      (vectorised addcmul_)
+//   p = p + (step * m) / (sqrt(v) / bc2s + eps)   (addcdiv_, step = -lr / (1 - b1^t))
+// and zero_grad: g = 0.  float4 streams: 32 algorithmic bytes per parameter.
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4f adam4(v4f pp, v4f gg, v4f& mm, v4f& vv, float w1, float b2, float s2, float bc2s,
+                                     float eps, float step) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        mm[j] = fmaf(w1, gg[j] - mm[j], mm[j]);
+        vv[j] = fmaf(s2 * gg[j], gg[j], vv[j] * b2);
+        const float den = sqrtf(vv[j]) / bc2s + eps;
+        pp[j] = pp[j] + (step * mm[j]) / den;
+    }
+    return pp;
+}
+
+// Streams are touched once per step: non-temporal loads/stores, two float4
+// per thread per iteration (8 loads in flight) over a grid-stride loop.
+__global__ __launch_bounds__(256) void adam_kernel(v4f* __restrict__ p, v4f* __restrict__ g, v4f* __restrict__ m,
+                                                   v4f* __restrict__ v, int64_t n4, float w1, float b2, float s2,
+                                                   float bc2s, float eps, float step, int zero_grad) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const v4f z4 = {0.f, 0.f, 0.f, 0.f};
+    for (; i + stride < n4; i += 2 * stride) {
+        const int64_t j = i + stride;
+        const v4f g0 = __builtin_nontemporal_load(g + i), g1 = __builtin_nontemporal_load(g + j);
+        v4f m0 = __builtin_nontemporal_load(m + i), m1 = __builtin_nontemporal_load(m + j);
+        v4f v0 = __builtin_nontemporal_load(v + i), v1 = __builtin_nontemporal_load(v + j);
+        const v4f p0 = __builtin_nontemporal_load(p + i), p1 = __builtin_nontemporal_load(p + j);
+        const v4f q0 = adam4(p0, g0, m0, v0, w1, b2, s2, bc2s, eps, step);
+        const v4f q1 = adam4(p1, g1, m1, v1, w1, b2, s2, bc2s, eps, step);
+        __builtin_nontemporal_store(m0, m + i); __builtin_nontemporal_store(m1, m + j);
+        __builtin_nontemporal_store(v0, v + i); __builtin_nontemporal_store(v1, v + j);
+        __builtin_nontemporal_store(q0, p + i); __builtin_nontemporal_store(q1, p + j);
+        if (zero_grad) { __builtin_nontemporal_store(z4, g + i); __builtin_nontemporal_store(z4, g + j); }
+    }
+    for (; i < n4; i += stride) {
+        v4f m0 = m[i], v0 = v[i];
+        p[i] = adam4(p[i], g[i], m0, v0, w1, b2, s2, bc2s, eps, step);
+        m[i] = m0;
+        v[i] = v0;
+        if (zero_grad) g[i] = z4;
+    }
+}
+
+// (D,H,W,32) -> (C,D,H,W): the parameter export of the trainer.
+__global__ void from_vm_kernel(const float* __restrict__ vm, int C, int64_t nvox, float* __restrict__ grid) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nvox * C) return;
+    const int c = (int)(e / nvox);
+    const int64_t vx = e - (int64_t)c * nvox;
+    grid[e] = vm[(vx << 5) + c];
+}
+
 }  // namespace sfmhip
 
 using namespace sfmhip;
@@ -689,4 +933,50 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
         if (rc != SFMHIP_OK) return rc;
     }
     return SFMHIP_OK;
+}
+
+extern "C" int sfmhip_grid_from_voxel_major(const float* grid_vm, int C, int D, int H, int W, float* grid,
+                                            void* stream) {
+    SFMHIP_REQUIRE(grid && grid_vm, "sfmhip_grid_from_voxel_major: null pointer");
+    SFMHIP_REQUIRE(C > 0 && C <= 32 && D > 0 && H > 0 && W > 0, "sfmhip_grid_from_voxel_major: bad shape");
+    const int64_t nvox = (int64_t)D * H * W;
+    hipLaunchKernelGGL(from_vm_kernel, dim3(ceil_div(nvox * C, 256)), dim3(256), 0, as_stream(stream), grid_vm, C,
+                       nvox, grid);
+    return check_launch("from_vm_kernel");
+}
+
+extern "C" int sfmhip_render_train(const float* grid_vm, int D, int H, int W, const float* bmin, const float* bmax,
+                                   int mask_mode, const float* rays_o, const float* rays_d, const float* z,
+                                   const float* gt, int64_t B, int S, float* rgb, float* sqerr, float* grad_vm,
+                                   void* stream) {
+    SFMHIP_REQUIRE(grid_vm && bmin && bmax && rays_o && rays_d && z && gt && rgb && sqerr && grad_vm,
+                   "sfmhip_render_train: null pointer");
+    SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && B >= 0 && S >= 1, "sfmhip_render_train: bad shape");
+    SFMHIP_REQUIRE(S <= 64 * kTrainChunks, "sfmhip_render_train: S must be <= %d", 64 * kTrainChunks);
+    SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_render_train: mask_mode must be 0 or 1");
+    if (B == 0) return SFMHIP_OK;
+    const float gscale = (float)(2.0 / (3.0 * (double)B));  // mse_loss mean over B x 3
+    hipLaunchKernelGGL(render_train_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, as_stream(stream), grid_vm, D, H,
+                       W, make_bounds(bmin, bmax), mask_mode, rays_o, rays_d, z, gt, B, S, gscale, rgb, sqerr,
+                       grad_vm);
+    return check_launch("render_train_kernel");
+}
+
+extern "C" int sfmhip_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                double lr, double beta1, double beta2, double eps, int64_t step, int zero_grad,
+                                void* stream) {
+    SFMHIP_REQUIRE(param && grad && exp_avg && exp_avg_sq, "sfmhip_adam_step: null pointer");
+    SFMHIP_REQUIRE(n >= 0 && n % 4 == 0, "sfmhip_adam_step: n must be a multiple of 4");
+    SFMHIP_REQUIRE(step >= 1, "sfmhip_adam_step: step counts from 1");
+    if (n == 0) return SFMHIP_OK;
+    // torch computes these in Python floats (double) and casts to the tensor dtype
+    const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, s2 = (float)(1.0 - beta2);
+    const float bc2s = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
+    const float stp = (float)(-lr / (1.0 - std::pow(beta1, (double)step)));
+    const int64_t n4 = n / 4;
+    const int blocks = (int)std::min<int64_t>(ceil_div(n4, 256), env_int("SFMHIP_ADAM_BLOCKS", 32768));
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), reinterpret_cast<v4f*>(param),
+                       reinterpret_cast<v4f*>(grad), reinterpret_cast<v4f*>(exp_avg),
+                       reinterpret_cast<v4f*>(exp_avg_sq), n4, w1, b2, s2, bc2s, (float)eps, stp, zero_grad);
+    return check_launch("adam_kernel");
 }

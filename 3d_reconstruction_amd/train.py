@@ -1,0 +1,97 @@
+"""§8f row 4: the grid training step of the reference, on the GPU.
+
+``GridTrainer.step(rays_o, rays_d, gt, z)`` is one iteration of
+plenoxel.py:100-111 (``train``) / sdf.py:427-438 (``__main__``)::
+
+    rgb = render_rays(model, rays_o, rays_d)     # NerfModel / SDFGrid forward
+    loss = mse_loss(gt, rgb)
+    optimizer.zero_grad(); loss.backward(); optimizer.step()   # Adam(lr=1e-2)
+
+as two launches: ``sfmhip_render_train`` (fused sample + SH colour + composite
+forward, mse gradient, analytic backward, trilinear scatter-add into the
+gradient — ATen grid_sampler_3d's backward weights) and ``sfmhip_adam_step``
+(torch's single-tensor Adam with the gradient reset fused in).  The
+parameters, gradient and Adam moments live in the voxel-major layout
+(D, H, W, 32) the renderer reads; ``grid`` exports the reference's
+(1, 28, D, H, W) tensor.  The sample depths ``z`` are an explicit input (the
+reference draws the jitter with ``torch.rand``).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._abi import call, dev, ptr, require_gpu, stream_ptr
+from .voxel import MASK_PLENOXEL, MASK_SDF, _f3, _host_ptr
+
+
+class GridTrainer:
+    def __init__(self, grid, min_bound, max_bound, mask_mode: int = MASK_SDF, lr: float = 1e-2,
+                 betas=(0.9, 0.999), eps: float = 1e-8):
+        require_gpu()
+        g = grid.detach() if isinstance(grid, torch.Tensor) else torch.as_tensor(grid)
+        if g.dim() == 5:
+            g = g[0]
+        g = dev(g, torch.float32)
+        self.C, self.D, self.H, self.W = (int(s) for s in g.shape)
+        if self.C > 32:
+            raise ValueError("GridTrainer supports C <= 32 channels")
+        self.bmin, self.bmax = _f3(min_bound), _f3(max_bound)
+        self.mask_mode = int(mask_mode)
+        self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
+        self.step_count = 0
+        shape = (self.D, self.H, self.W, 32)
+        self.param = torch.empty(shape, dtype=torch.float32, device=g.device)
+        call("sfmhip_grid_to_voxel_major", ptr(g), self.C, self.D, self.H, self.W, ptr(self.param), stream_ptr())
+        self.grad = torch.zeros(shape, dtype=torch.float32, device=g.device)
+        self.exp_avg = torch.zeros(shape, dtype=torch.float32, device=g.device)
+        self.exp_avg_sq = torch.zeros(shape, dtype=torch.float32, device=g.device)
+
+    @classmethod
+    def plenoxel(cls, voxel_grid, scale: float = 1.5, **kw) -> "GridTrainer":
+        """NerfModel(N, scale) (plenoxel.py:19-43): mask |x| < scale, idx = x / scale."""
+        return cls(voxel_grid, (-scale,) * 3, (scale,) * 3, MASK_PLENOXEL, **kw)
+
+    def _export(self, vm: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((self.C, self.D, self.H, self.W), dtype=torch.float32, device=vm.device)
+        call("sfmhip_grid_from_voxel_major", ptr(vm), self.C, self.D, self.H, self.W, ptr(out), stream_ptr())
+        return out[None]
+
+    @property
+    def grid(self) -> torch.Tensor:
+        """The parameter in the reference layout (1, C, D, H, W)."""
+        return self._export(self.param)
+
+    def state(self) -> dict:
+        return dict(exp_avg=self._export(self.exp_avg), exp_avg_sq=self._export(self.exp_avg_sq),
+                    step=self.step_count)
+
+    def backward(self, rays_o, rays_d, gt, z):
+        """Forward + loss + backward only (accumulates into self.grad).
+        Returns (loss float, rgb (B,3) tensor)."""
+        o = dev(rays_o, torch.float32).reshape(-1, 3)
+        d = dev(rays_d, torch.float32).reshape(-1, 3)
+        zz = dev(z, torch.float32)
+        t = dev(gt, torch.float32).reshape(-1, 3)
+        B, S = zz.shape
+        if o.shape[0] != B or d.shape[0] != B or t.shape[0] != B:
+            raise ValueError("rays_o, rays_d, gt and z must have the same number of rays")
+        rgb = torch.empty((B, 3), dtype=torch.float32, device=o.device)
+        sq = torch.empty(B, dtype=torch.float32, device=o.device)
+        call("sfmhip_render_train", ptr(self.param), self.D, self.H, self.W, _host_ptr(self.bmin),
+             _host_ptr(self.bmax), self.mask_mode, ptr(o), ptr(d), ptr(zz), ptr(t), B, S, ptr(rgb), ptr(sq),
+             ptr(self.grad), stream_ptr())
+        loss = float(sq.double().sum().item()) / (3 * B) if B else float("nan")
+        return loss, rgb
+
+    def optimizer_step(self, zero_grad: bool = True) -> None:
+        self.step_count += 1
+        call("sfmhip_adam_step", ptr(self.param), ptr(self.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
+             self.param.numel(), self.lr, self.betas[0], self.betas[1], self.eps, self.step_count,
+             1 if zero_grad else 0, stream_ptr())
+
+    def step(self, rays_o, rays_d, gt, z) -> float:
+        """One training iteration; returns loss.item()."""
+        loss, _ = self.backward(rays_o, rays_d, gt, z)
+        self.optimizer_step()
+        return loss

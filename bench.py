@@ -282,6 +282,78 @@ def verify_line(sfm, syn, device, args, barrier, cpu=True):
     return line
 
 
+def train_line(sfm, syn, device, args, barrier, cpu=True):
+    """§8f row 4: one plenoxel training step at the reference's config
+    (plenoxel.py:124-133: NerfModel(N=256), batch 2048 rays, 192 bins,
+    hn=2, hf=6): fused render forward+backward (scatter into the gradient)
+    + Adam over all 28 x 256^3 parameters with the gradient reset."""
+    tm = importlib.import_module("3d_reconstruction_amd.train")
+    N, B, S = 256, 2048, 192
+    g = torch.Generator(device=device)
+    g.manual_seed(11)
+    grid = torch.ones((28, N, N, N), device=device) / 100        # NerfModel init (plenoxel.py:29)
+    tr = tm.GridTrainer.plenoxel(grid, 1.5, lr=1e-2)
+    del grid
+    torch.cuda.empty_cache()
+    ro = torch.randn((B, 3), generator=g, device=device) * 0.2 + torch.tensor([0.0, 0.0, -3.0], device=device)
+    rd = torch.randn((B, 3), generator=g, device=device) * 0.2 + torch.tensor([0.0, 0.0, 1.0], device=device)
+    rd = (rd / rd.norm(dim=1, keepdim=True)).contiguous()
+    t = torch.linspace(2.0, 6.0, S, device=device).expand(B, S)
+    mid = (t[:, :-1] + t[:, 1:]) / 2
+    lower = torch.cat([t[:, :1], mid], 1)
+    upper = torch.cat([mid, t[:, -1:]], 1)
+    z = (lower + (upper - lower) * torch.rand((B, S), generator=g, device=device)).contiguous()
+    gt = torch.rand((B, 3), generator=g, device=device)
+    ev = {}
+
+    def step(record):
+        e0 = e1 = e2 = None
+        if record:
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record()
+        tr.backward(ro, rd, gt, z)
+        if record:
+            e1.record()
+        tr.optimizer_step()
+        if record:
+            e2.record()
+            ev.setdefault("a", []).append((e1, e2))
+        return (e0, e2)
+
+    wall, kms = timed(step, args.steps, 1, barrier)
+    ms = wall / args.steps * 1e3
+    adam_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["a"]]))
+    n_par = 28 * N ** 3
+    line = {"metric": "plenoxel training steps/sec", "value": 1e3 / ms, "unit": "steps/s", "ms_per_step": ms,
+            "config": {"workload": "plenoxel.py train step: NerfModel(N=256) 28x256^3, 2048 rays x 192 bins, "
+                                   "mse + backward + Adam(lr=1e-2)"},
+            "roofline": {"bound": "hbm", "kernel": "adam_kernel", "kernel_ms": adam_ms,
+                         "algorithmic_bytes_per_param": 32,
+                         "achieved_gbs": n_par * 32 / (adam_ms * 1e-3) / 1e9, "peak_gbs": PEAK_HBM_GBS,
+                         "frac": n_par * 32 / (adam_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                         "note": "params/grad/moments stored voxel-major with 32-channel lines (4 pad channels)"}}
+    if cpu:
+        from oracle import train as ot
+        Nc, Bc = 64, 64
+        gsmall = np.full((28, Nc, Nc, Nc), 0.01, np.float32)
+        zz = z[:Bc].cpu().numpy()
+        t0 = time.perf_counter()
+        _, _, grad = ot.render_loss_grad(gsmall, (-1.5,) * 3, (1.5,) * 3, 1, ro[:Bc].cpu().numpy(),
+                                         rd[:Bc].cpu().numpy(), zz, gt[:Bc].cpu().numpy())
+        t_r = (time.perf_counter() - t0) / Bc
+        t0 = time.perf_counter()
+        ot.adam_step(gsmall, grad, np.zeros_like(grad), np.zeros_like(grad), 1)
+        t_a = (time.perf_counter() - t0) / gsmall.size
+        est = t_r * B + t_a * n_par
+        line["cpu_baseline"] = {"value": 1.0 / est, "unit": "steps/s", "cores": 1, "kind": "port",
+                                "sample": f"oracle.train on {Bc} rays (render+backward, {t_r * 1e3:.2f} ms/ray) "
+                                          f"and Adam over 28x{Nc}^3 params ({t_a * 1e9:.1f} ns/param), "
+                                          f"extrapolated to 2048 rays + 28x256^3 params = {est:.1f} s/step"}
+    del tr
+    torch.cuda.empty_cache()
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -475,6 +547,7 @@ def main():
         result["secondary"].extend(voxel_and_vq_lines(sfm, syn, device, args, barrier,
                                                       cpu=(not args.no_cpu_baseline)))
         result["secondary"].append(verify_line(sfm, syn, device, args, barrier, cpu=(not args.no_cpu_baseline)))
+        result["secondary"].append(train_line(sfm, syn, device, args, barrier, cpu=(not args.no_cpu_baseline)))
 
     # ---------------- CPU baseline (rank 0, N=1 only) ------------------------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

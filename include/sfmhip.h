@@ -204,6 +204,27 @@ int sfmhip_recover_pose(const double* E, int64_t e_stride, const double* pts0, c
                         const uint8_t* mask_in, double distance_thresh, double* R, double* t,
                         uint8_t* mask_out, int32_t* n_good, void* stream);
 
+/* ---- §8f row 4: one grid training step (plenoxel.py:100-111, sdf.py:427-438)
+ * Fused render forward + mse_loss(gt, rgb) gradient + analytic backward +
+ * trilinear scatter-add into grad_vm (voxel-major (D,H,W,32), accumulated;
+ * zero it via sfmhip_adam_step's zero_grad).  S <= 256.  Out: rgb [B][3],
+ * sqerr [B] = sum_ch (rgb - gt)^2 (loss = sum(sqerr) / (3B)).               */
+int sfmhip_render_train(const float* grid_vm, int D, int H, int W, const float* bmin, const float* bmax,
+                        int mask_mode, const float* rays_o, const float* rays_d, const float* z,
+                        const float* gt, int64_t B, int S, float* rgb, float* sqerr, float* grad_vm,
+                        void* stream);
+
+/* torch.optim.Adam single-tensor step (weight_decay 0, amsgrad off) over n
+ * f32 parameters (n % 4 == 0), step = the step count after increment;
+ * zero_grad != 0 also clears grad (optimizer.zero_grad).                     */
+int sfmhip_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                     double lr, double beta1, double beta2, double eps, int64_t step, int zero_grad,
+                     void* stream);
+
+/* (D,H,W,32) voxel-major -> (C,D,H,W) reference layout (trainer export).     */
+int sfmhip_grid_from_voxel_major(const float* grid_vm, int C, int D, int H, int W, float* grid,
+                                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

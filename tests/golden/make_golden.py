@@ -7,7 +7,8 @@ Only numeric inputs/outputs are written (.npz).  The reference modules are
 loaded by file path at run time:
   * voxel_travesal.py   (torch injected: the file has no `import torch`)
   * sdf.py              (stub `cv2` module: cv2 is only used by SceneHelper)
-  * plenoxel.py         (main guarded)
+  * plenoxel.py         (main guarded; also its training-loop body with
+                        torch autograd + torch.optim.Adam, see gen_train)
   * lightglue/lightglue.py  (loaded standalone; filter_matches only — no weights)
   * sfm.py              ba_sparse extracted with `ast` (the module body needs cv2
                         and output/*.npy)
@@ -398,6 +399,49 @@ def gen_sfm_triangulate():
          focal=np.array(focal), cam1_out=cameras[1], points=P3, point_colors=C3)
 
 
+def gen_train():
+    """Two steps of plenoxel.py's training loop body (plenoxel.py:100-111):
+    render_rays -> mse_loss -> zero_grad/backward -> Adam(lr=1e-2).step(), on
+    CPU torch with the reference's NerfModel / render_rays.  The stratified
+    jitter u of each step is captured by re-seeding (render_rays draws it with
+    torch.rand)."""
+    pl = load("ref_plenoxel_train", os.path.join(REF, "plenoxel.py"))
+    torch.manual_seed(21)
+    model = pl.NerfModel(N=8, scale=1.5)
+    with torch.no_grad():
+        model.voxel_grid.copy_(torch.randn_like(model.voxel_grid) * 0.3 + 0.2)
+    grid0 = model.voxel_grid.detach().numpy().copy()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+    rng = np.random.default_rng(21)
+    B, nb, hn, hf = 32, 24, 2.0, 6.0
+    out = dict(grid0=grid0)
+    for step in (1, 2):
+        ro = (rng.normal(0, 0.3, (B, 3)) + np.array([0, 0, -4.0])).astype(np.float32)
+        rdir = (rng.normal(0, 0.15, (B, 3)) + np.array([0, 0, 1.0])).astype(np.float32)
+        rdir /= np.linalg.norm(rdir, axis=1, keepdims=True)
+        gt = rng.uniform(0, 1, (B, 3)).astype(np.float32)
+        seed = 100 + step
+        torch.manual_seed(seed)
+        rgb = pl.render_rays(model, torch.from_numpy(ro), torch.from_numpy(rdir), hn=hn, hf=hf, nb_bins=nb)
+        loss = torch.nn.functional.mse_loss(torch.from_numpy(gt), rgb)
+        opt.zero_grad()
+        loss.backward()
+        grad = model.voxel_grid.grad.detach().numpy().copy()
+        opt.step()
+        torch.manual_seed(seed)
+        t = torch.linspace(hn, hf, nb).expand(B, nb)
+        mid = (t[:, :-1] + t[:, 1:]) / 2.
+        lower = torch.cat((t[:, :1], mid), -1)
+        upper = torch.cat((mid, t[:, -1:]), -1)
+        z = lower + (upper - lower) * torch.rand(t.shape)
+        st = opt.state[model.voxel_grid]
+        out.update({f"ro{step}": ro, f"rd{step}": rdir, f"gt{step}": gt, f"z{step}": z.numpy(),
+                    f"rgb{step}": rgb.detach().numpy(), f"loss{step}": np.array(loss.item()),
+                    f"grad{step}": grad, f"grid{step}": model.voxel_grid.detach().numpy().copy()})
+    out.update(exp_avg2=st["exp_avg"].numpy().copy(), exp_avg_sq2=st["exp_avg_sq"].numpy().copy())
+    save("train_golden.npz", **out)
+
+
 if __name__ == "__main__":
     gen_vq()
     gen_filter_matches()
@@ -408,3 +452,4 @@ if __name__ == "__main__":
     gen_bow()
     gen_bfs()
     gen_sfm_triangulate()
+    gen_train()

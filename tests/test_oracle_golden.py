@@ -163,3 +163,29 @@ def test_bow_oracle_matches_reference():
     flat = [j for c in r["conn"] for j in c]
     assert flat == g["conn_flat"].tolist() and [len(c) for c in r["conn"]] == g["conn_len"].tolist()
     assert r["start"] == int(g["start"])
+
+
+# --- §8f row 4: grid training step ------------------------------------------------
+def test_train_oracle_matches_reference_torch():
+    """plenoxel.py's training-loop body (render_rays + mse + autograd + Adam) on
+    CPU torch vs the analytic-backward + Adam restatement."""
+    from oracle import train as ot
+    g = golden("train_golden.npz")
+    grid = g["grid0"][0]
+    m = np.zeros_like(grid)
+    v = np.zeros_like(grid)
+    for step in (1, 2):
+        loss, rgb, grad = ot.render_loss_grad(grid, (-1.5,) * 3, (1.5,) * 3, 1, g[f"ro{step}"], g[f"rd{step}"],
+                                              g[f"z{step}"], g[f"gt{step}"])
+        assert abs(loss - float(g[f"loss{step}"])) <= 1e-6 * float(g[f"loss{step}"])
+        np.testing.assert_allclose(rgb, g[f"rgb{step}"], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(grad, g[f"grad{step}"][0], rtol=1e-5, atol=1e-9)
+        grid, m, v = ot.adam_step(grid, grad, m, v, step)
+        np.testing.assert_allclose(grid, g[f"grid{step}"][0], rtol=0, atol=1e-5)
+    # Adam alone on torch's own gradients: bit-exact moments, >= 99.9 % bit-exact params (rest 1 ulp)
+    grid, m, v = g["grid0"][0], np.zeros_like(grid), np.zeros_like(grid)
+    for step in (1, 2):
+        grid, m, v = ot.adam_step(grid, g[f"grad{step}"][0], m, v, step)
+        assert (grid == g[f"grid{step}"][0]).mean() > 0.999
+        assert np.abs(grid - g[f"grid{step}"][0]).max() <= 3e-8
+    assert np.array_equal(m, g["exp_avg2"][0]) and np.array_equal(v, g["exp_avg_sq2"][0])

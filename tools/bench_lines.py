@@ -1,4 +1,4 @@
-"""Time the §8f row 2 verification line alone (bench.py's verify_line)."""
+"""Run selected secondary bench lines alone: python tools/bench_lines.py verify train [--cpu]."""
 import argparse
 import importlib
 import json
@@ -13,8 +13,11 @@ import bench  # noqa: E402
 sfm = importlib.import_module("3d_reconstruction_amd")
 syn = importlib.import_module("3d_reconstruction_amd.synthetic")
 ap = argparse.ArgumentParser()
+ap.add_argument("lines", nargs="+")
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--cpu", action="store_true")
 a = ap.parse_args()
-line = bench.verify_line(sfm, syn, torch.device("cuda", 0), a, lambda: None, cpu=a.cpu)
-print(json.dumps(line))
+dev = torch.device("cuda", 0)
+for name in a.lines:
+    fn = getattr(bench, f"{name}_line")
+    print(json.dumps(fn(sfm, syn, dev, a, lambda: None, cpu=a.cpu)), flush=True)
