@@ -19,6 +19,6 @@ from . import bow, pipeline, reconstruct, tracks, verify  # noqa: F401,E402
 from .bow import kmeans  # noqa: F401
 from .reconstruct import triangulate  # noqa: F401
 from .tracks import MatchGraph, bfs_tracks  # noqa: F401
-from .verify import findEssentialMat, recoverPose  # noqa: F401
+from .verify import findEssentialMat, recoverPose, solvePnPRansac  # noqa: F401
 
 __version__ = "0.1.0"

@@ -1,0 +1,819 @@
+// pnp.hip — SURVEY.md §8f row 2 (last part): cv2.solvePnPRansac at sfm.py:116
+//     cv2.solvePnPRansac(X, pts1, K, np.zeros((5, 1)), cv2.SOLVEPNP_ITERATIVE)
+// i.e. iterationsCount 100, reprojectionError 8, confidence 0.99, flags
+// ITERATIVE (the 5th positional argument is rvec), restated from OpenCV 4.x
+// (solvepnp.cpp, epnp.cpp, ptsetreg.cpp, calibration.cpp
+// cvFindExtrinsicCameraParams2 + CvLevMarq); CPU restatement oracle/pnp.py.
+// Parity with OpenCV is unpinned (cv2 absent).
+//
+// One workgroup (4 waves) per registration problem:
+//   * points are converted to float (solvePnPRansac's CV_32F conversion);
+//   * RANSAC: lane 0 draws 16 five-point samples per chunk from cv::RNG(-1);
+//     each sample is solved by EPnP in a 16-lane group (M^T M eigenvectors by
+//     a parallel-ordered two-sided Jacobi in LDS, the three beta
+//     approximations + Gauss-Newton in lanes 0..2, Procrustes), scored by all
+//     lanes (float squared reprojection error <= 64, wave ballots) and
+//     replayed in OpenCV's sequential order;
+//   * the RANSAC pose is refined on the inliers by Levenberg-Marquardt with
+//     CvLevMarq's control flow; J^T J / J^T e are block reductions in a fixed
+//     order, the 6x6 damped system is solved by thread 0.
+#include "common.h"
+#include "geom_dev.h"
+
+namespace sfmhip {
+namespace {
+
+constexpr int kPnThreads = 256;
+constexpr int kPnGL = 16;
+constexpr int kPnH = kPnThreads / kPnGL;  // hypotheses per chunk
+constexpr int kPnGS = 448;                // LDS doubles per group
+constexpr double kEps64 = 2.220446049250313e-16;
+constexpr double kDblMin64 = 2.2250738585072014e-308;
+
+// group scratch map (doubles)
+constexpr int gA = 0, gV = 144, gRot = 288 /* 6 x (c, s) */, gL = 300, gRho = 360, gSol = 366 /* 3 x 13 */,
+              gCws = 405 /* 12 */;
+
+struct CvRng {
+    uint64_t s;
+    __device__ unsigned next() {
+        s = (uint64_t)(unsigned)s * 4164903690ULL + (unsigned)(s >> 32);
+        return (unsigned)s;
+    }
+    __device__ int uniform0(unsigned n, double inv_n) {
+        const unsigned x = next();
+        unsigned qd = (unsigned)((double)x * inv_n);
+        long long r = (long long)x - (long long)qd * n;
+        if (r < 0) r += n;
+        else if (r >= (long long)n) r -= n;
+        return (int)r;
+    }
+};
+
+__device__ int update_num_iters(double p, double ep, int m, int max_iters) {
+    p = fmin(fmax(p, 0.0), 1.0);
+    ep = fmin(fmax(ep, 0.0), 1.0);
+    double num = fmax(1.0 - p, kDblMin64);
+    double denom = 1.0 - pow(1.0 - ep, (double)m);
+    if (denom < kDblMin64) return 0;
+    num = log(num);
+    denom = log(denom);
+    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
+}
+
+__device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
+
+// Symmetric 3x3 eigen-decomposition by cyclic Jacobi: eigenvalues descending,
+// rows of E = eigenvectors with the largest-|.| component positive.
+__device__ void eig3_desc(double A[3][3], double w[3], double E[3][3]) {
+    double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int sweep = 0; sweep < 30; ++sweep) {
+        const double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
+        const double dg = A[0][0] * A[0][0] + A[1][1] * A[1][1] + A[2][2] * A[2][2];
+        if (off <= 1e-32 * dg || off == 0.0) break;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                if (A[p][q] == 0.0) continue;
+                const double tau = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
+                const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+                const double c = 1.0 / sqrt(1.0 + t * t), s = t * c;
+                for (int k = 0; k < 3; ++k) {  // A <- A J (columns p, q)
+                    const double ap = A[k][p], aq = A[k][q];
+                    A[k][p] = c * ap - s * aq;
+                    A[k][q] = s * ap + c * aq;
+                }
+                for (int k = 0; k < 3; ++k) {  // A <- J^T A (rows p, q)
+                    const double ap = A[p][k], aq = A[q][k];
+                    A[p][k] = c * ap - s * aq;
+                    A[q][k] = s * ap + c * aq;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    const double vp = V[k][p], vq = V[k][q];
+                    V[k][p] = c * vp - s * vq;
+                    V[k][q] = s * vp + c * vq;
+                }
+            }
+    }
+    int o[3] = {0, 1, 2};
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2 - i; ++j)
+            if (A[o[j]][o[j]] < A[o[j + 1]][o[j + 1]]) { const int t = o[j]; o[j] = o[j + 1]; o[j + 1] = t; }
+    for (int i = 0; i < 3; ++i) {
+        w[i] = A[o[i]][o[i]];
+        int im = 0;
+        for (int k = 1; k < 3; ++k)
+            if (fabs(V[k][o[i]]) > fabs(V[im][o[i]])) im = k;
+        const double sg = V[im][o[i]] >= 0 ? 1.0 : -1.0;
+        for (int k = 0; k < 3; ++k) E[i][k] = sg * V[k][o[i]];
+    }
+}
+
+// SVD of a 3x3 (row-major A) by one-sided Jacobi: A = U diag(s) V^T, s descending.
+__device__ void svd3(const double* A, double U[3][3], double s[3], double V[3][3]) {
+    double B[3][3];  // B[col][row]
+    double W[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};  // W[col][row]
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) B[c][r] = A[3 * r + c];
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        bool rot = false;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                double al = 0, be = 0, ga = 0;
+                for (int r = 0; r < 3; ++r) {
+                    al += B[p][r] * B[p][r];
+                    be += B[q][r] * B[q][r];
+                    ga += B[p][r] * B[q][r];
+                }
+                if (ga == 0.0 || fabs(ga) <= 1e-15 * sqrt(al * be)) continue;
+                rot = true;
+                const double zeta = (be - al) / (2.0 * ga);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+                for (int r = 0; r < 3; ++r) {
+                    const double bp = B[p][r], bq = B[q][r];
+                    B[p][r] = c * bp - sn * bq;
+                    B[q][r] = sn * bp + c * bq;
+                    const double wp = W[p][r], wq = W[q][r];
+                    W[p][r] = c * wp - sn * wq;
+                    W[q][r] = sn * wp + c * wq;
+                }
+            }
+        if (!rot) break;
+    }
+    double sg[3];
+    int o[3] = {0, 1, 2};
+    for (int c = 0; c < 3; ++c) sg[c] = sqrt(B[c][0] * B[c][0] + B[c][1] * B[c][1] + B[c][2] * B[c][2]);
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2 - i; ++j)
+            if (sg[o[j]] < sg[o[j + 1]]) { const int t = o[j]; o[j] = o[j + 1]; o[j + 1] = t; }
+    for (int i = 0; i < 3; ++i) {
+        s[i] = sg[o[i]];
+        for (int r = 0; r < 3; ++r) V[r][i] = W[o[i]][r];
+    }
+    for (int i = 0; i < 2; ++i)
+        for (int r = 0; r < 3; ++r) U[r][i] = s[i] > 0 ? B[o[i]][r] / s[i] : (r == i ? 1.0 : 0.0);
+    if (s[2] > 1e-300 * s[0] && s[2] > 0) {
+        for (int r = 0; r < 3; ++r) U[r][2] = B[o[2]][r] / s[2];
+    } else {  // rank-deficient: complete the basis
+        U[0][2] = U[1][0] * U[2][1] - U[2][0] * U[1][1];
+        U[1][2] = U[2][0] * U[0][1] - U[0][0] * U[2][1];
+        U[2][2] = U[0][0] * U[1][1] - U[1][0] * U[0][1];
+    }
+}
+
+// cv::Rodrigues matrix -> vector (calibration.cpp): R projected on SO(3) by
+// SVD, then the axis-angle with OpenCV's small-s branch.
+__device__ void rodrigues_inv(const double* Rin, double* rv) {
+    double U[3][3], s[3], V[3][3], R[3][3];
+    svd3(Rin, U, s, V);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[i][j] = U[i][0] * V[j][0] + U[i][1] * V[j][1] + U[i][2] * V[j][2];
+    double rx = R[2][1] - R[1][2], ry = R[0][2] - R[2][0], rz = R[1][0] - R[0][1];
+    const double sn = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0][0] + R[1][1] + R[2][2] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double theta = acos(c);
+    if (sn < 1e-5) {
+        if (c > 0) { rv[0] = rv[1] = rv[2] = 0; return; }
+        double t = (R[0][0] + 1) * 0.5;
+        rx = sqrt(fmax(t, 0.));
+        t = (R[1][1] + 1) * 0.5;
+        ry = sqrt(fmax(t, 0.)) * (R[0][1] < 0 ? -1. : 1.);
+        t = (R[2][2] + 1) * 0.5;
+        rz = sqrt(fmax(t, 0.)) * (R[0][2] < 0 ? -1. : 1.);
+        if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[1][2] > 0) != (ry * rz > 0)) rz = -rz;
+        theta /= sqrt(rx * rx + ry * ry + rz * rz);
+        rv[0] = rx * theta; rv[1] = ry * theta; rv[2] = rz * theta;
+        return;
+    }
+    const double vth = 1 / (2 * sn) * theta;
+    rv[0] = rx * vth; rv[1] = ry * vth; rv[2] = rz * vth;
+}
+
+// cv::Rodrigues vector -> matrix Jacobian, J[i*9+k] = dR_k / dr_i.
+__device__ void rodrigues_jac(const double* rvec, double* J) {
+    const double theta = sqrt(rvec[0] * rvec[0] + rvec[1] * rvec[1] + rvec[2] * rvec[2]);
+    if (theta < kEps64) {
+        for (int k = 0; k < 27; ++k) J[k] = 0;
+        J[5] = -1; J[7] = 1; J[9 + 2] = 1; J[9 + 6] = -1; J[18 + 1] = -1; J[18 + 3] = 1;
+        return;
+    }
+    const double c = cos(theta), s = sin(theta), c1 = 1. - c, it = 1. / theta;
+    const double rx = rvec[0] * it, ry = rvec[1] * it, rz = rvec[2] * it;
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double rxm[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    const double drrt[27] = {rx + rx, ry, rz, ry, 0, 0, rz, 0, 0, 0, rx, 0, rx, ry + ry, rz, 0, rz, 0,
+                             0, 0, rx, 0, 0, ry, rx, ry, rz + rz};
+    const double drx[27] = {0, 0, 0, 0, 0, -1, 0, 1, 0, 0, 0, 1, 0, 0, 0, -1, 0, 0,
+                            0, -1, 0, 1, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 3; ++i) {
+        const double ri = i == 0 ? rx : i == 1 ? ry : rz;
+        const double a0 = -s * ri, a1 = (s - 2 * c1 * it) * ri, a2 = c1 * it, a3 = (c - s * it) * ri, a4 = s * it;
+        for (int k = 0; k < 9; ++k)
+            J[i * 9 + k] = a0 * I[k] + a1 * rrt[k] + a2 * drrt[i * 9 + k] + a3 * rxm[k] + a4 * drx[i * 9 + k];
+    }
+}
+
+// Least squares min ||A x - b|| for a 6 x nc (nc <= 5) full-column-rank A by
+// Householder QR (row-major A, modified in place).
+template <int NC>
+__device__ void lsq6(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
+    for (int k = 0; k < NC; ++k) {
+        double nrm = 0;
+        for (int r = k; r < 6; ++r) nrm += A[r][k] * A[r][k];
+        nrm = sqrt(nrm);
+        if (nrm == 0.0) continue;
+        const double alpha = A[k][k] >= 0 ? -nrm : nrm;
+        double v[6];
+        for (int r = 0; r < 6; ++r) v[r] = r < k ? 0.0 : A[r][k];
+        v[k] -= alpha;
+        double vn = 0;
+        for (int r = k; r < 6; ++r) vn += v[r] * v[r];
+        if (vn == 0.0) continue;
+        const double beta = 2.0 / vn;
+        for (int c = k; c < NC; ++c) {
+            double s = 0;
+            for (int r = k; r < 6; ++r) s += v[r] * A[r][c];
+            s *= beta;
+            for (int r = k; r < 6; ++r) A[r][c] -= s * v[r];
+        }
+        double s = 0;
+        for (int r = k; r < 6; ++r) s += v[r] * b[r];
+        s *= beta;
+        for (int r = k; r < 6; ++r) b[r] -= s * v[r];
+    }
+    for (int k = NC - 1; k >= 0; --k) {
+        double s = b[k];
+        for (int c = k + 1; c < NC; ++c) s -= A[k][c] * x[c];
+        x[k] = A[k][k] != 0.0 ? s / A[k][k] : 0.0;
+    }
+}
+
+struct EpnpData {
+    double pw[5][3], us[5][2], al[5][4];
+    double fu, fv, uc, vc;
+};
+
+// compute_R_and_t for one beta vector (epnp.cpp); returns the mean reprojection error.
+__device__ double epnp_R_t(const EpnpData& D, const double* G, const int* vi, const double* betas, double* R,
+                           double* t) {
+    double ccs[4][3] = {};
+    for (int i = 0; i < 4; ++i) {
+        const double* v = G + gV;  // eigenvector vi[i] = column vi[i] of V
+        for (int j = 0; j < 4; ++j)
+            for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * v[(3 * j + k) * 12 + vi[i]];
+    }
+    double pcs[5][3];
+    for (int p = 0; p < 5; ++p)
+        for (int j = 0; j < 3; ++j)
+            pcs[p][j] = D.al[p][0] * ccs[0][j] + D.al[p][1] * ccs[1][j] + D.al[p][2] * ccs[2][j] + D.al[p][3] * ccs[3][j];
+    if (pcs[0][2] < 0)
+        for (int p = 0; p < 5; ++p)
+            for (int j = 0; j < 3; ++j) pcs[p][j] = -pcs[p][j];
+    double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+    for (int p = 0; p < 5; ++p)
+        for (int j = 0; j < 3; ++j) { pc0[j] += pcs[p][j]; pw0[j] += D.pw[p][j]; }
+    for (int j = 0; j < 3; ++j) { pc0[j] /= 5; pw0[j] /= 5; }
+    double abt[9] = {};
+    for (int p = 0; p < 5; ++p)
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) abt[3 * j + k] += (pcs[p][j] - pc0[j]) * (D.pw[p][k] - pw0[k]);
+    double U[3][3], s[3], V[3][3];
+    svd3(abt, U, s, V);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = U[i][0] * V[j][0] + U[i][1] * V[j][1] + U[i][2] * V[j][2];
+    const double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] - R[2] * R[4] * R[6] -
+                       R[1] * R[3] * R[8] - R[0] * R[5] * R[7];
+    if (det < 0) { R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8]; }
+    for (int i = 0; i < 3; ++i) t[i] = pc0[i] - (R[3 * i] * pw0[0] + R[3 * i + 1] * pw0[1] + R[3 * i + 2] * pw0[2]);
+    double sum = 0;
+    for (int p = 0; p < 5; ++p) {
+        const double* pw = D.pw[p];
+        const double Xc = R[0] * pw[0] + R[1] * pw[1] + R[2] * pw[2] + t[0];
+        const double Yc = R[3] * pw[0] + R[4] * pw[1] + R[5] * pw[2] + t[1];
+        const double iz = 1.0 / (R[6] * pw[0] + R[7] * pw[1] + R[8] * pw[2] + t[2]);
+        const double ue = D.uc + D.fu * Xc * iz, ve = D.vc + D.fv * Yc * iz;
+        sum += sqrt((D.us[p][0] - ue) * (D.us[p][0] - ue) + (D.us[p][1] - ve) * (D.us[p][1] - ve));
+    }
+    return sum / 5;
+}
+
+// EPnP on 5 correspondences by a 16-lane group; writes (rvec, tvec) to out[6].
+__device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
+    // M^T M (12x12) into A, V = I
+    for (int e = gl; e < 144; e += kPnGL) {
+        const int i = e / 12, j = e % 12;
+        double acc = 0;
+        for (int p = 0; p < 5; ++p) {
+            // M rows 2p (u) and 2p+1 (v): col 3c -> a*fu / 0, col 3c+1 -> 0 / a*fv, col 3c+2 -> a*(uc-u) / a*(vc-v)
+            const int ci = i / 3, ki = i % 3, cj = j / 3, kj = j % 3;
+            const double ai = D.al[p][ci], aj = D.al[p][cj];
+            const double mu_i = ki == 0 ? ai * D.fu : ki == 1 ? 0.0 : ai * (D.uc - D.us[p][0]);
+            const double mu_j = kj == 0 ? aj * D.fu : kj == 1 ? 0.0 : aj * (D.uc - D.us[p][0]);
+            const double mv_i = ki == 0 ? 0.0 : ki == 1 ? ai * D.fv : ai * (D.vc - D.us[p][1]);
+            const double mv_j = kj == 0 ? 0.0 : kj == 1 ? aj * D.fv : aj * (D.vc - D.us[p][1]);
+            acc += mu_i * mu_j + mv_i * mv_j;
+        }
+        G[gA + e] = acc;
+        G[gV + e] = (i == j) ? 1.0 : 0.0;
+    }
+    lds_fence();
+    // parallel-ordered two-sided Jacobi: 11 rounds of 6 disjoint pairs per sweep
+    for (int sweep = 0; sweep < 15; ++sweep) {
+        // convergence: off-diagonal vs diagonal mass (group reduction)
+        double off = 0, dg = 0;
+        for (int e = gl; e < 144; e += kPnGL) {
+            const double a = G[gA + e];
+            if (e / 12 == e % 12) dg += a * a; else off += a * a;
+        }
+        for (int o = 8; o > 0; o >>= 1) { off += __shfl_xor(off, o, kPnGL); dg += __shfl_xor(dg, o, kPnGL); }
+        if (off <= 1e-30 * dg) break;
+        for (int rnd = 0; rnd < 11; ++rnd) {
+            if (gl < 6) {
+                int p, q;
+                if (gl == 0) { p = 11; q = rnd; } else { p = (rnd + gl) % 11; q = (rnd - gl + 11) % 11; }
+                if (p > q) { const int t = p; p = q; q = t; }
+                const double apq = G[gA + p * 12 + q];
+                double c = 1.0, s = 0.0;
+                if (apq != 0.0) {
+                    const double tau = (G[gA + q * 12 + q] - G[gA + p * 12 + p]) / (2.0 * apq);
+                    const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+                    c = 1.0 / sqrt(1.0 + t * t);
+                    s = t * c;
+                }
+                G[gRot + 2 * gl] = c;
+                G[gRot + 2 * gl + 1] = s;
+            }
+            lds_fence();
+            // rows: A <- J^T A (row pairs (p, q) of all 12 columns): 6 x 12 updates
+            for (int u = gl; u < 72; u += kPnGL) {
+                const int k = u / 12, col = u % 12;
+                int p, q;
+                if (k == 0) { p = 11; q = rnd; } else { p = (rnd + k) % 11; q = (rnd - k + 11) % 11; }
+                if (p > q) { const int t = p; p = q; q = t; }
+                const double c = G[gRot + 2 * k], s = G[gRot + 2 * k + 1];
+                const double ap = G[gA + p * 12 + col], aq = G[gA + q * 12 + col];
+                G[gA + p * 12 + col] = c * ap - s * aq;
+                G[gA + q * 12 + col] = s * ap + c * aq;
+            }
+            lds_fence();
+            // columns: A <- A J and V <- V J
+            for (int u = gl; u < 144; u += kPnGL) {
+                const int k = (u % 72) / 12, row = u % 12;
+                const bool isV = u >= 72;
+                int p, q;
+                if (k == 0) { p = 11; q = rnd; } else { p = (rnd + k) % 11; q = (rnd - k + 11) % 11; }
+                if (p > q) { const int t = p; p = q; q = t; }
+                const double c = G[gRot + 2 * k], s = G[gRot + 2 * k + 1];
+                double* M = G + (isV ? gV : gA);
+                const double ap = M[row * 12 + p], aq = M[row * 12 + q];
+                M[row * 12 + p] = c * ap - s * aq;
+                M[row * 12 + q] = s * ap + c * aq;
+            }
+            lds_fence();
+        }
+    }
+    // the 4 smallest eigenvalues (ascending), canonical signs
+    int vi[4];
+    {
+        double ev[12];
+        for (int i = 0; i < 12; ++i) ev[i] = G[gA + i * 13];
+        bool used[12] = {};
+        for (int k = 0; k < 4; ++k) {
+            int b = -1;
+            for (int i = 0; i < 12; ++i)
+                if (!used[i] && (b < 0 || ev[i] < ev[b])) b = i;
+            used[b] = true;
+            vi[k] = b;
+        }
+    }
+    lds_fence();
+    if (gl < 4) {
+        const int col = vi[gl];
+        int im = 0;
+        for (int r = 1; r < 12; ++r)
+            if (fabs(G[gV + r * 12 + col]) > fabs(G[gV + im * 12 + col])) im = r;
+        if (G[gV + im * 12 + col] < 0)
+            for (int r = 0; r < 12; ++r) G[gV + r * 12 + col] = -G[gV + r * 12 + col];
+    }
+    lds_fence();
+    // L_6x10 and rho: lane r < 6 builds row r
+    if (gl < 6) {
+        const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
+        const int a = pa[gl], b = pb[gl];
+        double dv[4][3];
+        for (int i = 0; i < 4; ++i)
+            for (int k = 0; k < 3; ++k)
+                dv[i][k] = G[gV + (3 * a + k) * 12 + vi[i]] - G[gV + (3 * b + k) * 12 + vi[i]];
+        auto dot = [&](int i, int j) { return dv[i][0] * dv[j][0] + dv[i][1] * dv[j][1] + dv[i][2] * dv[j][2]; };
+        double* row = G + gL + 10 * gl;
+        row[0] = dot(0, 0); row[1] = 2.0 * dot(0, 1); row[2] = dot(1, 1); row[3] = 2.0 * dot(0, 2);
+        row[4] = 2.0 * dot(1, 2); row[5] = dot(2, 2); row[6] = 2.0 * dot(0, 3); row[7] = 2.0 * dot(1, 3);
+        row[8] = 2.0 * dot(2, 3); row[9] = dot(3, 3);
+        const double* ca = G + gCws + 3 * a;
+        const double* cb = G + gCws + 3 * b;
+        G[gRho + gl] = (ca[0] - cb[0]) * (ca[0] - cb[0]) + (ca[1] - cb[1]) * (ca[1] - cb[1]) +
+                       (ca[2] - cb[2]) * (ca[2] - cb[2]);
+    }
+    lds_fence();
+    // three beta approximations (lane 0: B11 B12 B13 B14, 1: B11 B12 B22, 2: B11 B12 B22 B13 B23)
+    if (gl < 3) {
+        double L[6][10], rho[6];
+        for (int r = 0; r < 6; ++r) {
+            for (int c = 0; c < 10; ++c) L[r][c] = G[gL + 10 * r + c];
+            rho[r] = G[gRho + r];
+        }
+        double be[4] = {0, 0, 0, 0};
+        if (gl == 0) {
+            double A[6][4], b[6], x[4];
+            const int cs[4] = {0, 1, 3, 6};
+            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 4; ++c) A[r][c] = L[r][cs[c]]; b[r] = rho[r]; }
+            lsq6<4>(A, b, x);
+            if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = -x[1] / be[0]; be[2] = -x[2] / be[0]; be[3] = -x[3] / be[0]; }
+            else { be[0] = sqrt(x[0]); be[1] = x[1] / be[0]; be[2] = x[2] / be[0]; be[3] = x[3] / be[0]; }
+        } else if (gl == 1) {
+            double A[6][3], b[6], x[3];
+            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 3; ++c) A[r][c] = L[r][c]; b[r] = rho[r]; }
+            lsq6<3>(A, b, x);
+            if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0; }
+            else { be[0] = sqrt(x[0]); be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0; }
+            if (x[1] < 0) be[0] = -be[0];
+        } else {
+            double A[6][5], b[6], x[5];
+            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 5; ++c) A[r][c] = L[r][c]; b[r] = rho[r]; }
+            lsq6<5>(A, b, x);
+            if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0; }
+            else { be[0] = sqrt(x[0]); be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0; }
+            if (x[1] < 0) be[0] = -be[0];
+            be[2] = x[3] / be[0];
+        }
+        for (int it = 0; it < 5; ++it) {  // gauss_newton
+            double A[6][4], b[6], x[4];
+            for (int i = 0; i < 6; ++i) {
+                const double* l = L[i];
+                A[i][0] = 2 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
+                A[i][1] = l[1] * be[0] + 2 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
+                A[i][2] = l[3] * be[0] + l[4] * be[1] + 2 * l[5] * be[2] + l[8] * be[3];
+                A[i][3] = l[6] * be[0] + l[7] * be[1] + l[8] * be[2] + 2 * l[9] * be[3];
+                b[i] = rho[i] - (l[0] * be[0] * be[0] + l[1] * be[0] * be[1] + l[2] * be[1] * be[1] +
+                                 l[3] * be[0] * be[2] + l[4] * be[1] * be[2] + l[5] * be[2] * be[2] +
+                                 l[6] * be[0] * be[3] + l[7] * be[1] * be[3] + l[8] * be[2] * be[3] +
+                                 l[9] * be[3] * be[3]);
+            }
+            lsq6<4>(A, b, x);
+            for (int i = 0; i < 4; ++i) be[i] += x[i];
+        }
+        double R[9], t[3];
+        const double err = epnp_R_t(D, G, vi, be, R, t);
+        double* sol = G + gSol + 13 * gl;
+        for (int k = 0; k < 9; ++k) sol[k] = R[k];
+        for (int k = 0; k < 3; ++k) sol[9 + k] = t[k];
+        sol[12] = err;
+    }
+    lds_fence();
+    if (gl == 0) {
+        int N = 0;
+        if (G[gSol + 13 + 12] < G[gSol + 12]) N = 1;
+        if (G[gSol + 26 + 12] < G[gSol + 13 * N + 12]) N = 2;
+        const double* sol = G + gSol + 13 * N;
+        rodrigues_inv(sol, out);
+        out[3] = sol[9]; out[4] = sol[10]; out[5] = sol[11];
+    }
+    lds_fence();
+}
+
+// projection of a float object point (converted to double) with R, t, K;
+// the result rounded to float as cvProjectPoints2 stores into a CV_32F array.
+__device__ __forceinline__ void project_f(const double* R, const double* t, double fx, double fy, double cx,
+                                          double cy, float X, float Y, float Z, float& u, float& v) {
+    const double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    const double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    z = z ? 1.0 / z : 1.0;
+    u = (float)(x * z * fx + cx);
+    v = (float)(y * z * fy + cy);
+}
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
+    const double* __restrict__ obj, const double* __restrict__ img, const int64_t* __restrict__ offs,
+    const double* __restrict__ cam, int max_iters, double reproj, double confidence, float* __restrict__ wf,
+    double* __restrict__ rvec_out, double* __restrict__ tvec_out, uint8_t* __restrict__ mask,
+    int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out) {
+    __shared__ double s_grp[kPnH * kPnGS];
+    __shared__ double s_models[kPnH][6 + 9];  // rvec, tvec, R
+    __shared__ int s_cnt[kPnH];
+    __shared__ int s_sub[kPnH * 5];
+    __shared__ double s_best[6];
+    __shared__ double s_red[4 * 28];
+    __shared__ double s_lm[6 + 6 + 27 + 9];   // param, prev, dRdr, R
+    __shared__ int s_niters, s_maxgood, s_k0, s_last, s_flag;
+
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int h = tid / kPnGL, gl = tid % kPnGL;
+    const int64_t off = offs[p];
+    const int n = (int)(offs[p + 1] - off);
+    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
+    const float thr = (float)(reproj * reproj);
+    float* f = wf + off * 5;  // float copies: X, Y, Z, u, v
+    for (int i = tid; i < n; i += kPnThreads) {
+        for (int k = 0; k < 3; ++k) f[5 * i + k] = (float)obj[3 * (off + i) + k];
+        for (int k = 0; k < 2; ++k) f[5 * i + 3 + k] = (float)img[2 * (off + i) + k];
+        mask[off + i] = 0;
+    }
+    if (tid == 0) { s_niters = max(max_iters, 1); s_maxgood = 0; s_k0 = 0; s_last = -1; }
+    __syncthreads();
+    if (n < 5) {
+        if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
+        return;
+    }
+    auto load_sample = [&](const int* idx, EpnpData& D) {
+        D.fu = fx; D.fv = fy; D.uc = cx; D.vc = cy;
+        for (int j = 0; j < 5; ++j) {
+            for (int k = 0; k < 3; ++k) D.pw[j][k] = (double)f[5 * idx[j] + k];
+            for (int k = 0; k < 2; ++k) D.us[j][k] = (double)f[5 * idx[j] + 3 + k];
+        }
+    };
+    auto prepare = [&](EpnpData& D, double* G) {  // control points + alphas (every lane of the group)
+        double c0[3] = {0, 0, 0};
+        for (int j = 0; j < 5; ++j)
+            for (int k = 0; k < 3; ++k) c0[k] += D.pw[j][k];
+        for (int k = 0; k < 3; ++k) c0[k] /= 5;
+        double A[3][3] = {}, w[3], E[3][3];
+        for (int j = 0; j < 5; ++j)
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) A[a][b] += (D.pw[j][a] - c0[a]) * (D.pw[j][b] - c0[b]);
+        eig3_desc(A, w, E);
+        double cws[4][3];
+        for (int k = 0; k < 3; ++k) cws[0][k] = c0[k];
+        for (int i = 1; i < 4; ++i) {
+            const double kk = sqrt(fmax(w[i - 1], 0.0) / 5);
+            for (int k = 0; k < 3; ++k) cws[i][k] = c0[k] + kk * E[i - 1][k];
+        }
+        if (gl == 0)
+            for (int i = 0; i < 4; ++i)
+                for (int k = 0; k < 3; ++k) G[gCws + 3 * i + k] = cws[i][k];
+        double CC[3][3];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 1; j < 4; ++j) CC[i][j - 1] = cws[j][i] - cws[0][i];
+        const double det = CC[0][0] * (CC[1][1] * CC[2][2] - CC[1][2] * CC[2][1]) -
+                           CC[0][1] * (CC[1][0] * CC[2][2] - CC[1][2] * CC[2][0]) +
+                           CC[0][2] * (CC[1][0] * CC[2][1] - CC[1][1] * CC[2][0]);
+        const double id = det != 0.0 ? 1.0 / det : 0.0;
+        double ci[3][3];
+        ci[0][0] = (CC[1][1] * CC[2][2] - CC[1][2] * CC[2][1]) * id;
+        ci[0][1] = (CC[0][2] * CC[2][1] - CC[0][1] * CC[2][2]) * id;
+        ci[0][2] = (CC[0][1] * CC[1][2] - CC[0][2] * CC[1][1]) * id;
+        ci[1][0] = (CC[1][2] * CC[2][0] - CC[1][0] * CC[2][2]) * id;
+        ci[1][1] = (CC[0][0] * CC[2][2] - CC[0][2] * CC[2][0]) * id;
+        ci[1][2] = (CC[0][2] * CC[1][0] - CC[0][0] * CC[1][2]) * id;
+        ci[2][0] = (CC[1][0] * CC[2][1] - CC[1][1] * CC[2][0]) * id;
+        ci[2][1] = (CC[0][1] * CC[2][0] - CC[0][0] * CC[2][1]) * id;
+        ci[2][2] = (CC[0][0] * CC[1][1] - CC[0][1] * CC[1][0]) * id;
+        for (int j = 0; j < 5; ++j) {
+            const double d0 = D.pw[j][0] - cws[0][0], d1 = D.pw[j][1] - cws[0][1], d2 = D.pw[j][2] - cws[0][2];
+            for (int a = 0; a < 3; ++a) D.al[j][1 + a] = ci[a][0] * d0 + ci[a][1] * d1 + ci[a][2] * d2;
+            D.al[j][0] = 1.0 - D.al[j][1] - D.al[j][2] - D.al[j][3];
+        }
+        lds_fence();
+    };
+    if (n == 5) {  // model_points == npoints: solvePnP(EPnP) on all points, no refinement
+        if (h == 0) {
+            const int idx[5] = {0, 1, 2, 3, 4};
+            EpnpData D;
+            load_sample(idx, D);
+            prepare(D, s_grp);
+            epnp_group(D, gl, s_grp, s_best);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int k = 0; k < 3; ++k) { rvec_out[3 * p + k] = s_best[k]; tvec_out[3 * p + k] = s_best[3 + k]; }
+            ok_out[p] = 1; ninl_out[p] = 5; iters_out[p] = 1;
+        }
+        if (tid < 5) mask[off + tid] = 1;
+        return;
+    }
+    CvRng rng{~0ULL};
+    const double inv_n = 1.0 / (double)n;
+    for (;;) {
+        const int k0 = s_k0, niters = s_niters;
+        if (tid == 0) {
+            const int nh = min(kPnH, niters - k0);
+            for (int hh = 0; hh < nh; ++hh)
+                for (int i = 0; i < 5; ++i) {
+                    int idx;
+                    for (;;) {
+                        idx = rng.uniform0((unsigned)n, inv_n);
+                        int j = 0;
+                        while (j < i && s_sub[hh * 5 + j] != idx) ++j;
+                        if (j == i) break;
+                    }
+                    s_sub[hh * 5 + i] = idx;
+                }
+        }
+        if (tid < kPnH) s_cnt[tid] = 0;
+        __syncthreads();
+        const bool live = k0 + h < niters;
+        if (live) {
+            EpnpData D;
+            load_sample(s_sub + h * 5, D);
+            double* G = s_grp + h * kPnGS;
+            prepare(D, G);
+            epnp_group(D, gl, G, s_models[h]);
+            if (gl == 0) rodrigues(s_models[h], s_models[h] + 6);
+        }
+        __syncthreads();
+        for (int i0 = 0; i0 < n; i0 += kPnThreads) {
+            const int i = i0 + tid;
+            const bool valid = i < n;
+            float X = 0, Y = 0, Z = 0, u = 0, v = 0;
+            if (valid) { X = f[5 * i]; Y = f[5 * i + 1]; Z = f[5 * i + 2]; u = f[5 * i + 3]; v = f[5 * i + 4]; }
+            for (int hh = 0; hh < kPnH; ++hh) {
+                if (k0 + hh >= niters) break;
+                float pu, pv;
+                project_f(s_models[hh] + 6, s_models[hh] + 3, fx, fy, cx, cy, X, Y, Z, pu, pv);
+                const float du = u - pu, dv = v - pv;
+                const float e = du * du + dv * dv;
+                const int c = __popcll(__ballot(valid && e <= thr));
+                if (lane == 0 && c) atomicAdd(&s_cnt[hh], c);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int nit = niters, maxgood = s_maxgood, last = s_last;
+            for (int hh = 0; hh < kPnH; ++hh) {
+                const int k = k0 + hh;
+                if (k >= nit) break;
+                const int good = s_cnt[hh];
+                if (good > max(maxgood, 4)) {
+                    for (int e = 0; e < 6; ++e) s_best[e] = s_models[hh][e];
+                    maxgood = good;
+                    nit = update_num_iters(confidence, (double)(n - good) / n, 5, nit);
+                }
+                last = k;
+            }
+            s_niters = nit; s_maxgood = maxgood; s_last = last; s_k0 = k0 + kPnH;
+        }
+        __syncthreads();
+        if (s_k0 >= s_niters) break;
+    }
+    const int maxgood = s_maxgood;
+    if (maxgood <= 0) {
+        if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = s_last + 1; }
+        return;
+    }
+    // inlier mask of the best model
+    if (tid == 0) rodrigues(s_best, s_lm + 39);
+    __syncthreads();
+    for (int i = tid; i < n; i += kPnThreads) {
+        float pu, pv;
+        project_f(s_lm + 39, s_best + 3, fx, fy, cx, cy, f[5 * i], f[5 * i + 1], f[5 * i + 2], pu, pv);
+        const float du = f[5 * i + 3] - pu, dv = f[5 * i + 4] - pv;
+        mask[off + i] = (du * du + dv * dv <= thr) ? 1 : 0;
+    }
+    // Levenberg-Marquardt refinement on the inliers (CvLevMarq control flow)
+    double* prm = s_lm;       // param[6]
+    double* prev = s_lm + 6;  // prevParam[6]
+    double* dR = s_lm + 12;   // dR/dr (27)
+    double* Rm = s_lm + 39;   // R (9)
+    if (tid < 6) prm[tid] = s_best[tid];
+    __syncthreads();
+    auto eval = [&](bool with_j, double* jtj, double* jte) -> double {
+        if (tid == 0) {
+            rodrigues(prm, Rm);
+            rodrigues_jac(prm, dR);
+        }
+        __syncthreads();
+        double acc[28];
+        for (int k = 0; k < 28; ++k) acc[k] = 0;
+        for (int i = tid; i < n; i += kPnThreads) {
+            if (!mask[off + i]) continue;
+            const double X = f[5 * i], Y = f[5 * i + 1], Z = f[5 * i + 2];
+            const double xc = Rm[0] * X + Rm[1] * Y + Rm[2] * Z + prm[3];
+            const double yc = Rm[3] * X + Rm[4] * Y + Rm[5] * Z + prm[4];
+            double z = Rm[6] * X + Rm[7] * Y + Rm[8] * Z + prm[5];
+            z = z ? 1.0 / z : 1.0;
+            const double x = xc * z, y = yc * z;
+            const double eu = (x * fx + cx) - (double)f[5 * i + 3], ev = (y * fy + cy) - (double)f[5 * i + 4];
+            acc[27] += eu * eu + ev * ev;
+            if (with_j) {
+                double ju[6], jv[6];
+                for (int j = 0; j < 3; ++j) {
+                    const double dx0 = X * dR[j * 9 + 0] + Y * dR[j * 9 + 1] + Z * dR[j * 9 + 2];
+                    const double dy0 = X * dR[j * 9 + 3] + Y * dR[j * 9 + 4] + Z * dR[j * 9 + 5];
+                    const double dz0 = X * dR[j * 9 + 6] + Y * dR[j * 9 + 7] + Z * dR[j * 9 + 8];
+                    ju[j] = fx * (z * (dx0 - x * dz0));
+                    jv[j] = fy * (z * (dy0 - y * dz0));
+                }
+                ju[3] = fx * z; ju[4] = 0; ju[5] = fx * (-x * z);
+                jv[3] = 0; jv[4] = fy * z; jv[5] = fy * (-y * z);
+                int k = 0;
+                for (int a = 0; a < 6; ++a)
+                    for (int b = a; b < 6; ++b) acc[k++] += ju[a] * ju[b] + jv[a] * jv[b];
+                for (int a = 0; a < 6; ++a) acc[21 + a] += ju[a] * eu + jv[a] * ev;
+            }
+        }
+        double e2 = 0;
+        const int nk = with_j ? 28 : 1;
+        for (int k = 0; k < nk; ++k) {
+            const int kk = with_j ? k : 27;
+            const double s = block_sum(acc[kk], s_red);
+            if (kk == 27) e2 = s;
+            else if (kk < 21) jtj[kk] = s;
+            else jte[kk - 21] = s;
+        }
+        return sqrt(e2);
+    };
+    // thread 0 solves (JtJ + lambda diag) x = JtErr; param = prev - x
+    auto step = [&](const double* jtj, const double* jte, int lam) {
+        if (tid == 0) {
+            double A[6][7];
+            int k = 0;
+            for (int a = 0; a < 6; ++a)
+                for (int b = a; b < 6; ++b) { A[a][b] = jtj[k]; A[b][a] = jtj[k]; ++k; }
+            const double l = exp(lam * log(10.0));
+            for (int a = 0; a < 6; ++a) { A[a][a] *= 1.0 + l; A[a][6] = jte[a]; }
+            for (int c = 0; c < 6; ++c) {  // Gaussian elimination, partial pivoting
+                int pv = c;
+                for (int r = c + 1; r < 6; ++r)
+                    if (fabs(A[r][c]) > fabs(A[pv][c])) pv = r;
+                if (pv != c)
+                    for (int j = 0; j < 7; ++j) { const double t = A[c][j]; A[c][j] = A[pv][j]; A[pv][j] = t; }
+                if (A[c][c] == 0.0) continue;
+                for (int r = c + 1; r < 6; ++r) {
+                    const double fct = A[r][c] / A[c][c];
+                    for (int j = c; j < 7; ++j) A[r][j] -= fct * A[c][j];
+                }
+            }
+            double x[6];
+            for (int r = 5; r >= 0; --r) {
+                double s = A[r][6];
+                for (int j = r + 1; j < 6; ++j) s -= A[r][j] * x[j];
+                x[r] = A[r][r] != 0.0 ? s / A[r][r] : 0.0;
+            }
+            for (int a = 0; a < 6; ++a) prm[a] = prev[a] - x[a];
+        }
+        __syncthreads();
+    };
+    double jtj[21], jte[6];
+    int lam = -3, iters = 0;
+    double prev_err = 0;
+    double err = eval(true, jtj, jte);
+    for (;;) {
+        if (tid < 6) prev[tid] = prm[tid];
+        __syncthreads();
+        step(jtj, jte, lam);
+        if (iters == 0) prev_err = err;
+        double err_norm;
+        for (;;) {
+            err_norm = eval(false, nullptr, nullptr);
+            if (err_norm > prev_err) {
+                ++lam;
+                if (lam <= 16) { step(jtj, jte, lam); continue; }
+            }
+            break;
+        }
+        lam = max(lam - 1, -16);
+        ++iters;
+        double dn = 0, pn = 0;
+        for (int a = 0; a < 6; ++a) { dn += (prm[a] - prev[a]) * (prm[a] - prev[a]); pn += prev[a] * prev[a]; }
+        if (iters >= 20 || sqrt(dn) < 1.1920928955078125e-07 * sqrt(pn)) break;
+        prev_err = err_norm;
+        err = eval(true, jtj, jte);
+    }
+    if (tid == 0) {
+        for (int k = 0; k < 3; ++k) { rvec_out[3 * p + k] = prm[k]; tvec_out[3 * p + k] = prm[3 + k]; }
+        ok_out[p] = 1; ninl_out[p] = maxgood; iters_out[p] = s_last + 1;
+    }
+    (void)s_flag;
+}
+
+}  // namespace
+}  // namespace sfmhip
+
+using namespace sfmhip;
+
+extern "C" int sfmhip_pnp_ransac(const double* obj, const double* img, const int64_t* offsets, int n_problems,
+                                 const double* cam, int iterations, double reprojection_error, double confidence,
+                                 float* work, double* rvec, double* tvec, uint8_t* inlier_mask, int32_t* n_inliers,
+                                 int32_t* iters, int32_t* ok, void* stream) {
+    SFMHIP_REQUIRE(n_problems >= 0, "pnp_ransac: n_problems < 0");
+    if (n_problems == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(obj && img && offsets && cam && work && rvec && tvec && inlier_mask && n_inliers && iters && ok,
+                   "pnp_ransac: null pointer");
+    SFMHIP_REQUIRE(reprojection_error > 0 && confidence >= 0 && confidence <= 1,
+                   "pnp_ransac: reprojection_error > 0, confidence in [0, 1]");
+    hipLaunchKernelGGL(pnp_ransac_kernel, dim3(n_problems), dim3(kPnThreads), 0, as_stream(stream), obj, img,
+                       offsets, cam, iterations, reprojection_error, confidence, work, rvec, tvec, inlier_mask,
+                       n_inliers, iters, ok);
+    return check_launch("pnp_ransac_kernel");
+}

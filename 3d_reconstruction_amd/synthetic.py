@@ -158,6 +158,36 @@ def two_view_pairs(n_pairs=256, n_pts=2048, outlier_frac=0.3, noise_px=0.5, seed
     return out
 
 
+def sfm_scene(n_img=6, n_pts=800, noise_px=0.3, wrong_frac=0.08, seed=8):
+    """Inputs of sfm.py's loop for a chain of pairs (0,1), (1,2), ...: every
+    image sees every point (keypoints in a per-image random order, centred
+    pixels, f32), all_matches[p] = [idx0, idx1, track ids] with a fraction of
+    wrong correspondences, random colours."""
+    rng = np.random.default_rng(seed)
+    Rs, ts = orbit_cameras(4 * n_img, seed=seed)
+    X = rng.uniform(-1, 1, (n_pts, 3))
+    perm, pts = [], []
+    for c in range(n_img):
+        pm = rng.permutation(n_pts)
+        Xc = X @ Rs[c].T + ts[c]
+        uv = Xc[:, :2] / Xc[:, 2:] * FOCAL + rng.normal(0, noise_px, (n_pts, 2))
+        kp = np.empty((n_pts, 2), np.float32)
+        kp[pm] = uv                                   # keypoint pm[g] is point g
+        pts.append(kp)
+        perm.append(pm)
+    img_pairs, all_matches = [], []
+    for c in range(n_img - 1):
+        g = rng.permutation(n_pts)[: int(0.9 * n_pts)]
+        idx0, idx1 = perm[c][g], perm[c + 1][g].copy()
+        wrong = rng.random(len(g)) < wrong_frac
+        idx1[wrong] = rng.integers(0, n_pts, int(wrong.sum()))
+        img_pairs.append((c, c + 1))
+        all_matches.append([idx0.astype(np.int64), idx1.astype(np.int64), g.astype(np.int64)])
+    colors = [rng.integers(0, 256, (n_pts, 3)).astype(np.uint8) for _ in range(n_img)]
+    return dict(img_pairs=img_pairs, all_matches=all_matches, all_points=pts, all_colors=colors, X=X,
+                R=Rs[:n_img], t=ts[:n_img])
+
+
 # ---------------------------------------------------------------------------
 SPHERES = ((0.0, -0.2, 0.0, 0.45), (0.5, 0.1, 0.3, 0.25), (-0.45, 0.0, -0.35, 0.3))
 FLOOR_Y = -0.6

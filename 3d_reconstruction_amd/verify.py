@@ -172,3 +172,58 @@ class EssentialVerifier:
             b = np.asarray(self.points[nid])[idx1].astype(np.float32)
             n = essential_inliers(a, b, self.K, self.prob, self.threshold)
         return None if n < 0 else n
+
+
+SOLVEPNP_ITERATIVE = 0   # cv2.SOLVEPNP_ITERATIVE
+
+
+def pnp_ransac_batched(obj: torch.Tensor, img: torch.Tensor, offsets: torch.Tensor, cam, iterations: int = 100,
+                       reprojection_error: float = 8.0, confidence: float = 0.99) -> dict:
+    """Device (N,3) / (N,2) f64 correspondences, offsets (P+1,) int64, cam (P,4) or (4,).
+    Returns device rvec (P,3), tvec (P,3), mask (N,) u8, n_inliers, iters, ok (P,)."""
+    X = dev(obj, torch.float64)
+    u = dev(img, torch.float64)
+    of = dev(offsets, torch.int64)
+    P = of.numel() - 1
+    N = X.shape[0]
+    c = dev(np.broadcast_to(np.asarray(cam.cpu() if isinstance(cam, torch.Tensor) else cam, np.float64),
+                            (P, 4)).copy(), torch.float64)
+    d = X.device
+    out = dict(rvec=torch.empty((P, 3), dtype=torch.float64, device=d),
+               tvec=torch.empty((P, 3), dtype=torch.float64, device=d),
+               mask=torch.empty(N, dtype=torch.uint8, device=d),
+               n_inliers=torch.empty(P, dtype=torch.int32, device=d),
+               iters=torch.empty(P, dtype=torch.int32, device=d),
+               ok=torch.empty(P, dtype=torch.int32, device=d))
+    work = torch.empty((max(N, 1), 5), dtype=torch.float32, device=d)
+    call("sfmhip_pnp_ransac", ptr(X), ptr(u), ptr(of), P, ptr(c), int(iterations), float(reprojection_error),
+         float(confidence), ptr(work), ptr(out["rvec"]), ptr(out["tvec"]), ptr(out["mask"]), ptr(out["n_inliers"]),
+         ptr(out["iters"]), ptr(out["ok"]), stream_ptr())
+    return out
+
+
+def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs=None, rvec=None, tvec=None,
+                   useExtrinsicGuess: bool = False, iterationsCount: int = 100, reprojectionError: float = 8.0,
+                   confidence: float = 0.99, inliers=None, flags: int = SOLVEPNP_ITERATIVE):
+    """cv2.solvePnPRansac (sfm.py:116) -> (retval, rvec (3,1), tvec (3,1), inliers (k,1) int32).
+    ``rvec``/``tvec`` are outputs only (the reference passes SOLVEPNP_ITERATIVE
+    positionally as rvec); distortion must be absent or zero."""
+    if distCoeffs is not None and np.any(np.asarray(distCoeffs) != 0):
+        raise NotImplementedError("non-zero distortion is not part of the reference's call")
+    if useExtrinsicGuess:
+        raise NotImplementedError("useExtrinsicGuess=True is not part of the reference's call")
+    if flags != SOLVEPNP_ITERATIVE:
+        raise NotImplementedError("only SOLVEPNP_ITERATIVE (the reference's call) is implemented")
+    X = np.asarray(objectPoints, np.float64).reshape(-1, 3)
+    m = np.asarray(imagePoints, np.float64).reshape(-1, 2)
+    if len(X) != len(m):
+        raise ValueError("objectPoints and imagePoints must have the same number of points")
+    if len(X) < 5:
+        raise NotImplementedError("fewer than 5 points (OpenCV switches to P3P at 4)")
+    require_gpu()
+    offs = torch.tensor([0, len(X)], dtype=torch.int64)
+    r = pnp_ransac_batched(X, m, offs, _cam(cameraMatrix), iterationsCount, reprojectionError, confidence)
+    if not int(r["ok"][0]):
+        return False, None, None, None
+    inl = np.nonzero(r["mask"].cpu().numpy())[0].astype(np.int32).reshape(-1, 1)
+    return True, r["rvec"][0].cpu().numpy().reshape(3, 1), r["tvec"][0].cpu().numpy().reshape(3, 1), inl

@@ -354,6 +354,60 @@ def train_line(sfm, syn, device, args, barrier, cpu=True):
     return line
 
 
+def pnp_line(sfm, syn, device, args, barrier, cpu=True):
+    """sfm.py:116 solvePnPRansac batched: 256 registrations x 2000 2D-3D
+    correspondences (30 % outliers, 0.5 px noise), EPnP RANSAC + LM refine."""
+    from oracle import geometry as og
+    v = sfm.verify
+    rng = np.random.default_rng(12)
+    K = np.diag([syn.FOCAL, syn.FOCAL, 1.0])
+    P, n = 256, 2000
+    Xs, uvs = [], []
+    for _ in range(P):
+        rv = rng.normal(0, 0.2, 3)
+        t = np.array([rng.normal(0, 0.3), rng.normal(0, 0.3), 5.0 + rng.random()])
+        X = rng.uniform(-1, 1, (n, 3))
+        uv = og.project_points(X, rv, t, K) + rng.normal(0, 0.5, (n, 2))
+        bad = rng.random(n) < 0.3
+        uv[bad] = rng.uniform(-900, 900, (int(bad.sum()), 2))
+        Xs.append(X)
+        uvs.append(uv)
+    Xd = torch.tensor(np.concatenate(Xs), device=device)
+    ud = torch.tensor(np.concatenate(uvs), device=device)
+    of = torch.tensor(np.arange(P + 1, dtype=np.int64) * n, device=device)
+    cam = torch.tensor(v._cam(K), device=device).expand(P, 4).contiguous()
+    holder = {}
+
+    def step(record):
+        e0 = e1 = None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        holder["r"] = v.pnp_ransac_batched(Xd, ud, of, cam)
+        if record:
+            e1.record()
+        return (e0, e1)
+
+    wall, kms = timed(step, args.steps, 1, barrier)
+    ms = wall / args.steps * 1e3
+    line = {"metric": "PnP registrations/sec", "value": P / (ms * 1e-3), "unit": "registrations/s",
+            "ms_per_step": ms,
+            "config": {"workload": "solvePnPRansac (sfm.py:116: 100 iters, 8 px, 0.99) + LM refine: 256 problems x "
+                                   "2000 correspondences, 30% outliers",
+                       "mean_ransac_iters": holder["r"]["iters"].float().mean().item()},
+            "roofline": {"bound": "fp64", "kernel": "pnp_ransac_kernel", "kernel_ms": float(np.mean(kms))}}
+    if cpu:
+        from oracle import pnp as opnp
+        t0 = time.perf_counter()
+        for k in range(4):
+            opnp.solve_pnp_ransac(Xs[k], uvs[k], K)
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": 4 / dt, "unit": "registrations/s", "cores": 1, "kind": "port",
+                                "sample": f"4 of the 256 problems through oracle.pnp (numpy restatement of "
+                                          f"OpenCV's solvePnPRansac), {dt:.2f}s"}
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -547,6 +601,7 @@ def main():
         result["secondary"].extend(voxel_and_vq_lines(sfm, syn, device, args, barrier,
                                                       cpu=(not args.no_cpu_baseline)))
         result["secondary"].append(verify_line(sfm, syn, device, args, barrier, cpu=(not args.no_cpu_baseline)))
+        result["secondary"].append(pnp_line(sfm, syn, device, args, barrier, cpu=(not args.no_cpu_baseline)))
         result["secondary"].append(train_line(sfm, syn, device, args, barrier, cpu=(not args.no_cpu_baseline)))
 
     # ---------------- CPU baseline (rank 0, N=1 only) ------------------------

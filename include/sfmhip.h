@@ -204,6 +204,20 @@ int sfmhip_recover_pose(const double* E, int64_t e_stride, const double* pts0, c
                         const uint8_t* mask_in, double distance_thresh, double* R, double* t,
                         uint8_t* mask_out, int32_t* n_good, void* stream);
 
+/* cv2.solvePnPRansac(X, pts1, K, zeros(5,1), cv2.SOLVEPNP_ITERATIVE) at
+ * sfm.py:116 (iterationsCount 100, reprojectionError 8, confidence 0.99):
+ * points converted to float, cv::RNG(-1) 5-point samples solved by EPnP,
+ * float squared reprojection error <= reprojectionError^2, the RANSAC pose
+ * refined on its inliers by CvLevMarq (20 iterations).  Problem p owns rows
+ * [offsets[p], offsets[p+1]) of obj ([N][3] f64) / img ([N][2] f64 pixels);
+ * cam [n][4] = fx, fy, cx, cy; work [N][5] f32 scratch.  Out: rvec/tvec
+ * [n][3], inlier_mask [N] u8 (RANSAC inliers), n_inliers, iters, ok.
+ * n < 5 is reported as ok = 0 (OpenCV would use P3P at n == 4).           */
+int sfmhip_pnp_ransac(const double* obj, const double* img, const int64_t* offsets, int n_problems,
+                      const double* cam, int iterations, double reprojection_error, double confidence,
+                      float* work, double* rvec, double* tvec, uint8_t* inlier_mask, int32_t* n_inliers,
+                      int32_t* iters, int32_t* ok, void* stream);
+
 /* ---- §8f row 4: one grid training step (plenoxel.py:100-111, sdf.py:427-438)
  * Fused render forward + mse_loss(gt, rgb) gradient + analytic backward +
  * trilinear scatter-add into grad_vm (voxel-major (D,H,W,32), accumulated;

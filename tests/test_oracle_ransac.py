@@ -92,3 +92,40 @@ def test_ransac_edge_counts():
     assert orc.find_essential_mat(x1[:4], x2[:4], K) == (None, None)
     E, m = orc.find_essential_mat(x1, x2, K)
     assert E.shape[0] % 3 == 0 and E.shape[1] == 3 and (m == 1).all()
+
+
+# --- solvePnPRansac restatement (oracle/pnp.py) ---------------------------------
+def test_epnp_exact_and_pnp_ransac_known_answer():
+    from oracle import pnp as opnp
+    rng = np.random.default_rng(4)
+    f = 2378.98305085
+    K = np.array([[f, 0, 0], [0, f, 0], [0, 0, 1.0]])
+    rv, t = np.array([0.1, -0.2, 0.05]), np.array([0.3, -0.1, 5.0])
+    X = rng.uniform(-1, 1, (300, 3))
+    uv = og.project_points(X, rv, t, K)
+    R, tt = opnp.EPnP(K, X[:6], uv[:6]).compute_pose()          # noise-free EPnP is exact
+    np.testing.assert_allclose(R, og.rodrigues(rv), atol=1e-12)
+    np.testing.assert_allclose(tt, t, atol=1e-11)
+    bad = rng.random(300) < 0.3
+    uv[bad] = rng.uniform(-900, 900, (int(bad.sum()), 2))
+    ok, r, tv, inl = opnp.solve_pnp_ransac(X, uv, K)
+    assert ok and set(np.nonzero(~bad)[0]) <= set(inl.ravel())
+    np.testing.assert_allclose(r.ravel(), rv, atol=1e-6)
+    np.testing.assert_allclose(tv.ravel(), t, atol=1e-5)
+
+
+def test_projection_jacobian_matches_finite_differences():
+    from oracle import pnp as opnp
+    rng = np.random.default_rng(5)
+    K = np.diag([2000.0, 2100.0, 1.0])
+    X = rng.uniform(-1, 1, (20, 3)) + [0, 0, 6]
+    p = np.array([0.11, -0.2, 0.07, 0.3, -0.2, 0.5])
+    proj, J = opnp.project_with_jacobian(X, p, K)
+    Jn = np.zeros_like(J)
+    for k in range(6):
+        h = 1e-6
+        pp, pm = p.copy(), p.copy()
+        pp[k] += h
+        pm[k] -= h
+        Jn[:, k] = ((opnp.project_with_jacobian(X, pp, K)[0] - opnp.project_with_jacobian(X, pm, K)[0]) / (2 * h)).ravel()
+    assert np.abs(J - Jn).max() <= 1e-6 * np.abs(J).max()
