@@ -776,6 +776,60 @@ __global__ void from_vm_kernel(const float* __restrict__ vm, int C, int64_t nvox
     grid[e] = vm[(vx << 5) + c];
 }
 
+// ---------------------------------------------------------------------------
+// V3: GradientBasedSampler's effective output (sdf.py:154-180, 220-256): the
+// slab ray/AABB test and the stratified uniform samples (its importance
+// samples are computed and then discarded at sdf.py:251-252).  torch
+// semantics: NaN from 0 * inf propagates through min/max and makes the ray
+// invalid; linspace(0, 1, S) in f32 with torch's two-sided formula.
+__global__ void ray_aabb_kernel(const float* __restrict__ ro, const float* __restrict__ rd, int64_t B, Bounds bb,
+                                float* __restrict__ t_near, float* __restrict__ t_far, uint8_t* __restrict__ valid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    float tn = 0.f, tf = 0.f;
+    bool nan = false;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float inv = 1.0f / rd[3 * i + a];
+        const float t0 = (bb.mn[a] - ro[3 * i + a]) * inv;
+        const float t1 = (bb.mx[a] - ro[3 * i + a]) * inv;
+        nan = nan || (t0 != t0) || (t1 != t1);
+        const float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
+        tn = (a == 0) ? lo : fmaxf(tn, lo);
+        tf = (a == 0) ? hi : fminf(tf, hi);
+    }
+    if (nan) { tn = __int_as_float(0x7fc00000); tf = tn; }
+    tn = (tn != tn) ? tn : fmaxf(tn, 0.f);
+    t_near[i] = tn;
+    t_far[i] = tf;
+    valid[i] = (tf > tn) ? 1 : 0;
+}
+
+__device__ __forceinline__ float torch_linspace01(int k, int S) {
+    // start + step*k / end - step*(S-k-1), each a fused multiply-add as in the
+    // compiled torch kernel (bit-exact with torch.linspace(0, 1, S), f32)
+    const float step = (1.0f - 0.0f) / (float)(S - 1);
+    return (k < S / 2) ? fmaf(step, (float)k, 0.0f) : fmaf(-step, (float)(S - k - 1), 1.0f);
+}
+
+__global__ void stratified_kernel(const float* __restrict__ tn, const float* __restrict__ tf,
+                                  const float* __restrict__ t_rand, int64_t B, int S, int perturb,
+                                  float* __restrict__ z) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= B * S) return;
+    const int64_t r = e / S;
+    const int k = (int)(e - r * S);
+    auto zk = [&](int j) {
+        const float t = torch_linspace01(j, S);
+        return tn[r] * (1.0f - t) + tf[r] * t;
+    };
+    const float zc = zk(k);
+    if (!perturb) { z[e] = zc; return; }
+    const float lower = (k == 0) ? zc : 0.5f * (zc + zk(k - 1));
+    const float upper = (k == S - 1) ? zc : 0.5f * (zk(k + 1) + zc);
+    z[e] = lower + (upper - lower) * t_rand[e];
+}
+
 }  // namespace sfmhip
 
 using namespace sfmhip;
@@ -979,4 +1033,24 @@ extern "C" int sfmhip_adam_step(float* param, float* grad, float* exp_avg, float
                        reinterpret_cast<v4f*>(grad), reinterpret_cast<v4f*>(exp_avg),
                        reinterpret_cast<v4f*>(exp_avg_sq), n4, w1, b2, s2, bc2s, (float)eps, stp, zero_grad);
     return check_launch("adam_kernel");
+}
+
+extern "C" int sfmhip_ray_aabb(const float* rays_o, const float* rays_d, int64_t B, const float* bmin,
+                               const float* bmax, float* t_near, float* t_far, uint8_t* valid, void* stream) {
+    SFMHIP_REQUIRE(rays_o && rays_d && bmin && bmax && t_near && t_far && valid, "sfmhip_ray_aabb: null pointer");
+    SFMHIP_REQUIRE(B >= 0, "sfmhip_ray_aabb: B < 0");
+    if (B == 0) return SFMHIP_OK;
+    hipLaunchKernelGGL(ray_aabb_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, as_stream(stream), rays_o, rays_d, B,
+                       make_bounds(bmin, bmax), t_near, t_far, valid);
+    return check_launch("ray_aabb_kernel");
+}
+
+extern "C" int sfmhip_stratified_samples(const float* t_near, const float* t_far, const float* t_rand, int64_t B,
+                                         int S, int perturb, float* z, void* stream) {
+    SFMHIP_REQUIRE(t_near && t_far && z && (t_rand || !perturb), "sfmhip_stratified_samples: null pointer");
+    SFMHIP_REQUIRE(B >= 0 && S >= 2, "sfmhip_stratified_samples: bad shape");
+    if (B == 0) return SFMHIP_OK;
+    hipLaunchKernelGGL(stratified_kernel, dim3(ceil_div(B * S, 256)), dim3(256), 0, as_stream(stream), t_near, t_far,
+                       t_rand, B, S, perturb, z);
+    return check_launch("stratified_kernel");
 }

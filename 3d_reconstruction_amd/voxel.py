@@ -8,6 +8,9 @@
   ``SDFGrid.forward`` / ``render_rays`` (``sdf.py:391-406``,
   ``plenoxel.py:71-93``) for a given sample set ``z`` (the reference draws it
   with ``torch.rand``; callers pass it explicitly).
+* :func:`ray_aabb`, :func:`sample_uniform` and :meth:`VoxelGrid.sdf_forward` —
+  ``GradientBasedSampler`` (sdf.py:154-180, 220-256; its importance samples
+  are discarded by the reference at 251-252) + ``SDFGrid.forward``.
 * :func:`tsdf_integrate` — TSDF fusion of depth maps into a (D,H,W) grid laid
   out like the ``sdf.py`` grid (build-defined).
 """
@@ -47,6 +50,36 @@ def voxel_traversal(rays: torch.Tensor, _bin_size, max_steps: int = 1 << 20) -> 
     out = torch.empty((N, S, 3), dtype=torch.float32, device=r.device)
     call("sfmhip_voxel_traversal", ptr(r), N, b, S, ptr(out), stream_ptr())
     return out
+
+
+def ray_aabb(rays_o: torch.Tensor, rays_d: torch.Tensor, min_bound, max_bound):
+    """sdf.py:154-165 -> (t_near (B,), t_far (B,), valid (B,) bool) device tensors."""
+    require_gpu()
+    o = dev(rays_o, torch.float32).reshape(-1, 3)
+    d = dev(rays_d, torch.float32).reshape(-1, 3)
+    B = o.shape[0]
+    tn = torch.empty(B, dtype=torch.float32, device=o.device)
+    tf = torch.empty_like(tn)
+    valid = torch.empty(B, dtype=torch.uint8, device=o.device)
+    call("sfmhip_ray_aabb", ptr(o), ptr(d), B, _host_ptr(_f3(min_bound)), _host_ptr(_f3(max_bound)), ptr(tn),
+         ptr(tf), ptr(valid), stream_ptr())
+    return tn, tf, valid.bool()
+
+
+def sample_uniform(t_near: torch.Tensor, t_far: torch.Tensor, num_samples: int, t_rand=None,
+                   perturb: bool = True) -> torch.Tensor:
+    """sdf.py:167-180: stratified samples (B, S); ``t_rand`` (B, S) is the jitter
+    the reference draws with torch.rand_like (drawn here when omitted)."""
+    tn = dev(t_near, torch.float32)
+    tf = dev(t_far, torch.float32)
+    B = tn.shape[0]
+    if perturb and t_rand is None:
+        t_rand = torch.rand((B, num_samples), device=tn.device)
+    tr = dev(t_rand, torch.float32) if perturb else None
+    z = torch.empty((B, num_samples), dtype=torch.float32, device=tn.device)
+    call("sfmhip_stratified_samples", ptr(tn), ptr(tf), ptr(tr), B, int(num_samples), 1 if perturb else 0,
+         ptr(z), stream_ptr())
+    return z
 
 
 class VoxelGrid:
@@ -95,6 +128,20 @@ class VoxelGrid:
                  stream_ptr())
             self._vm = vm
         return self._vm
+
+    def sdf_forward(self, rays_o, rays_d, num_samples: int = 160, t_rand=None, perturb: bool = True):
+        """SDFGrid.forward (sdf.py:391-406) with its sampler (sdf.py:220-256):
+        -> (rgb (Bv,3), pts (Bv,S,3), valid (B,) bool)."""
+        o = dev(rays_o, torch.float32).reshape(-1, 3)
+        d = dev(rays_d, torch.float32).reshape(-1, 3)
+        tn, tf, valid = ray_aabb(o, d, self.bmin, self.bmax)
+        if not bool(valid.any()):
+            raise ValueError("No valid rays intersect the grid.")
+        idx = torch.nonzero(valid).squeeze(1)
+        ov, dv = o[idx].contiguous(), d[idx].contiguous()
+        z = sample_uniform(tn[idx].contiguous(), tf[idx].contiguous(), num_samples, t_rand, perturb)
+        pts = ov[:, None, :] + dv[:, None, :] * z[:, :, None]
+        return self.render(ov, dv, z), pts, valid
 
     def render(self, rays_o: torch.Tensor, rays_d: torch.Tensor, z: torch.Tensor) -> torch.Tensor:
         """Fused sample + SH colour + composite for sorted sample depths z (B,S): (B,3)."""

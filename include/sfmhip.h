@@ -239,6 +239,17 @@ int sfmhip_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_s
 int sfmhip_grid_from_voxel_major(const float* grid_vm, int C, int D, int H, int W, float* grid,
                                  void* stream);
 
+/* ---- V3: GradientBasedSampler's effective samples (sdf.py:154-180, 251-256)
+ * Slab ray/AABB test: t_near = max(max_a min(t0, t1), 0), t_far = min_a max(t0,
+ * t1), valid = t_far > t_near (NaN rays invalid).  Bounds are HOST float[3]. */
+int sfmhip_ray_aabb(const float* rays_o, const float* rays_d, int64_t B, const float* bmin,
+                    const float* bmax, float* t_near, float* t_far, uint8_t* valid, void* stream);
+
+/* Stratified uniform samples (sample_uniform, sdf.py:167-180): z = t_near (1-t)
+ * + t_far t with t = linspace(0,1,S); perturb: lower + (upper-lower) t_rand.  */
+int sfmhip_stratified_samples(const float* t_near, const float* t_far, const float* t_rand, int64_t B,
+                              int S, int perturb, float* z, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

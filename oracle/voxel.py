@@ -200,3 +200,47 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
     T[z0:z1] = Ts
     Wt[z0:z1] = Ws
     return T, Wt
+
+
+# ---------------------------------------------------------------------------
+def ray_aabb(rays_o, rays_d, bmin, bmax):
+    """GradientBasedSampler.ray_aabb_intersection (sdf.py:154-165), f32, NaN-propagating."""
+    o = np.asarray(rays_o, F32).reshape(-1, 3)
+    d = np.asarray(rays_d, F32).reshape(-1, 3)
+    mn = np.asarray(bmin, F32).ravel()
+    mx = np.asarray(bmax, F32).ravel()
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = (F32(1.0) / d).astype(F32)
+        t0 = ((mn - o) * inv).astype(F32)
+        t1 = ((mx - o) * inv).astype(F32)
+    tn = np.max(np.minimum(t0, t1), axis=-1)
+    tf = np.min(np.maximum(t0, t1), axis=-1)
+    tn = np.maximum(tn, F32(0))
+    with np.errstate(invalid="ignore"):
+        valid = tf > tn
+    return tn.astype(F32), tf.astype(F32), valid
+
+
+def torch_linspace01(S):
+    """torch.linspace(0, 1, S) f32 (RangeFactoriesKernel.cpp): start + step*k for
+    k < S/2, end - step*(S-k-1) after, each a fused multiply-add (the compiled
+    kernel contracts it; emulated in f64, the product is exact)."""
+    step = F32(1.0) / F32(S - 1)
+    k = np.arange(S)
+    lo = (np.float64(step) * k).astype(F32)
+    hi = (1.0 - np.float64(step) * (S - k - 1)).astype(F32)
+    return np.where(k < S // 2, lo, hi).astype(F32)
+
+
+def sample_uniform(t_near, t_far, S, t_rand=None):
+    """GradientBasedSampler.sample_uniform (sdf.py:167-180) with the jitter given."""
+    t = torch_linspace01(S)
+    tn = np.asarray(t_near, F32)[:, None]
+    tf = np.asarray(t_far, F32)[:, None]
+    z = (tn * (F32(1) - t) + tf * t).astype(F32)
+    if t_rand is None:
+        return z
+    mids = (F32(0.5) * (z[:, 1:] + z[:, :-1])).astype(F32)
+    upper = np.concatenate([mids, z[:, -1:]], 1)
+    lower = np.concatenate([z[:, :1], mids], 1)
+    return (lower + (upper - lower) * np.asarray(t_rand, F32)).astype(F32)

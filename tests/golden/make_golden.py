@@ -442,6 +442,39 @@ def gen_train():
     save("train_golden.npz", **out)
 
 
+def gen_sdf_sampler():
+    """SDFGrid.forward (sdf.py:391-406) with the GradientBasedSampler's perturbed
+    stratified samples (sdf.py:220-256): rays that miss the box, start inside it
+    or have a zero direction component; the jitter t_rand (torch.rand_like at
+    sdf.py:176) is captured by re-seeding."""
+    sys.modules.setdefault("cv2", types.ModuleType("cv2"))
+    sd = load("ref_sdf_sampler", os.path.join(REF, "sdf.py"))
+    torch.manual_seed(33)
+    res = (9, 10, 11)
+    mn, mx = (-2, -1, -3), (3, 2, 1)
+    model = sd.SDFGrid(res, mn, mx, "cpu")
+    with torch.no_grad():
+        model.grid.copy_(torch.randn_like(model.grid) * 0.5)
+    rng = np.random.default_rng(33)
+    B = 48
+    ro = (np.array([0.5, 0.2, 6.0]) + rng.normal(0, 1.5, (B, 3))).astype(np.float32)
+    tgt = rng.uniform([-2.5, -1.5, -3.5], [3.5, 2.5, 1.5], (B, 3)).astype(np.float32)
+    ro[:4] = rng.uniform([-1, 0, -2], [2, 1, 0], (4, 3))          # origins inside the box
+    rd = tgt - ro
+    rd[4, 0] = 0.0                                                  # zero direction components
+    rd[5, 1] = 0.0
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    ro_t, rd_t = torch.from_numpy(ro), torch.from_numpy(rd)
+    t_near, t_far, valid = model.sampler.ray_aabb_intersection(ro_t, rd_t, model.min_bound, model.max_bound)
+    torch.manual_seed(34)
+    c, pts, valid2 = model(ro_t, rd_t)
+    torch.manual_seed(34)
+    t_rand = torch.rand((int(valid.sum()), model.sampler.num_samples))
+    save("sdf_sampler_golden.npz", grid=model.grid.detach().numpy(), bmin=np.array(mn, np.float32),
+         bmax=np.array(mx, np.float32), rays_o=ro, rays_d=rd, t_near=t_near.numpy(), t_far=t_far.numpy(),
+         valid=valid.numpy(), t_rand=t_rand.numpy(), pts=pts.detach().numpy(), rgb=c.detach().numpy())
+
+
 if __name__ == "__main__":
     gen_vq()
     gen_filter_matches()
@@ -453,3 +486,4 @@ if __name__ == "__main__":
     gen_bfs()
     gen_sfm_triangulate()
     gen_train()
+    gen_sdf_sampler()

@@ -189,3 +189,16 @@ def test_train_oracle_matches_reference_torch():
         assert (grid == g[f"grid{step}"][0]).mean() > 0.999
         assert np.abs(grid - g[f"grid{step}"][0]).max() <= 3e-8
     assert np.array_equal(m, g["exp_avg2"][0]) and np.array_equal(v, g["exp_avg_sq2"][0])
+
+
+# --- V3: the SDF sampler's effective samples -----------------------------------------
+def test_sdf_sampler_oracle_matches_reference():
+    g = golden("sdf_sampler_golden.npz")
+    tn, tf, va = ov.ray_aabb(g["rays_o"], g["rays_d"], g["bmin"], g["bmax"])
+    assert np.array_equal(va, g["valid"])
+    assert np.array_equal(tn[va], g["t_near"][va]) and np.array_equal(tf[va], g["t_far"][va])
+    z = ov.sample_uniform(tn[va], tf[va], 160, g["t_rand"])
+    pts = g["rays_o"][va][:, None, :] + g["rays_d"][va][:, None, :] * z[:, :, None]
+    assert np.array_equal(pts, g["pts"])                                    # bit-exact incl. torch.linspace
+    rgb = ov.render(g["grid"], g["bmin"], g["bmax"], 0, g["rays_o"][va], g["rays_d"][va], z)
+    np.testing.assert_allclose(rgb, g["rgb"], rtol=1e-5, atol=1e-5)
