@@ -352,7 +352,7 @@ template <> struct TsdfTile<3> { static constexpr int X = 64, Y = 1, Z = 4; };
 // (64 x 64 x 16 voxels for MAP 0).  Workgroups resident on one XCD at the same
 // time then project onto one compact image region per frame, so the depth
 // lines they gather stay in that XCD's L2 (speed only, never correctness).
-struct SuperBrick { int x, y, z; };   // super-brick extent in bricks (default 4 x 4 x 16: 64 x 16 x 64 voxels, measured best)
+struct SuperBrick { int x, y, z; };   // super-brick extent in bricks (default 2 x 4 x 8: 32 x 16 x 32 voxels, measured best)
 
 template <int MAP, int U, bool SWZ>
 __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float* __restrict__ Wt, int D, int H,
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
         by = sy * kSbY + (in / kSbX) % kSbY;
         bz = sz * kSbZ + in / (kSbX * kSbY);
     }
-    __shared__ float cam[kTsdfMaxFrames * 16];
+    extern __shared__ float cam[];  // F x 16 (dynamic: a static 512-frame array capped occupancy at 5 waves)
     for (int t = threadIdx.x; t < F * 16; t += blockDim.x) {
         const int f = t >> 4, q = t & 15;
         cam[t] = (q < 12) ? poses[f * 12 + q] : Kf[f * 4 + (q - 12)];
@@ -938,9 +938,9 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     const int map = env_int("SFMHIP_TSDF_MAP", 0);
     const int unroll = env_int("SFMHIP_TSDF_U", 4);
     const int swz = env_int("SFMHIP_TSDF_SWZ", 1);
-    const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 4)), std::max(1, env_int("SFMHIP_TSDF_SBY", 4)),
-                        std::max(1, env_int("SFMHIP_TSDF_SBZ", 16))};
-    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", 32)));
+    const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 2)), std::max(1, env_int("SFMHIP_TSDF_SBY", 4)),
+                        std::max(1, env_int("SFMHIP_TSDF_SBZ", 8))};
+    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", 24)));
     static const int tx[4] = {16, 16, 8, 64}, ty[4] = {4, 4, 4, 1}, tz[4] = {4, 4, 8, 4};
     const int mi = swz ? 0 : ((map >= 0 && map < 4) ? map : 0);
     const int nbx = ceil_div(W, tx[mi]), nby = ceil_div(H, ty[mi]), nbz = ceil_div(z1 - z0, tz[mi]);
@@ -959,7 +959,8 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
         const float* kp = Kf + (size_t)f0 * 4;
         const Bounds bb = make_bounds(bmin, bmax);
 #define SFMHIP_TSDF(MM, UU, SS)                                                                              \
-    hipLaunchKernelGGL((tsdf_kernel<MM, UU, SS>), grid, dim3(256), 0, as_stream(stream), T, Wt, D, H, W, z0, \
+    hipLaunchKernelGGL((tsdf_kernel<MM, UU, SS>), grid, dim3(256), (size_t)nf * 16 * sizeof(float),             \
+                       as_stream(stream), T, Wt, D, H, W, z0,                                                 \
                        z1, dp, nf, Hd, Wd, pp, kp, bb, trunc, sb)
 #define SFMHIP_TSDF_M(MM)                          \
     switch (unroll) {                              \
