@@ -72,6 +72,7 @@ SIGNATURES = {
     "sfmhip_grid_from_voxel_major": [_p, _i32, _i32, _i32, _i32, _p, _p],
     "sfmhip_ray_aabb": [_p, _p, _i64, _p, _p, _p, _p, _p, _p],
     "sfmhip_stratified_samples": [_p, _p, _p, _i64, _i32, _i32, _p, _p],
+    "sfmhip_debug_ransac_prof": [_p],
 }
 
 

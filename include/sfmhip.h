@@ -250,6 +250,10 @@ int sfmhip_ray_aabb(const float* rays_o, const float* rays_d, int64_t B, const f
 int sfmhip_stratified_samples(const float* t_near, const float* t_far, const float* t_rand, int64_t B,
                               int S, int perturb, float* z, void* stream);
 
+/* Debug: phase timers of essential_ransac_kernel (tools/prof_ransac.py); all
+ * zero unless the library is built with -DSFMHIP_RANSAC_PROF.  out[16].       */
+int sfmhip_debug_ransac_prof(unsigned long long* out);
+
 #ifdef __cplusplus
 }
 #endif
