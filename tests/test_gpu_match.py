@@ -170,3 +170,20 @@ def test_vq_gpu_golden(sfm, gpu):
     codes, dist = sfm.vq(g["obs_f"], g["code_f"])
     assert (codes == g["codes_f"]).mean() > 0.99
     np.testing.assert_allclose(dist, g["dist_f"], rtol=1e-12)
+
+
+
+def test_match_empty_and_single_keypoint_images(sfm, gpu):
+    """Images with 0 and 1 keypoints: no candidate or no second-best -> -1 rows."""
+    x = syn.superpoint_like(3, 300, 128, seed=77).numpy()
+    nk = np.array([0, 1, 300], np.int32)
+    for i in range(3):
+        x[i, nk[i]:] = 0
+    pairs = np.array([[0, 2], [2, 0], [1, 2], [2, 1], [0, 1]], np.int32)
+    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=1)
+    m0 = bank.match(pairs, ratio=0.75).cpu().numpy()
+    q = om.quantize(x, 1)
+    ref, _, _ = _oracle_pairs(q, nk, pairs, (3, 4))
+    assert np.array_equal(m0[:, :300], ref[:, :300])
+    assert (m0[1] == -1).all() and (m0[3] == -1).all()       # B empty / single candidate
+    assert (m0[:, 300:] == -1).all()                          # padding rows never match
