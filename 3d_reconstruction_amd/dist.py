@@ -55,3 +55,60 @@ def allgather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tenso
         rl, rh = shard_range(n_total, r, world)
         parts.append(recv[r * per: r * per + (rh - rl)])
     return torch.cat(parts, 0)
+
+
+def chunk_rows(n: int, rank: int, world: int, chunks: int) -> list[tuple[int, int]]:
+    """Global row ranges of ``rank`` under the chunk-major layout of
+    :func:`overlapped_allgather`: chunk c covers rows [c*world*per,
+    (c+1)*world*per) and rank r owns [c*world*per + r*per, ... + per) of it
+    (clipped to n), with per = ceil(n / (world*chunks))."""
+    per = -(-int(n) // (int(world) * int(chunks))) if n else 0
+    out = []
+    for c in range(chunks):
+        lo = c * world * per + rank * per
+        out.append((min(lo, n), min(lo + per, n)))
+    return out
+
+
+def overlapped_allgather(compute, n: int, row_shape, dtype, device, chunks: int = 4, group=None,
+                         after_compute=None) -> torch.Tensor:
+    """Compute this rank's rows chunk by chunk and all-gather each chunk while
+    the next one computes (one collective per chunk on a side stream, so the
+    match kernels and the RCCL transfers overlap on the GPU).
+
+    ``compute(lo, hi, out)`` fills ``out`` (rows [lo, hi) of the global array,
+    shape (hi-lo,) + row_shape) on the current stream; ``after_compute()`` (if
+    given) runs once the last chunk is enqueued, before the collectives are
+    waited for.  Returns the full (n,) + row_shape array on every rank, rows
+    in global order."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    per = -(-int(n) // (world * chunks)) if n else 0
+    row_shape = tuple(row_shape)
+    out = torch.empty((chunks * world * per,) + row_shape, dtype=dtype, device=device)
+    use_streams = out.is_cuda and dist.get_backend(group) == "nccl"
+    comm = torch.cuda.Stream(device=device) if use_streams else None
+    sends, works = [], []
+    for c, (lo, hi) in enumerate(chunk_rows(n, rank, world, chunks)):
+        send = torch.zeros((per,) + row_shape, dtype=dtype, device=device)
+        if hi > lo:
+            compute(lo, hi, send[: hi - lo])
+        dst = out[c * world * per:(c + 1) * world * per]
+        if use_streams:
+            ev = torch.cuda.Event()
+            ev.record()
+            with torch.cuda.stream(comm):
+                comm.wait_event(ev)
+                works.append(dist.all_gather_into_tensor(dst.view(-1).view(torch.uint8),
+                                                         send.view(-1).view(torch.uint8), group=group,
+                                                         async_op=True))
+        else:   # gloo (tests): byte view, host tensors
+            dist.all_gather_into_tensor(dst.view(-1).view(torch.uint8), send.view(-1).view(torch.uint8),
+                                        group=group)
+        sends.append(send)
+    if after_compute is not None:
+        after_compute()
+    for w in works:
+        w.wait()            # the current stream waits for every chunk's collective
+    del sends
+    return out[:n]

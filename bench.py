@@ -38,6 +38,7 @@ TSDF_R, TSDF_F = 256, 257
 BA_PAIRS, BA_OBS = 256, 4096
 PEAK_INT8_TOPS = 5000.0       # MI355X dense int8 MFMA (MI355X_MICROARCH.md: 2x bf16 2.5 PF)
 PEAK_HBM_GBS = 8000.0         # HBM3E spec
+MATCH_CHUNKS = 4              # N>1 (RCCL): match launches per step, each overlapped with the previous all-gather
 PEAK_FP32_TFLOPS = 157.3      # vector fp32
 PEAK_FP64_TFLOPS = 78.6       # vector fp64
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1", "traffic.json")
@@ -417,6 +418,8 @@ def main():
     ap.add_argument("--skip-secondary", action="store_true")
     ap.add_argument("--n-img", type=int, default=N_IMG)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for rehearsal")
+    ap.add_argument("--rehearse-overlap", action="store_true",
+                    help="N=1 rehearsal of the N>1 RCCL path: a single-rank NCCL group + the overlapped all-gather")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -426,6 +429,10 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
+    if args.rehearse_overlap and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=device)
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
@@ -450,17 +457,34 @@ def main():
         f"{n_img}x{M_KPT}x{DIM} int8 = {bank.q.numel() / 1e6:.0f} MB")
     pairs_all = sfm.all_pairs(n_img)
     P = len(pairs_all)
-    lo, hi = sdist.shard_range(P, rank, world)
-    pairs_local = torch.from_numpy(pairs_all[lo:hi]).to(device)
-    m0 = torch.empty((hi - lo, bank.m_pad), dtype=torch.int32, device=device)
-    m16 = torch.empty((hi - lo, bank.m_pad), dtype=torch.int16, device=device)
     num, den = 3, 4
+    overlap = (world > 1 and args.dist_backend == "nccl") or args.rehearse_overlap
+    if overlap:
+        # chunk-major pair layout: each chunk's match launch overlaps the RCCL
+        # all-gather of the previous chunk (dist.overlapped_allgather)
+        pairs_dev = torch.from_numpy(pairs_all).to(device)
+        mine = [(a, b) for a, b in sdist.chunk_rows(P, rank, world, MATCH_CHUNKS) if b > a]
+        bufs = {a: torch.empty((b - a, bank.m_pad), dtype=torch.int32, device=device) for a, b in mine}
+        lo, hi = 0, sum(b - a for a, b in mine)
+    else:
+        lo, hi = sdist.shard_range(P, rank, world)
+        pairs_local = torch.from_numpy(pairs_all[lo:hi]).to(device)
+        m0 = torch.empty((hi - lo, bank.m_pad), dtype=torch.int32, device=device)
+        m16 = torch.empty((hi - lo, bank.m_pad), dtype=torch.int16, device=device)
+
+    def compute_chunk(a, b, out):
+        bank._launch(pairs_dev[a:b], num, den, bufs[a], None, None)
+        out.copy_(bufs[a])
 
     def match_step(record):
         e0 = e1 = None
         if record:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
+        if overlap:
+            sdist.overlapped_allgather(compute_chunk, P, (bank.m_pad,), torch.int16, device, chunks=MATCH_CHUNKS,
+                                       after_compute=(e1.record if record else None))
+            return (e0, e1)
         bank._launch(pairs_local, num, den, m0, None, None)
         if record:
             e1.record()
@@ -476,7 +500,8 @@ def main():
     pairs_per_launch = hi - lo
     ops_per_launch = 2.0 * M_KPT * M_KPT * DIM * pairs_per_launch
     achieved_tops = ops_per_launch / (kern_ms * 1e-3) / 1e12
-    n_matched = int((m0 >= 0).sum().item())
+    n_matched = int(sum(int((b >= 0).sum().item()) for b in bufs.values())) if overlap else \
+        int((m0 >= 0).sum().item())
     log(f"[rank {rank}] match: {ms_per_step:.2f} ms/step, kernel {kern_ms:.2f} ms, "
         f"{achieved_tops:.0f} TOPS, {n_matched} matches in shard")
 
@@ -494,7 +519,9 @@ def main():
         "dtype": "int8",
         "data": "synthetic (SuperPoint-like unit-norm descriptors, 40% cross-view overlap, seed 1)",
         "config": {"workload": f"C3/C4 all-pairs BF-L2 + ratio 0.75: {n_img} imgs x {M_KPT} kpts x {DIM}-d",
-                   "pairs": P, "parallelism": f"pairs/{world}" + (" + 1 RCCL all-gather (int16)" if world > 1 else "")},
+                   "pairs": P, "parallelism": f"pairs/{world}" + (
+                       f" + {MATCH_CHUNKS} RCCL all-gathers (int16) overlapped with the match launches" if overlap
+                       else (" + 1 all-gather (int16)" if world > 1 else ""))},
         "roofline": {"bound": "mfma", "achieved": achieved_tops, "peak": PEAK_INT8_TOPS, "unit": "TOPS",
                      "frac": achieved_tops / PEAK_INT8_TOPS,
                      "traffic": pmc_traffic("match", pairs_per_launch / P) if n_img == N_IMG else None,
@@ -627,7 +654,7 @@ def main():
 
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

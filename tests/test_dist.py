@@ -74,3 +74,46 @@ def test_zslab_shards_cover_grid():
         slabs = [sdist.shard_range(R, r, world) for r in range(world)]
         assert slabs[0][0] == 0 and slabs[-1][1] == R
         assert all(slabs[i][1] == slabs[i + 1][0] for i in range(world - 1))
+
+
+
+def _worker_overlap(rank, world, port, n_total, chunks, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+        def compute(lo, hi, out):
+            out.copy_((torch.arange(lo, hi, dtype=torch.int32)[:, None] * 10 +
+                       torch.arange(6, dtype=torch.int32)[None, :]).to(torch.int16))
+
+        full = sdist.overlapped_allgather(compute, n_total, (6,), torch.int16, "cpu", chunks=chunks)
+        exp = (torch.arange(n_total, dtype=torch.int32)[:, None] * 10 +
+               torch.arange(6, dtype=torch.int32)[None, :]).to(torch.int16)
+        q.put((rank, bool(torch.equal(full, exp))))
+    except Exception as e:
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,chunks", [(2, 11, 4), (3, 100, 4), (2, 3, 4)])
+def test_overlapped_allgather_gloo(world, n, chunks):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_overlap, args=(r, world, port, n, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v is True for v in res.values()), res
+
+
+def test_chunk_rows_partition():
+    for n, world, chunks in ((32896, 8, 4), (11, 2, 4), (3, 2, 4), (0, 2, 4)):
+        rows = sorted(r for rk in range(world) for (lo, hi) in sdist.chunk_rows(n, rk, world, chunks)
+                      for r in range(lo, hi))
+        assert rows == list(range(n))
