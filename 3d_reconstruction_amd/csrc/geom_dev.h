@@ -44,7 +44,7 @@ __device__ __forceinline__ void project(const double* R, const double* t, const 
 // one-sided (Hestenes) Jacobi on the 4 columns, V accumulates the rotations;
 // the right singular vector of the smallest singular value is V's column with
 // the smallest resulting column norm.  Output: unit norm, X[3] >= 0.
-__device__ inline void dlt_point(const double* P0, const double* P1, double x0, double y0, double x1,
+__device__ inline void dlt_point_jacobi(const double* P0, const double* P1, double x0, double y0, double x1,
                                  double y1, double* Xout) {
     const double* Pv[2] = {P0, P1};
     const double px[2] = {x0, x1};
@@ -119,6 +119,179 @@ __device__ inline void dlt_point(const double* P0, const double* P1, double x0, 
     const double sc = (X[3] < 0 ? -1.0 : 1.0) / nrm;
 #pragma unroll
     for (int r = 0; r < 4; ++r) Xout[r] = X[r] * sc;
+}
+
+// The same null vector, cheaper: Householder QR of A (6x4 -> R 4x4, backward
+// stable, no squaring of A); an exactly singular R (noise-free data) gives the
+// null vector by back-substitution; otherwise inverse iteration with R's
+// triangular solves (factor (sigma4/sigma3)^2 per step), started from
+// R^-1 e4, for at most kDltInvIters steps until the normalised iterate stops
+// moving (|dy| <= 1e-15); small-baseline points whose sigma3 ~ sigma4 make it
+// crawl finish with one-sided Jacobi on the 4 columns of R (A^T A = R^T R, so
+// the right singular vectors are A's).
+constexpr int kDltInvIters = 6;
+
+__device__ inline void null_vector_jacobi4(double (&R)[4][4], double* y) {
+    double C[4][4], V[4][4];  // C[col][row]
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { C[c][r] = R[r][c]; V[c][r] = (r == c) ? 1.0 : 0.0; }
+    for (int sweep = 0; sweep < 30; ++sweep) {
+        bool rotated = false;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+            for (int q = p + 1; q < 4; ++q) {
+                double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    alpha += C[p][r] * C[p][r];
+                    beta += C[q][r] * C[q][r];
+                    gamma += C[p][r] * C[q][r];
+                }
+                if (gamma == 0.0 || gamma * gamma <= 1e-30 * (alpha * beta)) continue;
+                rotated = true;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double ap = C[p][r], aq = C[q][r];
+                    C[p][r] = c * ap - s * aq;
+                    C[q][r] = s * ap + c * aq;
+                    const double vp = V[p][r], vq = V[q][r];
+                    V[p][r] = c * vp - s * vq;
+                    V[q][r] = s * vp + c * vq;
+                }
+            }
+        }
+        if (!rotated) break;
+    }
+    int best = 0;
+    double bn = C[0][0] * C[0][0] + C[0][1] * C[0][1] + C[0][2] * C[0][2] + C[0][3] * C[0][3];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        const double nk = C[k][0] * C[k][0] + C[k][1] * C[k][1] + C[k][2] * C[k][2] + C[k][3] * C[k][3];
+        if (nk < bn) { bn = nk; best = k; }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = V[0][r];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+        if (k == best)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = V[k][r];
+}
+
+__device__ inline void dlt_point(const double* P0, const double* P1, double x0, double y0, double x1, double y1,
+                                 double* Xout) {
+    const double* Pv[2] = {P0, P1};
+    const double px[2] = {x0, x1};
+    const double py[2] = {y0, y1};
+    double A[6][4];
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double p0 = Pv[v][k], p1 = Pv[v][4 + k], p2 = Pv[v][8 + k];
+            A[3 * v + 0][k] = px[v] * p2 - p0;
+            A[3 * v + 1][k] = py[v] * p2 - p1;
+            A[3 * v + 2][k] = px[v] * p1 - py[v] * p0;
+        }
+    double rmax = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double nrm2 = 0;
+#pragma unroll
+        for (int r = k; r < 6; ++r) nrm2 += A[r][k] * A[r][k];
+        const double nrm = sqrt(nrm2);
+        const double alpha = (A[k][k] >= 0) ? -nrm : nrm;
+        double v[6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) v[r] = (r < k) ? 0.0 : A[r][k];
+        v[k] -= alpha;
+        double vn2 = 0;
+#pragma unroll
+        for (int r = k; r < 6; ++r) vn2 += v[r] * v[r];
+        const double beta = (vn2 > 0) ? 2.0 / vn2 : 0.0;
+#pragma unroll
+        for (int c = k; c < 4; ++c) {
+            double sdot = 0;
+#pragma unroll
+            for (int r = k; r < 6; ++r) sdot += v[r] * A[r][c];
+            sdot *= beta;
+#pragma unroll
+            for (int r = k; r < 6; ++r) A[r][c] -= sdot * v[r];
+        }
+        rmax = fmax(rmax, fabs(A[k][k]));
+    }
+    double R[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) R[r][c] = (c >= r) ? A[r][c] : 0.0;
+    double y[4];
+    bool done = false;
+    if (fabs(R[3][3]) <= 1e-15 * rmax && fabs(R[2][2]) > 1e-15 * rmax) {  // exact null vector
+        y[3] = 1.0;
+#pragma unroll
+        for (int r = 2; r >= 0; --r) {
+            double sacc = -R[r][3];
+#pragma unroll
+            for (int c = r + 1; c < 3; ++c) sacc -= R[r][c] * y[c];
+            y[r] = sacc / R[r][r];
+        }
+        done = true;
+    } else if (fabs(R[3][3]) > 1e-15 * rmax && fabs(R[2][2]) > 1e-15 * rmax && fabs(R[1][1]) > 1e-15 * rmax &&
+               fabs(R[0][0]) > 1e-15 * rmax) {
+        double id[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) id[r] = 1.0 / R[r][r];
+        y[3] = id[3];
+#pragma unroll
+        for (int r = 2; r >= 0; --r) {
+            double sacc = 0;
+#pragma unroll
+            for (int c = r + 1; c < 4; ++c) sacc -= R[r][c] * y[c];
+            y[r] = sacc * id[r];
+        }
+        for (int it = 0; it < kDltInvIters && !done; ++it) {
+            double nn = sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+            double yo[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { y[r] /= nn; yo[r] = y[r]; }
+            double z[4];  // R^T z = y (forward)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double sacc = y[r];
+#pragma unroll
+                for (int c = 0; c < r; ++c) sacc -= R[c][r] * z[c];
+                z[r] = sacc * id[r];
+            }
+#pragma unroll
+            for (int r = 3; r >= 0; --r) {  // R y = z (backward)
+                double sacc = z[r];
+#pragma unroll
+                for (int c = r + 1; c < 4; ++c) sacc -= R[r][c] * y[c];
+                y[r] = sacc * id[r];
+            }
+            nn = sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+            double dd = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dd += (y[r] / nn - yo[r]) * (y[r] / nn - yo[r]);
+            done = dd <= 1e-30;
+        }
+    }
+    if (!done) null_vector_jacobi4(R, y);
+    const double nrm = sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+    if (!(nrm > 0) || !isfinite(nrm)) {
+        dlt_point_jacobi(P0, P1, x0, y0, x1, y1, Xout);
+        return;
+    }
+    const double sc = (y[3] < 0 ? -1.0 : 1.0) / nrm;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Xout[r] = y[r] * sc;
 }
 
 }  // namespace sfmhip

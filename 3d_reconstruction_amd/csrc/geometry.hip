@@ -35,17 +35,48 @@ __global__ void dlt_kernel(const double* __restrict__ P, const int32_t* __restri
 }
 
 // ---------------------------------------------------------------------------
+// Rotation(s) of the block's camera: when every observation of the block
+// belongs to one pair (sorted pair_of_obs, or a single pair), the first
+// `nrot` threads build them once in LDS (R0 = R(rvec), R1..3 = R(rvec + h e_k)
+// for the FD columns) instead of every thread re-evaluating sin/cos; values
+// are identical either way.  Returns true if the LDS copy is valid.
+__device__ __forceinline__ bool block_rotations(const double* __restrict__ cam,
+                                                const int32_t* __restrict__ pair_of_obs, int64_t n, int nrot,
+                                                double (*sR)[9]) {
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+    const int64_t i = min(i0 + (int64_t)threadIdx.x, n - 1);
+    const int pr = pair_of_obs ? pair_of_obs[i] : 0;
+    const int pr0 = pair_of_obs ? pair_of_obs[i0] : 0;
+    const bool uniform = __syncthreads_and(pr == pr0);
+    if (uniform && threadIdx.x < nrot) {
+        const double* c = cam + (size_t)pr0 * 6;
+        double p[3] = {c[0], c[1], c[2]};
+        const int q = threadIdx.x - 1;
+        if (q >= 0) p[q] = p[q] + fd_step(p[q]);
+        rodrigues(p, sR[threadIdx.x]);
+    }
+    __syncthreads();
+    return uniform;
+}
+
 __global__ void residual_kernel(const double* __restrict__ cam, const double* __restrict__ K,
                                 const double* __restrict__ X, const double* __restrict__ pts2d,
                                 const int32_t* __restrict__ pair_of_obs, int64_t n,
                                 double* __restrict__ r) {
+    __shared__ double sR[1][9];
+    const bool shared_R = block_rotations(cam, pair_of_obs, n, 1, sR);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int pr = pair_of_obs ? pair_of_obs[i] : 0;
     const double* c = cam + (size_t)pr * 6;
     const double* k = K + (size_t)pr * 9;
     double R[9];
-    rodrigues(c, R);
+    if (shared_R) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) R[e] = sR[0][e];
+    } else {
+        rodrigues(c, R);
+    }
     const double Xp[3] = {X[3 * i], X[3 * i + 1], X[3 * i + 2]};
     double u, v;
     project(R, c + 3, Xp, k[0], k[4], k[2], k[5], u, v);
@@ -63,6 +94,8 @@ __global__ void fdjac_kernel(const double* __restrict__ cam, const double* __res
                              const int32_t* __restrict__ pair_of_obs, int64_t n,
                              const double* __restrict__ f0, double* __restrict__ r,
                              double* __restrict__ jv) {
+    __shared__ double sR[4][9];
+    const bool shared_R = block_rotations(cam, pair_of_obs, n, 4, sR);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int pr = pair_of_obs ? pair_of_obs[i] : 0;
@@ -73,7 +106,12 @@ __global__ void fdjac_kernel(const double* __restrict__ cam, const double* __res
     double p[9] = {c[0], c[1], c[2], c[3], c[4], c[5], X[3 * i], X[3 * i + 1], X[3 * i + 2]};
 
     double R0[9];
-    rodrigues(p, R0);
+    if (shared_R) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) R0[e] = sR[0][e];
+    } else {
+        rodrigues(p, R0);
+    }
     double base_u, base_v;
     {
         double u, v;
@@ -96,7 +134,12 @@ __global__ void fdjac_kernel(const double* __restrict__ cam, const double* __res
         double u, v;
         if (q < 3) {
             double Rq[9];
-            rodrigues(p, Rq);
+            if (shared_R) {
+#pragma unroll
+                for (int e = 0; e < 9; ++e) Rq[e] = sR[1 + q][e];
+            } else {
+                rodrigues(p, Rq);
+            }
             project(Rq, p + 3, p + 6, fx, fy, cx, cy, u, v);
         } else {
             project(R0, p + 3, p + 6, fx, fy, cx, cy, u, v);
