@@ -40,7 +40,7 @@ PEAK_INT8_TOPS = 5000.0       # MI355X dense int8 MFMA (MI355X_MICROARCH.md: 2x 
 PEAK_HBM_GBS = 8000.0         # HBM3E spec
 MATCH_CHUNKS = 4              # N>1 (RCCL): match launches per step, each overlapped with the previous all-gather
 PEAK_FP32_TFLOPS = 157.3      # vector fp32
-PEAK_FP64_TFLOPS = 78.6       # vector fp64
+PEAK_FP64_TFLOPS = 78.6       # fp64 (vector and v_mfma_f64 matrix peaks are the same on MI355X)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1", "traffic.json")
 
 
@@ -222,8 +222,9 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
     ms = wall / args.steps * 1e3
     line = {"metric": "vq obs/sec", "value": obs.shape[0] / (ms * 1e-3), "unit": "obs/s", "ms_per_step": ms,
             "config": {"workload": "M2 vq (matching.py:27): 257x4096 obs x 200 codes x 128-d, f64"},
-            "roofline": {"bound": "fp64", "kernel": "vq_kernel", "kernel_ms": float(np.mean(kms)),
-                         "achieved_tflops": 3 * obs.shape[0] * 200 * 128 / (np.mean(kms) * 1e-3) / 1e12,
+            "roofline": {"bound": "mfma", "kernel": "vq_mfma_kernel", "kernel_ms": float(np.mean(kms)),
+                         # GEMM form: 2 flops per (obs, codeword, dim) on v_mfma_f64_16x16x4_f64
+                         "achieved_tflops": 2 * obs.shape[0] * 200 * 128 / (np.mean(kms) * 1e-3) / 1e12,
                          "peak_tflops": PEAK_FP64_TFLOPS}}
     if cpu:
         from scipy.cluster.vq import vq as scipy_vq

@@ -187,3 +187,18 @@ def test_match_empty_and_single_keypoint_images(sfm, gpu):
     assert np.array_equal(m0[:, :300], ref[:, :300])
     assert (m0[1] == -1).all() and (m0[3] == -1).all()       # B empty / single candidate
     assert (m0[:, 300:] == -1).all()                          # padding rows never match
+
+
+@pytest.mark.parametrize("n,k,d", [(5000, 200, 128), (777, 300, 40), (300, 1, 128), (1, 17, 64), (4097, 145, 20)])
+def test_vq_mfma_integer_bit_exact(sfm, gpu, n, k, d):
+    """f64-MFMA vq (GEMM form) on integer data: bit-exact with scipy, across
+    code-book passes (k > 144), padded dims (d not a power of two), a single
+    codeword and ragged observation tiles; ties resolve to the lowest index."""
+    rng = np.random.default_rng(n + k + d)
+    obs = rng.integers(-20, 21, (n, d)).astype(np.float64)
+    code = rng.integers(-20, 21, (k, d)).astype(np.float64)
+    if k > 3:
+        code[k - 1] = code[1]                                    # exact duplicate codeword -> tie
+    codes, dist = sfm.vq(obs, code)
+    rc, rd = om.vq(obs, code)
+    assert np.array_equal(codes, rc) and np.array_equal(dist, rd)

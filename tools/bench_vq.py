@@ -1,0 +1,37 @@
+"""A/B the M2 vq kernels: python tools/bench_vq.py  (SFMHIP_VQ_VARIANT: 0 MFMA two blocks/step, 2 MFMA one block/step, 1 FMA difference form)."""
+import importlib
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+abi = importlib.import_module("3d_reconstruction_amd._abi")
+syn = importlib.import_module("3d_reconstruction_amd.synthetic")
+dev = torch.device("cuda", 0)
+obs = syn.superpoint_like(257, 4096, 128, seed=3, device=dev).reshape(-1, 128).double().contiguous()
+book = obs[torch.randperm(obs.shape[0], device=dev)[:200]].contiguous()
+out = {}
+for variant in ("0", "2", "1"):
+    os.environ["SFMHIP_VQ_VARIANT"] = variant
+    codes = torch.empty(obs.shape[0], dtype=torch.int32, device=dev)
+    dist = torch.empty(obs.shape[0], dtype=torch.float64, device=dev)
+
+    def run():
+        abi.call("sfmhip_vq", obs.data_ptr(), obs.shape[0], book.data_ptr(), 200, 128, codes.data_ptr(),
+                 dist.data_ptr(), abi.stream_ptr())
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    out[variant] = (codes.clone(), dist.clone())
+    print(f"variant {variant}: {ms:.3f} ms  {obs.shape[0] / ms / 1e3:.1f} Mobs/s  "
+          f"{2 * obs.shape[0] * 200 * 128 / ms / 1e9:.2f} TFLOP/s (2nkd)", flush=True)
+c0, d0 = out["0"]
+c1, d1 = out["1"]
+print("codes agree", (c0 == c1).float().mean().item(), "max rel dist", ((d0 - d1).abs() / d1.clamp_min(1e-300)).max().item())
