@@ -392,8 +392,8 @@ __global__ __launch_bounds__(256) void vq_kernel(const double* __restrict__ obs,
 }
 
 // ---------------------------------------------------------------------------
-// vq on the f64 matrix cores: d2(x, c) = |x|^2 + |c|^2 - 2 x.c, the form
-// scipy's _vq uses (BLAS gemm + norms), with x.c from
+// vq on the f64 matrix cores: argmin_j of |c_j|^2 - 2 x.c_j (= d2 - |x|^2; the
+// GEMM form scipy's _vq uses, minus the row constant), with x.c from
 // v_mfma_f64_16x16x4_f64.  Exact for integer-valued data (every product and
 // partial sum is an integer below 2^53), so integer inputs give scipy's codes
 // and distances bit for bit; float inputs agree to rounding.
@@ -403,19 +403,21 @@ __global__ __launch_bounds__(256) void vq_kernel(const double* __restrict__ obs,
 // codewords (row stride DP+4 f64, i.e. == 4 mod 32, so the 16 rows x 4 k of an
 // MFMA B fragment hit distinct bank pairs).  Each wave keeps the A fragments
 // of its 32 observations (2 row tiles x DP/4 f64 per lane) in registers for a
-// whole pass; every B fragment read from LDS feeds two MFMAs, and (DP=128)
-// two code blocks run per step, i.e. four independent accumulator chains per
-// wave (measured 1.35 -> 1.29 ms on 1.05M x 200 x 128; 53% of the f64 peak).  Each lane
+// whole pass; every B fragment read from LDS feeds two MFMAs (PAIR: two code
+// blocks per step, four accumulator chains; measured slower once the
+// difference-form epilogue raised register pressure: 1.37 vs 1.33 ms).  Each lane
 // tracks the best codeword among j == lane (mod 16) for its 4 C rows, then a
 // 16-lane (d2, index) argmin with lowest-index tie-break; passes merge through
 // the output arrays (strict <: later passes hold higher indices), and the
-// last pass writes sqrt(max(d2, 0)).
+// last pass writes the winner's distance recomputed in difference form,
+// sqrt(sum (x - c)^2): the GEMM form's cancellation noise would otherwise show
+// where x equals its codeword (kmeans singletons), which scipy reports as 0.
 typedef double v4d __attribute__((ext_vector_type(4)));
 constexpr int kVqmWaves = 8;
 constexpr int kVqmObsPerWave = 32;
 constexpr int kVqmTile = kVqmWaves * kVqmObsPerWave;   // 256 observations
 
-template <int DP, bool PAIR>
+template <int DP, bool PAIR, bool FULL>   // FULL: d == DP (no k padding)
 __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
     const double* __restrict__ obs, int64_t n_obs, const double* __restrict__ code, int n_codes, int d,
     int codes_per_pass, int32_t* __restrict__ codes, double* __restrict__ dist) {
@@ -434,7 +436,7 @@ __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
         __syncthreads();
         for (int t = threadIdx.x; t < ncb * 16 * DP; t += blockDim.x) {
             const int r = t / DP, k = t - r * DP;
-            sc[r * LD + k] = (r < nc && k < d) ? code[(size_t)(c0 + r) * d + k] : 0.0;
+            sc[r * LD + k] = (r < nc && (FULL || k < d)) ? code[(size_t)(c0 + r) * d + k] : 0.0;
         }
         __syncthreads();
         for (int r = threadIdx.x; r < ncb * 16; r += blockDim.x) {
@@ -446,23 +448,15 @@ __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
         for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
             const int64_t ob = t * kVqmTile + wave * kVqmObsPerWave;
             double a[2][KS];
-            double xr[2][4];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int64_t o = ob + 16 * h + r16;
                 const double* xp = obs + o * d;
-                double p = 0.0;
 #pragma unroll
                 for (int s = 0; s < KS; ++s) {
                     const int k = 4 * s + kq;
-                    const double v = (o < n_obs && k < d) ? __builtin_nontemporal_load(xp + k) : 0.0;
-                    a[h][s] = v;
-                    p = __builtin_fma(v, v, p);
+                    a[h][s] = (o < n_obs && (FULL || k < d)) ? __builtin_nontemporal_load(xp + k) : 0.0;
                 }
-                p += __shfl_xor(p, 16);
-                p += __shfl_xor(p, 32);                  // |x|^2 of row r16 on all four kq lanes
-#pragma unroll
-                for (int g = 0; g < 4; ++g) xr[h][g] = __shfl(p, kq + 4 * g);   // C row kq + 4g
             }
             double best[2][4];
             int bj[2][4];
@@ -475,8 +469,8 @@ __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
                 const double cn = sn[j];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const double d0 = xr[0][g] + cn - 2.0 * acc0[g];
-                    const double d1 = xr[1][g] + cn - 2.0 * acc1[g];
+                    const double d0 = cn - 2.0 * acc0[g];     // d2 - |x|^2: the row constant drops out
+                    const double d1 = cn - 2.0 * acc1[g];
                     if (d0 < best[0][g]) { best[0][g] = d0; bj[0][g] = c0 + j; }
                     if (d1 < best[1][g]) { best[1][g] = d1; bj[1][g] = c0 + j; }
                 }
@@ -513,6 +507,7 @@ __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
             }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
+                int win = 0;    // the winning codeword of row r16 (for the last pass's distance)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     double bv = best[h][g];
@@ -523,14 +518,36 @@ __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
                         const int oi = __shfl_xor(bi, off, 16);
                         if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
                     }
+                    // all 16 lanes of the kq group now hold row kq + 4g's (d2, index)
                     const int64_t o = ob + 16 * h + kq + 4 * g;
-                    if (r16 == 0 && o < n_obs) {
-                        if (!first) {
-                            const double prev = dist[o];
-                            if (!(bv < prev)) { bv = prev; bi = codes[o]; }
-                        }
+                    if (!first && o < n_obs) {
+                        const double prev = dist[o];
+                        if (!(bv < prev)) { bv = prev; bi = codes[o]; }
+                    }
+                    if (!last && r16 == 0 && o < n_obs) {
                         codes[o] = bi;
-                        dist[o] = last ? sqrt(fmax(bv, 0.0)) : bv;
+                        dist[o] = bv;
+                    }
+                    const int w = __shfl(bi, (r16 & 3) * 16);        // row r16 = (r16 & 3) + 4 (r16 >> 2)
+                    if ((r16 >> 2) == g) win = w;
+                }
+                if (last) {
+                    // distance of the winner in difference form, sum (x - c)^2: exact 0 for x == c
+                    // (the GEMM form leaves cancellation noise there), otherwise within rounding
+                    const int64_t o = ob + 16 * h + r16;
+                    const double* cp = code + (size_t)win * d;
+                    double part = 0.0;
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) {
+                        const int k = 4 * s + kq;
+                        const double df = a[h][s] - ((o < n_obs && (FULL || k < d)) ? cp[k] : 0.0);
+                        part = __builtin_fma(df, df, part);
+                    }
+                    part += __shfl_xor(part, 16);
+                    part += __shfl_xor(part, 32);
+                    if (kq == 0 && o < n_obs) {
+                        codes[o] = win;
+                        dist[o] = sqrt(part);
                     }
                 }
             }
@@ -641,18 +658,19 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
         const int64_t n_tiles = (n_obs + kVqmTile - 1) / kVqmTile;
         const int grid = (int)std::min<int64_t>(n_tiles, n_cu);
         hipStream_t s = as_stream(stream);
-#define SFMHIP_LAUNCH_VQM(DP, PR)                                                                             \
+#define SFMHIP_LAUNCH_VQM(DP, PR, FL)                                                                             \
     do {                                                                                                  \
-        (void)hipFuncSetAttribute((const void*)vq_mfma_kernel<DP, PR>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+        (void)hipFuncSetAttribute((const void*)vq_mfma_kernel<DP, PR, FL>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)shm);                                                               \
-        hipLaunchKernelGGL((vq_mfma_kernel<DP, PR>), dim3(grid), dim3(kVqmWaves * 64), shm, s, obs, n_obs,      \
+        hipLaunchKernelGGL((vq_mfma_kernel<DP, PR, FL>), dim3(grid), dim3(kVqmWaves * 64), shm, s, obs, n_obs,      \
                            code_book, n_codes, d, cpp, codes, dist);                                       \
     } while (0)
-        const bool pair = !(venv && std::atoi(venv) == 2);   // 2: one code block per step (A/B runs)
-        if (dp == 32) SFMHIP_LAUNCH_VQM(32, false);
-        else if (dp == 64) SFMHIP_LAUNCH_VQM(64, false);
-        else if (pair) SFMHIP_LAUNCH_VQM(128, true);
-        else SFMHIP_LAUNCH_VQM(128, false);
+        const bool pair = venv && std::atoi(venv) == 2;   // 2: two code blocks per step (A/B runs)
+        if (dp == 32) SFMHIP_LAUNCH_VQM(32, false, false);
+        else if (dp == 64) SFMHIP_LAUNCH_VQM(64, false, false);
+        else if (d != 128) SFMHIP_LAUNCH_VQM(128, false, false);
+        else if (pair) SFMHIP_LAUNCH_VQM(128, true, true);
+        else SFMHIP_LAUNCH_VQM(128, false, true);
 #undef SFMHIP_LAUNCH_VQM
         return check_launch("vq_mfma_kernel");
     }

@@ -1,4 +1,4 @@
-"""A/B the M2 vq kernels: python tools/bench_vq.py  (SFMHIP_VQ_VARIANT: 0 MFMA two blocks/step, 2 MFMA one block/step, 1 FMA difference form)."""
+"""A/B the M2 vq kernels: python tools/bench_vq.py  (SFMHIP_VQ_VARIANT: 0 MFMA one block/step, 2 MFMA two blocks/step, 1 FMA difference form)."""
 import importlib
 import os
 import sys
