@@ -323,208 +323,190 @@ __global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ g
 }
 
 // ---------------------------------------------------------------------------
-// V5: TSDF integration.  Every thread keeps ONE voxel's (T, W) in registers
-// across all frames of the launch, so the grid is read and written once per
-// launch; poses/intrinsics are staged in LDS.  The kernel is bound by the
-// depth gathers: the thread->voxel map decides how many cache lines a wave's
-// 64 gathers touch (MAP 0: a wave = 16 x by 4 z at one y, i.e. one image-row
-// band for orbiting cameras; MAP 1: 16 x by 4 y; MAP 2: 8 x by 8 z; MAP 3: 64 x).
+// V5: TSDF integration (arithmetic defined op for op in oracle/voxel.py
+// tsdf_integrate).  Bound by the per-CU texture pipeline (TA/TD ~87 % busy,
+// profiles/r1): every depth gather costs one L1 tag lookup per distinct
+// cache line per 16-lane quarter-wave, and neighbouring voxels land ~5.6 px
+// apart, so the lane->voxel layout decides the cost:
+//   * each 16-lane quarter-wave covers a 4 x 4 (x, z) patch at one y (the
+//     orbiting cameras map y to image rows, and a compact x-z patch has the
+//     smallest depth spread, i.e. the fewest distinct rows); a wave covers
+//     8 x 8 (x, z).  Simulated over the C5 orbit: 0.44 line lookups per
+//     voxel-frame vs 0.60 for a 16 x 4 strip and 0.79 for x-pairs;
+//   * each lane owns TWO voxels adjacent in y, run as one packed-f32 pair
+//     (v_pk_mul/add/fma_f32: two results per instruction); their (T, W) stay
+//     in registers across all frames of the launch (grid read and written
+//     once per launch);
+//   * the x/z part of each camera row, Q = (P0 vx + P2 vz) + P3, is per lane and
+//     shared by the pair, so a voxel pays one multiply-add per camera row;
+//   * 1/Zc and the running-average division use the IEEE f32 division
+//     sequence without v_div_scale / v_div_fixup, which are identities on the
+//     ranges the algorithm admits (2^-60 <= Zc < 2^60; weights 0..2^24, |T| <=
+//     2^30, numerators |n| >= 2^-100); lanes outside those ranges take the
+//     full IEEE division (rare, divergent), so every result is the oracle's;
+//   * pixel = v_cvt_flr_i32_f32 of (f X) iz + (c + 0.5) and one unsigned
+//     compare per axis; the depth gather is a bounds-checked buffer load, so
+//     off-image lanes need no address select;
+//   * poses/intrinsics are validated once per frame while being staged in LDS
+//     (non-finite or >= 2^60 anywhere: Z row zeroed, so the frame is skipped).
 // U frames' projections + gathers are issued before their (ordered) updates.
 constexpr int kTsdfMaxFrames = 512;   // frames per launch (host splits longer runs)
-
-template <int MAP>
-__device__ __forceinline__ void tsdf_map(int t, int& x, int& y, int& z) {
-    // tile of 256 threads: returns offsets inside the tile (extents in tsdf_tile)
-    if (MAP == 0) { x = t & 15; z = (t >> 4) & 3; y = t >> 6; }            // 16 x 4(y) x 4(z), wave = x*z
-    else if (MAP == 1) { x = t & 15; y = (t >> 4) & 3; z = t >> 6; }       // wave = x*y
-    else if (MAP == 2) { x = t & 7; z = (t >> 3) & 7; y = t >> 6; }        // 8 x 4(y) x 8(z), wave = x*z
-    else { x = t & 63; y = 0; z = t >> 6; }                                // 64 x 1 x 4
-}
-template <int MAP> struct TsdfTile;
-template <> struct TsdfTile<0> { static constexpr int X = 16, Y = 4, Z = 4; };
-template <> struct TsdfTile<1> { static constexpr int X = 16, Y = 4, Z = 4; };
-template <> struct TsdfTile<2> { static constexpr int X = 8, Y = 4, Z = 8; };
-template <> struct TsdfTile<3> { static constexpr int X = 64, Y = 1, Z = 4; };
+constexpr int kTsdfTX = 8, kTsdfTY = 8, kTsdfTZ = 8;    // workgroup tile: 4 waves x (8 x, 2 y, 8 z)
 
 // Spatially compact brick order: the 1-D grid is dealt round-robin over the 8
 // XCDs, so xcd_remap gives each XCD a contiguous range of logical bricks, and
-// logical bricks are ordered by "super-bricks" of SB_X x SB_Y x SB_Z bricks
-// (64 x 64 x 16 voxels for MAP 0).  Workgroups resident on one XCD at the same
-// time then project onto one compact image region per frame, so the depth
-// lines they gather stay in that XCD's L2 (speed only, never correctness).
-struct SuperBrick { int x, y, z; };   // super-brick extent in bricks (default 2 x 4 x 8: 32 x 16 x 32 voxels, measured best)
+// logical bricks are ordered by "super-bricks" of SB_X x SB_Y x SB_Z bricks.
+// Workgroups resident on one XCD at the same time then project onto one
+// compact image region per frame, so the depth lines they gather stay in that
+// XCD's L2 (speed only, never correctness).
+struct SuperBrick { int x, y, z; };
 
-template <int MAP, int U, bool SWZ>
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 f2s(float a) { return f2{a, a}; }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 rcp2(f2 a) { return f2{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)}; }
+
+// RN(1/z) for z in [2^-60, 2^60): Fma0..Fma4 + div_fmas of the f32 IEEE
+// division with numerator 1 (Mul = 1 * Fma1 = Fma1).
+__device__ __forceinline__ f2 recip_rn(f2 z) {
+    const f2 one = f2s(1.f), nz = -z;
+    f2 r = rcp2(z);
+    r = fma2(fma2(nz, r, one), r, r);
+    const f2 q = fma2(fma2(nz, r, one), r, r);
+    return fma2(fma2(nz, q, one), r, q);
+}
+// RN(n/d) for d in [1, 2^25] and |n| in [2^-100, 2^60] (or any d, n of those
+// exponent ranges: no scaling, no fixup case).
+__device__ __forceinline__ f2 div_rn(f2 n, f2 d) {
+    const f2 one = f2s(1.f), nd = -d;
+    f2 r = rcp2(d);
+    r = fma2(fma2(nd, r, one), r, r);
+    f2 q = n * r;
+    q = fma2(fma2(nd, q, n), r, q);
+    return fma2(fma2(nd, q, n), r, q);
+}
+__device__ __forceinline__ int cvt_flr(float x) {
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+// Zc in [2^-60, 2^60) (false for <= 0, NaN, inf): one subtract + one compare
+__device__ __forceinline__ bool z_ok(float z) {
+    return __builtin_bit_cast(unsigned, z) - 0x21800000u < 0x3C000000u;
+}
+__device__ __forceinline__ bool tame(float t, float w) {
+    return fabsf(t) <= 0x1p30f && w >= 0.f && w <= 0x1p24f;
+}
+
+template <int U, bool SWZ>
 __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float* __restrict__ Wt, int D, int H,
                                                    int W, int z0, int z1, const float* __restrict__ depth, int F,
                                                    int Hd, int Wd, const float* __restrict__ poses,
                                                    const float* __restrict__ Kf, Bounds B, float trunc,
                                                    SuperBrick SB) {
-    const int kSbX = SB.x, kSbY = SB.y, kSbZ = SB.z;
-    using TT = TsdfTile<MAP>;
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (SWZ) {
-        const int nbx = (W + TT::X - 1) / TT::X, nby = (H + TT::Y - 1) / TT::Y;
-        const int nsx = (nbx + kSbX - 1) / kSbX, nsy = (nby + kSbY - 1) / kSbY;
+        const int nbx = (W + kTsdfTX - 1) / kTsdfTX, nby = (H + kTsdfTY - 1) / kTsdfTY;
+        const int nsx = (nbx + SB.x - 1) / SB.x, nsy = (nby + SB.y - 1) / SB.y;
         const int L = xcd_remap(blockIdx.x, gridDim.x);
-        const int sb = L / (kSbX * kSbY * kSbZ), in = L % (kSbX * kSbY * kSbZ);
+        const int sb = L / (SB.x * SB.y * SB.z), in = L % (SB.x * SB.y * SB.z);
         const int sx = sb % nsx, sy = (sb / nsx) % nsy, sz = sb / (nsx * nsy);
-        bx = sx * kSbX + in % kSbX;
-        by = sy * kSbY + (in / kSbX) % kSbY;
-        bz = sz * kSbZ + in / (kSbX * kSbY);
+        bx = sx * SB.x + in % SB.x;
+        by = sy * SB.y + (in / SB.x) % SB.y;
+        bz = sz * SB.z + in / (SB.x * SB.y);
     }
-    extern __shared__ float cam[];  // F x 16 (dynamic: a static 512-frame array capped occupancy at 5 waves)
-    for (int t = threadIdx.x; t < F * 16; t += blockDim.x) {
-        const int f = t >> 4, q = t & 15;
-        cam[t] = (q < 12) ? poses[f * 12 + q] : Kf[f * 4 + (q - 12)];
+    // Camera records, 16 floats per frame:
+    //   P0 P4 | P2 P6 | P3 P7 | P8 P10 P11 | P1 P5 P9 | fx fy | cx+.5 cy+.5
+    extern __shared__ float cam[];   // dynamic: a static 512-frame array would cap occupancy
+    for (int f = threadIdx.x; f < F; f += blockDim.x) {
+        float p[12], k[4];
+        bool good = true;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) { p[q] = poses[f * 12 + q]; good = good && fabsf(p[q]) < 0x1p60f; }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { k[q] = Kf[f * 4 + q]; good = good && fabsf(k[q]) < 0x1p60f; }
+        const float rec[16] = {p[0], p[4], p[2], p[6], p[3], p[7], p[8], p[10], p[11], p[1], p[5], p[9],
+                               k[0], k[1], k[2] + 0.5f, k[3] + 0.5f};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) cam[f * 16 + q] = good ? rec[q] : 0.f;   // Zc = 0 -> frame skipped
     }
     __syncthreads();
-    int ox, oy, oz;
-    tsdf_map<MAP>(threadIdx.x, ox, oy, oz);
-    const int x = bx * TT::X + ox;
-    const int y = by * TT::Y + oy;
-    const int z = z0 + bz * TT::Z + oz;
+    const int l = threadIdx.x & 63;
+    const int x = bx * kTsdfTX + (l & 3) + 4 * ((l >> 4) & 1);
+    const int z = z0 + bz * kTsdfTZ + ((l >> 2) & 3) + 4 * (l >> 5);
+    const int y = by * kTsdfTY + 2 * (threadIdx.x >> 6);
     if (x >= W || y >= H || z >= z1) return;  // (after the only barrier)
+    const bool two = y + 1 < H;
     const float sx = (B.mx[0] - B.mn[0]) / (float)(W - 1);
     const float sy = (B.mx[1] - B.mn[1]) / (float)(H - 1);
     const float sz = (B.mx[2] - B.mn[2]) / (float)(D - 1);
     const float vx = B.mn[0] + (float)x * sx;
-    const float vy = B.mn[1] + (float)y * sy;
+    const f2 vy = {B.mn[1] + (float)y * sy, B.mn[1] + (float)(y + 1) * sy};
     const float vz = B.mn[2] + (float)z * sz;
     const float inv_trunc = 1.0f / trunc;
     const size_t idx = ((size_t)z * H + y) * W + x;
-    float tv = T[idx], wv = Wt[idx];
+    f2 tv = {T[idx], two ? T[idx + W] : 0.f};
+    f2 wv = {Wt[idx], two ? Wt[idx + W] : 0.f};
+    // lanes whose stored (T, W) lie outside the fast division's range divide exactly throughout
+    const bool wild = !(tame(tv.x, wv.x) && tame(tv.y, wv.y));
     const size_t frame = (size_t)Hd * Wd;
+    const int nbytes = (int)(frame * 4);   // host-checked < 2^31
+    const int Wd4 = Wd * 4;                 // < 2^24: exact in v_mul_u32_u24
     for (int f0 = 0; f0 < F; f0 += U) {
-        size_t at[U];
-        float zc[U];
-        bool ok[U];
+        f2 zc[U];
+        float d0[U], d1[U];
+        bool ok0[U], ok1[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int f = f0 + u;
-            const float* P = cam + min(f, F - 1) * 16;
-            const float Xc = P[0] * vx + P[1] * vy + P[2] * vz + P[3];
-            const float Yc = P[4] * vx + P[5] * vy + P[6] * vz + P[7];
-            const float Zc = P[8] * vx + P[9] * vy + P[10] * vz + P[11];
-            const float iz = 1.0f / Zc;
-            const float uu = (P[12] * Xc) * iz + P[14];
-            const float vv = (P[13] * Yc) * iz + P[15];
-            const float fu = floorf(uu + 0.5f), fv = floorf(vv + 0.5f);
-            const bool good = (f < F) && (Zc > 0.f) && fu >= 0.f && fu < (float)Wd && fv >= 0.f && fv < (float)Hd;
-            ok[u] = good;
+            const bool live = f0 + u < F;   // wave-uniform
+            const int f = live ? f0 + u : F - 1;
+            const float* r = cam + f * 16;
+            const f2 Q = (f2{r[0], r[1]} * f2s(vx) + f2{r[2], r[3]} * f2s(vz)) + f2{r[4], r[5]};
+            const float Qz = (r[6] * vx + r[7] * vz) + r[8];
+            const f2 Xc = f2s(r[9]) * vy + f2s(Q.x);
+            const f2 Yc = f2s(r[10]) * vy + f2s(Q.y);
+            const f2 Zc = f2s(r[11]) * vy + f2s(Qz);
+            const f2 iz = recip_rn(Zc);
+            const f2 uu = (f2s(r[12]) * Xc) * iz + f2s(r[14]);
+            const f2 vv = (f2s(r[13]) * Yc) * iz + f2s(r[15]);
+            const int iu0 = cvt_flr(uu.x), iv0 = cvt_flr(vv.x);
+            const int iu1 = cvt_flr(uu.y), iv1 = cvt_flr(vv.y);
+            ok0[u] = live && z_ok(Zc.x) && (unsigned)iu0 < (unsigned)Wd && (unsigned)iv0 < (unsigned)Hd;
+            ok1[u] = live && two && z_ok(Zc.y) && (unsigned)iu1 < (unsigned)Wd && (unsigned)iv1 < (unsigned)Hd;
             zc[u] = Zc;
-            at[u] = good ? (size_t)f * frame + (size_t)fv * Wd + (size_t)fu : 0;
+            // bounds-checked gather: off-image lanes read 0 or a discarded in-frame value
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(depth + (size_t)f * frame), (short)0, nbytes, 0x00020000);
+            d0[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rs, (int)(__umul24(iv0, Wd4) + ((unsigned)iu0 << 2)), 0, 0));
+            d1[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rs, (int)(__umul24(iv1, Wd4) + ((unsigned)iu1 << 2)), 0, 0));
         }
-        float dep[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) dep[u] = depth[at[u]];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const float sdf = dep[u] - zc[u];
-            if (ok[u] && dep[u] > 0.f && !(sdf < -trunc)) {
-                const float ts = fminf(1.0f, sdf * inv_trunc);
-                tv = (tv * wv + ts) / (wv + 1.0f);
-                wv = wv + 1.0f;
-            }
+            const f2 dep = {d0[u], d1[u]};
+            const f2 sdf = dep - zc[u];
+            const bool g0 = ok0[u] && dep.x > 0.f && !(sdf.x < -trunc);
+            const bool g1 = ok1[u] && dep.y > 0.f && !(sdf.y < -trunc);
+            const f2 sc = sdf * f2s(inv_trunc);
+            const f2 ts = {fminf(1.0f, sc.x), fminf(1.0f, sc.y)};
+            const f2 n = tv * wv + ts;
+            const f2 d = wv + f2s(1.0f);
+            f2 q = div_rn(n, d);
+            if (wild || !(fabsf(n.x) >= 0x1p-100f)) q.x = n.x / d.x;
+            if (wild || !(fabsf(n.y) >= 0x1p-100f)) q.y = n.y / d.y;
+            tv.x = g0 ? q.x : tv.x;
+            wv.x = g0 ? d.x : wv.x;
+            tv.y = g1 ? q.y : tv.y;
+            wv.y = g1 ? d.y : wv.y;
         }
     }
-    T[idx] = tv;
-    Wt[idx] = wv;
-}
-
-// Persistent-band TSDF (SFMHIP_TSDF_KIND=1): the 8 XCD labels (blockIdx % 8)
-// each own a band of kBandRows voxel rows (y), so for cameras orbiting the y
-// axis an XCD's voxels project onto one horizontal image band that stays in
-// its L2 while all of that XCD's workgroups fuse the same frame (they start
-// together and do equal work per frame).  Workgroup = one z-slice of the band:
-// thread t owns voxel column x = x0 + t and the kBandRows voxels above it,
-// with their (T, W) in registers for all F frames (grid read/written once).
-// Gathers are issued kBandGroup at a time before their ordered updates.
-constexpr int kBandGroup = 8;
-
-template <int kBandRows, int OCC>
-__global__ __launch_bounds__(256, OCC) void tsdf_band_kernel(
-    float* __restrict__ T, float* __restrict__ Wt, int D, int H, int W, int x0, int y0, int zs, int nz,
-    const float* __restrict__ depth, int F, int Hd, int Wd, const float* __restrict__ poses,
-    const float* __restrict__ Kf, Bounds B, float trunc) {
-    __shared__ float cam[kTsdfMaxFrames * 16];
-    for (int t = threadIdx.x; t < F * 16; t += blockDim.x) {
-        const int f = t >> 4, q = t & 15;
-        cam[t] = (q < 12) ? poses[f * 12 + q] : Kf[f * 4 + (q - 12)];
+    T[idx] = tv.x;
+    Wt[idx] = wv.x;
+    if (two) {
+        T[idx + W] = tv.y;
+        Wt[idx + W] = wv.y;
     }
-    __syncthreads();
-    const int label = blockIdx.x % kNumXcd;          // shares an XCD (speed only)
-    const int zi = blockIdx.x / kNumXcd;
-    if (zi >= nz) return;
-    const int x = x0 + threadIdx.x;
-    const int ya = y0 + label * kBandRows;
-    const int z = zs + zi;
-    if (x >= W || ya >= H || z >= D) return;
-    const int ny = min(kBandRows, H - ya);
-    const float sx = (B.mx[0] - B.mn[0]) / (float)(W - 1);
-    const float sy = (B.mx[1] - B.mn[1]) / (float)(H - 1);
-    const float sz = (B.mx[2] - B.mn[2]) / (float)(D - 1);
-    const float vx = B.mn[0] + (float)x * sx;
-    const float vz = B.mn[2] + (float)z * sz;
-    const float inv_trunc = 1.0f / trunc;
-    float tv[kBandRows], wv[kBandRows];
-    const size_t plane = (size_t)H * W;
-    const size_t base = (size_t)z * plane + (size_t)ya * W + x;
-#pragma unroll
-    for (int v = 0; v < kBandRows; ++v) {
-        tv[v] = (v < ny) ? T[base + (size_t)v * W] : 0.f;
-        wv[v] = (v < ny) ? Wt[base + (size_t)v * W] : 0.f;
-    }
-    const size_t frame = (size_t)Hd * Wd;
-    for (int f = 0; f < F; ++f) {
-        const float* P = cam + f * 16;
-        const float* dp = depth + (size_t)f * frame;
-        // per-thread partial products (exactly the first terms of the left-to-right sums)
-        const float ax = P[0] * vx, ay = P[4] * vx, az = P[8] * vx;
-        const float cx = P[2] * vz, cy = P[6] * vz, cz = P[10] * vz;
-#pragma unroll
-        for (int g = 0; g < kBandRows; g += kBandGroup) {
-            int off[kBandGroup];
-            float zc[kBandGroup];
-            bool ok[kBandGroup];
-#pragma unroll
-            for (int u = 0; u < kBandGroup; ++u) {
-                const int v = g + u;
-                const float vyv = B.mn[1] + (float)(ya + v) * sy;
-                const float Xc = ((ax + P[1] * vyv) + cx) + P[3];
-                const float Yc = ((ay + P[5] * vyv) + cy) + P[7];
-                const float Zc = ((az + P[9] * vyv) + cz) + P[11];
-                const float iz = 1.0f / Zc;
-                const float uu = (P[12] * Xc) * iz + P[14];
-                const float vv = (P[13] * Yc) * iz + P[15];
-                const float fu = floorf(uu + 0.5f), fv = floorf(vv + 0.5f);
-                const bool good = (v < ny) && (Zc > 0.f) && fu >= 0.f && fu < (float)Wd && fv >= 0.f &&
-                                  fv < (float)Hd;
-                ok[u] = good;
-                zc[u] = Zc;
-                off[u] = good ? (int)fv * Wd + (int)fu : 0;
-            }
-            float dep[kBandGroup];
-#pragma unroll
-            for (int u = 0; u < kBandGroup; ++u) dep[u] = dp[off[u]];
-#pragma unroll
-            for (int u = 0; u < kBandGroup; ++u) {
-                const int v = g + u;
-                const float sdf = dep[u] - zc[u];
-                if (ok[u] && dep[u] > 0.f && !(sdf < -trunc)) {
-                    const float ts = fminf(1.0f, sdf * inv_trunc);
-                    tv[v] = (tv[v] * wv[v] + ts) / (wv[v] + 1.0f);
-                    wv[v] = wv[v] + 1.0f;
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int v = 0; v < kBandRows; ++v)
-        if (v < ny) {
-            T[base + (size_t)v * W] = tv[v];
-            Wt[base + (size_t)v * W] = wv[v];
-        }
 }
 
 static int env_int(const char* name, int dflt) {
@@ -903,47 +885,21 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     SFMHIP_REQUIRE(0 <= z0 && z0 <= z1 && z1 <= D, "sfmhip_tsdf_integrate: bad z range");
     SFMHIP_REQUIRE(trunc > 0.f, "sfmhip_tsdf_integrate: trunc must be > 0");
     if (F == 0 || z0 == z1) return SFMHIP_OK;
-    // Tuning knobs (A/B runs only): SFMHIP_TSDF_MAP, SFMHIP_TSDF_U, SFMHIP_TSDF_CHUNK
-    // (frames per launch: a shorter chunk bounds how many frames the resident
-    // workgroups touch at once, i.e. the depth working set in L2 / MALL).
-    if (env_int("SFMHIP_TSDF_KIND", 0) == 1 && (size_t)Hd * Wd < (size_t)INT_MAX) {
-        // persistent-band kernel; launches tile x (256 per WG), y (8 bands of
-        // `rows` rows), z (chunks sized to stay resident) and frames (<= 512).
-        const int rows = env_int("SFMHIP_TSDF_ROWS", 16) == 32 ? 32 : 16;
-        const int zchunk = std::max(1, env_int("SFMHIP_TSDF_ZCHUNK", rows == 16 ? 128 : 96));
-        const Bounds bb = make_bounds(bmin, bmax);
-        for (int f0 = 0; f0 < F; f0 += kTsdfMaxFrames) {
-            const int nf = std::min(kTsdfMaxFrames, F - f0);
-            for (int y0 = 0; y0 < H; y0 += kNumXcd * rows)
-                for (int x0 = 0; x0 < W; x0 += 256)
-                    for (int zs = z0; zs < z1; zs += zchunk) {
-                        const int nz = std::min(zchunk, z1 - zs);
-                        const float* dp = depth + (size_t)f0 * Hd * Wd;
-                        const float* pp = poses + (size_t)f0 * 12;
-                        const float* kp = Kf + (size_t)f0 * 4;
-                        if (rows == 32)
-                            hipLaunchKernelGGL((tsdf_band_kernel<32, 3>), dim3(kNumXcd * nz), dim3(256), 0,
-                                               as_stream(stream), T, Wt, D, H, W, x0, y0, zs, nz, dp, nf, Hd, Wd, pp,
-                                               kp, bb, trunc);
-                        else
-                            hipLaunchKernelGGL((tsdf_band_kernel<16, 4>), dim3(kNumXcd * nz), dim3(256), 0,
-                                               as_stream(stream), T, Wt, D, H, W, x0, y0, zs, nz, dp, nf, Hd, Wd, pp,
-                                               kp, bb, trunc);
-                        const int rc = check_launch("tsdf_band_kernel");
-                        if (rc != SFMHIP_OK) return rc;
-                    }
-        }
-        return SFMHIP_OK;
-    }
-    const int map = env_int("SFMHIP_TSDF_MAP", 0);
+    SFMHIP_REQUIRE((int64_t)Hd * Wd * 4 < (int64_t)INT_MAX && Wd < (1 << 22) && Hd < (1 << 22),
+                   "sfmhip_tsdf_integrate: depth map too large (4*Hd*Wd must be < 2^31)");
+    for (int a = 0; a < 3; ++a)
+        SFMHIP_REQUIRE(std::fabs(bmin[a]) < 0x1p60f && std::fabs(bmax[a]) < 0x1p60f,
+                       "sfmhip_tsdf_integrate: bounds must be finite and below 2^60 in magnitude");
+    // Tuning knobs (A/B runs only): SFMHIP_TSDF_U (frames in flight), SFMHIP_TSDF_SWZ
+    // (super-brick XCD order), SFMHIP_TSDF_SBX/SBY/SBZ and SFMHIP_TSDF_CHUNK (frames per
+    // launch: a shorter chunk bounds how many frames the resident workgroups
+    // touch at once, i.e. the depth working set in L2 / MALL).
     const int unroll = env_int("SFMHIP_TSDF_U", 4);
     const int swz = env_int("SFMHIP_TSDF_SWZ", 1);
-    const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 2)), std::max(1, env_int("SFMHIP_TSDF_SBY", 4)),
-                        std::max(1, env_int("SFMHIP_TSDF_SBZ", 8))};
+    const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 4)), std::max(1, env_int("SFMHIP_TSDF_SBY", 2)),
+                        std::max(1, env_int("SFMHIP_TSDF_SBZ", 4))};
     const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", 24)));
-    static const int tx[4] = {16, 16, 8, 64}, ty[4] = {4, 4, 4, 1}, tz[4] = {4, 4, 8, 4};
-    const int mi = swz ? 0 : ((map >= 0 && map < 4) ? map : 0);
-    const int nbx = ceil_div(W, tx[mi]), nby = ceil_div(H, ty[mi]), nbz = ceil_div(z1 - z0, tz[mi]);
+    const int nbx = ceil_div(W, kTsdfTX), nby = ceil_div(H, kTsdfTY), nbz = ceil_div(z1 - z0, kTsdfTZ);
     dim3 grid(nbx, nby, nbz);
     if (swz) {
         const int64_t slots = (int64_t)ceil_div(nbx, sb.x) * ceil_div(nby, sb.y) * ceil_div(nbz, sb.z) *
@@ -951,38 +907,24 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
         SFMHIP_REQUIRE(slots < INT_MAX, "sfmhip_tsdf_integrate: grid too large");
         grid = dim3((unsigned)slots, 1, 1);
     }
+    const Bounds bb = make_bounds(bmin, bmax);
     // frame chunks run in order on the stream, so per-voxel update order is kept
     for (int f0 = 0; f0 < F; f0 += chunk) {
         const int nf = std::min(chunk, F - f0);
         const float* dp = depth + (size_t)f0 * Hd * Wd;
         const float* pp = poses + (size_t)f0 * 12;
         const float* kp = Kf + (size_t)f0 * 4;
-        const Bounds bb = make_bounds(bmin, bmax);
-#define SFMHIP_TSDF(MM, UU, SS)                                                                              \
-    hipLaunchKernelGGL((tsdf_kernel<MM, UU, SS>), grid, dim3(256), (size_t)nf * 16 * sizeof(float),             \
-                       as_stream(stream), T, Wt, D, H, W, z0,                                                 \
-                       z1, dp, nf, Hd, Wd, pp, kp, bb, trunc, sb)
-#define SFMHIP_TSDF_M(MM)                          \
-    switch (unroll) {                              \
-        case 1: SFMHIP_TSDF(MM, 1, false); break;  \
-        case 8: SFMHIP_TSDF(MM, 8, false); break;  \
-        default: SFMHIP_TSDF(MM, 4, false); break; \
-    }
-        if (swz) {
-            switch (unroll) {
-                case 1: SFMHIP_TSDF(0, 1, true); break;
-                case 8: SFMHIP_TSDF(0, 8, true); break;
-                default: SFMHIP_TSDF(0, 4, true); break;
-            }
-        } else {
-            switch (mi) {
-                case 1: SFMHIP_TSDF_M(1); break;
-                case 2: SFMHIP_TSDF_M(2); break;
-                case 3: SFMHIP_TSDF_M(3); break;
-                default: SFMHIP_TSDF_M(0); break;
-            }
+#define SFMHIP_TSDF(UU, SS)                                                                                   \
+    hipLaunchKernelGGL((tsdf_kernel<UU, SS>), grid, dim3(256), (size_t)nf * 16 * sizeof(float),               \
+                       as_stream(stream), T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, pp, kp, bb, trunc, sb)
+        switch (unroll * 2 + (swz ? 1 : 0)) {
+            case 2: SFMHIP_TSDF(1, false); break;
+            case 3: SFMHIP_TSDF(1, true); break;
+            case 4: SFMHIP_TSDF(2, false); break;
+            case 5: SFMHIP_TSDF(2, true); break;
+            case 8: SFMHIP_TSDF(4, false); break;
+            default: SFMHIP_TSDF(4, true); break;
         }
-#undef SFMHIP_TSDF_M
 #undef SFMHIP_TSDF
         const int rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) return rc;

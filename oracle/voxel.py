@@ -151,10 +151,16 @@ def render(grid, bmin, bmax, mask_mode, rays_o, rays_d, z) -> np.ndarray:
 def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
     """Build-defined TSDF update, in place on copies; returns (T, Wt).
 
-    voxel (z,y,x) -> world bmin + idx*(bmax-bmin)/(R-1) (align_corners, x->W);
-    Xc = R v + t (left-to-right); skip Zc <= 0; iz = 1/Zc; u = (fx Xc) iz + cx;
-    pixel = floor(u + 0.5); skip off-image or depth <= 0; sdf = depth - Zc;
-    skip sdf < -mu; tsdf = min(1, sdf * (1/mu)); T = (T W + tsdf)/(W + 1); W += 1."""
+    Every f32 operation below is one IEEE round-to-nearest step, in the order
+    written (the HIP kernel tsdf_kernel computes exactly these, two voxels per
+    lane in packed f32):
+      voxel (z,y,x) -> v = bmin + idx*(bmax-bmin)/(R-1)  (align_corners, x->W)
+      Q = (P[r,0] vx + P[r,2] vz) + P[r,3];  c_r = P[r,1] vy + Q      (r = X, Y, Z rows)
+      frames with any non-finite or |.| >= 2^60 pose/intrinsic are skipped
+      skip unless 2^-60 <= Zc < 2^60;  iz = 1/Zc
+      pixel = floor((fx Xc) iz + (cx + 0.5)), floor((fy Yc) iz + (cy + 0.5))
+      skip off-image or depth <= 0; sdf = depth - Zc; skip sdf < -mu
+      tsdf = min(1, sdf * (1/mu)); T = (T W + tsdf)/(W + 1); W += 1."""
     T = np.array(T, F32, copy=True)
     Wt = np.array(Wt, F32, copy=True)
     D, H, W = T.shape
@@ -173,19 +179,23 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
     K = np.asarray(K, F32).reshape(F, 4)
     tr = F32(trunc)
     inv_tr = F32(1) / tr
+    big, zlo, zhi = F32(2.0 ** 60), F32(2.0 ** -60), F32(2.0 ** 60)
     Ts, Ws = T[z0:z1], Wt[z0:z1]
     for f in range(F):
         P = poses[f]
-        Xc = P[0] * vx + P[1] * vy + P[2] * vz + P[3]
-        Yc = P[4] * vx + P[5] * vy + P[6] * vz + P[7]
-        Zc = P[8] * vx + P[9] * vy + P[10] * vz + P[11]
-        ok = Zc > 0
+        with np.errstate(invalid="ignore"):
+            if not (np.abs(np.concatenate([P, K[f]])) < big).all():
+                continue
+        Xc = P[1] * vy + ((P[0] * vx + P[2] * vz) + P[3])
+        Yc = P[5] * vy + ((P[4] * vx + P[6] * vz) + P[7])
+        Zc = P[9] * vy + ((P[8] * vx + P[10] * vz) + P[11])
+        ok = (Zc >= zlo) & (Zc < zhi)
+        cxh = K[f, 2] + F32(0.5)
+        cyh = K[f, 3] + F32(0.5)
         with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
             iz = F32(1) / np.where(ok, Zc, F32(1))
-            u = (K[f, 0] * Xc) * iz + K[f, 2]
-            v = (K[f, 1] * Yc) * iz + K[f, 3]
-            fu = np.floor(u + F32(0.5))
-            fv = np.floor(v + F32(0.5))
+            fu = np.floor((K[f, 0] * Xc) * iz + cxh)
+            fv = np.floor((K[f, 1] * Yc) * iz + cyh)
         ok &= (fu >= 0) & (fu < Wd) & (fv >= 0) & (fv < Hd)
         ui = np.where(ok, fu, 0).astype(np.int64)
         vi = np.where(ok, fv, 0).astype(np.int64)

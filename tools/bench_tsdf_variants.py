@@ -1,6 +1,6 @@
 """A/B the TSDF kernel configurations on the C5 workload in one process,
 interleaved rounds; every config must give the same grids as the first.
-usage: python tools/bench_tsdf_variants.py "KIND=0,U=4,CHUNK=32;KIND=1,ROWS=16;..."
+usage: python tools/bench_tsdf_variants.py "U=4,CHUNK=24;U=2,SBX=4;..."
 (keys are SFMHIP_TSDF_<KEY> environment knobs read per call)"""
 import importlib
 import os
