@@ -398,12 +398,162 @@ __device__ __forceinline__ bool tame(float t, float w) {
     return fabsf(t) <= 0x1p30f && w >= 0.f && w <= 0x1p24f;
 }
 
+// ---------------------------------------------------------------------------
+// TSDF culling (exact: it only drops (tile, frame) pairs in which provably no
+// voxel of the 8x8x8 workgroup tile would update).  Two small pre-passes per
+// launch chunk:
+//   depth_blockmax_kernel: max depth of every 16x16 pixel block (NaN ignored:
+//     a NaN depth never updates), one coalesced pass over the chunk's maps;
+//   tsdf_cull_kernel: one lane per (tile, frame), 32 frames per ballot word.
+//     The tile's 8 corner voxels are projected in f64; if any corner is not
+//     comfortably in front of the camera the pair is kept.  Otherwise the
+//     pixel bbox of the corners (the projection of a box in front of the
+//     camera is the hull of its corner projections), widened by a margin far
+//     above the kernel's f32 rounding, bounds every voxel's pixel, and the
+//     tile's min corner depth (Zc is affine in the voxel position) bounds every
+//     voxel's Zc from below.  Culled: bbox off-image, or every block under it
+//     has max depth <= 0, or max depth + mu < min Zc (sdf < -mu everywhere).
+constexpr int kCullBlock = 16;
+constexpr int kCullMaxBlocks = 256;   // larger footprints are simply kept
+
+// VEC: Wd % 4 == 0, one float4 (4 pixels) per lane, 4 lanes per block column,
+// all 16 rows' loads in flight.  Otherwise one pixel per lane, 16 lanes per block.
+template <bool VEC>
+__global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __restrict__ depth, int F, int Hd, int Wd,
+                                                             int nbu, int nbv, float* __restrict__ bmax) {
+    const int f = blockIdx.z, bv = blockIdx.y;
+    const float* dp = depth + (size_t)f * Hd * Wd;
+    const int r0 = bv * kCullBlock, nr = min(kCullBlock, Hd - r0);
+    float m = -__builtin_inff();
+    if (VEC) {
+        const int u = (blockIdx.x * 256 + threadIdx.x) * 4;
+        if (u < Wd) {
+            float4 q[kCullBlock];
+#pragma unroll
+            for (int r = 0; r < kCullBlock; ++r)
+                q[r] = r < nr ? *reinterpret_cast<const float4*>(dp + (size_t)(r0 + r) * Wd + u)
+                              : make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff());
+#pragma unroll
+            for (int r = 0; r < kCullBlock; ++r) m = fmaxf(m, fmaxf(fmaxf(q[r].x, q[r].y), fmaxf(q[r].z, q[r].w)));
+        }
+        m = fmaxf(m, __shfl_xor(m, 1, 4));
+        m = fmaxf(m, __shfl_xor(m, 2, 4));
+        const int bu = u / kCullBlock;
+        if ((threadIdx.x & 3) == 0 && bu < nbu) bmax[((size_t)f * nbv + bv) * nbu + bu] = m;
+    } else {
+        const int u = blockIdx.x * 256 + threadIdx.x;
+        if (u < Wd)
+            for (int r = 0; r < nr; ++r) m = fmaxf(m, dp[(size_t)(r0 + r) * Wd + u]);
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 16));
+        const int bu = u / kCullBlock;
+        if ((threadIdx.x & 15) == 0 && bu < nbu) bmax[((size_t)f * nbv + bv) * nbu + bu] = m;
+    }
+}
+
+// One lane per (wave sub-tile, frame); sub-tile = the 8 x 2 x 8 voxels of one
+// wave of the workgroup tile.  Interval bounds on the affine camera
+// coordinates over the sub-tile (centre +- sum |P_rj| h_j), pixel bounds from
+// the X/Z and Y/Z interval quotients (a superset of the exact projection).
+constexpr int kCullSub = 4;   // waves per workgroup tile
+__global__ __launch_bounds__(256) void tsdf_cull_kernel(int D, int H, int W, int z0, int z1, int F, int Hd, int Wd,
+                                                        const float* __restrict__ poses, const float* __restrict__ Kf,
+                                                        Bounds B, float trunc, const float* __restrict__ bmax,
+                                                        int nbu, int nbv, int per_tile, unsigned* __restrict__ cull) {
+    // per_tile = 1: one test for the whole 8x8x8 tile (written to its 4 wave slots)
+    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
+    const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
+    const int64_t nsub = (int64_t)ntx * nty * ntz * per_tile;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t sub = g >> 5;
+    const int f = (int)(g & 31);
+    bool skip = false;
+    if (sub < nsub && f < F) {
+        const int64_t tile = sub / per_tile;
+        const int w = (int)(sub % per_tile);
+        const int bx = (int)(tile % ntx), by = (int)((tile / ntx) % nty), bz = (int)(tile / ((int64_t)ntx * nty));
+        const int xa = bx * kTsdfTX, xb = min(W, xa + kTsdfTX) - 1;
+        const int ya = by * kTsdfTY + (kTsdfTY / per_tile) * w, yb = min(H, ya + kTsdfTY / per_tile) - 1;
+        const int za = z0 + bz * kTsdfTZ, zb = min(z1, za + kTsdfTZ) - 1;
+        if (ya <= yb) {
+            const double sx = ((double)B.mx[0] - B.mn[0]) / (W - 1), sy = ((double)B.mx[1] - B.mn[1]) / (H - 1),
+                         sz = ((double)B.mx[2] - B.mn[2]) / (D - 1);
+            const double cxw = B.mn[0] + 0.5 * (xa + xb) * sx, hx = 0.5 * (xb - xa) * fabs(sx);
+            const double cyw = B.mn[1] + 0.5 * (ya + yb) * sy, hy = 0.5 * (yb - ya) * fabs(sy);
+            const double czw = B.mn[2] + 0.5 * (za + zb) * sz, hz = 0.5 * (zb - za) * fabs(sz);
+            const double mxw = fabs(cxw) + hx, myw = fabs(cyw) + hy, mzw = fabs(czw) + hz;   // |coord| bounds
+            const float* P = poses + f * 12;
+            const float* k = Kf + f * 4;
+            double c[3], e[3], mag[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const double p0 = P[4 * r], p1 = P[4 * r + 1], p2 = P[4 * r + 2], p3 = P[4 * r + 3];
+                c[r] = p0 * cxw + p1 * cyw + p2 * czw + p3;
+                e[r] = fabs(p0) * hx + fabs(p1) * hy + fabs(p2) * hz;
+                mag[r] = fabs(p0) * mxw + fabs(p1) * myw + fabs(p2) * mzw + fabs(p3);
+            }
+            // f32 error of the kernel's Zc / Xc / Yc (unit roundoff 2^-24, generous op counts)
+            const double eps = 0x1p-24;
+            const double dz = 8 * eps * mag[2];
+            const double zlo = c[2] - e[2] - dz, zhi = c[2] + e[2] + dz;
+            if (zlo > 1e-3 && zhi < 1e30 && c[0] == c[0] && c[1] == c[1]) {
+                const double izl = 1.0 / zlo, izh = 1.0 / zhi;
+                const double xl = c[0] - e[0] - 8 * eps * mag[0], xh = c[0] + e[0] + 8 * eps * mag[0];
+                const double yl = c[1] - e[1] - 8 * eps * mag[1], yh = c[1] + e[1] + 8 * eps * mag[1];
+                const double qx0 = fmin(fmin(xl * izl, xl * izh), fmin(xh * izl, xh * izh));
+                const double qx1 = fmax(fmax(xl * izl, xl * izh), fmax(xh * izl, xh * izh));
+                const double qy0 = fmin(fmin(yl * izl, yl * izh), fmin(yh * izl, yh * izh));
+                const double qy1 = fmax(fmax(yl * izl, yl * izh), fmax(yh * izl, yh * izh));
+                const double fx = k[0], fy = k[1];
+                const double ua = fx * qx0, ub = fx * qx1, va = fy * qy0, vb = fy * qy1;
+                const double um0 = fmin(ua, ub) + k[2] + 0.5, um1 = fmax(ua, ub) + k[2] + 0.5;
+                const double vm0 = fmin(va, vb) + k[3] + 0.5, vm1 = fmax(va, vb) + k[3] + 0.5;
+                // rounding of (f X) iz + c: a few ulps of the magnitudes involved
+                const double du = 8 * eps * (fmax(fabs(um0), fabs(um1)) + fabs((double)k[2]) + 1) + 1e-3;
+                const double dv = 8 * eps * (fmax(fabs(vm0), fabs(vm1)) + fabs((double)k[3]) + 1) + 1e-3;
+                if (um0 > -1e9 && um1 < 1e9 && vm0 > -1e9 && vm1 < 1e9) {
+                    const int u0 = (int)floor(um0 - du), u1 = (int)floor(um1 + du);
+                    const int v0 = (int)floor(vm0 - dv), v1 = (int)floor(vm1 + dv);
+                    if (u1 < 0 || v1 < 0 || u0 >= Wd || v0 >= Hd) {
+                        skip = true;
+                    } else {
+                        const int bu0 = max(u0, 0) / kCullBlock, bu1 = min(u1, Wd - 1) / kCullBlock;
+                        const int bv0 = max(v0, 0) / kCullBlock, bv1 = min(v1, Hd - 1) / kCullBlock;
+                        const int nu = bu1 - bu0 + 1, nb = nu * (bv1 - bv0 + 1);
+                        if (nb <= kCullMaxBlocks) {
+                            const float* bp = bmax + ((size_t)f * nbv + bv0) * nbu + bu0;
+                            float m = -__builtin_inff();
+                            for (int bv = bv0; bv <= bv1; ++bv, bp += nbu) {
+                                int i = 0;
+                                for (; i + 4 <= nu; i += 4)   // 4 independent loads in flight
+                                    m = fmaxf(fmaxf(m, fmaxf(bp[i], bp[i + 1])), fmaxf(bp[i + 2], bp[i + 3]));
+                                for (; i < nu; ++i) m = fmaxf(m, bp[i]);
+                            }
+                            // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for
+                            // the rounding of (depth - Zc), so !(sdf < -trunc) fails everywhere
+                            skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * eps) + 1e-30 < zlo);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    const unsigned long long bal = __ballot(skip);
+    const int lane = threadIdx.x & 63;
+    if ((lane & 31) == 0 && sub < nsub) {
+        const unsigned word = (unsigned)(bal >> lane);
+        if (per_tile == kCullSub) cull[sub] = word;
+        else
+            for (int w = 0; w < kCullSub; ++w) cull[(sub / per_tile) * kCullSub + w] = word;
+    }
+}
+
 template <int U, bool SWZ>
 __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float* __restrict__ Wt, int D, int H,
                                                    int W, int z0, int z1, const float* __restrict__ depth, int F,
                                                    int Hd, int Wd, const float* __restrict__ poses,
                                                    const float* __restrict__ Kf, Bounds B, float trunc,
-                                                   SuperBrick SB) {
+                                                   SuperBrick SB, const unsigned* __restrict__ cull) {
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (SWZ) {
         const int nbx = (W + kTsdfTX - 1) / kTsdfTX, nby = (H + kTsdfTY - 1) / kTsdfTY;
@@ -452,14 +602,34 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
     const size_t frame = (size_t)Hd * Wd;
     const int nbytes = (int)(frame * 4);   // host-checked < 2^31
     const int Wd4 = Wd * 4;                 // < 2^24: exact in v_mul_u32_u24
-    for (int f0 = 0; f0 < F; f0 += U) {
+    // Frames to fuse, in order: with a cull mask (F <= 32) the frames whose
+    // (tile, frame) test proved that no voxel of this tile updates are dropped,
+    // and the next U surviving frames are issued together.
+    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
+    unsigned todo = F >= 32 ? ~0u : ((1u << F) - 1u);
+    if (cull) todo &= ~cull[(((size_t)bz * nty + by) * ntx + bx) * kCullSub + (threadIdx.x >> 6)];
+    for (int f0 = 0;; f0 += U) {
+        int fr[U];
+        bool lv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (F <= 32) {
+                lv[u] = todo != 0u;
+                fr[u] = lv[u] ? __builtin_ctz(todo) : F - 1;
+                todo &= todo - 1u;
+            } else {
+                lv[u] = f0 + u < F;
+                fr[u] = lv[u] ? f0 + u : F - 1;
+            }
+        }
+        if (!lv[0]) break;
         f2 zc[U];
         float d0[U], d1[U];
         bool ok0[U], ok1[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const bool live = f0 + u < F;   // wave-uniform
-            const int f = live ? f0 + u : F - 1;
+            const bool live = lv[u];   // wave-uniform
+            const int f = fr[u];
             const float* r = cam + f * 16;
             const f2 Q = (f2{r[0], r[1]} * f2s(vx) + f2{r[2], r[3]} * f2s(vz)) + f2{r[4], r[5]};
             const float Qz = (r[6] * vx + r[7] * vz) + r[8];
@@ -894,7 +1064,7 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     // (super-brick XCD order), SFMHIP_TSDF_SBX/SBY/SBZ and SFMHIP_TSDF_CHUNK (frames per
     // launch: a shorter chunk bounds how many frames the resident workgroups
     // touch at once, i.e. the depth working set in L2 / MALL).
-    const int unroll = env_int("SFMHIP_TSDF_U", 4);
+    const int unroll = env_int("SFMHIP_TSDF_U", 1);
     const int swz = env_int("SFMHIP_TSDF_SWZ", 1);
     const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 4)), std::max(1, env_int("SFMHIP_TSDF_SBY", 2)),
                         std::max(1, env_int("SFMHIP_TSDF_SBZ", 4))};
@@ -908,15 +1078,42 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
         grid = dim3((unsigned)slots, 1, 1);
     }
     const Bounds bb = make_bounds(bmin, bmax);
+    hipStream_t st = as_stream(stream);
+    // Culling scratch (stream-ordered; SFMHIP_TSDF_CULL=0 disables culling, for A/B runs).
+    // Any allocation failure only disables the culling: the fusion itself is unchanged.
+    const int nbu = ceil_div(Wd, kCullBlock), nbv = ceil_div(Hd, kCullBlock);
+    const int64_t nsub = (int64_t)nbx * nby * nbz * kCullSub;
+    const int per_tile = env_int("SFMHIP_TSDF_CULLSUB", 1) == 4 ? kCullSub : 1;
+    const int64_t ntests = (int64_t)nbx * nby * nbz * per_tile;
+    float* cbmax = nullptr;
+    unsigned* cmask = nullptr;
+    if (env_int("SFMHIP_TSDF_CULL", 1) && chunk <= 32) {
+        if (hipMallocAsync((void**)&cbmax, (size_t)chunk * nbu * nbv * sizeof(float), st) != hipSuccess) cbmax = nullptr;
+        if (cbmax && hipMallocAsync((void**)&cmask, (size_t)nsub * sizeof(unsigned), st) != hipSuccess) {
+            (void)hipFreeAsync(cbmax, st);
+            cbmax = nullptr;
+        }
+        (void)hipGetLastError();
+    }
     // frame chunks run in order on the stream, so per-voxel update order is kept
     for (int f0 = 0; f0 < F; f0 += chunk) {
         const int nf = std::min(chunk, F - f0);
         const float* dp = depth + (size_t)f0 * Hd * Wd;
         const float* pp = poses + (size_t)f0 * 12;
         const float* kp = Kf + (size_t)f0 * 4;
+        if (cmask) {
+            if (Wd % 4 == 0)
+                hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st,
+                                   dp, nf, Hd, Wd, nbu, nbv, cbmax);
+            else
+                hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st,
+                                   dp, nf, Hd, Wd, nbu, nbv, cbmax);
+            hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)ceil_div(ntests * 32, (int64_t)256)), dim3(256), 0, st,
+                               D, H, W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, cbmax, nbu, nbv, per_tile, cmask);
+        }
 #define SFMHIP_TSDF(UU, SS)                                                                                   \
-    hipLaunchKernelGGL((tsdf_kernel<UU, SS>), grid, dim3(256), (size_t)nf * 16 * sizeof(float),               \
-                       as_stream(stream), T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, pp, kp, bb, trunc, sb)
+    hipLaunchKernelGGL((tsdf_kernel<UU, SS>), grid, dim3(256), (size_t)nf * 16 * sizeof(float), st, T, Wt, D, H, \
+                       W, z0, z1, dp, nf, Hd, Wd, pp, kp, bb, trunc, sb, cmask)
         switch (unroll * 2 + (swz ? 1 : 0)) {
             case 2: SFMHIP_TSDF(1, false); break;
             case 3: SFMHIP_TSDF(1, true); break;
@@ -928,6 +1125,10 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
 #undef SFMHIP_TSDF
         const int rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) return rc;
+    }
+    if (cmask) {
+        (void)hipFreeAsync(cmask, st);
+        (void)hipFreeAsync(cbmax, st);
     }
     return SFMHIP_OK;
 }

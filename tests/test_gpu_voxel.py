@@ -134,6 +134,21 @@ def test_tsdf_edge_cases_bitexact(sfm, gpu):
     assert (Wr > W0).mean() > 0.1
 
 
+def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
+    """The (tile, frame) culling pre-pass only drops work: grids with and
+    without it are bit-identical (full-resolution frames, 96^3 grid, z-slab)."""
+    depth, poses, K = syn.tsdf_scene(10, seed=3)
+    out = []
+    for cull in ("0", "1"):
+        monkeypatch.setenv("SFMHIP_TSDF_CULL", cull)
+        T = torch.zeros((96, 96, 96), dtype=torch.float32, device=gpu)
+        W = torch.zeros_like(T)
+        sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95, z0=5, z1=90)
+        out.append((T.cpu(), W.cpu()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert (out[0][1] > 0).float().mean() > 0.3
+
+
 def test_tsdf_zslab_split_equals_whole(sfm, gpu):
     R, depth, poses, K = _tsdf_case(R=40, F=6)
     args = (torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K), (-1, -1, -1), (1, 1, 1), 0.12)
