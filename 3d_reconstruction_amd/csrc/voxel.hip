@@ -359,7 +359,7 @@ constexpr int kTsdfTX = 8, kTsdfTY = 8, kTsdfTZ = 8;    // workgroup tile: 4 wav
 // Workgroups resident on one XCD at the same time then project onto one
 // compact image region per frame, so the depth lines they gather stay in that
 // XCD's L2 (speed only, never correctness).
-struct SuperBrick { int x, y, z; };
+struct SuperBrick { int x, y, z, il; };   // il: super-bricks dealt round-robin over the XCDs
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 f2s(float a) { return f2{a, a}; }
@@ -558,8 +558,17 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
     if (SWZ) {
         const int nbx = (W + kTsdfTX - 1) / kTsdfTX, nby = (H + kTsdfTY - 1) / kTsdfTY;
         const int nsx = (nbx + SB.x - 1) / SB.x, nsy = (nby + SB.y - 1) / SB.y;
-        const int L = xcd_remap(blockIdx.x, gridDim.x);
-        const int sb = L / (SB.x * SB.y * SB.z), in = L % (SB.x * SB.y * SB.z);
+        const int sbn = SB.x * SB.y * SB.z;
+        int sb, in;
+        if (SB.il) {   // XCD x fuses super-bricks x, x+8, x+16, ...: spreads uneven (culled) work
+            const int j = blockIdx.x / kNumXcd;
+            sb = (j / sbn) * kNumXcd + blockIdx.x % kNumXcd;
+            in = j % sbn;
+        } else {       // XCD x fuses one contiguous range of super-bricks
+            const int L = xcd_remap(blockIdx.x, gridDim.x);
+            sb = L / sbn;
+            in = L % sbn;
+        }
         const int sx = sb % nsx, sy = (sb / nsx) % nsy, sz = sb / (nsx * nsy);
         bx = sx * SB.x + in % SB.x;
         by = sy * SB.y + (in / SB.x) % SB.y;
@@ -1066,14 +1075,18 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     // touch at once, i.e. the depth working set in L2 / MALL).
     const int unroll = env_int("SFMHIP_TSDF_U", 1);
     const int swz = env_int("SFMHIP_TSDF_SWZ", 1);
-    const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 4)), std::max(1, env_int("SFMHIP_TSDF_SBY", 2)),
-                        std::max(1, env_int("SFMHIP_TSDF_SBZ", 4))};
+    // default: super-bricks of 3 x 2 x 8 tiles (24 x 16 x 64 voxels) dealt round-robin over the
+    // XCDs (sweeps in tools/bench_tsdf_variants.py; with culling the work per tile is uneven, and
+    // the interleave plus a width that does not divide the grid spreads it over the XCDs)
+    const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 3)), std::max(1, env_int("SFMHIP_TSDF_SBY", 2)),
+                        std::max(1, env_int("SFMHIP_TSDF_SBZ", 8)), env_int("SFMHIP_TSDF_IL", 1)};
     const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", 24)));
     const int nbx = ceil_div(W, kTsdfTX), nby = ceil_div(H, kTsdfTY), nbz = ceil_div(z1 - z0, kTsdfTZ);
     dim3 grid(nbx, nby, nbz);
     if (swz) {
-        const int64_t slots = (int64_t)ceil_div(nbx, sb.x) * ceil_div(nby, sb.y) * ceil_div(nbz, sb.z) *
-                              (sb.x * sb.y * sb.z);
+        int64_t nsb = (int64_t)ceil_div(nbx, sb.x) * ceil_div(nby, sb.y) * ceil_div(nbz, sb.z);
+        if (sb.il) nsb = (nsb + kNumXcd - 1) / kNumXcd * kNumXcd;   // padding super-bricks exit at once
+        const int64_t slots = nsb * (sb.x * sb.y * sb.z);
         SFMHIP_REQUIRE(slots < INT_MAX, "sfmhip_tsdf_integrate: grid too large");
         grid = dim3((unsigned)slots, 1, 1);
     }
