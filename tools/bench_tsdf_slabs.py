@@ -1,0 +1,36 @@
+"""Time the C5 fusion of each z-slab of an N-way split on one GPU (what each rank of
+`bench.py --gpus N` fuses): python tools/bench_tsdf_slabs.py 8"""
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sfm = importlib.import_module("3d_reconstruction_amd")
+syn = importlib.import_module("3d_reconstruction_amd.synthetic")
+sdist = importlib.import_module("3d_reconstruction_amd.dist")
+dev = torch.device("cuda", 0)
+depth, poses, K = syn.tsdf_scene(257, syn.IMG_H, syn.IMG_W, device=dev)
+R = 256
+T = torch.zeros((R, R, R), dtype=torch.float32, device=dev)
+W = torch.zeros_like(T)
+for n in [int(a) for a in sys.argv[1:]] or [8]:
+    for cull in ("0", "1"):
+        os.environ["SFMHIP_TSDF_CULL"] = cull
+        ts = []
+        for r in range(n):
+            z0, z1 = sdist.shard_range(R, r, n)
+            best = 1e9
+            for _ in range(3):
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / (R - 1), z0, z1)
+                e1.record()
+                torch.cuda.synchronize()
+                best = min(best, e0.elapsed_time(e1))
+            ts.append(best)
+        print(f"N={n} CULL={cull}: max {max(ts):.3f} ms  mean {np.mean(ts):.3f}  slabs {[round(t, 2) for t in ts]}",
+              flush=True)
