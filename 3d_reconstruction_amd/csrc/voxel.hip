@@ -1115,6 +1115,7 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
         (void)hipGetLastError();
     }
     // frame chunks run in order on the stream, so per-voxel update order is kept
+    int rc = SFMHIP_OK;
     for (int f0 = 0; f0 < F; f0 += chunk) {
         const int nf = std::min(chunk, F - f0);
         const float* dp = depth + (size_t)f0 * Hd * Wd;
@@ -1142,14 +1143,12 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
             default: SFMHIP_TSDF(4, true); break;
         }
 #undef SFMHIP_TSDF
-        const int rc = check_launch("tsdf_kernel");
-        if (rc != SFMHIP_OK) return rc;
+        rc = check_launch("tsdf_kernel");
+        if (rc != SFMHIP_OK) break;
     }
-    if (cmask) {
-        (void)hipFreeAsync(cmask, st);
-        (void)hipFreeAsync(cbmax, st);
-    }
-    return SFMHIP_OK;
+    if (cmask) (void)hipFreeAsync(cmask, st);
+    if (cbmax) (void)hipFreeAsync(cbmax, st);
+    return rc;
 }
 
 extern "C" int sfmhip_grid_from_voxel_major(const float* grid_vm, int C, int D, int H, int W, float* grid,
