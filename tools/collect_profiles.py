@@ -21,24 +21,26 @@ for a, b in copies.items():
 
 
 def per_dispatch(kind):
-    """average FETCH_SIZE / WRITE_SIZE (KB) per dispatch over the pass CSVs"""
+    """{kernel: {counter: average per dispatch}} over the pass CSVs"""
     out = {}
     for i, f in enumerate(sorted(glob.glob(os.path.join(src, f"pmc_{kind}_{tag}", "p*", "p_counter_collection.csv")))):
         shutil.copy(f, os.path.join(dst, "pmc_raw", f"{kind}_pass{i + 1}.csv"))
         for r in csv.DictReader(open(f)):
-            out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            k = r["Kernel_Name"].split("(")[0]
+            out.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     summ = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"),
                            os.path.join(src, f"pmc_{kind}_{tag}")], capture_output=True, text=True).stdout
     open(os.path.join(dst, f"pmc_{kind}_kernel.txt"), "w").write(summ)
-    return {k: sum(v) / len(v) for k, v in out.items()}
+    return {k: {n: sum(v) / len(v) for n, v in c.items()} for k, c in out.items()}
 
 
 traffic = {}
 for kind, nd in (("match", 1), ("tsdf", math.ceil(257 / 24))):
-    c = per_dispatch(kind)
-    rd, wr = 2 * c["FETCH_SIZE"] * 1024 * nd, c["WRITE_SIZE"] * 1024 * nd
+    kern = per_dispatch(kind)
+    rd = sum(2 * c["FETCH_SIZE"] * 1024 * nd for c in kern.values())
+    wr = sum(c["WRITE_SIZE"] * 1024 * nd for c in kern.values())
     traffic[kind] = {"bytes_per_step": rd + wr, "read_bytes_per_step": rd, "write_bytes_per_step": wr,
-                     "dispatches_per_step": nd}
+                     "dispatches_per_step": nd, "kernels": sorted(kern)}
 traffic["source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/pmc.sh, GPU round {tag}, "
                      "profiles/r1/pmc_raw); FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half the bytes "
                      "of wide streaming reads); workloads: C3 all-pairs match launch (tools/run_match_once.py), C5 "

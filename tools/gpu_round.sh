@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/bench_prof_$TAG.err || { echo "rocprof failed"; tail -20 gpurun_out/bench_prof_$TAG.err; exit 1; }
 find gpurun_out/prof_$TAG -type f ! -name "*stats*" -delete
 bash tools/pmc.sh match_$TAG match_kernel tools/run_match_once.py || exit 1
-bash tools/pmc.sh tsdf_$TAG tsdf_kernel tools/run_tsdf_once.py || exit 1
+bash tools/pmc.sh tsdf_$TAG "tsdf_kernel|tsdf_cull|depth_blockmax" tools/run_tsdf_once.py || exit 1
 SFMHIP_BENCH_SAME_DEVICE=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --n-img 48 --dist-backend gloo --no-cpu-baseline > gpurun_out/bench_rehearsal_$TAG.json 2> gpurun_out/bench_rehearsal_$TAG.err || { echo "rehearsal failed"; tail -20 gpurun_out/bench_rehearsal_$TAG.err; exit 1; }
 cat gpurun_out/bench_rehearsal_$TAG.json
 du -sh gpurun_out
