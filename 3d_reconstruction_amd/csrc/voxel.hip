@@ -416,12 +416,87 @@ __device__ __forceinline__ bool tame(float t, float w) {
 constexpr int kCullBlock = 16;
 constexpr int kCullMaxBlocks = 256;   // larger footprints are simply kept
 
+// Conservative pixel footprint of the voxel box [xa,xb] x [ya,yb] x [za,zb] in
+// frame (P, k): interval bounds on the affine camera coordinates (centre +-
+// sum |P_rj| h_j) widened by a bound on the fusion kernel's f32 rounding, and
+// the X/Z, Y/Z interval quotients.  Returns 0 (no bound: box not safely in
+// front of the camera), 1 (every voxel's pixel is off-image) or 2 (pixel range
+// [u0,u1] x [v0,v1], clipped to the image, and zlo <= every f32 Zc).
+__device__ int box_footprint(const float* P, const float* k, const Bounds& B, int D, int H, int W, int xa, int xb,
+                             int ya, int yb, int za, int zb, int Hd, int Wd, int& u0, int& u1, int& v0, int& v1,
+                             double& zlo) {
+    const double sx = ((double)B.mx[0] - B.mn[0]) / (W - 1), sy = ((double)B.mx[1] - B.mn[1]) / (H - 1),
+                 sz = ((double)B.mx[2] - B.mn[2]) / (D - 1);
+    const double cxw = B.mn[0] + 0.5 * (xa + xb) * sx, hx = 0.5 * (xb - xa) * fabs(sx);
+    const double cyw = B.mn[1] + 0.5 * (ya + yb) * sy, hy = 0.5 * (yb - ya) * fabs(sy);
+    const double czw = B.mn[2] + 0.5 * (za + zb) * sz, hz = 0.5 * (zb - za) * fabs(sz);
+    const double mxw = fabs(cxw) + hx, myw = fabs(cyw) + hy, mzw = fabs(czw) + hz;   // |coord| bounds
+    double c[3], e[3], mag[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const double p0 = P[4 * r], p1 = P[4 * r + 1], p2 = P[4 * r + 2], p3 = P[4 * r + 3];
+        c[r] = p0 * cxw + p1 * cyw + p2 * czw + p3;
+        e[r] = fabs(p0) * hx + fabs(p1) * hy + fabs(p2) * hz;
+        mag[r] = fabs(p0) * mxw + fabs(p1) * myw + fabs(p2) * mzw + fabs(p3);
+    }
+    // f32 error of the kernel's Zc / Xc / Yc (unit roundoff 2^-24, generous op counts)
+    const double eps = 0x1p-24;
+    const double dz = 8 * eps * mag[2];
+    zlo = c[2] - e[2] - dz;
+    const double zhi = c[2] + e[2] + dz;
+    if (!(zlo > 1e-3 && zhi < 1e30 && c[0] == c[0] && c[1] == c[1])) return 0;
+    const double izl = 1.0 / zlo, izh = 1.0 / zhi;
+    const double xl = c[0] - e[0] - 8 * eps * mag[0], xh = c[0] + e[0] + 8 * eps * mag[0];
+    const double yl = c[1] - e[1] - 8 * eps * mag[1], yh = c[1] + e[1] + 8 * eps * mag[1];
+    const double qx0 = fmin(fmin(xl * izl, xl * izh), fmin(xh * izl, xh * izh));
+    const double qx1 = fmax(fmax(xl * izl, xl * izh), fmax(xh * izl, xh * izh));
+    const double qy0 = fmin(fmin(yl * izl, yl * izh), fmin(yh * izl, yh * izh));
+    const double qy1 = fmax(fmax(yl * izl, yl * izh), fmax(yh * izl, yh * izh));
+    const double ua = (double)k[0] * qx0, ub = (double)k[0] * qx1, va = (double)k[1] * qy0, vb = (double)k[1] * qy1;
+    const double um0 = fmin(ua, ub) + k[2] + 0.5, um1 = fmax(ua, ub) + k[2] + 0.5;
+    const double vm0 = fmin(va, vb) + k[3] + 0.5, vm1 = fmax(va, vb) + k[3] + 0.5;
+    if (!(um0 > -1e9 && um1 < 1e9 && vm0 > -1e9 && vm1 < 1e9)) return 0;
+    // rounding of (f X) iz + c: a few ulps of the magnitudes involved
+    const double du = 8 * eps * (fmax(fabs(um0), fabs(um1)) + fabs((double)k[2]) + 1) + 1e-3;
+    const double dv = 8 * eps * (fmax(fabs(vm0), fabs(vm1)) + fabs((double)k[3]) + 1) + 1e-3;
+    u0 = (int)floor(um0 - du);
+    u1 = (int)floor(um1 + du);
+    v0 = (int)floor(vm0 - dv);
+    v1 = (int)floor(vm1 + dv);
+    if (u1 < 0 || v1 < 0 || u0 >= Wd || v0 >= Hd) return 1;
+    u0 = max(u0, 0); u1 = min(u1, Wd - 1); v0 = max(v0, 0); v1 = min(v1, Hd - 1);
+    return 2;
+}
+
+// Per frame: the depth blocks the slab [z0, z1) can touch (int4 {bu0, bu1, bv0,
+// bv1}; an empty range when the whole slab is off-image, every block when the
+// footprint cannot be bounded).  The block-max pass fills only these blocks and
+// the tile test reads only inside them.
+__global__ void tsdf_footprint_kernel(int D, int H, int W, int z0, int z1, int F, int Hd, int Wd,
+                                      const float* __restrict__ poses, const float* __restrict__ Kf, Bounds B,
+                                      int nbu, int nbv, int4* __restrict__ range) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    int u0, u1, v0, v1;
+    double zlo;
+    const int st = box_footprint(poses + f * 12, Kf + f * 4, B, D, H, W, 0, W - 1, 0, H - 1, z0, z1 - 1, Hd, Wd, u0,
+                                 u1, v0, v1, zlo);
+    range[f] = st == 2   ? make_int4(u0 / kCullBlock, u1 / kCullBlock, v0 / kCullBlock, v1 / kCullBlock)
+               : st == 1 ? make_int4(1, 0, 1, 0)
+                         : make_int4(0, nbu - 1, 0, nbv - 1);
+}
+
 // VEC: Wd % 4 == 0, one float4 (4 pixels) per lane, 4 lanes per block column,
 // all 16 rows' loads in flight.  Otherwise one pixel per lane, 16 lanes per block.
 template <bool VEC>
 __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __restrict__ depth, int F, int Hd, int Wd,
-                                                             int nbu, int nbv, float* __restrict__ bmax) {
+                                                             int nbu, int nbv, const int4* __restrict__ range,
+                                                             float* __restrict__ bmax) {
     const int f = blockIdx.z, bv = blockIdx.y;
+    const int4 rg = range[f];                       // blocks the slab can touch in this frame
+    if (bv < rg.z || bv > rg.w) return;
+    const int ucol0 = blockIdx.x * (VEC ? 1024 : 256);
+    if (ucol0 / kCullBlock > rg.y || (ucol0 + (VEC ? 1024 : 256) - 1) / kCullBlock < rg.x) return;
     const float* dp = depth + (size_t)f * Hd * Wd;
     const int r0 = bv * kCullBlock, nr = min(kCullBlock, Hd - r0);
     float m = -__builtin_inff();
@@ -459,7 +534,8 @@ constexpr int kCullSub = 4;   // waves per workgroup tile
 __global__ __launch_bounds__(256) void tsdf_cull_kernel(int D, int H, int W, int z0, int z1, int F, int Hd, int Wd,
                                                         const float* __restrict__ poses, const float* __restrict__ Kf,
                                                         Bounds B, float trunc, const float* __restrict__ bmax,
-                                                        int nbu, int nbv, int per_tile, unsigned* __restrict__ cull) {
+                                                        int nbu, int nbv, const int4* __restrict__ range,
+                                                        int per_tile, unsigned* __restrict__ cull) {
     // per_tile = 1: one test for the whole 8x8x8 tile (written to its 4 wave slots)
     const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
     const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
@@ -475,66 +551,29 @@ __global__ __launch_bounds__(256) void tsdf_cull_kernel(int D, int H, int W, int
         const int xa = bx * kTsdfTX, xb = min(W, xa + kTsdfTX) - 1;
         const int ya = by * kTsdfTY + (kTsdfTY / per_tile) * w, yb = min(H, ya + kTsdfTY / per_tile) - 1;
         const int za = z0 + bz * kTsdfTZ, zb = min(z1, za + kTsdfTZ) - 1;
-        if (ya <= yb) {
-            const double sx = ((double)B.mx[0] - B.mn[0]) / (W - 1), sy = ((double)B.mx[1] - B.mn[1]) / (H - 1),
-                         sz = ((double)B.mx[2] - B.mn[2]) / (D - 1);
-            const double cxw = B.mn[0] + 0.5 * (xa + xb) * sx, hx = 0.5 * (xb - xa) * fabs(sx);
-            const double cyw = B.mn[1] + 0.5 * (ya + yb) * sy, hy = 0.5 * (yb - ya) * fabs(sy);
-            const double czw = B.mn[2] + 0.5 * (za + zb) * sz, hz = 0.5 * (zb - za) * fabs(sz);
-            const double mxw = fabs(cxw) + hx, myw = fabs(cyw) + hy, mzw = fabs(czw) + hz;   // |coord| bounds
-            const float* P = poses + f * 12;
-            const float* k = Kf + f * 4;
-            double c[3], e[3], mag[3];
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const double p0 = P[4 * r], p1 = P[4 * r + 1], p2 = P[4 * r + 2], p3 = P[4 * r + 3];
-                c[r] = p0 * cxw + p1 * cyw + p2 * czw + p3;
-                e[r] = fabs(p0) * hx + fabs(p1) * hy + fabs(p2) * hz;
-                mag[r] = fabs(p0) * mxw + fabs(p1) * myw + fabs(p2) * mzw + fabs(p3);
-            }
-            // f32 error of the kernel's Zc / Xc / Yc (unit roundoff 2^-24, generous op counts)
-            const double eps = 0x1p-24;
-            const double dz = 8 * eps * mag[2];
-            const double zlo = c[2] - e[2] - dz, zhi = c[2] + e[2] + dz;
-            if (zlo > 1e-3 && zhi < 1e30 && c[0] == c[0] && c[1] == c[1]) {
-                const double izl = 1.0 / zlo, izh = 1.0 / zhi;
-                const double xl = c[0] - e[0] - 8 * eps * mag[0], xh = c[0] + e[0] + 8 * eps * mag[0];
-                const double yl = c[1] - e[1] - 8 * eps * mag[1], yh = c[1] + e[1] + 8 * eps * mag[1];
-                const double qx0 = fmin(fmin(xl * izl, xl * izh), fmin(xh * izl, xh * izh));
-                const double qx1 = fmax(fmax(xl * izl, xl * izh), fmax(xh * izl, xh * izh));
-                const double qy0 = fmin(fmin(yl * izl, yl * izh), fmin(yh * izl, yh * izh));
-                const double qy1 = fmax(fmax(yl * izl, yl * izh), fmax(yh * izl, yh * izh));
-                const double fx = k[0], fy = k[1];
-                const double ua = fx * qx0, ub = fx * qx1, va = fy * qy0, vb = fy * qy1;
-                const double um0 = fmin(ua, ub) + k[2] + 0.5, um1 = fmax(ua, ub) + k[2] + 0.5;
-                const double vm0 = fmin(va, vb) + k[3] + 0.5, vm1 = fmax(va, vb) + k[3] + 0.5;
-                // rounding of (f X) iz + c: a few ulps of the magnitudes involved
-                const double du = 8 * eps * (fmax(fabs(um0), fabs(um1)) + fabs((double)k[2]) + 1) + 1e-3;
-                const double dv = 8 * eps * (fmax(fabs(vm0), fabs(vm1)) + fabs((double)k[3]) + 1) + 1e-3;
-                if (um0 > -1e9 && um1 < 1e9 && vm0 > -1e9 && vm1 < 1e9) {
-                    const int u0 = (int)floor(um0 - du), u1 = (int)floor(um1 + du);
-                    const int v0 = (int)floor(vm0 - dv), v1 = (int)floor(vm1 + dv);
-                    if (u1 < 0 || v1 < 0 || u0 >= Wd || v0 >= Hd) {
-                        skip = true;
-                    } else {
-                        const int bu0 = max(u0, 0) / kCullBlock, bu1 = min(u1, Wd - 1) / kCullBlock;
-                        const int bv0 = max(v0, 0) / kCullBlock, bv1 = min(v1, Hd - 1) / kCullBlock;
-                        const int nu = bu1 - bu0 + 1, nb = nu * (bv1 - bv0 + 1);
-                        if (nb <= kCullMaxBlocks) {
-                            const float* bp = bmax + ((size_t)f * nbv + bv0) * nbu + bu0;
-                            float m = -__builtin_inff();
-                            for (int bv = bv0; bv <= bv1; ++bv, bp += nbu) {
-                                int i = 0;
-                                for (; i + 4 <= nu; i += 4)   // 4 independent loads in flight
-                                    m = fmaxf(fmaxf(m, fmaxf(bp[i], bp[i + 1])), fmaxf(bp[i + 2], bp[i + 3]));
-                                for (; i < nu; ++i) m = fmaxf(m, bp[i]);
-                            }
-                            // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for
-                            // the rounding of (depth - Zc), so !(sdf < -trunc) fails everywhere
-                            skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * eps) + 1e-30 < zlo);
-                        }
-                    }
+        int u0, u1, v0, v1;
+        double zlo;
+        const int st = ya <= yb ? box_footprint(poses + f * 12, Kf + f * 4, B, D, H, W, xa, xb, ya, yb, za, zb, Hd, Wd,
+                                                u0, u1, v0, v1, zlo)
+                                : 0;
+        if (st == 1) {
+            skip = true;
+        } else if (st == 2) {
+            const int bu0 = u0 / kCullBlock, bu1 = u1 / kCullBlock, bv0 = v0 / kCullBlock, bv1 = v1 / kCullBlock;
+            const int4 rg = range[f];   // only blocks inside the slab's range were computed
+            const int nu = bu1 - bu0 + 1, nb = nu * (bv1 - bv0 + 1);
+            if (nb <= kCullMaxBlocks && bu0 >= rg.x && bu1 <= rg.y && bv0 >= rg.z && bv1 <= rg.w) {
+                const float* bp = bmax + ((size_t)f * nbv + bv0) * nbu + bu0;
+                float m = -__builtin_inff();
+                for (int bv = bv0; bv <= bv1; ++bv, bp += nbu) {
+                    int i = 0;
+                    for (; i + 4 <= nu; i += 4)   // 4 independent loads in flight
+                        m = fmaxf(fmaxf(m, fmaxf(bp[i], bp[i + 1])), fmaxf(bp[i + 2], bp[i + 3]));
+                    for (; i < nu; ++i) m = fmaxf(m, bp[i]);
                 }
+                // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for the
+                // rounding of (depth - Zc), so the kernel's !(sdf < -trunc) test fails everywhere
+                skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * 0x1p-24) + 1e-30 < zlo);
             }
         }
     }
@@ -1078,10 +1117,19 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     // default: super-bricks of 3 x 2 x 8 tiles (24 x 16 x 64 voxels) dealt round-robin over the
     // XCDs (sweeps in tools/bench_tsdf_variants.py; with culling the work per tile is uneven, and
     // the interleave plus a width that does not divide the grid spreads it over the XCDs)
-    const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 3)), std::max(1, env_int("SFMHIP_TSDF_SBY", 2)),
-                        std::max(1, env_int("SFMHIP_TSDF_SBZ", 8)), env_int("SFMHIP_TSDF_IL", 1)};
-    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", 24)));
     const int nbx = ceil_div(W, kTsdfTX), nby = ceil_div(H, kTsdfTY), nbz = ceil_div(z1 - z0, kTsdfTZ);
+    // SFMHIP_TSDF_CULL: 0 off, 2 on, 1 (default) on when the slab is big enough that
+    // the skipped gathers outweigh the block-max pass over every depth pixel (cost
+    // model from the C5 measurements: ~35 % of ~1.7 ps per voxel-frame saved vs
+    // ~0.8 ps per depth pixel read, i.e. worth it above ~1.5 voxels per pixel).
+    const int cull_env = env_int("SFMHIP_TSDF_CULL", 1);
+    const bool cull_pays = (double)(z1 - z0) * H * W >= 1.5 * (double)Hd * Wd;
+    const bool want_cull = cull_env == 2 || (cull_env == 1 && cull_pays);
+    // frames per launch: 24 with culling (its 32-bit frame mask), 64 without (thin
+    // z-slabs of an N-way split: fewer launch tails; tools/bench_tsdf_slabs.py)
+    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", want_cull ? 24 : 64)));
+    const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 3)), std::max(1, env_int("SFMHIP_TSDF_SBY", 2)),
+                        std::max(1, env_int("SFMHIP_TSDF_SBZ", std::min(8, nbz))), env_int("SFMHIP_TSDF_IL", 1)};
     dim3 grid(nbx, nby, nbz);
     if (swz) {
         int64_t nsb = (int64_t)ceil_div(nbx, sb.x) * ceil_div(nby, sb.y) * ceil_div(nbz, sb.z);
@@ -1100,17 +1148,16 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     const int64_t ntests = (int64_t)nbx * nby * nbz * per_tile;
     float* cbmax = nullptr;
     unsigned* cmask = nullptr;
-    // SFMHIP_TSDF_CULL: 0 off, 2 on, 1 (default) on when the slab is big enough that
-    // the skipped gathers outweigh the block-max pass over every depth pixel (cost
-    // model from the C5 measurements: ~35 % of ~1.7 ps per voxel-frame saved vs
-    // ~0.8 ps per depth pixel read, i.e. worth it above ~1.5 voxels per pixel).
-    const int cull_env = env_int("SFMHIP_TSDF_CULL", 1);
-    const bool cull_pays = (double)(z1 - z0) * H * W >= 1.5 * (double)Hd * Wd;
-    if ((cull_env == 2 || (cull_env == 1 && cull_pays)) && chunk <= 32) {
+    int4* crange = nullptr;
+    if (want_cull && chunk <= 32) {
         if (hipMallocAsync((void**)&cbmax, (size_t)chunk * nbu * nbv * sizeof(float), st) != hipSuccess) cbmax = nullptr;
-        if (cbmax && hipMallocAsync((void**)&cmask, (size_t)nsub * sizeof(unsigned), st) != hipSuccess) {
+        if (cbmax && (hipMallocAsync((void**)&cmask, (size_t)nsub * sizeof(unsigned), st) != hipSuccess ||
+                      hipMallocAsync((void**)&crange, (size_t)chunk * sizeof(int4), st) != hipSuccess)) {
+            if (cmask) (void)hipFreeAsync(cmask, st);
             (void)hipFreeAsync(cbmax, st);
             cbmax = nullptr;
+            cmask = nullptr;
+            crange = nullptr;
         }
         (void)hipGetLastError();
     }
@@ -1122,14 +1169,17 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
         const float* pp = poses + (size_t)f0 * 12;
         const float* kp = Kf + (size_t)f0 * 4;
         if (cmask) {
+            hipLaunchKernelGGL(tsdf_footprint_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, D, H, W, z0, z1, nf, Hd,
+                               Wd, pp, kp, bb, nbu, nbv, crange);
             if (Wd % 4 == 0)
                 hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st,
-                                   dp, nf, Hd, Wd, nbu, nbv, cbmax);
+                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmax);
             else
                 hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st,
-                                   dp, nf, Hd, Wd, nbu, nbv, cbmax);
+                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmax);
             hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)ceil_div(ntests * 32, (int64_t)256)), dim3(256), 0, st,
-                               D, H, W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, cbmax, nbu, nbv, per_tile, cmask);
+                               D, H, W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, cbmax, nbu, nbv, crange, per_tile,
+                               cmask);
         }
 #define SFMHIP_TSDF(UU, SS)                                                                                   \
     hipLaunchKernelGGL((tsdf_kernel<UU, SS>), grid, dim3(256), (size_t)nf * 16 * sizeof(float), st, T, Wt, D, H, \
@@ -1146,6 +1196,7 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }
+    if (crange) (void)hipFreeAsync(crange, st);
     if (cmask) (void)hipFreeAsync(cmask, st);
     if (cbmax) (void)hipFreeAsync(cbmax, st);
     return rc;

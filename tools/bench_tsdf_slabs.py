@@ -17,7 +17,7 @@ R = 256
 T = torch.zeros((R, R, R), dtype=torch.float32, device=dev)
 W = torch.zeros_like(T)
 for n in [int(a) for a in sys.argv[1:]] or [8]:
-    for cull in ("0", "1"):
+    for cull in ("0", "1", "2"):
         os.environ["SFMHIP_TSDF_CULL"] = cull
         ts = []
         for r in range(n):
