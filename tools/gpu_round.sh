@@ -8,6 +8,8 @@ TAG=${TAG:-r1}
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu_$TAG.log 2>&1
 echo "pytest exit $?" >> gpurun_out/pytest_gpu_$TAG.log
 tail -3 gpurun_out/pytest_gpu_$TAG.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
+tail -1 gpurun_out/smoke_$TAG.log
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
 export TMPDIR=/tmp
