@@ -21,7 +21,9 @@
 //      interval per lane; one lane per root back-substitutes;
 //   3. all 512 lanes score every model of the chunk (points in registers,
 //      Sampson error as float with an exact division only near the
-//      threshold, wave reductions, LDS atomics);
+//      threshold): the chunk's models are listed once, then scored two at a
+//      time (independent chains for latency hiding at 2 waves/SIMD), each
+//      wave's ballot counts stored per (model, wave) in LDS without atomics;
 //   4. lane 0 replays the chunk in OpenCV's sequential order: a model
 //      replaces the best iff count > max(best, 4), niters shrinks by
 //      RANSACUpdateNumIters — so the chosen model and the iteration count are
@@ -38,6 +40,7 @@ constexpr int kRH = kRThreads / kGL;    // hypotheses per chunk (32)
 constexpr int kMaxModels = 10;
 constexpr int kGS = 224;                // LDS doubles per group
 constexpr int kPB = 4;                  // points per lane per scoring block
+constexpr int kRWaves = kRThreads / 64;
 constexpr int kPThreads = 256;          // recover_pose kernel
 constexpr double kDblEps = 2.220446049250313e-16;
 constexpr double kDblMin = 2.2250738585072014e-308;
@@ -521,6 +524,20 @@ __device__ __forceinline__ bool sampson_in(const double* E, double x1, double y1
     return (float)(num / den) <= tf;
 }
 
+// Sampson numerator and denominator (cv::EMEstimatorCallback::computeError's
+// double arithmetic); inlier iff (float)(num / den) <= t^2 as a float.
+__device__ __forceinline__ void sampson_nd(const double* E, double x1, double y1, double x2, double y2, double& num,
+                                           double& den) {
+    const double ex0 = (E[0] * x1 + E[1] * y1) + E[2];
+    const double ex1 = (E[3] * x1 + E[4] * y1) + E[5];
+    const double ex2 = (E[6] * x1 + E[7] * y1) + E[8];
+    const double et0 = (E[0] * x2 + E[3] * y2) + E[6];
+    const double et1 = (E[1] * x2 + E[4] * y2) + E[7];
+    const double d = (x2 * ex0 + y2 * ex1) + ex2;
+    num = d * d;
+    den = ((ex0 * ex0 + ex1 * ex1) + et0 * et0) + et1 * et1;
+}
+
 __device__ __forceinline__ float sampson(const double* E, double x1, double y1, double x2, double y2) {
     const double ex0 = (E[0] * x1 + E[1] * y1) + E[2];
     const double ex1 = (E[3] * x1 + E[4] * y1) + E[5];
@@ -547,7 +564,9 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
     __shared__ double s_grp[kRH * kGS];
     __shared__ double s_models[kRH * kMaxModels * 9];
     __shared__ int s_nmod[kRH];
-    __shared__ int s_cnt[kRH * kMaxModels];
+    __shared__ int s_cnt[kRH * kMaxModels][kRWaves];   // per-wave inlier counts
+    __shared__ int s_list[kRH * kMaxModels];           // the chunk's models, in replay order
+    __shared__ int s_nlist;
     __shared__ int s_sub[kRH * 5];
     __shared__ double s_best[9];
     __shared__ int s_niters, s_maxgood, s_k0, s_last;
@@ -621,7 +640,7 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
                     s_sub[hh * 5 + i] = idx;
                 }
         }
-        for (int i = tid; i < kRH * kMaxModels; i += kRThreads) s_cnt[i] = 0;
+        for (int i = tid; i < kRH * kMaxModels * kRWaves; i += kRThreads) (&s_cnt[0][0])[i] = 0;
         __syncthreads();
         RPROF(0, tp);
         {
@@ -639,7 +658,15 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
             if (gl == 0) s_nmod[h] = nm;
         }
         __syncthreads();
+        if (tid == 0) {
+            int c = 0;
+            for (int hh = 0; hh < kRH; ++hh)
+                for (int m = 0; m < s_nmod[hh]; ++m) s_list[c++] = hh * kMaxModels + m;
+            s_nlist = c;
+        }
+        __syncthreads();
         RPROF(1, tp);
+        const int nlist = s_nlist, wave = tid >> 6;
         for (int b0 = 0; b0 < n; b0 += kRThreads * kPB) {
             double pt[kPB][4];
             bool val[kPB];
@@ -650,18 +677,49 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
 #pragma unroll
                 for (int c = 0; c < 4; ++c) pt[u][c] = val[u] ? q[4 * i + c] : 0.0;
             }
-            for (int hh = 0; hh < kRH; ++hh) {
-                const int nm = s_nmod[hh];
-                for (int m = 0; m < nm; ++m) {
-                    const double* Em = s_models + (hh * kMaxModels + m) * 9;
-                    double Er[9];
+            for (int j = 0; j < nlist; j += 2) {   // two models per step: independent chains
+                const int ma = s_list[j], mb = s_list[min(j + 1, nlist - 1)];
+                double Ea[9], Eb[9];
 #pragma unroll
-                    for (int e = 0; e < 9; ++e) Er[e] = Em[e];
-                    int cnt = 0;  // wave-uniform: ballots + scalar popcounts
+                for (int e = 0; e < 9; ++e) {
+                    Ea[e] = s_models[ma * 9 + e];
+                    Eb[e] = s_models[mb * 9 + e];
+                }
+                // branch-free margin tests for all 2 x kPB (model, point) pairs, so the
+                // chains interleave; the exact division only where a test is ambiguous
+                double nm[2][kPB], dn[2][kPB];
+                bool in[2][kPB], amb = false;
 #pragma unroll
-                    for (int u = 0; u < kPB; ++u)
-                        cnt += wave_count(val[u] && sampson_in(Er, pt[u][0], pt[u][1], pt[u][2], pt[u][3], tf, tlo, thi));
-                    if (lane == 0 && cnt) atomicAdd(&s_cnt[hh * kMaxModels + m], cnt);
+                for (int u = 0; u < kPB; ++u) {
+                    sampson_nd(Ea, pt[u][0], pt[u][1], pt[u][2], pt[u][3], nm[0][u], dn[0][u]);
+                    sampson_nd(Eb, pt[u][0], pt[u][1], pt[u][2], pt[u][3], nm[1][u], dn[1][u]);
+                }
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+#pragma unroll
+                    for (int u = 0; u < kPB; ++u) {
+                        in[k][u] = nm[k][u] <= dn[k][u] * tlo;
+                        amb = amb || !(in[k][u] || nm[k][u] > dn[k][u] * thi) || !(dn[k][u] > 0);
+                    }
+                if (amb) {   // rare: near the threshold (2^-40 relative) or a degenerate denominator
+#pragma unroll
+                    for (int k = 0; k < 2; ++k)
+#pragma unroll
+                        for (int u = 0; u < kPB; ++u) {
+                            const double n_ = nm[k][u], d_ = dn[k][u];
+                            const bool sure = d_ > 0 && (n_ <= d_ * tlo || n_ > d_ * thi);
+                            if (!sure) in[k][u] = (float)(n_ / d_) <= tf;
+                        }
+                }
+                int ca = 0, cb = 0;  // wave-uniform: ballots + scalar popcounts
+#pragma unroll
+                for (int u = 0; u < kPB; ++u) {
+                    ca += wave_count(val[u] && in[0][u]);
+                    cb += wave_count(val[u] && in[1][u]);
+                }
+                if (lane == 0) {
+                    s_cnt[ma][wave] += ca;
+                    if (j + 1 < nlist) s_cnt[mb][wave] += cb;
                 }
             }
         }
@@ -673,7 +731,8 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
                 const int k = k0 + hh;
                 if (k >= nit) break;
                 for (int m = 0; m < s_nmod[hh]; ++m) {
-                    const int good = s_cnt[hh * kMaxModels + m];
+                    int good = 0;
+                    for (int w = 0; w < kRWaves; ++w) good += s_cnt[hh * kMaxModels + m][w];
                     if (good > max(maxgood, 4)) {
                         for (int e = 0; e < 9; ++e) s_best[e] = s_models[(hh * kMaxModels + m) * 9 + e];
                         maxgood = good;
