@@ -47,6 +47,7 @@ SIGNATURES = {
     "sfmhip_device_arch": [ctypes.c_char_p, _i32],
     "sfmhip_desc_quantize": [_p, _i32, _i32, _i32, _p, _i32, _p, _p],
     "sfmhip_desc_prepare": [_p, _i32, _i32, _i32, _p, _p, _p, _p],
+    "sfmhip_desc_prepare_shifted": [_p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p],
     "sfmhip_match_pairs": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p],
     "sfmhip_mutual_filter": [_p, _p, _i32, _i32, _p],
     "sfmhip_vq": [_p, _i64, _p, _i32, _i32, _p, _p, _p],

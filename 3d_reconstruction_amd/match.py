@@ -20,6 +20,7 @@ LightGlue's ``filter_matches`` semantics (``lightglue/lightglue.py:235-254``).
 """
 from __future__ import annotations
 
+import os
 from fractions import Fraction
 
 import numpy as np
@@ -30,6 +31,7 @@ from ._abi import call, dev, ptr, require_gpu, stream_ptr
 MODE_SIFT = 0    # integer-valued 0..255 descriptors (SIFT): q = x - 128
 MODE_FLOAT = 1   # float descriptors (SuperPoint / DISK, L2-normalised): q = rint(127 x)
 _JB = 128        # m_pad granularity required by the kernel
+_SHIFT = 64      # operand shift of the matcher (sfmhip_desc_prepare_shifted)
 
 
 def _ratio(ratio) -> tuple[int, int]:
@@ -65,8 +67,18 @@ class DescriptorBank:
         self.n_img, self.m_pad, self.d = int(n_img), int(m_pad), int(d)
         self.norms = torch.empty((n_img, m_pad), dtype=torch.int32, device=q.device)
         self.keys = torch.empty((n_img, m_pad), dtype=torch.int32, device=q.device)
-        call("sfmhip_desc_prepare", ptr(self.q), self.n_img, self.m_pad, self.d, ptr(self.n_kpts),
-             ptr(self.norms), ptr(self.keys), stream_ptr())
+        # Matcher operands: q itself, or (default, when every value fits) q + 64 with
+        # adjusted norms/keys -- identical results, non-negative MFMA operands run the
+        # int8 array at a higher clock (SFMHIP_MATCH_SHIFT=0 disables).
+        self.qm = self.q
+        shift = _SHIFT if os.environ.get("SFMHIP_MATCH_SHIFT", "1") != "0" else 0
+        if shift and self.q.numel() and int(self.q.min()) >= -shift and int(self.q.max()) <= 127 - shift:
+            self.qm = torch.empty_like(self.q)
+            call("sfmhip_desc_prepare_shifted", ptr(self.q), self.n_img, self.m_pad, self.d, ptr(self.n_kpts),
+                 shift, ptr(self.qm), ptr(self.norms), ptr(self.keys), stream_ptr())
+        else:
+            call("sfmhip_desc_prepare", ptr(self.q), self.n_img, self.m_pad, self.d, ptr(self.n_kpts),
+                 ptr(self.norms), ptr(self.keys), stream_ptr())
 
     # -- construction -------------------------------------------------------
     @classmethod
@@ -124,7 +136,7 @@ class DescriptorBank:
         return (m0, m1, d1, d2, e1, e2) if with_dist else (m0, m1)
 
     def _launch(self, pr, num, den, m0, d1, d2):
-        call("sfmhip_match_pairs", ptr(self.q), ptr(self.norms), ptr(self.keys), ptr(self.n_kpts),
+        call("sfmhip_match_pairs", ptr(self.qm), ptr(self.norms), ptr(self.keys), ptr(self.n_kpts),
              self.n_img, self.m_pad, self.d, ptr(pr), int(pr.shape[0]), num, den,
              ptr(m0), ptr(d1), ptr(d2), stream_ptr())
 

@@ -56,6 +56,16 @@ int sfmhip_desc_prepare(const int8_t* desc, int n_img, int m_pad, int d,
                         const int32_t* n_kpts, int32_t* norms, int32_t* keys,
                         void* stream);
 
+/* Same as sfmhip_desc_prepare, plus a shifted operand copy for the matcher:
+ * desc_shifted = q + shift on valid rows (0 on padding rows), norms and keys
+ * adjusted so that sfmhip_match_pairs on (desc_shifted, norms, keys) returns
+ * exactly the matches and distances of the unshifted q.  Caller guarantees
+ * q + shift <= 127 for every valid element (shift 64: |q| <= 63 or q = -64).
+ * Speed only (lower MFMA switching power).                      */
+int sfmhip_desc_prepare_shifted(const int8_t* desc, int n_img, int m_pad, int d,
+                                const int32_t* n_kpts, int shift, int8_t* desc_shifted,
+                                int32_t* norms, int32_t* keys, void* stream);
+
 /* For every pair p=(a,b) and every row i < n_kpts[a] of image a: best column j1
  * (lowest index on ties) and second-best distance d2 over j != j1 in image b.
  * matches0[p][i] = j1 if ratio_den^2 * d1 < ratio_num^2 * d2 (exact, int64)

@@ -57,6 +57,36 @@ def test_match_ragged_pairs_bitexact(sfm, gpu, d, mode):
             assert np.array_equal(g2[p, :nk[a]], rd2[p, :nk[a]])
 
 
+@pytest.mark.parametrize("lo,hi", [(-64, 63), (-40, 40), (-65, 63), (-64, 64)])
+def test_match_shifted_operands_identical(sfm, gpu, monkeypatch, lo, hi):
+    """The +64 operand shift (default when every value fits: [-64, 63]) returns the
+    oracle's matches and distances; values outside fall back to the plain operands.
+    Integer data with many duplicate rows (ties) and the range extremes present."""
+    rng = np.random.default_rng(1000 + lo * 7 + hi)
+    n_img, m, d = 4, 300, 256
+    base = rng.integers(lo, hi + 1, (120, d)).astype(np.float32)
+    base[0, :] = lo
+    base[1, :] = hi
+    x = base[rng.integers(0, 120, (n_img, m))] / np.float32(127)
+    nk = np.array([300, 257, 3, 300], np.int32)
+    for i in range(n_img):
+        x[i, nk[i]:] = 0
+    pairs = np.array([[0, 1], [1, 0], [2, 3], [3, 2], [0, 3]], np.int32)
+    out = []
+    for shift in ("1", "0"):
+        monkeypatch.setenv("SFMHIP_MATCH_SHIFT", shift)
+        bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=1)
+        assert (bank.qm is not bank.q) == (shift == "1" and lo >= -64 and hi <= 63)
+        out.append([t.cpu().numpy() for t in bank.match(pairs, ratio=0.8, with_dist=True)])
+    q = om.quantize(x, 1)
+    ref, rd1, rd2 = _oracle_pairs(q, nk, pairs, (4, 5))
+    for m0, d1, d2 in out:
+        assert np.array_equal(m0[:, :m], ref)
+        for p, (a, b) in enumerate(pairs):
+            assert np.array_equal(d1[p, :nk[a]], rd1[p, :nk[a]])
+            assert np.array_equal(d2[p, :nk[a]], rd2[p, :nk[a]])
+
+
 def test_match_ties_lowest_index(sfm, gpu):
     """Equal nonzero best distances at several candidates (same tile, across
     32-row tiles and across 128-row blocks): accepted at ratio 2 and the index

@@ -102,14 +102,16 @@ def test_tsdf_vs_oracle_bitexact(sfm, gpu):
     assert (Wg > 0).mean() > 0.2
 
 
-def test_tsdf_edge_cases_bitexact(sfm, gpu):
+@pytest.mark.parametrize("Wd", [96, 97])
+def test_tsdf_edge_cases_bitexact(sfm, gpu, monkeypatch, Wd):
     """Odd / non-cubic grid (a lane's second voxel off the grid), 30 frames (two
     frame-chunk launches), prior (T, W) state including values outside the fast
     division's range, depth holes / negative depth, a camera plane cutting the
     grid (Zc <= 0), and frames with a NaN pose, an infinite intrinsic and a
     >= 2^60 translation (skipped as a whole): bit-exact with the oracle."""
+    monkeypatch.setenv("SFMHIP_TSDF_CHUNK", "7")  # several launches; Wd = 97: unaligned depth rows
     D, H, W_ = 20, 33, 45
-    F, Hd, Wd = 30, 72, 96
+    F, Hd = 30, 72
     depth, poses, K = syn.tsdf_scene(F, Hd, Wd, focal=80.0, seed=11)
     depth, poses, K = depth.numpy().copy(), poses.numpy().copy(), K.numpy().copy()
     rng = np.random.default_rng(5)

@@ -60,9 +60,27 @@ int main(int argc, char** argv) {
     hipMalloc(&seed, 4096 * 4);
     hipMalloc(&out, blocks * 256 * 4);
     int h[4096];
-    for (int zero = 0; zero < 2; ++zero) {
+    // operand byte distributions: 0 uniform random bytes, 1 zero, 2 SuperPoint-like small
+    // signed values (round(N(0, 8)), two's complement), 3 the same offset by +64
+    const char* names[4] = {"random", "zero", "small-signed", "small+64"};
+    const int modes = argc > 2 ? atoi(argv[2]) : 2;
+    for (int zero = 0; zero < modes; ++zero) {
         unsigned x = 12345;
-        for (int i = 0; i < 4096; ++i) { x = x * 1664525u + 1013904223u; h[i] = zero ? 0 : (int)x; }
+        for (int i = 0; i < 4096; ++i) {
+            x = x * 1664525u + 1013904223u;
+            if (zero < 2) { h[i] = zero ? 0 : (int)x; continue; }
+            unsigned w = 0;
+            for (int b = 0; b < 4; ++b) {
+                x = x * 1664525u + 1013904223u;
+                // sum of 4 uniforms ~ N(0, 8) approximately
+                int v = 0;
+                for (int t = 0; t < 4; ++t) { x = x * 1664525u + 1013904223u; v += (int)((x >> 24) & 15) - 8; }
+                v = v * 2;
+                if (zero == 3) v += 64;
+                w |= (unsigned)(v & 255) << (8 * b);
+            }
+            h[i] = (int)w;
+        }
         hipMemcpy(seed, h, sizeof(h), hipMemcpyHostToDevice);
         for (int epi = 0; epi < 2; ++epi) {
             hipEvent_t e0, e1;
@@ -78,7 +96,7 @@ int main(int argc, char** argv) {
                 hipEventElapsedTime(&ms, e0, e1);
                 const double ops = (double)blocks * 4 * iters * 16 * 65536.0;
                 if (rep == 2)
-                    printf("%s operands, %s epilogue: %.2f ms  %.0f TOPS (%.1f%% of 5000)\n", zero ? "zero" : "random",
+                    printf("%s operands, %s epilogue: %.2f ms  %.0f TOPS (%.1f%% of 5000)\n", names[zero],
                            epi ? "with" : "no", ms, ops / ms / 1e9, ops / ms / 1e9 / 50.0);
             }
         }
