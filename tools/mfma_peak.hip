@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
@@ -60,9 +61,10 @@ int main(int argc, char** argv) {
     hipMalloc(&seed, 4096 * 4);
     hipMalloc(&out, blocks * 256 * 4);
     int h[4096];
-    // operand byte distributions: 0 uniform random bytes, 1 zero, 2 SuperPoint-like small
-    // signed values (round(N(0, 8)), two's complement), 3 the same offset by +64
-    const char* names[4] = {"random", "zero", "small-signed", "small+64"};
+    // operand byte distributions: 0 uniform random bytes, 1 zero, then C3-like small
+    // signed values round(N(0, 8)) (two's complement) shifted by 0, 64, 88, 100
+    const char* names[6] = {"random", "zero", "N(0,8)+0", "N(0,8)+64", "N(0,8)+88", "N(0,8)+100"};
+    const int shifts[6] = {0, 0, 0, 64, 88, 100};
     const int modes = argc > 2 ? atoi(argv[2]) : 2;
     for (int zero = 0; zero < modes; ++zero) {
         unsigned x = 12345;
@@ -71,12 +73,12 @@ int main(int argc, char** argv) {
             if (zero < 2) { h[i] = zero ? 0 : (int)x; continue; }
             unsigned w = 0;
             for (int b = 0; b < 4; ++b) {
-                x = x * 1664525u + 1013904223u;
-                // sum of 4 uniforms ~ N(0, 8) approximately
-                int v = 0;
-                for (int t = 0; t < 4; ++t) { x = x * 1664525u + 1013904223u; v += (int)((x >> 24) & 15) - 8; }
-                v = v * 2;
-                if (zero == 3) v += 64;
+                // Irwin-Hall(12) - 6 ~ N(0, 1), times 8, rounded, clamped to [-40, 39]
+                float g = -6.f;
+                for (int t = 0; t < 12; ++t) { x = x * 1664525u + 1013904223u; g += (float)(x >> 8) / 16777216.f; }
+                int v = (int)lrintf(8.f * g);
+                v = v < -40 ? -40 : (v > 39 ? 39 : v);
+                v += shifts[zero];
                 w |= (unsigned)(v & 255) << (8 * b);
             }
             h[i] = (int)w;
