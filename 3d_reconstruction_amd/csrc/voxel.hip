@@ -7,6 +7,7 @@
 #include <climits>
 #include <cstdlib>
 #include <algorithm>
+#include <vector>
 
 namespace sfmhip {
 
@@ -424,7 +425,7 @@ constexpr int kCullMaxBlocks = 256;   // larger footprints are simply kept
 // [u0,u1] x [v0,v1], clipped to the image, and zlo <= every f32 Zc).
 __device__ int box_footprint(const float* P, const float* k, const Bounds& B, int D, int H, int W, int xa, int xb,
                              int ya, int yb, int za, int zb, int Hd, int Wd, int& u0, int& u1, int& v0, int& v1,
-                             double& zlo) {
+                             double& zlo, double& zhi, bool& inside) {
     const double sx = ((double)B.mx[0] - B.mn[0]) / (W - 1), sy = ((double)B.mx[1] - B.mn[1]) / (H - 1),
                  sz = ((double)B.mx[2] - B.mn[2]) / (D - 1);
     const double cxw = B.mn[0] + 0.5 * (xa + xb) * sx, hx = 0.5 * (xb - xa) * fabs(sx);
@@ -443,7 +444,8 @@ __device__ int box_footprint(const float* P, const float* k, const Bounds& B, in
     const double eps = 0x1p-24;
     const double dz = 8 * eps * mag[2];
     zlo = c[2] - e[2] - dz;
-    const double zhi = c[2] + e[2] + dz;
+    zhi = c[2] + e[2] + dz;
+    inside = false;
     if (!(zlo > 1e-3 && zhi < 1e30 && c[0] == c[0] && c[1] == c[1])) return 0;
     const double izl = 1.0 / zlo, izh = 1.0 / zhi;
     const double xl = c[0] - e[0] - 8 * eps * mag[0], xh = c[0] + e[0] + 8 * eps * mag[0];
@@ -464,6 +466,7 @@ __device__ int box_footprint(const float* P, const float* k, const Bounds& B, in
     v0 = (int)floor(vm0 - dv);
     v1 = (int)floor(vm1 + dv);
     if (u1 < 0 || v1 < 0 || u0 >= Wd || v0 >= Hd) return 1;
+    inside = u0 >= 0 && v0 >= 0 && u1 < Wd && v1 < Hd;
     u0 = max(u0, 0); u1 = min(u1, Wd - 1); v0 = max(v0, 0); v1 = min(v1, Hd - 1);
     return 2;
 }
@@ -478,9 +481,10 @@ __global__ void tsdf_footprint_kernel(int D, int H, int W, int z0, int z1, int F
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= F) return;
     int u0, u1, v0, v1;
-    double zlo;
+    double zlo, zhi;
+    bool inside;
     const int st = box_footprint(poses + f * 12, Kf + f * 4, B, D, H, W, 0, W - 1, 0, H - 1, z0, z1 - 1, Hd, Wd, u0,
-                                 u1, v0, v1, zlo);
+                                 u1, v0, v1, zlo, zhi, inside);
     range[f] = st == 2   ? make_int4(u0 / kCullBlock, u1 / kCullBlock, v0 / kCullBlock, v1 / kCullBlock)
                : st == 1 ? make_int4(1, 0, 1, 0)
                          : make_int4(0, nbu - 1, 0, nbv - 1);
@@ -488,10 +492,13 @@ __global__ void tsdf_footprint_kernel(int D, int H, int W, int z0, int z1, int F
 
 // VEC: Wd % 4 == 0, one float4 (4 pixels) per lane, 4 lanes per block column,
 // all 16 rows' loads in flight.  Otherwise one pixel per lane, 16 lanes per block.
+// bmax ignores NaN (a NaN depth never updates); bmin (when non-null) is poisoned
+// by NaN (-inf: such a block never proves free space).
+__device__ __forceinline__ float nan_low(float x) { return x == x ? x : -__builtin_inff(); }
 template <bool VEC>
 __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __restrict__ depth, int F, int Hd, int Wd,
                                                              int nbu, int nbv, const int4* __restrict__ range,
-                                                             float* __restrict__ bmax) {
+                                                             float* __restrict__ bmax, float* __restrict__ bmin) {
     const int f = blockIdx.z, bv = blockIdx.y;
     const int4 rg = range[f];                       // blocks the slab can touch in this frame
     if (bv < rg.z || bv > rg.w) return;
@@ -499,7 +506,8 @@ __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __rest
     if (ucol0 / kCullBlock > rg.y || (ucol0 + (VEC ? 1024 : 256) - 1) / kCullBlock < rg.x) return;
     const float* dp = depth + (size_t)f * Hd * Wd;
     const int r0 = bv * kCullBlock, nr = min(kCullBlock, Hd - r0);
-    float m = -__builtin_inff();
+    float m = -__builtin_inff(), mn = __builtin_inff();
+    const size_t slot = (size_t)f * nbv + bv;
     if (VEC) {
         const int u = (blockIdx.x * 256 + threadIdx.x) * 4;
         if (u < Wd) {
@@ -510,19 +518,40 @@ __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __rest
                               : make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff());
 #pragma unroll
             for (int r = 0; r < kCullBlock; ++r) m = fmaxf(m, fmaxf(fmaxf(q[r].x, q[r].y), fmaxf(q[r].z, q[r].w)));
+            if (bmin)
+#pragma unroll
+                for (int r = 0; r < kCullBlock; ++r)
+                    if (r < nr)
+                        mn = fminf(mn, fminf(fminf(nan_low(q[r].x), nan_low(q[r].y)),
+                                             fminf(nan_low(q[r].z), nan_low(q[r].w))));
         }
         m = fmaxf(m, __shfl_xor(m, 1, 4));
         m = fmaxf(m, __shfl_xor(m, 2, 4));
+        mn = fminf(mn, __shfl_xor(mn, 1, 4));
+        mn = fminf(mn, __shfl_xor(mn, 2, 4));
         const int bu = u / kCullBlock;
-        if ((threadIdx.x & 3) == 0 && bu < nbu) bmax[((size_t)f * nbv + bv) * nbu + bu] = m;
+        if ((threadIdx.x & 3) == 0 && bu < nbu) {
+            bmax[slot * nbu + bu] = m;
+            if (bmin) bmin[slot * nbu + bu] = mn;
+        }
     } else {
         const int u = blockIdx.x * 256 + threadIdx.x;
         if (u < Wd)
-            for (int r = 0; r < nr; ++r) m = fmaxf(m, dp[(size_t)(r0 + r) * Wd + u]);
+            for (int r = 0; r < nr; ++r) {
+                const float x = dp[(size_t)(r0 + r) * Wd + u];
+                m = fmaxf(m, x);
+                mn = fminf(mn, nan_low(x));
+            }
 #pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 16));
+        for (int off = 8; off >= 1; off >>= 1) {
+            m = fmaxf(m, __shfl_xor(m, off, 16));
+            mn = fminf(mn, __shfl_xor(mn, off, 16));
+        }
         const int bu = u / kCullBlock;
-        if ((threadIdx.x & 15) == 0 && bu < nbu) bmax[((size_t)f * nbv + bv) * nbu + bu] = m;
+        if ((threadIdx.x & 15) == 0 && bu < nbu) {
+            bmax[slot * nbu + bu] = m;
+            if (bmin) bmin[slot * nbu + bu] = mn;
+        }
     }
 }
 
@@ -530,31 +559,55 @@ __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __rest
 // wave of the workgroup tile.  Interval bounds on the affine camera
 // coordinates over the sub-tile (centre +- sum |P_rj| h_j), pixel bounds from
 // the X/Z and Y/Z interval quotients (a superset of the exact projection).
+// Two ballot words per (sub-tile, 32 frames):
+//   cull: no voxel of the sub-tile updates in this frame (dropped);
+//   free: every voxel updates with tsdf = 1 exactly (free space in front of the
+//     surface), so the fusion kernel applies T = (T W + 1)/(W + 1) without
+//     projecting or gathering.  Proven when the frame's record is one the kernel
+//     fuses (every pose / intrinsic finite and < 2^60), the unclipped pixel box
+//     lies inside the image, every f32 Zc is in [2^-59, 2^59], and the smallest
+//     depth under the box (NaN-poisoned block minima) exceeds the largest f32 Zc by
+//     at least mu (1 + 2^-20): then fl(depth - Zc) >= mu (1 + 2^-20) and
+//     fl(fl(depth - Zc) * fl(1/mu)) >= 1, i.e. the kernel's tsdf is min(1, .) = 1.
 constexpr int kCullSub = 4;   // waves per workgroup tile
-__global__ __launch_bounds__(256) void tsdf_cull_kernel(int D, int H, int W, int z0, int z1, int F, int Hd, int Wd,
-                                                        const float* __restrict__ poses, const float* __restrict__ Kf,
-                                                        Bounds B, float trunc, const float* __restrict__ bmax,
-                                                        int nbu, int nbv, const int4* __restrict__ range,
-                                                        int per_tile, unsigned* __restrict__ cull) {
-    // per_tile = 1: one test for the whole 8x8x8 tile (written to its 4 wave slots)
+// One workgroup per (4x4x4 brick of sub-tiles, 16 frames): wave j tests frame
+// 16 h + j for the brick's 64 sub-tiles (one per lane), so the camera loads are
+// scalar and the block-table reads of neighbouring footprints share cache
+// lines; the 16 bits of each sub-tile are packed through LDS and stored as the
+// low or high half of its mask word.  Masks are [sub-tile slot][nw] words, bit j
+// of word w = frame 32 w + j.
+constexpr int kCullFrames = 16;
+__global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, int z0, int z1, int F, int Hd, int Wd,
+                                                         const float* __restrict__ poses, const float* __restrict__ Kf,
+                                                         Bounds B, float trunc, const float* __restrict__ bmax,
+                                                         const float* __restrict__ bmin, int nbu, int nbv,
+                                                         const int4* __restrict__ range, int per_tile, int nw,
+                                                         unsigned short* __restrict__ cull,
+                                                         unsigned short* __restrict__ freem) {
+    __shared__ unsigned char bits[kCullFrames][64];
     const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
     const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
-    const int64_t nsub = (int64_t)ntx * nty * ntz * per_tile;
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t sub = g >> 5;
-    const int f = (int)(g & 31);
-    bool skip = false;
-    if (sub < nsub && f < F) {
-        const int64_t tile = sub / per_tile;
-        const int w = (int)(sub % per_tile);
-        const int bx = (int)(tile % ntx), by = (int)((tile / ntx) % nty), bz = (int)(tile / ((int64_t)ntx * nty));
-        const int xa = bx * kTsdfTX, xb = min(W, xa + kTsdfTX) - 1;
-        const int ya = by * kTsdfTY + (kTsdfTY / per_tile) * w, yb = min(H, ya + kTsdfTY / per_tile) - 1;
-        const int za = z0 + bz * kTsdfTZ, zb = min(z1, za + kTsdfTZ) - 1;
+    const int nsy = nty * per_tile;                        // sub-tile rows in y
+    const int nqx = (ntx + 3) >> 2, nqy = (nsy + 3) >> 2;  // 4x4x4 bricks of sub-tiles
+    const int nh = 2 * nw;                                 // 16-frame halves per launch
+    const int hf = blockIdx.x % nh, brick = blockIdx.x / nh;
+    const int l = threadIdx.x & 63, j = threadIdx.x >> 6;
+    const int f = hf * kCullFrames + j;
+    const int tx = (brick % nqx) * 4 + (l & 3);
+    const int sy = ((brick / nqx) % nqy) * 4 + ((l >> 2) & 3);
+    const int tz = (brick / (nqx * nqy)) * 4 + (l >> 4);
+    const bool tile_ok = tx < ntx && sy < nsy && tz < ntz;
+    const int ty = sy / per_tile, w = sy % per_tile;
+    bool skip = false, fre = false;
+    if (tile_ok && f < F) {
+        const int xa = tx * kTsdfTX, xb = min(W, xa + kTsdfTX) - 1;
+        const int ya = ty * kTsdfTY + (kTsdfTY / per_tile) * w, yb = min(H, ya + kTsdfTY / per_tile) - 1;
+        const int za = z0 + tz * kTsdfTZ, zb = min(z1, za + kTsdfTZ) - 1;
         int u0, u1, v0, v1;
-        double zlo;
+        double zlo, zhi;
+        bool inside = false;
         const int st = ya <= yb ? box_footprint(poses + f * 12, Kf + f * 4, B, D, H, W, xa, xb, ya, yb, za, zb, Hd, Wd,
-                                                u0, u1, v0, v1, zlo)
+                                                u0, u1, v0, v1, zlo, zhi, inside)
                                 : 0;
         if (st == 1) {
             skip = true;
@@ -563,7 +616,8 @@ __global__ __launch_bounds__(256) void tsdf_cull_kernel(int D, int H, int W, int
             const int4 rg = range[f];   // only blocks inside the slab's range were computed
             const int nu = bu1 - bu0 + 1, nb = nu * (bv1 - bv0 + 1);
             if (nb <= kCullMaxBlocks && bu0 >= rg.x && bu1 <= rg.y && bv0 >= rg.z && bv1 <= rg.w) {
-                const float* bp = bmax + ((size_t)f * nbv + bv0) * nbu + bu0;
+                const size_t o = ((size_t)f * nbv + bv0) * nbu + bu0;
+                const float* bp = bmax + o;
                 float m = -__builtin_inff();
                 for (int bv = bv0; bv <= bv1; ++bv, bp += nbu) {
                     int i = 0;
@@ -574,25 +628,90 @@ __global__ __launch_bounds__(256) void tsdf_cull_kernel(int D, int H, int W, int
                 // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for the
                 // rounding of (depth - Zc), so the kernel's !(sdf < -trunc) test fails everywhere
                 skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * 0x1p-24) + 1e-30 < zlo);
+                if (!skip && bmin && inside && zlo >= 0x1p-59 && zhi <= 0x1p59) {
+                    bool good = true;
+#pragma unroll
+                    for (int q = 0; q < 12; ++q) good = good && fabsf(poses[f * 12 + q]) < 0x1p60f;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) good = good && fabsf(Kf[f * 4 + q]) < 0x1p60f;
+                    if (good) {
+                        const float* bq = bmin + o;
+                        float mn = __builtin_inff();
+                        for (int bv = bv0; bv <= bv1; ++bv, bq += nbu) {
+                            int i = 0;
+                            for (; i + 4 <= nu; i += 4)
+                                mn = fminf(fminf(mn, fminf(bq[i], bq[i + 1])), fminf(bq[i + 2], bq[i + 3]));
+                            for (; i < nu; ++i) mn = fminf(mn, bq[i]);   // never NaN (poisoned to -inf)
+                        }
+                        fre = (double)mn - zhi >= (double)trunc * (1 + 0x1p-20);
+                    }
+                }
             }
         }
     }
-    const unsigned long long bal = __ballot(skip);
-    const int lane = threadIdx.x & 63;
-    if ((lane & 31) == 0 && sub < nsub) {
-        const unsigned word = (unsigned)(bal >> lane);
-        if (per_tile == kCullSub) cull[sub] = word;
-        else
-            for (int w = 0; w < kCullSub; ++w) cull[(sub / per_tile) * kCullSub + w] = word;
+    bits[j][l] = (unsigned char)(skip | (fre << 1));
+    __syncthreads();
+    if (j == 0 && tile_ok) {
+        unsigned cw = 0u, fw = 0u;
+#pragma unroll
+        for (int q = 0; q < kCullFrames; ++q) {
+            const unsigned b = bits[q][l];
+            cw |= (b & 1u) << q;
+            fw |= (b >> 1) << q;
+        }
+        const int64_t tile = ((int64_t)tz * nty + ty) * ntx + tx;
+        const int q0 = per_tile == kCullSub ? w : 0, q1 = per_tile == kCullSub ? w + 1 : kCullSub;
+        for (int q = q0; q < q1; ++q) {
+            const int64_t h = ((tile * kCullSub + q) * nw) * 2 + hf;   // half hf of word hf / 2
+            cull[h] = (unsigned short)cw;
+            if (freem) freem[h] = (unsigned short)fw;
+        }
     }
 }
 
-template <int U, bool SWZ>
+// Timing probes only (SFMHIP_TSDF_FREE=3: free-space frames dropped instead of fused;
+// =4: every frame dropped): results are wrong by design, never the default.
+__global__ void tsdf_probe_mask_kernel(unsigned* __restrict__ cull, const unsigned* __restrict__ freem, int64_t n,
+                                       int all) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) cull[i] = all ? ~0u : (cull[i] | freem[i]);
+}
+
+// Validated camera records, 16 floats per frame (non-finite or >= 2^60 anywhere:
+// all zero, so Zc = 0 and the frame is skipped):
+//   P0 P4 | P2 P6 | P3 P7 | P8 P10 P11 | P1 P5 P9 | fx fy | cx+.5 cy+.5
+__global__ void tsdf_cam_kernel(const float* __restrict__ poses, const float* __restrict__ Kf, int F,
+                                float* __restrict__ rec) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    float p[12], k[4];
+    bool good = true;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) { p[q] = poses[f * 12 + q]; good = good && fabsf(p[q]) < 0x1p60f; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { k[q] = Kf[f * 4 + q]; good = good && fabsf(k[q]) < 0x1p60f; }
+    const float r[16] = {p[0], p[4], p[2], p[6], p[3], p[7], p[8], p[10], p[11], p[1], p[5], p[9],
+                         k[0], k[1], k[2] + 0.5f, k[3] + 0.5f};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) rec[f * 16 + q] = good ? r[q] : 0.f;
+}
+
+// W may take k more exact +1 steps with T = 1 fixed: an integer in [0, 2^24 - 512]
+__device__ __forceinline__ bool w_runs(float w) { return w >= 0.f && w <= 0x1p24f - 512.f && w == truncf(w); }
+
+// One workgroup = one 8x8x8 tile; every frame of the launch is fused with the
+// tile's (T, W) in registers.  The (tile, frame) masks of the cull pass drive a
+// scalar walk over the frames: culled frames are skipped, a run of k free-space
+// frames is applied as k updates with tsdf = 1 — or, when every voxel of the
+// wave holds T = 1 and an integer weight, as W += k (each of the k updates would
+// compute (1 W + 1)/(W + 1) = 1 exactly and W + 1 exactly) — and every other
+// frame is projected and gathered.
+template <bool SWZ>
 __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float* __restrict__ Wt, int D, int H,
                                                    int W, int z0, int z1, const float* __restrict__ depth, int F,
-                                                   int Hd, int Wd, const float* __restrict__ poses,
-                                                   const float* __restrict__ Kf, Bounds B, float trunc,
-                                                   SuperBrick SB, const unsigned* __restrict__ cull) {
+                                                   int Hd, int Wd, const float* __restrict__ rec, Bounds B,
+                                                   float trunc, SuperBrick SB, const unsigned* __restrict__ cull,
+                                                   const unsigned* __restrict__ freem, int nw, float free_ts) {
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (SWZ) {
         const int nbx = (W + kTsdfTX - 1) / kTsdfTX, nby = (H + kTsdfTY - 1) / kTsdfTY;
@@ -613,27 +732,12 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
         by = sy * SB.y + (in / SB.x) % SB.y;
         bz = sz * SB.z + in / (SB.x * SB.y);
     }
-    // Camera records, 16 floats per frame:
-    //   P0 P4 | P2 P6 | P3 P7 | P8 P10 P11 | P1 P5 P9 | fx fy | cx+.5 cy+.5
-    extern __shared__ float cam[];   // dynamic: a static 512-frame array would cap occupancy
-    for (int f = threadIdx.x; f < F; f += blockDim.x) {
-        float p[12], k[4];
-        bool good = true;
-#pragma unroll
-        for (int q = 0; q < 12; ++q) { p[q] = poses[f * 12 + q]; good = good && fabsf(p[q]) < 0x1p60f; }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { k[q] = Kf[f * 4 + q]; good = good && fabsf(k[q]) < 0x1p60f; }
-        const float rec[16] = {p[0], p[4], p[2], p[6], p[3], p[7], p[8], p[10], p[11], p[1], p[5], p[9],
-                               k[0], k[1], k[2] + 0.5f, k[3] + 0.5f};
-#pragma unroll
-        for (int q = 0; q < 16; ++q) cam[f * 16 + q] = good ? rec[q] : 0.f;   // Zc = 0 -> frame skipped
-    }
-    __syncthreads();
     const int l = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int x = bx * kTsdfTX + (l & 3) + 4 * ((l >> 4) & 1);
     const int z = z0 + bz * kTsdfTZ + ((l >> 2) & 3) + 4 * (l >> 5);
-    const int y = by * kTsdfTY + 2 * (threadIdx.x >> 6);
-    if (x >= W || y >= H || z >= z1) return;  // (after the only barrier)
+    const int y = by * kTsdfTY + 2 * wave;
+    if (x >= W || y >= H || z >= z1) return;  // no barrier in this kernel
     const bool two = y + 1 < H;
     const float sx = (B.mx[0] - B.mn[0]) / (float)(W - 1);
     const float sy = (B.mx[1] - B.mn[1]) / (float)(H - 1);
@@ -642,43 +746,61 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
     const f2 vy = {B.mn[1] + (float)y * sy, B.mn[1] + (float)(y + 1) * sy};
     const float vz = B.mn[2] + (float)z * sz;
     const float inv_trunc = 1.0f / trunc;
+    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
+    const size_t slot = ((((size_t)bz * nty + by) * ntx + bx) * kCullSub + wave) * (size_t)nw;
+    if (cull) {   // every frame of the launch culled for this wave: the grid is not even read
+        unsigned any = 0u;
+        for (int w0 = 0; w0 < F; w0 += 32)
+            any |= ~cull[slot + (w0 >> 5)] & (F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u));
+        if (__builtin_amdgcn_readfirstlane((int)any) == 0) return;
+    }
     const size_t idx = ((size_t)z * H + y) * W + x;
-    f2 tv = {T[idx], two ? T[idx + W] : 0.f};
+    f2 tv = {T[idx], two ? T[idx + W] : 1.f};   // the absent voxel reads as T = 1, W = 0 (never stored)
     f2 wv = {Wt[idx], two ? Wt[idx + W] : 0.f};
     // lanes whose stored (T, W) lie outside the fast division's range divide exactly throughout
     const bool wild = !(tame(tv.x, wv.x) && tame(tv.y, wv.y));
     const size_t frame = (size_t)Hd * Wd;
     const int nbytes = (int)(frame * 4);   // host-checked < 2^31
     const int Wd4 = Wd * 4;                 // < 2^24: exact in v_mul_u32_u24
-    // Frames to fuse, in order: with a cull mask (F <= 32) the frames whose
-    // (tile, frame) test proved that no voxel of this tile updates are dropped,
-    // and the next U surviving frames are issued together.
-    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
-    unsigned todo = F >= 32 ? ~0u : ((1u << F) - 1u);
-    if (cull) todo &= ~cull[(((size_t)bz * nty + by) * ntx + bx) * kCullSub + (threadIdx.x >> 6)];
-    for (int f0 = 0;; f0 += U) {
-        int fr[U];
-        bool lv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (F <= 32) {
-                lv[u] = todo != 0u;
-                fr[u] = lv[u] ? __builtin_ctz(todo) : F - 1;
-                todo &= todo - 1u;
-            } else {
-                lv[u] = f0 + u < F;
-                fr[u] = lv[u] ? f0 + u : F - 1;
-            }
+
+    auto update = [&](f2 ts, bool g0, bool g1) {
+        const f2 n = tv * wv + ts;
+        const f2 d = wv + f2s(1.0f);
+        f2 q = div_rn(n, d);
+        if (wild || !(fabsf(n.x) >= 0x1p-100f)) q.x = n.x / d.x;
+        if (wild || !(fabsf(n.y) >= 0x1p-100f)) q.y = n.y / d.y;
+        tv.x = g0 ? q.x : tv.x;
+        wv.x = g0 ? d.x : wv.x;
+        tv.y = g1 ? q.y : tv.y;
+        wv.y = g1 ? d.y : wv.y;
+    };
+
+    for (int w0 = 0; w0 < F; w0 += 32) {
+        const int wd = w0 >> 5;
+        unsigned todo = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u), fre = 0u;
+        if (cull) {   // wave-uniform address: scalar loads
+            todo &= ~cull[slot + wd];
+            if (freem) fre = freem[slot + wd] & todo;
         }
-        if (!lv[0]) break;
-        f2 zc[U];
-        float d0[U], d1[U];
-        bool ok0[U], ok1[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool live = lv[u];   // wave-uniform
-            const int f = fr[u];
-            const float* r = cam + f * 16;
+        todo = (unsigned)__builtin_amdgcn_readfirstlane((int)todo);
+        fre = (unsigned)__builtin_amdgcn_readfirstlane((int)fre);
+        while (todo) {
+            if (fre & todo & (0u - todo)) {   // lowest pending frame is free space: take its run
+                const unsigned full = todo & ~fre;
+                const unsigned run = todo & (full ? (full & (0u - full)) - 1u : ~0u);
+                todo &= ~run;
+                const int k = __builtin_popcount(run);
+                const bool ones = tv.x == 1.f && tv.y == 1.f && w_runs(wv.x) && w_runs(wv.y);
+                if (free_ts == 1.f && __builtin_amdgcn_ballot_w64(!ones) == 0) {
+                    wv = wv + f2s((float)k);
+                } else {
+                    for (int i = 0; i < k; ++i) update(f2s(free_ts), true, two);
+                }
+                continue;
+            }
+            const int f = w0 + __builtin_ctz(todo);
+            todo &= todo - 1u;
+            const float* r = rec + f * 16;   // uniform: scalar loads
             const f2 Q = (f2{r[0], r[1]} * f2s(vx) + f2{r[2], r[3]} * f2s(vz)) + f2{r[4], r[5]};
             const float Qz = (r[6] * vx + r[7] * vz) + r[8];
             const f2 Xc = f2s(r[9]) * vy + f2s(Q.x);
@@ -689,34 +811,20 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
             const f2 vv = (f2s(r[13]) * Yc) * iz + f2s(r[15]);
             const int iu0 = cvt_flr(uu.x), iv0 = cvt_flr(vv.x);
             const int iu1 = cvt_flr(uu.y), iv1 = cvt_flr(vv.y);
-            ok0[u] = live && z_ok(Zc.x) && (unsigned)iu0 < (unsigned)Wd && (unsigned)iv0 < (unsigned)Hd;
-            ok1[u] = live && two && z_ok(Zc.y) && (unsigned)iu1 < (unsigned)Wd && (unsigned)iv1 < (unsigned)Hd;
-            zc[u] = Zc;
+            const bool ok0 = z_ok(Zc.x) && (unsigned)iu0 < (unsigned)Wd && (unsigned)iv0 < (unsigned)Hd;
+            const bool ok1 = two && z_ok(Zc.y) && (unsigned)iu1 < (unsigned)Wd && (unsigned)iv1 < (unsigned)Hd;
             // bounds-checked gather: off-image lanes read 0 or a discarded in-frame value
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc((void*)(depth + (size_t)f * frame), (short)0, nbytes, 0x00020000);
-            d0[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                  rs, (int)(__umul24(iv0, Wd4) + ((unsigned)iu0 << 2)), 0, 0));
-            d1[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                  rs, (int)(__umul24(iv1, Wd4) + ((unsigned)iu1 << 2)), 0, 0));
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const f2 dep = {d0[u], d1[u]};
-            const f2 sdf = dep - zc[u];
-            const bool g0 = ok0[u] && dep.x > 0.f && !(sdf.x < -trunc);
-            const bool g1 = ok1[u] && dep.y > 0.f && !(sdf.y < -trunc);
+            const f2 dep = {__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                          rs, (int)(__umul24(iv0, Wd4) + ((unsigned)iu0 << 2)), 0, 0)),
+                            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                          rs, (int)(__umul24(iv1, Wd4) + ((unsigned)iu1 << 2)), 0, 0))};
+            const f2 sdf = dep - Zc;
+            const bool g0 = ok0 && dep.x > 0.f && !(sdf.x < -trunc);
+            const bool g1 = ok1 && dep.y > 0.f && !(sdf.y < -trunc);
             const f2 sc = sdf * f2s(inv_trunc);
-            const f2 ts = {fminf(1.0f, sc.x), fminf(1.0f, sc.y)};
-            const f2 n = tv * wv + ts;
-            const f2 d = wv + f2s(1.0f);
-            f2 q = div_rn(n, d);
-            if (wild || !(fabsf(n.x) >= 0x1p-100f)) q.x = n.x / d.x;
-            if (wild || !(fabsf(n.y) >= 0x1p-100f)) q.y = n.y / d.y;
-            tv.x = g0 ? q.x : tv.x;
-            wv.x = g0 ? d.x : wv.x;
-            tv.y = g1 ? q.y : tv.y;
-            wv.y = g1 ? d.y : wv.y;
+            update(f2{fminf(1.0f, sc.x), fminf(1.0f, sc.y)}, g0, g1);
         }
     }
     T[idx] = tv.x;
@@ -1094,10 +1202,11 @@ extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, con
     return check_launch("render_kernel");
 }
 
-extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, int z0, int z1,
-                                     const float* depth, int F, int Hd, int Wd, const float* poses,
-                                     const float* Kf, const float* bmin, const float* bmax, float trunc,
-                                     void* stream) {
+// stats != nullptr: run only the culling pre-passes (forced on) and count
+// (wave sub-tile, frame) pairs: stats[0] tested, [1] culled, [2] free space.
+static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, const float* depth, int F, int Hd,
+                    int Wd, const float* poses, const float* Kf, const float* bmin, const float* bmax, float trunc,
+                    void* stream, int64_t* stats) {
     SFMHIP_REQUIRE(T && Wt && depth && poses && Kf && bmin && bmax, "sfmhip_tsdf_integrate: null pointer");
     SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && F >= 0 && Hd > 0 && Wd > 0, "sfmhip_tsdf_integrate: bad shape");
     SFMHIP_REQUIRE(0 <= z0 && z0 <= z1 && z1 <= D, "sfmhip_tsdf_integrate: bad z range");
@@ -1108,11 +1217,8 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     for (int a = 0; a < 3; ++a)
         SFMHIP_REQUIRE(std::fabs(bmin[a]) < 0x1p60f && std::fabs(bmax[a]) < 0x1p60f,
                        "sfmhip_tsdf_integrate: bounds must be finite and below 2^60 in magnitude");
-    // Tuning knobs (A/B runs only): SFMHIP_TSDF_U (frames in flight), SFMHIP_TSDF_SWZ
-    // (super-brick XCD order), SFMHIP_TSDF_SBX/SBY/SBZ and SFMHIP_TSDF_CHUNK (frames per
-    // launch: a shorter chunk bounds how many frames the resident workgroups
-    // touch at once, i.e. the depth working set in L2 / MALL).
-    const int unroll = env_int("SFMHIP_TSDF_U", 1);
+    // Tuning knobs (A/B runs only): SFMHIP_TSDF_SWZ (super-brick XCD order),
+    // SFMHIP_TSDF_SBX/SBY/SBZ/IL and SFMHIP_TSDF_CHUNK (frames per launch).
     const int swz = env_int("SFMHIP_TSDF_SWZ", 1);
     // default: super-bricks of 3 x 2 x 8 tiles (24 x 16 x 64 voxels) dealt round-robin over the
     // XCDs (sweeps in tools/bench_tsdf_variants.py; with culling the work per tile is uneven, and
@@ -1124,10 +1230,13 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     // ~0.8 ps per depth pixel read, i.e. worth it above ~1.5 voxels per pixel).
     const int cull_env = env_int("SFMHIP_TSDF_CULL", 1);
     const bool cull_pays = (double)(z1 - z0) * H * W >= 1.5 * (double)Hd * Wd;
-    const bool want_cull = cull_env == 2 || (cull_env == 1 && cull_pays);
-    // frames per launch: 24 with culling (its 32-bit frame mask), 64 without (thin
-    // z-slabs of an N-way split: fewer launch tails; tools/bench_tsdf_slabs.py)
-    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", want_cull ? 24 : 64)));
+    const bool want_cull = stats || cull_env == 2 || (cull_env == 1 && cull_pays);
+    // 64 frames per launch: the resident workgroups then gather from a bounded set of
+    // frames (L2 locality; one launch over all 257 C5 frames ran the fusion ~10 % slower)
+    // while the grid traffic / dispatch cost per launch stays small (fully culled waves
+    // do not even read the grid)
+    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", 64)));
+    const int nw = ceil_div(std::min(chunk, F), 32);   // mask words per sub-tile slot
     const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 3)), std::max(1, env_int("SFMHIP_TSDF_SBY", 2)),
                         std::max(1, env_int("SFMHIP_TSDF_SBZ", std::min(8, nbz))), env_int("SFMHIP_TSDF_IL", 1)};
     dim3 grid(nbx, nby, nbz);
@@ -1140,24 +1249,48 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     }
     const Bounds bb = make_bounds(bmin, bmax);
     hipStream_t st = as_stream(stream);
-    // Culling scratch (stream-ordered; SFMHIP_TSDF_CULL=0 disables culling, for A/B runs).
-    // Any allocation failure only disables the culling: the fusion itself is unchanged.
+    // Scratch (stream-ordered): validated camera records; culling buffers
+    // (SFMHIP_TSDF_CULL=0 disables culling, SFMHIP_TSDF_FREE=0 the free-space path, for A/B
+    // runs).  An allocation failure of the culling buffers only disables culling.
     const int nbu = ceil_div(Wd, kCullBlock), nbv = ceil_div(Hd, kCullBlock);
     const int64_t nsub = (int64_t)nbx * nby * nbz * kCullSub;
     const int per_tile = env_int("SFMHIP_TSDF_CULLSUB", 1) == 4 ? kCullSub : 1;
-    const int64_t ntests = (int64_t)nbx * nby * nbz * per_tile;
+    // cull pass: one workgroup per (4x4x4 brick of sub-tiles, 16 frames)
+    const int64_t cull_bricks = (int64_t)ceil_div(nbx, 4) * ceil_div(nby * per_tile, 4) * ceil_div(nbz, 4);
+    SFMHIP_REQUIRE(cull_bricks * ceil_div(std::min(chunk, F), 16) < INT_MAX, "sfmhip_tsdf_integrate: grid too large");
+    // the free-space proof needs a trunc whose f32 reciprocal is a normal number
+    const int free_env = env_int("SFMHIP_TSDF_FREE", 1);
+    const bool want_free = free_env != 0 && trunc >= 0x1p-100f && trunc <= 0x1p100f;
+    const float free_ts = free_env == 2 ? 0.5f : 1.0f;
+    const int cf = std::min(chunk, F);
+    const size_t nblk = (size_t)cf * nbu * nbv;
+    float* rec = nullptr;
+    if (hipMallocAsync((void**)&rec, (size_t)cf * 16 * sizeof(float), st) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("sfmhip_tsdf_integrate: camera table allocation failed");
+        return SFMHIP_E_HIP;
+    }
     float* cbmax = nullptr;
+    float* cbmin = nullptr;
+    unsigned* cfree = nullptr;
     unsigned* cmask = nullptr;
     int4* crange = nullptr;
-    if (want_cull && chunk <= 32) {
-        if (hipMallocAsync((void**)&cbmax, (size_t)chunk * nbu * nbv * sizeof(float), st) != hipSuccess) cbmax = nullptr;
-        if (cbmax && (hipMallocAsync((void**)&cmask, (size_t)nsub * sizeof(unsigned), st) != hipSuccess ||
-                      hipMallocAsync((void**)&crange, (size_t)chunk * sizeof(int4), st) != hipSuccess)) {
+    if (want_cull) {
+        if (hipMallocAsync((void**)&cbmax, nblk * sizeof(float), st) != hipSuccess) cbmax = nullptr;
+        if (cbmax && (hipMallocAsync((void**)&cmask, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess ||
+                      hipMallocAsync((void**)&crange, (size_t)cf * sizeof(int4), st) != hipSuccess)) {
             if (cmask) (void)hipFreeAsync(cmask, st);
             (void)hipFreeAsync(cbmax, st);
             cbmax = nullptr;
             cmask = nullptr;
             crange = nullptr;
+        }
+        if (cmask && want_free &&
+            (hipMallocAsync((void**)&cbmin, nblk * sizeof(float), st) != hipSuccess ||
+             hipMallocAsync((void**)&cfree, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess)) {
+            if (cbmin) (void)hipFreeAsync(cbmin, st);   // free-space path off, culling unchanged
+            cbmin = nullptr;
+            cfree = nullptr;
         }
         (void)hipGetLastError();
     }
@@ -1165,41 +1298,87 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
     int rc = SFMHIP_OK;
     for (int f0 = 0; f0 < F; f0 += chunk) {
         const int nf = std::min(chunk, F - f0);
+        const int nwf = ceil_div(nf, 32);
         const float* dp = depth + (size_t)f0 * Hd * Wd;
         const float* pp = poses + (size_t)f0 * 12;
         const float* kp = Kf + (size_t)f0 * 4;
+        hipLaunchKernelGGL(tsdf_cam_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, pp, kp, nf, rec);
         if (cmask) {
             hipLaunchKernelGGL(tsdf_footprint_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, D, H, W, z0, z1, nf, Hd,
                                Wd, pp, kp, bb, nbu, nbv, crange);
             if (Wd % 4 == 0)
                 hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st,
-                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmax);
+                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmax, cbmin);
             else
                 hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st,
-                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmax);
-            hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)ceil_div(ntests * 32, (int64_t)256)), dim3(256), 0, st,
-                               D, H, W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, cbmax, nbu, nbv, crange, per_tile,
-                               cmask);
+                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmax, cbmin);
+            hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nwf * 2)), dim3(1024), 0, st, D, H,
+                               W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, cbmax, cbmin, nbu, nbv, crange, per_tile,
+                               nwf, (unsigned short*)cmask, (unsigned short*)cfree);
         }
-#define SFMHIP_TSDF(UU, SS)                                                                                   \
-    hipLaunchKernelGGL((tsdf_kernel<UU, SS>), grid, dim3(256), (size_t)nf * 16 * sizeof(float), st, T, Wt, D, H, \
-                       W, z0, z1, dp, nf, Hd, Wd, pp, kp, bb, trunc, sb, cmask)
-        switch (unroll * 2 + (swz ? 1 : 0)) {
-            case 2: SFMHIP_TSDF(1, false); break;
-            case 3: SFMHIP_TSDF(1, true); break;
-            case 4: SFMHIP_TSDF(2, false); break;
-            case 5: SFMHIP_TSDF(2, true); break;
-            case 8: SFMHIP_TSDF(4, false); break;
-            default: SFMHIP_TSDF(4, true); break;
+        if (stats) {
+            if (!cmask) {
+                set_error("sfmhip_tsdf_cull_stats: scratch allocation failed");
+                rc = SFMHIP_E_HIP;
+                break;
+            }
+            std::vector<unsigned> mc((size_t)nsub * nwf), mf((size_t)nsub * nwf, 0u);
+            hipError_t e = hipMemcpyAsync(mc.data(), cmask, mc.size() * sizeof(unsigned), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess && cfree)
+                e = hipMemcpyAsync(mf.data(), cfree, mf.size() * sizeof(unsigned), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) {
+                set_error("sfmhip_tsdf_cull_stats: %s", hipGetErrorString(e));
+                rc = SFMHIP_E_HIP;
+                break;
+            }
+            for (size_t i = 0; i < mc.size(); ++i) {
+                const int nb = std::min(32, nf - 32 * (int)(i % nwf));
+                const unsigned live = nb >= 32 ? ~0u : ((1u << nb) - 1u);
+                stats[0] += nb;
+                stats[1] += __builtin_popcount(mc[i] & live);
+                stats[2] += __builtin_popcount(mf[i] & live & ~mc[i]);
+            }
+            continue;
         }
-#undef SFMHIP_TSDF
+        const unsigned* fmask = cfree;
+        if (cmask && cfree && free_env >= 3) {
+            hipLaunchKernelGGL(tsdf_probe_mask_kernel, dim3((unsigned)ceil_div(nsub * nwf, (int64_t)256)), dim3(256),
+                               0, st, cmask, cfree, nsub * nwf, free_env == 4 ? 1 : 0);
+            fmask = nullptr;
+        }
+        if (swz)
+            hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts);
+        else
+            hipLaunchKernelGGL(tsdf_kernel<false>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts);
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }
+    (void)hipFreeAsync(rec, st);
     if (crange) (void)hipFreeAsync(crange, st);
     if (cmask) (void)hipFreeAsync(cmask, st);
     if (cbmax) (void)hipFreeAsync(cbmax, st);
+    if (cfree) (void)hipFreeAsync(cfree, st);
+    if (cbmin) (void)hipFreeAsync(cbmin, st);
     return rc;
+}
+
+extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, int z0, int z1,
+                                     const float* depth, int F, int Hd, int Wd, const float* poses,
+                                     const float* Kf, const float* bmin, const float* bmax, float trunc,
+                                     void* stream) {
+    return tsdf_run(T, Wt, D, H, W, z0, z1, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, nullptr);
+}
+
+extern "C" int sfmhip_tsdf_cull_stats(int D, int H, int W, int z0, int z1, const float* depth, int F, int Hd,
+                                      int Wd, const float* poses, const float* Kf, const float* bmin,
+                                      const float* bmax, float trunc, int64_t* stats, void* stream) {
+    SFMHIP_REQUIRE(stats, "sfmhip_tsdf_cull_stats: null pointer");
+    stats[0] = stats[1] = stats[2] = 0;
+    float dummy = 0.f;   // the grids are not touched
+    return tsdf_run(&dummy, &dummy, D, H, W, z0, z1, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, stats);
 }
 
 extern "C" int sfmhip_grid_from_voxel_major(const float* grid_vm, int C, int D, int H, int W, float* grid,

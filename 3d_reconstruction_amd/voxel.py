@@ -31,6 +31,7 @@ def _f3(v) -> np.ndarray:
 
 
 def _host_ptr(a: np.ndarray) -> int:
+    """Address of a host array; the caller must keep `a` referenced until the call returns."""
     return a.ctypes.data
 
 
@@ -61,8 +62,9 @@ def ray_aabb(rays_o: torch.Tensor, rays_d: torch.Tensor, min_bound, max_bound):
     tn = torch.empty(B, dtype=torch.float32, device=o.device)
     tf = torch.empty_like(tn)
     valid = torch.empty(B, dtype=torch.uint8, device=o.device)
-    call("sfmhip_ray_aabb", ptr(o), ptr(d), B, _host_ptr(_f3(min_bound)), _host_ptr(_f3(max_bound)), ptr(tn),
-         ptr(tf), ptr(valid), stream_ptr())
+    bmn, bmx = _f3(min_bound), _f3(max_bound)   # kept alive across the call
+    call("sfmhip_ray_aabb", ptr(o), ptr(d), B, _host_ptr(bmn), _host_ptr(bmx), ptr(tn), ptr(tf), ptr(valid),
+         stream_ptr())
     return tn, tf, valid.bool()
 
 
@@ -175,3 +177,24 @@ def tsdf_integrate(T: torch.Tensor, Wt: torch.Tensor, depth: torch.Tensor, poses
     bmn, bmx = _f3(bmin), _f3(bmax)
     call("sfmhip_tsdf_integrate", ptr(T), ptr(Wt), D, H, W, int(z0), z1, ptr(dp), F, Hd, Wd, ptr(ps), ptr(kk),
          _host_ptr(bmn), _host_ptr(bmx), float(trunc), stream_ptr())
+
+
+def tsdf_cull_stats(shape, depth: torch.Tensor, poses: torch.Tensor, K: torch.Tensor, bmin, bmax, trunc: float,
+                    z0: int = 0, z1: int | None = None) -> dict:
+    """Diagnostics of tsdf_integrate's pre-passes on grid `shape` = (D,H,W):
+    how many (8x2x8 wave sub-tile, frame) pairs are culled and how many are
+    fused as free space (tsdf = 1, no depth gather)."""
+    require_gpu()
+    D, H, W = (int(v) for v in shape)
+    z1 = D if z1 is None else int(z1)
+    dp = dev(depth, torch.float32)
+    ps = dev(poses, torch.float32)
+    kk = dev(K, torch.float32)
+    F, Hd, Wd = dp.shape
+    st = np.zeros(3, np.int64)
+    bmn, bmx = _f3(bmin), _f3(bmax)   # kept alive across the call
+    call("sfmhip_tsdf_cull_stats", D, H, W, int(z0), z1, ptr(dp), F, Hd, Wd, ptr(ps), ptr(kk),
+         _host_ptr(bmn), _host_ptr(bmx), float(trunc), st.ctypes.data, stream_ptr())
+    n = max(int(st[0]), 1)
+    return {"tested": int(st[0]), "culled": int(st[1]), "free": int(st[2]),
+            "culled_frac": st[1] / n, "free_frac": st[2] / n, "full_frac": 1 - (st[1] + st[2]) / n}

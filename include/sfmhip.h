@@ -186,6 +186,17 @@ int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, int z0, int 
                           const float* bmin, const float* bmax, float trunc,
                           void* stream);
 
+/* Diagnostics for the TSDF pre-passes (no reference counterpart): runs only
+ * the culling / free-space tests of sfmhip_tsdf_integrate over the same
+ * arguments and returns HOST int64 stats[3] = (wave sub-tile, frame) pairs
+ * tested, culled (no voxel updates), free space (every voxel updates with
+ * tsdf = 1, fused without depth gathers).  Synchronises the stream.         */
+int sfmhip_tsdf_cull_stats(int D, int H, int W, int z0, int z1,
+                           const float* depth, int F, int Hd, int Wd,
+                           const float* poses, const float* Kf,
+                           const float* bmin, const float* bmax, float trunc,
+                           int64_t* stats, void* stream);
+
 /* ---- §8f row 2: geometric verification (batched over image pairs) --------
  * cv2.findEssentialMat(pts0, pts1, K, method=cv2.RANSAC, prob=0.999,
  * threshold=1) at matching.py:134 and sfm.py:108 (OpenCV five-point.cpp +

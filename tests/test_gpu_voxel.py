@@ -137,18 +137,58 @@ def test_tsdf_edge_cases_bitexact(sfm, gpu, monkeypatch, Wd):
 
 
 def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
-    """The (tile, frame) culling pre-pass only drops work: grids with and
-    without it are bit-identical (full-resolution frames, 96^3 grid, z-slab)."""
-    depth, poses, K = syn.tsdf_scene(10, seed=3)
+    """The (tile, frame) culling pre-pass only drops work and the free-space
+    path only skips gathers: grids with culling off, culling without the
+    free-space path and both on are bit-identical (full-resolution frames,
+    96^3 grid, z-slab), and the free-space path is exercised (probe mode
+    SFMHIP_TSDF_FREE=2 writes tsdf 0.5 there, which must change the grid)."""
+    depth, poses, K = syn.tsdf_scene(40, seed=3)   # two mask words per sub-tile
     out = []
-    for cull in ("0", "2"):
+    for cull, free, sub, chunk in (("0", "1", "1", "512"), ("2", "0", "1", "512"), ("2", "1", "1", "512"),
+                                   ("2", "2", "1", "512"), ("2", "1", "4", "512"), ("2", "1", "1", "3")):
         monkeypatch.setenv("SFMHIP_TSDF_CULL", cull)
+        monkeypatch.setenv("SFMHIP_TSDF_FREE", free)
+        monkeypatch.setenv("SFMHIP_TSDF_CULLSUB", sub)
+        monkeypatch.setenv("SFMHIP_TSDF_CHUNK", chunk)
         T = torch.zeros((96, 96, 96), dtype=torch.float32, device=gpu)
         W = torch.zeros_like(T)
         sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95, z0=5, z1=90)
         out.append((T.cpu(), W.cpu()))
-    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    for i in (1, 2, 4, 5):
+        assert torch.equal(out[0][0], out[i][0]) and torch.equal(out[0][1], out[i][1])
     assert (out[0][1] > 0).float().mean() > 0.3
+    assert torch.equal(out[0][1], out[3][1])            # probe: same update pattern ...
+    assert (out[3][0] != out[0][0]).float().mean() > 0.05  # ... and many free-space updates
+
+
+@pytest.mark.parametrize("trunc", [0.1, 0.3, 3 * 2.0 / 31, 0.0625])
+def test_tsdf_free_space_near_trunc_bitexact(sfm, gpu, monkeypatch, trunc):
+    """Frontal planes placed so that whole tiles sit just in front of depth - mu
+    (the free-space proof's boundary), several truncation distances, prior
+    (T, W) state: bit-exact with the oracle, with culling + free space forced."""
+    monkeypatch.setenv("SFMHIP_TSDF_CULL", "2")
+    R, F, Hd, Wd = 32, 6, 64, 80
+    rng = np.random.default_rng(int(trunc * 1000))
+    zs = (np.float32(-1) + np.arange(R, dtype=np.float32) * (np.float32(2) / np.float32(R - 1)))
+    depth = np.empty((F, Hd, Wd), np.float32)
+    poses = np.zeros((F, 3, 4), np.float32)
+    poses[:, 0, 0] = poses[:, 1, 1] = poses[:, 2, 2] = 1.0
+    poses[:, 2, 3] = 4.0
+    for f in range(F):
+        # plane at the Zc of a voxel layer + mu (+ a few ulps either way)
+        zl = zs[rng.integers(4, R - 4)] + np.float32(4.0)
+        depth[f] = np.nextafter(zl + np.float32(trunc), np.float32(np.inf if f % 2 else -np.inf))
+        depth[f, :, : Wd // 3] += np.float32(0.5 * trunc)
+    K = np.tile(np.array([[60.0, 60.0, Wd / 2, Hd / 2]], np.float32), (F, 1))
+    T0 = rng.uniform(-1, 1, (R, R, R)).astype(np.float32)
+    W0 = rng.integers(0, 3, (R, R, R)).astype(np.float32)
+    T = torch.from_numpy(T0).to(gpu)
+    Wt = torch.from_numpy(W0).to(gpu)
+    sfm.tsdf_integrate(T, Wt, torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K),
+                       (-1, -1, -1), (1, 1, 1), trunc)
+    Tr, Wr = ov.tsdf_integrate(T0, W0, depth, poses, K, (-1, -1, -1), (1, 1, 1), np.float32(trunc))
+    np.testing.assert_array_equal(Wt.cpu().numpy(), Wr)
+    np.testing.assert_array_equal(T.cpu().numpy(), Tr)
 
 
 def test_tsdf_zslab_split_equals_whole(sfm, gpu):
