@@ -492,13 +492,13 @@ __global__ void tsdf_footprint_kernel(int D, int H, int W, int z0, int z1, int F
 
 // VEC: Wd % 4 == 0, one float4 (4 pixels) per lane, 4 lanes per block column,
 // all 16 rows' loads in flight.  Otherwise one pixel per lane, 16 lanes per block.
-// bmax ignores NaN (a NaN depth never updates); bmin (when non-null) is poisoned
-// by NaN (-inf: such a block never proves free space).
+// Table entry {min, max} per 16x16 block: max ignores NaN (a NaN depth never
+// updates), min is poisoned by NaN (-inf: such a block never proves free space).
 __device__ __forceinline__ float nan_low(float x) { return x == x ? x : -__builtin_inff(); }
 template <bool VEC>
 __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __restrict__ depth, int F, int Hd, int Wd,
                                                              int nbu, int nbv, const int4* __restrict__ range,
-                                                             float* __restrict__ bmax, float* __restrict__ bmin) {
+                                                             float2* __restrict__ bmm) {
     const int f = blockIdx.z, bv = blockIdx.y;
     const int4 rg = range[f];                       // blocks the slab can touch in this frame
     if (bv < rg.z || bv > rg.w) return;
@@ -518,22 +518,17 @@ __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __rest
                               : make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff());
 #pragma unroll
             for (int r = 0; r < kCullBlock; ++r) m = fmaxf(m, fmaxf(fmaxf(q[r].x, q[r].y), fmaxf(q[r].z, q[r].w)));
-            if (bmin)
 #pragma unroll
-                for (int r = 0; r < kCullBlock; ++r)
-                    if (r < nr)
-                        mn = fminf(mn, fminf(fminf(nan_low(q[r].x), nan_low(q[r].y)),
-                                             fminf(nan_low(q[r].z), nan_low(q[r].w))));
+            for (int r = 0; r < kCullBlock; ++r)
+                if (r < nr)
+                    mn = fminf(mn, fminf(fminf(nan_low(q[r].x), nan_low(q[r].y)), fminf(nan_low(q[r].z), nan_low(q[r].w))));
         }
         m = fmaxf(m, __shfl_xor(m, 1, 4));
         m = fmaxf(m, __shfl_xor(m, 2, 4));
         mn = fminf(mn, __shfl_xor(mn, 1, 4));
         mn = fminf(mn, __shfl_xor(mn, 2, 4));
         const int bu = u / kCullBlock;
-        if ((threadIdx.x & 3) == 0 && bu < nbu) {
-            bmax[slot * nbu + bu] = m;
-            if (bmin) bmin[slot * nbu + bu] = mn;
-        }
+        if ((threadIdx.x & 3) == 0 && bu < nbu) bmm[slot * nbu + bu] = make_float2(mn, m);
     } else {
         const int u = blockIdx.x * 256 + threadIdx.x;
         if (u < Wd)
@@ -548,27 +543,10 @@ __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __rest
             mn = fminf(mn, __shfl_xor(mn, off, 16));
         }
         const int bu = u / kCullBlock;
-        if ((threadIdx.x & 15) == 0 && bu < nbu) {
-            bmax[slot * nbu + bu] = m;
-            if (bmin) bmin[slot * nbu + bu] = mn;
-        }
+        if ((threadIdx.x & 15) == 0 && bu < nbu) bmm[slot * nbu + bu] = make_float2(mn, m);
     }
 }
 
-// One lane per (wave sub-tile, frame); sub-tile = the 8 x 2 x 8 voxels of one
-// wave of the workgroup tile.  Interval bounds on the affine camera
-// coordinates over the sub-tile (centre +- sum |P_rj| h_j), pixel bounds from
-// the X/Z and Y/Z interval quotients (a superset of the exact projection).
-// Two ballot words per (sub-tile, 32 frames):
-//   cull: no voxel of the sub-tile updates in this frame (dropped);
-//   free: every voxel updates with tsdf = 1 exactly (free space in front of the
-//     surface), so the fusion kernel applies T = (T W + 1)/(W + 1) without
-//     projecting or gathering.  Proven when the frame's record is one the kernel
-//     fuses (every pose / intrinsic finite and < 2^60), the unclipped pixel box
-//     lies inside the image, every f32 Zc is in [2^-59, 2^59], and the smallest
-//     depth under the box (NaN-poisoned block minima) exceeds the largest f32 Zc by
-//     at least mu (1 + 2^-20): then fl(depth - Zc) >= mu (1 + 2^-20) and
-//     fl(fl(depth - Zc) * fl(1/mu)) >= 1, i.e. the kernel's tsdf is min(1, .) = 1.
 constexpr int kCullSub = 4;   // waves per workgroup tile
 // One workgroup per (4x4x4 brick of sub-tiles, 16 frames): wave j tests frame
 // 16 h + j for the brick's 64 sub-tiles (one per lane), so the camera loads are
@@ -579,8 +557,8 @@ constexpr int kCullSub = 4;   // waves per workgroup tile
 constexpr int kCullFrames = 16;
 __global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, int z0, int z1, int F, int Hd, int Wd,
                                                          const float* __restrict__ poses, const float* __restrict__ Kf,
-                                                         Bounds B, float trunc, const float* __restrict__ bmax,
-                                                         const float* __restrict__ bmin, int nbu, int nbv,
+                                                         Bounds B, float trunc, const float2* __restrict__ bmm,
+                                                         int use_free, int nbu, int nbv,
                                                          const int4* __restrict__ range, int per_tile, int nw,
                                                          unsigned short* __restrict__ cull,
                                                          unsigned short* __restrict__ freem) {
@@ -616,35 +594,30 @@ __global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, in
             const int4 rg = range[f];   // only blocks inside the slab's range were computed
             const int nu = bu1 - bu0 + 1, nb = nu * (bv1 - bv0 + 1);
             if (nb <= kCullMaxBlocks && bu0 >= rg.x && bu1 <= rg.y && bv0 >= rg.z && bv1 <= rg.w) {
-                const size_t o = ((size_t)f * nbv + bv0) * nbu + bu0;
-                const float* bp = bmax + o;
-                float m = -__builtin_inff();
+                const float2* bp = bmm + ((size_t)f * nbv + bv0) * nbu + bu0;
+                float m = -__builtin_inff(), mn = __builtin_inff();
                 for (int bv = bv0; bv <= bv1; ++bv, bp += nbu) {
                     int i = 0;
-                    for (; i + 4 <= nu; i += 4)   // 4 independent loads in flight
-                        m = fmaxf(fmaxf(m, fmaxf(bp[i], bp[i + 1])), fmaxf(bp[i + 2], bp[i + 3]));
-                    for (; i < nu; ++i) m = fmaxf(m, bp[i]);
+                    for (; i + 4 <= nu; i += 4) {   // 4 independent loads in flight
+                        const float2 e0 = bp[i], e1 = bp[i + 1], e2 = bp[i + 2], e3 = bp[i + 3];
+                        m = fmaxf(fmaxf(m, fmaxf(e0.y, e1.y)), fmaxf(e2.y, e3.y));
+                        mn = fminf(fminf(mn, fminf(e0.x, e1.x)), fminf(e2.x, e3.x));
+                    }
+                    for (; i < nu; ++i) {
+                        m = fmaxf(m, bp[i].y);
+                        mn = fminf(mn, bp[i].x);   // never NaN (poisoned to -inf)
+                    }
                 }
                 // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for the
                 // rounding of (depth - Zc), so the kernel's !(sdf < -trunc) test fails everywhere
                 skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * 0x1p-24) + 1e-30 < zlo);
-                if (!skip && bmin && inside && zlo >= 0x1p-59 && zhi <= 0x1p59) {
+                if (!skip && use_free && inside && zlo >= 0x1p-59 && zhi <= 0x1p59) {
                     bool good = true;
 #pragma unroll
                     for (int q = 0; q < 12; ++q) good = good && fabsf(poses[f * 12 + q]) < 0x1p60f;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) good = good && fabsf(Kf[f * 4 + q]) < 0x1p60f;
-                    if (good) {
-                        const float* bq = bmin + o;
-                        float mn = __builtin_inff();
-                        for (int bv = bv0; bv <= bv1; ++bv, bq += nbu) {
-                            int i = 0;
-                            for (; i + 4 <= nu; i += 4)
-                                mn = fminf(fminf(mn, fminf(bq[i], bq[i + 1])), fminf(bq[i + 2], bq[i + 3]));
-                            for (; i < nu; ++i) mn = fminf(mn, bq[i]);   // never NaN (poisoned to -inf)
-                        }
-                        fre = (double)mn - zhi >= (double)trunc * (1 + 0x1p-20);
-                    }
+                    fre = good && (double)mn - zhi >= (double)trunc * (1 + 0x1p-20);
                 }
             }
         }
@@ -711,7 +684,8 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
                                                    int W, int z0, int z1, const float* __restrict__ depth, int F,
                                                    int Hd, int Wd, const float* __restrict__ rec, Bounds B,
                                                    float trunc, SuperBrick SB, const unsigned* __restrict__ cull,
-                                                   const unsigned* __restrict__ freem, int nw, float free_ts) {
+                                                   const unsigned* __restrict__ freem, int nw, float free_ts,
+                                                   const float2* __restrict__ bmm, int nbu, int nbv) {
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (SWZ) {
         const int nbx = (W + kTsdfTX - 1) / kTsdfTX, nby = (H + kTsdfTY - 1) / kTsdfTY;
@@ -813,18 +787,39 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
             const int iu1 = cvt_flr(uu.y), iv1 = cvt_flr(vv.y);
             const bool ok0 = z_ok(Zc.x) && (unsigned)iu0 < (unsigned)Wd && (unsigned)iv0 < (unsigned)Hd;
             const bool ok1 = two && z_ok(Zc.y) && (unsigned)iu1 < (unsigned)Wd && (unsigned)iv1 < (unsigned)Hd;
-            // bounds-checked gather: off-image lanes read 0 or a discarded in-frame value
+            // Per-voxel test against the pixel's 16x16 block {min, max} (exact, with this
+            // kernel's own f32 Zc: every depth d of the block has fl(d - Zc) between
+            // fl(min - Zc) and fl(max - Zc)): free (tsdf = 1) or no update without the depth.
+            bool fr0 = false, fr1 = false, need0 = ok0, need1 = ok1;
+            if (bmm) {
+                const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+                    (void*)(bmm + (size_t)f * nbv * nbu), (short)0, nbv * nbu * 8, 0x00020000);
+                const auto e0 = __builtin_amdgcn_raw_buffer_load_b64(rb, ((iv0 >> 4) * nbu + (iu0 >> 4)) * 8, 0, 0);
+                const auto e1 = __builtin_amdgcn_raw_buffer_load_b64(rb, ((iv1 >> 4) * nbu + (iu1 >> 4)) * 8, 0, 0);
+                const f2 bmn = {__builtin_bit_cast(float, (unsigned)e0[0]), __builtin_bit_cast(float, (unsigned)e1[0])};
+                const f2 bmx = {__builtin_bit_cast(float, (unsigned)e0[1]), __builtin_bit_cast(float, (unsigned)e1[1])};
+                const f2 scm = (bmn - Zc) * f2s(inv_trunc);
+                const f2 smx = bmx - Zc;
+                fr0 = ok0 && bmn.x > 0.f && scm.x >= 1.f;
+                fr1 = ok1 && bmn.y > 0.f && scm.y >= 1.f;
+                need0 = ok0 && !fr0 && bmx.x > 0.f && !(smx.x < -trunc);
+                need1 = ok1 && !fr1 && bmx.y > 0.f && !(smx.y < -trunc);
+            }
+            // bounds-checked gather, only where the block test did not decide
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc((void*)(depth + (size_t)f * frame), (short)0, nbytes, 0x00020000);
-            const f2 dep = {__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                          rs, (int)(__umul24(iv0, Wd4) + ((unsigned)iu0 << 2)), 0, 0)),
-                            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                          rs, (int)(__umul24(iv1, Wd4) + ((unsigned)iu1 << 2)), 0, 0))};
+            f2 dep = {0.f, 0.f};
+            if (need0)
+                dep.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     rs, (int)(__umul24(iv0, Wd4) + ((unsigned)iu0 << 2)), 0, 0));
+            if (need1)
+                dep.y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     rs, (int)(__umul24(iv1, Wd4) + ((unsigned)iu1 << 2)), 0, 0));
             const f2 sdf = dep - Zc;
-            const bool g0 = ok0 && dep.x > 0.f && !(sdf.x < -trunc);
-            const bool g1 = ok1 && dep.y > 0.f && !(sdf.y < -trunc);
+            const bool g0 = fr0 || (need0 && dep.x > 0.f && !(sdf.x < -trunc));
+            const bool g1 = fr1 || (need1 && dep.y > 0.f && !(sdf.y < -trunc));
             const f2 sc = sdf * f2s(inv_trunc);
-            update(f2{fminf(1.0f, sc.x), fminf(1.0f, sc.y)}, g0, g1);
+            update(f2{fr0 ? free_ts : fminf(1.0f, sc.x), fr1 ? free_ts : fminf(1.0f, sc.y)}, g0, g1);
         }
     }
     T[idx] = tv.x;
@@ -1231,11 +1226,9 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const int cull_env = env_int("SFMHIP_TSDF_CULL", 1);
     const bool cull_pays = (double)(z1 - z0) * H * W >= 1.5 * (double)Hd * Wd;
     const bool want_cull = stats || cull_env == 2 || (cull_env == 1 && cull_pays);
-    // 64 frames per launch: the resident workgroups then gather from a bounded set of
-    // frames (L2 locality; one launch over all 257 C5 frames ran the fusion ~10 % slower)
-    // while the grid traffic / dispatch cost per launch stays small (fully culled waves
-    // do not even read the grid)
-    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", 64)));
+    // every frame in one launch (<= 512): the grid is read and written once and there is
+    // one dispatch; 64-frame launches measured 2.65 vs 2.29 ms on C5
+    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", kTsdfMaxFrames)));
     const int nw = ceil_div(std::min(chunk, F), 32);   // mask words per sub-tile slot
     const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 3)), std::max(1, env_int("SFMHIP_TSDF_SBY", 2)),
                         std::max(1, env_int("SFMHIP_TSDF_SBZ", std::min(8, nbz))), env_int("SFMHIP_TSDF_IL", 1)};
@@ -1270,30 +1263,26 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         set_error("sfmhip_tsdf_integrate: camera table allocation failed");
         return SFMHIP_E_HIP;
     }
-    float* cbmax = nullptr;
-    float* cbmin = nullptr;
+    float2* cbmm = nullptr;
     unsigned* cfree = nullptr;
     unsigned* cmask = nullptr;
     int4* crange = nullptr;
     if (want_cull) {
-        if (hipMallocAsync((void**)&cbmax, nblk * sizeof(float), st) != hipSuccess) cbmax = nullptr;
-        if (cbmax && (hipMallocAsync((void**)&cmask, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess ||
-                      hipMallocAsync((void**)&crange, (size_t)cf * sizeof(int4), st) != hipSuccess)) {
+        if (hipMallocAsync((void**)&cbmm, nblk * sizeof(float2), st) != hipSuccess) cbmm = nullptr;
+        if (cbmm && (hipMallocAsync((void**)&cmask, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess ||
+                     hipMallocAsync((void**)&crange, (size_t)cf * sizeof(int4), st) != hipSuccess)) {
             if (cmask) (void)hipFreeAsync(cmask, st);
-            (void)hipFreeAsync(cbmax, st);
-            cbmax = nullptr;
+            (void)hipFreeAsync(cbmm, st);
+            cbmm = nullptr;
             cmask = nullptr;
             crange = nullptr;
         }
-        if (cmask && want_free &&
-            (hipMallocAsync((void**)&cbmin, nblk * sizeof(float), st) != hipSuccess ||
-             hipMallocAsync((void**)&cfree, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess)) {
-            if (cbmin) (void)hipFreeAsync(cbmin, st);   // free-space path off, culling unchanged
-            cbmin = nullptr;
-            cfree = nullptr;
-        }
+        if (cmask && want_free && hipMallocAsync((void**)&cfree, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess)
+            cfree = nullptr;   // free-space path off, culling unchanged
         (void)hipGetLastError();
     }
+    // per-voxel block test in the fusion kernel (with the free-space path; SFMHIP_TSDF_VOXTEST=0 off)
+    const float2* vox_bmm = cfree && env_int("SFMHIP_TSDF_VOXTEST", 1) != 0 ? cbmm : nullptr;
     // frame chunks run in order on the stream, so per-voxel update order is kept
     int rc = SFMHIP_OK;
     for (int f0 = 0; f0 < F; f0 += chunk) {
@@ -1308,12 +1297,12 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                                Wd, pp, kp, bb, nbu, nbv, crange);
             if (Wd % 4 == 0)
                 hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st,
-                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmax, cbmin);
+                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
             else
                 hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st,
-                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmax, cbmin);
+                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
             hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nwf * 2)), dim3(1024), 0, st, D, H,
-                               W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, cbmax, cbmin, nbu, nbv, crange, per_tile,
+                               W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, cbmm, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
                                nwf, (unsigned short*)cmask, (unsigned short*)cfree);
         }
         if (stats) {
@@ -1349,19 +1338,18 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         }
         if (swz)
             hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_bmm, nbu, nbv);
         else
             hipLaunchKernelGGL(tsdf_kernel<false>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_bmm, nbu, nbv);
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }
     (void)hipFreeAsync(rec, st);
     if (crange) (void)hipFreeAsync(crange, st);
     if (cmask) (void)hipFreeAsync(cmask, st);
-    if (cbmax) (void)hipFreeAsync(cbmax, st);
+    if (cbmm) (void)hipFreeAsync(cbmm, st);
     if (cfree) (void)hipFreeAsync(cfree, st);
-    if (cbmin) (void)hipFreeAsync(cbmin, st);
     return rc;
 }
 

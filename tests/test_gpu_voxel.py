@@ -144,18 +144,20 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
     SFMHIP_TSDF_FREE=2 writes tsdf 0.5 there, which must change the grid)."""
     depth, poses, K = syn.tsdf_scene(40, seed=3)   # two mask words per sub-tile
     out = []
-    for cull, free, sub, chunk in (("0", "1", "1", "512"), ("2", "0", "1", "512"), ("2", "1", "1", "512"),
-                                   ("2", "2", "1", "512"), ("2", "1", "4", "512"), ("2", "1", "1", "3")):
-        monkeypatch.setenv("SFMHIP_TSDF_CULL", cull)
-        monkeypatch.setenv("SFMHIP_TSDF_FREE", free)
-        monkeypatch.setenv("SFMHIP_TSDF_CULLSUB", sub)
-        monkeypatch.setenv("SFMHIP_TSDF_CHUNK", chunk)
+    variants = [dict(CULL="0"), dict(CULL="2", FREE="0"), dict(CULL="2"), dict(CULL="2", FREE="2"),
+                dict(CULL="2", CULLSUB="4"), dict(CULL="2", CHUNK="3"), dict(CULL="2", VOXTEST="0"),
+                dict(CULL="2", CHUNK="512")]
+    for v in variants:
+        for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST"):
+            monkeypatch.delenv("SFMHIP_TSDF_" + k, raising=False)
+        for k, x in v.items():
+            monkeypatch.setenv("SFMHIP_TSDF_" + k, x)
         T = torch.zeros((96, 96, 96), dtype=torch.float32, device=gpu)
         W = torch.zeros_like(T)
         sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95, z0=5, z1=90)
         out.append((T.cpu(), W.cpu()))
-    for i in (1, 2, 4, 5):
-        assert torch.equal(out[0][0], out[i][0]) and torch.equal(out[0][1], out[i][1])
+    for i in (1, 2, 4, 5, 6, 7):
+        assert torch.equal(out[0][0], out[i][0]) and torch.equal(out[0][1], out[i][1]), variants[i]
     assert (out[0][1] > 0).float().mean() > 0.3
     assert torch.equal(out[0][1], out[3][1])            # probe: same update pattern ...
     assert (out[3][0] != out[0][0]).float().mean() > 0.05  # ... and many free-space updates

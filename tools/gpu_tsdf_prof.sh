@@ -2,8 +2,8 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 mkdir -p gpurun_out
-for FR in 1 0 3 4; do
-  SFMHIP_TSDF_CHUNK=64 SFMHIP_TSDF_FREE=$FR timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tprof_free$FR -o run -- python tools/run_tsdf_once.py > gpurun_out/tprof_free$FR.log 2>&1 || { echo "prof $FR failed"; tail -5 gpurun_out/tprof_free$FR.log; exit 1; }
+for FR in 1 4; do
+  SFMHIP_TSDF_FREE=$FR timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tprof_free$FR -o run -- python tools/run_tsdf_once.py > gpurun_out/tprof_free$FR.log 2>&1 || { echo "prof $FR failed"; tail -5 gpurun_out/tprof_free$FR.log; exit 1; }
   find gpurun_out/tprof_free$FR -type f ! -name "*stats*" -delete
   python - "$FR" <<'PY'
 import csv, glob, sys
