@@ -1219,16 +1219,15 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     // XCDs (sweeps in tools/bench_tsdf_variants.py; with culling the work per tile is uneven, and
     // the interleave plus a width that does not divide the grid spreads it over the XCDs)
     const int nbx = ceil_div(W, kTsdfTX), nby = ceil_div(H, kTsdfTY), nbz = ceil_div(z1 - z0, kTsdfTZ);
-    // SFMHIP_TSDF_CULL: 0 off, 2 on, 1 (default) on when the slab is big enough that
-    // the skipped gathers outweigh the block-max pass over every depth pixel (cost
-    // model from the C5 measurements: ~35 % of ~1.7 ps per voxel-frame saved vs
-    // ~0.8 ps per depth pixel read, i.e. worth it above ~1.5 voxels per pixel).
+    // SFMHIP_TSDF_CULL: 0 off (A/B runs), otherwise on: with the free-space path the
+    // pre-passes pay even for the thin z-slabs of an 8-way split (tools/bench_tsdf_slabs.py:
+    // N=8 slab 0.92 vs 1.34 ms without them)
     const int cull_env = env_int("SFMHIP_TSDF_CULL", 1);
-    const bool cull_pays = (double)(z1 - z0) * H * W >= 1.5 * (double)Hd * Wd;
-    const bool want_cull = stats || cull_env == 2 || (cull_env == 1 && cull_pays);
-    // every frame in one launch (<= 512): the grid is read and written once and there is
-    // one dispatch; 64-frame launches measured 2.65 vs 2.29 ms on C5
-    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", kTsdfMaxFrames)));
+    const bool want_cull = stats || cull_env != 0;
+    // every frame in one launch (<= 512) with culling: the grid is read and written once and
+    // there is one dispatch (64-frame launches: 2.65 vs 2.29 ms on C5); without culling every
+    // frame gathers, and 64-frame launches keep the resident workgroups' depth set in L2
+    const int chunk = std::max(1, std::min(kTsdfMaxFrames, env_int("SFMHIP_TSDF_CHUNK", want_cull ? kTsdfMaxFrames : 64)));
     const int nw = ceil_div(std::min(chunk, F), 32);   // mask words per sub-tile slot
     const SuperBrick sb{std::max(1, env_int("SFMHIP_TSDF_SBX", 3)), std::max(1, env_int("SFMHIP_TSDF_SBY", 2)),
                         std::max(1, env_int("SFMHIP_TSDF_SBZ", std::min(8, nbz))), env_int("SFMHIP_TSDF_IL", 1)};

@@ -35,7 +35,7 @@ def per_dispatch(kind):
 
 
 traffic = {}
-for kind, nd in (("match", 1), ("tsdf", math.ceil(257 / 24))):
+for kind, nd in (("match", 1), ("tsdf", 1)):
     kern = per_dispatch(kind)
     rd = sum(2 * c["FETCH_SIZE"] * 1024 * nd for c in kern.values())
     wr = sum(c["WRITE_SIZE"] * 1024 * nd for c in kern.values())
@@ -44,6 +44,6 @@ for kind, nd in (("match", 1), ("tsdf", math.ceil(257 / 24))):
 traffic["source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/pmc.sh, GPU round {tag}, "
                      "profiles/r1/pmc_raw); FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half the bytes "
                      "of wide streaming reads); workloads: C3 all-pairs match launch (tools/run_match_once.py), C5 "
-                     "full 257-frame fusion in 24-frame launches (tools/run_tsdf_once.py)")
+                     "full 257-frame fusion, one launch of each pre-pass and of the fusion kernel (tools/run_tsdf_once.py)")
 json.dump(traffic, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
 print(json.dumps(traffic, indent=1))
