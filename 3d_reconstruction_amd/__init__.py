@@ -13,7 +13,7 @@ from .match import (MODE_FLOAT, MODE_SIFT, DescriptorBank, Matcher, all_pairs,  
 from .geometry import (Rodrigues, ba_sparse, calculate_reprojection_error,  # noqa: F401
                        convertPointsFromHomogeneous, fd_jacobian, projectPoints,
                        residual_jacobian_batched, triangulatePoints, triangulate_batched)
-from .voxel import (MASK_PLENOXEL, MASK_SDF, VoxelGrid, tsdf_cull_stats, tsdf_integrate,  # noqa: F401
+from .voxel import (MASK_PLENOXEL, MASK_SDF, VoxelGrid, tsdf_block_table, tsdf_cull_stats, tsdf_integrate,  # noqa: F401,E501
                     voxel_traversal)
 from . import bow, pipeline, reconstruct, tracks, verify  # noqa: F401,E402
 from .bow import kmeans  # noqa: F401

@@ -65,6 +65,9 @@ SIGNATURES = {
     "sfmhip_render_rays": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _i64, _i32, _p, _p],
     "sfmhip_tsdf_integrate": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p,
                               _f32, _p],
+    "sfmhip_tsdf_block_table": [_p, _i32, _i32, _i32, _i32, _i32, _p, _p],
+    "sfmhip_tsdf_integrate_tab": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p,
+                                  _f32, _p, _p],
     "sfmhip_tsdf_cull_stats": [_i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p, _f32, _p, _p],
     "sfmhip_find_essential": [_p, _p, _p, _i32, _p, _f64, _f64, _i32, _p, _p, _p, _p, _p, _p, _p],
     "sfmhip_recover_pose": [_p, _i64, _p, _p, _p, _i32, _p, _p, _f64, _p, _p, _p, _p, _p],

@@ -471,6 +471,11 @@ __device__ int box_footprint(const float* P, const float* k, const Bounds& B, in
     return 2;
 }
 
+__global__ void full_range_kernel(int F, int nbu, int nbv, int4* __restrict__ range) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < F) range[f] = make_int4(0, nbu - 1, 0, nbv - 1);
+}
+
 // Per frame: the depth blocks the slab [z0, z1) can touch (int4 {bu0, bu1, bv0,
 // bv1}; an empty range when the whole slab is off-image, every block when the
 // footprint cannot be bounded).  The block-max pass fills only these blocks and
@@ -1199,9 +1204,11 @@ extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, con
 
 // stats != nullptr: run only the culling pre-passes (forced on) and count
 // (wave sub-tile, frame) pairs: stats[0] tested, [1] culled, [2] free space.
+// ext_table != nullptr: the caller's {min, max} block table of every frame over the
+// whole image ([F][nbv][nbu] float2, sfmhip_tsdf_block_table); the block pass is skipped.
 static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, const float* depth, int F, int Hd,
                     int Wd, const float* poses, const float* Kf, const float* bmin, const float* bmax, float trunc,
-                    void* stream, int64_t* stats) {
+                    void* stream, int64_t* stats, const float2* ext_table) {
     SFMHIP_REQUIRE(T && Wt && depth && poses && Kf && bmin && bmax, "sfmhip_tsdf_integrate: null pointer");
     SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && F >= 0 && Hd > 0 && Wd > 0, "sfmhip_tsdf_integrate: bad shape");
     SFMHIP_REQUIRE(0 <= z0 && z0 <= z1 && z1 <= D, "sfmhip_tsdf_integrate: bad z range");
@@ -1267,11 +1274,12 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     unsigned* cmask = nullptr;
     int4* crange = nullptr;
     if (want_cull) {
-        if (hipMallocAsync((void**)&cbmm, nblk * sizeof(float2), st) != hipSuccess) cbmm = nullptr;
+        if (ext_table) cbmm = const_cast<float2*>(ext_table);
+        else if (hipMallocAsync((void**)&cbmm, nblk * sizeof(float2), st) != hipSuccess) cbmm = nullptr;
         if (cbmm && (hipMallocAsync((void**)&cmask, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess ||
                      hipMallocAsync((void**)&crange, (size_t)cf * sizeof(int4), st) != hipSuccess)) {
             if (cmask) (void)hipFreeAsync(cmask, st);
-            (void)hipFreeAsync(cbmm, st);
+            if (!ext_table) (void)hipFreeAsync(cbmm, st);
             cbmm = nullptr;
             cmask = nullptr;
             crange = nullptr;
@@ -1281,7 +1289,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         (void)hipGetLastError();
     }
     // per-voxel block test in the fusion kernel (with the free-space path; SFMHIP_TSDF_VOXTEST=0 off)
-    const float2* vox_bmm = cfree && env_int("SFMHIP_TSDF_VOXTEST", 1) != 0 ? cbmm : nullptr;
+    const bool vox_test = cfree && env_int("SFMHIP_TSDF_VOXTEST", 1) != 0;
     // frame chunks run in order on the stream, so per-voxel update order is kept
     int rc = SFMHIP_OK;
     for (int f0 = 0; f0 < F; f0 += chunk) {
@@ -1291,7 +1299,10 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         const float* pp = poses + (size_t)f0 * 12;
         const float* kp = Kf + (size_t)f0 * 4;
         hipLaunchKernelGGL(tsdf_cam_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, pp, kp, nf, rec);
-        if (cmask) {
+        const float2* tab = ext_table ? ext_table + (size_t)f0 * nbv * nbu : cbmm;
+        if (cmask && ext_table) {
+            hipLaunchKernelGGL(full_range_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, nf, nbu, nbv, crange);
+        } else if (cmask) {
             hipLaunchKernelGGL(tsdf_footprint_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, D, H, W, z0, z1, nf, Hd,
                                Wd, pp, kp, bb, nbu, nbv, crange);
             if (Wd % 4 == 0)
@@ -1300,10 +1311,11 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             else
                 hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st,
                                    dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
-            hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nwf * 2)), dim3(1024), 0, st, D, H,
-                               W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, cbmm, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
-                               nwf, (unsigned short*)cmask, (unsigned short*)cfree);
         }
+        if (cmask)
+            hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nwf * 2)), dim3(1024), 0, st, D, H,
+                               W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
+                               nwf, (unsigned short*)cmask, (unsigned short*)cfree);
         if (stats) {
             if (!cmask) {
                 set_error("sfmhip_tsdf_cull_stats: scratch allocation failed");
@@ -1337,17 +1349,17 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         }
         if (swz)
             hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_bmm, nbu, nbv);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv);
         else
             hipLaunchKernelGGL(tsdf_kernel<false>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_bmm, nbu, nbv);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv);
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }
     (void)hipFreeAsync(rec, st);
     if (crange) (void)hipFreeAsync(crange, st);
     if (cmask) (void)hipFreeAsync(cmask, st);
-    if (cbmm) (void)hipFreeAsync(cbmm, st);
+    if (cbmm && !ext_table) (void)hipFreeAsync(cbmm, st);
     if (cfree) (void)hipFreeAsync(cfree, st);
     return rc;
 }
@@ -1356,7 +1368,46 @@ extern "C" int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, i
                                      const float* depth, int F, int Hd, int Wd, const float* poses,
                                      const float* Kf, const float* bmin, const float* bmax, float trunc,
                                      void* stream) {
-    return tsdf_run(T, Wt, D, H, W, z0, z1, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, nullptr);
+    return tsdf_run(T, Wt, D, H, W, z0, z1, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, nullptr,
+                    nullptr);
+}
+
+extern "C" int sfmhip_tsdf_integrate_tab(float* T, float* Wt, int D, int H, int W, int z0, int z1,
+                                         const float* depth, int F, int Hd, int Wd, const float* poses,
+                                         const float* Kf, const float* bmin, const float* bmax, float trunc,
+                                         const float* table, void* stream) {
+    SFMHIP_REQUIRE(table, "sfmhip_tsdf_integrate_tab: null pointer");
+    return tsdf_run(T, Wt, D, H, W, z0, z1, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, nullptr,
+                    reinterpret_cast<const float2*>(table));
+}
+
+extern "C" int sfmhip_tsdf_block_table(const float* depth, int F, int Hd, int Wd, int f0, int f1, float* table,
+                                       void* stream) {
+    SFMHIP_REQUIRE(depth && table, "sfmhip_tsdf_block_table: null pointer");
+    SFMHIP_REQUIRE(F >= 0 && Hd > 0 && Wd > 0 && 0 <= f0 && f0 <= f1 && f1 <= F,
+                   "sfmhip_tsdf_block_table: bad shape or frame range");
+    if (f0 == f1) return SFMHIP_OK;
+    SFMHIP_REQUIRE((int64_t)Hd * Wd * 4 < (int64_t)INT_MAX, "sfmhip_tsdf_block_table: depth map too large");
+    const int nbu = ceil_div(Wd, kCullBlock), nbv = ceil_div(Hd, kCullBlock), nf = f1 - f0;
+    hipStream_t st = as_stream(stream);
+    int4* rg = nullptr;
+    if (hipMallocAsync((void**)&rg, (size_t)nf * sizeof(int4), st) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("sfmhip_tsdf_block_table: scratch allocation failed");
+        return SFMHIP_E_HIP;
+    }
+    hipLaunchKernelGGL(full_range_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, nf, nbu, nbv, rg);
+    const float* dp = depth + (size_t)f0 * Hd * Wd;
+    float2* tp = reinterpret_cast<float2*>(table) + (size_t)f0 * nbv * nbu;
+    if (Wd % 4 == 0)
+        hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st, dp, nf,
+                           Hd, Wd, nbu, nbv, rg, tp);
+    else
+        hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st, dp, nf,
+                           Hd, Wd, nbu, nbv, rg, tp);
+    const int rc = check_launch("depth_blockmax_kernel");
+    (void)hipFreeAsync(rg, st);
+    return rc;
 }
 
 extern "C" int sfmhip_tsdf_cull_stats(int D, int H, int W, int z0, int z1, const float* depth, int F, int Hd,
@@ -1365,7 +1416,8 @@ extern "C" int sfmhip_tsdf_cull_stats(int D, int H, int W, int z0, int z1, const
     SFMHIP_REQUIRE(stats, "sfmhip_tsdf_cull_stats: null pointer");
     stats[0] = stats[1] = stats[2] = 0;
     float dummy = 0.f;   // the grids are not touched
-    return tsdf_run(&dummy, &dummy, D, H, W, z0, z1, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, stats);
+    return tsdf_run(&dummy, &dummy, D, H, W, z0, z1, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, stats,
+                    nullptr);
 }
 
 extern "C" int sfmhip_grid_from_voxel_major(const float* grid_vm, int C, int D, int H, int W, float* grid,

@@ -3,7 +3,11 @@
 * matching: image pairs are independent -> contiguous balanced pair ranges per
   rank, descriptors replicated, then ONE all-gather of the fixed-size
   ``matches0`` block so every rank holds the full match graph.
-* TSDF: z-slabs [z0, z1) per rank; no exchange during fusion.
+* TSDF: z-slabs [z0, z1) per rank; no exchange during fusion.  The fusion's
+  pre-pass table ({min, max} of every 16x16 depth block, ~20 MB for C5) does
+  not shrink with the slab (an orbiting camera sees most of any slab), so each
+  rank computes the table of 1/N of the frames and one all-gather assembles it
+  (:func:`shared_block_table`) instead of every rank reading every depth map.
 """
 from __future__ import annotations
 
@@ -112,3 +116,18 @@ def overlapped_allgather(compute, n: int, row_shape, dtype, device, chunks: int 
         w.wait()            # the current stream waits for every chunk's collective
     del sends
     return out[:n]
+
+
+def shared_block_table(depth: torch.Tensor, group=None, compute=None) -> torch.Tensor:
+    """The (F, ceil(Hd/16), ceil(Wd/16), 2) TSDF block table assembled across
+    ranks: rank r computes the rows of its frame range (:func:`shard_range`)
+    and one all-gather gives every rank the full table (bit-identical to a
+    single-process table; pass it to ``tsdf_integrate(block_table=...)``).
+    ``compute(depth_rows) -> table_rows`` defaults to the GPU kernel."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = shard_range(depth.shape[0], rank, world)
+    if compute is None:
+        from .voxel import tsdf_block_table
+        compute = tsdf_block_table
+    return allgather_rows(compute(depth[lo:hi]), depth.shape[0], group)

@@ -160,11 +160,15 @@ class VoxelGrid:
 
 
 def tsdf_integrate(T: torch.Tensor, Wt: torch.Tensor, depth: torch.Tensor, poses: torch.Tensor,
-                   K: torch.Tensor, bmin, bmax, trunc: float, z0: int = 0, z1: int | None = None) -> None:
+                   K: torch.Tensor, bmin, bmax, trunc: float, z0: int = 0, z1: int | None = None,
+                   block_table: torch.Tensor | None = None) -> None:
     """In-place TSDF update of z-slices [z0, z1) of T/Wt (D,H,W) from F depth maps.
 
     depth (F,Hd,Wd) f32 (<=0 invalid), poses (F,3,4) world->camera f32,
-    K (F,4) [fx, fy, cx, cy] f32, bounds in world units, trunc = mu."""
+    K (F,4) [fx, fy, cx, cy] f32, bounds in world units, trunc = mu.
+    block_table: optional (F, ceil(Hd/16), ceil(Wd/16), 2) f32 device table from
+    tsdf_block_table (e.g. assembled across ranks by dist.shared_block_table);
+    the result is bit-identical, the call's own pass over the depth maps skipped."""
     require_gpu()
     if T.dtype != torch.float32 or Wt.dtype != torch.float32 or not T.is_contiguous() or not Wt.is_contiguous():
         raise ValueError("T and Wt must be contiguous float32 device tensors")
@@ -175,8 +179,35 @@ def tsdf_integrate(T: torch.Tensor, Wt: torch.Tensor, depth: torch.Tensor, poses
     kk = dev(K, torch.float32)
     F, Hd, Wd = dp.shape
     bmn, bmx = _f3(bmin), _f3(bmax)
-    call("sfmhip_tsdf_integrate", ptr(T), ptr(Wt), D, H, W, int(z0), z1, ptr(dp), F, Hd, Wd, ptr(ps), ptr(kk),
-         _host_ptr(bmn), _host_ptr(bmx), float(trunc), stream_ptr())
+    if block_table is None:
+        call("sfmhip_tsdf_integrate", ptr(T), ptr(Wt), D, H, W, int(z0), z1, ptr(dp), F, Hd, Wd, ptr(ps), ptr(kk),
+             _host_ptr(bmn), _host_ptr(bmx), float(trunc), stream_ptr())
+        return
+    if tuple(block_table.shape) != block_table_shape(F, Hd, Wd) or block_table.dtype != torch.float32 or \
+            not block_table.is_contiguous() or block_table.device != T.device:
+        raise ValueError(f"block_table must be a contiguous float32 {block_table_shape(F, Hd, Wd)} tensor on {T.device}")
+    call("sfmhip_tsdf_integrate_tab", ptr(T), ptr(Wt), D, H, W, int(z0), z1, ptr(dp), F, Hd, Wd, ptr(ps), ptr(kk),
+         _host_ptr(bmn), _host_ptr(bmx), float(trunc), ptr(block_table), stream_ptr())
+
+
+def block_table_shape(F: int, Hd: int, Wd: int) -> tuple:
+    return (int(F), -(-int(Hd) // 16), -(-int(Wd) // 16), 2)
+
+
+def tsdf_block_table(depth: torch.Tensor, f0: int = 0, f1: int | None = None,
+                     out: torch.Tensor | None = None) -> torch.Tensor:
+    """{min, max} of every 16x16 block of depth maps [f0, f1) (rows f0..f1 of `out`,
+    an (F, ceil(Hd/16), ceil(Wd/16), 2) f32 device table, allocated when None)."""
+    require_gpu()
+    dp = dev(depth, torch.float32)
+    F, Hd, Wd = dp.shape
+    f1 = F if f1 is None else int(f1)
+    if out is None:
+        out = torch.empty(block_table_shape(F, Hd, Wd), dtype=torch.float32, device=dp.device)
+    elif tuple(out.shape) != block_table_shape(F, Hd, Wd) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous float32 {block_table_shape(F, Hd, Wd)} tensor")
+    call("sfmhip_tsdf_block_table", ptr(dp), F, Hd, Wd, int(f0), f1, ptr(out), stream_ptr())
+    return out
 
 
 def tsdf_cull_stats(shape, depth: torch.Tensor, poses: torch.Tensor, K: torch.Tensor, bmin, bmax, trunc: float,

@@ -186,6 +186,23 @@ int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, int z0, int 
                           const float* bmin, const float* bmax, float trunc,
                           void* stream);
 
+/* The TSDF pre-pass table on its own, for sharing across ranks (multi-GPU
+ * z-slabs: each rank computes the table of a frame range and an all-gather
+ * assembles it, instead of every rank reading every depth map): {min, max}
+ * of every 16x16 depth block, table [F][ceil(Hd/16)][ceil(Wd/16)][2] f32
+ * (min poisoned by NaN, max ignoring NaN); rows [f0, f1) are written.      */
+int sfmhip_tsdf_block_table(const float* depth, int F, int Hd, int Wd,
+                            int f0, int f1, float* table, void* stream);
+
+/* sfmhip_tsdf_integrate with the caller's full block table (all F frames,
+ * whole image, as written by sfmhip_tsdf_block_table): bit-identical
+ * result, the call's own block pass skipped.                                 */
+int sfmhip_tsdf_integrate_tab(float* T, float* Wt, int D, int H, int W, int z0, int z1,
+                              const float* depth, int F, int Hd, int Wd,
+                              const float* poses, const float* Kf,
+                              const float* bmin, const float* bmax, float trunc,
+                              const float* table, void* stream);
+
 /* Diagnostics for the TSDF pre-passes (no reference counterpart): runs only
  * the culling / free-space tests of sfmhip_tsdf_integrate over the same
  * arguments and returns HOST int64 stats[3] = (wave sub-tile, frame) pairs

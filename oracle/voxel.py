@@ -8,6 +8,8 @@ float32 restatements with the reference's op order:
   sh_colour        sdf.py:361-369 / plenoxel.py:9-16
   composite        sdf.py:391-406 / plenoxel.py:71-93
   tsdf_integrate   build-defined, parity unpinned.
+  block_table      the TSDF pre-pass table (build-defined): {min, max} per 16x16
+                   depth block, min poisoned by NaN, max ignoring NaN.
 """
 from __future__ import annotations
 
@@ -213,6 +215,23 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
 
 
 # ---------------------------------------------------------------------------
+def block_table(depth) -> np.ndarray:
+    """(F,Hd,Wd) f32 -> (F, ceil(Hd/16), ceil(Wd/16), 2) f32 {min, max} of every
+    16x16 block (blocks clipped at the image edge): min is -inf when the block
+    holds a NaN, max ignores NaN (-inf when every pixel is NaN)."""
+    d = np.asarray(depth, F32)
+    F, Hd, Wd = d.shape
+    nbv, nbu = -(-Hd // 16), -(-Wd // 16)
+    out = np.empty((F, nbv, nbu, 2), F32)
+    for bv in range(nbv):
+        for bu in range(nbu):
+            b = d[:, bv * 16:(bv + 1) * 16, bu * 16:(bu + 1) * 16].reshape(F, -1)
+            nan = np.isnan(b)
+            out[:, bv, bu, 0] = np.where(nan.any(1), -np.inf, np.where(nan, np.inf, b).min(1))
+            out[:, bv, bu, 1] = np.where(nan, -np.inf, b).max(1)
+    return out
+
+
 def ray_aabb(rays_o, rays_d, bmin, bmax):
     """GradientBasedSampler.ray_aabb_intersection (sdf.py:154-165), f32, NaN-propagating."""
     o = np.asarray(rays_o, F32).reshape(-1, 3)

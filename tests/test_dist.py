@@ -117,3 +117,41 @@ def test_chunk_rows_partition():
         rows = sorted(r for rk in range(world) for (lo, hi) in sdist.chunk_rows(n, rk, world, chunks)
                       for r in range(lo, hi))
         assert rows == list(range(n))
+
+
+def _cpu_block_table(depth):
+    from oracle import voxel as ov
+    return torch.from_numpy(ov.block_table(depth.numpy()))
+
+
+def _worker_table(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        g = torch.Generator().manual_seed(0)
+        depth = torch.rand((7, 37, 50), generator=g) * 4 - 1
+        depth[2, 5, 7] = float("nan")
+        full = sdist.shared_block_table(depth, compute=_cpu_block_table)
+        q.put((rank, bool(torch.equal(full, _cpu_block_table(depth)))))
+    except Exception as e:
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shared_block_table_gloo(world):
+    """The TSDF block table assembled from per-rank frame ranges by one
+    all-gather equals the single-process table."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_table, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v is True for v in res.values()), res

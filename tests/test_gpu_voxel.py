@@ -193,6 +193,39 @@ def test_tsdf_free_space_near_trunc_bitexact(sfm, gpu, monkeypatch, trunc):
     np.testing.assert_array_equal(T.cpu().numpy(), Tr)
 
 
+@pytest.mark.parametrize("Wd", [96, 97])
+def test_tsdf_block_table_vs_oracle(sfm, gpu, Wd):
+    """The pre-pass table ({min, max} per 16x16 block, NaN rules) built in two
+    frame ranges equals the oracle; ragged last block row/column."""
+    rng = np.random.default_rng(9)
+    depth = (rng.random((5, 41, Wd), dtype=np.float32) * 4 - 1).astype(np.float32)
+    depth[1, 3, 4] = np.nan
+    depth[2, 32:, 80:] = np.nan      # a block of NaN only
+    depth[3, 0, 0] = np.inf
+    d = torch.from_numpy(depth).to(gpu)
+    tab = sfm.tsdf_block_table(d, 0, 2)
+    sfm.tsdf_block_table(d, 2, 5, out=tab)
+    np.testing.assert_array_equal(tab.cpu().numpy(), ov.block_table(depth))
+
+
+def test_tsdf_with_shared_table_bitexact(sfm, gpu):
+    """tsdf_integrate with a caller-supplied block table (what the z-slab ranks
+    share by all-gather) is bit-identical to the call's own pre-pass, per slab."""
+    depth, poses, K = syn.tsdf_scene(20, seed=4)
+    d = depth.to(gpu)
+    tab = sfm.tsdf_block_table(d, 0, 9)
+    sfm.tsdf_block_table(d, 9, 20, out=tab)
+    args = (d, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 79)
+    T1 = torch.zeros((80, 80, 80), dtype=torch.float32, device=gpu)
+    W1 = torch.zeros_like(T1)
+    sfm.tsdf_integrate(T1, W1, *args)
+    T2, W2 = torch.zeros_like(T1), torch.zeros_like(T1)
+    for z0, z1 in ((0, 10), (10, 47), (47, 80)):
+        sfm.tsdf_integrate(T2, W2, *args, z0=z0, z1=z1, block_table=tab)
+    assert torch.equal(T1, T2) and torch.equal(W1, W2)
+    assert (W1 > 0).float().mean() > 0.3
+
+
 def test_tsdf_zslab_split_equals_whole(sfm, gpu):
     R, depth, poses, K = _tsdf_case(R=40, F=6)
     args = (torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K), (-1, -1, -1), (1, 1, 1), 0.12)

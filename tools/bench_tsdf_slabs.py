@@ -16,21 +16,32 @@ depth, poses, K = syn.tsdf_scene(257, syn.IMG_H, syn.IMG_W, device=dev)
 R = 256
 T = torch.zeros((R, R, R), dtype=torch.float32, device=dev)
 W = torch.zeros_like(T)
+def timed(fn):
+    best = 1e9
+    for _ in range(3):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    return best
+
+
+args = (depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / (R - 1))
+full_tab = sfm.tsdf_block_table(depth)
 for n in [int(a) for a in sys.argv[1:]] or [8]:
-    for cull in ("0", "1", "2"):
-        os.environ["SFMHIP_TSDF_CULL"] = cull
+    for mode in ("0", "1", "tab"):
+        os.environ["SFMHIP_TSDF_CULL"] = "1" if mode == "tab" else mode
         ts = []
         for r in range(n):
             z0, z1 = sdist.shard_range(R, r, n)
-            best = 1e9
-            for _ in range(3):
-                torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / (R - 1), z0, z1)
-                e1.record()
-                torch.cuda.synchronize()
-                best = min(best, e0.elapsed_time(e1))
-            ts.append(best)
-        print(f"N={n} CULL={cull}: max {max(ts):.3f} ms  mean {np.mean(ts):.3f}  slabs {[round(t, 2) for t in ts]}",
-              flush=True)
+            if mode == "tab":   # rank r: table of its 1/n of the frames + fusion with the shared table
+                f0, f1 = sdist.shard_range(depth.shape[0], r, n)
+                t_tab = timed(lambda: sfm.tsdf_block_table(depth, f0, f1, out=full_tab))
+                ts.append(t_tab + timed(lambda: sfm.tsdf_integrate(T, W, *args, z0, z1, block_table=full_tab)))
+            else:
+                ts.append(timed(lambda: sfm.tsdf_integrate(T, W, *args, z0, z1)))
+        print(f"N={n} {'CULL=' + mode if mode != 'tab' else 'shared table (excl. all-gather)'}: max {max(ts):.3f} ms"
+              f"  mean {np.mean(ts):.3f}  slabs {[round(t, 2) for t in ts]}", flush=True)
