@@ -84,70 +84,98 @@ __global__ void residual_kernel(const double* __restrict__ cam, const double* __
     r[2 * i + 1] = pts2d[2 * i + 1] - v;
 }
 
+// Rotations of every pair for the FD Jacobian: Rt[pair][0] = R(rvec),
+// Rt[pair][1 + k] = R(rvec + h_k e_k) (scipy's step h_k), one thread each —
+// the sin/cos work is per pair, not per observation.
+__global__ void fd_rotations_kernel(const double* __restrict__ cam, int n_pairs, double* __restrict__ Rt) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 4 * n_pairs) return;
+    const double* c = cam + (size_t)(t >> 2) * 6;
+    double p[3] = {c[0], c[1], c[2]};
+    const int q = (t & 3) - 1;
+    if (q >= 0) p[q] = p[q] + fd_step(p[q]);
+    rodrigues(p, Rt + (size_t)t * 9);
+}
+
 // 2-point FD: for each of the 9 parameters touching observation i, perturb it
 // by h (scipy step), re-project, J = (f(x+h) - f0) / ((x+h) - x).  Groups of
 // structurally orthogonal columns are perturbed together by scipy, but only
 // one column of each group touches row i, so each value depends only on that
-// column's perturbation (DESIGN.md "FD Jacobian").
-__global__ void fdjac_kernel(const double* __restrict__ cam, const double* __restrict__ K,
-                             const double* __restrict__ X, const double* __restrict__ pts2d,
-                             const int32_t* __restrict__ pair_of_obs, int64_t n,
-                             const double* __restrict__ f0, double* __restrict__ r,
-                             double* __restrict__ jv) {
-    __shared__ double sR[4][9];
-    const bool shared_R = block_rotations(cam, pair_of_obs, n, 4, sR);
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int pr = pair_of_obs ? pair_of_obs[i] : 0;
-    const double* c = cam + (size_t)pr * 6;
-    const double* k = K + (size_t)pr * 9;
-    const double fx = k[0], fy = k[4], cx = k[2], cy = k[5];
-    const double obs_u = pts2d[2 * i], obs_v = pts2d[2 * i + 1];
-    double p[9] = {c[0], c[1], c[2], c[3], c[4], c[5], X[3 * i], X[3 * i + 1], X[3 * i + 2]};
-
-    double R0[9];
-    if (shared_R) {
+// column's perturbation (DESIGN.md "FD Jacobian").  Every projection is the
+// op sequence of `project`; a perturbed t_k only changes the last addition of
+// camera coordinate k, so those three re-use the base partial sums (the same
+// operations, hence the same values).  The 18 values per observation are staged
+// in LDS and written as one contiguous, coalesced block per workgroup.
+constexpr int kFdThreads = 256;
+__global__ __launch_bounds__(kFdThreads) void fdjac_kernel(const double* __restrict__ Rt,
+                                                           const double* __restrict__ cam,
+                                                           const double* __restrict__ K,
+                                                           const double* __restrict__ X,
+                                                           const double* __restrict__ pts2d,
+                                                           const int32_t* __restrict__ pair_of_obs, int64_t n,
+                                                           const double* __restrict__ f0, double* __restrict__ r,
+                                                           double* __restrict__ jv) {
+    __shared__ double sj[kFdThreads * 18];
+    const int64_t i0 = (int64_t)blockIdx.x * kFdThreads;
+    const int64_t i = i0 + threadIdx.x;
+    if (i < n) {
+        const int pr = pair_of_obs ? pair_of_obs[i] : 0;
+        const double* c = cam + (size_t)pr * 6;
+        const double* k = K + (size_t)pr * 9;
+        const double* R = Rt + (size_t)pr * 36;
+        const double fx = k[0], fy = k[4], cx = k[2], cy = k[5];
+        const double obs_u = pts2d[2 * i], obs_v = pts2d[2 * i + 1];
+        const double t[3] = {c[3], c[4], c[5]};
+        const double Xp[3] = {X[3 * i], X[3 * i + 1], X[3 * i + 2]};
+        // base projection, keeping the partial sums R X
+        const double sx = R[0] * Xp[0] + R[1] * Xp[1] + R[2] * Xp[2];
+        const double sy = R[3] * Xp[0] + R[4] * Xp[1] + R[5] * Xp[2];
+        const double sz = R[6] * Xp[0] + R[7] * Xp[1] + R[8] * Xp[2];
+        const double zb = sz + t[2];
+        const double izb = (zb != 0.0) ? 1.0 / zb : 1.0;
+        const double xb = (sx + t[0]) * izb, yb = (sy + t[1]) * izb;
+        const double base_u = obs_u - (xb * fx + cx), base_v = obs_v - (yb * fy + cy);
+        if (r) { r[2 * i] = base_u; r[2 * i + 1] = base_v; }
+        const double f0u = f0 ? f0[2 * i] : base_u;
+        const double f0v = f0 ? f0[2 * i + 1] : base_v;
+        double* row = sj + threadIdx.x * 18;
+        auto put = [&](int q, double u, double v, double dx) {
+            row[q] = ((obs_u - u) - f0u) / dx;
+            row[9 + q] = ((obs_v - v) - f0v) / dx;
+        };
+        // rvec: the pair's perturbed rotations
 #pragma unroll
-        for (int e = 0; e < 9; ++e) R0[e] = sR[0][e];
-    } else {
-        rodrigues(p, R0);
-    }
-    double base_u, base_v;
-    {
-        double u, v;
-        project(R0, p + 3, p + 6, fx, fy, cx, cy, u, v);
-        base_u = obs_u - u;
-        base_v = obs_v - v;
-    }
-    if (r) { r[2 * i] = base_u; r[2 * i + 1] = base_v; }
-    const double f0u = f0 ? f0[2 * i] : base_u;
-    const double f0v = f0 ? f0[2 * i + 1] : base_v;
-
-    double* row0 = jv + (size_t)i * 18;
-    double* row1 = row0 + 9;
-#pragma unroll 1
-    for (int q = 0; q < 9; ++q) {
-        const double x0v = p[q];
-        const double hx = x0v + fd_step(x0v);
-        const double dx = hx - x0v;
-        p[q] = hx;
-        double u, v;
-        if (q < 3) {
-            double Rq[9];
-            if (shared_R) {
-#pragma unroll
-                for (int e = 0; e < 9; ++e) Rq[e] = sR[1 + q][e];
-            } else {
-                rodrigues(p, Rq);
-            }
-            project(Rq, p + 3, p + 6, fx, fy, cx, cy, u, v);
-        } else {
-            project(R0, p + 3, p + 6, fx, fy, cx, cy, u, v);
+        for (int q = 0; q < 3; ++q) {
+            const double hx = c[q] + fd_step(c[q]);
+            double u, v;
+            project(R + 9 * (q + 1), t, Xp, fx, fy, cx, cy, u, v);
+            put(q, u, v, hx - c[q]);
         }
-        p[q] = x0v;
-        row0[q] = ((obs_u - u) - f0u) / dx;
-        row1[q] = ((obs_v - v) - f0v) / dx;
+        // t: only the last addition of coordinate q changes
+        {
+            const double h0 = t[0] + fd_step(t[0]), h1 = t[1] + fd_step(t[1]), h2 = t[2] + fd_step(t[2]);
+            put(3, ((sx + h0) * izb) * fx + cx, yb * fy + cy, h0 - t[0]);
+            put(4, xb * fx + cx, ((sy + h1) * izb) * fy + cy, h1 - t[1]);
+            const double z2 = sz + h2;
+            const double iz2 = (z2 != 0.0) ? 1.0 / z2 : 1.0;
+            put(5, ((sx + t[0]) * iz2) * fx + cx, ((sy + t[1]) * iz2) * fy + cy, h2 - t[2]);
+        }
+        // X: full re-projection (the perturbed term sits inside the sums)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            double Xq[3] = {Xp[0], Xp[1], Xp[2]};
+            const double hx = Xp[q] + fd_step(Xp[q]);
+            Xq[q] = hx;
+            double u, v;
+            project(R, t, Xq, fx, fy, cx, cy, u, v);
+            put(6 + q, u, v, hx - Xp[q]);
+        }
     }
+    __syncthreads();
+    // coalesced write-out of the workgroup's rows [i0, min(n, i0 + 256)) x 18 doubles
+    const int64_t nv = (min(n, i0 + kFdThreads) - i0) * 18;
+    double* out = jv + i0 * 18;
+    for (int64_t e = threadIdx.x; e < nv; e += kFdThreads) out[e] = sj[e];
 }
 
 }  // namespace sfmhip
@@ -182,7 +210,17 @@ extern "C" int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, con
     SFMHIP_REQUIRE(cam && K && X && pts2d && jvals, "sfmhip_reproj_fd_jacobian: null pointer");
     SFMHIP_REQUIRE(n >= 0 && n_pairs >= 1, "sfmhip_reproj_fd_jacobian: bad counts");
     if (n == 0) return SFMHIP_OK;
-    hipLaunchKernelGGL(fdjac_kernel, dim3(ceil_div(n, 128)), dim3(128), 0, as_stream(stream), cam, K, X,
+    hipStream_t st = as_stream(stream);
+    double* Rt = nullptr;
+    if (hipMallocAsync((void**)&Rt, (size_t)n_pairs * 36 * sizeof(double), st) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("sfmhip_reproj_fd_jacobian: rotation table allocation failed");
+        return SFMHIP_E_HIP;
+    }
+    hipLaunchKernelGGL(fd_rotations_kernel, dim3(ceil_div(4 * n_pairs, 64)), dim3(64), 0, st, cam, n_pairs, Rt);
+    hipLaunchKernelGGL(fdjac_kernel, dim3(ceil_div(n, kFdThreads)), dim3(kFdThreads), 0, st, Rt, cam, K, X,
                        pts2d, pair_of_obs, n, f0, r, jvals);
-    return check_launch("fdjac_kernel");
+    const int rc = check_launch("fdjac_kernel");
+    (void)hipFreeAsync(Rt, st);
+    return rc;
 }

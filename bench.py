@@ -410,6 +410,50 @@ def pnp_line(sfm, syn, device, args, barrier, cpu=True):
     return line
 
 
+def ba_line(sfm, syn, device, args, barrier, cpu=True):
+    """DLT + residual + FD-Jacobian over BA_PAIRS pairs x BA_OBS observations
+    (pair ranges per rank)."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    sdist = importlib.import_module("3d_reconstruction_amd.dist")
+    s = syn.ba_scene(BA_PAIRS, BA_OBS, seed=4)
+    n = BA_PAIRS * BA_OBS
+    olo, ohi = sdist.shard_range(BA_PAIRS, rank, world)
+    sl = slice(olo * BA_OBS, ohi * BA_OBS)
+    tt = {k: torch.from_numpy(np.ascontiguousarray(v)).to(device) for k, v in s.items()}
+    x0l, x1l = tt["x0"][:, sl].contiguous(), tt["x1"][:, sl].contiguous()
+    Xl, p2l, pol = tt["X"][sl].contiguous(), tt["pts2d"][sl].contiguous(), tt["pair_of_obs"][sl].contiguous()
+    X4 = torch.empty((4, x0l.shape[1]), dtype=torch.float64, device=device)
+    rr = torch.empty((Xl.shape[0], 2), dtype=torch.float64, device=device)
+    jv = torch.empty((Xl.shape[0], 2, 9), dtype=torch.float64, device=device)
+
+    def ba_step(record):
+        e0 = e1 = None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        sfm.triangulate_batched(tt["P"], pol, x0l, x1l, out=X4)
+        sfm.residual_jacobian_batched(tt["cam"], tt["K"], Xl, p2l, pol, r=rr, jv=jv)
+        if record:
+            e1.record()
+        return (e0, e1)
+
+    wall_b, kms_b = timed(ba_step, args.steps, args.warmup, barrier)
+    wall_b = max_over_ranks(wall_b, world, device)
+    b_ms = wall_b / args.steps * 1e3
+    k_ms = max_over_ranks(float(np.mean(kms_b)), world, device)
+    local = (ohi - olo) * BA_OBS
+    gbs = local * (64 + 200) / (k_ms * 1e-3) / 1e9
+    return {
+        "metric": "BA obs/sec (DLT + residual + FD-Jacobian)", "value": n / (b_ms * 1e-3), "unit": "obs/s",
+        "ms_per_step": b_ms, "scaling": "strong",
+        "config": {"workload": f"{BA_PAIRS} pairs x {BA_OBS} obs, f64", "parallelism": f"pairs/{world}"},
+        "roofline": {"bound": "hbm", "kernel": "dlt_kernel+fdjac_kernel", "kernel_ms": k_ms,
+                     "algorithmic_bytes_per_obs": 64 + 200, "achieved_gbs": gbs, "peak_gbs": PEAK_HBM_GBS,
+                     "frac": gbs / PEAK_HBM_GBS},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -595,39 +639,7 @@ def main():
         torch.cuda.empty_cache()
 
         # ---------------- BA: DLT + residual + FD Jacobian ------------------
-        s = syn.ba_scene(BA_PAIRS, BA_OBS, seed=4)
-        n = BA_PAIRS * BA_OBS
-        olo, ohi = sdist.shard_range(BA_PAIRS, rank, world)
-        sl = slice(olo * BA_OBS, ohi * BA_OBS)
-        tt = {k: torch.from_numpy(np.ascontiguousarray(v)).to(device) for k, v in s.items()}
-        x0l, x1l = tt["x0"][:, sl].contiguous(), tt["x1"][:, sl].contiguous()
-        Xl, p2l, pol = tt["X"][sl].contiguous(), tt["pts2d"][sl].contiguous(), tt["pair_of_obs"][sl].contiguous()
-        X4 = torch.empty((4, x0l.shape[1]), dtype=torch.float64, device=device)
-        rr = torch.empty((Xl.shape[0], 2), dtype=torch.float64, device=device)
-        jv = torch.empty((Xl.shape[0], 2, 9), dtype=torch.float64, device=device)
-
-        def ba_step(record):
-            e0 = e1 = None
-            if record:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            sfm.triangulate_batched(tt["P"], pol, x0l, x1l, out=X4)
-            sfm.residual_jacobian_batched(tt["cam"], tt["K"], Xl, p2l, pol, r=rr, jv=jv)
-            if record:
-                e1.record()
-            return (e0, e1)
-
-        wall_b, kms_b = timed(ba_step, args.steps, args.warmup, barrier)
-        wall_b = max_over_ranks(wall_b, world, device)
-        b_ms = wall_b / args.steps * 1e3
-        result["secondary"].append({
-            "metric": "BA obs/sec (DLT + residual + FD-Jacobian)", "value": n / (b_ms * 1e-3), "unit": "obs/s",
-            "ms_per_step": b_ms, "scaling": "strong",
-            "config": {"workload": f"{BA_PAIRS} pairs x {BA_OBS} obs, f64", "parallelism": f"pairs/{world}"},
-            "roofline": {"bound": "hbm", "kernel": "dlt_kernel+fdjac_kernel",
-                         "kernel_ms": max_over_ranks(float(np.mean(kms_b)), world, device),
-                         "algorithmic_bytes_per_obs": 64 + 200},
-        })
+        result["secondary"].append(ba_line(sfm, syn, device, args, barrier))
 
     # ---------------- voxel anchors + vq (N=1 only; rays / obs are independent) --
     if not args.skip_secondary and world == 1:

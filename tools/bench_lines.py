@@ -15,6 +15,7 @@ syn = importlib.import_module("3d_reconstruction_amd.synthetic")
 ap = argparse.ArgumentParser()
 ap.add_argument("lines", nargs="+")
 ap.add_argument("--steps", type=int, default=5)
+ap.add_argument("--warmup", type=int, default=2)
 ap.add_argument("--cpu", action="store_true")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
