@@ -72,8 +72,9 @@ SIGNATURES = {
     "sfmhip_find_essential": [_p, _p, _p, _i32, _p, _f64, _f64, _i32, _p, _p, _p, _p, _p, _p, _p],
     "sfmhip_recover_pose": [_p, _i64, _p, _p, _p, _i32, _p, _p, _f64, _p, _p, _p, _p, _p],
     "sfmhip_pnp_ransac": [_p, _p, _p, _i32, _p, _i32, _f64, _f64, _p, _p, _p, _p, _p, _p, _p, _p],
-    "sfmhip_render_train": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _p, _i64, _i32, _p, _p, _p, _p],
+    "sfmhip_render_train": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _p, _i64, _i32, _p, _p, _p, _p, _p],
     "sfmhip_adam_step": [_p, _p, _p, _p, _i64, _f64, _f64, _f64, _f64, _i64, _i32, _p],
+    "sfmhip_adam_step_flagged": [_p, _p, _p, _p, _i64, _f64, _f64, _f64, _f64, _i64, _i32, _p, _i32, _p],
     "sfmhip_grid_from_voxel_major": [_p, _i32, _i32, _i32, _i32, _p, _p],
     "sfmhip_ray_aabb": [_p, _p, _i64, _p, _p, _p, _p, _p, _p],
     "sfmhip_stratified_samples": [_p, _p, _p, _i64, _i32, _i32, _p, _p],

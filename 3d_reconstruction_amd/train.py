@@ -46,6 +46,9 @@ class GridTrainer:
         self.grad = torch.zeros(shape, dtype=torch.float32, device=g.device)
         self.exp_avg = torch.zeros(shape, dtype=torch.float32, device=g.device)
         self.exp_avg_sq = torch.zeros(shape, dtype=torch.float32, device=g.device)
+        # 1 per voxel whose gradient line the scatter added to since the last zero_grad step:
+        # elsewhere grad is 0, so Adam neither reads nor re-zeroes it
+        self.touched = torch.zeros(shape[:3], dtype=torch.uint8, device=g.device)
 
     @classmethod
     def plenoxel(cls, voxel_grid, scale: float = 1.5, **kw) -> "GridTrainer":
@@ -80,15 +83,16 @@ class GridTrainer:
         sq = torch.empty(B, dtype=torch.float32, device=o.device)
         call("sfmhip_render_train", ptr(self.param), self.D, self.H, self.W, _host_ptr(self.bmin),
              _host_ptr(self.bmax), self.mask_mode, ptr(o), ptr(d), ptr(zz), ptr(t), B, S, ptr(rgb), ptr(sq),
-             ptr(self.grad), stream_ptr())
+             ptr(self.grad), ptr(self.touched), stream_ptr())
         loss = float(sq.double().sum().item()) / (3 * B) if B else float("nan")
         return loss, rgb
 
     def optimizer_step(self, zero_grad: bool = True) -> None:
         self.step_count += 1
-        call("sfmhip_adam_step", ptr(self.param), ptr(self.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
+        # only the voxels the scatter touched can have a non-zero gradient (flag per 32-float line)
+        call("sfmhip_adam_step_flagged", ptr(self.param), ptr(self.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
              self.param.numel(), self.lr, self.betas[0], self.betas[1], self.eps, self.step_count,
-             1 if zero_grad else 0, stream_ptr())
+             1 if zero_grad else 0, ptr(self.touched), 5, stream_ptr())
 
     def step(self, rays_o, rays_d, gt, z) -> float:
         """One training iteration; returns loss.item()."""

@@ -260,11 +260,12 @@ int sfmhip_pnp_ransac(const double* obj, const double* img, const int64_t* offse
  * Fused render forward + mse_loss(gt, rgb) gradient + analytic backward +
  * trilinear scatter-add into grad_vm (voxel-major (D,H,W,32), accumulated;
  * zero it via sfmhip_adam_step's zero_grad).  S <= 256.  Out: rgb [B][3],
- * sqerr [B] = sum_ch (rgb - gt)^2 (loss = sum(sqerr) / (3B)).               */
+ * sqerr [B] = sum_ch (rgb - gt)^2 (loss = sum(sqerr) / (3B)); touched
+ * [D*H*W] u8 (nullable): set to 1 for every voxel the scatter adds to.      */
 int sfmhip_render_train(const float* grid_vm, int D, int H, int W, const float* bmin, const float* bmax,
                         int mask_mode, const float* rays_o, const float* rays_d, const float* z,
                         const float* gt, int64_t B, int S, float* rgb, float* sqerr, float* grad_vm,
-                        void* stream);
+                        uint8_t* touched, void* stream);
 
 /* torch.optim.Adam single-tensor step (weight_decay 0, amsgrad off) over n
  * f32 parameters (n % 4 == 0), step = the step count after increment;
@@ -272,6 +273,15 @@ int sfmhip_render_train(const float* grid_vm, int D, int H, int W, const float* 
 int sfmhip_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                      double lr, double beta1, double beta2, double eps, int64_t step, int zero_grad,
                      void* stream);
+
+/* The same Adam step when the gradient is known to be 0 outside flagged
+ * runs: flags [ceil(n / 2^flag_shift)] u8, one per 2^flag_shift parameters
+ * (the trainer: one per 32-channel voxel line, set by sfmhip_render_train's
+ * `touched`); unflagged gradients are neither read nor re-zeroed, and with
+ * zero_grad the flags are cleared too.  Results equal sfmhip_adam_step's.     */
+int sfmhip_adam_step_flagged(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                             double lr, double beta1, double beta2, double eps, int64_t step, int zero_grad,
+                             uint8_t* flags, int flag_shift, void* stream);
 
 /* (D,H,W,32) voxel-major -> (C,D,H,W) reference layout (trainer export).     */
 int sfmhip_grid_from_voxel_major(const float* grid_vm, int C, int D, int H, int W, float* grid,

@@ -43,6 +43,36 @@ def test_adam_kernel_bitexact_vs_oracle(sfm, gpu):
         assert not gd.any()                                   # zero_grad fused
 
 
+def test_flagged_adam_bitexact_vs_oracle(sfm, gpu):
+    """Adam with a flag per 32-float line: gradients are zero outside flagged
+    lines (neither read nor re-zeroed there, the buffer holds junk to prove it);
+    results equal the plain step's, flags are cleared with zero_grad."""
+    import ctypes
+    rng = np.random.default_rng(1)
+    n = 32 * 1000 + 32
+    p = rng.standard_normal(n).astype(np.float32)
+    m = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    v = (rng.random(n) * 1e-5).astype(np.float32)
+    for step in (1, 3):
+        flags = (rng.random(n // 32) < 0.2).astype(np.uint8)
+        g = (rng.standard_normal(n) * 1e-2).astype(np.float32) * np.repeat(flags, 32)
+        gj = g.copy()
+        gj[np.repeat(flags, 32) == 0] = 7.0          # never read: the kernel must use 0
+        pd, gd, md, vd = (torch.tensor(a, device=gpu) for a in (p, gj, m, v))
+        fd = torch.tensor(flags, device=gpu)
+        rc = sfm.lib.sfmhip_adam_step_flagged(pd.data_ptr(), gd.data_ptr(), md.data_ptr(), vd.data_ptr(), n,
+                                              *(ctypes.c_double(x) for x in (1e-2, 0.9, 0.999, 1e-8)), step, 1,
+                                              fd.data_ptr(), 5, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        p, m, v = ot.adam_step(p, g, m, v, step)
+        assert np.array_equal(md.cpu().numpy(), m)
+        assert np.array_equal(vd.cpu().numpy(), v)
+        assert np.array_equal(pd.cpu().numpy(), p)
+        gz = gd.cpu().numpy()
+        assert not gz[np.repeat(flags, 32) == 1].any() and (gz[np.repeat(flags, 32) == 0] == 7.0).all()
+        assert not fd.any()
+
+
 def test_render_backward_matches_oracle(sfm, gpu):
     g = golden("train_golden.npz")
     tr = trainmod.GridTrainer.plenoxel(torch.tensor(g["grid0"]), 1.5)
@@ -88,6 +118,9 @@ def test_larger_grid_sdf_mode_gradient(sfm, gpu):
     gg = tr._export(tr.grad)[0].cpu().numpy()
     scale = np.abs(grado).max()
     assert np.abs(gg - grado).max() <= 1e-4 * scale
+    touched = tr.touched.cpu().numpy().astype(bool)
+    assert touched[np.abs(grado).max(0) > 0].all() and touched.mean() < 0.9   # every non-zero line flagged
     tr.optimizer_step()
+    assert not tr.touched.any() and not tr.grad.any()
     p1, _, _ = ot.adam_step(grid[0], gg, np.zeros_like(gg), np.zeros_like(gg), 1)
     assert np.array_equal(tr.grid[0].cpu().numpy(), p1)       # Adam on the same gradient: bit-exact
