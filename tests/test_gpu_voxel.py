@@ -226,6 +226,30 @@ def test_tsdf_with_shared_table_bitexact(sfm, gpu):
     assert (W1 > 0).float().mean() > 0.3
 
 
+def test_tsdf_c5_full_size_slabs_bitexact(sfm, gpu, monkeypatch):
+    """The bench workload itself (C5: 256^3 grid, 257 depth maps 1936x1296, every
+    pre-pass and fast path at its default): three 2-slice z-slabs of the fused
+    grid equal the oracle bit for bit, and culling off gives the same grid."""
+    depth, poses, K = syn.tsdf_scene(257, syn.IMG_H, syn.IMG_W, device=gpu)
+    R = 256
+    args = (depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / (R - 1))
+    T = torch.zeros((R, R, R), dtype=torch.float32, device=gpu)
+    W = torch.zeros_like(T)
+    sfm.tsdf_integrate(T, W, *args)
+    dc, pc, kc = depth.cpu().numpy(), poses.cpu().numpy(), K.cpu().numpy()
+    zeros = np.zeros((R, R, R), np.float32)
+    for z0 in (0, 127, 254):
+        Tr, Wr = ov.tsdf_integrate(zeros, zeros, dc, pc, kc, (-1.2,) * 3, (1.2,) * 3, np.float32(3 * 2.4 / (R - 1)),
+                                   z0, z0 + 2)
+        np.testing.assert_array_equal(W[z0:z0 + 2].cpu().numpy(), Wr[z0:z0 + 2])
+        np.testing.assert_array_equal(T[z0:z0 + 2].cpu().numpy(), Tr[z0:z0 + 2])
+    assert (W > 0).float().mean() > 0.5
+    T2, W2 = torch.zeros_like(T), torch.zeros_like(T)
+    monkeypatch.setenv("SFMHIP_TSDF_CULL", "0")
+    sfm.tsdf_integrate(T2, W2, *args)
+    assert torch.equal(T, T2) and torch.equal(W, W2)
+
+
 def test_tsdf_zslab_split_equals_whole(sfm, gpu):
     R, depth, poses, K = _tsdf_case(R=40, F=6)
     args = (torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K), (-1, -1, -1), (1, 1, 1), 0.12)
