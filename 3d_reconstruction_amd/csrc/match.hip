@@ -631,7 +631,7 @@ extern "C" int sfmhip_desc_prepare_shifted(const int8_t* desc, int n_img, int m_
     SFMHIP_REQUIRE(desc && n_kpts && desc_shifted && norms && keys, "sfmhip_desc_prepare_shifted: null pointer");
     SFMHIP_REQUIRE(n_img > 0 && m_pad > 0 && d > 0 && d % 16 == 0 && d <= 256,
                    "sfmhip_desc_prepare_shifted: bad shape");
-    SFMHIP_REQUIRE(shift >= 0 && shift <= 64, "sfmhip_desc_prepare_shifted: shift must be in [0, 64]");
+    SFMHIP_REQUIRE(shift >= 0 && shift <= 127, "sfmhip_desc_prepare_shifted: shift must be in [0, 127]");
     const int rows = n_img * m_pad;
     hipLaunchKernelGGL(prepare_shifted_kernel, dim3(ceil_div(rows, 256)), dim3(256), 0, as_stream(stream), desc,
                        rows, m_pad, d, n_kpts, shift, desc_shifted, norms, keys);

@@ -31,7 +31,7 @@ from ._abi import call, dev, ptr, require_gpu, stream_ptr
 MODE_SIFT = 0    # integer-valued 0..255 descriptors (SIFT): q = x - 128
 MODE_FLOAT = 1   # float descriptors (SuperPoint / DISK, L2-normalised): q = rint(127 x)
 _JB = 128        # m_pad granularity required by the kernel
-_SHIFT = 64      # operand shift of the matcher (sfmhip_desc_prepare_shifted)
+_SHIFTS = (48, 64)   # operand shifts of the matcher, in order of preference (sfmhip_desc_prepare_shifted)
 
 
 def _ratio(ratio) -> tuple[int, int]:
@@ -67,12 +67,20 @@ class DescriptorBank:
         self.n_img, self.m_pad, self.d = int(n_img), int(m_pad), int(d)
         self.norms = torch.empty((n_img, m_pad), dtype=torch.int32, device=q.device)
         self.keys = torch.empty((n_img, m_pad), dtype=torch.int32, device=q.device)
-        # Matcher operands: q itself, or (default, when every value fits) q + 64 with
-        # adjusted norms/keys -- identical results, non-negative MFMA operands run the
-        # int8 array at a higher clock (SFMHIP_MATCH_SHIFT=0 disables).
+        # Matcher operands: q itself, or (default, when every value fits) q + c with
+        # adjusted norms/keys -- identical results; non-negative operands in a narrow
+        # bit band run the int8 array at a higher clock.  c = 48 puts
+        # zero-mean descriptors in [32, 64) (bit 5 set, bit 6 clear: only the low bits
+        # toggle; measured 105.3 vs 109.9 ms for c = 64 and 115 ms unshifted on C3);
+        # c = 64 when the values reach below -48.  SFMHIP_MATCH_SHIFT: 0 off, 1 auto,
+        # >= 2 that shift (A/B runs).
         self.qm = self.q
-        shift = _SHIFT if os.environ.get("SFMHIP_MATCH_SHIFT", "1") != "0" else 0
-        if shift and self.q.numel() and int(self.q.min()) >= -shift and int(self.q.max()) <= 127 - shift:
+        env = int(os.environ.get("SFMHIP_MATCH_SHIFT", "1"))
+        qmin, qmax = (int(self.q.min()), int(self.q.max())) if self.q.numel() else (0, 0)
+        cands = () if env == 0 else (_SHIFTS if env == 1 else (env,))
+        shift = next((c for c in cands if qmin >= -c and qmax <= 127 - c), 0)
+        self.shift = shift
+        if shift:
             self.qm = torch.empty_like(self.q)
             call("sfmhip_desc_prepare_shifted", ptr(self.q), self.n_img, self.m_pad, self.d, ptr(self.n_kpts),
                  shift, ptr(self.qm), ptr(self.norms), ptr(self.keys), stream_ptr())

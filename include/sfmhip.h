@@ -59,8 +59,9 @@ int sfmhip_desc_prepare(const int8_t* desc, int n_img, int m_pad, int d,
 /* Same as sfmhip_desc_prepare, plus a shifted operand copy for the matcher:
  * desc_shifted = q + shift on valid rows (0 on padding rows), norms and keys
  * adjusted so that sfmhip_match_pairs on (desc_shifted, norms, keys) returns
- * exactly the matches and distances of the unshifted q.  Caller guarantees
- * q + shift <= 127 for every valid element (shift 64: |q| <= 63 or q = -64).
+ * exactly the matches and distances of the unshifted q.  shift in [0, 127];
+ * caller guarantees q + shift <= 127 for every valid element (shift 64:
+ * q <= 63).
  * Speed only (lower MFMA switching power).                      */
 int sfmhip_desc_prepare_shifted(const int8_t* desc, int n_img, int m_pad, int d,
                                 const int32_t* n_kpts, int shift, int8_t* desc_shifted,

@@ -57,11 +57,12 @@ def test_match_ragged_pairs_bitexact(sfm, gpu, d, mode):
             assert np.array_equal(g2[p, :nk[a]], rd2[p, :nk[a]])
 
 
-@pytest.mark.parametrize("lo,hi", [(-64, 63), (-40, 40), (-65, 63), (-64, 64)])
+@pytest.mark.parametrize("lo,hi", [(-64, 63), (-40, 40), (-48, 79), (-49, 63), (-65, 63), (-64, 64)])
 def test_match_shifted_operands_identical(sfm, gpu, monkeypatch, lo, hi):
-    """The +64 operand shift (default when every value fits: [-64, 63]) returns the
-    oracle's matches and distances; values outside fall back to the plain operands.
-    Integer data with many duplicate rows (ties) and the range extremes present."""
+    """The operand shift (default: +48 when every value fits [-48, 79], else +64
+    when it fits [-64, 63], else none) returns the oracle's matches and
+    distances with every shift; integer data with many duplicate rows (ties)
+    and the range extremes present."""
     rng = np.random.default_rng(1000 + lo * 7 + hi)
     n_img, m, d = 4, 300, 256
     base = rng.integers(lo, hi + 1, (120, d)).astype(np.float32)
@@ -73,10 +74,12 @@ def test_match_shifted_operands_identical(sfm, gpu, monkeypatch, lo, hi):
         x[i, nk[i]:] = 0
     pairs = np.array([[0, 1], [1, 0], [2, 3], [3, 2], [0, 3]], np.int32)
     out = []
-    for shift in ("1", "0"):
+    auto = 48 if lo >= -48 and hi <= 79 else (64 if lo >= -64 and hi <= 63 else 0)
+    for shift, exp in (("1", auto), ("0", 0), ("48", 48 if lo >= -48 and hi <= 79 else 0),
+                       ("64", 64 if lo >= -64 and hi <= 63 else 0)):
         monkeypatch.setenv("SFMHIP_MATCH_SHIFT", shift)
         bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=1)
-        assert (bank.qm is not bank.q) == (shift == "1" and lo >= -64 and hi <= 63)
+        assert bank.shift == exp and (bank.qm is not bank.q) == (exp != 0)
         out.append([t.cpu().numpy() for t in bank.match(pairs, ratio=0.8, with_dist=True)])
     q = om.quantize(x, 1)
     ref, rd1, rd2 = _oracle_pairs(q, nk, pairs, (4, 5))
