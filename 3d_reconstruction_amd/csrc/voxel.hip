@@ -516,11 +516,16 @@ __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __rest
     if (VEC) {
         const int u = (blockIdx.x * 256 + threadIdx.x) * 4;
         if (u < Wd) {
+            typedef float f4v __attribute__((ext_vector_type(4)));
             float4 q[kCullBlock];
 #pragma unroll
-            for (int r = 0; r < kCullBlock; ++r)
-                q[r] = r < nr ? *reinterpret_cast<const float4*>(dp + (size_t)(r0 + r) * Wd + u)
-                              : make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff());
+            for (int r = 0; r < kCullBlock; ++r) {   // streamed once here: non-temporal
+                q[r] = make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff());
+                if (r < nr) {
+                    const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(dp + (size_t)(r0 + r) * Wd + u));
+                    q[r] = make_float4(t.x, t.y, t.z, t.w);
+                }
+            }
 #pragma unroll
             for (int r = 0; r < kCullBlock; ++r) m = fmaxf(m, fmaxf(fmaxf(q[r].x, q[r].y), fmaxf(q[r].z, q[r].w)));
 #pragma unroll
