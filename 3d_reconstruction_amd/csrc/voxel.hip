@@ -558,12 +558,64 @@ __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __rest
 }
 
 constexpr int kCullSub = 4;   // waves per workgroup tile
-// One workgroup per (4x4x4 brick of sub-tiles, 16 frames): wave j tests frame
-// 16 h + j for the brick's 64 sub-tiles (one per lane), so the camera loads are
-// scalar and the block-table reads of neighbouring footprints share cache
-// lines; the 16 bits of each sub-tile are packed through LDS and stored as the
-// low or high half of its mask word.  Masks are [sub-tile slot][nw] words, bit j
-// of word w = frame 32 w + j.
+
+// The (box, frame) test: skip = provably no voxel of the box updates; fre = every
+// voxel of the box updates with tsdf = 1 (free space).
+__device__ __forceinline__ void cull_test(const float* __restrict__ poses, const float* __restrict__ Kf, int f,
+                                          const Bounds& B, int D, int H, int W, int xa, int xb, int ya, int yb,
+                                          int za, int zb, int Hd, int Wd, float trunc,
+                                          const float2* __restrict__ bmm, int use_free, int nbu, int nbv,
+                                          const int4* __restrict__ range, bool& skip, bool& fre) {
+    skip = fre = false;
+    int u0, u1, v0, v1;
+    double zlo, zhi;
+    bool inside = false;
+    const int st = ya <= yb ? box_footprint(poses + f * 12, Kf + f * 4, B, D, H, W, xa, xb, ya, yb, za, zb, Hd, Wd,
+                                            u0, u1, v0, v1, zlo, zhi, inside)
+                            : 0;
+    if (st == 1) {
+        skip = true;
+    } else if (st == 2) {
+        const int bu0 = u0 / kCullBlock, bu1 = u1 / kCullBlock, bv0 = v0 / kCullBlock, bv1 = v1 / kCullBlock;
+        const int4 rg = range[f];   // only blocks inside the slab's range were computed
+        const int nu = bu1 - bu0 + 1, nb = nu * (bv1 - bv0 + 1);
+        if (nb <= kCullMaxBlocks && bu0 >= rg.x && bu1 <= rg.y && bv0 >= rg.z && bv1 <= rg.w) {
+            const float2* bp = bmm + ((size_t)f * nbv + bv0) * nbu + bu0;
+            float m = -__builtin_inff(), mn = __builtin_inff();
+            for (int bv = bv0; bv <= bv1; ++bv, bp += nbu) {
+                int i = 0;
+                for (; i + 4 <= nu; i += 4) {   // 4 independent loads in flight
+                    const float2 e0 = bp[i], e1 = bp[i + 1], e2 = bp[i + 2], e3 = bp[i + 3];
+                    m = fmaxf(fmaxf(m, fmaxf(e0.y, e1.y)), fmaxf(e2.y, e3.y));
+                    mn = fminf(fminf(mn, fminf(e0.x, e1.x)), fminf(e2.x, e3.x));
+                }
+                for (; i < nu; ++i) {
+                    m = fmaxf(m, bp[i].y);
+                    mn = fminf(mn, bp[i].x);   // never NaN (poisoned to -inf)
+                }
+            }
+            // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for the
+            // rounding of (depth - Zc), so the kernel's !(sdf < -trunc) test fails everywhere
+            skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * 0x1p-24) + 1e-30 < zlo);
+            if (!skip && use_free && inside && zlo >= 0x1p-59 && zhi <= 0x1p59) {
+                bool good = true;
+#pragma unroll
+                for (int q = 0; q < 12; ++q) good = good && fabsf(poses[f * 12 + q]) < 0x1p60f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) good = good && fabsf(Kf[f * 4 + q]) < 0x1p60f;
+                fre = good && (double)mn - zhi >= (double)trunc * (1 + 0x1p-20);
+            }
+        }
+    }
+}
+
+// One workgroup per (4x4x4 brick of tiles or sub-tiles, 16 frames): wave j tests
+// frame 16 h + j for the brick's 64 boxes (one per lane), so the camera loads are
+// scalar and the block-table reads of neighbouring footprints share cache lines;
+// the 16 bits of each box are packed through LDS and stored as the low or high
+// half of its mask word.  Masks are [wave slot][nw] words, bit j of word w =
+// frame 32 w + j.  With `plist` (per_tile = 1), every (tile, frame) that is
+// neither culled nor free space is appended to a list for tsdf_refine_kernel.
 constexpr int kCullFrames = 16;
 __global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, int z0, int z1, int F, int Hd, int Wd,
                                                          const float* __restrict__ poses, const float* __restrict__ Kf,
@@ -571,12 +623,13 @@ __global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, in
                                                          int use_free, int nbu, int nbv,
                                                          const int4* __restrict__ range, int per_tile, int nw,
                                                          unsigned short* __restrict__ cull,
-                                                         unsigned short* __restrict__ freem) {
+                                                         unsigned short* __restrict__ freem,
+                                                         unsigned* __restrict__ plist, unsigned* __restrict__ pcount) {
     __shared__ unsigned char bits[kCullFrames][64];
     const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
     const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
     const int nsy = nty * per_tile;                        // sub-tile rows in y
-    const int nqx = (ntx + 3) >> 2, nqy = (nsy + 3) >> 2;  // 4x4x4 bricks of sub-tiles
+    const int nqx = (ntx + 3) >> 2, nqy = (nsy + 3) >> 2;  // 4x4x4 bricks of boxes
     const int nh = 2 * nw;                                 // 16-frame halves per launch
     const int hf = blockIdx.x % nh, brick = blockIdx.x / nh;
     const int l = threadIdx.x & 63, j = threadIdx.x >> 6;
@@ -586,54 +639,37 @@ __global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, in
     const int tz = (brick / (nqx * nqy)) * 4 + (l >> 4);
     const bool tile_ok = tx < ntx && sy < nsy && tz < ntz;
     const int ty = sy / per_tile, w = sy % per_tile;
+    const int64_t tile = ((int64_t)tz * nty + ty) * ntx + tx;
     bool skip = false, fre = false;
     if (tile_ok && f < F) {
         const int xa = tx * kTsdfTX, xb = min(W, xa + kTsdfTX) - 1;
         const int ya = ty * kTsdfTY + (kTsdfTY / per_tile) * w, yb = min(H, ya + kTsdfTY / per_tile) - 1;
         const int za = z0 + tz * kTsdfTZ, zb = min(z1, za + kTsdfTZ) - 1;
-        int u0, u1, v0, v1;
-        double zlo, zhi;
-        bool inside = false;
-        const int st = ya <= yb ? box_footprint(poses + f * 12, Kf + f * 4, B, D, H, W, xa, xb, ya, yb, za, zb, Hd, Wd,
-                                                u0, u1, v0, v1, zlo, zhi, inside)
-                                : 0;
-        if (st == 1) {
-            skip = true;
-        } else if (st == 2) {
-            const int bu0 = u0 / kCullBlock, bu1 = u1 / kCullBlock, bv0 = v0 / kCullBlock, bv1 = v1 / kCullBlock;
-            const int4 rg = range[f];   // only blocks inside the slab's range were computed
-            const int nu = bu1 - bu0 + 1, nb = nu * (bv1 - bv0 + 1);
-            if (nb <= kCullMaxBlocks && bu0 >= rg.x && bu1 <= rg.y && bv0 >= rg.z && bv1 <= rg.w) {
-                const float2* bp = bmm + ((size_t)f * nbv + bv0) * nbu + bu0;
-                float m = -__builtin_inff(), mn = __builtin_inff();
-                for (int bv = bv0; bv <= bv1; ++bv, bp += nbu) {
-                    int i = 0;
-                    for (; i + 4 <= nu; i += 4) {   // 4 independent loads in flight
-                        const float2 e0 = bp[i], e1 = bp[i + 1], e2 = bp[i + 2], e3 = bp[i + 3];
-                        m = fmaxf(fmaxf(m, fmaxf(e0.y, e1.y)), fmaxf(e2.y, e3.y));
-                        mn = fminf(fminf(mn, fminf(e0.x, e1.x)), fminf(e2.x, e3.x));
-                    }
-                    for (; i < nu; ++i) {
-                        m = fmaxf(m, bp[i].y);
-                        mn = fminf(mn, bp[i].x);   // never NaN (poisoned to -inf)
-                    }
-                }
-                // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for the
-                // rounding of (depth - Zc), so the kernel's !(sdf < -trunc) test fails everywhere
-                skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * 0x1p-24) + 1e-30 < zlo);
-                if (!skip && use_free && inside && zlo >= 0x1p-59 && zhi <= 0x1p59) {
-                    bool good = true;
-#pragma unroll
-                    for (int q = 0; q < 12; ++q) good = good && fabsf(poses[f * 12 + q]) < 0x1p60f;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) good = good && fabsf(Kf[f * 4 + q]) < 0x1p60f;
-                    fre = good && (double)mn - zhi >= (double)trunc * (1 + 0x1p-20);
-                }
-            }
-        }
+        cull_test(poses, Kf, f, B, D, H, W, xa, xb, ya, yb, za, zb, Hd, Wd, trunc, bmm, use_free, nbu, nbv, range,
+                  skip, fre);
     }
+    // compact list of the projected (tile, frame) pairs: one atomic per workgroup
+    __shared__ unsigned wcnt[kCullFrames + 1];
+    const bool proj = plist && tile_ok && f < F && !skip && !fre;
+    const unsigned long long bal = __ballot(proj);
+    if (l == 0) wcnt[j] = (unsigned)__popcll(bal);
     bits[j][l] = (unsigned char)(skip | (fre << 1));
     __syncthreads();
+    if (plist) {
+        if (threadIdx.x == 0) {
+            unsigned tot = 0u;
+            for (int q = 0; q < kCullFrames; ++q) {
+                const unsigned c = wcnt[q];
+                wcnt[q] = tot;
+                tot += c;
+            }
+            wcnt[kCullFrames] = tot ? atomicAdd(pcount, tot) : 0u;
+        }
+        __syncthreads();
+        if (proj)
+            plist[wcnt[kCullFrames] + wcnt[j] + __popcll(bal & ((1ull << l) - 1ull))] =
+                ((unsigned)tile << 9) | (unsigned)f;
+    }
     if (j == 0 && tile_ok) {
         unsigned cw = 0u, fw = 0u;
 #pragma unroll
@@ -642,13 +678,44 @@ __global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, in
             cw |= (b & 1u) << q;
             fw |= (b >> 1) << q;
         }
-        const int64_t tile = ((int64_t)tz * nty + ty) * ntx + tx;
         const int q0 = per_tile == kCullSub ? w : 0, q1 = per_tile == kCullSub ? w + 1 : kCullSub;
         for (int q = q0; q < q1; ++q) {
             const int64_t h = ((tile * kCullSub + q) * nw) * 2 + hf;   // half hf of word hf / 2
             cull[h] = (unsigned short)cw;
             if (freem) freem[h] = (unsigned short)fw;
         }
+    }
+}
+
+// Second, finer pass over the projected (tile, frame) pairs only: one lane per
+// (pair, wave sub-tile of 8x2x8 voxels); a sub-tile proven culled or free space
+// gets its bit set in its own wave slot's mask (the tile-level bits of a
+// projected pair are 0, so OR-ing refines them).  Grid-stride over the device-side
+// count, so the host never waits for it.
+__global__ __launch_bounds__(256) void tsdf_refine_kernel(int D, int H, int W, int z0, int z1, int F, int Hd,
+                                                          int Wd, const float* __restrict__ poses,
+                                                          const float* __restrict__ Kf, Bounds B, float trunc,
+                                                          const float2* __restrict__ bmm, int use_free, int nbu,
+                                                          int nbv, const int4* __restrict__ range, int nw,
+                                                          unsigned* __restrict__ cull, unsigned* __restrict__ freem,
+                                                          const unsigned* __restrict__ plist,
+                                                          const unsigned* __restrict__ pcount) {
+    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
+    const int64_t n = (int64_t)(*pcount) * kCullSub;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned e = plist[g >> 2];
+        const int q = (int)(g & 3), f = (int)(e & 511u);
+        const int64_t tile = e >> 9;
+        const int tx = (int)(tile % ntx), ty = (int)((tile / ntx) % nty), tz = (int)(tile / ((int64_t)ntx * nty));
+        const int xa = tx * kTsdfTX, xb = min(W, xa + kTsdfTX) - 1;
+        const int ya = ty * kTsdfTY + (kTsdfTY / kCullSub) * q, yb = min(H, ya + kTsdfTY / kCullSub) - 1;
+        const int za = z0 + tz * kTsdfTZ, zb = min(z1, za + kTsdfTZ) - 1;
+        bool skip, fre;
+        cull_test(poses, Kf, f, B, D, H, W, xa, xb, ya, yb, za, zb, Hd, Wd, trunc, bmm, use_free, nbu, nbv, range,
+                  skip, fre);
+        const int64_t word = (tile * kCullSub + q) * nw + (f >> 5);
+        if (skip) atomicOr(cull + word, 1u << (f & 31));
+        else if (fre && freem) atomicOr(freem + word, 1u << (f & 31));
     }
 }
 
@@ -1301,6 +1368,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const int nbu = ceil_div(Wd, kCullBlock), nbv = ceil_div(Hd, kCullBlock);
     const int64_t nsub = (int64_t)nbx * nby * nbz * kCullSub;
     const int per_tile = env_int("SFMHIP_TSDF_CULLSUB", 1) == 4 ? kCullSub : 1;
+    // SFMHIP_TSDF_REFINE=0: no per-wave second pass over the projected tile-frames (A/B runs)
+    const bool want_refine = per_tile == 1 && env_int("SFMHIP_TSDF_REFINE", 1) != 0;
     // cull pass: one workgroup per (4x4x4 brick of sub-tiles, 16 frames)
     const int64_t cull_bricks = (int64_t)ceil_div(nbx, 4) * ceil_div(nby * per_tile, 4) * ceil_div(nbz, 4);
     SFMHIP_REQUIRE(cull_bricks * ceil_div(std::min(chunk, F), 16) < INT_MAX, "sfmhip_tsdf_integrate: grid too large");
@@ -1319,7 +1388,9 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     float2* cbmm = nullptr;
     unsigned* cfree = nullptr;
     unsigned* cmask = nullptr;
+    unsigned* plist = nullptr;   // projected (tile, frame) list + its count (last element)
     int4* crange = nullptr;
+    const int64_t ntile_frames = (int64_t)nbx * nby * nbz * std::min(chunk, F);
     if (want_cull) {
         if (ext_table) cbmm = const_cast<float2*>(ext_table);
         else if (hipMallocAsync((void**)&cbmm, nblk * sizeof(float2), st) != hipSuccess) cbmm = nullptr;
@@ -1333,6 +1404,9 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         }
         if (cmask && want_free && hipMallocAsync((void**)&cfree, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess)
             cfree = nullptr;   // free-space path off, culling unchanged
+        if (cmask && want_refine && ntile_frames < (int64_t)1 << 30 && nbx * nby * nbz < (1 << 23) &&
+            hipMallocAsync((void**)&plist, (size_t)(ntile_frames + 1) * sizeof(unsigned), st) != hipSuccess)
+            plist = nullptr;   // no second pass
         (void)hipGetLastError();
     }
     // per-voxel block test in the fusion kernel (with the free-space path; SFMHIP_TSDF_VOXTEST=0 off)
@@ -1359,10 +1433,17 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                 hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st,
                                    dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
         }
-        if (cmask)
+        if (cmask) {
+            unsigned* pcount = plist ? plist + ntile_frames : nullptr;
+            if (plist) (void)hipMemsetAsync(pcount, 0, sizeof(unsigned), st);
             hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nwf * 2)), dim3(1024), 0, st, D, H,
                                W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
-                               nwf, (unsigned short*)cmask, (unsigned short*)cfree);
+                               nwf, (unsigned short*)cmask, (unsigned short*)cfree, plist, pcount);
+            if (plist)
+                hipLaunchKernelGGL(tsdf_refine_kernel, dim3(2048), dim3(256), 0, st, D, H, W, z0, z1, nf, Hd, Wd, pp,
+                                   kp, bb, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, nwf, cmask, cfree, plist,
+                                   pcount);
+        }
         if (stats) {
             if (!cmask) {
                 set_error("sfmhip_tsdf_cull_stats: scratch allocation failed");
@@ -1406,6 +1487,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     (void)hipFreeAsync(rec, st);
     if (crange) (void)hipFreeAsync(crange, st);
     if (cmask) (void)hipFreeAsync(cmask, st);
+    if (plist) (void)hipFreeAsync(plist, st);
     if (cbmm && !ext_table) (void)hipFreeAsync(cbmm, st);
     if (cfree) (void)hipFreeAsync(cfree, st);
     return rc;

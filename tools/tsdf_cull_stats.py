@@ -14,10 +14,11 @@ sdist = importlib.import_module("3d_reconstruction_amd.dist")
 dev = torch.device("cuda", 0)
 depth, poses, K = syn.tsdf_scene(257, syn.IMG_H, syn.IMG_W, device=dev)
 R = 256
-for sub in ("1", "4"):
+for sub, ref in (("1", "0"), ("1", "1"), ("4", "0")):
     os.environ["SFMHIP_TSDF_CULLSUB"] = sub
+    os.environ["SFMHIP_TSDF_REFINE"] = ref
     for n in (1, 8):
         z0, z1 = sdist.shard_range(R, 0, n)
         s = sfm.tsdf_cull_stats((R, R, R), depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / (R - 1), z0, z1)
-        print(f"CULLSUB={sub} slab 0/{n}: culled {s['culled_frac']:.3f} free {s['free_frac']:.3f} "
+        print(f"CULLSUB={sub} REFINE={ref} slab 0/{n}: culled {s['culled_frac']:.3f} free {s['free_frac']:.3f} "
               f"full {s['full_frac']:.3f}", flush=True)
