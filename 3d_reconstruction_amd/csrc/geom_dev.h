@@ -257,10 +257,11 @@ __device__ inline void dlt_point(const double* P0, const double* P1, double x0, 
             y[r] = sacc * id[r];
         }
         for (int it = 0; it < kDltInvIters && !done; ++it) {
-            double nn = sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+            // normalisation by one reciprocal (the iterate's scale is arbitrary)
+            const double inn = 1.0 / sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
             double yo[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) { y[r] /= nn; yo[r] = y[r]; }
+            for (int r = 0; r < 4; ++r) { y[r] *= inn; yo[r] = y[r]; }
             double z[4];  // R^T z = y (forward)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -276,10 +277,10 @@ __device__ inline void dlt_point(const double* P0, const double* P1, double x0, 
                 for (int c = r + 1; c < 4; ++c) sacc -= R[r][c] * y[c];
                 y[r] = sacc * id[r];
             }
-            nn = sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+            const double inn2 = 1.0 / sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
             double dd = 0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dd += (y[r] / nn - yo[r]) * (y[r] / nn - yo[r]);
+            for (int r = 0; r < 4; ++r) dd += (y[r] * inn2 - yo[r]) * (y[r] * inn2 - yo[r]);
             done = dd <= 1e-30;
         }
     }
