@@ -555,6 +555,188 @@ __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// vq, d = 128, <= 256 codewords: f32 filter + exact decision (default).
+// The f32 MFMA (2x the f64 matrix rate) computes the GEMM-form scores
+// s_j = fl32(|c_j|^2) - 2 (x_f . c_f)_f32 with a proven bound on |s_j - (|c_j|^2 - 2 x.c_j)|:
+//   input rounding of x and c (2^-24 each), the f32 accumulation of d products
+//   (gamma_d), the norm's rounding: eps = 1.01 ((2d + 5) 2^-24 |x| cmax + 2^-24 cmax^2).
+// An observation whose best two scores are more than 2 eps apart has a unique
+// exact argmin, the best one; its distance is then computed in f64 difference form
+// (sqrt(sum (x - c)^2)).  The others (near-ties, exact ties) go to a list that
+// vq_exact_kernel settles in f64 difference form over every codeword (lowest index
+// on ties) — on integer data every value involved is exact, so codes and distances
+// are scipy's bit for bit; on floats the decided argmins are the exact ones.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kVqfWaves = 12;
+constexpr int kVqfTile = kVqfWaves * 32;   // observations per tile (32 per wave)
+__global__ __launch_bounds__(kVqfWaves * 64) void vq_f32f_kernel(const double* __restrict__ obs, int64_t n_obs,
+                                                                  const double* __restrict__ code, int n_codes,
+                                                                  int32_t* __restrict__ codes,
+                                                                  double* __restrict__ dist,
+                                                                  unsigned* __restrict__ amb,
+                                                                  unsigned* __restrict__ namb) {
+    constexpr int DP = 128, LD = DP + 4, KS = DP / 4;
+    extern __shared__ float smf[];
+    const int ncb = (n_codes + 15) >> 4;
+    float* sc = smf;                              // [ncb * 16][LD] codebook (f32)
+    float* sn = smf + (size_t)ncb * 16 * LD;      // [ncb * 16] squared norms (f32)
+    __shared__ int s_win[kVqfWaves][32];
+    __shared__ unsigned s_cmax;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r16 = lane & 15, kq = lane >> 4;
+    if (threadIdx.x == 0) s_cmax = 0u;
+    for (int t = threadIdx.x; t < ncb * 16 * DP; t += blockDim.x) {
+        const int r = t / DP, k = t - r * DP;
+        sc[r * LD + k] = r < n_codes ? (float)code[(size_t)r * DP + k] : 0.f;
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < ncb * 16; r += blockDim.x) {
+        double q = 0.0;
+        if (r < n_codes)
+            for (int k = 0; k < DP; ++k) q = __builtin_fma(code[(size_t)r * DP + k], code[(size_t)r * DP + k], q);
+        sn[r] = r < n_codes ? (float)q : __builtin_inff();   // padded codewords never win
+        if (r < n_codes) atomicMax(&s_cmax, __float_as_uint((float)sqrt(q) * 1.001f));   // positive floats
+    }
+    __syncthreads();
+    const double cmax = (double)__uint_as_float(s_cmax);
+    const double u = 0x1p-24;
+    const int64_t n_tiles = (n_obs + kVqfTile - 1) / kVqfTile;
+    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const int64_t ob = t * kVqfTile + wave * 32;
+        float a[2][KS];
+        double xn[2] = {0.0, 0.0};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t o = ob + 16 * h + r16;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const double x = o < n_obs ? __builtin_nontemporal_load(obs + o * DP + 4 * s + kq) : 0.0;
+                a[h][s] = (float)x;
+                xn[h] = __builtin_fma(x, x, xn[h]);
+            }
+            xn[h] += __shfl_xor(xn[h], 16);
+            xn[h] += __shfl_xor(xn[h], 32);   // |x|^2 of row r16, in every lane group
+            __builtin_amdgcn_sched_barrier(0);   // one row tile's f64 loads in flight at a time (VGPRs)
+        }
+        float b1[2][4], b2[2][4];
+        int i1[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) { b1[h][g] = b2[h][g] = __builtin_inff(); i1[h][g] = INT_MAX; }
+        for (int cb = 0; cb < ncb; ++cb) {
+            const int j = cb * 16 + r16;
+            const float* bp = sc + j * LD + kq;
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const float b = bp[4 * s];
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s], b, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1][s], b, acc1, 0, 0, 0);
+            }
+            const float cn = sn[j];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {   // C row 4 kq + g (observation), column r16 (codeword j)
+                const float d0 = cn - 2.f * acc0[g], d1 = cn - 2.f * acc1[g];
+                if (d0 < b1[0][g]) { b2[0][g] = b1[0][g]; b1[0][g] = d0; i1[0][g] = j; }
+                else if (d0 < b2[0][g]) b2[0][g] = d0;
+                if (d1 < b1[1][g]) { b2[1][g] = b1[1][g]; b1[1][g] = d1; i1[1][g] = j; }
+                else if (d1 < b2[1][g]) b2[1][g] = d1;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float v1 = b1[h][g], v2 = b2[h][g];
+                int x1 = i1[h][g];
+#pragma unroll
+                for (int off = 8; off >= 1; off >>= 1) {   // top-2 over the 16 codeword lanes
+                    const float o1 = __shfl_xor(v1, off, 16), o2 = __shfl_xor(v2, off, 16);
+                    const int ox = __shfl_xor(x1, off, 16);
+                    if (o1 < v1 || (o1 == v1 && ox < x1)) { v2 = fminf(v1, o2); v1 = o1; x1 = ox; }
+                    else v2 = fminf(o1, v2);
+                }
+                const int row = 4 * kq + g;
+                const double xr = __shfl(xn[h], row);   // lane `row` (group 0) holds |x|^2 of that row
+                const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax);
+                if (r16 == 0) s_win[wave][16 * h + row] = ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
+            }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // exact distances of the proven winners, difference form, 8 rows' loads in flight at a time
+        for (int r0 = 0; r0 < 32; r0 += 8) {
+            double part[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int64_t o = min(ob + r0 + q, n_obs - 1);
+                const int w = max(s_win[wave][r0 + q], 0);
+                const double* xp = obs + o * DP;
+                const double* cp = code + (size_t)w * DP;
+                const double d0 = xp[lane] - cp[lane], d1 = xp[lane + 64] - cp[lane + 64];
+                part[q] = __builtin_fma(d1, d1, d0 * d0);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) part[q] += __shfl_xor(part[q], off);
+            if (lane == 0)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int64_t o = ob + r0 + q;
+                    const int w = s_win[wave][r0 + q];
+                    if (o < n_obs) {
+                        if (w >= 0) {
+                            codes[o] = w;
+                            dist[o] = sqrt(part[q]);
+                        } else {
+                            amb[atomicAdd(namb, 1u)] = (unsigned)o;
+                        }
+                    }
+                }
+        }
+        __builtin_amdgcn_wave_barrier();   // s_win reused by the next tile
+    }
+}
+
+// The observations vq_f32f_kernel could not decide: one wave each, every codeword
+// in f64 difference form, lowest index on ties.
+__global__ __launch_bounds__(256) void vq_exact_kernel(const double* __restrict__ obs, const double* __restrict__ code,
+                                                       int n_codes, int d, const unsigned* __restrict__ amb,
+                                                       const unsigned* __restrict__ namb, int32_t* __restrict__ codes,
+                                                       double* __restrict__ dist) {
+    const int lane = threadIdx.x & 63;
+    const unsigned n = *namb;
+    for (unsigned e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
+        const int64_t o = amb[e];
+        const double* xp = obs + o * d;
+        double best = __builtin_inf();
+        int bi = INT_MAX;
+        for (int j = lane; j < n_codes; j += 64) {
+            const double* cp = code + (size_t)j * d;
+            double q = 0.0;
+            for (int k = 0; k < d; ++k) {
+                const double df = xp[k] - cp[k];
+                q = __builtin_fma(df, df, q);
+            }
+            if (q < best) { best = q; bi = j; }   // j increasing per lane: first (lowest) kept
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double ob = __shfl_xor(best, off);
+            const int oi = __shfl_xor(bi, off);
+            if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        }
+        if (lane == 0) {
+            codes[o] = bi;
+            dist[o] = sqrt(best);
+        }
+    }
+}
+
 }  // namespace sfmhip
 
 using namespace sfmhip;
@@ -702,8 +884,36 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
     SFMHIP_REQUIRE(n_obs >= 0 && n_codes > 0 && d > 0 && d <= 256, "sfmhip_vq: bad shape (d <= 256)");
     if (n_obs == 0) return SFMHIP_OK;
     const char* venv = std::getenv("SFMHIP_VQ_VARIANT");    // 1: the FMA difference-form kernel (A/B runs)
+    const int variant = venv ? std::atoi(venv) : 0;          // 3: the f64-MFMA GEMM-form kernel (A/B runs)
+    if (d == 128 && n_codes <= 256 && variant == 0) {
+        const int ncb = ceil_div(n_codes, 16);
+        const size_t shm = (size_t)ncb * 16 * (128 + 4 + 1) * sizeof(float);
+        hipStream_t s = as_stream(stream);
+        unsigned* amb = nullptr;
+        if (hipMallocAsync((void**)&amb, (size_t)(n_obs + 1) * sizeof(unsigned), s) == hipSuccess &&
+            n_obs < ((int64_t)1 << 32) - 1) {
+            unsigned* namb = amb + n_obs;
+            (void)hipMemsetAsync(namb, 0, sizeof(unsigned), s);
+            int dev = 0, n_cu = 256;
+            if (hipGetDevice(&dev) == hipSuccess)
+                (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+            const int64_t n_tiles = (n_obs + kVqfTile - 1) / kVqfTile;
+            (void)hipFuncSetAttribute((const void*)vq_f32f_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+            hipLaunchKernelGGL(vq_f32f_kernel, dim3((unsigned)std::min<int64_t>(n_tiles, n_cu)),
+                               dim3(kVqfWaves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb, namb);
+            int rc = check_launch("vq_f32f_kernel");
+            if (rc == SFMHIP_OK) {
+                hipLaunchKernelGGL(vq_exact_kernel, dim3(1024), dim3(256), 0, s, obs, code_book, n_codes, 128, amb,
+                                   namb, codes, dist);
+                rc = check_launch("vq_exact_kernel");
+            }
+            (void)hipFreeAsync(amb, s);
+            return rc;
+        }
+        (void)hipGetLastError();   // no scratch: the f64 kernels below
+    }
     const int dp = d <= 32 ? 32 : d <= 64 ? 64 : d <= 128 ? 128 : 0;
-    if (dp && !(venv && std::atoi(venv) == 1)) {
+    if (dp && variant != 1) {
         const int ld = dp + 4;
         const int max_cpp = std::min(144, (int)((150 * 1024 / 8) / (ld + 1)) / 16 * 16);
         const int passes = ceil_div(n_codes, max_cpp);
@@ -721,7 +931,7 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
         hipLaunchKernelGGL((vq_mfma_kernel<DP, PR, FL>), dim3(grid), dim3(kVqmWaves * 64), shm, s, obs, n_obs,      \
                            code_book, n_codes, d, cpp, codes, dist);                                       \
     } while (0)
-        const bool pair = venv && std::atoi(venv) == 2;   // 2: two code blocks per step (A/B runs)
+        const bool pair = variant == 2;   // 2: two code blocks per step (A/B runs)
         if (dp == 32) SFMHIP_LAUNCH_VQM(32, false, false);
         else if (dp == 64) SFMHIP_LAUNCH_VQM(64, false, false);
         else if (d != 128) SFMHIP_LAUNCH_VQM(128, false, false);

@@ -222,11 +222,14 @@ def test_match_empty_and_single_keypoint_images(sfm, gpu):
     assert (m0[:, 300:] == -1).all()                          # padding rows never match
 
 
-@pytest.mark.parametrize("n,k,d", [(5000, 200, 128), (777, 300, 40), (300, 1, 128), (1, 17, 64), (4097, 145, 20)])
+@pytest.mark.parametrize("n,k,d", [(5000, 200, 128), (777, 300, 40), (300, 1, 128), (1, 17, 64), (4097, 145, 20),
+                                   (3001, 256, 128), (257, 16, 128)])
 def test_vq_mfma_integer_bit_exact(sfm, gpu, n, k, d):
-    """f64-MFMA vq (GEMM form) on integer data: bit-exact with scipy, across
-    code-book passes (k > 144), padded dims (d not a power of two), a single
-    codeword and ragged observation tiles; ties resolve to the lowest index."""
+    """vq on integer data: bit-exact with scipy — the f32-filter path (d = 128,
+    k <= 256; exact ties go through the f64 exact pass) and the f64-MFMA GEMM
+    form (other shapes), across code-book passes (k > 144), padded dims (d not
+    a power of two), a single codeword and ragged observation tiles; ties
+    resolve to the lowest index."""
     rng = np.random.default_rng(n + k + d)
     obs = rng.integers(-20, 21, (n, d)).astype(np.float64)
     code = rng.integers(-20, 21, (k, d)).astype(np.float64)
@@ -235,3 +238,27 @@ def test_vq_mfma_integer_bit_exact(sfm, gpu, n, k, d):
     codes, dist = sfm.vq(obs, code)
     rc, rd = om.vq(obs, code)
     assert np.array_equal(codes, rc) and np.array_equal(dist, rd)
+
+
+def test_vq_f32_filter_floats_vs_scipy(sfm, gpu, monkeypatch):
+    """Float data (unit-norm descriptors, codewords not representable in f32):
+    the f32-filter path agrees with scipy's f64 vq on the codes (any difference
+    is a near-tie within f64 rounding) and on the distances to 1e-12, as the
+    f64-MFMA path does."""
+    x = syn.superpoint_like(5, 4096, 128, seed=21).reshape(-1, 128).double().numpy()
+    rng = np.random.default_rng(3)
+    code = x[rng.choice(len(x), 200, replace=False)] + rng.normal(0, 1e-3, (200, 128))
+    code[7] = code[3]                                             # an exact tie too
+    rc, rd = om.vq(x, code)
+    for variant in ("0", "3"):
+        monkeypatch.setenv("SFMHIP_VQ_VARIANT", variant)
+        codes, dist = sfm.vq(x, code)
+        # scipy's GEMM-form sqrt(|x|^2 + |c|^2 - 2 x.c) carries ~1e-16 |x|^2 of cancellation
+        # (obs next to a codeword); both GPU paths return the difference form
+        np.testing.assert_allclose(dist, rd, rtol=1e-12, atol=1e-12)
+        bad = np.nonzero(codes != rc)[0]
+        assert len(bad) <= 0.001 * len(x)
+        for i in bad:                                             # only near-ties may differ
+            da = ((x[i] - code[codes[i]]) ** 2).sum()
+            db = ((x[i] - code[rc[i]]) ** 2).sum()
+            assert abs(da - db) <= 1e-12 * max(da, db)
