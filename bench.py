@@ -10,9 +10,13 @@ dataset) and ONE all-gather of the int16 match graph runs inside the step.
 
 Secondary lines (same JSON object):
   * TSDF Mvoxel/sec — 256^3 grid fused from 257 synthetic 1936x1296 depth maps
-    (C5), z-slab sharded over ranks, no exchange.
+    (C5), z-slab sharded over ranks (N > 1: the depth block table is built per
+    frame range and all-gathered; no grid data is exchanged).
   * BA obs/sec — DLT triangulation + residual + FD Jacobian over 256 pairs x
     4096 observations.
+  * N = 1 only: DDA traversal, plenoxel render, vq, geometric verification,
+    PnP and the plenoxel training step, each with a CPU
+    baseline sample.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
         python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
