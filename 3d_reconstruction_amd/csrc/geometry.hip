@@ -212,7 +212,7 @@ extern "C" int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, con
     if (n == 0) return SFMHIP_OK;
     hipStream_t st = as_stream(stream);
     double* Rt = nullptr;
-    if (hipMallocAsync((void**)&Rt, (size_t)n_pairs * 36 * sizeof(double), st) != hipSuccess) {
+    if (scratch_alloc((void**)&Rt, (size_t)n_pairs * 36 * sizeof(double), st) != hipSuccess) {
         (void)hipGetLastError();
         set_error("sfmhip_reproj_fd_jacobian: rotation table allocation failed");
         return SFMHIP_E_HIP;

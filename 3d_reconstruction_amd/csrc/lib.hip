@@ -1,6 +1,7 @@
 // lib.hip — library-level entry points: version, thread-local error, arch probe.
 #include "common.h"
 #include <cstring>
+#include <mutex>
 
 namespace sfmhip {
 static thread_local char g_err[512] = "";
@@ -10,6 +11,23 @@ void set_error(const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof(g_err), fmt, ap);
     va_end(ap);
+}
+
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDev) {
+        std::call_once(once[dev], [dev] {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+                uint64_t thr = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+            }
+            (void)hipGetLastError();
+        });
+    }
+    return hipMallocAsync(p, bytes, s);
 }
 }  // namespace sfmhip
 

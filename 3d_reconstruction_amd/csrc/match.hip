@@ -890,7 +890,7 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
         const size_t shm = (size_t)ncb * 16 * (128 + 4 + 1) * sizeof(float);
         hipStream_t s = as_stream(stream);
         unsigned* amb = nullptr;
-        if (hipMallocAsync((void**)&amb, (size_t)(n_obs + 1) * sizeof(unsigned), s) == hipSuccess &&
+        if (scratch_alloc((void**)&amb, (size_t)(n_obs + 1) * sizeof(unsigned), s) == hipSuccess &&
             n_obs < ((int64_t)1 << 32) - 1) {
             unsigned* namb = amb + n_obs;
             (void)hipMemsetAsync(namb, 0, sizeof(unsigned), s);

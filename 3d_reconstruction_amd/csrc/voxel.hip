@@ -1380,7 +1380,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const int cf = std::min(chunk, F);
     const size_t nblk = (size_t)cf * nbu * nbv;
     float* rec = nullptr;
-    if (hipMallocAsync((void**)&rec, (size_t)cf * 16 * sizeof(float), st) != hipSuccess) {
+    if (scratch_alloc((void**)&rec, (size_t)cf * 16 * sizeof(float), st) != hipSuccess) {
         (void)hipGetLastError();
         set_error("sfmhip_tsdf_integrate: camera table allocation failed");
         return SFMHIP_E_HIP;
@@ -1393,19 +1393,19 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const int64_t ntile_frames = (int64_t)nbx * nby * nbz * std::min(chunk, F);
     if (want_cull) {
         if (ext_table) cbmm = const_cast<float2*>(ext_table);
-        else if (hipMallocAsync((void**)&cbmm, nblk * sizeof(float2), st) != hipSuccess) cbmm = nullptr;
-        if (cbmm && (hipMallocAsync((void**)&cmask, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess ||
-                     hipMallocAsync((void**)&crange, (size_t)cf * sizeof(int4), st) != hipSuccess)) {
+        else if (scratch_alloc((void**)&cbmm, nblk * sizeof(float2), st) != hipSuccess) cbmm = nullptr;
+        if (cbmm && (scratch_alloc((void**)&cmask, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess ||
+                     scratch_alloc((void**)&crange, (size_t)cf * sizeof(int4), st) != hipSuccess)) {
             if (cmask) (void)hipFreeAsync(cmask, st);
             if (!ext_table) (void)hipFreeAsync(cbmm, st);
             cbmm = nullptr;
             cmask = nullptr;
             crange = nullptr;
         }
-        if (cmask && want_free && hipMallocAsync((void**)&cfree, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess)
+        if (cmask && want_free && scratch_alloc((void**)&cfree, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess)
             cfree = nullptr;   // free-space path off, culling unchanged
         if (cmask && want_refine && ntile_frames < (int64_t)1 << 30 && nbx * nby * nbz < (1 << 23) &&
-            hipMallocAsync((void**)&plist, (size_t)(ntile_frames + 1) * sizeof(unsigned), st) != hipSuccess)
+            scratch_alloc((void**)&plist, (size_t)(ntile_frames + 1) * sizeof(unsigned), st) != hipSuccess)
             plist = nullptr;   // no second pass
         (void)hipGetLastError();
     }
@@ -1520,7 +1520,7 @@ extern "C" int sfmhip_tsdf_block_table(const float* depth, int F, int Hd, int Wd
     const int nbu = ceil_div(Wd, kCullBlock), nbv = ceil_div(Hd, kCullBlock), nf = f1 - f0;
     hipStream_t st = as_stream(stream);
     int4* rg = nullptr;
-    if (hipMallocAsync((void**)&rg, (size_t)nf * sizeof(int4), st) != hipSuccess) {
+    if (scratch_alloc((void**)&rg, (size_t)nf * sizeof(int4), st) != hipSuccess) {
         (void)hipGetLastError();
         set_error("sfmhip_tsdf_block_table: scratch allocation failed");
         return SFMHIP_E_HIP;
