@@ -72,6 +72,12 @@ class GridTrainer:
     def backward(self, rays_o, rays_d, gt, z):
         """Forward + loss + backward only (accumulates into self.grad).
         Returns (loss float, rgb (B,3) tensor)."""
+        loss, rgb, B = self._backward(rays_o, rays_d, gt, z)
+        return (float(loss.item()) / (3 * B) if B else float("nan")), rgb
+
+    def _backward(self, rays_o, rays_d, gt, z):
+        """backward() without the host synchronisation: (sum of squared errors as a
+        device f64 scalar, rgb, B)."""
         o = dev(rays_o, torch.float32).reshape(-1, 3)
         d = dev(rays_d, torch.float32).reshape(-1, 3)
         zz = dev(z, torch.float32)
@@ -84,8 +90,7 @@ class GridTrainer:
         call("sfmhip_render_train", ptr(self.param), self.D, self.H, self.W, _host_ptr(self.bmin),
              _host_ptr(self.bmax), self.mask_mode, ptr(o), ptr(d), ptr(zz), ptr(t), B, S, ptr(rgb), ptr(sq),
              ptr(self.grad), ptr(self.touched), stream_ptr())
-        loss = float(sq.double().sum().item()) / (3 * B) if B else float("nan")
-        return loss, rgb
+        return sq.double().sum(), rgb, B
 
     def optimizer_step(self, zero_grad: bool = True) -> None:
         self.step_count += 1
@@ -95,7 +100,8 @@ class GridTrainer:
              1 if zero_grad else 0, ptr(self.touched), 5, stream_ptr())
 
     def step(self, rays_o, rays_d, gt, z) -> float:
-        """One training iteration; returns loss.item()."""
-        loss, _ = self.backward(rays_o, rays_d, gt, z)
+        """One training iteration; returns loss.item() (plenoxel.py:105-111 reads it
+        every step).  The host waits once, after the Adam step is enqueued."""
+        loss, _, B = self._backward(rays_o, rays_d, gt, z)
         self.optimizer_step()
-        return loss
+        return float(loss.item()) / (3 * B) if B else float("nan")

@@ -319,13 +319,14 @@ def train_line(sfm, syn, device, args, barrier, cpu=True):
         if record:
             e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
             e0.record()
-        tr.backward(ro, rd, gt, z)
+        loss, _, nb = tr._backward(ro, rd, gt, z)
         if record:
             e1.record()
         tr.optimizer_step()
         if record:
             e2.record()
             ev.setdefault("a", []).append((e1, e2))
+        float(loss.item()) / (3 * nb)              # loss.item() every step, as plenoxel.py:110
         return (e0, e2)
 
     wall, kms = timed(step, args.steps, 1, barrier)
