@@ -702,7 +702,180 @@ __global__ __launch_bounds__(kVqfWaves * 64) void vq_f32f_kernel(const double* _
     }
 }
 
-// The observations vq_f32f_kernel could not decide: one wave each, every codeword
+// vq, d = 128, <= 256 codewords, register-resident observations (default).  Same
+// filter and bound as vq_f32f_kernel, re-shaped so that every observation byte is
+// read from HBM once: a wave owns 16 observations, lane (r, q) holds row r's f64
+// values k = 8t + 2q + {0,1} (t < 16) in VGPRs for the whole unit — each load
+// instruction reads 64 contiguous bytes per row, so the texture path handles 16
+// half-lines per instruction, not 64 scattered 16-B pieces — (k-step 2t + e feeds
+// the MFMA with k = 8t + 2q + e; the codebook fragments are laid out to match),
+// and the proven winner's difference-form distance is summed from those registers
+// against the f64 codeword (L2-resident).  The f32 codebook sits in LDS in MFMA
+// B-fragment order ([block][k-quad][lane] float4: one conflict-free ds_read_b128
+// per 4 k-steps), two codeword blocks per pass (two independent MFMA chains).
+// 8 waves per workgroup (2 per SIMD, 256 VGPRs each), units dealt wave by wave;
+// each wave's next unit is loaded while the current one computes.
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+constexpr int kVqrWaves = 8;
+template <int PROBE>   // PROBE (timing ablations only, never the product): 1 no HBM loads,
+                       // 3 no codeword loads in the exact tail, 4 cached (not non-temporal) loads
+__global__ __launch_bounds__(kVqrWaves * 64) void vq_f32r_kernel(const double* __restrict__ obs, int64_t n_obs,
+                                                                  const double* __restrict__ code, int n_codes,
+                                                                  int32_t* __restrict__ codes,
+                                                                  double* __restrict__ dist,
+                                                                  unsigned* __restrict__ amb,
+                                                                  unsigned* __restrict__ namb) {
+    constexpr int DP = 128, KS = 32;
+    extern __shared__ f32x4 smv[];
+    const int ncb = (n_codes + 15) >> 4;           // codeword blocks of 16
+    const int ncp = (ncb + 1) & ~1;                // LDS blocks (even count)
+    f32x4* sc = smv;                                // [ncp][8][64] B fragments
+    float* sn = reinterpret_cast<float*>(smv + ncp * 8 * 64);   // [ncp * 16] squared norms
+    __shared__ unsigned s_cmax;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r16 = lane & 15, kq = lane >> 4;
+    if (threadIdx.x == 0) s_cmax = 0u;
+    for (int t = threadIdx.x; t < ncp * 16 * DP; t += blockDim.x) {
+        const int j = t >> 7, k = t & (DP - 1);
+        const float v = j < n_codes ? (float)code[(size_t)j * DP + k] : 0.f;
+        const int ln = (((k >> 1) & 3) << 4) | (j & 15), s = ((k >> 3) << 1) | (k & 1);
+        reinterpret_cast<float*>(sc)[((((j >> 4) * 8 + (s >> 2)) * 64 + ln) << 2) | (s & 3)] = v;
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < ncp * 16; r += blockDim.x) {
+        double q = 0.0;
+        if (r < n_codes)
+            for (int k = 0; k < DP; ++k) q = __builtin_fma(code[(size_t)r * DP + k], code[(size_t)r * DP + k], q);
+        sn[r] = r < n_codes ? (float)q : __builtin_inff();   // padded codewords never win
+        if (r < n_codes) atomicMax(&s_cmax, __float_as_uint((float)sqrt(q) * 1.001f));
+    }
+    __syncthreads();
+    const double cmax = (double)__uint_as_float(s_cmax);
+    const double u = 0x1p-24;
+    const int64_t n_units = (n_obs + 15) >> 4;
+    const int64_t ustep = (int64_t)gridDim.x * kVqrWaves;
+    f64x2 nx[KS / 2];   // the next unit's observations, in flight while this unit computes
+    auto fetch = [&](int64_t un) {
+        const f64x2* xp = reinterpret_cast<const f64x2*>(obs + min(un * 16 + r16, n_obs - 1) * DP) + kq;
+#pragma unroll
+        for (int s2 = 0; s2 < KS / 2; ++s2) {
+            if (PROBE == 1) nx[s2] = f64x2{(double)(lane + un), (double)s2};
+            else if (PROBE == 4) nx[s2] = xp[4 * s2];
+            else nx[s2] = __builtin_nontemporal_load(xp + 4 * s2);
+        }
+    };
+    fetch(min((int64_t)blockIdx.x * kVqrWaves + wave, n_units - 1));
+    for (int64_t un = (int64_t)blockIdx.x * kVqrWaves + wave; un < n_units; un += ustep) {
+        const int64_t o = un * 16 + r16;
+        double x[KS];
+#pragma unroll
+        for (int s2 = 0; s2 < KS / 2; ++s2) {
+            x[2 * s2] = nx[s2].x;
+            x[2 * s2 + 1] = nx[s2].y;
+        }
+        fetch(min(un + ustep, n_units - 1));
+        double xn = 0.0;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) xn = __builtin_fma(x[s], x[s], xn);
+        xn += __shfl_xor(xn, 16);
+        xn += __shfl_xor(xn, 32);   // |x|^2 of row r16, in every lane group
+        float b1[4], b2[4];
+        int i1[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) { b1[g] = b2[g] = __builtin_inff(); i1[g] = INT_MAX; }
+        auto take = [&](int g, float dd, int j) {   // branch-free top-2 (selects, no exec-mask branches)
+            const bool l = dd < b1[g];
+            b2[g] = l ? b1[g] : fminf(dd, b2[g]);
+            i1[g] = l ? j : i1[g];
+            b1[g] = l ? dd : b1[g];
+        };
+        for (int cb = 0; cb + 1 < ncb; cb += 2) {
+            const f32x4* bp = sc + cb * 8 * 64 + lane;
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+            for (int s4 = 0; s4 < KS / 4; ++s4) {
+                const f32x4 c0 = bp[s4 * 64], c1 = bp[(8 + s4) * 64];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float a = (float)x[4 * s4 + e];
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, c0[e], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, c1[e], acc1, 0, 0, 0);
+                }
+                if (s4 & 1) __builtin_amdgcn_sched_barrier(0);   // LDS fragments two k-quads ahead at most
+            }
+            const int j0 = cb * 16 + r16;
+            const float cn0 = sn[j0], cn1 = sn[j0 + 16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {   // C row 4 kq + g (observation), columns j0, j0 + 16
+                take(g, cn0 - 2.f * acc0[g], j0);
+                take(g, cn1 - 2.f * acc1[g], j0 + 16);
+            }
+        }
+        if (ncb & 1) {   // odd block count: the last block alone (its padded partner is never computed)
+            const int cb = ncb - 1;
+            const f32x4* bp = sc + cb * 8 * 64 + lane;
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;   // even / odd k-steps: two chains
+#pragma unroll
+            for (int s4 = 0; s4 < KS / 4; ++s4) {
+                const f32x4 c0 = bp[s4 * 64];
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x[4 * s4], c0[0], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x[4 * s4 + 1], c0[1], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x[4 * s4 + 2], c0[2], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x[4 * s4 + 3], c0[3], acc1, 0, 0, 0);
+            }
+            const int j0 = cb * 16 + r16;
+            const float cn0 = sn[j0];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) take(g, cn0 - 2.f * (acc0[g] + acc1[g]), j0);
+        }
+        int win[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            float v1 = b1[g], v2 = b2[g];
+            int x1 = i1[g];
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) {   // top-2 over the 16 codeword lanes
+                const float o1 = __shfl_xor(v1, off, 16), o2 = __shfl_xor(v2, off, 16);
+                const int ox = __shfl_xor(x1, off, 16);
+                const bool t = o1 < v1 || (o1 == v1 && ox < x1);
+                v2 = t ? fminf(v1, o2) : fminf(o1, v2);
+                v1 = t ? o1 : v1;
+                x1 = t ? ox : x1;
+            }
+            const double xr = __shfl(xn, 4 * kq + g);   // lane 4kq+g holds |x|^2 of that row
+            const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax);
+            win[g] = ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
+        }
+        int w = -1;   // row r16's verdict: group r16 >> 2, entry r16 & 3
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int t = __shfl(win[g], (r16 >> 2) << 4);
+            if ((r16 & 3) == g) w = t;
+        }
+        const f64x2* cp = reinterpret_cast<const f64x2*>(code + (size_t)max(w, 0) * DP) + kq;
+        double part = 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < KS / 2; ++s2) {
+            const f64x2 c = PROBE == 3 ? f64x2{x[2 * s2 + 1], x[2 * s2]} : cp[4 * s2];
+            const double d0 = x[2 * s2] - c.x, d1 = x[2 * s2 + 1] - c.y;
+            part = __builtin_fma(d0, d0, part);
+            part = __builtin_fma(d1, d1, part);
+            if ((s2 & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // 4 codeword loads in flight (VGPRs)
+        }
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+        if (kq == 0 && o < n_obs) {
+            if (w >= 0) {
+                codes[o] = w;
+                dist[o] = sqrt(part);
+            } else {
+                amb[atomicAdd(namb, 1u)] = (unsigned)o;
+            }
+        }
+    }
+}
+
+// The observations vq_f32f_kernel / vq_f32r_kernel could not decide: one wave each, every codeword
 // in f64 difference form, lowest index on ties.
 __global__ __launch_bounds__(256) void vq_exact_kernel(const double* __restrict__ obs, const double* __restrict__ code,
                                                        int n_codes, int d, const unsigned* __restrict__ amb,
@@ -885,9 +1058,11 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
     if (n_obs == 0) return SFMHIP_OK;
     const char* venv = std::getenv("SFMHIP_VQ_VARIANT");    // 1: the FMA difference-form kernel (A/B runs)
     const int variant = venv ? std::atoi(venv) : 0;          // 3: the f64-MFMA GEMM-form kernel (A/B runs)
-    if (d == 128 && n_codes <= 256 && variant == 0) {
-        const int ncb = ceil_div(n_codes, 16);
-        const size_t shm = (size_t)ncb * 16 * (128 + 4 + 1) * sizeof(float);
+    if (d == 128 && n_codes <= 256 && (variant == 0 || variant == 4)) {   // 4: vq_f32f_kernel (A/B runs)
+        const bool reg = variant == 0;
+        const int ncb = ceil_div(n_codes, 16), ncp = ceil_div(n_codes, 32) * 2;
+        const size_t shm = reg ? (size_t)ncp * 16 * (128 + 1) * sizeof(float)
+                               : (size_t)ncb * 16 * (128 + 4 + 1) * sizeof(float);
         hipStream_t s = as_stream(stream);
         unsigned* amb = nullptr;
         if (scratch_alloc((void**)&amb, (size_t)(n_obs + 1) * sizeof(unsigned), s) == hipSuccess &&
@@ -897,11 +1072,27 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
             int dev = 0, n_cu = 256;
             if (hipGetDevice(&dev) == hipSuccess)
                 (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-            const int64_t n_tiles = (n_obs + kVqfTile - 1) / kVqfTile;
-            (void)hipFuncSetAttribute((const void*)vq_f32f_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-            hipLaunchKernelGGL(vq_f32f_kernel, dim3((unsigned)std::min<int64_t>(n_tiles, n_cu)),
-                               dim3(kVqfWaves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb, namb);
-            int rc = check_launch("vq_f32f_kernel");
+            int rc;
+            if (reg) {
+                const int64_t n_wg = ((n_obs + 15) / 16 + kVqrWaves - 1) / kVqrWaves;
+                const char* penv = std::getenv("SFMHIP_VQ_PROBE");   // timing ablations (tools/bench_vq.py)
+                const int probe = penv ? std::atoi(penv) : 0;
+                auto kern = probe == 1 ? vq_f32r_kernel<1>
+                           : probe == 3 ? vq_f32r_kernel<3> : probe == 4 ? vq_f32r_kernel<4> : vq_f32r_kernel<0>;
+                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+                hipLaunchKernelGGL(kern, dim3((unsigned)std::min<int64_t>(n_wg, n_cu)),
+                                   dim3(kVqrWaves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
+                                   namb);
+                rc = check_launch("vq_f32r_kernel");
+            } else {
+                const int64_t n_tiles = (n_obs + kVqfTile - 1) / kVqfTile;
+                (void)hipFuncSetAttribute((const void*)vq_f32f_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)shm);
+                hipLaunchKernelGGL(vq_f32f_kernel, dim3((unsigned)std::min<int64_t>(n_tiles, n_cu)),
+                                   dim3(kVqfWaves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
+                                   namb);
+                rc = check_launch("vq_f32f_kernel");
+            }
             if (rc == SFMHIP_OK) {
                 hipLaunchKernelGGL(vq_exact_kernel, dim3(1024), dim3(256), 0, s, obs, code_book, n_codes, 128, amb,
                                    namb, codes, dist);

@@ -226,7 +226,7 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
     ms = wall / args.steps * 1e3
     line = {"metric": "vq obs/sec", "value": obs.shape[0] / (ms * 1e-3), "unit": "obs/s", "ms_per_step": ms,
             "config": {"workload": "M2 vq (matching.py:27): 257x4096 obs x 200 codes x 128-d, f64"},
-            "roofline": {"bound": "mfma", "kernel": "vq_f32f_kernel+vq_exact_kernel", "kernel_ms": float(np.mean(kms)),
+            "roofline": {"bound": "mfma", "kernel": "vq_f32r_kernel+vq_exact_kernel", "kernel_ms": float(np.mean(kms)),
                          # GEMM form: 2 flops per (obs, codeword, dim) on v_mfma_f32_16x16x4_f32 (f32 filter
                          # with a proven error bound; undecided observations settled in f64)
                          "achieved_tflops": 2 * obs.shape[0] * 200 * 128 / (np.mean(kms) * 1e-3) / 1e12,

@@ -224,12 +224,15 @@ def test_match_empty_and_single_keypoint_images(sfm, gpu):
 
 @pytest.mark.parametrize("n,k,d", [(5000, 200, 128), (777, 300, 40), (300, 1, 128), (1, 17, 64), (4097, 145, 20),
                                    (3001, 256, 128), (257, 16, 128)])
-def test_vq_mfma_integer_bit_exact(sfm, gpu, n, k, d):
+@pytest.mark.parametrize("variant", ["0", "4"])
+def test_vq_mfma_integer_bit_exact(sfm, gpu, monkeypatch, variant, n, k, d):
     """vq on integer data: bit-exact with scipy — the f32-filter path (d = 128,
     k <= 256; exact ties go through the f64 exact pass) and the f64-MFMA GEMM
     form (other shapes), across code-book passes (k > 144), padded dims (d not
     a power of two), a single codeword and ragged observation tiles; ties
-    resolve to the lowest index."""
+    resolve to the lowest index.  Variant 4 is the tile-staged f32 filter
+    (vq_f32f_kernel) beside the default register-resident one."""
+    monkeypatch.setenv("SFMHIP_VQ_VARIANT", variant)
     rng = np.random.default_rng(n + k + d)
     obs = rng.integers(-20, 21, (n, d)).astype(np.float64)
     code = rng.integers(-20, 21, (k, d)).astype(np.float64)
@@ -250,7 +253,7 @@ def test_vq_f32_filter_floats_vs_scipy(sfm, gpu, monkeypatch):
     code = x[rng.choice(len(x), 200, replace=False)] + rng.normal(0, 1e-3, (200, 128))
     code[7] = code[3]                                             # an exact tie too
     rc, rd = om.vq(x, code)
-    for variant in ("0", "3"):
+    for variant in ("0", "4", "3"):
         monkeypatch.setenv("SFMHIP_VQ_VARIANT", variant)
         codes, dist = sfm.vq(x, code)
         # scipy's GEMM-form sqrt(|x|^2 + |c|^2 - 2 x.c) carries ~1e-16 |x|^2 of cancellation

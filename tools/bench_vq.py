@@ -1,5 +1,5 @@
-"""A/B the M2 vq kernels: python tools/bench_vq.py  (SFMHIP_VQ_VARIANT: 0 f32 filter + exact decision
-(default), 3 f64 MFMA one block/step, 2 f64 MFMA two blocks/step, 1 FMA difference form)."""
+"""A/B the M2 vq kernels: python tools/bench_vq.py  (SFMHIP_VQ_VARIANT: 0 f32 filter + exact decision,
+register-resident observations (default), 4 the same filter tile-staged, 3 f64 MFMA one block/step, 2 f64 MFMA two blocks/step, 1 FMA difference form)."""
 import importlib
 import os
 import sys
@@ -13,7 +13,7 @@ dev = torch.device("cuda", 0)
 obs = syn.superpoint_like(257, 4096, 128, seed=3, device=dev).reshape(-1, 128).double().contiguous()
 book = obs[torch.randperm(obs.shape[0], device=dev)[:200]].contiguous()
 out = {}
-for variant in ("0", "3", "2", "1"):
+for variant in (sys.argv[1].split(",") if len(sys.argv) > 1 else ("0", "4", "3", "2", "1")):
     os.environ["SFMHIP_VQ_VARIANT"] = variant
     codes = torch.empty(obs.shape[0], dtype=torch.int32, device=dev)
     dist = torch.empty(obs.shape[0], dtype=torch.float64, device=dev)
@@ -34,7 +34,7 @@ for variant in ("0", "3", "2", "1"):
     print(f"variant {variant}: {ms:.3f} ms  {obs.shape[0] / ms / 1e3:.1f} Mobs/s  "
           f"{2 * obs.shape[0] * 200 * 128 / ms / 1e9:.2f} TFLOP/s (2nkd)", flush=True)
 c0, d0 = out["0"]
-for v in ("3", "1"):
+for v in [v for v in ("4", "3", "1") if v in out]:
     c1, d1 = out[v]
     print(f"0 vs {v}: codes agree", (c0 == c1).float().mean().item(), "max rel dist",
           ((d0 - d1).abs() / d1.clamp_min(1e-300)).max().item())
