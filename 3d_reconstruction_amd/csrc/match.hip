@@ -717,9 +717,9 @@ __global__ __launch_bounds__(kVqfWaves * 64) void vq_f32f_kernel(const double* _
 // each wave's next unit is loaded while the current one computes.
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 constexpr int kVqrWaves = 8;
-template <int PROBE>   // PROBE (timing ablations only, never the product): 1 no HBM loads,
+template <int PROBE, int WAVES = kVqrWaves>   // WAVES 16: 4 per SIMD, no prefetch (A/B);  PROBE (timing ablations only, never the product): 1 no HBM loads,
                        // 3 no codeword loads in the exact tail, 4 cached (not non-temporal) loads
-__global__ __launch_bounds__(kVqrWaves * 64) void vq_f32r_kernel(const double* __restrict__ obs, int64_t n_obs,
+__global__ __launch_bounds__(WAVES * 64) void vq_f32r_kernel(const double* __restrict__ obs, int64_t n_obs,
                                                                   const double* __restrict__ code, int n_codes,
                                                                   int32_t* __restrict__ codes,
                                                                   double* __restrict__ dist,
@@ -753,7 +753,8 @@ __global__ __launch_bounds__(kVqrWaves * 64) void vq_f32r_kernel(const double* _
     const double cmax = (double)__uint_as_float(s_cmax);
     const double u = 0x1p-24;
     const int64_t n_units = (n_obs + 15) >> 4;
-    const int64_t ustep = (int64_t)gridDim.x * kVqrWaves;
+    constexpr bool kPre = WAVES <= 8;   // the prefetch needs the VGPRs of 2 waves per SIMD
+    const int64_t ustep = (int64_t)gridDim.x * WAVES;
     f64x2 nx[KS / 2];   // the next unit's observations, in flight while this unit computes
     auto fetch = [&](int64_t un) {
         const f64x2* xp = reinterpret_cast<const f64x2*>(obs + min(un * 16 + r16, n_obs - 1) * DP) + kq;
@@ -764,16 +765,17 @@ __global__ __launch_bounds__(kVqrWaves * 64) void vq_f32r_kernel(const double* _
             else nx[s2] = __builtin_nontemporal_load(xp + 4 * s2);
         }
     };
-    fetch(min((int64_t)blockIdx.x * kVqrWaves + wave, n_units - 1));
-    for (int64_t un = (int64_t)blockIdx.x * kVqrWaves + wave; un < n_units; un += ustep) {
+    if (kPre) fetch(min((int64_t)blockIdx.x * WAVES + wave, n_units - 1));
+    for (int64_t un = (int64_t)blockIdx.x * WAVES + wave; un < n_units; un += ustep) {
         const int64_t o = un * 16 + r16;
+        if (!kPre) fetch(un);
         double x[KS];
 #pragma unroll
         for (int s2 = 0; s2 < KS / 2; ++s2) {
             x[2 * s2] = nx[s2].x;
             x[2 * s2 + 1] = nx[s2].y;
         }
-        fetch(min(un + ustep, n_units - 1));
+        if (kPre) fetch(min(un + ustep, n_units - 1));
         double xn = 0.0;
 #pragma unroll
         for (int s = 0; s < KS; ++s) xn = __builtin_fma(x[s], x[s], xn);
@@ -790,6 +792,10 @@ __global__ __launch_bounds__(kVqrWaves * 64) void vq_f32r_kernel(const double* _
             b1[g] = l ? dd : b1[g];
         };
         for (int cb = 0; cb + 1 < ncb; cb += 2) {
+            if (!kPre) {
+#pragma unroll
+                for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(x[s]));   // convert per pass (VGPRs)
+            }
             const f32x4* bp = sc + cb * 8 * 64 + lane;
             f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
 #pragma unroll
@@ -1074,14 +1080,16 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
                 (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
             int rc;
             if (reg) {
-                const int64_t n_wg = ((n_obs + 15) / 16 + kVqrWaves - 1) / kVqrWaves;
                 const char* penv = std::getenv("SFMHIP_VQ_PROBE");   // timing ablations (tools/bench_vq.py)
                 const int probe = penv ? std::atoi(penv) : 0;
+                const int waves = probe == 5 ? 16 : kVqrWaves;
+                const int64_t n_wg = ((n_obs + 15) / 16 + waves - 1) / waves;
                 auto kern = probe == 1 ? vq_f32r_kernel<1>
-                           : probe == 3 ? vq_f32r_kernel<3> : probe == 4 ? vq_f32r_kernel<4> : vq_f32r_kernel<0>;
+                           : probe == 3 ? vq_f32r_kernel<3> : probe == 4 ? vq_f32r_kernel<4>
+                           : probe == 5 ? vq_f32r_kernel<0, 16> : vq_f32r_kernel<0>;
                 (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
                 hipLaunchKernelGGL(kern, dim3((unsigned)std::min<int64_t>(n_wg, n_cu)),
-                                   dim3(kVqrWaves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
+                                   dim3(waves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
                                    namb);
                 rc = check_launch("vq_f32r_kernel");
             } else {
