@@ -64,9 +64,13 @@ __device__ __forceinline__ void ray_step(Ray& R) {
     const bool mx = (tx < ty) && (tx < tz);
     const bool my = (ty <= tx) && (ty < tz);
     const bool mz = ((tx >= ty) && (ty >= tz)) || ((tx >= tz) && (ty > tx));
-    if (mx) { R.cur[0] = R.cur[0] + R.step[0]; R.tmax[0] = R.tmax[0] + R.tdelta[0]; }
-    if (my) { R.cur[1] = R.cur[1] + R.step[1]; R.tmax[1] = R.tmax[1] + R.tdelta[1]; }
-    if (mz) { R.cur[2] = R.cur[2] + R.step[2]; R.tmax[2] = R.tmax[2] + R.tdelta[2]; }
+    // selects, not branches: the walk is one long dependent chain per ray
+    R.cur[0] = mx ? R.cur[0] + R.step[0] : R.cur[0];
+    R.tmax[0] = mx ? R.tmax[0] + R.tdelta[0] : R.tmax[0];
+    R.cur[1] = my ? R.cur[1] + R.step[1] : R.cur[1];
+    R.tmax[1] = my ? R.tmax[1] + R.tdelta[1] : R.tmax[1];
+    R.cur[2] = mz ? R.cur[2] + R.step[2] : R.cur[2];
+    R.tmax[2] = mz ? R.tmax[2] + R.tdelta[2] : R.tmax[2];
 }
 
 __global__ void dda_count_kernel(const float* __restrict__ rays, int64_t N, float bin, int max_steps,
@@ -109,6 +113,17 @@ __global__ __launch_bounds__(256) void dda_fill_kernel(const float* __restrict__
     float* t = tile[w];
     const int nrows = (int)min((int64_t)64, N - ray0);
     for (int s0 = 0; s0 < S; s0 += kDdaCh) {
+        if (s0 >= 2 && !__any(act)) {
+            // Every ray of the wave has ended (S is the longest ray of the whole
+            // batch): the rest of these rows is NaN padding, stored row by row in
+            // 64-lane contiguous runs without walking the remaining steps.
+            const int rest = (S - s0) * 3;
+            for (int r = 0; r < nrows; ++r) {
+                float* o = out + ((size_t)(ray0 + r) * S + s0) * 3;
+                for (int f = lane; f < rest; f += 64) o[f] = nan;
+            }
+            return;
+        }
         const int cnt = min(kDdaCh, S - s0);
         for (int q = 0; q < cnt; ++q) {
             const int s = s0 + q;
@@ -128,10 +143,18 @@ __global__ __launch_bounds__(256) void dda_fill_kernel(const float* __restrict__
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        const int per_row = cnt * 3;
-        for (int f = lane; f < nrows * per_row; f += 64) {
-            const int r = f / per_row, c = f - r * per_row;
-            out[((size_t)(ray0 + r) * S + s0) * 3 + c] = t[r * kDdaCh * 3 + c];
+        if (cnt == kDdaCh) {   // full chunk: constant row length (division by a constant)
+            constexpr int per_row = kDdaCh * 3;
+            for (int f = lane; f < nrows * per_row; f += 64) {
+                const int r = f / per_row, c = f - r * per_row;
+                out[((size_t)(ray0 + r) * S + s0) * 3 + c] = t[r * kDdaCh * 3 + c];
+            }
+        } else {
+            const int per_row = cnt * 3;
+            for (int f = lane; f < nrows * per_row; f += 64) {
+                const int r = f / per_row, c = f - r * per_row;
+                out[((size_t)(ray0 + r) * S + s0) * 3 + c] = t[r * kDdaCh * 3 + c];
+            }
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -37,6 +37,25 @@ def test_voxel_traversal_random_vs_oracle(sfm, gpu):
     np.testing.assert_array_equal(out, ov.voxel_traversal(rays, 1.0))
 
 
+def test_voxel_traversal_padding_early_exit_vs_oracle(sfm, gpu):
+    """One long ray sets S for the whole batch, so most waves end long before S
+    and store their NaN padding without walking the remaining steps; a ragged
+    last wave (N = 1000) and rays inactive from the start (emitted twice)."""
+    rng = np.random.default_rng(5)
+    N = 1000
+    o = rng.uniform(-20, 20, (N, 3)).astype(np.float32)
+    d = rng.standard_normal((N, 3)).astype(np.float32)
+    near = rng.uniform(0, 2, (N, 1)).astype(np.float32)
+    far = near + rng.uniform(0, 8, (N, 1)).astype(np.float32)
+    far[::13] = near[::13]                         # inactive from the start
+    far[131] = near[131] + 150.0                   # the longest ray, in the third wave
+    rays = np.concatenate([o, d, near, far], 1)
+    out = sfm.voxel_traversal(torch.from_numpy(rays).to(gpu), 1.0).cpu().numpy()
+    ref = ov.voxel_traversal(rays, 1.0)
+    assert out.shape == ref.shape and out.shape[1] > 100
+    np.testing.assert_array_equal(out, ref)
+
+
 def test_grid_sample_sdf_golden(sfm, gpu):
     g = golden("sdf_golden.npz")
     vg = sfm.VoxelGrid(torch.from_numpy(g["grid"]).to(gpu), g["bmin"], g["bmax"], sfm.MASK_SDF)

@@ -20,5 +20,5 @@ ap.add_argument("--cpu", action="store_true")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 for name in a.lines:
-    fn = getattr(bench, f"{name}_line")
+    fn = getattr(bench, f"{name}_line", None) or getattr(bench, f"{name}_lines")
     print(json.dumps(fn(sfm, syn, dev, a, lambda: None, cpu=a.cpu)), flush=True)
