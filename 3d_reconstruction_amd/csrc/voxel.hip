@@ -161,6 +161,49 @@ __global__ __launch_bounds__(256) void dda_fill_kernel(const float* __restrict__
     }
 }
 
+// Pass 2, few rays (latency-bound: the launch lasts as long as its longest ray):
+// each lane stores its own row directly, one 12-B store per step, no LDS
+// staging; lanes whose rays have ended store NaN rows, and a wave whose rays
+// have all ended stores the remaining padding in 64-lane runs and exits.
+__global__ __launch_bounds__(64) void dda_fill_direct_kernel(const float* __restrict__ rays, int64_t N, float bin,
+                                                             int S, float* __restrict__ out) {
+    const int lane = threadIdx.x;
+    const int64_t ray0 = (int64_t)blockIdx.x * 64, i = ray0 + lane;
+    const float nan = __builtin_nanf("");
+    Ray R;
+    bool act = false, dup = false;
+    if (i < N) {
+        ray_setup(rays + 8 * i, bin, R);
+        act = ray_active(R);
+        dup = !act;
+    }
+    const int nrows = (int)min((int64_t)64, N - ray0);
+    float* row = out + (size_t)min(i, N - 1) * S * 3;
+    for (int s = 0; s < S; ++s) {
+        if (s >= 2 && !__any(act)) {
+            const int rest = (S - s) * 3;
+            for (int r = 0; r < nrows; ++r) {
+                float* o = out + ((size_t)(ray0 + r) * S + s) * 3;
+                for (int f = lane; f < rest; f += 64) o[f] = nan;
+            }
+            return;
+        }
+        float v0 = nan, v1 = nan, v2 = nan;
+        if (s == 0 || (s == 1 && dup)) {
+            v0 = R.cur[0]; v1 = R.cur[1]; v2 = R.cur[2];
+        } else if (act) {
+            ray_step(R);
+            v0 = R.cur[0]; v1 = R.cur[1]; v2 = R.cur[2];
+            act = ray_active(R);
+        }
+        if (i < N) {
+            row[3 * s] = v0;
+            row[3 * s + 1] = v1;
+            row[3 * s + 2] = v2;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // V2: sdf.py:287-291 / plenoxel.py:34-37 normalisation, then ATen
 // grid_sampler_3d (bilinear, zeros, align_corners=True) weight formulas.
@@ -1294,6 +1337,15 @@ extern "C" int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, i
     SFMHIP_REQUIRE(rays && out, "sfmhip_voxel_traversal: null pointer");
     SFMHIP_REQUIRE(N >= 0 && S >= 1, "sfmhip_voxel_traversal: bad args");
     if (N == 0) return SFMHIP_OK;
+    // SFMHIP_DDA_DIRECT (A/B): 1 per-lane row stores, 0 LDS-staged coalesced
+    // chunks; default: direct below 64k rays (latency-bound), staged above.
+    const char* denv = std::getenv("SFMHIP_DDA_DIRECT");
+    const bool direct = denv ? std::atoi(denv) != 0 : N < 65536;
+    if (direct) {
+        hipLaunchKernelGGL(dda_fill_direct_kernel, dim3(ceil_div(N, 64)), dim3(64), 0, as_stream(stream), rays, N,
+                           bin, S, out);
+        return check_launch("dda_fill_direct_kernel");
+    }
     hipLaunchKernelGGL(dda_fill_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, as_stream(stream), rays, N, bin, S,
                        out);  // 4 waves x 64 rays per workgroup
     return check_launch("dda_fill_kernel");

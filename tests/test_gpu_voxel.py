@@ -37,7 +37,8 @@ def test_voxel_traversal_random_vs_oracle(sfm, gpu):
     np.testing.assert_array_equal(out, ov.voxel_traversal(rays, 1.0))
 
 
-def test_voxel_traversal_padding_early_exit_vs_oracle(sfm, gpu):
+@pytest.mark.parametrize("direct", ["0", "1"])
+def test_voxel_traversal_padding_early_exit_vs_oracle(sfm, gpu, monkeypatch, direct):
     """One long ray sets S for the whole batch, so most waves end long before S
     and store their NaN padding without walking the remaining steps; a ragged
     last wave (N = 1000) and rays inactive from the start (emitted twice)."""
@@ -50,6 +51,7 @@ def test_voxel_traversal_padding_early_exit_vs_oracle(sfm, gpu):
     far[::13] = near[::13]                         # inactive from the start
     far[131] = near[131] + 150.0                   # the longest ray, in the third wave
     rays = np.concatenate([o, d, near, far], 1)
+    monkeypatch.setenv("SFMHIP_DDA_DIRECT", direct)   # both fill kernels
     out = sfm.voxel_traversal(torch.from_numpy(rays).to(gpu), 1.0).cpu().numpy()
     ref = ov.voxel_traversal(rays, 1.0)
     assert out.shape == ref.shape and out.shape[1] > 100
