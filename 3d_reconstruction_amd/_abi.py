@@ -24,6 +24,12 @@ SFMHIP_E_ARG = -1
 SFMHIP_E_HIP = -2
 SFMHIP_E_UNSUPPORTED = -3
 SFMHIP_E_OVERFLOW = -4
+SFMHIP_E_COMM = -5
+
+# sfmhip_allgather element types (include/sfmhip.h SFMHIP_DT_*)
+DT_INT8, DT_UINT8, DT_INT16, DT_INT32, DT_INT64, DT_FLOAT32, DT_FLOAT64 = range(7)
+DT_OF = {torch.int8: DT_INT8, torch.uint8: DT_UINT8, torch.int16: DT_INT16, torch.int32: DT_INT32,
+         torch.int64: DT_INT64, torch.float32: DT_FLOAT32, torch.float64: DT_FLOAT64}
 
 
 class SfmHipError(RuntimeError):
@@ -39,17 +45,23 @@ _i32 = ctypes.c_int
 _i64 = ctypes.c_int64
 _f32 = ctypes.c_float
 _f64 = ctypes.c_double
+_u64 = ctypes.c_uint64
+_sz = ctypes.c_size_t
 
 # name -> argtypes, in the order of include/sfmhip.h
 SIGNATURES = {
     "sfmhip_version": [],
     "sfmhip_last_error": [],
     "sfmhip_device_arch": [ctypes.c_char_p, _i32],
+    "sfmhip_scratch_trim": [_u64],
     "sfmhip_desc_quantize": [_p, _i32, _i32, _i32, _p, _i32, _p, _p],
     "sfmhip_desc_prepare": [_p, _i32, _i32, _i32, _p, _p, _p, _p],
     "sfmhip_desc_prepare_shifted": [_p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p],
     "sfmhip_match_pairs": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p],
     "sfmhip_mutual_filter": [_p, _p, _i32, _i32, _p],
+    "sfmhip_desc_residual": [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p],
+    "sfmhip_match_pairs_exact": [_p, _p, _p, _p, _p, _p, _p, _i32, _p, _i32, _i32, _i32, _p, _i32, _i32, _i32,
+                                 _p, _p, _p, _p, _p],
     "sfmhip_vq": [_p, _i64, _p, _i32, _i32, _p, _p, _p],
     "sfmhip_word_histogram": [_p, _p, _i32, _i32, _p, _p],
     "sfmhip_kmeans_update": [_p, _i64, _i32, _p, _i32, _p, _p, _p],
@@ -61,6 +73,7 @@ SIGNATURES = {
     "sfmhip_voxel_traversal_count": [_p, _i64, _f32, _i32, _p, _p],
     "sfmhip_voxel_traversal": [_p, _i64, _f32, _i32, _p, _p],
     "sfmhip_grid_sample": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i64, _p, _p],
+    "sfmhip_nerf_forward": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _i64, _p, _p, _p],
     "sfmhip_grid_to_voxel_major": [_p, _i32, _i32, _i32, _i32, _p, _p],
     "sfmhip_render_rays": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _i64, _i32, _p, _p],
     "sfmhip_tsdf_integrate": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p,
@@ -69,6 +82,7 @@ SIGNATURES = {
     "sfmhip_tsdf_integrate_tab": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p,
                                   _f32, _p, _p],
     "sfmhip_tsdf_cull_stats": [_i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p, _f32, _p, _p],
+    "sfmhip_tsdf_layer_stats": [_i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p, _f32, _p, _p],
     "sfmhip_find_essential": [_p, _p, _p, _i32, _p, _f64, _f64, _i32, _p, _p, _p, _p, _p, _p, _p],
     "sfmhip_recover_pose": [_p, _i64, _p, _p, _p, _i32, _p, _p, _f64, _p, _p, _p, _p, _p],
     "sfmhip_pnp_ransac": [_p, _p, _p, _i32, _p, _i32, _f64, _f64, _p, _p, _p, _p, _p, _p, _p, _p],
@@ -79,6 +93,14 @@ SIGNATURES = {
     "sfmhip_ray_aabb": [_p, _p, _i64, _p, _p, _p, _p, _p, _p],
     "sfmhip_stratified_samples": [_p, _p, _p, _i64, _i32, _i32, _p, _p],
     "sfmhip_debug_ransac_prof": [_p],
+    "sfmhip_comm_unique_id": [_p],
+    "sfmhip_comm_init_rank": [_i32, _p, _i32, _p],
+    "sfmhip_comm_init_all": [_i32, _p, _p],
+    "sfmhip_comm_info": [_p, _p, _p, _p],
+    "sfmhip_allgather": [_p, _p, _p, _sz, _i32, _p],
+    "sfmhip_comm_group_start": [],
+    "sfmhip_comm_group_end": [],
+    "sfmhip_comm_destroy": [_p],
 }
 
 

@@ -42,11 +42,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
-// Stream-ordered scratch (hipMallocAsync from the device's default pool).  The
-// first use on a device raises that pool's release threshold so freed scratch
-// stays mapped between calls instead of going back to the driver at every
-// synchronisation (C5 TSDF: 2.32 -> 2.14 ms per call; tools/tsdf_call_gap.py).
-// The PyTorch caching allocator does not use this pool.
+// Stream-ordered scratch from a library-owned memory pool per device (lib.hip):
+// freed scratch (up to 1 GiB) stays mapped between calls instead of going back
+// to the driver at every synchronisation (C5 TSDF: 2.32 -> 2.14 ms per call;
+// tools/tsdf_call_gap.py); sfmhip_scratch_trim releases it.
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 
 }  // namespace sfmhip

@@ -168,15 +168,52 @@ template <> struct Mfma<16> {
     __device__ static int row(int q, int grp) { return 4 * grp + q; }
 };
 
+// ---------------------------------------------------------------------------
+// Exact float mode (SURVEY.md §7 hard part 1: an int8 candidate pass with an
+// exact re-score).  Float descriptors x are matched through their int8
+// quantisation q with a rigorous bound on the quantisation residual:
+//   x = v(q) + delta,  v(q) = q / 127 (MODE_FLOAT) or q + 128 (MODE_SIFT),
+//   | |x_a - x_b| - |v_a - v_b| | <= |delta_a| + |delta_b| =: E    (triangle inequality)
+// with |v_a - v_b| = sqrt(D) / s (D the matcher's exact integer distance, s =
+// 127 or 1).  The order statistics obey the same bound, so from the matcher's
+// (D1, D2) a row is decided without the floats when the bound settles it:
+//   reject  if  den^2 * lo(d1) >= num^2 * hi(d2)
+//   accept  if  hi(d1) < lo(d2)  (unique winner = the int8 winner)  and  den^2 hi(d1) < num^2 lo(d2)
+// where lo/hi bound the reference distance d = sum_k (x_ak - x_bk)^2 as the
+// oracle evaluates it in f64 (relative error <= (d + 2) 2^-53 < 1e-13 for
+// d <= 256, covered by the 1e-12 widening; the sqrt/scale/sum roundings by the
+// 2^-50 operand margins).  Undecided rows are marked -(3 + D2) and settled
+// exactly by match_resolve_kernel.
+struct CertArgs {
+    const double* erow;   // [n_img][m_pad] residual bound per row (desc_residual_kernel)
+    const double* eimg;   // [n_img] max over the image's rows
+    double inv_s;         // 1/127 (MODE_FLOAT) or 1 (MODE_SIFT)
+    int force;            // 1: no row is certified (every row takes the exact path; tests)
+};
+constexpr int kUndecidedBase = -3;   // matches0 = kUndecidedBase - D2 marks an undecided row
+
+// 1 accept, 0 reject, -1 undecided
+__device__ __forceinline__ int certify(int d1, int d2, double E, double inv_s, double rn2, double rd2) {
+    const double up = 1.0 + 0x1p-50, dn = 1.0 - 0x1p-50;
+    const double s1 = sqrt((double)d1) * inv_s, s2 = sqrt((double)d2) * inv_s;
+    const double a1 = fmax(s1 * dn - E * up, 0.0), b1 = (s1 + E) * up;
+    const double a2 = fmax(s2 * dn - E * up, 0.0), b2 = (s2 + E) * up;
+    const double wl = 1.0 - 1e-12, wh = 1.0 + 1e-12;
+    const double lo1 = a1 * a1 * wl, hi1 = b1 * b1 * wh, lo2 = a2 * a2 * wl, hi2 = b2 * b2 * wh;
+    if (rd2 * lo1 >= rn2 * hi2) return 0;
+    if (hi1 < lo2 && rd2 * hi1 < rn2 * lo2) return 1;
+    return -1;
+}
+
 // One workgroup = one pair x (WAVES * NS * MF) query rows of image a.  Each
 // wave owns NS column tiles of MF query rows as resident B-operand fragments
 // and streams image b's 128-row blocks from the LDS ring (LDS-DMA filled).
-template <int D, int MF, int NS, int WAVES>
+template <int D, int MF, int NS, int WAVES, bool CERT = false>
 __global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
     const int8_t* __restrict__ desc, const int32_t* __restrict__ norms,
     const int32_t* __restrict__ keys, const int32_t* __restrict__ nk, int m_pad,
     const int32_t* __restrict__ pairs, int n_iblk, int nwg, long long rn2, long long rd2,
-    int32_t* __restrict__ m0, int32_t* __restrict__ dist1, int32_t* __restrict__ dist2) {
+    int32_t* __restrict__ m0, int32_t* __restrict__ dist1, int32_t* __restrict__ dist2, CertArgs ca) {
     using S = Stager<D, WAVES>;
     using M = Mfma<MF>;
     using acc_t = typename M::acc_t;
@@ -302,7 +339,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
             const int na = norms[(size_t)a * m_pad + i];
             d1 = na - g1k[s];
             d2 = na - g2k[s];
-            if (rd2 * (long long)d1 < rn2 * (long long)d2) res = g1i[s];
+            if (CERT) {
+                const int v = ca.force ? -1
+                                       : certify(d1, d2, ca.erow[(size_t)a * m_pad + i] + ca.eimg[b], ca.inv_s,
+                                                 (double)rn2, (double)rd2);
+                res = v > 0 ? g1i[s] : (v == 0 ? -1 : kUndecidedBase - d2);
+            } else if (rd2 * (long long)d1 < rn2 * (long long)d2) {
+                res = g1i[s];
+            }
         }
         out_m[i] = res;
         if (dist1) dist1[(size_t)pair * m_pad + i] = d1;
@@ -569,6 +613,16 @@ __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
 // on ties) — on integer data every value involved is exact, so codes and distances
 // are scipy's bit for bit; on floats the decided argmins are the exact ones.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// Absolute part of the f32 filter's error bound: an input, product or norm that
+// lands in (or is flushed from) the f32 subnormal range carries an absolute
+// error up to 2^-126 times the other factor, whatever the relative bound says
+// (data scaled to ~1e-21).  Per product <= 2^-126 (|c_k| + |x_k| + 1); summed
+// over DP products, times 2 in the score, plus the norm:
+// <= 2^-126 (2 sqrt(DP) (cmax + |x|) + 2 DP + 4).  Scores closer than that go
+// to the exact f64 pass.
+__device__ __forceinline__ double vq_eps_abs(int DP, double xn, double cmax) {
+    return 0x1p-126 * (2.0 * sqrt((double)DP) * (cmax + xn) + 2.0 * DP + 4.0) * 1.01;
+}
 constexpr int kVqfWaves = 12;
 constexpr int kVqfTile = kVqfWaves * 32;   // observations per tile (32 per wave)
 __global__ __launch_bounds__(kVqfWaves * 64) void vq_f32f_kernel(const double* __restrict__ obs, int64_t n_obs,
@@ -661,7 +715,8 @@ __global__ __launch_bounds__(kVqfWaves * 64) void vq_f32f_kernel(const double* _
                 }
                 const int row = 4 * kq + g;
                 const double xr = __shfl(xn[h], row);   // lane `row` (group 0) holds |x|^2 of that row
-                const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax);
+                const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax) +
+                                   vq_eps_abs(DP, sqrt(xr), cmax);
                 if (r16 == 0) s_win[wave][16 * h + row] = ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
             }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -849,7 +904,8 @@ __global__ __launch_bounds__(WAVES * 64) void vq_f32r_kernel(const double* __res
                 x1 = t ? ox : x1;
             }
             const double xr = __shfl(xn, 4 * kq + g);   // lane 4kq+g holds |x|^2 of that row
-            const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax);
+            const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax) +
+                               vq_eps_abs(DP, sqrt(xr), cmax);
             win[g] = ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
         }
         int w = -1;   // row r16's verdict: group r16 >> 2, entry r16 & 3
@@ -912,6 +968,182 @@ __global__ __launch_bounds__(256) void vq_exact_kernel(const double* __restrict_
         if (lane == 0) {
             codes[o] = bi;
             dist[o] = sqrt(best);
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Exact float mode, part 1: per-row residual bounds E_row >= |x - v(q)| (f64,
+// outward margins: the sum of squares and sqrt carry <= d 2^-53 relative, the
+// computed components <= 2^-52 (|x| + |v|) absolute) and E_img = max per image
+// (non-negative doubles order as their bit patterns).  A non-finite row gets
+// +inf: every match it takes part in goes to the exact path.  One wave per row.
+__global__ __launch_bounds__(256) void desc_residual_kernel(const float* __restrict__ x, const int8_t* __restrict__ q,
+                                                            int n_rows, int m_pad, int d, const int32_t* __restrict__ nk,
+                                                            int mode, double* __restrict__ erow,
+                                                            unsigned long long* __restrict__ eimg) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n_rows) return;
+    const int img = row / m_pad, r = row % m_pad;
+    if (r >= nk[img]) {
+        if (lane == 0) erow[row] = 0.0;
+        return;
+    }
+    const float* xr = x + (size_t)row * d;
+    const int8_t* qr = q + (size_t)row * d;
+    double s2 = 0.0, x2 = 0.0, v2 = 0.0;
+    bool finite = true;
+    for (int k = lane; k < d; k += 64) {
+        const float xf = xr[k];
+        const double xv = (double)xf;
+        const double v = mode == 0 ? (double)((int)qr[k] + 128) : (double)qr[k] / 127.0;
+        const double dl = xv - v;
+        s2 = __builtin_fma(dl, dl, s2);
+        x2 = __builtin_fma(xv, xv, x2);
+        v2 = __builtin_fma(v, v, v2);
+        finite = finite && __builtin_isfinite(xf);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        s2 += __shfl_xor(s2, off);
+        x2 += __shfl_xor(x2, off);
+        v2 += __shfl_xor(v2, off);
+    }
+    const bool all_finite = __all(finite);
+    if (lane == 0) {
+        const double e = all_finite ? sqrt(s2) * (1.0 + 0x1p-40) + 0x1p-50 * (sqrt(x2) + sqrt(v2)) * (1.0 + 0x1p-40)
+                                    : __builtin_inf();
+        erow[row] = e;
+        atomicMax(eimg + img, (unsigned long long)__double_as_longlong(e));
+    }
+}
+
+// Exact float mode, part 2: every row the certificate left undecided
+// (matches0 <= kUndecidedBase, carrying the int8 second-best D2) is settled
+// against the f32 descriptors, one wave per row, with the oracle's arithmetic:
+//   d(i,j) = sum_k (f64(x_ak) - f64(x_bj,k))^2, one IEEE op per step in k order
+//   j1 = lowest index attaining min d, d2 = min over j != j1,
+//   accept iff den^2 d1 < num^2 d2 exactly (two-product comparison).
+// Candidates: only j whose int8 distance D_j can still reach the top two,
+//   sqrt(D_j) <= s E + (sqrt(D2) + s E) (1 + 1e-12)  (E = E_row[a,i] + E_img[b]),
+// found with v_dot4 over the int8 rows; the f64 distances are evaluated for
+// those (at most kResolveCap, else for every j).  A persistent scan over the
+// match graph finds the marked rows (grid-stride over 64-row chunks).
+constexpr int kResolveCap = 512;
+template <int D>
+__global__ __launch_bounds__(256) void match_resolve_kernel(const int8_t* __restrict__ q, const float* __restrict__ x,
+                                                            const int32_t* __restrict__ nk, int m_pad,
+                                                            const int32_t* __restrict__ pairs, int P,
+                                                            const double* __restrict__ erow,
+                                                            const double* __restrict__ eimg, double s, double rn2,
+                                                            double rd2, int32_t* __restrict__ m0,
+                                                            unsigned* __restrict__ n_resolved) {
+    constexpr int W4 = D / 4;
+    __shared__ float sxa[4][D];
+    __shared__ __attribute__((aligned(16))) int sqa[4][W4];
+    __shared__ int scand[4][kResolveCap];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t total = (int64_t)P * m_pad;
+    const int64_t nchunk = (total + 63) >> 6;
+    for (int64_t c = (int64_t)blockIdx.x * 4 + wave; c < nchunk; c += (int64_t)gridDim.x * 4) {
+        const int64_t e0 = c << 6;
+        const int v = (e0 + lane < total) ? m0[e0 + lane] : -1;
+        unsigned long long bal = __ballot(v <= kUndecidedBase);
+        while (bal) {
+            const int l = __builtin_ctzll(bal);
+            bal &= bal - 1;
+            const int mark = __shfl(v, l);
+            const int64_t e = e0 + l;
+            const int pair = (int)(e / m_pad), i = (int)(e % m_pad);
+            const int a = pairs[2 * pair], b = pairs[2 * pair + 1], nb = nk[b];
+            const int d2q = kUndecidedBase - mark;
+            const size_t arow = (size_t)a * m_pad + i;
+            for (int k = lane; k < D; k += 64) sxa[wave][k] = x[arow * D + k];
+            for (int w = lane; w < W4; w += 64) sqa[wave][w] = reinterpret_cast<const int*>(q + arow * D)[w];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // |q_a|^2
+            int na = 0;
+            for (int w = lane; w < W4; w += 64) na = __builtin_amdgcn_sdot4(sqa[wave][w], sqa[wave][w], na, false);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) na += __shfl_xor(na, off);
+            const double se = (erow[arow] + eimg[b]) * s * (1.0 + 1e-12);
+            const double bq = (se + (sqrt((double)d2q) + se) * (1.0 + 1e-12)) * (1.0 + 1e-12);
+            const double tq = floor(bq * bq) + 1.0;   // every j with D_j <= tq may reach the top two
+            int ncand = 0;
+            for (int j0 = 0; j0 < nb; j0 += 64) {
+                const int j = j0 + lane;
+                bool in = false;
+                if (j < nb) {
+                    const int4* qb = reinterpret_cast<const int4*>(q + ((size_t)b * m_pad + j) * D);
+                    int dot = 0, nbn = 0;
+#pragma unroll 4
+                    for (int w4 = 0; w4 < W4 / 4; ++w4) {
+                        const int4 t = qb[w4];
+                        const int4 u = reinterpret_cast<const int4*>(sqa[wave])[w4];
+                        dot = __builtin_amdgcn_sdot4(t.x, u.x, dot, false);
+                        dot = __builtin_amdgcn_sdot4(t.y, u.y, dot, false);
+                        dot = __builtin_amdgcn_sdot4(t.z, u.z, dot, false);
+                        dot = __builtin_amdgcn_sdot4(t.w, u.w, dot, false);
+                        nbn = __builtin_amdgcn_sdot4(t.x, t.x, nbn, false);
+                        nbn = __builtin_amdgcn_sdot4(t.y, t.y, nbn, false);
+                        nbn = __builtin_amdgcn_sdot4(t.z, t.z, nbn, false);
+                        nbn = __builtin_amdgcn_sdot4(t.w, t.w, nbn, false);
+                    }
+                    in = (double)((long long)na + nbn - 2LL * dot) <= tq;
+                }
+                const unsigned long long cb = __ballot(in);
+                const int pos = ncand + __popcll(cb & ((1ull << lane) - 1ull));
+                if (in && pos < kResolveCap) scand[wave][pos] = j;
+                ncand += __popcll(cb);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const bool every = ncand > kResolveCap;
+            const int nc = every ? nb : ncand;
+            double v1 = __builtin_inf(), v2 = __builtin_inf();
+            int j1 = INT_MAX;
+            for (int t = lane; t < nc; t += 64) {   // ascending j per lane
+                const int j = every ? t : scand[wave][t];
+                const float4* xb = reinterpret_cast<const float4*>(x + ((size_t)b * m_pad + j) * D);
+                double acc = 0.0;
+                for (int k4 = 0; k4 < D / 4; ++k4) {
+                    const float4 xv = xb[k4];
+                    double df;
+                    df = (double)sxa[wave][4 * k4] - (double)xv.x;
+                    acc = acc + df * df;
+                    df = (double)sxa[wave][4 * k4 + 1] - (double)xv.y;
+                    acc = acc + df * df;
+                    df = (double)sxa[wave][4 * k4 + 2] - (double)xv.z;
+                    acc = acc + df * df;
+                    df = (double)sxa[wave][4 * k4 + 3] - (double)xv.w;
+                    acc = acc + df * df;
+                }
+                if (acc < v1) { v2 = v1; v1 = acc; j1 = j; }
+                else if (acc < v2) v2 = acc;
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                const double o1 = __shfl_xor(v1, off), o2 = __shfl_xor(v2, off);
+                const int oj = __shfl_xor(j1, off);
+                const bool mine = v1 < o1 || (v1 == o1 && j1 < oj);
+                const double n2 = mine ? fmin(v2, o1) : fmin(o2, v1);
+                if (!mine) { v1 = o1; j1 = oj; }
+                v2 = n2;
+            }
+            // den^2 d1 < num^2 d2, exactly: (p, e) two-products compare lexicographically (RN is monotone)
+            const double p1 = rd2 * v1, e1 = __builtin_fma(rd2, v1, -p1);
+            const double p2 = rn2 * v2, e2 = __builtin_fma(rn2, v2, -p2);
+            const bool acc_ok = p1 < p2 || (p1 == p2 && e1 < e2);
+            if (lane == 0) {
+                m0[e] = acc_ok ? j1 : -1;
+                if (n_resolved) atomicAdd(n_resolved, 1u);
+            }
+            __builtin_amdgcn_wave_barrier();   // LDS rows reused by the next marked row
         }
     }
 }
@@ -1024,7 +1256,7 @@ extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, cons
     hipStream_t s = as_stream(stream);
 #define SFMHIP_LAUNCH_MATCH(DD, MF, NS, WW)                                                              \
     hipLaunchKernelGGL((match_kernel<DD, MF, NS, WW>), dim3(nwg), dim3(64 * WW), 0, s, desc, norms, keys, \
-                       n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2)
+                       n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2, CertArgs{})
 #define SFMHIP_LAUNCH_D(DD)                                        \
     switch (variant) {                                             \
         case 1: SFMHIP_LAUNCH_MATCH(DD, 32, 2, 4); break;          \
@@ -1146,4 +1378,66 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
     hipLaunchKernelGGL(vq_kernel, dim3((int)blocks), dim3(256), shm, as_stream(stream), obs, n_obs, code_book,
                        n_codes, d, codes, dist);
     return check_launch("vq_kernel");
+}
+
+extern "C" int sfmhip_desc_residual(const float* desc_f, const int8_t* desc_q, int n_img, int m_pad, int d,
+                                    const int32_t* n_kpts, int mode, double* resid_row, double* resid_img,
+                                    void* stream) {
+    SFMHIP_REQUIRE(desc_f && desc_q && n_kpts && resid_row && resid_img, "sfmhip_desc_residual: null pointer");
+    SFMHIP_REQUIRE(n_img > 0 && m_pad > 0 && d > 0, "sfmhip_desc_residual: bad shape");
+    SFMHIP_REQUIRE(mode == 0 || mode == 1, "sfmhip_desc_residual: mode must be 0 or 1");
+    const int64_t rows = (int64_t)n_img * m_pad;
+    SFMHIP_REQUIRE(rows < INT_MAX, "sfmhip_desc_residual: too many rows");
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(resid_img, 0, (size_t)n_img * sizeof(double), s) != hipSuccess) return check_launch("memset");
+    hipLaunchKernelGGL(desc_residual_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, s, desc_f, desc_q, (int)rows, m_pad,
+                       d, n_kpts, mode, resid_row, reinterpret_cast<unsigned long long*>(resid_img));
+    return check_launch("desc_residual_kernel");
+}
+
+extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                                        const int8_t* desc_q, const float* desc_f, const double* resid_row,
+                                        const double* resid_img, int mode, const int32_t* n_kpts, int n_img,
+                                        int m_pad, int d, const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                                        int32_t* matches0, int32_t* dist1, int32_t* dist2, uint32_t* n_resolved,
+                                        void* stream) {
+    SFMHIP_REQUIRE(desc && norms && keys && desc_q && desc_f && resid_row && resid_img && n_kpts && pairs && matches0,
+                   "sfmhip_match_pairs_exact: null pointer");
+    SFMHIP_REQUIRE(n_img > 0 && P >= 0, "sfmhip_match_pairs_exact: bad counts");
+    SFMHIP_REQUIRE(m_pad > 0 && m_pad % kJB == 0, "sfmhip_match_pairs_exact: m_pad must be a positive multiple of 128");
+    SFMHIP_REQUIRE(mode == 0 || mode == 1, "sfmhip_match_pairs_exact: mode must be 0 or 1");
+    SFMHIP_REQUIRE(ratio_num > 0 && ratio_den > 0 && ratio_num <= 65535 && ratio_den <= 65535,
+                   "sfmhip_match_pairs_exact: ratio must be a positive fraction");
+    if (P == 0) return SFMHIP_OK;
+    constexpr int IB = 256;   // the default variant's query rows per workgroup (16x16 tiles, 4 per wave, 4 waves)
+    const int n_iblk = ceil_div(m_pad, IB);
+    const int64_t nwg64 = (int64_t)P * n_iblk;
+    SFMHIP_REQUIRE(nwg64 < INT_MAX, "sfmhip_match_pairs_exact: too many pairs for one launch");
+    const int nwg = (int)nwg64;
+    const long long rn2 = (long long)ratio_num * ratio_num, rd2 = (long long)ratio_den * ratio_den;
+    const char* cenv = std::getenv("SFMHIP_MATCH_CERT");   // 0: every row through the exact pass (tests)
+    const CertArgs ca{resid_row, resid_img, mode == 0 ? 1.0 : 1.0 / 127.0, (cenv && std::atoi(cenv) == 0) ? 1 : 0};
+    hipStream_t s = as_stream(stream);
+    int dev = 0, n_cu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t nchunk = ((int64_t)P * m_pad + 63) / 64;
+    const int rgrid = (int)std::min<int64_t>((nchunk + 3) / 4, (int64_t)n_cu * 8);
+    if (n_resolved && hipMemsetAsync(n_resolved, 0, sizeof(uint32_t), s) != hipSuccess) return check_launch("memset");
+#define SFMHIP_LAUNCH_EXACT(DD)                                                                                  \
+    hipLaunchKernelGGL((match_kernel<DD, 16, 4, 4, true>), dim3(nwg), dim3(256), 0, s, desc, norms, keys, n_kpts, \
+                       m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2, ca);                         \
+    if (int rc = check_launch("match_kernel<cert>")) return rc;                                                   \
+    hipLaunchKernelGGL((match_resolve_kernel<DD>), dim3(rgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts, m_pad,   \
+                       pairs, P, resid_row, resid_img, mode == 0 ? 1.0 : 127.0, (double)rn2, (double)rd2,        \
+                       matches0, n_resolved)
+    switch (d) {
+        case 64: SFMHIP_LAUNCH_EXACT(64); break;
+        case 128: SFMHIP_LAUNCH_EXACT(128); break;
+        case 256: SFMHIP_LAUNCH_EXACT(256); break;
+        default:
+            set_error("sfmhip_match_pairs_exact: descriptor dim %d not in {64,128,256}", d);
+            return SFMHIP_E_UNSUPPORTED;
+    }
+#undef SFMHIP_LAUNCH_EXACT
+    return check_launch("match_resolve_kernel");
 }

@@ -389,6 +389,51 @@ __global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ g
     }
 }
 
+// NerfModel.forward (plenoxel.py:31-43): the 28 channels at each point
+// (grid_sample arithmetic of grid_sample_kernel, reference layout), sigma =
+// ReLU(channel 0), colour = eval_spherical_function(channels 1..27, d); both
+// zero outside the mask.  One thread per point.
+__global__ void nerf_forward_kernel(const float* __restrict__ grid, int D, int H, int W, Bounds B, int mode,
+                                    const float* __restrict__ pts, const float* __restrict__ dirs, int64_t P,
+                                    float* __restrict__ color, float* __restrict__ sigma) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float p[3] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+    float g[3];
+    if (!normalise(p, B, mode, g)) {
+        color[3 * i] = color[3 * i + 1] = color[3 * i + 2] = 0.f;
+        sigma[i] = 0.f;
+        return;
+    }
+    Corners cn;
+    corners(g, D, H, W, cn);
+    int64_t off[8];
+    bool in[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int x, y, z;
+        in[k] = corner_in(cn, k, D, H, W, x, y, z);
+        off[k] = ((int64_t)z * H + y) * W + x;
+    }
+    const int64_t plane = (int64_t)D * H * W;
+    float v[28];
+#pragma unroll
+    for (int c = 0; c < 28; ++c) {
+        const float* gc = grid + (size_t)c * plane;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (in[k]) acc = acc + gc[off[k]] * cn.w[k];
+        v[c] = acc;
+    }
+    float col[3];
+    sh_colour(v + 1, dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], col);
+    sigma[i] = fmaxf(v[0], 0.f);
+    color[3 * i] = col[0];
+    color[3 * i + 1] = col[1];
+    color[3 * i + 2] = col[2];
+}
+
 // ---------------------------------------------------------------------------
 // V5: TSDF integration (arithmetic defined op for op in oracle/voxel.py
 // tsdf_integrate).  Bound by the per-CU texture pipeline (TA/TD ~87 % busy,
@@ -1369,6 +1414,19 @@ extern "C" int sfmhip_grid_sample(const float* grid, int C, int D, int H, int W,
     return check_launch("grid_sample_kernel");
 }
 
+extern "C" int sfmhip_nerf_forward(const float* grid, int D, int H, int W, const float* bmin, const float* bmax,
+                                   int mask_mode, const float* pts, const float* dirs, int64_t P, float* color,
+                                   float* sigma, void* stream) {
+    SFMHIP_REQUIRE(grid && bmin && bmax && pts && dirs && color && sigma, "sfmhip_nerf_forward: null pointer");
+    SFMHIP_REQUIRE(D > 0 && H > 0 && W > 0 && P >= 0, "sfmhip_nerf_forward: bad shape");
+    SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_nerf_forward: mask_mode must be 0 or 1");
+    if (P == 0) return SFMHIP_OK;
+    const Bounds bb = make_bounds(bmin, bmax);
+    hipLaunchKernelGGL(nerf_forward_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, as_stream(stream), grid, D, H, W, bb,
+                       mask_mode, pts, dirs, P, color, sigma);
+    return check_launch("nerf_forward_kernel");
+}
+
 extern "C" int sfmhip_grid_to_voxel_major(const float* grid, int C, int D, int H, int W, float* grid_vm,
                                           void* stream) {
     SFMHIP_REQUIRE(grid && grid_vm, "sfmhip_grid_to_voxel_major: null pointer");
@@ -1397,7 +1455,7 @@ extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, con
 // whole image ([F][nbv][nbu] float2, sfmhip_tsdf_block_table); the block pass is skipped.
 static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, const float* depth, int F, int Hd,
                     int Wd, const float* poses, const float* Kf, const float* bmin, const float* bmax, float trunc,
-                    void* stream, int64_t* stats, const float2* ext_table) {
+                    void* stream, int64_t* stats, const float2* ext_table, int64_t* layer_stats = nullptr) {
     SFMHIP_REQUIRE(T && Wt && depth && poses && Kf && bmin && bmax, "sfmhip_tsdf_integrate: null pointer");
     SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && F >= 0 && Hd > 0 && Wd > 0, "sfmhip_tsdf_integrate: bad shape");
     SFMHIP_REQUIRE(0 <= z0 && z0 <= z1 && z1 <= D, "sfmhip_tsdf_integrate: bad z range");
@@ -1538,9 +1596,18 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             for (size_t i = 0; i < mc.size(); ++i) {
                 const int nb = std::min(32, nf - 32 * (int)(i % nwf));
                 const unsigned live = nb >= 32 ? ~0u : ((1u << nb) - 1u);
-                stats[0] += nb;
-                stats[1] += __builtin_popcount(mc[i] & live);
-                stats[2] += __builtin_popcount(mf[i] & live & ~mc[i]);
+                const int tested = nb, culled = __builtin_popcount(mc[i] & live);
+                const int fre = __builtin_popcount(mf[i] & live & ~mc[i]);
+                stats[0] += tested;
+                stats[1] += culled;
+                stats[2] += fre;
+                if (layer_stats) {   // slot = tile * kCullSub + wave, tile = (tz * nby + ty) * nbx + tx
+                    const int64_t tile = (int64_t)(i / nwf) / kCullSub;
+                    int64_t* ls = layer_stats + 3 * (tile / ((int64_t)nbx * nby));
+                    ls[0] += tested;
+                    ls[1] += culled;
+                    ls[2] += fre;
+                }
             }
             continue;
         }
@@ -1622,6 +1689,18 @@ extern "C" int sfmhip_tsdf_cull_stats(int D, int H, int W, int z0, int z1, const
     float dummy = 0.f;   // the grids are not touched
     return tsdf_run(&dummy, &dummy, D, H, W, z0, z1, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, stats,
                     nullptr);
+}
+
+extern "C" int sfmhip_tsdf_layer_stats(int D, int H, int W, const float* depth, int F, int Hd, int Wd,
+                                       const float* poses, const float* Kf, const float* bmin, const float* bmax,
+                                       float trunc, int64_t* layer_stats, void* stream) {
+    SFMHIP_REQUIRE(layer_stats, "sfmhip_tsdf_layer_stats: null pointer");
+    const int nl = ceil_div(std::max(D, 0), kTsdfTZ);
+    for (int i = 0; i < 3 * nl; ++i) layer_stats[i] = 0;
+    int64_t tot[3] = {0, 0, 0};
+    float dummy = 0.f;   // the grids are not touched
+    return tsdf_run(&dummy, &dummy, D, H, W, 0, D, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, tot,
+                    nullptr, layer_stats);
 }
 
 extern "C" int sfmhip_grid_from_voxel_major(const float* grid_vm, int C, int D, int H, int W, float* grid,

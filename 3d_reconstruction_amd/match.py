@@ -13,10 +13,18 @@ Drop-in surfaces:
 * :func:`vq` — ``scipy.cluster.vq.vq`` signature (``matching.py:27``).
 
 Semantics of the BF matcher are build-defined (the reference has no BF
-matcher) and pinned by ``oracle/match.py``: exact integer squared-L2 on int8
-descriptors, best index = lowest on ties, Lowe ratio test
-``den^2 * d1 < num^2 * d2`` evaluated exactly, optional mutual check with
-LightGlue's ``filter_matches`` semantics (``lightglue/lightglue.py:235-254``).
+matcher) and pinned by ``oracle/match.py``: best index = lowest on ties, Lowe
+ratio test ``den^2 * d1 < num^2 * d2`` evaluated exactly, optional mutual
+check with LightGlue's ``filter_matches`` semantics
+(``lightglue/lightglue.py:235-254``).  Two distance definitions:
+
+* quantised (default for ``DescriptorBank``): exact integer squared L2 of the
+  int8 quantisation (SIFT: q = x - 128; float: q = rint(127 x));
+* exact float (``exact=True``; default for :class:`Matcher`, which receives
+  the float DISK / SuperPoint descriptors of matching.py:111-122): squared L2
+  of the f32 descriptors summed in f64 in k order.  The int8 MFMA pass runs
+  with a proven bound on the quantisation residual and certifies most rows;
+  the rest are re-scored exactly (DESIGN.md "exact float mode").
 """
 from __future__ import annotations
 
@@ -53,7 +61,8 @@ class DescriptorBank:
     ``[n_img][m_pad]`` (DESIGN.md "packed key").
     """
 
-    def __init__(self, q: torch.Tensor, n_kpts: torch.Tensor):
+    def __init__(self, q: torch.Tensor, n_kpts: torch.Tensor, x: torch.Tensor | None = None,
+                 mode: int = MODE_FLOAT):
         require_gpu()
         if q.dtype != torch.int8 or q.dim() != 3:
             raise ValueError("q must be an int8 tensor [n_img, m_pad, d]")
@@ -87,12 +96,36 @@ class DescriptorBank:
         else:
             call("sfmhip_desc_prepare", ptr(self.q), self.n_img, self.m_pad, self.d, ptr(self.n_kpts),
                  ptr(self.norms), ptr(self.keys), stream_ptr())
+        # exact float mode: the f32 descriptors and the per-row residual bounds
+        self.mode = int(mode)
+        self.x = None
+        self.last_resolved = None
+        if x is not None:
+            if x.dtype != torch.float32 or tuple(x.shape) != tuple(self.q.shape):
+                raise ValueError("x must be float32 of the bank's shape [n_img, m_pad, d]")
+            self.x = x.contiguous()
+            self.erow = torch.empty((self.n_img, self.m_pad), dtype=torch.float64, device=q.device)
+            self.eimg = torch.empty(self.n_img, dtype=torch.float64, device=q.device)
+            call("sfmhip_desc_residual", ptr(self.x), ptr(self.q), self.n_img, self.m_pad, self.d, ptr(self.n_kpts),
+                 self.mode, ptr(self.erow), ptr(self.eimg), stream_ptr())
+            self._nres = torch.zeros(1, dtype=torch.int32, device=q.device)
+
+    @property
+    def device(self) -> torch.device:
+        return self.q.device
+
+    @property
+    def exact(self) -> bool:
+        """True when the bank holds the float descriptors (exact float mode available)."""
+        return self.x is not None
 
     # -- construction -------------------------------------------------------
     @classmethod
-    def from_float(cls, desc, n_kpts=None, mode: int = MODE_FLOAT) -> "DescriptorBank":
+    def from_float(cls, desc, n_kpts=None, mode: int = MODE_FLOAT, exact: bool = False) -> "DescriptorBank":
         """``desc``: f32 [n_img, M, d] array/tensor or a list of (K_i, d) arrays
-        (the ``all_descriptors.npy`` object-array format, ``feature_extraction.py:50``)."""
+        (the ``all_descriptors.npy`` object-array format, ``feature_extraction.py:50``).
+        ``exact``: keep the f32 descriptors for the exact float mode (finite
+        values required; padding rows are zeroed)."""
         d0 = require_gpu()
         if isinstance(desc, (list, tuple)) or (isinstance(desc, np.ndarray) and desc.dtype == object):
             rows = [dev(r, torch.float32) for r in desc]
@@ -115,17 +148,29 @@ class DescriptorBank:
         x = x.contiguous()
         q = torch.empty((n_img, m_pad, d), dtype=torch.int8, device=d0)
         call("sfmhip_desc_quantize", ptr(x), n_img, m_pad, d, ptr(nk), int(mode), ptr(q), stream_ptr())
-        return cls(q, nk)
+        if not exact:
+            return cls(q, nk)
+        valid = torch.arange(m_pad, device=d0)[None, :] < nk[:, None].long()
+        x = torch.where(valid[:, :, None], x, torch.zeros((), dtype=x.dtype, device=d0)).contiguous()
+        if not bool(torch.isfinite(x).all()):
+            raise ValueError("exact matching needs finite descriptors")
+        return cls(q, nk, x=x, mode=mode)
 
     # -- matching ------------------------------------------------------------
     def match(self, pairs, ratio=0.75, mutual: bool = False, with_dist: bool = False,
-              out: torch.Tensor | None = None):
+              out: torch.Tensor | None = None, exact: bool | None = None):
         """Match every pair (a, b): for each row of a, its ratio-tested nearest row of b.
 
         Returns ``matches0`` int32 [P, m_pad] on the device (-1 = no match); with
-        ``with_dist`` also int32 squared distances ``dist1``, ``dist2``; with
-        ``mutual`` also the backward ``matches1`` after the mutual filter.
+        ``with_dist`` also int32 squared distances ``dist1``, ``dist2`` (of the
+        int8 quantisation); with ``mutual`` also the backward ``matches1``
+        after the mutual filter.  ``exact`` (default: the bank's mode) selects
+        the exact float distance (module docstring).
         """
+        exact = self.exact if exact is None else bool(exact)
+        if exact and self.x is None:
+            raise ValueError("exact float matching needs a bank built with from_float(..., exact=True)")
+        self._exact_now = exact
         num, den = _ratio(ratio)
         pr = dev(pairs, torch.int32).reshape(-1, 2)
         P = pr.shape[0]
@@ -143,7 +188,14 @@ class DescriptorBank:
         call("sfmhip_mutual_filter", ptr(m0), ptr(m1), P, self.m_pad, stream_ptr())
         return (m0, m1, d1, d2, e1, e2) if with_dist else (m0, m1)
 
-    def _launch(self, pr, num, den, m0, d1, d2):
+    def _launch(self, pr, num, den, m0, d1, d2, exact: bool | None = None):
+        exact = getattr(self, "_exact_now", False) if exact is None else exact
+        if exact:
+            call("sfmhip_match_pairs_exact", ptr(self.qm), ptr(self.norms), ptr(self.keys), ptr(self.q), ptr(self.x),
+                 ptr(self.erow), ptr(self.eimg), self.mode, ptr(self.n_kpts), self.n_img, self.m_pad, self.d,
+                 ptr(pr), int(pr.shape[0]), num, den, ptr(m0), ptr(d1), ptr(d2), ptr(self._nres), stream_ptr())
+            self.last_resolved = self._nres
+            return
         call("sfmhip_match_pairs", ptr(self.qm), ptr(self.norms), ptr(self.keys), ptr(self.n_kpts),
              self.n_img, self.m_pad, self.d, ptr(pr), int(pr.shape[0]), num, den,
              ptr(m0), ptr(d1), ptr(d2), stream_ptr())
@@ -155,11 +207,11 @@ def all_pairs(n_img: int) -> np.ndarray:
     return np.stack([a, b], 1).astype(np.int32)
 
 
-def bf_match(desc0, desc1, ratio=0.75, mutual: bool = False, mode: int = MODE_FLOAT):
+def bf_match(desc0, desc1, ratio=0.75, mutual: bool = False, mode: int = MODE_FLOAT, exact: bool = False):
     """One pair, numpy in / numpy out: ``matches0`` int64 (M,), -1 = no match."""
     d0 = np.asarray(desc0, dtype=np.float32)
     d1 = np.asarray(desc1, dtype=np.float32)
-    bank = DescriptorBank.from_float([d0, d1], mode=mode)
+    bank = DescriptorBank.from_float([d0, d1], mode=mode, exact=exact)
     res = bank.match(np.array([[0, 1]], dtype=np.int32), ratio=ratio, mutual=mutual)
     m0 = res[0] if mutual else res
     torch.cuda.synchronize()
@@ -172,10 +224,11 @@ class Matcher(torch.nn.Module):
     ``Matcher(ratio=0.75, mutual=True, mode=MODE_FLOAT)(data)`` where ``data`` is
     ``{'image0': {'descriptors': (1,M,d), ...}, 'image1': {...}}`` as built at
     ``matching.py:107-120``.  ``matching_scores0`` = 1 - sqrt(d1/d2) (Lowe
-    margin) for matched keypoints, 0 otherwise.
+    margin of the int8 pass) for matched keypoints, 0 otherwise.  ``exact``
+    (default True): the exact float distance on the descriptors as given.
     """
 
-    default_conf = {"ratio": 0.75, "mutual": True, "mode": MODE_FLOAT}
+    default_conf = {"ratio": 0.75, "mutual": True, "mode": MODE_FLOAT, "exact": True}
 
     def __init__(self, features: str | None = None, **conf):
         super().__init__()
@@ -190,7 +243,8 @@ class Matcher(torch.nn.Module):
             raise ValueError("Matcher expects batch size 1 descriptors (1, M, d)")
         out_dev = desc0.device
         M, N = desc0.shape[1], desc1.shape[1]
-        bank = DescriptorBank.from_float([desc0[0].detach(), desc1[0].detach()], mode=self.conf["mode"])
+        bank = DescriptorBank.from_float([desc0[0].detach(), desc1[0].detach()], mode=self.conf["mode"],
+                                         exact=self.conf["exact"])
         pr = np.array([[0, 1]], dtype=np.int32)
         if self.conf["mutual"]:
             m0, m1, d1, d2, e1, e2 = bank.match(pr, ratio=self.conf["ratio"], mutual=True, with_dist=True)

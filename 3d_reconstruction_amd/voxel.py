@@ -114,6 +114,21 @@ class VoxelGrid:
              _host_ptr(self.bmax), self.mask_mode, ptr(p), p.shape[0], ptr(out), stream_ptr())
         return out
 
+    def nerf_forward(self, x: torch.Tensor, d: torch.Tensor):
+        """NerfModel.forward (plenoxel.py:31-43): (color (P,3), sigma (P,)) at
+        points x (P,3) seen along unit directions d (P,3); zero outside."""
+        if self.C != 28:
+            raise ValueError("nerf_forward needs the 28-channel SDF+SH grid")
+        p = dev(x, torch.float32).reshape(-1, 3)
+        dd = dev(d, torch.float32).reshape(-1, 3)
+        if dd.shape != p.shape:
+            raise ValueError("x and d must both be (P, 3)")
+        color = torch.empty((p.shape[0], 3), dtype=torch.float32, device=p.device)
+        sigma = torch.empty(p.shape[0], dtype=torch.float32, device=p.device)
+        call("sfmhip_nerf_forward", ptr(self.grid), self.D, self.H, self.W, _host_ptr(self.bmin), _host_ptr(self.bmax),
+             self.mask_mode, ptr(p), ptr(dd), p.shape[0], ptr(color), ptr(sigma), stream_ptr())
+        return color, sigma
+
     def get_sdf(self, points: torch.Tensor) -> torch.Tensor:
         return self.sample(points)[:, 0]
 
@@ -169,15 +184,28 @@ def tsdf_integrate(T: torch.Tensor, Wt: torch.Tensor, depth: torch.Tensor, poses
     block_table: optional (F, ceil(Hd/16), ceil(Wd/16), 2) f32 device table from
     tsdf_block_table (e.g. assembled across ranks by dist.shared_block_table);
     the result is bit-identical, the call's own pass over the depth maps skipped."""
-    require_gpu()
+    gpu = require_gpu()
     if T.dtype != torch.float32 or Wt.dtype != torch.float32 or not T.is_contiguous() or not Wt.is_contiguous():
         raise ValueError("T and Wt must be contiguous float32 device tensors")
+    if T.dim() != 3 or tuple(Wt.shape) != tuple(T.shape):
+        raise ValueError(f"T and Wt must be (D,H,W) tensors of one shape, got {tuple(T.shape)} and "
+                         f"{tuple(Wt.shape)}")
+    if T.device != gpu or Wt.device != gpu:
+        raise ValueError(f"T and Wt must live on the current HIP device {gpu}, got {T.device} / {Wt.device}")
     D, H, W = T.shape
     z1 = D if z1 is None else int(z1)
+    if not 0 <= int(z0) <= z1 <= D:
+        raise ValueError(f"z-slab [{z0}, {z1}) outside [0, {D}]")
     dp = dev(depth, torch.float32)
     ps = dev(poses, torch.float32)
     kk = dev(K, torch.float32)
+    if dp.dim() != 3:
+        raise ValueError(f"depth must be (F,Hd,Wd), got {tuple(dp.shape)}")
     F, Hd, Wd = dp.shape
+    if tuple(ps.shape) != (F, 3, 4):
+        raise ValueError(f"poses must be ({F},3,4) to match depth, got {tuple(ps.shape)}")
+    if tuple(kk.shape) != (F, 4):
+        raise ValueError(f"K must be ({F},4) to match depth, got {tuple(kk.shape)}")
     bmn, bmx = _f3(bmin), _f3(bmax)
     if block_table is None:
         call("sfmhip_tsdf_integrate", ptr(T), ptr(Wt), D, H, W, int(z0), z1, ptr(dp), F, Hd, Wd, ptr(ps), ptr(kk),
@@ -208,6 +236,33 @@ def tsdf_block_table(depth: torch.Tensor, f0: int = 0, f1: int | None = None,
         raise ValueError(f"out must be a contiguous float32 {block_table_shape(F, Hd, Wd)} tensor")
     call("sfmhip_tsdf_block_table", ptr(dp), F, Hd, Wd, int(f0), f1, ptr(out), stream_ptr())
     return out
+
+
+def tsdf_layer_stats(shape, depth: torch.Tensor, poses: torch.Tensor, K: torch.Tensor, bmin, bmax,
+                     trunc: float) -> np.ndarray:
+    """Per 8-voxel z layer of the grid `shape` = (D,H,W): (tested, culled, free)
+    counts of (wave sub-tile, frame) pairs -- what :func:`tsdf_integrate`'s
+    pre-passes decide.  Feeds dist.plan_slabs (cost-balanced z-slabs)."""
+    require_gpu()
+    D, H, W = (int(v) for v in shape)
+    dp = dev(depth, torch.float32)
+    ps = dev(poses, torch.float32)
+    kk = dev(K, torch.float32)
+    F, Hd, Wd = dp.shape
+    out = np.zeros((-(-D // 8), 3), np.int64)
+    bmn, bmx = _f3(bmin), _f3(bmax)
+    call("sfmhip_tsdf_layer_stats", D, H, W, ptr(dp), F, Hd, Wd, ptr(ps), ptr(kk), _host_ptr(bmn), _host_ptr(bmx),
+         float(trunc), out.ctypes.data, stream_ptr())
+    return out
+
+
+def tsdf_layer_cost(stats: np.ndarray, w_proj: float = 1.0, w_free: float = 0.12, w_tested: float = 0.02) -> np.ndarray:
+    """Cost model of a tile layer from :func:`tsdf_layer_stats`: projected
+    (sub-tile, frame) pairs dominate the fusion, free-space runs cost a
+    fraction, every tested pair a little (mask walk, cull test)."""
+    st = np.asarray(stats, np.float64)
+    proj = st[:, 0] - st[:, 1] - st[:, 2]
+    return w_proj * proj + w_free * st[:, 2] + w_tested * st[:, 0]
 
 
 def tsdf_cull_stats(shape, depth: torch.Tensor, poses: torch.Tensor, K: torch.Tensor, bmin, bmax, trunc: float,

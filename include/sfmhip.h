@@ -20,6 +20,7 @@
 #ifndef SFMHIP_H
 #define SFMHIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -31,11 +32,26 @@ extern "C" {
 #define SFMHIP_E_HIP        -2   /* HIP runtime error (launch / memory)        */
 #define SFMHIP_E_UNSUPPORTED -3  /* e.g. descriptor dim not in {64,128,256}    */
 #define SFMHIP_E_OVERFLOW   -4   /* a bounded loop hit its cap                 */
+#define SFMHIP_E_COMM       -5   /* RCCL reported an error                      */
+
+/* element types of sfmhip_allgather */
+#define SFMHIP_DT_INT8    0
+#define SFMHIP_DT_UINT8   1
+#define SFMHIP_DT_INT16   2
+#define SFMHIP_DT_INT32   3
+#define SFMHIP_DT_INT64   4
+#define SFMHIP_DT_FLOAT32 5
+#define SFMHIP_DT_FLOAT64 6
 
 /* ---- library ---------------------------------------------------------- */
 int         sfmhip_version(void);            /* (major<<16)|(minor<<8)|patch */
 const char* sfmhip_last_error(void);         /* thread-local message          */
 int         sfmhip_device_arch(char* buf, int len); /* "gfx950" of device 0   */
+
+/* Stream-ordered scratch comes from a library-owned memory pool per device
+ * (never the device's default pool); up to 1 GiB of freed scratch stays
+ * mapped between calls.  Trim the current device's pool to `keep` bytes.    */
+int         sfmhip_scratch_trim(uint64_t keep);
 
 /* ---- M1: brute-force L2 matching + ratio test --------------------------
  * Replaces the matcher call site matching.py:20,122-128 (LightGlue forward,
@@ -85,6 +101,32 @@ int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, const int32_t* 
  * clear every match that is not mutual, in place.                           */
 int sfmhip_mutual_filter(int32_t* matches0, int32_t* matches1, int P, int m_pad,
                          void* stream);
+
+/* Exact float mode (matching.py:111-122 feeds FLOAT DISK / SuperPoint
+ * descriptors to the matcher).  Semantics (oracle/match.py bf_match_exact):
+ * d(i,j) = sum_k (f64(x_ai,k) - f64(x_bj,k))^2 in k order, one IEEE f64 op
+ * per step; j1 = lowest index attaining the minimum, d2 = min over j != j1;
+ * accept iff ratio_den^2 * d1 < ratio_num^2 * d2 exactly.
+ * sfmhip_desc_residual: per-row bound resid_row [n_img][m_pad] >= |x - v(q)|
+ * (v(q) = q/127 for mode 1, q + 128 for mode 0; the int8 q of
+ * sfmhip_desc_quantize) and resid_img [n_img] = the image's maximum.          */
+int sfmhip_desc_residual(const float* desc_f /* [n_img][m_pad][d] */, const int8_t* desc_q, int n_img, int m_pad,
+                         int d, const int32_t* n_kpts, int mode, double* resid_row, double* resid_img,
+                         void* stream);
+
+/* The int8 MFMA pass (desc/norms/keys as for sfmhip_match_pairs, shifted or
+ * not) certifies every row whose outcome the residual bound decides; the rest
+ * are settled against desc_f (f32) by an exact pass over the int8 candidates
+ * that can still reach the top two.  matches0 is bit-identical to the exact
+ * definition above; dist1/dist2 (nullable) are the int8 pass's quantised
+ * distances; n_resolved (nullable, device uint32) = rows the exact pass
+ * settled.  desc_q = the unshifted int8 descriptors.                         */
+int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                             const int8_t* desc_q, const float* desc_f, const double* resid_row,
+                             const double* resid_img, int mode, const int32_t* n_kpts, int n_img, int m_pad, int d,
+                             const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                             int32_t* matches0, int32_t* dist1, int32_t* dist2, uint32_t* n_resolved,
+                             void* stream);
 
 /* ---- M2: scipy.cluster.vq.vq (matching.py:27, bow.py:23) ---------------
  * codes[i] = argmin_c sum_k (obs[i,k]-code[c,k])^2 (lowest index on ties),
@@ -162,6 +204,14 @@ int sfmhip_grid_sample(const float* grid, int C, int D, int H, int W,
                        const float* bmin, const float* bmax, int mask_mode,
                        const float* pts, int64_t P, float* out, void* stream);
 
+/* NerfModel.forward (plenoxel.py:31-43) for C = 28 grids in the reference
+ * layout: color [P][3] = eval_spherical_function(channels 1..27, dirs),
+ * sigma [P] = ReLU(channel 0), both zero outside the mask (mask_mode as in
+ * sfmhip_grid_sample); dirs [P][3].  bmin/bmax are HOST float[3].           */
+int sfmhip_nerf_forward(const float* grid, int D, int H, int W, const float* bmin, const float* bmax,
+                        int mask_mode, const float* pts, const float* dirs, int64_t P, float* color,
+                        float* sigma, void* stream);
+
 /* Voxel-major relayout (C,D,H,W) -> (D,H,W,Cp) with Cp = 32 (zero pad) so a
  * corner's channels are one 128-byte line; used by the fused renderer.       */
 int sfmhip_grid_to_voxel_major(const float* grid, int C, int D, int H, int W,
@@ -214,6 +264,13 @@ int sfmhip_tsdf_cull_stats(int D, int H, int W, int z0, int z1,
                            const float* poses, const float* Kf,
                            const float* bmin, const float* bmax, float trunc,
                            int64_t* stats, void* stream);
+
+/* Per-layer version for z-slab planning (multi-GPU): the same tests over the
+ * whole grid, HOST int64 layer_stats[ceil(D/8)][3] (tested, culled, free) per
+ * 8-voxel tile layer in z.  Synchronises the stream.                         */
+int sfmhip_tsdf_layer_stats(int D, int H, int W, const float* depth, int F, int Hd, int Wd,
+                            const float* poses, const float* Kf, const float* bmin, const float* bmax,
+                            float trunc, int64_t* layer_stats, void* stream);
 
 /* ---- §8f row 2: geometric verification (batched over image pairs) --------
  * cv2.findEssentialMat(pts0, pts1, K, method=cv2.RANSAC, prob=0.999,
@@ -302,6 +359,27 @@ int sfmhip_stratified_samples(const float* t_near, const float* t_far, const flo
 /* Debug: phase timers of essential_ransac_kernel (tools/prof_ransac.py); all
  * zero unless the library is built with -DSFMHIP_RANSAC_PROF.  out[16].       */
 int sfmhip_debug_ransac_prof(unsigned long long* out);
+
+/* ---- multi-GPU: the match-graph collective ---------
+ * Thin C-ABI over RCCL (resolved with dlopen at first use: the RCCL already
+ * mapped into the process, else $SFMHIP_RCCL, else /opt/rocm/lib/librccl.so.1).
+ * The reference has no distributed code; these serve the pair-sharded
+ * exhaustive matcher: every rank matches its pairs, then ONE all-gather of the
+ * fixed-size matches0 block over xGMI gives every rank the full graph.
+ *   one process per GPU: sfmhip_comm_unique_id (one rank) -> broadcast the 128
+ *     bytes -> sfmhip_comm_init_rank on every rank (current HIP device);
+ *   one process, several GPUs: sfmhip_comm_init_all(ndev, devs, comms[ndev]),
+ *     each rank's collective issued between sfmhip_comm_group_start/_end.
+ * sfmhip_allgather: `count` elements of SFMHIP_DT_* per rank from `send`,
+ * recv = nranks * count elements in rank order; asynchronous on `stream`.    */
+int sfmhip_comm_unique_id(void* id /* 128 bytes, host */);
+int sfmhip_comm_init_rank(int nranks, const void* id, int rank, void** comm);
+int sfmhip_comm_init_all(int ndev, const int* devs /* NULL = 0..ndev-1 */, void** comms /* [ndev] */);
+int sfmhip_comm_info(void* comm, int* nranks, int* rank, int* device);
+int sfmhip_allgather(void* comm, const void* send, void* recv, size_t count, int dtype, void* stream);
+int sfmhip_comm_group_start(void);
+int sfmhip_comm_group_end(void);
+int sfmhip_comm_destroy(void* comm);
 
 #ifdef __cplusplus
 }

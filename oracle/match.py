@@ -12,8 +12,20 @@ matching.py:20,122-128.  The build's semantics:
     reverse direction (lightglue/lightglue.py:241-253 mutual rule).
 Distances use float32 GEMM on integer operands: every product and partial sum
 is an integer below 2^24, so the GEMM is exact (|dot| <= 127^2*256 < 2^23).
+
+Exact float mode (bf_match_exact; the matcher receives FLOAT descriptors at
+matching.py:111-122 — DISK from feature_extraction.py:10, SuperPoint-256 in
+config C3): the same top-2 / ratio rules on
+  d(i,j) = sum_k (f64(a_ik) - f64(b_jk))^2
+accumulated in k order with one IEEE f64 operation per step (subtract, square,
+add: no FMA), and the ratio test den^2*d1 < num^2*d2 decided on those f64
+values as exact rationals.  Build-defined (no reference BF matcher); on
+integer-valued data it equals the quantised semantics above (pinned by the vq
+and filter_matches goldens), parity of the float rounding rule unpinned.
 """
 from __future__ import annotations
+
+from fractions import Fraction
 
 import numpy as np
 from scipy.cluster.vq import vq as _scipy_vq
@@ -93,6 +105,59 @@ def bf_match(desc0, desc1, ratio=0.75, mutual=False, mode=MODE_FLOAT):
     from fractions import Fraction
     fr = Fraction(str(ratio)).limit_denominator(65535)
     return bf_match_q(quantize(desc0, mode), quantize(desc1, mode), (fr.numerator, fr.denominator), mutual)
+
+
+def sq_dist_exact(xa, xb) -> np.ndarray:
+    """Exact-float-mode distance (module docstring), f64 (M, N)."""
+    A = np.asarray(xa, np.float32).astype(np.float64)
+    B = np.asarray(xb, np.float32).astype(np.float64)
+    D = np.zeros((A.shape[0], B.shape[0]))
+    for k in range(A.shape[1]):
+        t = A[:, k][:, None] - B[:, k][None, :]
+        D += t * t
+    return D
+
+
+def top2_f(D: np.ndarray):
+    """(j1, d1, d2) of a float distance matrix; j1 lowest index on ties; d2 = min over j != j1."""
+    M = D.shape[0]
+    j1 = D.argmin(1)
+    d1 = D[np.arange(M), j1]
+    D2 = D.copy()
+    D2[np.arange(M), j1] = np.inf
+    return j1, d1, D2.min(1)
+
+
+def ratio_accept_exact(d1, d2, num: int, den: int) -> np.ndarray:
+    """den^2 * d1 < num^2 * d2 on f64 values, decided as exact rationals."""
+    return np.array([Fraction(float(a)) * (den * den) < Fraction(float(b)) * (num * num)
+                     for a, b in zip(np.ravel(d1), np.ravel(d2))], dtype=bool)
+
+
+def bf_match_exact(xa, xb, ratio=(3, 4), mutual: bool = False, return_dist: bool = False):
+    """Exact-float-mode matches0 (M,) int64 for f32 descriptors xa (M,d), xb (N,d)."""
+    num, den = ratio
+    xa = np.asarray(xa, np.float32)
+    xb = np.asarray(xb, np.float32)
+    M, N = xa.shape[0], xb.shape[0]
+    if M == 0 or N < 2:
+        out = np.full(M, -1, np.int64)
+        nan = np.full(M, np.nan)
+        return (out, nan, nan) if return_dist else out
+    D = sq_dist_exact(xa, xb)
+    j1, d1, d2 = top2_f(D)
+    m0 = np.where(ratio_accept_exact(d1, d2, num, den), j1, -1).astype(np.int64)
+    if mutual:
+        j1b, d1b, d2b = top2_f(D.T)
+        m1 = np.where(ratio_accept_exact(d1b, d2b, num, den), j1b, -1)
+        keep = (m0 >= 0) & (m1[np.clip(m0, 0, None)] == np.arange(M))
+        m0 = np.where(keep, m0, -1)
+    return (m0, d1, d2) if return_dist else m0
+
+
+def bf_match_exact_mutual_pair(xa, xb, ratio=(3, 4)):
+    """(matches0, matches1) of the exact float mode after the mutual filter."""
+    return bf_match_exact(xa, xb, ratio, mutual=True), bf_match_exact(xb, xa, ratio, mutual=True)
 
 
 def vq(obs, code_book):

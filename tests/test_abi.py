@@ -49,6 +49,25 @@ def test_version_and_error_channel(sfm):
     assert rc == -1 and b"z range" in sfm.lib.sfmhip_last_error()
 
 
+def test_sfmhip_alias_and_cv2_names(sfm):
+    """`import sfmhip as cv2` binds what sfm.py / matching.py call (one import line)."""
+    import sfmhip
+    assert sfmhip is sfm
+    assert sfmhip.RANSAC == 8 and sfmhip.SOLVEPNP_ITERATIVE == 0
+    for name in ("triangulatePoints", "convertPointsFromHomogeneous", "Rodrigues", "projectPoints",
+                 "findEssentialMat", "recoverPose", "solvePnPRansac", "Matcher", "vq", "kmeans",
+                 "match_all_pairs_sharded", "RcclComm"):
+        assert callable(getattr(sfmhip, name)), name
+
+
+def test_comm_argument_errors_without_gpu(sfm):
+    """The comm entry points report argument errors without touching RCCL or a GPU."""
+    assert sfm.lib.sfmhip_comm_init_rank(0, None, 0, None) == -1
+    assert b"null pointer" in sfm.lib.sfmhip_last_error()
+    assert sfm.lib.sfmhip_allgather(None, None, None, 0, 0, None) == -1
+    assert sfm.lib.sfmhip_comm_destroy(None) == 0
+
+
 def test_product_has_no_oracle_dependency():
     """The product package must never import the oracle (no CPU fallback)."""
     pkg = os.path.join(ROOT, "3d_reconstruction_amd")

@@ -155,3 +155,129 @@ def test_shared_block_table_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert all(v is True for v in res.values()), res
+
+
+# --- the product's sharded matcher (match_all_pairs_sharded) on gloo ------------
+class _StubBank:
+    """Stands in for a DescriptorBank on the CPU: row i of pair (a, b) 'matches'
+    a deterministic function of (a, b, i) (the GPU matcher is tested on the box)."""
+
+    def __init__(self, m_pad):
+        self.m_pad = m_pad
+        self.device = torch.device("cpu")
+
+    def match(self, pairs, ratio=0.75, out=None, exact=None):
+        pr = pairs.to(torch.int64)
+        vals = (pr[:, :1] * 7 + pr[:, 1:] * 3 + torch.arange(self.m_pad)[None, :]) % (self.m_pad + 1) - 1
+        out.copy_(vals.to(torch.int32))
+        return out
+
+
+def _expected_graph(pairs, m_pad):
+    pr = torch.from_numpy(pairs).to(torch.int64)
+    return (pr[:, :1] * 7 + pr[:, 1:] * 3 + torch.arange(m_pad)[None, :]) % (m_pad + 1) - 1
+
+
+def _worker_sharded(rank, world, port, n_img, m_pad, chunks, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pairs = np.stack(np.triu_indices(n_img, 1), 1).astype(np.int32)
+        full = sdist.match_all_pairs_sharded(_StubBank(m_pad), pairs, chunks=chunks)
+        exp = _expected_graph(pairs, m_pad)
+        ok = full.dtype == sdist.graph_dtype(m_pad) and torch.equal(full.to(torch.int64), exp)
+        q.put((rank, bool(ok)))
+    except Exception as e:
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_img,m_pad,chunks", [(2, 9, 256, 4), (2, 7, 40000, 1), (3, 6, 128, None)])
+def test_match_all_pairs_sharded_gloo(world, n_img, m_pad, chunks):
+    """Pair split + chunked all-gather of the product API: every rank ends with
+    the full graph in pair order; int16 while m_pad <= 32767, int32 beyond."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_sharded, args=(r, world, port, n_img, m_pad, chunks, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=90) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v is True for v in res.values()), res
+
+
+def test_graph_dtype_guard():
+    assert sdist.graph_dtype(4096) == torch.int16 and sdist.graph_dtype(32767) == torch.int16
+    assert sdist.graph_dtype(32768) == torch.int32
+
+
+def test_match_all_pairs_single_process_stub():
+    pairs = np.stack(np.triu_indices(5, 1), 1).astype(np.int32)
+    full = sdist.match_all_pairs_sharded(_StubBank(128), pairs)
+    assert torch.equal(full.to(torch.int64), _expected_graph(pairs, 128))
+
+
+# --- cost-balanced TSDF z-slabs -------------------------------------------------------
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_plan_slabs_partitions_and_balances(world):
+    rng = np.random.default_rng(world)
+    cost = rng.uniform(0, 1, 32) * np.hanning(32) * 10 + 0.1      # centre-heavy, as an orbit scene
+    slabs = sdist.plan_slabs(cost, world, layer=8, depth=256)
+    assert slabs[0][0] == 0 and slabs[-1][1] == 256 and len(slabs) == world
+    assert all(slabs[i][1] == slabs[i + 1][0] for i in range(world - 1))
+    assert all(z0 % 8 == 0 and z0 <= z1 for z0, z1 in slabs)
+    worst = max(cost[z0 // 8:z1 // 8].sum() for z0, z1 in slabs)
+    # optimal among contiguous splits: no better split by brute force for small worlds
+    if world <= 3:
+        import itertools
+        best = min(max(cost[a:b].sum() for a, b in zip((0,) + cuts, cuts + (32,)))
+                   for cuts in itertools.combinations(range(33), world - 1) if list(cuts) == sorted(cuts))
+        assert worst <= best + 1e-9
+    assert worst <= cost.sum() / world + cost.max() + 1e-9
+
+
+def _worker_uneven_slabs(rank, world, port, q):
+    """Each rank fuses its cost-planned (uneven) z-slab with the oracle, then
+    one all-gather of the slabs rebuilds the whole grid == single-process grid."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        from oracle import voxel as ov
+        syn = importlib.import_module("3d_reconstruction_amd.synthetic")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        R = 24
+        depth, poses, K = syn.tsdf_scene(5, 40, 56, focal=50.0, seed=3)
+        args = (depth.numpy(), poses.numpy(), K.numpy(), (-1, -1, -1), (1, 1, 1), np.float32(0.2))
+        cost = np.array([1.0, 5.0, 0.5])                     # 3 layers of 8 voxels, uneven
+        slabs = sdist.plan_slabs(cost, world, layer=8, depth=R)
+        z0, z1 = slabs[rank]
+        T, W = ov.tsdf_integrate(np.zeros((R, R, R), np.float32), np.zeros((R, R, R), np.float32), *args, z0, z1)
+        mine = torch.from_numpy(np.stack([T[z0:z1], W[z0:z1]], 1))            # (z1-z0, 2, R, R)
+        full = sdist.allgather_slabs(mine, slabs)
+        Tr, Wr = ov.tsdf_integrate(np.zeros((R, R, R), np.float32), np.zeros((R, R, R), np.float32), *args)
+        q.put((rank, bool(np.array_equal(full[:, 0].numpy(), Tr) and np.array_equal(full[:, 1].numpy(), Wr))))
+    except Exception as e:
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_uneven_slabs_allgather_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_uneven_slabs, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v is True for v in res.values()), res

