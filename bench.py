@@ -4,19 +4,22 @@
 Primary line (BASELINE.json metric, config C3/C4): image-pairs matched/sec —
 all 32,896 pairs of 257 synthetic images x 4096 SuperPoint-like 256-d
 descriptors (int8-quantised, resident in HBM), BF-L2 + ratio test 0.75 on the
-MFMA kernel.  With N ranks (one process per GPU, torch.distributed over RCCL)
-the pairs are split into N contiguous ranges (strong scaling over the fixed
-dataset) and ONE all-gather of the int16 match graph runs inside the step.
+MFMA kernel, through the product API ``dist.match_all_pairs_sharded``.  With N
+ranks (one process per GPU) the pairs are split over the ranks (strong scaling
+over the fixed dataset) and the int16 match graph is all-gathered by the
+C-ABI's RCCL collective (``sfmhip_allgather``), chunk by chunk, overlapped with
+the match launches.
 
-Secondary lines (same JSON object):
-  * TSDF Mvoxel/sec — 256^3 grid fused from 257 synthetic 1936x1296 depth maps
-    (C5), z-slab sharded over ranks (N > 1: the depth block table is built per
-    frame range and all-gathered; no grid data is exchanged).
-  * BA obs/sec — DLT triangulation + residual + FD Jacobian over 256 pairs x
-    4096 observations.
-  * N = 1 only: DDA traversal, plenoxel render, vq, geometric verification,
-    PnP and the plenoxel training step, each with a CPU
-    baseline sample.
+Secondary lines (``secondary`` list of the same JSON object):
+  * TSDF Mvoxel/sec (C5), z-slab sharded over ranks;
+  * BA obs/sec: DLT + residual + FD Jacobian (C3 BA workload), DLT and FD-J
+    kernels timed apart, with the numpy/scipy CPU baseline;
+  * N = 1 only: C2 (64 x 2048 SIFT-128), the exact float matching mode on C3,
+    the north-star composite (C3 match + C3 DLT/BA evaluation + C5 TSDF vs the
+    summed CPU wall-clock), DDA traversal, plenoxel render, vq, geometric
+    verification, PnP and the plenoxel training step.
+CPU baselines follow BASELINE.md §2: 1 warm-up + median of 3 timed runs, with
+every host thread the box gives us and again with 1 thread (``value_1thread``).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
         python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -24,6 +27,8 @@ Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 from __future__ import annotations
 
 import argparse
+import concurrent.futures as cf
+import contextlib
 import importlib
 import json
 import os
@@ -38,13 +43,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 N_IMG, M_KPT, DIM = 257, 4096, 256
+C2_IMG, C2_KPT, C2_DIM = 64, 2048, 128
 TSDF_R, TSDF_F = 256, 257
 BA_PAIRS, BA_OBS = 256, 4096
 PEAK_INT8_TOPS = 5000.0       # MI355X dense int8 MFMA (MI355X_MICROARCH.md: 2x bf16 2.5 PF)
 PEAK_HBM_GBS = 8000.0         # HBM3E spec
-MATCH_CHUNKS = 4              # N>1 (RCCL): match launches per step, each overlapped with the previous all-gather
+MATCH_CHUNKS = 4              # N>1: match launches per step, each overlapped with the previous all-gather
 PEAK_FP32_TFLOPS = 157.3      # vector fp32
 PEAK_FP64_TFLOPS = 78.6       # fp64 (vector and v_mfma_f64 matrix peaks are the same on MI355X)
+DLT_FLOP_PER_OBS = 1200.0     # 6x4 f64 DLT null vector, ~1.2 kflop per observation
+FDJ_BYTES_PER_OBS = 200.0     # 40 B in + 16 B residual + 144 B Jacobian values
+DLT_BYTES_PER_OBS = 64.0      # 2 x 2 f64 pixels in, 4 f64 out
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1", "traffic.json")
 
 
@@ -61,6 +70,10 @@ def pmc_traffic(kind: str, frac: float = 1.0):
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def events():
+    return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
 
 def timed(fn, steps, warmup, barrier):
@@ -90,39 +103,199 @@ def max_over_ranks(x: float, world: int, device) -> float:
     return float(t.item())
 
 
-def blas_threads() -> int:
+# ---------------------------------------------------------------------------
+# CPU baseline methodology: host threads, 1 warm-up + median of 3
+def host_threads() -> int:
+    """Threads this process may use on the host: OMP_NUM_THREADS (16 on the GPU
+    box: our share of its CPUs) or the affinity mask."""
     try:
-        from threadpoolctl import threadpool_info
-        n = [i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"]
-        return int(max(n)) if n else 1
-    except Exception:
-        return int(os.environ.get("OMP_NUM_THREADS", "1"))
+        return max(1, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        return max(1, min(16, len(os.sched_getaffinity(0))))
 
 
-def baseline_sample(pairs, n=48):
-    """Deterministic spread of pair indices used for the CPU baseline."""
-    return [(i * 997) % len(pairs) for i in range(n)]
+def host_info() -> dict:
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_count": os.cpu_count(), "threads_used": host_threads(), "model": model,
+            "numpy": np.__version__, "torch_threads": torch.get_num_threads()}
 
 
-def cpu_baseline_match(qcpu, pairs, sample, budget_s=12.0):
-    """Oracle (numpy GEMM-form, exact ints) on a bounded sample of the same pairs."""
-    from oracle import match as om
-    n_done, t_used = 0, 0.0
-    for i in sample:
-        if t_used >= budget_s:
-            break
-        a, b = (int(v) for v in pairs[i])
+@contextlib.contextmanager
+def blas_limit(n: int):
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:
+        yield
+        return
+    with threadpool_limits(limits=int(n)):
+        yield
+
+
+def cpu_median(fn, reps: int = 3):
+    fn()                                     # warm-up
+    ts = []
+    for _ in range(reps):
         t0 = time.perf_counter()
-        om.bf_match_q(qcpu[a], qcpu[b], (3, 4))
-        t_used += time.perf_counter() - t0
-        n_done += 1
-    return n_done / t_used, n_done, t_used
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def cpu_leg(run, n_all: int, n_one: int, unit: str, kind: str, sample: str, scale: float = 1.0) -> dict:
+    """``run(k, threads)`` does k units of the CPU path with that many threads
+    (BLAS pool and/or a thread pool over independent pieces).  Timed with every
+    host thread on k = n_all units and with 1 thread on k = n_one units; the
+    rates are units/s times ``scale`` (units -> metric unit)."""
+    nt = host_threads()
+    with blas_limit(nt):
+        t_all, ts_all = cpu_median(lambda: run(n_all, nt))
+    with blas_limit(1):
+        t_one, ts_one = cpu_median(lambda: run(n_one, 1))
+    return {"value": n_all / t_all * scale, "unit": unit, "cores": nt, "kind": kind,
+            "value_1thread": n_one / t_one * scale, "sample": sample,
+            "timing": f"median of 3 after 1 warm-up: {nt} threads on {n_all} units "
+                      f"({', '.join(f'{t:.3f}' for t in ts_all)} s), 1 thread on {n_one} units "
+                      f"({', '.join(f'{t:.3f}' for t in ts_one)} s)"}
+
+
+def pool_map(fn, items, threads: int):
+    if threads <= 1:
+        return [fn(i) for i in items]
+    with cf.ThreadPoolExecutor(threads) as ex:
+        return list(ex.map(fn, items))
+
+
+# ---------------------------------------------------------------------------
+def match_cpu_leg(qcpu, pairs, sample, n_one=3):
+    """Oracle (numpy GEMM form on exact int8 values + top-2 + exact ratio) on a
+    spread sample of the same pairs; BLAS threads = the leg's threads."""
+    from oracle import match as om
+
+    def run(k, nt):
+        for i in sample[:k]:
+            a, b = (int(v) for v in pairs[i])
+            om.bf_match_q(qcpu[a], qcpu[b], (3, 4))
+    return cpu_leg(run, len(sample), n_one, "pairs/s", "port",
+                   f"oracle.match.bf_match_q on {len(sample)} (all threads) / {n_one} (1 thread) pairs spread "
+                   f"over the pair list")
+
+
+def spread(n_total: int, n: int):
+    return [(i * 997) % n_total for i in range(n)]
+
+
+def c2_line(sfm, syn, device, args, barrier, cpu=True):
+    """Config C2: 64 images x 2048 SIFT-128 (integer 0..255 values), all 2016
+    pairs, MODE_SIFT quantisation, ratio 0.75; roofline 2.165 T int8-ops."""
+    sdist = importlib.import_module("3d_reconstruction_amd.dist")
+    x = syn.sift_like(C2_IMG, C2_KPT, C2_DIM, seed=0, device=device)
+    bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_SIFT)
+    del x
+    pairs = sfm.all_pairs(C2_IMG)
+    pdev = torch.from_numpy(pairs).to(device)
+    P = len(pairs)
+
+    def step(record):
+        e0, e1 = events() if record else (None, None)
+        if record:
+            e0.record()
+        sdist.match_all_pairs_sharded(bank, pdev, chunks=1, after_compute=(e1.record if record else None))
+        return (e0, e1)
+
+    wall, kms = timed(step, max(args.steps, 10), 2, barrier)
+    ms = wall / max(args.steps, 10) * 1e3
+    k_ms = float(np.mean(kms))
+    ops = 2.0 * C2_KPT * C2_KPT * C2_DIM * P
+    line = {"metric": "C2 image-pairs matched/sec", "value": P / (ms * 1e-3), "unit": "pairs/s", "ms_per_step": ms,
+            "dtype": "int8",
+            "config": {"workload": f"C2: {C2_IMG} imgs x {C2_KPT} SIFT-128 (0..255), all {P} pairs, MODE_SIFT "
+                                   f"(q = x - 128), ratio 0.75", "operand_shift": bank.shift},
+            "roofline": {"bound": "mfma", "kernel": "match_kernel<128>", "kernel_ms": k_ms, "unit": "TOPS",
+                         "achieved": ops / (k_ms * 1e-3) / 1e12, "peak": PEAK_INT8_TOPS,
+                         "frac": ops / (k_ms * 1e-3) / 1e12 / PEAK_INT8_TOPS,
+                         "note": "kernel_ms spans the match launch and the int16 graph copy"}}
+    if cpu:
+        sample = spread(P, 16)
+        qcpu = {int(k): bank.q[int(k)].cpu().numpy() for i in sample for k in pairs[i]}
+        line["cpu_baseline"] = match_cpu_leg(qcpu, pairs, sample)
+    del bank
+    torch.cuda.empty_cache()
+    return line
+
+
+def exact_line(sfm, syn, device, args, barrier, cpu=True, int8_ms=None):
+    """The exact float matching mode (Matcher default for float DISK/SuperPoint
+    descriptors, matching.py:111-122) on all C3 pairs: int8 MFMA pass with a
+    proven bound on the quantisation residual, uncertified rows re-scored in
+    f64.  Reported as its cost relative to the int8 path."""
+    sdist = importlib.import_module("3d_reconstruction_amd.dist")
+    x = syn.superpoint_like(N_IMG, M_KPT, DIM, seed=1, device=device)
+    bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_FLOAT, exact=True)
+    del x
+    pdev = torch.from_numpy(sfm.all_pairs(N_IMG)).to(device)
+    P = pdev.shape[0]
+
+    def step(record):
+        e0, e1 = events() if record else (None, None)
+        if record:
+            e0.record()
+        sdist.match_all_pairs_sharded(bank, pdev, exact=True, chunks=1,
+                                      after_compute=(e1.record if record else None))
+        return (e0, e1)
+
+    wall, kms = timed(step, args.steps, 1, barrier)
+    ms = wall / args.steps * 1e3
+    res = int(bank.last_resolved.item()) if bank.last_resolved is not None else None
+    line = {"metric": "exact-float image-pairs matched/sec", "value": P / (ms * 1e-3), "unit": "pairs/s",
+            "ms_per_step": ms, "dtype": "int8 filter + f64 re-score",
+            "config": {"workload": f"C3 float descriptors, exact f64 BF-L2 + ratio 0.75 (Matcher(exact=True)): "
+                                   f"{N_IMG} imgs x {M_KPT} x {DIM}, all {P} pairs"},
+            "kernel_ms": float(np.mean(kms)),
+            "rows_rescored": res, "rows_rescored_frac": (res / (P * M_KPT)) if res is not None else None,
+            "cost_vs_int8": (ms / int8_ms) if int8_ms else None}
+    del bank
+    torch.cuda.empty_cache()
+    return line
+
+
+def render_compulsory_bytes(vg, ro, rd, z) -> int:
+    """Exact compulsory HBM bytes of one render launch: every distinct 128-B
+    voxel line (voxel-major, 32 f32 channels) the trilinear corners of the
+    in-bounds samples touch (plenoxel mask |p| < scale, align_corners), plus
+    the rays, sample depths and colours read/written once."""
+    D, H, W = vg.D, vg.H, vg.W
+    lo = torch.tensor(vg.bmin, device=ro.device)
+    hi = torch.tensor(vg.bmax, device=ro.device)
+    size = torch.tensor([W - 1, H - 1, D - 1], dtype=torch.float32, device=ro.device)
+    seen = torch.zeros(D * H * W, dtype=torch.bool, device=ro.device)
+    for s in range(0, ro.shape[0], 2048):
+        p = ro[s:s + 2048, None, :] + rd[s:s + 2048, None, :] * z[s:s + 2048, :, None]
+        inb = ((p.abs() < hi) if vg.mask_mode == 1 else ((p >= lo) & (p <= hi))).all(-1)
+        q = ((p - lo) / (hi - lo) * 2 - 1).clamp(-1, 1)
+        f = ((q + 1) / 2 * size)[inb]
+        i0 = f.floor().long()
+        for c in range(8):
+            ix = (i0[:, 0] + (c & 1)).clamp(0, W - 1)
+            iy = (i0[:, 1] + ((c >> 1) & 1)).clamp(0, H - 1)
+            iz = (i0[:, 2] + ((c >> 2) & 1)).clamp(0, D - 1)
+            seen[(iz * H + iy) * W + ix] = True
+    n_lines = int(seen.sum().item())
+    B, S = z.shape
+    return n_lines * 128 + B * (24 + 4 * S + 12)
 
 
 def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
     """V1 DDA traversal, V2+V4 fused sample/SH/composite at the plenoxel config
-    (28 x 256^3 grid, 2048 rays x 192 bins per batch) and M2 vq (C3 descriptors
-    as f64 vs a 200-word codebook), each with an oracle CPU baseline sample."""
+    (28 x 256^3 grid, 16 x 2048 rays x 192 bins per launch) and M2 vq (C3
+    descriptors as f64 vs a 200-word codebook), each with a CPU baseline."""
     out = []
     g = torch.Generator(device=device)
     g.manual_seed(7)
@@ -136,11 +309,10 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
     rays = torch.cat([o, dvec / dvec.norm(dim=1, keepdim=True), torch.zeros_like(far), far], 1).contiguous()
 
     def dda_step(record):
-        e0 = e1 = None
+        e0, e1 = events() if record else (None, None)
         if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        vt = sfm.voxel_traversal(rays, 1.0)
+        sfm.voxel_traversal(rays, 1.0)
         if record:
             e1.record()
         return (e0, e1)
@@ -153,11 +325,9 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
     if cpu:
         from oracle import voxel as ov
         rr = rays.cpu().numpy()
-        t0 = time.perf_counter()
-        ov.voxel_traversal(rr, 1.0)
-        dt = time.perf_counter() - t0
-        line["cpu_baseline"] = {"value": nr / dt, "unit": "rays/s", "cores": 1, "kind": "port",
-                                "sample": f"the same {nr} rays through oracle.voxel.voxel_traversal (numpy), {dt:.2f}s"}
+        line["cpu_baseline"] = cpu_leg(lambda k, nt: ov.voxel_traversal(rr[:k], 1.0), nr, nr, "rays/s", "port",
+                                       f"the same {nr} rays through oracle.voxel.voxel_traversal (numpy; the "
+                                       f"reference loop is single-threaded, so threads only reach numpy)")
     out.append(line)
     # V2+V4: plenoxel N=256 grid, 16 batches of 2048 rays x 192 bins
     N, B, S, NB = 256, 2048, 192, 16
@@ -175,9 +345,8 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
     z = z.contiguous()
 
     def render_step(record):
-        e0 = e1 = None
+        e0, e1 = events() if record else (None, None)
         if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         vg.render(ro, rd, z)
         if record:
@@ -186,19 +355,31 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
 
     wall, kms = timed(render_step, args.steps, 1, barrier)
     ms = wall / args.steps * 1e3
+    k_ms = float(np.mean(kms))
+    comp = render_compulsory_bytes(vg, ro, rd, z)
     line = {"metric": "render_rays rays/sec", "value": NB * B / (ms * 1e-3), "unit": "rays/s", "ms_per_step": ms,
-            "config": {"workload": "V2+V4 plenoxel render_rays: 28x256^3 grid, 16 x (2048 rays x 192 bins)"},
-            "roofline": {"bound": "hbm", "kernel": "render_kernel", "kernel_ms": float(np.mean(kms)),
-                         "algorithmic_bytes_per_sample": 8 * 112}}
+            "config": {"workload": "V2+V4 plenoxel render_rays: 28x256^3 grid, 16 x (2048 rays x 192 bins) "
+                                   "in one launch"},
+            "roofline": {"bound": "hbm", "kernel": "render_kernel", "kernel_ms": k_ms, "unit": "GB/s",
+                         "compulsory_bytes": comp,
+                         "achieved": comp / (k_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+                         "frac": comp / (k_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                         "note": "compulsory = distinct 128-B voxel lines under the in-bounds samples' trilinear "
+                                 "corners (exact count) + rays/z read + colours written; the 8-corner x 28-channel "
+                                 "gather volume (896 B/sample) mostly hits in L2"}}
     if cpu:
         from oracle import voxel as ov
         gsmall = vg.grid.cpu().numpy()
-        t0 = time.perf_counter()
-        ov.render(gsmall, (-1.5,) * 3, (1.5,) * 3, 1, ro[:64].cpu().numpy(), rd[:64].cpu().numpy(),
-                  z[:64].cpu().numpy())
-        dt = time.perf_counter() - t0
-        line["cpu_baseline"] = {"value": 64 / dt, "unit": "rays/s", "cores": 1, "kind": "port",
-                                "sample": f"64 rays x 192 bins through oracle.voxel.render (numpy f32), {dt:.2f}s"}
+        ro_c, rd_c, z_c = ro[:256].cpu().numpy(), rd[:256].cpu().numpy(), z[:256].cpu().numpy()
+
+        def run(k, nt):
+            parts = [(s, min(k, s + max(1, k // nt))) for s in range(0, k, max(1, k // nt))]
+            pool_map(lambda ab: ov.render(gsmall, (-1.5,) * 3, (1.5,) * 3, 1, ro_c[ab[0]:ab[1]], rd_c[ab[0]:ab[1]],
+                                          z_c[ab[0]:ab[1]]), parts, nt)
+        line["cpu_baseline"] = cpu_leg(run, 256, 64, "rays/s", "port",
+                                       "oracle.voxel.render (numpy f32 restatement of plenoxel.render_rays) on "
+                                       "256 rays x 192 bins (all threads: ray blocks over a thread pool) / 64 rays "
+                                       "(1 thread)")
         del gsmall
     out.append(line)
     del vg
@@ -207,39 +388,38 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
     obs = syn.superpoint_like(N_IMG, M_KPT, 128, seed=3, device=device).reshape(-1, 128).double().contiguous()
     book = obs[torch.randperm(obs.shape[0], generator=g, device=device)[:200]].contiguous()
     codes = torch.empty(obs.shape[0], dtype=torch.int32, device=device)
-    dist = torch.empty(obs.shape[0], dtype=torch.float64, device=device)
-    from importlib import import_module
-    abi = import_module("3d_reconstruction_amd._abi")
+    dst = torch.empty(obs.shape[0], dtype=torch.float64, device=device)
+    abi = importlib.import_module("3d_reconstruction_amd._abi")
 
     def vq_step(record):
-        e0 = e1 = None
+        e0, e1 = events() if record else (None, None)
         if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         abi.call("sfmhip_vq", obs.data_ptr(), obs.shape[0], book.data_ptr(), 200, 128, codes.data_ptr(),
-                 dist.data_ptr(), abi.stream_ptr())
+                 dst.data_ptr(), abi.stream_ptr())
         if record:
             e1.record()
         return (e0, e1)
 
     wall, kms = timed(vq_step, args.steps, 1, barrier)
     ms = wall / args.steps * 1e3
+    fl = 2 * obs.shape[0] * 200 * 128 / (np.mean(kms) * 1e-3) / 1e12
     line = {"metric": "vq obs/sec", "value": obs.shape[0] / (ms * 1e-3), "unit": "obs/s", "ms_per_step": ms,
             "config": {"workload": "M2 vq (matching.py:27): 257x4096 obs x 200 codes x 128-d, f64"},
+            # GEMM form: 2 flops per (obs, codeword, dim) on v_mfma_f32_16x16x4_f32 (f32 filter
+            # with a proven error bound; undecided observations settled in f64)
             "roofline": {"bound": "mfma", "kernel": "vq_f32r_kernel+vq_exact_kernel", "kernel_ms": float(np.mean(kms)),
-                         # GEMM form: 2 flops per (obs, codeword, dim) on v_mfma_f32_16x16x4_f32 (f32 filter
-                         # with a proven error bound; undecided observations settled in f64)
-                         "achieved_tflops": 2 * obs.shape[0] * 200 * 128 / (np.mean(kms) * 1e-3) / 1e12,
-                         "peak_tflops": PEAK_FP32_TFLOPS,
-                         "frac": 2 * obs.shape[0] * 200 * 128 / (np.mean(kms) * 1e-3) / 1e12 / PEAK_FP32_TFLOPS}}
+                         "unit": "TFLOP/s", "achieved": fl, "peak": PEAK_FP32_TFLOPS, "frac": fl / PEAK_FP32_TFLOPS}}
     if cpu:
         from scipy.cluster.vq import vq as scipy_vq
-        oo, bb = obs[:4096].cpu().numpy(), book.cpu().numpy()
-        t0 = time.perf_counter()
-        scipy_vq(oo, bb)
-        dt = time.perf_counter() - t0
-        line["cpu_baseline"] = {"value": 4096 / dt, "unit": "obs/s", "cores": blas_threads(), "kind": "reference",
-                                "sample": f"scipy.cluster.vq.vq (the reference's own call) on 4096 obs, {dt:.3f}s"}
+        oo, bb = obs[:65536].cpu().numpy(), book.cpu().numpy()
+
+        def run(k, nt):
+            step_ = max(1, k // nt)
+            pool_map(lambda s: scipy_vq(oo[s:s + step_], bb), range(0, k, step_), nt)
+        line["cpu_baseline"] = cpu_leg(run, 65536, 16384, "obs/s", "reference",
+                                       "scipy.cluster.vq.vq (the reference's own call) on 65,536 obs (all threads: "
+                                       "row blocks over a thread pool) / 16,384 obs (1 thread)")
     out.append(line)
     return out
 
@@ -247,7 +427,7 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
 def verify_line(sfm, syn, device, args, barrier, cpu=True):
     """§8f row 2: findEssentialMat (RANSAC, prob 0.999, 1 px) + recoverPose for
     256 BFS-candidate pairs x 2048 matches (30 % outliers, 0.5 px noise), one
-    batched launch each; CPU baseline = the oracle restatement on 2 pairs."""
+    batched launch each; CPU baseline = the oracle restatement."""
     v = sfm.verify
     s = syn.two_view_pairs(256, 2048, outlier_frac=0.3, noise_px=0.5, seed=6)
     a, b, of = v.pack_pairs(s["pts0"], s["pts1"])
@@ -255,9 +435,8 @@ def verify_line(sfm, syn, device, args, barrier, cpu=True):
     holder = {}
 
     def step(record):
-        e0 = e1 = None
+        e0, e1 = events() if record else (None, None)
         if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         r = v.find_essential_batched(a, b, of, cam)
         holder["rp"] = v.recover_pose_batched(r["E"], a, b, of, cam, mask=r["mask"])
@@ -278,15 +457,14 @@ def verify_line(sfm, syn, device, args, barrier, cpu=True):
                          "kernel_ms": float(np.mean(kms))}}
     if cpu:
         from oracle import ransac as orc
-        t0 = time.perf_counter()
-        for p in range(2):
+
+        def one(p):
             E, m = orc.find_essential_mat(s["pts0"][p], s["pts1"][p], s["K"])
             keep = m.ravel() > 0
             orc.recover_pose(E, s["pts0"][p][keep], s["pts1"][p][keep], s["K"])
-        dt = time.perf_counter() - t0
-        line["cpu_baseline"] = {"value": 2 / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
-                                "sample": f"2 of the 256 pairs through oracle.ransac (numpy restatement of "
-                                          f"OpenCV's findEssentialMat + recoverPose), {dt:.2f}s"}
+        line["cpu_baseline"] = cpu_leg(lambda k, nt: pool_map(one, range(k), nt), 8, 2, "pairs/s", "port",
+                                       "oracle.ransac (numpy restatement of OpenCV's findEssentialMat + "
+                                       "recoverPose) on 8 pairs over a thread pool / 2 pairs on 1 thread")
     return line
 
 
@@ -340,9 +518,9 @@ def train_line(sfm, syn, device, args, barrier, cpu=True):
     line = {"metric": "plenoxel training steps/sec", "value": 1e3 / ms, "unit": "steps/s", "ms_per_step": ms,
             "config": {"workload": "plenoxel.py train step: NerfModel(N=256) 28x256^3, 2048 rays x 192 bins, "
                                    "mse + backward + Adam(lr=1e-2)"},
-            "roofline": {"bound": "hbm", "kernel": "adam_flagged_kernel", "kernel_ms": adam_ms,
+            "roofline": {"bound": "hbm", "kernel": "adam_flagged_kernel", "kernel_ms": adam_ms, "unit": "GB/s",
                          "algorithmic_bytes_per_param": 32,
-                         "achieved_gbs": n_par * 32 / (adam_ms * 1e-3) / 1e9, "peak_gbs": PEAK_HBM_GBS,
+                         "achieved": n_par * 32 / (adam_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                          "frac": n_par * 32 / (adam_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                          "touched_line_frac": touched,
                          "moved_gbs": n_par * 32 / 28 * moved / (adam_ms * 1e-3) / 1e9,
@@ -354,19 +532,18 @@ def train_line(sfm, syn, device, args, barrier, cpu=True):
         from oracle import train as ot
         Nc, Bc = 64, 64
         gsmall = np.full((28, Nc, Nc, Nc), 0.01, np.float32)
-        zz = z[:Bc].cpu().numpy()
-        t0 = time.perf_counter()
-        _, _, grad = ot.render_loss_grad(gsmall, (-1.5,) * 3, (1.5,) * 3, 1, ro[:Bc].cpu().numpy(),
-                                         rd[:Bc].cpu().numpy(), zz, gt[:Bc].cpu().numpy())
-        t_r = (time.perf_counter() - t0) / Bc
-        t0 = time.perf_counter()
-        ot.adam_step(gsmall, grad, np.zeros_like(grad), np.zeros_like(grad), 1)
-        t_a = (time.perf_counter() - t0) / gsmall.size
+        zz, roc, rdc, gtc = z[:Bc].cpu().numpy(), ro[:Bc].cpu().numpy(), rd[:Bc].cpu().numpy(), gt[:Bc].cpu().numpy()
+        t_r, _ = cpu_median(lambda: ot.render_loss_grad(gsmall, (-1.5,) * 3, (1.5,) * 3, 1, roc, rdc, zz, gtc))
+        t_r /= Bc
+        _, _, grad = ot.render_loss_grad(gsmall, (-1.5,) * 3, (1.5,) * 3, 1, roc, rdc, zz, gtc)
+        t_a, _ = cpu_median(lambda: ot.adam_step(gsmall, grad, np.zeros_like(grad), np.zeros_like(grad), 1))
+        t_a /= gsmall.size
         est = t_r * B + t_a * n_par
         line["cpu_baseline"] = {"value": 1.0 / est, "unit": "steps/s", "cores": 1, "kind": "port",
                                 "sample": f"oracle.train on {Bc} rays (render+backward, {t_r * 1e3:.2f} ms/ray) "
-                                          f"and Adam over 28x{Nc}^3 params ({t_a * 1e9:.1f} ns/param), "
-                                          f"extrapolated to 2048 rays + 28x256^3 params = {est:.1f} s/step"}
+                                          f"and Adam over 28x{Nc}^3 params ({t_a * 1e9:.1f} ns/param), each the "
+                                          f"median of 3 after 1 warm-up, extrapolated to 2048 rays + 28x256^3 "
+                                          f"params = {est:.1f} s/step (single-threaded numpy)"}
     del tr
     torch.cuda.empty_cache()
     return line
@@ -397,9 +574,8 @@ def pnp_line(sfm, syn, device, args, barrier, cpu=True):
     holder = {}
 
     def step(record):
-        e0 = e1 = None
+        e0, e1 = events() if record else (None, None)
         if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         holder["r"] = v.pnp_ransac_batched(Xd, ud, of, cam)
         if record:
@@ -416,19 +592,53 @@ def pnp_line(sfm, syn, device, args, barrier, cpu=True):
             "roofline": {"bound": "fp64", "kernel": "pnp_ransac_kernel", "kernel_ms": float(np.mean(kms))}}
     if cpu:
         from oracle import pnp as opnp
-        t0 = time.perf_counter()
-        for k in range(4):
-            opnp.solve_pnp_ransac(Xs[k], uvs[k], K)
-        dt = time.perf_counter() - t0
-        line["cpu_baseline"] = {"value": 4 / dt, "unit": "registrations/s", "cores": 1, "kind": "port",
-                                "sample": f"4 of the 256 problems through oracle.pnp (numpy restatement of "
-                                          f"OpenCV's solvePnPRansac), {dt:.2f}s"}
+        line["cpu_baseline"] = cpu_leg(lambda k, nt: pool_map(lambda i: opnp.solve_pnp_ransac(Xs[i], uvs[i], K),
+                                                              range(k), nt),
+                                       16, 4, "registrations/s", "port",
+                                       "oracle.pnp (numpy restatement of OpenCV's solvePnPRansac) on 16 problems "
+                                       "over a thread pool / 4 problems on 1 thread")
     return line
+
+
+def ba_cpu_leg(s):
+    """The reference's per-pair CPU path for the same work (sfm.py:27-38): numpy
+    batched-SVD DLT (cv2.triangulatePoints restatement) + the residual and
+    scipy approx_derivative grouped 2-point Jacobian with the ba_sparse
+    pattern (what least_squares evaluates per TRF iteration); pairs over a
+    thread pool for the all-threads run.  Also the full scipy least_squares
+    solve per pair with sfm.py:38's settings (reported, not in the rate)."""
+    from oracle import geometry as og
+
+    def one(p):
+        sl = slice(p * BA_OBS, (p + 1) * BA_OBS)
+        og.triangulate_points(s["P"][p, 0], s["P"][p, 1], s["x0"][:, sl], s["x1"][:, sl])
+        xv = np.concatenate([s["cam"][p], s["X"][sl].ravel()])
+        og.fd_jacobian(xv, s["K"][p], s["pts2d"][sl])
+
+    sample = spread(BA_PAIRS, 16)
+    leg = cpu_leg(lambda k, nt: pool_map(one, sample[:k], nt), 16, 4, "obs/s", "port",
+                  "per pair: oracle.geometry.triangulate_points (numpy batched SVD, cv2.triangulatePoints "
+                  "restatement) + oracle.geometry.fd_jacobian (residual + scipy approx_derivative with the "
+                  "ba_sparse groups) on 16 pairs over a thread pool / 4 pairs on 1 thread", scale=BA_OBS)
+    from scipy.optimize import least_squares
+    p = sample[0]
+    sl = slice(p * BA_OBS, (p + 1) * BA_OBS)
+    xv = np.concatenate([s["cam"][p], s["X"][sl].ravel()])
+    A = og.ba_sparse(BA_OBS, len(xv), 6)
+    holder = {}
+
+    def solve():
+        holder["r"] = least_squares(og.reprojection_error, xv, jac_sparsity=A, verbose=0, x_scale="jac",
+                                    ftol=1e-8, args=(s["K"][p], s["pts2d"][sl]))
+    t_ls, _ = cpu_median(solve)
+    leg["least_squares_s_per_pair"] = t_ls
+    leg["least_squares_nfev"] = int(holder["r"].nfev)
+    return leg
 
 
 def ba_line(sfm, syn, device, args, barrier, cpu=True):
     """DLT + residual + FD-Jacobian over BA_PAIRS pairs x BA_OBS observations
-    (pair ranges per rank)."""
+    (pair ranges per rank); DLT and residual/FD-J kernels timed apart."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     sdist = importlib.import_module("3d_reconstruction_amd.dist")
@@ -442,32 +652,103 @@ def ba_line(sfm, syn, device, args, barrier, cpu=True):
     X4 = torch.empty((4, x0l.shape[1]), dtype=torch.float64, device=device)
     rr = torch.empty((Xl.shape[0], 2), dtype=torch.float64, device=device)
     jv = torch.empty((Xl.shape[0], 2, 9), dtype=torch.float64, device=device)
+    mids = []
 
     def ba_step(record):
-        e0 = e1 = None
+        e0 = e1 = em = None
         if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, e1 = events()
+            em = torch.cuda.Event(enable_timing=True)
             e0.record()
         sfm.triangulate_batched(tt["P"], pol, x0l, x1l, out=X4)
+        if record:
+            em.record()
         sfm.residual_jacobian_batched(tt["cam"], tt["K"], Xl, p2l, pol, r=rr, jv=jv)
         if record:
             e1.record()
+            mids.append((e0, em, e1))
         return (e0, e1)
 
     wall_b, kms_b = timed(ba_step, args.steps, args.warmup, barrier)
     wall_b = max_over_ranks(wall_b, world, device)
     b_ms = wall_b / args.steps * 1e3
     k_ms = max_over_ranks(float(np.mean(kms_b)), world, device)
+    dlt_ms = max_over_ranks(float(np.mean([a.elapsed_time(m) for a, m, _ in mids])), world, device)
+    fdj_ms = max_over_ranks(float(np.mean([m.elapsed_time(b) for _, m, b in mids])), world, device)
     local = (ohi - olo) * BA_OBS
-    gbs = local * (64 + 200) / (k_ms * 1e-3) / 1e9
-    return {
+    dlt_tf = local * DLT_FLOP_PER_OBS / (dlt_ms * 1e-3) / 1e12
+    fdj_gbs = local * FDJ_BYTES_PER_OBS / (fdj_ms * 1e-3) / 1e9
+    line = {
         "metric": "BA obs/sec (DLT + residual + FD-Jacobian)", "value": n / (b_ms * 1e-3), "unit": "obs/s",
-        "ms_per_step": b_ms, "scaling": "strong",
-        "config": {"workload": f"{BA_PAIRS} pairs x {BA_OBS} obs, f64", "parallelism": f"pairs/{world}"},
-        "roofline": {"bound": "hbm", "kernel": "dlt_kernel+fdjac_kernel", "kernel_ms": k_ms,
-                     "algorithmic_bytes_per_obs": 64 + 200, "achieved_gbs": gbs, "peak_gbs": PEAK_HBM_GBS,
-                     "frac": gbs / PEAK_HBM_GBS},
+        "ms_per_step": b_ms, "scaling": "strong", "dtype": "f64",
+        "config": {"workload": f"C3 BA: {BA_PAIRS} pairs x {BA_OBS} obs, f64", "parallelism": f"pairs/{world}"},
+        "roofline": {"kernel_ms": k_ms,
+                     "dlt": {"bound": "fp64", "kernel": "dlt_kernel", "kernel_ms": dlt_ms, "unit": "TFLOP/s",
+                             "algorithmic_flop_per_obs": DLT_FLOP_PER_OBS, "achieved": dlt_tf,
+                             "peak": PEAK_FP64_TFLOPS, "frac": dlt_tf / PEAK_FP64_TFLOPS,
+                             "achieved_gbs": local * DLT_BYTES_PER_OBS / (dlt_ms * 1e-3) / 1e9},
+                     "fdjac": {"bound": "hbm", "kernel": "fdjac_kernel", "kernel_ms": fdj_ms, "unit": "GB/s",
+                               "algorithmic_bytes_per_obs": FDJ_BYTES_PER_OBS, "achieved": fdj_gbs,
+                               "peak": PEAK_HBM_GBS, "frac": fdj_gbs / PEAK_HBM_GBS}},
     }
+    if cpu and rank == 0 and world == 1:
+        line["cpu_baseline"] = ba_cpu_leg(s)
+    return line
+
+
+def tsdf_cpu_leg(syn):
+    """numpy per-frame TSDF oracle (oracle.voxel.tsdf_integrate) on frames of
+    the same C5 scene; all threads = z-slabs over a thread pool (numpy drops
+    the GIL inside its array loops), 1 thread = the whole grid."""
+    from oracle import voxel as ov
+    dep, ps, Kk = syn.tsdf_scene(4, syn.IMG_H, syn.IMG_W, device="cpu")
+    dep, ps, Kk = dep.numpy(), ps.numpy(), Kk.numpy()
+    R = TSDF_R
+    args = ((-1.2,) * 3, (1.2,) * 3, np.float32(3 * 2.4 / (R - 1)))
+
+    def run(k, nt):
+        if nt <= 1:
+            ov.tsdf_integrate(np.zeros((R, R, R), np.float32), np.zeros((R, R, R), np.float32), dep[:k], ps[:k],
+                              Kk[:k], *args)
+            return
+        step_ = -(-R // nt)
+        pool_map(lambda z0: ov.tsdf_integrate(np.zeros((min(R, z0 + step_) - z0, R, R), np.float32),
+                                              np.zeros((min(R, z0 + step_) - z0, R, R), np.float32), dep[:k], ps[:k],
+                                              Kk[:k], *args, z0=z0, z1=min(R, z0 + step_), grid_depth=R),
+                 range(0, R, step_), nt)
+    return cpu_leg(run, 4, 1, "Mvoxel-updates/s", "port",
+                   "oracle.voxel.tsdf_integrate (numpy f32) on 4 frames of the C5 scene (all threads: z-slabs "
+                   "over a thread pool) / 1 frame (1 thread, whole grid)", scale=R ** 3 / 1e6)
+
+
+def composite_line(result, match_cpu, ba, tsdf):
+    """North-star composite (BASELINE.json): C3 all-pairs match step + C3 DLT/BA
+    evaluation (256 pairs x 4096 obs) + C5 TSDF step on 1 MI355X against the
+    summed CPU wall-clock of the same three workloads (each extrapolated from
+    its timed sample), target >= 50x."""
+    P = result["config"]["pairs"]
+    gpu_s = (result["ms_per_step"] + ba["ms_per_step"] + tsdf["ms_per_step"]) * 1e-3
+    cb, ct = ba.get("cpu_baseline"), tsdf.get("cpu_baseline")
+    if not (match_cpu and cb and ct):
+        return None
+    n_obs = BA_PAIRS * BA_OBS
+    upd = TSDF_R ** 3 * TSDF_F / 1e6
+
+    def cpu_s(key):
+        return P / match_cpu[key] + n_obs / cb[key] + upd / ct[key]
+    cpu_all, cpu_one = cpu_s("value"), cpu_s("value_1thread")
+    return {"metric": "north-star composite speedup vs reference CPU path", "value": cpu_all / gpu_s, "unit": "x",
+            "target": 50.0, "value_1thread": cpu_one / gpu_s, "gpu_s": gpu_s,
+            "cpu_s": cpu_all, "cpu_s_1thread": cpu_one, "cores": match_cpu["cores"],
+            "parts_s": {"gpu": {"match": result["ms_per_step"] * 1e-3, "ba": ba["ms_per_step"] * 1e-3,
+                                "tsdf": tsdf["ms_per_step"] * 1e-3},
+                        "cpu": {"match": P / match_cpu["value"], "ba": n_obs / cb["value"],
+                                "tsdf": upd / ct["value"]},
+                        "cpu_1thread": {"match": P / match_cpu["value_1thread"], "ba": n_obs / cb["value_1thread"],
+                                        "tsdf": upd / ct["value_1thread"]}},
+            "config": {"workload": "C3 all-pairs matching (32,896 pairs) + C3 DLT + residual + FD Jacobian "
+                                   "(256 x 4096 obs) + C5 TSDF (256^3 x 257 frames), 1 GPU vs host CPU; CPU "
+                                   "times are linear extrapolations of the timed samples"}}
 
 
 def main():
@@ -480,7 +761,7 @@ def main():
     ap.add_argument("--n-img", type=int, default=N_IMG)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for rehearsal")
     ap.add_argument("--rehearse-overlap", action="store_true",
-                    help="N=1 rehearsal of the N>1 RCCL path: a single-rank NCCL group + the overlapped all-gather")
+                    help="N=1 rehearsal of the N>1 path: a one-rank RCCL communicator + the overlapped all-gather")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -490,10 +771,6 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if args.rehearse_overlap and world == 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29561")
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=device)
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
@@ -506,6 +783,13 @@ def main():
     sfm = importlib.import_module("3d_reconstruction_amd")
     syn = importlib.import_module("3d_reconstruction_amd.synthetic")
     sdist = importlib.import_module("3d_reconstruction_amd.dist")
+    cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+
+    # the match-graph collective: the C-ABI's RCCL communicator (sfmhip_comm_*),
+    # bootstrapped over the torch.distributed group; gloo rehearsals use torch
+    comm = None
+    if (world > 1 and args.dist_backend == "nccl") or args.rehearse_overlap:
+        comm = sdist.RcclComm() if world > 1 else sdist.RcclComm.single()
 
     # ---------------- C3/C4: all-pairs matching ----------------------------
     n_img = args.n_img
@@ -518,53 +802,29 @@ def main():
         f"{n_img}x{M_KPT}x{DIM} int8 = {bank.q.numel() / 1e6:.0f} MB")
     pairs_all = sfm.all_pairs(n_img)
     P = len(pairs_all)
-    num, den = 3, 4
-    overlap = (world > 1 and args.dist_backend == "nccl") or args.rehearse_overlap
-    if overlap:
-        # chunk-major pair layout: each chunk's match launch overlaps the RCCL
-        # all-gather of the previous chunk (dist.overlapped_allgather)
-        pairs_dev = torch.from_numpy(pairs_all).to(device)
-        mine = [(a, b) for a, b in sdist.chunk_rows(P, rank, world, MATCH_CHUNKS) if b > a]
-        bufs = {a: torch.empty((b - a, bank.m_pad), dtype=torch.int32, device=device) for a, b in mine}
-        lo, hi = 0, sum(b - a for a, b in mine)
-    else:
-        lo, hi = sdist.shard_range(P, rank, world)
-        pairs_local = torch.from_numpy(pairs_all[lo:hi]).to(device)
-        m0 = torch.empty((hi - lo, bank.m_pad), dtype=torch.int32, device=device)
-        m16 = torch.empty((hi - lo, bank.m_pad), dtype=torch.int16, device=device)
-
-    def compute_chunk(a, b, out):
-        bank._launch(pairs_dev[a:b], num, den, bufs[a], None, None)
-        out.copy_(bufs[a])
+    pairs_dev = torch.from_numpy(pairs_all).to(device)
+    chunks = MATCH_CHUNKS if (world > 1 or comm is not None) else 1
+    holder = {}
 
     def match_step(record):
-        e0 = e1 = None
+        e0, e1 = events() if record else (None, None)
         if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        if overlap:
-            sdist.overlapped_allgather(compute_chunk, P, (bank.m_pad,), torch.int16, device, chunks=MATCH_CHUNKS,
-                                       after_compute=(e1.record if record else None))
-            return (e0, e1)
-        bank._launch(pairs_local, num, den, m0, None, None)
-        if record:
-            e1.record()
-        m16.copy_(m0)
-        if world > 1:
-            sdist.allgather_rows(m16, P)
+        holder["g"] = sdist.match_all_pairs_sharded(bank, pairs_dev, ratio=(3, 4), exact=False, comm=comm,
+                                                    chunks=chunks, after_compute=(e1.record if record else None))
         return (e0, e1)
 
     wall, kms = timed(match_step, args.steps, args.warmup, barrier)
     wall = max_over_ranks(wall, world, device)
     ms_per_step = wall / args.steps * 1e3
     kern_ms = max_over_ranks(float(np.mean(kms)), world, device)
-    pairs_per_launch = hi - lo
+    pairs_per_launch = sum(max(0, b - a) for a, b in sdist.chunk_rows(P, rank, world, chunks))
     ops_per_launch = 2.0 * M_KPT * M_KPT * DIM * pairs_per_launch
     achieved_tops = ops_per_launch / (kern_ms * 1e-3) / 1e12
-    n_matched = int(sum(int((b >= 0).sum().item()) for b in bufs.values())) if overlap else \
-        int((m0 >= 0).sum().item())
+    graph = holder["g"]
+    n_matched = int((graph >= 0).sum().item())
     log(f"[rank {rank}] match: {ms_per_step:.2f} ms/step, kernel {kern_ms:.2f} ms, "
-        f"{achieved_tops:.0f} TOPS, {n_matched} matches in shard")
+        f"{achieved_tops:.0f} TOPS, {n_matched} matches in the gathered graph {tuple(graph.shape)} {graph.dtype}")
 
     result = {
         "metric": "image-pairs matched/sec",
@@ -580,9 +840,10 @@ def main():
         "dtype": "int8",
         "data": "synthetic (SuperPoint-like unit-norm descriptors, 40% cross-view overlap, seed 1)",
         "config": {"workload": f"C3/C4 all-pairs BF-L2 + ratio 0.75: {n_img} imgs x {M_KPT} kpts x {DIM}-d",
-                   "pairs": P, "parallelism": f"pairs/{world}" + (
-                       f" + {MATCH_CHUNKS} RCCL all-gathers (int16) overlapped with the match launches" if overlap
-                       else (" + 1 all-gather (int16)" if world > 1 else ""))},
+                   "pairs": P, "api": "dist.match_all_pairs_sharded",
+                   "parallelism": f"pairs/{world}" + (
+                       f" + {chunks} RCCL all-gathers (int16, sfmhip_allgather) overlapped with the match launches"
+                       if comm is not None else (" + torch.distributed all-gather (rehearsal)" if world > 1 else ""))},
         "roofline": {"bound": "mfma", "achieved": achieved_tops, "peak": PEAK_INT8_TOPS, "unit": "TOPS",
                      "frac": achieved_tops / PEAK_INT8_TOPS,
                      "traffic": pmc_traffic("match", pairs_per_launch / P) if n_img == N_IMG else None,
@@ -590,18 +851,15 @@ def main():
                      "kernel": "match_kernel<256>", "kernel_ms": kern_ms,
                      "algorithmic": "2*M*N*d int8 ops per pair x pairs per launch"},
     }
+    match_cpu = None
+    if cpu:
+        sample = spread(P, 16)
+        qcpu = {int(k): bank.q[int(k)].cpu().numpy() for i in sample for k in pairs_all[i]}
+    del bank, holder["g"], graph
+    torch.cuda.empty_cache()
 
-    qcpu = {}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        for i in baseline_sample(pairs_all):
-            for k in pairs_all[i]:
-                if int(k) not in qcpu:
-                    qcpu[int(k)] = bank.q[int(k)].cpu().numpy()
-
-    # ---------------- C5: TSDF ------------------------------------------
     if not args.skip_secondary:
-        del bank
-        torch.cuda.empty_cache()
+        # ---------------- C5: TSDF ------------------------------------------
         t0 = time.perf_counter()
         depth, poses, K = syn.tsdf_scene(TSDF_F, syn.IMG_H, syn.IMG_W, device=device)
         torch.cuda.synchronize()
@@ -614,14 +872,13 @@ def main():
         bmin, bmax = (-1.2, -1.2, -1.2), (1.2, 1.2, 1.2)
 
         def tsdf_step(record):
-            e0 = e1 = None
             T[z0:z1].zero_()
             Wt[z0:z1].zero_()
+            e0, e1 = events() if record else (None, None)
             if record:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
             if world > 1:   # each rank builds the block table of 1/N of the frames; one all-gather
-                tab = sdist.shared_block_table(depth)
+                tab = sdist.shared_block_table(depth, comm=comm)
                 sfm.tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0, z1, block_table=tab)
             else:
                 sfm.tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0, z1)
@@ -636,58 +893,53 @@ def main():
         upd = R ** 3 * TSDF_F
         local_upd = (z1 - z0) * R * R * TSDF_F
         comp_bytes = (z1 - z0) * R * R * 16 + depth.numel() * 4
-        result["secondary"] = [{
+        tsdf = {
             "metric": "TSDF Mvoxel/sec", "value": upd / (t_ms * 1e-3) / 1e6, "unit": "Mvoxel-updates/s",
-            "ms_per_step": t_ms, "scaling": "strong",
+            "ms_per_step": t_ms, "scaling": "strong", "dtype": "f32",
             "config": {"workload": f"C5: {R}^3 grid x {TSDF_F} depth maps {syn.IMG_W}x{syn.IMG_H}",
                        "parallelism": f"z-slabs/{world}" + (" + 1 all-gather of the depth block table" if world > 1
                                                              else "")},
-            "roofline": {"bound": "valu", "kernel": "tsdf_kernel", "kernel_ms": tk_ms,
-                         "achieved_hbm_gbs": comp_bytes / (tk_ms * 1e-3) / 1e9, "peak_hbm_gbs": PEAK_HBM_GBS,
-                         "achieved_tflops": 32.0 * local_upd / (tk_ms * 1e-3) / 1e12,
-                         "peak_tflops": PEAK_FP32_TFLOPS,
+            "roofline": {"bound": "valu", "kernel": "tsdf_kernel + pre-passes", "kernel_ms": tk_ms, "unit": "TFLOP/s",
+                         "achieved": 32.0 * local_upd / (tk_ms * 1e-3) / 1e12, "peak": PEAK_FP32_TFLOPS,
                          "frac": (32.0 * local_upd / (tk_ms * 1e-3) / 1e12) / PEAK_FP32_TFLOPS,
+                         "achieved_hbm_gbs": comp_bytes / (tk_ms * 1e-3) / 1e9, "peak_hbm_gbs": PEAK_HBM_GBS,
                          "traffic": pmc_traffic("tsdf", (z1 - z0) / R),
                          "traffic_unit": "bytes per step (all frame-chunk launches, profiles/r1/traffic.json)"},
             "updated_voxel_frac": float((Wt[z0:z1] > 0).float().mean().item()),
-        }]
+        }
         del depth, T, Wt
         torch.cuda.empty_cache()
+        if cpu:
+            tsdf["cpu_baseline"] = tsdf_cpu_leg(syn)
+        result["secondary"] = [tsdf]
 
         # ---------------- BA: DLT + residual + FD Jacobian ------------------
-        result["secondary"].append(ba_line(sfm, syn, device, args, barrier))
+        ba = ba_line(sfm, syn, device, args, barrier, cpu=cpu)
+        result["secondary"].append(ba)
 
-    # ---------------- voxel anchors + vq (N=1 only; rays / obs are independent) --
-    if not args.skip_secondary and world == 1:
-        result["secondary"].extend(voxel_and_vq_lines(sfm, syn, device, args, barrier,
-                                                      cpu=(not args.no_cpu_baseline)))
-        result["secondary"].append(verify_line(sfm, syn, device, args, barrier, cpu=(not args.no_cpu_baseline)))
-        result["secondary"].append(pnp_line(sfm, syn, device, args, barrier, cpu=(not args.no_cpu_baseline)))
-        result["secondary"].append(train_line(sfm, syn, device, args, barrier, cpu=(not args.no_cpu_baseline)))
+        if world == 1:
+            result["secondary"].append(c2_line(sfm, syn, device, args, barrier, cpu=cpu))
+            result["secondary"].append(exact_line(sfm, syn, device, args, barrier, cpu=cpu, int8_ms=ms_per_step))
+            result["secondary"].extend(voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=cpu))
+            result["secondary"].append(verify_line(sfm, syn, device, args, barrier, cpu=cpu))
+            result["secondary"].append(pnp_line(sfm, syn, device, args, barrier, cpu=cpu))
+            result["secondary"].append(train_line(sfm, syn, device, args, barrier, cpu=cpu))
 
     # ---------------- CPU baseline (rank 0, N=1 only) ------------------------
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rate, nd, tu = cpu_baseline_match(qcpu, pairs_all, baseline_sample(pairs_all))
-        result["cpu_baseline"] = {
-            "value": rate, "unit": "pairs/s", "cores": blas_threads(), "kind": "port",
-            "sample": f"{nd} of the {P} C3 pairs through oracle.match.bf_match_q (numpy f32 GEMM on exact "
-                      f"int8 values + top-2 + exact ratio), {tu:.1f}s; linear extrapolation to all pairs "
-                      f"= {P / rate:.0f}s",
-        }
+    if cpu:
+        match_cpu = match_cpu_leg(qcpu, pairs_all, sample)
+        match_cpu["sample"] += f"; linear extrapolation to all {P} pairs = {P / match_cpu['value']:.0f} s"
+        result["cpu_baseline"] = match_cpu
+        result["host"] = host_info()
         if "secondary" in result:
-            from oracle import voxel as ov
-            dep, ps, Kk = syn.tsdf_scene(3, syn.IMG_H, syn.IMG_W, device="cpu")
-            R = TSDF_R
-            t0 = time.perf_counter()
-            ov.tsdf_integrate(np.zeros((R, R, R), np.float32), np.zeros((R, R, R), np.float32), dep.numpy(),
-                              ps.numpy(), Kk.numpy(), (-1.2,) * 3, (1.2,) * 3, np.float32(3 * 2.4 / (R - 1)))
-            dt = time.perf_counter() - t0
-            result["secondary"][0]["cpu_baseline"] = {
-                "value": R ** 3 * 3 / dt / 1e6, "unit": "Mvoxel-updates/s", "cores": 1, "kind": "port",
-                "sample": f"3 of 257 frames through oracle.voxel.tsdf_integrate (numpy f32), {dt:.1f}s"}
+            comp = composite_line(result, match_cpu, result["secondary"][1], result["secondary"][0])
+            if comp is not None:
+                result["secondary"].insert(0, comp)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if comm is not None:
+        comm.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -150,8 +150,11 @@ def render(grid, bmin, bmax, mask_mode, rays_o, rays_d, z) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------
-def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
+def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None, grid_depth=None):
     """Build-defined TSDF update, in place on copies; returns (T, Wt).
+
+    ``grid_depth``: when given, T/Wt hold only the z-slices [z0, z1) of a grid
+    of that depth (the slab a CPU worker thread owns), else the whole grid.
 
     Every f32 operation below is one IEEE round-to-nearest step, in the order
     written (the HIP kernel tsdf_kernel computes exactly these, two voxels per
@@ -166,6 +169,12 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
     T = np.array(T, F32, copy=True)
     Wt = np.array(Wt, F32, copy=True)
     D, H, W = T.shape
+    slab_only = grid_depth is not None
+    if slab_only:
+        z1 = z0 + D if z1 is None else z1
+        if z1 - z0 != D:
+            raise ValueError("slab arrays must hold z1 - z0 slices")
+        D = int(grid_depth)
     z1 = D if z1 is None else z1
     mn = np.asarray(bmin, F32).ravel()
     mx = np.asarray(bmax, F32).ravel()
@@ -182,7 +191,7 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
     tr = F32(trunc)
     inv_tr = F32(1) / tr
     big, zlo, zhi = F32(2.0 ** 60), F32(2.0 ** -60), F32(2.0 ** 60)
-    Ts, Ws = T[z0:z1], Wt[z0:z1]
+    Ts, Ws = (T, Wt) if slab_only else (T[z0:z1], Wt[z0:z1])
     for f in range(F):
         P = poses[f]
         with np.errstate(invalid="ignore"):
@@ -209,6 +218,8 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None):
         Tn = (Ts * Ws + ts) / (Ws + F32(1))
         Ts = np.where(ok, Tn, Ts).astype(F32)
         Ws = np.where(ok, Ws + F32(1), Ws).astype(F32)
+    if slab_only:
+        return Ts, Ws
     T[z0:z1] = Ts
     Wt[z0:z1] = Ws
     return T, Wt

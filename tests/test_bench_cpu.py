@@ -1,0 +1,57 @@
+"""CPU checks of bench.py's CPU-baseline legs (BASELINE.md §2 methodology) and of
+the oracle's z-slab mode they use for the all-threads TSDF run."""
+import importlib
+
+import numpy as np
+
+import bench
+from oracle import voxel as ov
+
+syn = importlib.import_module("3d_reconstruction_amd.synthetic")
+
+
+def test_tsdf_oracle_slab_mode_equals_whole_grid():
+    depth, poses, K = syn.tsdf_scene(3, 40, 56, focal=50.0, seed=31)
+    R = 24
+    args = (depth.numpy(), poses.numpy(), K.numpy(), (-1, -1, -1), (1, 1, 1), np.float32(0.25))
+    Tw, Ww = ov.tsdf_integrate(np.zeros((R, R, R), np.float32), np.zeros((R, R, R), np.float32), *args)
+    for z0, z1 in ((0, 7), (7, 16), (16, 24)):
+        Ts, Ws = ov.tsdf_integrate(np.zeros((z1 - z0, R, R), np.float32), np.zeros((z1 - z0, R, R), np.float32),
+                                   *args, z0=z0, z1=z1, grid_depth=R)
+        np.testing.assert_array_equal(Ts, Tw[z0:z1])
+        np.testing.assert_array_equal(Ws, Ww[z0:z1])
+    assert (Ww > 0).any()
+
+
+def test_cpu_leg_reports_both_thread_counts():
+    calls = []
+
+    def run(k, nt):
+        calls.append((k, nt))
+        np.linalg.norm(np.ones(1000))
+    leg = bench.cpu_leg(run, 8, 2, "units/s", "port", "toy", scale=10.0)
+    assert leg["cores"] == bench.host_threads()
+    assert leg["value"] > 0 and leg["value_1thread"] > 0
+    # 1 warm-up + 3 timed runs on each leg
+    assert calls == [(8, bench.host_threads())] * 4 + [(2, 1)] * 4
+    assert "median of 3" in leg["timing"]
+
+
+def test_pool_map_keeps_order():
+    assert bench.pool_map(lambda i: i * i, range(10), 4) == [i * i for i in range(10)]
+    assert bench.pool_map(lambda i: i + 1, [3, 1], 1) == [4, 2]
+
+
+def test_composite_line_arithmetic():
+    res = {"config": {"pairs": 100}, "ms_per_step": 10.0}
+    match_cpu = {"value": 10.0, "value_1thread": 1.0, "cores": 16}
+    ba = {"ms_per_step": 1.0, "cpu_baseline": {"value": bench.BA_PAIRS * bench.BA_OBS / 2.0,
+                                               "value_1thread": bench.BA_PAIRS * bench.BA_OBS / 4.0}}
+    upd = bench.TSDF_R ** 3 * bench.TSDF_F / 1e6
+    tsdf = {"ms_per_step": 9.0, "cpu_baseline": {"value": upd / 3.0, "value_1thread": upd / 6.0}}
+    c = bench.composite_line(res, match_cpu, ba, tsdf)
+    assert abs(c["gpu_s"] - 0.02) < 1e-12
+    assert abs(c["cpu_s"] - (10.0 + 2.0 + 3.0)) < 1e-9
+    assert abs(c["value"] - 15.0 / 0.02) < 1e-6
+    assert abs(c["cpu_s_1thread"] - (100.0 + 4.0 + 6.0)) < 1e-9
+    assert bench.composite_line(res, None, ba, tsdf) is None
