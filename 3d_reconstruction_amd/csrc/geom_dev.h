@@ -184,8 +184,26 @@ __device__ inline void null_vector_jacobi4(double (&R)[4][4], double* y) {
             for (int r = 0; r < 4; ++r) y[r] = V[k][r];
 }
 
-__device__ inline void dlt_point(const double* P0, const double* P1, double x0, double y0, double x1, double y1,
-                                 double* Xout) {
+// 1/x and sqrt(x) on v_rcp_f64 / v_rsq_f64 with two Newton steps (within an ulp;
+// the IEEE sequences cost ~3x the latency): the FAST paths of the DLT list pass
+__device__ __forceinline__ double rcp_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return fma(fma(-x, r, 1.0), r, r);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+    r = r * fma(-0.5 * x * r, r, 1.5);
+    return r * fma(-0.5 * x * r, r, 1.5);
+}
+__device__ __forceinline__ double sqrt_nr(double x) { return x > 0.0 ? x * rsq_nr(x) : 0.0; }
+
+// Householder QR of the 6x4 DLT system: R (upper 4x4; A^T A = R^T R), rmax = max |R_kk|.
+// FAST: Newton reciprocal / square root instead of the IEEE sequences (dlt_point,
+// which recoverPose also uses, keeps the IEEE ones).
+template <bool FAST = false>
+__device__ inline void dlt_qr(const double* P0, const double* P1, double x0, double y0, double x1, double y1,
+                              double (&R)[4][4], double& rmax) {
     const double* Pv[2] = {P0, P1};
     const double px[2] = {x0, x1};
     const double py[2] = {y0, y1};
@@ -199,13 +217,13 @@ __device__ inline void dlt_point(const double* P0, const double* P1, double x0, 
             A[3 * v + 1][k] = py[v] * p2 - p1;
             A[3 * v + 2][k] = px[v] * p1 - py[v] * p0;
         }
-    double rmax = 0;
+    rmax = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         double nrm2 = 0;
 #pragma unroll
         for (int r = k; r < 6; ++r) nrm2 += A[r][k] * A[r][k];
-        const double nrm = sqrt(nrm2);
+        const double nrm = FAST ? sqrt_nr(nrm2) : sqrt(nrm2);
         const double alpha = (A[k][k] >= 0) ? -nrm : nrm;
         double v[6];
 #pragma unroll
@@ -214,7 +232,7 @@ __device__ inline void dlt_point(const double* P0, const double* P1, double x0, 
         double vn2 = 0;
 #pragma unroll
         for (int r = k; r < 6; ++r) vn2 += v[r] * v[r];
-        const double beta = (vn2 > 0) ? 2.0 / vn2 : 0.0;
+        const double beta = (vn2 > 0) ? (FAST ? 2.0 * rcp_nr(vn2) : 2.0 / vn2) : 0.0;
 #pragma unroll
         for (int c = k; c < 4; ++c) {
             double sdot = 0;
@@ -226,11 +244,16 @@ __device__ inline void dlt_point(const double* P0, const double* P1, double x0, 
         }
         rmax = fmax(rmax, fabs(A[k][k]));
     }
-    double R[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c < 4; ++c) R[r][c] = (c >= r) ? A[r][c] : 0.0;
+}
+
+__device__ inline void dlt_point(const double* P0, const double* P1, double x0, double y0, double x1, double y1,
+                                 double* Xout) {
+    double R[4][4], rmax;
+    dlt_qr(P0, P1, x0, y0, x1, y1, R, rmax);
     double y[4];
     bool done = false;
     if (fabs(R[3][3]) <= 1e-15 * rmax && fabs(R[2][2]) > 1e-15 * rmax) {  // exact null vector

@@ -22,6 +22,350 @@ __device__ __forceinline__ double fd_step(double x) {
 }
 
 // ---------------------------------------------------------------------------
+// DLT, two passes (sfm.py:27, cv2.triangulatePoints).
+//
+// Fast pass (dlt_normal_kernel, one lane per observation, 72 VGPRs): the
+// null vector of A (6x4) is the eigenvector of the smallest eigenvalue of the
+// normal matrix M = A^T A (10 distinct sums of the 6 rank-1 row products).
+// M = L D L^T (no pivoting; M is positive semi-definite), then inverse
+// iteration started from L^-T e4 (= M^-1 applied to L e4), normalising each
+// iterate, until two iterates agree to 1e-13 (factor lambda4/lambda3 per step:
+// median 2e-7 on the C3 scene, so 2-3 steps).  Forming M squares A's
+// condition, so a lane is kept only if a lower bound on lambda3 (the leading
+// 3x3 block's smallest eigenvalue >= 1 / trace(M3^-1), by interlacing) is at
+// least 1e-7 trace(M): the eigenvector's perturbation is then below ~1e-9.
+// Lanes that fail either test (~1.2 % of C3 observations: small-baseline
+// points whose lambda3 is tiny or close to lambda4) go to their wave's slot
+// list, and the list pass decides them with the backward-stable Householder QR
+// and a three-vector block inverse iteration (dlt_point_qr3; tried and dropped:
+// a Rayleigh-quotient iteration on M for the slow-converging ones, 1.7e-8 off
+// the SVD where lambda4/lambda3 -> 1 from M's rounding, and a two-vector block,
+// 2e-7 off where sigma2 ~ sigma3), and with geom_dev.h's dlt_point (inverse
+// iteration + 4x4 Jacobi) what that cannot decide.
+constexpr int kDltNormalIters = 6;
+constexpr double kDltLam3Floor = 1e-7;
+
+typedef const double __attribute__((address_space(4))) const_f64;   // constant space: uniform -> s_load
+
+// M = A^T A: m = {00, 01, 02, 03, 11, 12, 13, 22, 23, 33}
+template <class PT>
+__device__ __forceinline__ void dlt_normal_matrix(PT Pa, double xa, double ya, double xb, double yb, double (&m)[10]) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) m[k] = 0.0;
+    auto acc = [&](double r0, double r1, double r2, double r3) {
+        m[0] = fma(r0, r0, m[0]); m[1] = fma(r0, r1, m[1]); m[2] = fma(r0, r2, m[2]); m[3] = fma(r0, r3, m[3]);
+        m[4] = fma(r1, r1, m[4]); m[5] = fma(r1, r2, m[5]); m[6] = fma(r1, r3, m[6]);
+        m[7] = fma(r2, r2, m[7]); m[8] = fma(r2, r3, m[8]); m[9] = fma(r3, r3, m[9]);
+    };
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+        const PT Q = Pa + 12 * v;
+        const double x = v ? xb : xa, y = v ? yb : ya;
+        // rows x p2 - p0, y p2 - p1, x p1 - y p0 (cvTriangulatePoints matrA)
+        acc(fma(x, Q[8], -Q[0]), fma(x, Q[9], -Q[1]), fma(x, Q[10], -Q[2]), fma(x, Q[11], -Q[3]));
+        acc(fma(y, Q[8], -Q[4]), fma(y, Q[9], -Q[5]), fma(y, Q[10], -Q[6]), fma(y, Q[11], -Q[7]));
+        acc(fma(x, Q[4], -y * Q[0]), fma(x, Q[5], -y * Q[1]), fma(x, Q[6], -y * Q[2]), fma(x, Q[7], -y * Q[3]));
+        // the sums are complete here: without this the compiler sinks the off-diagonal
+        // sums to their first use and keeps all 24 row entries live (110 VGPRs)
+        asm volatile("" : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]), "+v"(m[3]), "+v"(m[4]), "+v"(m[5]), "+v"(m[6]),
+                     "+v"(m[7]), "+v"(m[8]), "+v"(m[9]));
+    }
+}
+
+// L D L^T of M - shift I (unit lower L: l10 l20 l30 l21 l31 l32; inverse pivots i0..i3)
+struct Ldl {
+    double l10, l20, l30, l21, l31, l32, i0, i1, i2, i3;
+    bool pd3;      // the leading 3x3 pivots are positive
+    double t3;     // trace of the leading 3x3 block's inverse (bounds its smallest eigenvalue)
+};
+
+__device__ __forceinline__ Ldl dlt_ldl(const double (&m)[10], double shift, double floor3) {
+    Ldl f;
+    const double d0 = m[0] - shift;
+    f.i0 = rcp_nr(d0);
+    f.l10 = m[1] * f.i0; f.l20 = m[2] * f.i0; f.l30 = m[3] * f.i0;
+    const double d1 = fma(-f.l10, m[1], m[4] - shift);
+    f.i1 = rcp_nr(d1);
+    const double a21 = fma(-f.l20, m[1], m[5]), a31 = fma(-f.l30, m[1], m[6]);
+    f.l21 = a21 * f.i1; f.l31 = a31 * f.i1;
+    const double d2 = fma(-f.l21, a21, fma(-f.l20, m[2], m[7] - shift));
+    f.i2 = rcp_nr(d2);
+    const double a32 = fma(-f.l31, a21, fma(-f.l30, m[2], m[8]));
+    f.l32 = a32 * f.i2;
+    const double d3 = fma(-f.l32, a32, fma(-f.l31, a31, fma(-f.l30, m[3], m[9] - shift)));
+    // d3 ~ lambda4 - shift may round to ~0: keep its sign, floor its size at the rounding level of M
+    f.i3 = rcp_nr(d3 < 0.0 ? fmin(d3, -floor3) : fmax(d3, floor3));
+    f.pd3 = d0 > 0.0 && d1 > 0.0 && d2 > 0.0;
+    const double g = fma(f.l10, f.l21, -f.l20);
+    f.t3 = fma(fma(g, g, fma(f.l21, f.l21, 1.0)), f.i2, fma(fma(f.l10, f.l10, 1.0), f.i1, f.i0));
+    return f;
+}
+
+// One inverse-iteration step on a unit iterate: y <- (M - shift I)^-1 y, renormalised
+// (sign aligned with the old y: an indefinite shifted matrix may flip it);
+// returns |y_new - y_old|^2.
+__device__ __forceinline__ double dlt_inv_step(const Ldl& f, double& y0, double& y1, double& y2, double& y3) {
+    const double o0 = y0, o1 = y1, o2 = y2, o3 = y3;
+    // L w = o, w /= d, L^T z = w
+    const double w0 = o0 * f.i0;
+    const double u1 = fma(-f.l10, o0, o1);
+    const double w1 = u1 * f.i1;
+    const double v2 = fma(-f.l21, u1, fma(-f.l20, o0, o2));
+    const double w2 = v2 * f.i2;
+    const double z3 = fma(-f.l32, v2, fma(-f.l31, u1, fma(-f.l30, o0, o3))) * f.i3;
+    const double z2 = fma(-f.l32, z3, w2);
+    const double z1 = fma(-f.l31, z3, fma(-f.l21, z2, w1));
+    const double z0 = fma(-f.l30, z3, fma(-f.l20, z2, fma(-f.l10, z1, w0)));
+    double s2 = rsq_nr(fma(z0, z0, fma(z1, z1, fma(z2, z2, z3 * z3))));
+    if (fma(z0, o0, fma(z1, o1, fma(z2, o2, z3 * o3))) < 0.0) s2 = -s2;
+    y0 = z0 * s2;
+    y1 = z1 * s2;
+    y2 = z2 * s2;
+    y3 = z3 * s2;
+    const double e0 = y0 - o0, e1 = y1 - o1, e2 = y2 - o2, e3 = y3 - o3;
+    return fma(e0, e0, fma(e1, e1, fma(e2, e2, e3 * e3)));
+}
+
+__device__ __forceinline__ bool dlt_store_unit(double y0, double y1, double y2, double y3, double* Xout) {
+    const double nn = fma(y0, y0, fma(y1, y1, fma(y2, y2, y3 * y3)));
+    if (!(nn > 0.0) || !(nn < 1e300)) return false;
+    const double sc = (y3 < 0 ? -1.0 : 1.0) / sqrt(nn);
+    Xout[0] = y0 * sc;
+    Xout[1] = y1 * sc;
+    Xout[2] = y2 * sc;
+    Xout[3] = y3 * sc;
+    return true;
+}
+
+// 0: decided (Xout written); 1: lambda3 bound met but not converged; 2: the QR path decides
+__device__ __forceinline__ int dlt_point_normal(const const_f64* __restrict__ Pa, double xa, double ya, double xb,
+                                                double yb, double* Xout) {
+    double m[10];
+    dlt_normal_matrix(Pa, xa, ya, xb, yb, m);
+    // branch-free up to the iteration (an early exit lets the compiler sink the
+    // off-diagonal sums past it and keep all 24 row entries live)
+    const double tr = (m[0] + m[4]) + (m[7] + m[9]);
+    const Ldl f = dlt_ldl(m, 0.0, 1e-30 * tr);
+    const bool good = f.pd3 && tr < 1e300 && f.t3 * (kDltLam3Floor * tr) <= 1.0;
+    double y0, y1, y2, y3 = 1.0;                        // L^T y = e4, normalised
+    y2 = -f.l32;
+    y1 = fma(-f.l21, y2, -f.l31);
+    y0 = fma(-f.l10, y1, fma(-f.l20, y2, -f.l30));
+    const double s0 = rsq_nr(fma(y0, y0, fma(y1, y1, fma(y2, y2, 1.0))));
+    y0 *= s0; y1 *= s0; y2 *= s0; y3 = s0;
+    bool done = false;
+#pragma unroll 1
+    for (int it = 0; it < kDltNormalIters && good && !done; ++it) done = dlt_inv_step(f, y0, y1, y2, y3) <= 1e-26;
+    if (!good) return 2;
+    if (!done) return 1;
+    return dlt_store_unit(y0, y1, y2, y3, Xout) ? 0 : 2;
+}
+
+// Listed observations: Householder QR of A (backward stable: no squaring of the
+// condition), then a three-vector block inverse iteration with R's triangular
+// solves and a 3x3 Rayleigh-Ritz.  On the C3 scene sigma1 (the x p2 - y p1
+// rows, ~x f) exceeds sigma2..sigma4 (~f) by ~1e3, so the block {v2, v3, v4}
+// converges at (sigma2/sigma1)^2 ~ 1e-5 per step whatever the sigma3/sigma4 gap
+// (a two-vector block converges at (sigma3/sigma2)^2, ~0.5 on the listed
+// points), and B^T B for B = R Z holds only lambda2..lambda4, so forming it
+// costs no accuracy; cyclic Jacobi on that 3x3 finishes in a few sweeps.
+// Fixed cost, no 4x4 Jacobi.  false: dlt_point decides.
+__device__ inline bool dlt_point_qr3(const double* P0, const double* P1, double xa, double ya, double xb, double yb,
+                                     double* Xout) {
+    double R[4][4], rmax;
+    dlt_qr<true>(P0, P1, xa, ya, xb, yb, R, rmax);
+    double id[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (!(fabs(R[k][k]) > 1e-15 * rmax) || !(rmax < 1e300)) return false;
+        id[k] = rcp_nr(R[k][k]);
+    }
+    auto bsolve = [&](double (&z)[4]) {   // R z = z
+#pragma unroll
+        for (int r = 3; r >= 0; --r) {
+            double a = z[r];
+#pragma unroll
+            for (int c = r + 1; c < 4; ++c) a = fma(-R[r][c], z[c], a);
+            z[r] = a * id[r];
+        }
+    };
+    auto fsolve = [&](double (&z)[4]) {   // R^T z = z
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double a = z[r];
+#pragma unroll
+            for (int c = 0; c < r; ++c) a = fma(-R[c][r], z[c], a);
+            z[r] = a * id[r];
+        }
+    };
+    auto dot = [](const double (&u)[4], const double (&v)[4]) {
+        return fma(u[0], v[0], fma(u[1], v[1], fma(u[2], v[2], u[3] * v[3])));
+    };
+    auto unit = [&](double (&u)[4]) {
+        const double sc = rsq_nr(dot(u, u));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] *= sc;
+    };
+    auto drop = [&](const double (&u)[4], double (&v)[4]) {   // v -= (u.v) u, twice
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+            const double c = dot(u, v);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = fma(-c, u[k], v[k]);
+        }
+    };
+    double Z[3][4] = {{0, 0, 0, 1}, {0, 0, 1, 0}, {0, 1, 0, 0}};   // R^-1 [e4 e3 e2]
+    auto orth = [&]() {
+        unit(Z[0]);
+        drop(Z[0], Z[1]);
+        unit(Z[1]);
+        drop(Z[0], Z[2]);
+        drop(Z[1], Z[2]);
+        unit(Z[2]);
+    };
+#pragma unroll
+    for (int k = 0; k < 3; ++k) bsolve(Z[k]);
+#pragma unroll 1
+    for (int it = 0; it < 2; ++it) {   // 2 steps: 1e-13 on the C3 and test scenes (1 step: 8e-10)
+        orth();
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { fsolve(Z[k]); bsolve(Z[k]); }
+    }
+    orth();
+    double B[3][4];   // B = R Z
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double a = 0.0;
+#pragma unroll
+            for (int c = r; c < 4; ++c) a = fma(R[r][c], Z[k][c], a);
+            B[k][r] = a;
+        }
+    double G[3][3], V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = i; j < 3; ++j) G[i][j] = G[j][i] = dot(B[i], B[j]);
+    for (int sweep = 0; sweep < 12; ++sweep) {
+        bool rotated = false;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int q = p + 1; q < 3; ++q) {
+                const double gpq = G[p][q];
+                if (fabs(gpq) <= 1e-18 * sqrt_nr(fabs(G[p][p] * G[q][q])) || gpq == 0.0) continue;
+                rotated = true;
+                const double zeta = (G[q][q] - G[p][p]) * (0.5 * rcp_nr(gpq));
+                const double t = (zeta >= 0.0 ? 1.0 : -1.0) * rcp_nr(fabs(zeta) + sqrt_nr(fma(zeta, zeta, 1.0)));
+                const double c = rsq_nr(fma(t, t, 1.0)), sn = t * c;
+                // G <- J^T G J with J = [[c, sn], [-sn, c]] on (p, q)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double gkp = G[k][p], gkq = G[k][q];
+                    G[k][p] = c * gkp - sn * gkq;
+                    G[k][q] = sn * gkp + c * gkq;
+                }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double gpk = G[p][k], gqk = G[q][k];
+                    G[p][k] = c * gpk - sn * gqk;
+                    G[q][k] = sn * gpk + c * gqk;
+                }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double vkp = V[k][p], vkq = V[k][q];
+                    V[k][p] = c * vkp - sn * vkq;
+                    V[k][q] = sn * vkp + c * vkq;
+                }
+            }
+        if (!rotated) break;
+    }
+    int best = 0;
+#pragma unroll
+    for (int k = 1; k < 3; ++k)
+        if (G[k][k] < G[best][best]) best = k;
+    double u[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) u[k] = best == 0 ? V[k][0] : (best == 1 ? V[k][1] : V[k][2]);
+    double y[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = fma(u[0], Z[0][r], fma(u[1], Z[1][r], u[2] * Z[2][r]));
+    return dlt_store_unit(y[0], y[1], y[2], y[3], Xout);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void dlt_normal_kernel(const double* __restrict__ P,
+                                                         const int32_t* __restrict__ pair_of_obs,
+                                                         const double* __restrict__ x0, const double* __restrict__ x1,
+                                                         int64_t n, double* __restrict__ X4,
+                                                         unsigned* __restrict__ slots, unsigned* __restrict__ counts) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t wave = i >> 6;   // global wave index (n_waves = ceil(n / 64) slots of 64)
+    if (i >= n) return;
+    const int pr = pair_of_obs ? pair_of_obs[i] : 0;
+    const double xa = x0[i], ya = x0[n + i], xb = x1[i], yb = x1[n + i];
+    double X[4];
+    int st = 2;
+    // waterfall over the wave's pairs (sorted observations: one or two per wave),
+    // so each pair's projection matrices are wave-uniform scalar loads
+    while (true) {
+        const int cur = __builtin_amdgcn_readfirstlane(pr);
+        int cs = cur;
+        asm volatile("" : "+s"(cs));   // an opaque SGPR copy: under pr == cur the compiler would address with pr
+        if (pr == cur) {
+            st = dlt_point_normal((const const_f64*)(P + (size_t)cs * 24), xa, ya, xb, yb, X);
+            break;
+        }
+    }
+    if (st == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) X4[(int64_t)r * n + i] = X[r];
+    }
+    // the undecided lanes go to this wave's own 64-entry slot, the count to counts[wave]: no atomics (one returning
+    // atomic per wave on a shared counter serialised the kernel: 101 us, 71 % of
+    // wave cycles waiting)
+    const unsigned long long m = __ballot(st != 0);
+    const int lane = threadIdx.x & 63;
+    if (st != 0)
+        slots[(wave << 6) + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)i;
+    if (lane == __ffsll((long long)__ballot(true)) - 1) counts[wave] = (unsigned)__popcll(m);
+}
+
+// List pass: one 64-lane workgroup per 64 source waves gathers their slots
+// densely into LDS (prefix sum of the counts across lanes); each lane then
+// decides one gathered observation at a time.
+__global__ __launch_bounds__(64) void dlt_list_kernel(const double* __restrict__ P,
+                                                      const int32_t* __restrict__ pair_of_obs,
+                                                      const double* __restrict__ x0, const double* __restrict__ x1,
+                                                      int64_t n, double* __restrict__ X4,
+                                                      const unsigned* __restrict__ slots,
+                                                      const unsigned* __restrict__ counts, int64_t n_waves) {
+    __shared__ unsigned items[64 * 64];
+    const int lane = threadIdx.x;
+    const int64_t w = (int64_t)blockIdx.x * 64 + lane;
+    const unsigned c = w < n_waves ? counts[w] : 0u;
+    unsigned pre = c;   // inclusive scan over the 64 lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned t = __shfl_up(pre, d);
+        if (lane >= d) pre += t;
+    }
+    const unsigned total = __shfl(pre, 63);
+    if (total == 0) return;
+    for (unsigned t = 0; t < c; ++t) items[pre - c + t] = slots[(w << 6) + t];
+    __syncthreads();
+    for (unsigned k = lane; k < total; k += 64) {
+        const int64_t i = items[k];
+        const int pr = pair_of_obs ? pair_of_obs[i] : 0;
+        double X[4];
+        const double *Pa = P + (size_t)pr * 24, xa = x0[i], ya = x0[n + i], xb = x1[i], yb = x1[n + i];
+        if (!dlt_point_qr3(Pa, Pa + 12, xa, ya, xb, yb, X)) dlt_point(Pa, Pa + 12, xa, ya, xb, yb, X);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) X4[(int64_t)r * n + i] = X[r];
+    }
+}
+
+// the QR path for every observation (SFMHIP_DLT_QR=1 A/B runs; scratch failure)
 __global__ void dlt_kernel(const double* __restrict__ P, const int32_t* __restrict__ pair_of_obs,
                            const double* __restrict__ x0, const double* __restrict__ x1, int64_t n,
                            double* __restrict__ X4) {
@@ -187,8 +531,26 @@ extern "C" int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_ob
     SFMHIP_REQUIRE(P && x0 && x1 && X4, "sfmhip_triangulate_dlt: null pointer");
     SFMHIP_REQUIRE(n >= 0, "sfmhip_triangulate_dlt: negative n");
     if (n == 0) return SFMHIP_OK;
-    hipLaunchKernelGGL(dlt_kernel, dim3(ceil_div(n, 128)), dim3(128), 0, as_stream(stream), P,
-                       pair_of_obs, x0, x1, n, X4);
+    hipStream_t st = as_stream(stream);
+    unsigned* slots = nullptr;   // [n_waves][64] listed observations + [n_waves] counts
+    const int64_t n_waves = ceil_div(n, 64);
+    const char* qr = std::getenv("SFMHIP_DLT_QR");
+    if (!(qr && std::atoi(qr) != 0) && n < ((int64_t)1 << 31) &&
+        scratch_alloc((void**)&slots, (size_t)n_waves * 65 * sizeof(unsigned), st) == hipSuccess) {
+        unsigned* counts = slots + n_waves * 64;
+        hipLaunchKernelGGL(dlt_normal_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, P, pair_of_obs, x0, x1, n,
+                           X4, slots, counts);
+        int rc = check_launch("dlt_normal_kernel");
+        if (rc == SFMHIP_OK) {
+            hipLaunchKernelGGL(dlt_list_kernel, dim3((unsigned)ceil_div(n_waves, 64)), dim3(64), 0, st, P, pair_of_obs,
+                               x0, x1, n, X4, slots, counts, n_waves);
+            rc = check_launch("dlt_list_kernel");
+        }
+        (void)hipFreeAsync(slots, st);
+        return rc;
+    }
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(dlt_kernel, dim3(ceil_div(n, 128)), dim3(128), 0, st, P, pair_of_obs, x0, x1, n, X4);
     return check_launch("dlt_kernel");
 }
 

@@ -176,16 +176,23 @@ def pool_map(fn, items, threads: int):
 # ---------------------------------------------------------------------------
 def match_cpu_leg(qcpu, pairs, sample, n_one=3):
     """Oracle (numpy GEMM form on exact int8 values + top-2 + exact ratio) on a
-    spread sample of the same pairs; BLAS threads = the leg's threads."""
+    spread sample of the same pairs.  All threads: pairs over a thread pool,
+    one BLAS thread per worker (numpy drops the GIL in the GEMM and the
+    reductions; one pair at a time on a 16-thread BLAS leaves the top-2
+    passes single-threaded: 83 vs 108 ms per pair for 16 vs 1 threads in
+    profiles/r2/bench.json)."""
     from oracle import match as om
 
+    def one(i):
+        a, b = (int(v) for v in pairs[i])
+        om.bf_match_q(qcpu[a], qcpu[b], (3, 4))
+
     def run(k, nt):
-        for i in sample[:k]:
-            a, b = (int(v) for v in pairs[i])
-            om.bf_match_q(qcpu[a], qcpu[b], (3, 4))
+        with blas_limit(1):
+            pool_map(one, sample[:k], nt)
     return cpu_leg(run, len(sample), n_one, "pairs/s", "port",
-                   f"oracle.match.bf_match_q on {len(sample)} (all threads) / {n_one} (1 thread) pairs spread "
-                   f"over the pair list")
+                   f"oracle.match.bf_match_q on {len(sample)} pairs over a thread pool (all threads) / {n_one} "
+                   f"pairs (1 thread), spread over the pair list")
 
 
 def spread(n_total: int, n: int):
@@ -763,6 +770,12 @@ def main():
     ap.add_argument("--rehearse-overlap", action="store_true",
                     help="N=1 rehearsal of the N>1 path: a one-rank RCCL communicator + the overlapped all-gather")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: RCCL (version banner at communicator
+    # init) and other libraries print to fd 1, so fd 1 becomes stderr for the run
+    # and the result goes to a private copy of the original stdout
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -937,7 +950,7 @@ def main():
                 result["secondary"].insert(0, comp)
 
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=out, flush=True)
     if comm is not None:
         comm.close()
     if dist.is_initialized():

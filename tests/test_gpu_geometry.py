@@ -60,6 +60,40 @@ def test_triangulate_batched_pairs(sfm, gpu):
         np.testing.assert_allclose((X4[:3, sl] / X4[3, sl]).T, (ref[:3] / ref[3]).T, rtol=1e-8)
 
 
+def test_triangulate_normal_and_qr_paths(sfm, gpu, monkeypatch):
+    """The normal-equation fast pass + QR list pass (default) and the QR path for
+    every observation (SFMHIP_DLT_QR=1) agree with the oracle and each other,
+    including small-baseline pairs whose observations go to the QR list."""
+    s = syn.ba_scene(16, 1000, seed=14)
+    # pairs 0-3: shrink the second camera's baseline so lambda3 ~ lambda4 for many points
+    P = s["P"].copy()
+    rng = np.random.default_rng(3)
+    for p in range(4):
+        P[p, 1] = P[p, 0] + 1e-3 * rng.normal(size=(3, 4)) * np.abs(P[p, 0]).max()
+    dv = gpu
+    args = (torch.from_numpy(P).to(dv), torch.from_numpy(s["pair_of_obs"]).to(dv),
+            torch.from_numpy(s["x0"]).to(dv), torch.from_numpy(s["x1"]).to(dv))
+    fast = sfm.triangulate_batched(*args).cpu().numpy()
+    monkeypatch.setenv("SFMHIP_DLT_QR", "1")
+    qr = sfm.triangulate_batched(*args).cpu().numpy()
+    monkeypatch.delenv("SFMHIP_DLT_QR")
+    for p in range(4, 16):      # well-conditioned pairs: both paths equal the oracle
+        sl = slice(p * 1000, (p + 1) * 1000)
+        ref = og.triangulate_points(P[p, 0], P[p, 1], s["x0"][:, sl], s["x1"][:, sl])
+        for got in (fast[:, sl], qr[:, sl]):
+            np.testing.assert_allclose((got[:3] / got[3]).T, (ref[:3] / ref[3]).T, rtol=1e-4)
+            assert np.abs(got - ref).max() < 1e-9          # unit null vectors (w >= 0)
+    # small-baseline pairs: the fast pass lists most of them (RQI on the normal
+    # matrix or the QR path decide them); the unit null vectors still agree
+    for p in range(4):
+        sl = slice(p * 1000, (p + 1) * 1000)
+        ref = og.triangulate_points(P[p, 0], P[p, 1], s["x0"][:, sl], s["x1"][:, sl])
+        assert np.abs(fast[:, sl] - ref).max() < 1e-6
+    assert np.abs(fast - qr).max() < 1e-6
+    np.testing.assert_allclose(np.linalg.norm(fast, axis=0), 1.0, rtol=1e-12)
+    assert (fast[3] >= 0).all()
+
+
 def _x_of(s, p, n):
     return np.concatenate([s["cam"][p], s["X"][p * n:(p + 1) * n].ravel()])
 
