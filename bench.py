@@ -732,7 +732,8 @@ def composite_line(result, match_cpu, ba, tsdf):
     """North-star composite (BASELINE.json): C3 all-pairs match step + C3 DLT/BA
     evaluation (256 pairs x 4096 obs) + C5 TSDF step on 1 MI355X against the
     summed CPU wall-clock of the same three workloads (each extrapolated from
-    its timed sample), target >= 50x."""
+    its timed sample, the faster of its all-threads and 1-thread runs), target
+    >= 50x; value_1thread: every CPU part on one thread."""
     P = result["config"]["pairs"]
     gpu_s = (result["ms_per_step"] + ba["ms_per_step"] + tsdf["ms_per_step"]) * 1e-3
     cb, ct = ba.get("cpu_baseline"), tsdf.get("cpu_baseline")
@@ -743,14 +744,17 @@ def composite_line(result, match_cpu, ba, tsdf):
 
     def cpu_s(key):
         return P / match_cpu[key] + n_obs / cb[key] + upd / ct[key]
-    cpu_all, cpu_one = cpu_s("value"), cpu_s("value_1thread")
+
+    def best(leg):   # the faster of the two thread counts (GIL-bound legs run slower on the pool)
+        return max(leg["value"], leg["value_1thread"])
+    cpu_all = P / best(match_cpu) + n_obs / best(cb) + upd / best(ct)
+    cpu_one = cpu_s("value_1thread")
     return {"metric": "north-star composite speedup vs reference CPU path", "value": cpu_all / gpu_s, "unit": "x",
             "target": 50.0, "value_1thread": cpu_one / gpu_s, "gpu_s": gpu_s,
             "cpu_s": cpu_all, "cpu_s_1thread": cpu_one, "cores": match_cpu["cores"],
             "parts_s": {"gpu": {"match": result["ms_per_step"] * 1e-3, "ba": ba["ms_per_step"] * 1e-3,
                                 "tsdf": tsdf["ms_per_step"] * 1e-3},
-                        "cpu": {"match": P / match_cpu["value"], "ba": n_obs / cb["value"],
-                                "tsdf": upd / ct["value"]},
+                        "cpu": {"match": P / best(match_cpu), "ba": n_obs / best(cb), "tsdf": upd / best(ct)},
                         "cpu_1thread": {"match": P / match_cpu["value_1thread"], "ba": n_obs / cb["value_1thread"],
                                         "tsdf": upd / ct["value_1thread"]}},
             "config": {"workload": "C3 all-pairs matching (32,896 pairs) + C3 DLT + residual + FD Jacobian "

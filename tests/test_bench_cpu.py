@@ -53,5 +53,9 @@ def test_composite_line_arithmetic():
     assert abs(c["gpu_s"] - 0.02) < 1e-12
     assert abs(c["cpu_s"] - (10.0 + 2.0 + 3.0)) < 1e-9
     assert abs(c["value"] - 15.0 / 0.02) < 1e-6
+    # a part whose 1-thread run is faster counts at that rate
+    ba["cpu_baseline"]["value_1thread"] = bench.BA_PAIRS * bench.BA_OBS / 1.0
+    c = bench.composite_line(res, match_cpu, ba, tsdf)
+    assert abs(c["cpu_s"] - (10.0 + 1.0 + 3.0)) < 1e-9
     assert abs(c["cpu_s_1thread"] - (100.0 + 4.0 + 6.0)) < 1e-9
     assert bench.composite_line(res, None, ba, tsdf) is None
