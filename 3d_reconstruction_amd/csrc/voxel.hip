@@ -857,6 +857,97 @@ __global__ void tsdf_cam_kernel(const float* __restrict__ poses, const float* __
     for (int q = 0; q < 16; ++q) rec[f * 16 + q] = good ? r[q] : 0.f;
 }
 
+// Workgroup slot -> tile of the super-brick order: the 1-D grid is dealt
+// round-robin over the 8 XCDs (slot % 8), so XCD x fuses super-bricks x, x+8,
+// ... (il; spreads uneven culled work) or one contiguous range of them.
+__device__ __forceinline__ void tsdf_slot_tile(int slot, int nslots, int W, int H, const SuperBrick& SB, int& bx,
+                                               int& by, int& bz) {
+    const int nbx = (W + kTsdfTX - 1) / kTsdfTX, nby = (H + kTsdfTY - 1) / kTsdfTY;
+    const int nsx = (nbx + SB.x - 1) / SB.x, nsy = (nby + SB.y - 1) / SB.y;
+    const int sbn = SB.x * SB.y * SB.z;
+    int sb, in;
+    if (SB.il) {
+        const int j = slot / kNumXcd;
+        sb = (j / sbn) * kNumXcd + slot % kNumXcd;
+        in = j % sbn;
+    } else {
+        const int L = xcd_remap(slot, nslots);
+        sb = L / sbn;
+        in = L % sbn;
+    }
+    const int sx = sb % nsx, sy = (sb / nsx) % nsy, sz = sb / (nsx * nsy);
+    bx = sx * SB.x + in % SB.x;
+    by = sy * SB.y + (in / SB.x) % SB.y;
+    bz = sz * SB.z + in / (SB.x * SB.y);
+}
+
+// Longest-first order of the fusion's workgroups (per XCD class, so each slot
+// stays on the XCD its super-brick was dealt to): with few workgroups per CU
+// (a z-slab of an N-way split: ~2 rounds) the surface tiles, up to ~10x the
+// work of a free-space tile, otherwise land in the last round.
+//   tsdf_cost_kernel: per slot a cost bucket 0..63 from its tile's masks
+//     (4 x projected frames + free-space frames, over the 4 wave sub-tiles);
+//   tsdf_order_kernel: one workgroup per XCD class, stable counting sort of the
+//     class's slots by bucket, heaviest first: order[x + 8 k] = k-th slot.
+constexpr int kOrderBuckets = 64;
+__global__ __launch_bounds__(256) void tsdf_cost_kernel(int nslots, int W, int H, int D, int z0, int z1, SuperBrick SB,
+                                                        int F, int nw, const unsigned* __restrict__ cull,
+                                                        const unsigned* __restrict__ freem,
+                                                        unsigned char* __restrict__ bucket) {
+    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
+    const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
+    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += gridDim.x * blockDim.x) {
+        int bx, by, bz;
+        tsdf_slot_tile(s, nslots, W, H, SB, bx, by, bz);
+        unsigned cost = 0;
+        if (bx < ntx && by < nty && bz < ntz) {
+            const size_t base = ((((size_t)bz * nty + by) * ntx + bx) * kCullSub) * (size_t)nw;
+            for (int q = 0; q < kCullSub; ++q)
+                for (int w = 0; w < nw; ++w) {
+                    const unsigned live = F - 32 * w >= 32 ? ~0u : ((1u << (F - 32 * w)) - 1u);
+                    const unsigned c = cull[base + (size_t)q * nw + w], f = freem ? freem[base + (size_t)q * nw + w] : 0u;
+                    cost += 4u * __popc(live & ~c & ~f) + __popc(live & f & ~c);
+                }
+        }
+        bucket[s] = (unsigned char)min((unsigned)(kOrderBuckets - 1), cost * kOrderBuckets / (16u * F + 1u));
+    }
+}
+
+__global__ __launch_bounds__(256) void tsdf_order_kernel(int nslots, const unsigned char* __restrict__ bucket,
+                                                         unsigned* __restrict__ order) {
+    __shared__ unsigned short hist[kOrderBuckets][256];
+    __shared__ unsigned part[256];
+    const int x = blockIdx.x, t = threadIdx.x;
+    const int m = nslots > x ? (nslots - x + kNumXcd - 1) / kNumXcd : 0;   // slots x, x+8, ... of this class
+    const int per = (m + 255) / 256, j0 = min(m, t * per), j1 = min(m, j0 + per);
+    for (int b = 0; b < kOrderBuckets; ++b) hist[b][t] = 0;
+    for (int j = j0; j < j1; ++j) ++hist[bucket[x + kNumXcd * j]][t];
+    __syncthreads();
+    // exclusive scan over (bucket descending, thread): thread u owns entries [64u, 64u + 64)
+    unsigned run = 0;
+    for (int e = 64 * t; e < 64 * t + 64; ++e) run += hist[kOrderBuckets - 1 - e / 256][e % 256];
+    part[t] = run;
+    __syncthreads();
+    if (t == 0) {
+        unsigned acc = 0;
+        for (int u = 0; u < 256; ++u) { const unsigned v = part[u]; part[u] = acc; acc += v; }
+    }
+    __syncthreads();
+    run = part[t];
+    for (int e = 64 * t; e < 64 * t + 64; ++e) {
+        unsigned short& h = hist[kOrderBuckets - 1 - e / 256][e % 256];
+        const unsigned v = h;
+        h = (unsigned short)run;   // positions < m <= 65535
+        run += v;
+    }
+    __syncthreads();
+    for (int j = j0; j < j1; ++j) {
+        const int s = x + kNumXcd * j;
+        const unsigned pos = hist[bucket[s]][t]++;
+        order[x + kNumXcd * pos] = (unsigned)s;
+    }
+}
+
 // W may take k more exact +1 steps with T = 1 fixed: an integer in [0, 2^24 - 512]
 __device__ __forceinline__ bool w_runs(float w) { return w >= 0.f && w <= 0x1p24f - 512.f && w == truncf(w); }
 
@@ -873,27 +964,10 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
                                                    int Hd, int Wd, const float* __restrict__ rec, Bounds B,
                                                    float trunc, SuperBrick SB, const unsigned* __restrict__ cull,
                                                    const unsigned* __restrict__ freem, int nw, float free_ts,
-                                                   const float2* __restrict__ bmm, int nbu, int nbv) {
+                                                   const float2* __restrict__ bmm, int nbu, int nbv,
+                                                   const unsigned* __restrict__ order) {
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    if (SWZ) {
-        const int nbx = (W + kTsdfTX - 1) / kTsdfTX, nby = (H + kTsdfTY - 1) / kTsdfTY;
-        const int nsx = (nbx + SB.x - 1) / SB.x, nsy = (nby + SB.y - 1) / SB.y;
-        const int sbn = SB.x * SB.y * SB.z;
-        int sb, in;
-        if (SB.il) {   // XCD x fuses super-bricks x, x+8, x+16, ...: spreads uneven (culled) work
-            const int j = blockIdx.x / kNumXcd;
-            sb = (j / sbn) * kNumXcd + blockIdx.x % kNumXcd;
-            in = j % sbn;
-        } else {       // XCD x fuses one contiguous range of super-bricks
-            const int L = xcd_remap(blockIdx.x, gridDim.x);
-            sb = L / sbn;
-            in = L % sbn;
-        }
-        const int sx = sb % nsx, sy = (sb / nsx) % nsy, sz = sb / (nsx * nsy);
-        bx = sx * SB.x + in % SB.x;
-        by = sy * SB.y + (in / SB.x) % SB.y;
-        bz = sz * SB.z + in / (SB.x * SB.y);
-    }
+    if (SWZ) tsdf_slot_tile(order ? (int)order[blockIdx.x] : (int)blockIdx.x, gridDim.x, W, H, SB, bx, by, bz);
     const int l = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int x = bx * kTsdfTX + (l & 3) + 4 * ((l >> 4) & 1);
@@ -1544,6 +1618,17 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     }
     // per-voxel block test in the fusion kernel (with the free-space path; SFMHIP_TSDF_VOXTEST=0 off)
     const bool vox_test = cfree && env_int("SFMHIP_TSDF_VOXTEST", 1) != 0;
+    // longest-first workgroup order (SFMHIP_TSDF_ORDER=0 off): needs the masks and the 1-D slot grid;
+    // bucket sort positions are 16-bit, so at most 65535 slots per XCD class
+    unsigned* ord = nullptr;
+    unsigned char* obucket = nullptr;
+    if (cmask && swz && !stats && env_int("SFMHIP_TSDF_ORDER", 1) != 0 && (int64_t)grid.x <= 65535LL * kNumXcd) {
+        if (scratch_alloc((void**)&ord, (size_t)grid.x * (sizeof(unsigned) + 1), st) == hipSuccess)
+            obucket = reinterpret_cast<unsigned char*>(ord + grid.x);
+        else
+            ord = nullptr;
+        (void)hipGetLastError();
+    }
     // frame chunks run in order on the stream, so per-voxel update order is kept
     int rc = SFMHIP_OK;
     for (int f0 = 0; f0 < F; f0 += chunk) {
@@ -1617,16 +1702,22 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                                0, st, cmask, cfree, nsub * nwf, free_env == 4 ? 1 : 0);
             fmask = nullptr;
         }
+        if (ord) {   // longest-first workgroup order within each XCD class (bit-identical results)
+            hipLaunchKernelGGL(tsdf_cost_kernel, dim3((unsigned)std::min<int64_t>(ceil_div((int64_t)grid.x, 256), 1024)),
+                               dim3(256), 0, st, (int)grid.x, W, H, D, z0, z1, sb, nf, nwf, cmask, cfree, obucket);
+            hipLaunchKernelGGL(tsdf_order_kernel, dim3(kNumXcd), dim3(256), 0, st, (int)grid.x, obucket, ord);
+        }
         if (swz)
             hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, ord);
         else
             hipLaunchKernelGGL(tsdf_kernel<false>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, nullptr);
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }
     (void)hipFreeAsync(rec, st);
+    if (ord) (void)hipFreeAsync(ord, st);
     if (crange) (void)hipFreeAsync(crange, st);
     if (cmask) (void)hipFreeAsync(cmask, st);
     if (plist) (void)hipFreeAsync(plist, st);
