@@ -1244,10 +1244,11 @@ extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, cons
     if (P == 0) return SFMHIP_OK;
     // Variant (SFMHIP_MATCH_VARIANT, for A/B runs): {MFMA tile, tiles/wave, waves/WG}
     //   0: 16x16, 4, 4 (default; fastest measured)   1: 32x32, 2, 4   2: 16x16, 8, 4   3: 32x32, 4, 4   4: 16x16, 4, 8
+    //   5: 16x16, 2, 8 (half the resident query rows per wave: 4 waves/SIMD instead of 2)
     const char* venv = std::getenv("SFMHIP_MATCH_VARIANT");
     const int variant = venv ? std::atoi(venv) : 0;
-    static const int kIBv[5] = {256, 256, 512, 512, 512};
-    const int iblk = kIBv[(variant >= 0 && variant < 5) ? variant : 0];
+    static const int kIBv[6] = {256, 256, 512, 512, 512, 256};
+    const int iblk = kIBv[(variant >= 0 && variant < 6) ? variant : 0];
     const int n_iblk = ceil_div(m_pad, iblk);
     const int64_t nwg64 = (int64_t)P * n_iblk;
     SFMHIP_REQUIRE(nwg64 < INT_MAX, "sfmhip_match_pairs: too many pairs for one launch");
@@ -1263,6 +1264,7 @@ extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, cons
         case 2: SFMHIP_LAUNCH_MATCH(DD, 16, 8, 4); break;          \
         case 3: SFMHIP_LAUNCH_MATCH(DD, 32, 4, 4); break;          \
         case 4: SFMHIP_LAUNCH_MATCH(DD, 16, 4, 8); break;          \
+        case 5: SFMHIP_LAUNCH_MATCH(DD, 16, 2, 8); break;          \
         default: SFMHIP_LAUNCH_MATCH(DD, 16, 4, 4); break;         \
     }
     switch (d) {
