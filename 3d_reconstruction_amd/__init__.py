@@ -15,7 +15,8 @@ from .match import (MODE_FLOAT, MODE_SIFT, DescriptorBank, Matcher, all_pairs,  
                     bf_match, vq)
 from .geometry import (Rodrigues, ba_sparse, calculate_reprojection_error,  # noqa: F401
                        convertPointsFromHomogeneous, fd_jacobian, projectPoints,
-                       residual_jacobian_batched, triangulatePoints, triangulate_batched)
+                       residual_jacobian_batched, triangulatePoints, triangulate_batched, ba_solve_batched,
+                       least_squares_ba)
 from .voxel import (MASK_PLENOXEL, MASK_SDF, VoxelGrid, tsdf_block_table, tsdf_cull_stats, tsdf_integrate,  # noqa: F401,E501
                     tsdf_layer_cost, tsdf_layer_stats, voxel_traversal)
 from . import bow, pipeline, reconstruct, tracks, verify  # noqa: F401,E402

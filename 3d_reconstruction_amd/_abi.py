@@ -70,6 +70,7 @@ SIGNATURES = {
     "sfmhip_triangulate_dlt": [_p, _p, _p, _p, _i64, _p, _p],
     "sfmhip_reproj_residual": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "sfmhip_reproj_fd_jacobian": [_p, _p, _p, _p, _p, _i32, _i64, _p, _p, _p, _p],
+    "sfmhip_ba_solve": [_p, _p, _p, _p, _p, _i32, _f64, _f64, _f64, _i32, _p, _p, _p, _p, _p],
     "sfmhip_voxel_traversal_count": [_p, _i64, _f32, _i32, _p, _p],
     "sfmhip_voxel_traversal": [_p, _i64, _f32, _i32, _p, _p],
     "sfmhip_grid_sample": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i64, _p, _p],

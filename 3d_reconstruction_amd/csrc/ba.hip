@@ -1,0 +1,572 @@
+// ba.hip — the BA solve of sfm.py:37-38 on the GPU, all pairs at once:
+//   least_squares(calculate_reprojection_error, [rvec, t, X...], jac_sparsity=
+//                 ba_sparse(...), x_scale='jac', ftol=1e-8, args=(K, pts1))
+// i.e. scipy's 'trf' with tr_solver 'lsmr' and the grouped 2-point FD
+// Jacobian, restated on the BA structure (oracle/ba.py is the same algorithm
+// in numpy, pinned against scipy itself by tests/test_oracle_ba.py):
+//   * J: scipy's FD values per observation (geom_dev.h fd_obs), 2x6 camera +
+//     2x3 point block, scale = 1 / column norms (max with the previous ones);
+//   * the Gauss-Newton direction lsmr(J_h, f, damp = sqrt(reg)) (scipy stops
+//     LSMR at atol = btol = 1e-6) is the EXACT damped solution
+//     J_h^T (J_h J_h^T + mu I)^-1 f by Woodbury over the 2x2 point blocks
+//     (one 6x6 Cholesky per iteration);
+//   * the 2-D subspace {g_h, gn_h}, its trust-region solve, the radius update
+//     and the ftol / xtol / gtol tests as scipy's trf_no_bounds.
+// One workgroup per pair (the pair's observations are a contiguous range), the
+// per-observation J / f / column scales in a scratch record, every scalar of
+// the iteration reduced across the workgroup and held in LDS; thread 0 does the
+// 6x6 and 2x2 algebra.
+#include "common.h"
+#include "geom_dev.h"
+#include <climits>
+
+namespace sfmhip {
+namespace {
+
+constexpr int kBaThreads = 256;
+constexpr int kRec = 26;   // per observation: J (18: u row, v row), f (2), scale_inv of the point (3), X_new (3)
+
+// sum of K doubles over the workgroup; every thread receives the totals in out[]
+template <int K>
+__device__ void block_sum(double (&v)[K], double* red /* [4][K] */, double* out /* [K] */) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double x = v[k];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+        v[k] = x;
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[wave * K + k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < K) out[threadIdx.x] = (red[threadIdx.x] + red[K + threadIdx.x]) + (red[2 * K + threadIdx.x] + red[3 * K + threadIdx.x]);
+    __syncthreads();
+}
+
+__device__ double block_max(double v, double* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    const double m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    __syncthreads();
+    return m;
+}
+
+// 6x6 SPD solve (lower Cholesky), in place on b; false if not positive definite
+__device__ bool chol6_solve(double (&A)[6][6], double (&b)[6]) {
+    for (int j = 0; j < 6; ++j) {
+        double s = A[j][j];
+        for (int k = 0; k < j; ++k) s -= A[j][k] * A[j][k];
+        if (!(s > 0.0)) return false;
+        const double d = sqrt(s);
+        A[j][j] = d;
+        for (int i = j + 1; i < 6; ++i) {
+            double t = A[i][j];
+            for (int k = 0; k < j; ++k) t -= A[i][k] * A[j][k];
+            A[i][j] = t / d;
+        }
+    }
+    for (int i = 0; i < 6; ++i) {
+        double t = b[i];
+        for (int k = 0; k < i; ++k) t -= A[i][k] * b[k];
+        b[i] = t / A[i][i];
+    }
+    for (int i = 5; i >= 0; --i) {
+        double t = b[i];
+        for (int k = i + 1; k < 6; ++k) t -= A[k][i] * b[k];
+        b[i] = t / A[i][i];
+    }
+    return true;
+}
+
+// scipy solve_trust_region_2d: the interior Newton point if B is positive
+// definite and it fits, else the minimiser of the quadratic on the circle
+// |p| = Delta (scipy takes the best real root of its quartic; here the same
+// point from a scan of the circle refined by Newton on the angle).
+__device__ void tr_solve_2d(const double B[3] /* b00, b01, b11 */, const double g[2], double Delta, double p[2]) {
+    const double b00 = B[0], b01 = B[1], b11 = B[2];
+    if (b00 > 0.0) {
+        const double l00 = sqrt(b00), l10 = b01 / l00, s = b11 - l10 * l10;
+        if (s > 0.0) {
+            const double l11 = sqrt(s);
+            const double y0 = g[0] / l00, y1 = (g[1] - l10 * y0) / l11;
+            const double x1 = y1 / l11, x0 = (y0 - l10 * x1) / l00;
+            if (x0 * x0 + x1 * x1 <= Delta * Delta) { p[0] = -x0; p[1] = -x1; return; }
+        }
+    }
+    // q(phi) = 0.5 D^2 (b00 c^2 + 2 b01 c s + b11 s^2) + D (g0 c + g1 s)
+    auto val = [&](double ph) {
+        const double c = cos(ph), s = sin(ph);
+        return 0.5 * Delta * Delta * (b00 * c * c + 2.0 * b01 * c * s + b11 * s * s) + Delta * (g[0] * c + g[1] * s);
+    };
+    double best = 0.0, bv = val(0.0);
+    constexpr int kScan = 64;
+    for (int k = 1; k < kScan; ++k) {
+        const double ph = 6.283185307179586 * k / kScan, v = val(ph);
+        if (v < bv) { bv = v; best = ph; }
+    }
+    for (int it = 0; it < 40; ++it) {   // Newton on dq/dphi
+        const double c = cos(best), s = sin(best);
+        const double d1 = Delta * Delta * ((b11 - b00) * c * s + b01 * (c * c - s * s)) + Delta * (g[1] * c - g[0] * s);
+        const double d2 = Delta * Delta * ((b11 - b00) * (c * c - s * s) - 4.0 * b01 * c * s) - Delta * (g[0] * c + g[1] * s);
+        if (!(d2 > 0.0)) break;
+        const double step = d1 / d2;
+        best -= step;
+        if (fabs(step) < 1e-16) break;
+    }
+    p[0] = Delta * cos(best);
+    p[1] = Delta * sin(best);
+}
+
+struct BaState {   // LDS: the iteration's scalars, written by thread 0 or by block_sum
+    double cam[6], cam_new[6], R[4][9], Rn[9];
+    double gc[6], sic[6], dc[6], ghc[6], gnc[6], s1c[6], s2c[6], shc[6];
+    double G[6][6], z[6];
+    double red[4 * 27], tot[27];
+    double Delta, mu, cost, cost_new, pS[2];
+    double gmax, gh2, ghn, c12, s2n, BS[3], gS[2];
+    int status, nfev, njev, done, accept;
+};
+
+__device__ __forceinline__ const double* rec_of(double* scratch, int64_t i) { return scratch + (size_t)i * kRec; }
+
+// residual of one observation at (camera rotation R, c = [rvec, t], X)
+__device__ __forceinline__ void resid(const double* R, const double* c, const double* k, const double* X,
+                                      const double* pts, double& ru, double& rv) {
+    double u, v;
+    project(R, c + 3, X, k[0], k[4], k[2], k[5], u, v);
+    ru = pts[0] - u;
+    rv = pts[1] - v;
+}
+
+__global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__ cam_io, const double* __restrict__ Kall,
+                                                            double* __restrict__ X, const double* __restrict__ pts2d,
+                                                            const int64_t* __restrict__ off, double ftol, double xtol,
+                                                            double gtol, int max_nfev_arg, double* __restrict__ scratch,
+                                                            double* __restrict__ cost_out, int32_t* __restrict__ nfev_out,
+                                                            int32_t* __restrict__ njev_out,
+                                                            int32_t* __restrict__ status_out) {
+    __shared__ BaState S;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int64_t o0 = off[p], o1 = off[p + 1];
+    const int n = (int)(o1 - o0);
+    const double* k = Kall + (size_t)p * 9;
+    double* Xp = X + 3 * o0;
+    const double* pts = pts2d + 2 * o0;
+    double* rec = scratch + (size_t)o0 * kRec;
+    if (tid < 6) S.cam[tid] = cam_io[(size_t)p * 6 + tid];
+    __syncthreads();
+    if (n == 0) {
+        if (tid == 0) { cost_out[p] = 0.0; nfev_out[p] = 0; njev_out[p] = 0; status_out[p] = 1; }
+        return;
+    }
+    const int max_nfev = max_nfev_arg > 0 ? max_nfev_arg : (int)min((int64_t)INT_MAX, 100 * (6 + 3 * (int64_t)n));
+
+    // J, f at the current point; scale_inv (max with the old unless first); gc, cost, |g|_inf
+    auto jacobian = [&](bool first) {
+        if (tid < 4) {   // R(rvec) and the three perturbed rotations of the FD
+            double q[3] = {S.cam[0], S.cam[1], S.cam[2]};
+            if (tid > 0) q[tid - 1] = q[tid - 1] + fd_step(q[tid - 1]);
+            rodrigues(q, S.R[tid]);
+        }
+        __syncthreads();
+        double acc[13] = {0};   // gc (6), column sums of squares (6), cost
+        double gmax = 0.0;
+        for (int i = tid; i < n; i += kBaThreads) {
+            double* r = scratch + (size_t)(o0 + i) * kRec;
+            double f[2];
+            fd_obs(&S.R[0][0], S.cam, k, Xp + 3 * i, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
+            r[18] = f[0];
+            r[19] = f[1];
+            acc[12] += f[0] * f[0] + f[1] * f[1];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                acc[c] += r[c] * f[0] + r[9 + c] * f[1];
+                acc[6 + c] += r[c] * r[c] + r[9 + c] * r[9 + c];
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const double gp = r[6 + c] * f[0] + r[15 + c] * f[1];
+                gmax = fmax(gmax, fabs(gp));
+                double si = sqrt(r[6 + c] * r[6 + c] + r[15 + c] * r[15 + c]);
+                if (first) si = si == 0.0 ? 1.0 : si;
+                else si = fmax(si, r[20 + c]);
+                r[20 + c] = si;
+            }
+        }
+        gmax = block_max(gmax, S.red);
+        block_sum<13>(acc, S.red, S.tot);
+        if (tid == 0) {
+            double gm = gmax;
+            for (int c = 0; c < 6; ++c) {
+                S.gc[c] = S.tot[c];
+                gm = fmax(gm, fabs(S.gc[c]));
+                const double si = sqrt(S.tot[6 + c]);
+                S.sic[c] = first ? (si == 0.0 ? 1.0 : si) : fmax(si, S.sic[c]);
+            }
+            S.gmax = gm;
+            S.cost = 0.5 * S.tot[12];
+        }
+        __syncthreads();
+    };
+
+    jacobian(true);
+    // Delta = |x0 * scale_inv|
+    {
+        double acc[1] = {0.0};
+        for (int i = tid; i < n; i += kBaThreads) {
+            const double* r = rec_of(rec, i);
+            for (int c = 0; c < 3; ++c) { const double t = Xp[3 * i + c] * r[20 + c]; acc[0] += t * t; }
+        }
+        block_sum<1>(acc, S.red, S.tot);
+        if (tid == 0) {
+            double d2 = S.tot[0];
+            for (int c = 0; c < 6; ++c) d2 += (S.cam[c] * S.sic[c]) * (S.cam[c] * S.sic[c]);
+            S.Delta = sqrt(d2);
+            if (S.Delta == 0.0) S.Delta = 1.0;
+            S.nfev = 1; S.njev = 1; S.status = -1; S.done = 0;
+        }
+        __syncthreads();
+    }
+
+    while (true) {
+        if (tid == 0) {
+            if (S.gmax < gtol) S.status = 1;
+            S.done = S.status >= 0 || S.nfev == max_nfev;
+            for (int c = 0; c < 6; ++c) { S.dc[c] = 1.0 / S.sic[c]; S.ghc[c] = S.dc[c] * S.gc[c]; }
+        }
+        __syncthreads();
+        if (S.done) break;
+        // regularize: a = 0.5 |J_h (-g_h)|^2, |g_h|^2 (build_quadratic_1d along -g_h)
+        {
+            double acc[2] = {0.0, 0.0};
+            for (int i = tid; i < n; i += kBaThreads) {
+                const double* r = rec_of(rec, i);
+                double vu = 0.0, vv = 0.0;
+                for (int c = 0; c < 6; ++c) { vu -= r[c] * S.dc[c] * S.ghc[c]; vv -= r[9 + c] * S.dc[c] * S.ghc[c]; }
+                for (int c = 0; c < 3; ++c) {
+                    const double d = 1.0 / r[20 + c];
+                    const double gh = d * (r[6 + c] * r[18] + r[15 + c] * r[19]);
+                    vu -= r[6 + c] * d * gh;
+                    vv -= r[15 + c] * d * gh;
+                    acc[1] += gh * gh;
+                }
+                acc[0] += vu * vu + vv * vv;
+            }
+            block_sum<2>(acc, S.red, S.tot);
+            if (tid == 0) {
+                double gh2 = S.tot[1];
+                for (int c = 0; c < 6; ++c) gh2 += S.ghc[c] * S.ghc[c];
+                const double a = 0.5 * S.tot[0], b = -gh2, to_tr = S.Delta / sqrt(gh2);
+                double ag = 0.0;                                  // t = 0
+                ag = fmin(ag, to_tr * (a * to_tr + b));           // t = to_tr (argmin keeps the first on ties)
+                if (a != 0.0) {
+                    const double ext = -0.5 * b / a;
+                    if (0.0 < ext && ext < to_tr) ag = fmin(ag, ext * (a * ext + b));
+                }
+                S.mu = -ag / (S.Delta * S.Delta);
+                S.gh2 = gh2;
+            }
+            __syncthreads();
+        }
+        const double mu = S.mu;
+        // ridge: G = I + sum C^T B^-1 C, h = sum C^T B^-1 f  (C = J_h camera block, B = Jp_h Jp_h^T + mu I)
+        {
+            double acc[27];
+#pragma unroll
+            for (int e = 0; e < 27; ++e) acc[e] = 0.0;
+            for (int i = tid; i < n; i += kBaThreads) {
+                const double* r = rec_of(rec, i);
+                double C[2][6], Pp[2][3];
+                for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
+                for (int c = 0; c < 3; ++c) {
+                    const double d = 1.0 / r[20 + c];
+                    Pp[0][c] = r[6 + c] * d;
+                    Pp[1][c] = r[15 + c] * d;
+                }
+                const double b00 = Pp[0][0] * Pp[0][0] + Pp[0][1] * Pp[0][1] + Pp[0][2] * Pp[0][2] + mu;
+                const double b01 = Pp[0][0] * Pp[1][0] + Pp[0][1] * Pp[1][1] + Pp[0][2] * Pp[1][2];
+                const double b11 = Pp[1][0] * Pp[1][0] + Pp[1][1] * Pp[1][1] + Pp[1][2] * Pp[1][2] + mu;
+                const double idet = 1.0 / (b00 * b11 - b01 * b01);
+                const double i00 = b11 * idet, i01 = -b01 * idet, i11 = b00 * idet;
+                const double u0 = i00 * r[18] + i01 * r[19], u1 = i01 * r[18] + i11 * r[19];
+                double Y[2][6];
+                for (int c = 0; c < 6; ++c) { Y[0][c] = i00 * C[0][c] + i01 * C[1][c]; Y[1][c] = i01 * C[0][c] + i11 * C[1][c]; }
+                int e = 0;
+                for (int a = 0; a < 6; ++a)
+                    for (int b = a; b < 6; ++b) acc[e++] += C[0][a] * Y[0][b] + C[1][a] * Y[1][b];
+                for (int a = 0; a < 6; ++a) acc[21 + a] += C[0][a] * u0 + C[1][a] * u1;
+            }
+            block_sum<27>(acc, S.red, S.tot);
+            if (tid == 0) {
+                double G[6][6], h[6];
+                int e = 0;
+                for (int a = 0; a < 6; ++a)
+                    for (int b = a; b < 6; ++b) { G[a][b] = G[b][a] = S.tot[e++] + (a == b ? 1.0 : 0.0); }
+                for (int a = 0; a < 6; ++a) h[a] = S.tot[21 + a];
+                if (!chol6_solve(G, h)) S.status = -2;   // not expected: G = I + PSD
+                for (int a = 0; a < 6; ++a) S.z[a] = h[a];
+            }
+            __syncthreads();
+        }
+        // gn_h = J_h^T y, y = B^-1 f - B^-1 C z; g_h . gn_h and |gn_h|^2 (Gram-Schmidt of [g_h, gn_h])
+        {
+            double acc[7] = {0};   // gnc (6), point part of g_h . gn_h
+            for (int i = tid; i < n; i += kBaThreads) {
+                const double* r = rec_of(rec, i);
+                double C[2][6], Pp[2][3];
+                for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
+                for (int c = 0; c < 3; ++c) {
+                    const double d = 1.0 / r[20 + c];
+                    Pp[0][c] = r[6 + c] * d;
+                    Pp[1][c] = r[15 + c] * d;
+                }
+                const double b00 = Pp[0][0] * Pp[0][0] + Pp[0][1] * Pp[0][1] + Pp[0][2] * Pp[0][2] + mu;
+                const double b01 = Pp[0][0] * Pp[1][0] + Pp[0][1] * Pp[1][1] + Pp[0][2] * Pp[1][2];
+                const double b11 = Pp[1][0] * Pp[1][0] + Pp[1][1] * Pp[1][1] + Pp[1][2] * Pp[1][2] + mu;
+                const double idet = 1.0 / (b00 * b11 - b01 * b01);
+                const double i00 = b11 * idet, i01 = -b01 * idet, i11 = b00 * idet;
+                double w0 = r[18], w1 = r[19];
+                for (int c = 0; c < 6; ++c) { w0 -= C[0][c] * S.z[c]; w1 -= C[1][c] * S.z[c]; }
+                const double y0 = i00 * w0 + i01 * w1, y1 = i01 * w0 + i11 * w1;
+                for (int c = 0; c < 6; ++c) acc[c] += C[0][c] * y0 + C[1][c] * y1;
+                for (int c = 0; c < 3; ++c) {
+                    const double gn = Pp[0][c] * y0 + Pp[1][c] * y1;
+                    const double gh = Pp[0][c] * r[18] + Pp[1][c] * r[19];   // d * (J^T f) = g_h
+                    acc[6] += gh * gn;
+                }
+            }
+            block_sum<7>(acc, S.red, S.tot);
+            if (tid == 0) {
+                const double ghn = sqrt(S.gh2);
+                double dot = S.tot[6];
+                for (int c = 0; c < 6; ++c) {
+                    S.gnc[c] = S.tot[c];
+                    dot += S.ghc[c] * S.gnc[c];
+                    S.s1c[c] = S.ghc[c] / ghn;
+                }
+                S.c12 = dot / ghn;   // s2 = gn_h - (s1 . gn_h) s1, normalised by the next pass
+                for (int c = 0; c < 6; ++c) S.s2c[c] = S.gnc[c] - S.c12 * S.s1c[c];
+                S.ghn = ghn;
+            }
+            __syncthreads();
+        }
+        // |s2|^2 exactly; then JS (2 columns) -> B_S, g_S
+        const double ghn = S.ghn, c12 = S.c12;
+        auto point_vecs = [&](const double* r, double (&s1)[3], double (&s2)[3]) {
+            double C[2][6], Pp[2][3];
+            for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
+            for (int c = 0; c < 3; ++c) {
+                const double d = 1.0 / r[20 + c];
+                Pp[0][c] = r[6 + c] * d;
+                Pp[1][c] = r[15 + c] * d;
+            }
+            const double b00 = Pp[0][0] * Pp[0][0] + Pp[0][1] * Pp[0][1] + Pp[0][2] * Pp[0][2] + mu;
+            const double b01 = Pp[0][0] * Pp[1][0] + Pp[0][1] * Pp[1][1] + Pp[0][2] * Pp[1][2];
+            const double b11 = Pp[1][0] * Pp[1][0] + Pp[1][1] * Pp[1][1] + Pp[1][2] * Pp[1][2] + mu;
+            const double idet = 1.0 / (b00 * b11 - b01 * b01);
+            const double i00 = b11 * idet, i01 = -b01 * idet, i11 = b00 * idet;
+            double w0 = r[18], w1 = r[19];
+            for (int c = 0; c < 6; ++c) { w0 -= C[0][c] * S.z[c]; w1 -= C[1][c] * S.z[c]; }
+            const double y0 = i00 * w0 + i01 * w1, y1 = i01 * w0 + i11 * w1;
+            for (int c = 0; c < 3; ++c) {
+                const double gn = Pp[0][c] * y0 + Pp[1][c] * y1;
+                const double gh = Pp[0][c] * r[18] + Pp[1][c] * r[19];
+                s1[c] = gh / ghn;
+                s2[c] = gn - c12 * s1[c];
+            }
+        };
+        {
+            double acc[1] = {0.0};
+            for (int i = tid; i < n; i += kBaThreads) {
+                double s1[3], s2[3];
+                point_vecs(rec_of(rec, i), s1, s2);
+                acc[0] += s2[0] * s2[0] + s2[1] * s2[1] + s2[2] * s2[2];
+            }
+            block_sum<1>(acc, S.red, S.tot);
+            if (tid == 0) {
+                double n2 = S.tot[0];
+                for (int c = 0; c < 6; ++c) n2 += S.s2c[c] * S.s2c[c];
+                S.s2n = sqrt(n2);
+                for (int c = 0; c < 6; ++c) S.s2c[c] /= S.s2n;
+            }
+            __syncthreads();
+        }
+        const double s2n = S.s2n;
+        {
+            double acc[5] = {0};   // JS1.JS1, JS1.JS2, JS2.JS2, s2 . g_h and s1 . g_h (point parts)
+            for (int i = tid; i < n; i += kBaThreads) {
+                const double* r = rec_of(rec, i);
+                double s1[3], s2[3];
+                point_vecs(r, s1, s2);
+                double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+                for (int c = 0; c < 6; ++c) {
+                    a0 += r[c] * S.dc[c] * S.s1c[c];
+                    a1 += r[9 + c] * S.dc[c] * S.s1c[c];
+                    b0 += r[c] * S.dc[c] * S.s2c[c];
+                    b1 += r[9 + c] * S.dc[c] * S.s2c[c];
+                }
+                for (int c = 0; c < 3; ++c) {
+                    const double d = 1.0 / r[20 + c];
+                    const double s2c = s2[c] / s2n;
+                    a0 += r[6 + c] * d * s1[c];
+                    a1 += r[15 + c] * d * s1[c];
+                    b0 += r[6 + c] * d * s2c;
+                    b1 += r[15 + c] * d * s2c;
+                    const double gh = d * (r[6 + c] * r[18] + r[15 + c] * r[19]);
+                    acc[3] += s2c * gh;
+                    acc[4] += s1[c] * gh;
+                }
+                acc[0] += a0 * a0 + a1 * a1;
+                acc[1] += a0 * b0 + a1 * b1;
+                acc[2] += b0 * b0 + b1 * b1;
+            }
+            block_sum<5>(acc, S.red, S.tot);
+            if (tid == 0) {
+                double g0 = S.tot[4], g1 = S.tot[3];
+                for (int c = 0; c < 6; ++c) { g0 += S.s1c[c] * S.ghc[c]; g1 += S.s2c[c] * S.ghc[c]; }
+                S.BS[0] = S.tot[0]; S.BS[1] = S.tot[1]; S.BS[2] = S.tot[2];
+                S.gS[0] = g0; S.gS[1] = g1;
+            }
+            __syncthreads();
+        }
+        // inner loop: trial steps until the cost decreases
+        if (tid == 0) S.accept = 0;
+        __syncthreads();
+        while (true) {
+            if (tid == 0) {
+                S.done = !(S.nfev < max_nfev);
+                if (!S.done) {
+                    tr_solve_2d(S.BS, S.gS, S.Delta, S.pS);
+                    for (int c = 0; c < 6; ++c) {
+                        S.shc[c] = S.pS[0] * S.s1c[c] + S.pS[1] * S.s2c[c];
+                        S.cam_new[c] = S.cam[c] + S.dc[c] * S.shc[c];
+                    }
+                    rodrigues(S.cam_new, S.Rn);
+                }
+            }
+            __syncthreads();
+            if (S.done) break;
+            // step, J_h step, f(x_new): predicted reduction, cost_new, |step_h|, |step|, |x|, finiteness
+            double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
+            for (int i = tid; i < n; i += kBaThreads) {
+                double* r = scratch + (size_t)(o0 + i) * kRec;
+                double s1[3], s2[3];
+                point_vecs(r, s1, s2);
+                double ju = 0, jv = 0;
+                for (int c = 0; c < 6; ++c) { ju += r[c] * S.dc[c] * S.shc[c]; jv += r[9 + c] * S.dc[c] * S.shc[c]; }
+                double Xn[3];
+                for (int c = 0; c < 3; ++c) {
+                    const double d = 1.0 / r[20 + c];
+                    const double sh = S.pS[0] * s1[c] + S.pS[1] * (s2[c] / s2n);
+                    ju += r[6 + c] * d * sh;
+                    jv += r[15 + c] * d * sh;
+                    acc[1] += sh * (d * (r[6 + c] * r[18] + r[15 + c] * r[19]));
+                    acc[3] += sh * sh;
+                    const double st = d * sh;
+                    acc[4] += st * st;
+                    const double x = Xp[3 * i + c];
+                    acc[5] += x * x;
+                    Xn[c] = x + st;
+                    r[23 + c] = Xn[c];
+                }
+                acc[0] += ju * ju + jv * jv;
+                double ru, rv;
+                resid(S.Rn, S.cam_new, k, Xn, pts + 2 * i, ru, rv);
+                acc[2] += ru * ru + rv * rv;
+                if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
+            }
+            block_sum<7>(acc, S.red, S.tot);
+            if (tid == 0) {
+                double sg = S.tot[1], sh2 = S.tot[3], st2 = S.tot[4], x2 = S.tot[5];
+                for (int c = 0; c < 6; ++c) {
+                    sg += S.shc[c] * S.ghc[c];
+                    sh2 += S.shc[c] * S.shc[c];
+                    st2 += (S.dc[c] * S.shc[c]) * (S.dc[c] * S.shc[c]);
+                    x2 += S.cam[c] * S.cam[c];
+                }
+                const double predicted = -(0.5 * S.tot[0] + sg);
+                S.nfev += 1;
+                const double sh_norm = sqrt(sh2);
+                if (S.tot[6] > 0.0) {   // non-finite residuals: shrink and retry
+                    S.Delta = 0.25 * sh_norm;
+                    S.accept = -1;
+                } else {
+                    S.cost_new = 0.5 * S.tot[2];
+                    const double actual = S.cost - S.cost_new;
+                    double ratio;
+                    if (predicted > 0.0) ratio = actual / predicted;
+                    else if (predicted == 0.0 && actual == 0.0) ratio = 1.0;
+                    else ratio = 0.0;
+                    double Dn = S.Delta;
+                    if (ratio < 0.25) Dn = 0.25 * sh_norm;
+                    else if (ratio > 0.75 && sh_norm > 0.95 * S.Delta) Dn = S.Delta * 2.0;
+                    const double step_norm = sqrt(st2), x_norm = sqrt(x2);
+                    const bool fok = actual < ftol * S.cost && ratio > 0.25;
+                    const bool xok = step_norm < xtol * (xtol + x_norm);
+                    S.status = (fok && xok) ? 4 : fok ? 2 : xok ? 3 : -1;
+                    S.accept = actual > 0.0 ? 1 : 0;
+                    if (S.status < 0) S.Delta = Dn;
+                }
+            }
+            __syncthreads();
+            if (S.status >= 0 || S.accept == 1) break;
+        }
+        if (S.accept == 1) {   // x = x_new; J at the new point
+            for (int i = tid; i < n; i += kBaThreads) {
+                const double* r = rec_of(rec, i);
+                for (int c = 0; c < 3; ++c) Xp[3 * i + c] = r[23 + c];
+            }
+            if (tid < 6) S.cam[tid] = S.cam_new[tid];
+            __syncthreads();
+            jacobian(false);
+            if (tid == 0) { S.njev += 1; }
+            __syncthreads();
+        }
+        if (S.done) break;
+    }
+    if (tid < 6) cam_io[(size_t)p * 6 + tid] = S.cam[tid];
+    if (tid == 0) {
+        cost_out[p] = S.cost;
+        nfev_out[p] = S.nfev;
+        njev_out[p] = S.njev;
+        status_out[p] = S.status < 0 ? 0 : S.status;
+    }
+}
+
+}  // namespace
+}  // namespace sfmhip
+
+using namespace sfmhip;
+
+extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const double* pts2d, const int64_t* pair_off,
+                               int n_pairs, double ftol, double xtol, double gtol, int max_nfev, double* cost,
+                               int32_t* nfev, int32_t* njev, int32_t* status, void* stream) {
+    SFMHIP_REQUIRE(cam && K && X && pts2d && pair_off && cost && nfev && njev && status,
+                   "sfmhip_ba_solve: null pointer");
+    SFMHIP_REQUIRE(n_pairs >= 0, "sfmhip_ba_solve: negative n_pairs");
+    if (n_pairs == 0) return SFMHIP_OK;
+    hipStream_t st = as_stream(stream);
+    int64_t n_obs = 0;
+    if (hipMemcpyAsync(&n_obs, pair_off + n_pairs, sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        set_error("sfmhip_ba_solve: reading the observation count failed");
+        return SFMHIP_E_HIP;
+    }
+    SFMHIP_REQUIRE(n_obs >= 0, "sfmhip_ba_solve: bad pair offsets");
+    double* scratch = nullptr;
+    if (scratch_alloc((void**)&scratch, (size_t)std::max<int64_t>(n_obs, 1) * kRec * sizeof(double), st) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("sfmhip_ba_solve: scratch allocation failed");
+        return SFMHIP_E_HIP;
+    }
+    hipLaunchKernelGGL(ba_trf_kernel, dim3(n_pairs), dim3(kBaThreads), 0, st, cam, K, X, pts2d, pair_off, ftol, xtol,
+                       gtol, max_nfev, scratch, cost, nfev, njev, status);
+    const int rc = check_launch("ba_trf_kernel");
+    (void)hipFreeAsync(scratch, st);
+    return rc;
+}

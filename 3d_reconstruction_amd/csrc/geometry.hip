@@ -14,13 +14,6 @@
 
 namespace sfmhip {
 
-// scipy _compute_absolute_step for '2-point': EPS**0.5 * sign0(x) * max(1, |x|)
-__device__ __forceinline__ double fd_step(double x) {
-    const double rstep = 1.4901161193847656e-08;  // np.finfo(float64).eps ** 0.5
-    const double sgn = (x >= 0.0) ? 1.0 : -1.0;
-    return rstep * sgn * fmax(1.0, fabs(x));
-}
-
 // ---------------------------------------------------------------------------
 // DLT, two passes (sfm.py:27, cv2.triangulatePoints).
 //
@@ -466,54 +459,8 @@ __global__ __launch_bounds__(kFdThreads) void fdjac_kernel(const double* __restr
         const int pr = pair_of_obs ? pair_of_obs[i] : 0;
         const double* c = cam + (size_t)pr * 6;
         const double* k = K + (size_t)pr * 9;
-        const double* R = Rt + (size_t)pr * 36;
-        const double fx = k[0], fy = k[4], cx = k[2], cy = k[5];
-        const double obs_u = pts2d[2 * i], obs_v = pts2d[2 * i + 1];
-        const double t[3] = {c[3], c[4], c[5]};
-        const double Xp[3] = {X[3 * i], X[3 * i + 1], X[3 * i + 2]};
-        // base projection, keeping the partial sums R X
-        const double sx = R[0] * Xp[0] + R[1] * Xp[1] + R[2] * Xp[2];
-        const double sy = R[3] * Xp[0] + R[4] * Xp[1] + R[5] * Xp[2];
-        const double sz = R[6] * Xp[0] + R[7] * Xp[1] + R[8] * Xp[2];
-        const double zb = sz + t[2];
-        const double izb = (zb != 0.0) ? 1.0 / zb : 1.0;
-        const double xb = (sx + t[0]) * izb, yb = (sy + t[1]) * izb;
-        const double base_u = obs_u - (xb * fx + cx), base_v = obs_v - (yb * fy + cy);
-        if (r) { r[2 * i] = base_u; r[2 * i + 1] = base_v; }
-        const double f0u = f0 ? f0[2 * i] : base_u;
-        const double f0v = f0 ? f0[2 * i + 1] : base_v;
-        double* row = sj + threadIdx.x * 18;
-        auto put = [&](int q, double u, double v, double dx) {
-            row[q] = ((obs_u - u) - f0u) / dx;
-            row[9 + q] = ((obs_v - v) - f0v) / dx;
-        };
-        // rvec: the pair's perturbed rotations
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const double hx = c[q] + fd_step(c[q]);
-            double u, v;
-            project(R + 9 * (q + 1), t, Xp, fx, fy, cx, cy, u, v);
-            put(q, u, v, hx - c[q]);
-        }
-        // t: only the last addition of coordinate q changes
-        {
-            const double h0 = t[0] + fd_step(t[0]), h1 = t[1] + fd_step(t[1]), h2 = t[2] + fd_step(t[2]);
-            put(3, ((sx + h0) * izb) * fx + cx, yb * fy + cy, h0 - t[0]);
-            put(4, xb * fx + cx, ((sy + h1) * izb) * fy + cy, h1 - t[1]);
-            const double z2 = sz + h2;
-            const double iz2 = (z2 != 0.0) ? 1.0 / z2 : 1.0;
-            put(5, ((sx + t[0]) * iz2) * fx + cx, ((sy + t[1]) * iz2) * fy + cy, h2 - t[2]);
-        }
-        // X: full re-projection (the perturbed term sits inside the sums)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            double Xq[3] = {Xp[0], Xp[1], Xp[2]};
-            const double hx = Xp[q] + fd_step(Xp[q]);
-            Xq[q] = hx;
-            double u, v;
-            project(R, t, Xq, fx, fy, cx, cy, u, v);
-            put(6 + q, u, v, hx - Xp[q]);
-        }
+        fd_obs(Rt + (size_t)pr * 36, c, k, X + 3 * i, pts2d[2 * i], pts2d[2 * i + 1], f0 ? f0 + 2 * i : nullptr,
+               r ? r + 2 * i : nullptr, sj + threadIdx.x * 18);
     }
     __syncthreads();
     // coalesced write-out of the workgroup's rows [i0, min(n, i0 + 256)) x 18 doubles

@@ -199,3 +199,61 @@ def residual_jacobian_batched(cam: torch.Tensor, K: torch.Tensor, X: torch.Tenso
     call("sfmhip_reproj_fd_jacobian", ptr(cam), ptr(K), ptr(X), ptr(pts2d), ptr(pair_of_obs),
          int(cam.shape[0]), n, None, ptr(r), ptr(jv), stream_ptr())
     return r, jv
+
+
+def ba_solve_batched(cam: torch.Tensor, K: torch.Tensor, X: torch.Tensor, pts2d: torch.Tensor,
+                     pair_off: torch.Tensor, ftol: float = 1e-8, xtol: float = 1e-8, gtol: float = 1e-8,
+                     max_nfev: int | None = None) -> dict:
+    """The BA solve of sfm.py:37-38 for every pair at once, on the GPU (ba.hip):
+    scipy ``least_squares(calculate_reprojection_error, [rvec, t, X], jac_sparsity=
+    ba_sparse(...), x_scale='jac', ftol=ftol)`` restated (oracle/ba.py).
+
+    cam (P,6) and X (n,3) f64 device tensors are updated in place; K (P,3,3),
+    pts2d (n,2) f64; pair_off (P+1) int64 (pair p owns observations
+    [pair_off[p], pair_off[p+1])).  Returns device tensors cost (P,) f64 and
+    nfev, njev, status (P,) int32 (scipy's meanings)."""
+    require_gpu()
+    P = int(cam.shape[0])
+    for name, t, dt in (("cam", cam, torch.float64), ("K", K, torch.float64), ("X", X, torch.float64),
+                        ("pts2d", pts2d, torch.float64), ("pair_off", pair_off, torch.int64)):
+        if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous {dt} device tensor")
+    n = int(X.shape[0])
+    if tuple(cam.shape) != (P, 6) or tuple(K.shape) != (P, 3, 3) or tuple(X.shape) != (n, 3) or \
+            tuple(pts2d.shape) != (n, 2) or tuple(pair_off.shape) != (P + 1,):
+        raise ValueError("shapes must be cam (P,6), K (P,3,3), X (n,3), pts2d (n,2), pair_off (P+1,)")
+    dvc = cam.device
+    cost = torch.empty(P, dtype=torch.float64, device=dvc)
+    nfev = torch.empty(P, dtype=torch.int32, device=dvc)
+    njev = torch.empty(P, dtype=torch.int32, device=dvc)
+    status = torch.empty(P, dtype=torch.int32, device=dvc)
+    call("sfmhip_ba_solve", ptr(cam), ptr(K), ptr(X), ptr(pts2d), ptr(pair_off), P, float(ftol), float(xtol),
+         float(gtol), int(max_nfev or 0), ptr(cost), ptr(nfev), ptr(njev), ptr(status), stream_ptr())
+    return {"cost": cost, "nfev": nfev, "njev": njev, "status": status}
+
+
+def least_squares_ba(x0, K, point_2D, ftol: float = 1e-8, xtol: float = 1e-8, gtol: float = 1e-8,
+                     max_nfev: int | None = None):
+    """Drop-in for sfm.py:38 ``least_squares(calculate_reprojection_error, x0,
+    jac_sparsity=ba_sparse(...), x_scale='jac', ftol=1e-8, args=(K, point_2D))``
+    on one pair: returns an object with scipy's ``x``, ``cost``, ``fun``,
+    ``nfev``, ``njev``, ``status`` and ``success``."""
+    from types import SimpleNamespace
+    dv = require_gpu()
+    x0 = np.asarray(x0, np.float64)
+    p2 = np.asarray(point_2D, np.float64).reshape(-1, 2)
+    n = len(p2)
+    if x0.shape != (6 + 3 * n,):
+        raise ValueError(f"x0 must have 6 + 3 * {n} entries")
+    cam = torch.tensor(x0[:6].reshape(1, 6), device=dv)
+    X = torch.tensor(x0[6:].reshape(n, 3), device=dv)
+    Kt = torch.tensor(np.asarray(K, np.float64).reshape(1, 3, 3), device=dv)
+    pt = torch.tensor(p2, device=dv)
+    off = torch.tensor([0, n], dtype=torch.int64, device=dv)
+    res = ba_solve_batched(cam, Kt, X, pt, off, ftol, xtol, gtol, max_nfev)
+    torch.cuda.synchronize()
+    x = np.concatenate([cam.cpu().numpy().ravel(), X.cpu().numpy().ravel()])
+    status = int(res["status"].item())
+    return SimpleNamespace(x=x, cost=float(res["cost"].item()), fun=calculate_reprojection_error(x, K, p2),
+                           nfev=int(res["nfev"].item()), njev=int(res["njev"].item()), status=status,
+                           success=status > 0)

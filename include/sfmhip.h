@@ -185,6 +185,21 @@ int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, const double* 
                               int n_pairs, int64_t n, const double* f0,
                               double* r, double* jvals, void* stream);
 
+/* The BA solve of sfm.py:37-38 (scipy least_squares, method 'trf', tr_solver
+ * 'lsmr', jac_sparsity = ba_sparse, x_scale = 'jac', ftol / xtol / gtol) for
+ * n_pairs independent problems at once, one workgroup each.  Problem p:
+ * x = [cam[p] (rvec 3, t 3), X[off[p]..off[p+1]) (3 each)], residual
+ * pts2d - projectPoints(X, rvec, t, K[p]) (calculate_reprojection_error,
+ * sfm.py:87-91).  cam (n_pairs, 6) and X (n, 3) are updated in place;
+ * pair_off (n_pairs + 1) int64 device offsets (off[0] = 0, observations of a
+ * pair contiguous); max_nfev <= 0: scipy's default 100 * len(x).  Outputs per
+ * pair: final cost 0.5 |f|^2, nfev, njev, status (scipy's codes 0..4).
+ * The Gauss-Newton direction is the exact damped least-squares solution where
+ * scipy runs LSMR to 1e-6 (oracle/ba.py). */
+int sfmhip_ba_solve(double* cam, const double* K, double* X, const double* pts2d, const int64_t* pair_off,
+                    int n_pairs, double ftol, double xtol, double gtol, int max_nfev, double* cost,
+                    int32_t* nfev, int32_t* njev, int32_t* status, void* stream);
+
 /* ---- V1: voxel_traversal (voxel_travesal.py:1-73), quirks included -------
  * rays [N][8] f32 = o(3), d(3), near, far.  Pass 1 counts per-ray steps
  * (n_steps[N]; a ray still active after max_steps reports max_steps + 1),
