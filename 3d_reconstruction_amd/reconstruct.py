@@ -13,15 +13,20 @@ from __future__ import annotations
 import numpy as np
 from scipy.optimize import least_squares
 
-from .geometry import (Rodrigues, calculate_reprojection_error, convertPointsFromHomogeneous, fd_jacobian,
+from .geometry import (Rodrigues, calculate_reprojection_error, convertPointsFromHomogeneous, fd_jacobian, least_squares_ba,
                        triangulatePoints)
 from . import verify as _verify
 
 FOCAL = 2378.98305085   # sfm.py:24
 
 
-def triangulate(i, j, pts0, pts1, idx0, idx1, idx3d, K, cameras, all_point3ds, all_colors):
-    """sfm.py:26-52.  Returns the focal length (K[0][0]) like the reference."""
+def triangulate(i, j, pts0, pts1, idx0, idx1, idx3d, K, cameras, all_point3ds, all_colors, solver: str = "host"):
+    """sfm.py:26-52.  Returns the focal length (K[0][0]) like the reference.
+
+    ``solver`` for the BA of sfm.py:38: "host" = scipy's least_squares driving
+    the GPU residual and FD Jacobian (the reference's iteration, one device
+    round trip per evaluation); "device" = the whole TRF solve on the GPU
+    (geometry.least_squares_ba: one launch, the same algorithm restated)."""
     X4 = triangulatePoints(np.matmul(K, cameras[i]), np.matmul(K, cameras[j]), pts0.T, pts1.T)
     X4 = X4 / X4[3]
     new_pts = convertPointsFromHomogeneous(X4.T)[:, 0, :]
@@ -30,8 +35,13 @@ def triangulate(i, j, pts0, pts1, idx0, idx1, idx3d, K, cameras, all_point3ds, a
         all_point3ds[1][track] = all_colors[i][idx0[w]]
     rvec = Rodrigues(cameras[j][:3, :3])[0].ravel()
     x0 = np.hstack((rvec, cameras[j][:3, 3].ravel(), np.stack([all_point3ds[0][t] for t in idx3d]).ravel()))
-    res = least_squares(calculate_reprojection_error, x0, jac=fd_jacobian, x_scale="jac", ftol=1e-8,
-                        args=(K, pts1))
+    if solver == "device":
+        res = least_squares_ba(x0, K, pts1, ftol=1e-8)
+    elif solver == "host":
+        res = least_squares(calculate_reprojection_error, x0, jac=fd_jacobian, x_scale="jac", ftol=1e-8,
+                            args=(K, pts1))
+    else:
+        raise ValueError(f"solver must be 'host' or 'device', got {solver!r}")
     R = Rodrigues(res.x[:3])[0]
     t = res.x[3:6]
     refined = res.x[6:].reshape(len(idx3d), 3)

@@ -703,6 +703,57 @@ def ba_line(sfm, syn, device, args, barrier, cpu=True):
     return line
 
 
+def ba_solve_line(sfm, syn, device, args, barrier, cpu=True):
+    """The whole BA solve of sfm.py:37-38 for C3's 256 pairs x 4096 observations
+    on the GPU (ba.hip: scipy's TRF/lsmr iteration restated, one workgroup per
+    pair); the step re-stages the initial cameras/points (device copies) and
+    solves every pair to scipy's termination.  CPU: scipy least_squares with
+    sfm.py:38's settings per pair (the reference call)."""
+    s = syn.ba_scene(BA_PAIRS, BA_OBS, seed=4)
+    tt = {k: torch.from_numpy(np.ascontiguousarray(v)).to(device) for k, v in s.items()}
+    off = torch.arange(BA_PAIRS + 1, dtype=torch.int64, device=device) * BA_OBS
+    cam, X = tt["cam"].clone(), tt["X"].clone()
+    holder = {}
+
+    def step(record):
+        e0, e1 = events() if record else (None, None)
+        if record:
+            e0.record()
+        cam.copy_(tt["cam"])
+        X.copy_(tt["X"])
+        holder["r"] = sfm.ba_solve_batched(cam, tt["K"], X, tt["pts2d"], off)
+        if record:
+            e1.record()
+        return (e0, e1)
+
+    wall, kms = timed(step, args.steps, 1, barrier)
+    ms = wall / args.steps * 1e3
+    r = holder["r"]
+    line = {"metric": "BA solves/sec (sfm.py:38 least_squares, on device)", "value": BA_PAIRS / (ms * 1e-3),
+            "unit": "pairs/s", "ms_per_step": ms, "dtype": "f64",
+            "config": {"workload": f"C3 BA: {BA_PAIRS} pairs x {BA_OBS} obs, scipy TRF (x_scale='jac', ftol 1e-8) "
+                                   f"restated, one workgroup per pair",
+                       "mean_nfev": float(r["nfev"].float().mean().item()),
+                       "status_ok": int((r["status"] > 0).sum().item())},
+            "kernel_ms": float(np.mean(kms))}
+    if cpu:
+        from scipy.optimize import least_squares
+        from oracle import geometry as og
+        sample = spread(BA_PAIRS, 8)
+        A = og.ba_sparse(BA_OBS, 6 + 3 * BA_OBS, 6)
+
+        def one(p):
+            sl = slice(p * BA_OBS, (p + 1) * BA_OBS)
+            x0 = np.concatenate([s["cam"][p], s["X"][sl].ravel()])
+            least_squares(og.reprojection_error, x0, jac_sparsity=A, x_scale="jac", ftol=1e-8,
+                          args=(s["K"][p], s["pts2d"][sl]))
+        line["cpu_baseline"] = cpu_leg(lambda k, nt: pool_map(one, sample[:k], nt), 8, 2, "pairs/s", "reference",
+                                       "scipy.optimize.least_squares with sfm.py:38's arguments (the reference "
+                                       "call) on the restated residual: 8 pairs over a thread pool / 2 pairs on "
+                                       "1 thread")
+    return line
+
+
 def tsdf_cpu_leg(syn):
     """numpy per-frame TSDF oracle (oracle.voxel.tsdf_integrate) on frames of
     the same C5 scene; all threads = z-slabs over a thread pool (numpy drops
@@ -935,6 +986,7 @@ def main():
         result["secondary"].append(ba)
 
         if world == 1:
+            result["secondary"].append(ba_solve_line(sfm, syn, device, args, barrier, cpu=cpu))
             result["secondary"].append(c2_line(sfm, syn, device, args, barrier, cpu=cpu))
             result["secondary"].append(exact_line(sfm, syn, device, args, barrier, cpu=cpu, int8_ms=ms_per_step))
             result["secondary"].extend(voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=cpu))
