@@ -463,6 +463,7 @@ __global__ void nerf_forward_kernel(const float* __restrict__ grid, int D, int H
 //     (non-finite or >= 2^60 anywhere: Z row zeroed, so the frame is skipped).
 // U frames' projections + gathers are issued before their (ordered) updates.
 constexpr int kTsdfMaxFrames = 512;   // frames per launch (host splits longer runs)
+constexpr double kTsdfLatencyRounds = 4.0;   // below: latency mode (tsdf_run)
 constexpr int kTsdfTX = 8, kTsdfTY = 8, kTsdfTZ = 8;    // workgroup tile: 4 waves x (8 x, 2 y, 8 z)
 
 // Spatially compact brick order: the 1-D grid is dealt round-robin over the 8
@@ -1576,7 +1577,24 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const int64_t nsub = (int64_t)nbx * nby * nbz * kCullSub;
     const int per_tile = env_int("SFMHIP_TSDF_CULLSUB", 1) == 4 ? kCullSub : 1;
     // SFMHIP_TSDF_REFINE=0: no per-wave second pass over the projected tile-frames (A/B runs)
-    const bool want_refine = per_tile == 1 && env_int("SFMHIP_TSDF_REFINE", 1) != 0;
+    // Few fusion workgroups per CU (a z-slab of a multi-GPU split: ~2 waves per SIMD slot
+    // at N = 8) make the call latency-bound on its longest waves: then each projected
+    // frame's depth is gathered without the block-table lookup in front of it and the
+    // per-wave refinement pass is skipped (N = 8 centre slab 0.44 -> 0.39 ms; on the
+    // whole grid, 16 rounds, the lookup saves more gathers than it costs: 2.63 vs 2.14 ms).
+    // SFMHIP_TSDF_LATENCY: 0 never, 1 always, default by the rounds of resident waves.
+    int ncu = 256;
+    {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        (void)hipGetLastError();
+    }
+    const double rounds = (double)nbx * nby * nbz * kCullSub / (ncu * 32.0);   // 4 waves per tile, 32 per CU
+    const int lat_env = env_int("SFMHIP_TSDF_LATENCY", -1);
+    const bool latency_mode = lat_env >= 0 ? lat_env != 0 : rounds < kTsdfLatencyRounds;
+    const bool want_refine = per_tile == 1 && env_int("SFMHIP_TSDF_REFINE", latency_mode ? 0 : 1) != 0;
     // cull pass: one workgroup per (4x4x4 brick of sub-tiles, 16 frames)
     const int64_t cull_bricks = (int64_t)ceil_div(nbx, 4) * ceil_div(nby * per_tile, 4) * ceil_div(nbz, 4);
     SFMHIP_REQUIRE(cull_bricks * ceil_div(std::min(chunk, F), 16) < INT_MAX, "sfmhip_tsdf_integrate: grid too large");
@@ -1617,7 +1635,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         (void)hipGetLastError();
     }
     // per-voxel block test in the fusion kernel (with the free-space path; SFMHIP_TSDF_VOXTEST=0 off)
-    const bool vox_test = cfree && env_int("SFMHIP_TSDF_VOXTEST", 1) != 0;
+    const bool vox_test = cfree && env_int("SFMHIP_TSDF_VOXTEST", latency_mode ? 0 : 1) != 0;
     // longest-first workgroup order (SFMHIP_TSDF_ORDER=0 off): needs the masks and the 1-D slot grid;
     // bucket sort positions are 16-bit, so at most 65535 slots per XCD class
     unsigned* ord = nullptr;

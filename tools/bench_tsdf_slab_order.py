@@ -29,7 +29,8 @@ def timed(reps=7):
         W[z0:z1].zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        sfm.tsdf_integrate(T, W, *args, z0, z1, block_table=tab)
+        sfm.tsdf_integrate(T, W, *args, z0, z1, block_table=tab) if tab is not None else \
+            sfm.tsdf_integrate(T, W, *args, z0, z1)
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
@@ -37,8 +38,10 @@ def timed(reps=7):
 
 
 ref = None
-VARIANTS = [("default", {}), ("ORDER=0", {"SFMHIP_TSDF_ORDER": "0"}), ("SWZ=0", {"SFMHIP_TSDF_SWZ": "0"}),
-            ("default", {}), ("ORDER=0", {"SFMHIP_TSDF_ORDER": "0"})]
+VARIANTS = [("default", {}), ("LATENCY=0", {"SFMHIP_TSDF_LATENCY": "0"}), ("LATENCY=1", {"SFMHIP_TSDF_LATENCY": "1"}),
+            ("default", {}), ("LATENCY=0", {"SFMHIP_TSDF_LATENCY": "0"}), ("LATENCY=1", {"SFMHIP_TSDF_LATENCY": "1"})]
+if os.environ.get("NO_TABLE"):   # the single-GPU call: the block pass inside tsdf_integrate
+    tab = None
 for name, env in VARIANTS:
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
