@@ -535,22 +535,60 @@ constexpr int kCullMaxBlocks = 256;   // larger footprints are simply kept
 // the X/Z, Y/Z interval quotients.  Returns 0 (no bound: box not safely in
 // front of the camera), 1 (every voxel's pixel is off-image) or 2 (pixel range
 // [u0,u1] x [v0,v1], clipped to the image, and zlo <= every f32 Zc).
-__device__ int box_footprint(const float* P, const float* k, const Bounds& B, int D, int H, int W, int xa, int xb,
-                             int ya, int yb, int za, int zb, int Hd, int Wd, int& u0, int& u1, int& v0, int& v1,
-                             double& zlo, double& zhi, bool& inside) {
-    const double sx = ((double)B.mx[0] - B.mn[0]) / (W - 1), sy = ((double)B.mx[1] - B.mn[1]) / (H - 1),
-                 sz = ((double)B.mx[2] - B.mn[2]) / (D - 1);
-    const double cxw = B.mn[0] + 0.5 * (xa + xb) * sx, hx = 0.5 * (xb - xa) * fabs(sx);
-    const double cyw = B.mn[1] + 0.5 * (ya + yb) * sy, hy = 0.5 * (yb - ya) * fabs(sy);
-    const double czw = B.mn[2] + 0.5 * (za + zb) * sz, hz = 0.5 * (zb - za) * fabs(sz);
+// The culling passes' f64 view of the grid (host-computed: the same IEEE divisions
+// as before, once per call) and of a frame (CullCam, built once per frame by
+// cull_cam_kernel and read with scalar loads where the frame is wave-uniform).
+struct CullGeom { double mn[3], s[3], as[3]; };
+struct CullCam { double P[12], aP[12], k[4], good, pad[3]; };   // 256 B
+
+__device__ __forceinline__ void cull_cam(const float* __restrict__ poses, const float* __restrict__ Kf, int f,
+                                         CullCam& c) {
+    bool good = true;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+        const float x = poses[f * 12 + q];
+        c.P[q] = x;
+        c.aP[q] = fabs((double)x);
+        good = good && fabsf(x) < 0x1p60f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float x = Kf[f * 4 + q];
+        c.k[q] = x;
+        good = good && fabsf(x) < 0x1p60f;
+    }
+    c.good = good ? 1.0 : 0.0;
+}
+
+// Newton-refined v_rcp_f64 (a few ulps of 1/z; the bounds below carry margins of
+// ~2^-21 relative, so the footprint stays conservative).
+__device__ __forceinline__ double cull_rcp(double z) {
+    double r = __builtin_amdgcn_rcp(z);
+    r = fma(fma(-z, r, 1.0), r, r);
+    return fma(fma(-z, r, 1.0), r, r);
+}
+
+// Conservative pixel footprint of the voxel box [xa,xb] x [ya,yb] x [za,zb] in
+// frame c: interval bounds on the affine camera coordinates (centre +- sum |P_rj|
+// h_j) widened by a bound on the fusion kernel's f32 rounding, and the X/Z, Y/Z
+// interval quotients.  Returns 0 (no bound: box not safely in front of the
+// camera), 1 (every voxel's pixel is off-image) or 2 (pixel range [u0,u1] x
+// [v0,v1], clipped to the image, and zlo <= every f32 Zc).
+__device__ __forceinline__ int box_footprint(const CullCam& cc, const CullGeom& G, int xa, int xb, int ya, int yb,
+                                             int za, int zb, int Hd, int Wd, int& u0, int& u1, int& v0, int& v1,
+                                             double& zlo, double& zhi, bool& inside) {
+    const double cxw = G.mn[0] + 0.5 * (xa + xb) * G.s[0], hx = 0.5 * (xb - xa) * G.as[0];
+    const double cyw = G.mn[1] + 0.5 * (ya + yb) * G.s[1], hy = 0.5 * (yb - ya) * G.as[1];
+    const double czw = G.mn[2] + 0.5 * (za + zb) * G.s[2], hz = 0.5 * (zb - za) * G.as[2];
     const double mxw = fabs(cxw) + hx, myw = fabs(cyw) + hy, mzw = fabs(czw) + hz;   // |coord| bounds
     double c[3], e[3], mag[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-        const double p0 = P[4 * r], p1 = P[4 * r + 1], p2 = P[4 * r + 2], p3 = P[4 * r + 3];
-        c[r] = p0 * cxw + p1 * cyw + p2 * czw + p3;
-        e[r] = fabs(p0) * hx + fabs(p1) * hy + fabs(p2) * hz;
-        mag[r] = fabs(p0) * mxw + fabs(p1) * myw + fabs(p2) * mzw + fabs(p3);
+        const double* p = cc.P + 4 * r;
+        const double* a = cc.aP + 4 * r;
+        c[r] = p[0] * cxw + p[1] * cyw + p[2] * czw + p[3];
+        e[r] = a[0] * hx + a[1] * hy + a[2] * hz;
+        mag[r] = a[0] * mxw + a[1] * myw + a[2] * mzw + a[3];
     }
     // f32 error of the kernel's Zc / Xc / Yc (unit roundoff 2^-24, generous op counts)
     const double eps = 0x1p-24;
@@ -559,20 +597,20 @@ __device__ int box_footprint(const float* P, const float* k, const Bounds& B, in
     zhi = c[2] + e[2] + dz;
     inside = false;
     if (!(zlo > 1e-3 && zhi < 1e30 && c[0] == c[0] && c[1] == c[1])) return 0;
-    const double izl = 1.0 / zlo, izh = 1.0 / zhi;
+    const double izl = cull_rcp(zlo), izh = cull_rcp(zhi);
     const double xl = c[0] - e[0] - 8 * eps * mag[0], xh = c[0] + e[0] + 8 * eps * mag[0];
     const double yl = c[1] - e[1] - 8 * eps * mag[1], yh = c[1] + e[1] + 8 * eps * mag[1];
     const double qx0 = fmin(fmin(xl * izl, xl * izh), fmin(xh * izl, xh * izh));
     const double qx1 = fmax(fmax(xl * izl, xl * izh), fmax(xh * izl, xh * izh));
     const double qy0 = fmin(fmin(yl * izl, yl * izh), fmin(yh * izl, yh * izh));
     const double qy1 = fmax(fmax(yl * izl, yl * izh), fmax(yh * izl, yh * izh));
-    const double ua = (double)k[0] * qx0, ub = (double)k[0] * qx1, va = (double)k[1] * qy0, vb = (double)k[1] * qy1;
-    const double um0 = fmin(ua, ub) + k[2] + 0.5, um1 = fmax(ua, ub) + k[2] + 0.5;
-    const double vm0 = fmin(va, vb) + k[3] + 0.5, vm1 = fmax(va, vb) + k[3] + 0.5;
+    const double ua = cc.k[0] * qx0, ub = cc.k[0] * qx1, va = cc.k[1] * qy0, vb = cc.k[1] * qy1;
+    const double um0 = fmin(ua, ub) + cc.k[2] + 0.5, um1 = fmax(ua, ub) + cc.k[2] + 0.5;
+    const double vm0 = fmin(va, vb) + cc.k[3] + 0.5, vm1 = fmax(va, vb) + cc.k[3] + 0.5;
     if (!(um0 > -1e9 && um1 < 1e9 && vm0 > -1e9 && vm1 < 1e9)) return 0;
     // rounding of (f X) iz + c: a few ulps of the magnitudes involved
-    const double du = 8 * eps * (fmax(fabs(um0), fabs(um1)) + fabs((double)k[2]) + 1) + 1e-3;
-    const double dv = 8 * eps * (fmax(fabs(vm0), fabs(vm1)) + fabs((double)k[3]) + 1) + 1e-3;
+    const double du = 8 * eps * (fmax(fabs(um0), fabs(um1)) + fabs(cc.k[2]) + 1) + 1e-3;
+    const double dv = 8 * eps * (fmax(fabs(vm0), fabs(vm1)) + fabs(cc.k[3]) + 1) + 1e-3;
     u0 = (int)floor(um0 - du);
     u1 = (int)floor(um1 + du);
     v0 = (int)floor(vm0 - dv);
@@ -581,6 +619,16 @@ __device__ int box_footprint(const float* P, const float* k, const Bounds& B, in
     inside = u0 >= 0 && v0 >= 0 && u1 < Wd && v1 < Hd;
     u0 = max(u0, 0); u1 = min(u1, Wd - 1); v0 = max(v0, 0); v1 = min(v1, Hd - 1);
     return 2;
+}
+
+__global__ void cull_cam_kernel(const float* __restrict__ poses, const float* __restrict__ Kf, int F,
+                                CullCam* __restrict__ out) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    CullCam c;
+    cull_cam(poses, Kf, f, c);
+    c.pad[0] = c.pad[1] = c.pad[2] = 0.0;
+    out[f] = c;
 }
 
 __global__ void full_range_kernel(int F, int nbu, int nbv, int4* __restrict__ range) {
@@ -592,16 +640,17 @@ __global__ void full_range_kernel(int F, int nbu, int nbv, int4* __restrict__ ra
 // bv1}; an empty range when the whole slab is off-image, every block when the
 // footprint cannot be bounded).  The block-max pass fills only these blocks and
 // the tile test reads only inside them.
-__global__ void tsdf_footprint_kernel(int D, int H, int W, int z0, int z1, int F, int Hd, int Wd,
-                                      const float* __restrict__ poses, const float* __restrict__ Kf, Bounds B,
+__global__ void tsdf_footprint_kernel(int H, int W, int z0, int z1, int F, int Hd, int Wd,
+                                      const float* __restrict__ poses, const float* __restrict__ Kf, CullGeom G,
                                       int nbu, int nbv, int4* __restrict__ range) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= F) return;
     int u0, u1, v0, v1;
     double zlo, zhi;
     bool inside;
-    const int st = box_footprint(poses + f * 12, Kf + f * 4, B, D, H, W, 0, W - 1, 0, H - 1, z0, z1 - 1, Hd, Wd, u0,
-                                 u1, v0, v1, zlo, zhi, inside);
+    CullCam cc;
+    cull_cam(poses, Kf, f, cc);
+    const int st = box_footprint(cc, G, 0, W - 1, 0, H - 1, z0, z1 - 1, Hd, Wd, u0, u1, v0, v1, zlo, zhi, inside);
     range[f] = st == 2   ? make_int4(u0 / kCullBlock, u1 / kCullBlock, v0 / kCullBlock, v1 / kCullBlock)
                : st == 1 ? make_int4(1, 0, 1, 0)
                          : make_int4(0, nbu - 1, 0, nbv - 1);
@@ -673,25 +722,27 @@ constexpr int kCullSub = 4;   // waves per workgroup tile
 
 // The (box, frame) test: skip = provably no voxel of the box updates; fre = every
 // voxel of the box updates with tsdf = 1 (free space).
-__device__ __forceinline__ void cull_test(const float* __restrict__ poses, const float* __restrict__ Kf, int f,
-                                          const Bounds& B, int D, int H, int W, int xa, int xb, int ya, int yb,
-                                          int za, int zb, int Hd, int Wd, float trunc,
+// BLK: pixel edge of the table's blocks; CAP: larger footprints are kept; range null:
+// every entry of the table is valid.
+template <int BLK = kCullBlock, int CAP = kCullMaxBlocks>
+__device__ __forceinline__ void cull_test(const CullCam& cc, const CullGeom& G, int xa, int xb, int ya, int yb,
+                                          int za, int zb, int Hd, int Wd, float trunc, int f,
                                           const float2* __restrict__ bmm, int use_free, int nbu, int nbv,
                                           const int4* __restrict__ range, bool& skip, bool& fre) {
     skip = fre = false;
     int u0, u1, v0, v1;
     double zlo, zhi;
     bool inside = false;
-    const int st = ya <= yb ? box_footprint(poses + f * 12, Kf + f * 4, B, D, H, W, xa, xb, ya, yb, za, zb, Hd, Wd,
-                                            u0, u1, v0, v1, zlo, zhi, inside)
+    const int st = ya <= yb ? box_footprint(cc, G, xa, xb, ya, yb, za, zb, Hd, Wd, u0, u1, v0, v1, zlo, zhi, inside)
                             : 0;
     if (st == 1) {
         skip = true;
     } else if (st == 2) {
-        const int bu0 = u0 / kCullBlock, bu1 = u1 / kCullBlock, bv0 = v0 / kCullBlock, bv1 = v1 / kCullBlock;
-        const int4 rg = range[f];   // only blocks inside the slab's range were computed
+        const int bu0 = u0 / BLK, bu1 = u1 / BLK, bv0 = v0 / BLK, bv1 = v1 / BLK;
+        // only blocks inside the slab's range were computed
+        const int4 rg = range ? range[f] : make_int4(0, nbu - 1, 0, nbv - 1);
         const int nu = bu1 - bu0 + 1, nb = nu * (bv1 - bv0 + 1);
-        if (nb <= kCullMaxBlocks && bu0 >= rg.x && bu1 <= rg.y && bv0 >= rg.z && bv1 <= rg.w) {
+        if (nb <= CAP && bu0 >= rg.x && bu1 <= rg.y && bv0 >= rg.z && bv1 <= rg.w) {
             const float2* bp = bmm + ((size_t)f * nbv + bv0) * nbu + bu0;
             float m = -__builtin_inff(), mn = __builtin_inff();
             for (int bv = bv0; bv <= bv1; ++bv, bp += nbu) {
@@ -709,16 +760,90 @@ __device__ __forceinline__ void cull_test(const float* __restrict__ poses, const
             // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for the
             // rounding of (depth - Zc), so the kernel's !(sdf < -trunc) test fails everywhere
             skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * 0x1p-24) + 1e-30 < zlo);
-            if (!skip && use_free && inside && zlo >= 0x1p-59 && zhi <= 0x1p59) {
-                bool good = true;
-#pragma unroll
-                for (int q = 0; q < 12; ++q) good = good && fabsf(poses[f * 12 + q]) < 0x1p60f;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) good = good && fabsf(Kf[f * 4 + q]) < 0x1p60f;
-                fre = good && (double)mn - zhi >= (double)trunc * (1 + 0x1p-20);
-            }
+            // free space needs a frame record the fusion kernel fuses (every parameter < 2^60)
+            if (!skip && use_free && inside && zlo >= 0x1p-59 && zhi <= 0x1p59 && cc.good != 0.0)
+                fre = (double)mn - zhi >= (double)trunc * (1 + 0x1p-20);
         }
     }
+}
+
+// The frame record of frame f from the per-call table: f is wave-uniform at every
+// call site that uses it, so these are scalar loads.
+__device__ __forceinline__ void load_cull_cam(const CullCam* __restrict__ tab, int f, CullCam& c) {
+    const CullCam* p = tab + __builtin_amdgcn_readfirstlane(f);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) { c.P[q] = p->P[q]; c.aP[q] = p->aP[q]; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c.k[q] = p->k[q];
+    c.good = p->good;
+}
+
+// Brick pre-pass (SFMHIP_TSDF_BRICK=0 off).  The cull pass's workgroups are 4x4x4
+// bricks of tiles (32^3 voxels); a brick-level test decides ~40 % of the (brick,
+// frame) pairs of C5 outright (culled or free space; tools/sim_brick_cull.py), and
+// the cull pass's wave for such a pair writes the decision without its 64 tile tests.
+// The brick test reads a 4x coarser table (64x64-pixel blocks), so a brick footprint
+// of up to 512 px square costs at most 64 loads.  Every decision is the same proof
+// as the tile test's, on a box that contains the tile's voxels.
+constexpr int kCoarse = 4;
+constexpr int kCoarseBlock = kCullBlock * kCoarse;
+constexpr int kCoarseMaxBlocks = 64;
+
+// Coarse {min, max} of kCoarse x kCoarse fine blocks; an entry with a fine block the
+// slab's range did not compute is (-inf, +inf), which never decides anything.
+__global__ void coarse_table_kernel(const float2* __restrict__ bmm, int nf, int nbu, int nbv, int ncu, int ncv,
+                                    const int4* __restrict__ range, float2* __restrict__ cmm) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)nf * ncu * ncv) return;
+    const int cu = (int)(i % ncu), cv = (int)((i / ncu) % ncv), f = (int)(i / ((int64_t)ncu * ncv));
+    const int4 rg = range ? range[f] : make_int4(0, nbu - 1, 0, nbv - 1);
+    const int bu0 = cu * kCoarse, bu1 = min(nbu, bu0 + kCoarse) - 1;
+    const int bv0 = cv * kCoarse, bv1 = min(nbv, bv0 + kCoarse) - 1;
+    float mn = __builtin_inff(), m = -__builtin_inff();
+    if (bu0 >= rg.x && bu1 <= rg.y && bv0 >= rg.z && bv1 <= rg.w) {
+        for (int bv = bv0; bv <= bv1; ++bv)
+            for (int bu = bu0; bu <= bu1; ++bu) {
+                const float2 e = bmm[((size_t)f * nbv + bv) * nbu + bu];
+                mn = fminf(mn, e.x);
+                m = fmaxf(m, e.y);
+            }
+    } else {
+        mn = -__builtin_inff();
+        m = __builtin_inff();
+    }
+    cmm[i] = make_float2(mn, m);
+}
+
+// One lane per (cull brick, frame): byte 0 undecided, 1 culled, 2 free space.
+// Lanes are (frame, brick) with the brick count padded to whole waves, so the
+// frame, and its record, is wave-uniform.
+__global__ __launch_bounds__(256) void tsdf_brick_kernel(int H, int W, int z0, int z1, int F, int Hd, int Wd,
+                                                         const CullCam* __restrict__ cams, CullGeom G, float trunc,
+                                                         const float2* __restrict__ cmm, int use_free, int ncu,
+                                                         int ncv, int per_tile, int nbricks,
+                                                         unsigned char* __restrict__ bdec) {
+    const int npad = (nbricks + 63) & ~63;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int f = (int)(g / npad), brick = (int)(g % npad);
+    if (f >= F) return;   // wave-uniform
+    CullCam cc;
+    load_cull_cam(cams, f, cc);
+    if (brick >= nbricks) return;
+    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
+    const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
+    const int nsy = nty * per_tile;
+    const int nqx = (ntx + 3) >> 2, nqy = (nsy + 3) >> 2;
+    const int qx = brick % nqx, qy = (brick / nqx) % nqy, qz = brick / (nqx * nqy);
+    const int sub = kTsdfTY / per_tile;   // voxel rows per sub-tile
+    const int sy0 = qy * 4, sy1 = min(nsy, sy0 + 4) - 1;
+    const int xa = qx * 4 * kTsdfTX, xb = min(W, (qx * 4 + 4) * kTsdfTX) - 1;
+    const int ya = (sy0 / per_tile) * kTsdfTY + sub * (sy0 % per_tile);
+    const int yb = min(H, (sy1 / per_tile) * kTsdfTY + sub * (sy1 % per_tile + 1)) - 1;
+    const int za = z0 + qz * 4 * kTsdfTZ, zb = min(z1, z0 + min(ntz, qz * 4 + 4) * kTsdfTZ) - 1;
+    bool skip, fre;
+    cull_test<kCoarseBlock, kCoarseMaxBlocks>(cc, G, xa, xb, ya, yb, za, zb, Hd, Wd, trunc, f, cmm, use_free, ncu,
+                                              ncv, nullptr, skip, fre);
+    bdec[(size_t)f * nbricks + brick] = (unsigned char)(skip ? 1 : fre ? 2 : 0);
 }
 
 // One workgroup per (4x4x4 brick of tiles or sub-tiles, 16 frames): wave j tests
@@ -729,11 +854,13 @@ __device__ __forceinline__ void cull_test(const float* __restrict__ poses, const
 // frame 32 w + j.  With `plist` (per_tile = 1), every (tile, frame) that is
 // neither culled nor free space is appended to a list for tsdf_refine_kernel.
 constexpr int kCullFrames = 16;
-__global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, int z0, int z1, int F, int Hd, int Wd,
-                                                         const float* __restrict__ poses, const float* __restrict__ Kf,
-                                                         Bounds B, float trunc, const float2* __restrict__ bmm,
+// waves_per_eu(8): two 16-wave workgroups per CU (the f64 frame record lives in SGPRs)
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void tsdf_cull_kernel(int H, int W, int z0, int z1, int F, int Hd, int Wd,
+                                                         const CullCam* __restrict__ cams, CullGeom G, float trunc,
+                                                         const float2* __restrict__ bmm,
                                                          int use_free, int nbu, int nbv,
                                                          const int4* __restrict__ range, int per_tile, int nw,
+                                                         const unsigned char* __restrict__ bdec,
                                                          unsigned short* __restrict__ cull,
                                                          unsigned short* __restrict__ freem,
                                                          unsigned* __restrict__ plist, unsigned* __restrict__ pcount) {
@@ -753,12 +880,18 @@ __global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, in
     const int ty = sy / per_tile, w = sy % per_tile;
     const int64_t tile = ((int64_t)tz * nty + ty) * ntx + tx;
     bool skip = false, fre = false;
-    if (tile_ok && f < F) {
+    // the brick pre-pass's decision for (brick, frame f): wave-uniform
+    const int dec = bdec && f < F ? bdec[(size_t)__builtin_amdgcn_readfirstlane(f) * (gridDim.x / nh) + brick] : 0;
+    if (tile_ok && f < F && dec) {
+        skip = dec == 1;
+        fre = dec == 2;
+    } else if (tile_ok && f < F) {
         const int xa = tx * kTsdfTX, xb = min(W, xa + kTsdfTX) - 1;
         const int ya = ty * kTsdfTY + (kTsdfTY / per_tile) * w, yb = min(H, ya + kTsdfTY / per_tile) - 1;
         const int za = z0 + tz * kTsdfTZ, zb = min(z1, za + kTsdfTZ) - 1;
-        cull_test(poses, Kf, f, B, D, H, W, xa, xb, ya, yb, za, zb, Hd, Wd, trunc, bmm, use_free, nbu, nbv, range,
-                  skip, fre);
+        CullCam cc;
+        load_cull_cam(cams, f, cc);
+        cull_test(cc, G, xa, xb, ya, yb, za, zb, Hd, Wd, trunc, f, bmm, use_free, nbu, nbv, range, skip, fre);
     }
     // compact list of the projected (tile, frame) pairs: one atomic per workgroup
     __shared__ unsigned wcnt[kCullFrames + 1];
@@ -804,9 +937,9 @@ __global__ __launch_bounds__(1024) void tsdf_cull_kernel(int D, int H, int W, in
 // gets its bit set in its own wave slot's mask (the tile-level bits of a
 // projected pair are 0, so OR-ing refines them).  Grid-stride over the device-side
 // count, so the host never waits for it.
-__global__ __launch_bounds__(256) void tsdf_refine_kernel(int D, int H, int W, int z0, int z1, int F, int Hd,
+__global__ __launch_bounds__(256) void tsdf_refine_kernel(int H, int W, int z0, int z1, int F, int Hd,
                                                           int Wd, const float* __restrict__ poses,
-                                                          const float* __restrict__ Kf, Bounds B, float trunc,
+                                                          const float* __restrict__ Kf, CullGeom G, float trunc,
                                                           const float2* __restrict__ bmm, int use_free, int nbu,
                                                           int nbv, const int4* __restrict__ range, int nw,
                                                           unsigned* __restrict__ cull, unsigned* __restrict__ freem,
@@ -823,8 +956,9 @@ __global__ __launch_bounds__(256) void tsdf_refine_kernel(int D, int H, int W, i
         const int ya = ty * kTsdfTY + (kTsdfTY / kCullSub) * q, yb = min(H, ya + kTsdfTY / kCullSub) - 1;
         const int za = z0 + tz * kTsdfTZ, zb = min(z1, za + kTsdfTZ) - 1;
         bool skip, fre;
-        cull_test(poses, Kf, f, B, D, H, W, xa, xb, ya, yb, za, zb, Hd, Wd, trunc, bmm, use_free, nbu, nbv, range,
-                  skip, fre);
+        CullCam cc;   // f differs per lane here: the record from the f32 inputs
+        cull_cam(poses, Kf, f, cc);
+        cull_test(cc, G, xa, xb, ya, yb, za, zb, Hd, Wd, trunc, f, bmm, use_free, nbu, nbv, range, skip, fre);
         const int64_t word = (tile * kCullSub + q) * nw + (f >> 5);
         if (skip) atomicOr(cull + word, 1u << (f & 31));
         else if (fre && freem) atomicOr(freem + word, 1u << (f & 31));
@@ -966,7 +1100,7 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
                                                    float trunc, SuperBrick SB, const unsigned* __restrict__ cull,
                                                    const unsigned* __restrict__ freem, int nw, float free_ts,
                                                    const float2* __restrict__ bmm, int nbu, int nbv,
-                                                   const unsigned* __restrict__ order) {
+                                                   const unsigned* __restrict__ order, int easy) {
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (SWZ) tsdf_slot_tile(order ? (int)order[blockIdx.x] : (int)blockIdx.x, gridDim.x, W, H, SB, bx, by, bz);
     const int l = threadIdx.x & 63;
@@ -1082,7 +1216,17 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
             const bool g0 = fr0 || (need0 && dep.x > 0.f && !(sdf.x < -trunc));
             const bool g1 = fr1 || (need1 && dep.y > 0.f && !(sdf.y < -trunc));
             const f2 sc = sdf * f2s(inv_trunc);
-            update(f2{fr0 ? free_ts : fminf(1.0f, sc.x), fr1 ? free_ts : fminf(1.0f, sc.y)}, g0, g1);
+            const f2 ts = {fr0 ? free_ts : fminf(1.0f, sc.x), fr1 ? free_ts : fminf(1.0f, sc.y)};
+            // every updating voxel of the wave has tsdf = 1, T = 1 and an integer W: each
+            // update is (1 W + 1)/(W + 1) = 1 and W + 1, exactly (no division)
+            const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && w_runs(wv.x));
+            const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && w_runs(wv.y));
+            if (easy && __builtin_amdgcn_ballot_w64(!(easy0 && easy1)) == 0) {
+                wv.x = g0 ? wv.x + 1.f : wv.x;
+                wv.y = g1 ? wv.y + 1.f : wv.y;
+            } else {
+                update(ts, g0, g1);
+            }
         }
     }
     T[idx] = tv.x;
@@ -1569,6 +1713,15 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         grid = dim3((unsigned)slots, 1, 1);
     }
     const Bounds bb = make_bounds(bmin, bmax);
+    CullGeom cg;
+    {
+        const int n[3] = {W, H, D};
+        for (int a = 0; a < 3; ++a) {
+            cg.mn[a] = bb.mn[a];
+            cg.s[a] = ((double)bb.mx[a] - bb.mn[a]) / (n[a] - 1);
+            cg.as[a] = std::fabs(cg.s[a]);
+        }
+    }
     hipStream_t st = as_stream(stream);
     // Scratch (stream-ordered): validated camera records; culling buffers
     // (SFMHIP_TSDF_CULL=0 disables culling, SFMHIP_TSDF_FREE=0 the free-space path, for A/B
@@ -1604,8 +1757,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const float free_ts = free_env == 2 ? 0.5f : 1.0f;
     const int cf = std::min(chunk, F);
     const size_t nblk = (size_t)cf * nbu * nbv;
-    float* rec = nullptr;
-    if (scratch_alloc((void**)&rec, (size_t)cf * 16 * sizeof(float), st) != hipSuccess) {
+    float* rec = nullptr;   // the fusion kernel's f32 records, then the culling passes' CullCam table
+    if (scratch_alloc((void**)&rec, (size_t)cf * (16 * sizeof(float) + sizeof(CullCam)), st) != hipSuccess) {
         (void)hipGetLastError();
         set_error("sfmhip_tsdf_integrate: camera table allocation failed");
         return SFMHIP_E_HIP;
@@ -1614,6 +1767,9 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     unsigned* cfree = nullptr;
     unsigned* cmask = nullptr;
     unsigned* plist = nullptr;   // projected (tile, frame) list + its count (last element)
+    float2* ctab = nullptr;      // coarse table + brick decisions (brick pre-pass)
+    unsigned char* bdec = nullptr;
+    const int ncbu = ceil_div(nbu, kCoarse), ncbv = ceil_div(nbv, kCoarse);
     int4* crange = nullptr;
     const int64_t ntile_frames = (int64_t)nbx * nby * nbz * std::min(chunk, F);
     if (want_cull) {
@@ -1629,6 +1785,13 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         }
         if (cmask && want_free && scratch_alloc((void**)&cfree, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess)
             cfree = nullptr;   // free-space path off, culling unchanged
+        if (cmask && env_int("SFMHIP_TSDF_BRICK", 1) != 0) {
+            if (scratch_alloc((void**)&ctab, (size_t)cf * ncbu * ncbv * sizeof(float2) + (size_t)cull_bricks * cf, st) ==
+                hipSuccess)
+                bdec = reinterpret_cast<unsigned char*>(ctab + (size_t)cf * ncbu * ncbv);
+            else
+                ctab = nullptr;   // no brick pre-pass
+        }
         if (cmask && want_refine && ntile_frames < (int64_t)1 << 30 && nbx * nby * nbz < (1 << 23) &&
             scratch_alloc((void**)&plist, (size_t)(ntile_frames + 1) * sizeof(unsigned), st) != hipSuccess)
             plist = nullptr;   // no second pass
@@ -1636,6 +1799,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     }
     // per-voxel block test in the fusion kernel (with the free-space path; SFMHIP_TSDF_VOXTEST=0 off)
     const bool vox_test = cfree && env_int("SFMHIP_TSDF_VOXTEST", latency_mode ? 0 : 1) != 0;
+    // division-free update of projected frames whose updates are all tsdf = 1 on T = 1 (SFMHIP_TSDF_EASY=0 off)
+    const int easy = env_int("SFMHIP_TSDF_EASY", 1) != 0;
     // longest-first workgroup order (SFMHIP_TSDF_ORDER=0 off): needs the masks and the 1-D slot grid;
     // bucket sort positions are 16-bit, so at most 65535 slots per XCD class
     unsigned* ord = nullptr;
@@ -1656,12 +1821,14 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         const float* pp = poses + (size_t)f0 * 12;
         const float* kp = Kf + (size_t)f0 * 4;
         hipLaunchKernelGGL(tsdf_cam_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, pp, kp, nf, rec);
+        CullCam* ccam = reinterpret_cast<CullCam*>(rec + (size_t)cf * 16);
+        if (cmask) hipLaunchKernelGGL(cull_cam_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, pp, kp, nf, ccam);
         const float2* tab = ext_table ? ext_table + (size_t)f0 * nbv * nbu : cbmm;
         if (cmask && ext_table) {
             hipLaunchKernelGGL(full_range_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, nf, nbu, nbv, crange);
         } else if (cmask) {
-            hipLaunchKernelGGL(tsdf_footprint_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, D, H, W, z0, z1, nf, Hd,
-                               Wd, pp, kp, bb, nbu, nbv, crange);
+            hipLaunchKernelGGL(tsdf_footprint_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, H, W, z0, z1, nf, Hd,
+                               Wd, pp, kp, cg, nbu, nbv, crange);
             if (Wd % 4 == 0)
                 hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st,
                                    dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
@@ -1672,12 +1839,20 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         if (cmask) {
             unsigned* pcount = plist ? plist + ntile_frames : nullptr;
             if (plist) (void)hipMemsetAsync(pcount, 0, sizeof(unsigned), st);
-            hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nwf * 2)), dim3(1024), 0, st, D, H,
-                               W, z0, z1, nf, Hd, Wd, pp, kp, bb, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
-                               nwf, (unsigned short*)cmask, (unsigned short*)cfree, plist, pcount);
+            if (bdec) {
+                const int64_t nc = (int64_t)nf * ncbu * ncbv, nd = (cull_bricks + 63) / 64 * 64 * nf;
+                hipLaunchKernelGGL(coarse_table_kernel, dim3((unsigned)ceil_div(nc, (int64_t)256)), dim3(256), 0, st,
+                                   tab, nf, nbu, nbv, ncbu, ncbv, ext_table ? nullptr : crange, ctab);
+                hipLaunchKernelGGL(tsdf_brick_kernel, dim3((unsigned)ceil_div(nd, (int64_t)256)), dim3(256), 0, st, H,
+                                   W, z0, z1, nf, Hd, Wd, ccam, cg, trunc, ctab, cfree ? 1 : 0, ncbu, ncbv, per_tile,
+                                   (int)cull_bricks, bdec);
+            }
+            hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nwf * 2)), dim3(1024), 0, st, H,
+                               W, z0, z1, nf, Hd, Wd, ccam, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
+                               nwf, bdec, (unsigned short*)cmask, (unsigned short*)cfree, plist, pcount);
             if (plist)
-                hipLaunchKernelGGL(tsdf_refine_kernel, dim3(2048), dim3(256), 0, st, D, H, W, z0, z1, nf, Hd, Wd, pp,
-                                   kp, bb, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, nwf, cmask, cfree, plist,
+                hipLaunchKernelGGL(tsdf_refine_kernel, dim3(2048), dim3(256), 0, st, H, W, z0, z1, nf, Hd, Wd, pp,
+                                   kp, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, nwf, cmask, cfree, plist,
                                    pcount);
         }
         if (stats) {
@@ -1727,10 +1902,10 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         }
         if (swz)
             hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, ord);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, ord, easy);
         else
             hipLaunchKernelGGL(tsdf_kernel<false>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, nullptr);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, nullptr, easy);
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }
@@ -1739,6 +1914,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     if (crange) (void)hipFreeAsync(crange, st);
     if (cmask) (void)hipFreeAsync(cmask, st);
     if (plist) (void)hipFreeAsync(plist, st);
+    if (ctab) (void)hipFreeAsync(ctab, st);
     if (cbmm && !ext_table) (void)hipFreeAsync(cbmm, st);
     if (cfree) (void)hipFreeAsync(cfree, st);
     return rc;
