@@ -537,7 +537,7 @@ constexpr int kCullMaxBlocks = 256;   // larger footprints are simply kept
 // [u0,u1] x [v0,v1], clipped to the image, and zlo <= every f32 Zc).
 // The culling passes' f64 view of the grid (host-computed: the same IEEE divisions
 // as before, once per call) and of a frame (CullCam, built once per frame by
-// cull_cam_kernel and read with scalar loads where the frame is wave-uniform).
+// tsdf_setup_kernel and read with scalar loads where the frame is wave-uniform).
 struct CullGeom { double mn[3], s[3], as[3]; };
 struct CullCam { double P[12], aP[12], k[4], good, pad[3]; };   // 256 B
 
@@ -621,40 +621,15 @@ __device__ __forceinline__ int box_footprint(const CullCam& cc, const CullGeom& 
     return 2;
 }
 
-__global__ void cull_cam_kernel(const float* __restrict__ poses, const float* __restrict__ Kf, int F,
-                                CullCam* __restrict__ out) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= F) return;
-    CullCam c;
-    cull_cam(poses, Kf, f, c);
-    c.pad[0] = c.pad[1] = c.pad[2] = 0.0;
-    out[f] = c;
-}
-
 __global__ void full_range_kernel(int F, int nbu, int nbv, int4* __restrict__ range) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f < F) range[f] = make_int4(0, nbu - 1, 0, nbv - 1);
 }
 
-// Per frame: the depth blocks the slab [z0, z1) can touch (int4 {bu0, bu1, bv0,
-// bv1}; an empty range when the whole slab is off-image, every block when the
-// footprint cannot be bounded).  The block-max pass fills only these blocks and
-// the tile test reads only inside them.
-__global__ void tsdf_footprint_kernel(int H, int W, int z0, int z1, int F, int Hd, int Wd,
-                                      const float* __restrict__ poses, const float* __restrict__ Kf, CullGeom G,
-                                      int nbu, int nbv, int4* __restrict__ range) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= F) return;
-    int u0, u1, v0, v1;
-    double zlo, zhi;
-    bool inside;
-    CullCam cc;
-    cull_cam(poses, Kf, f, cc);
-    const int st = box_footprint(cc, G, 0, W - 1, 0, H - 1, z0, z1 - 1, Hd, Wd, u0, u1, v0, v1, zlo, zhi, inside);
-    range[f] = st == 2   ? make_int4(u0 / kCullBlock, u1 / kCullBlock, v0 / kCullBlock, v1 / kCullBlock)
-               : st == 1 ? make_int4(1, 0, 1, 0)
-                         : make_int4(0, nbu - 1, 0, nbv - 1);
-}
+// The depth blocks the slab [z0, z1) can touch in a frame (tsdf_setup_kernel,
+// int4 {bu0, bu1, bv0, bv1}): an empty range when the whole slab is off-image,
+// every block when the footprint cannot be bounded.  The block-max pass fills only
+// these blocks and the tile test reads only inside them.
 
 // VEC: Wd % 4 == 0, one float4 (4 pixels) per lane, 4 lanes per block column,
 // all 16 rows' loads in flight.  Otherwise one pixel per lane, 16 lanes per block.
@@ -863,7 +838,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                                                          const unsigned char* __restrict__ bdec,
                                                          unsigned short* __restrict__ cull,
                                                          unsigned short* __restrict__ freem,
-                                                         unsigned* __restrict__ plist, unsigned* __restrict__ pcount) {
+                                                         unsigned* __restrict__ plist, unsigned* __restrict__ pcount,
+                                                         unsigned* __restrict__ tcost) {
     __shared__ unsigned char bits[kCullFrames][64];
     const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
     const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
@@ -923,6 +899,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             cw |= (b & 1u) << q;
             fw |= (b >> 1) << q;
         }
+        if (tcost) {   // the fusion's workgroup order: 4 x projected + free-space frames per wave sub-tile
+            const int nlive = min(kCullFrames, F - hf * kCullFrames);
+            const unsigned live = nlive >= kCullFrames ? 0xFFFFu : (nlive > 0 ? (1u << nlive) - 1u : 0u);
+            const unsigned c = 4u * __popc(live & ~cw & ~fw) + __popc(live & fw & ~cw);
+            if (c) atomicAdd(tcost + tile, per_tile == kCullSub ? c : 4u * c);
+        }
         const int q0 = per_tile == kCullSub ? w : 0, q1 = per_tile == kCullSub ? w + 1 : kCullSub;
         for (int q = q0; q < q1; ++q) {
             const int64_t h = ((tile * kCullSub + q) * nw) * 2 + hf;   // half hf of word hf / 2
@@ -976,10 +958,8 @@ __global__ void tsdf_probe_mask_kernel(unsigned* __restrict__ cull, const unsign
 // Validated camera records, 16 floats per frame (non-finite or >= 2^60 anywhere:
 // all zero, so Zc = 0 and the frame is skipped):
 //   P0 P4 | P2 P6 | P3 P7 | P8 P10 P11 | P1 P5 P9 | fx fy | cx+.5 cy+.5
-__global__ void tsdf_cam_kernel(const float* __restrict__ poses, const float* __restrict__ Kf, int F,
-                                float* __restrict__ rec) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= F) return;
+__device__ __forceinline__ void tsdf_cam_record(const float* __restrict__ poses, const float* __restrict__ Kf, int f,
+                                                float* __restrict__ rec) {
     float p[12], k[4];
     bool good = true;
 #pragma unroll
@@ -990,6 +970,44 @@ __global__ void tsdf_cam_kernel(const float* __restrict__ poses, const float* __
                          k[0], k[1], k[2] + 0.5f, k[3] + 0.5f};
 #pragma unroll
     for (int q = 0; q < 16; ++q) rec[f * 16 + q] = good ? r[q] : 0.f;
+}
+
+// Per-call setup in one launch: per frame the fusion's f32 record, the culling
+// passes' CullCam (ccam non-null) and the slab's block range (range_mode 1: every
+// block, an external table; 2: the slab's footprint); the workgroups past the
+// frames zero the per-tile cost counters (nzero words) and the refinement list count.
+__global__ __launch_bounds__(64) void tsdf_setup_kernel(const float* __restrict__ poses, const float* __restrict__ Kf,
+                                                        int F, float* __restrict__ rec, CullCam* __restrict__ ccam,
+                                                        int range_mode, int H, int W, int z0, int z1, int Hd, int Wd,
+                                                        CullGeom G, int nbu, int nbv, int4* __restrict__ range,
+                                                        unsigned* __restrict__ zero, int nzero,
+                                                        unsigned* __restrict__ pcount) {
+    const int fb = (F + 63) / 64;
+    if ((int)blockIdx.x >= fb) {
+        const int nb = gridDim.x - fb, b = blockIdx.x - fb;
+        if (b == 0 && threadIdx.x == 0 && pcount) *pcount = 0u;
+        for (int i = b * 64 + threadIdx.x; i < nzero; i += nb * 64) zero[i] = 0u;
+        return;
+    }
+    const int f = blockIdx.x * 64 + threadIdx.x;
+    if (f >= F) return;
+    tsdf_cam_record(poses, Kf, f, rec);
+    if (!ccam) return;
+    CullCam c;
+    cull_cam(poses, Kf, f, c);
+    c.pad[0] = c.pad[1] = c.pad[2] = 0.0;
+    ccam[f] = c;
+    if (range_mode == 1) {
+        range[f] = make_int4(0, nbu - 1, 0, nbv - 1);
+    } else if (range_mode == 2) {
+        int u0, u1, v0, v1;
+        double zlo, zhi;
+        bool inside;
+        const int st = box_footprint(c, G, 0, W - 1, 0, H - 1, z0, z1 - 1, Hd, Wd, u0, u1, v0, v1, zlo, zhi, inside);
+        range[f] = st == 2   ? make_int4(u0 / kCullBlock, u1 / kCullBlock, v0 / kCullBlock, v1 / kCullBlock)
+                   : st == 1 ? make_int4(1, 0, 1, 0)
+                             : make_int4(0, nbu - 1, 0, nbv - 1);
+    }
 }
 
 // Workgroup slot -> tile of the super-brick order: the 1-D grid is dealt
@@ -1020,55 +1038,51 @@ __device__ __forceinline__ void tsdf_slot_tile(int slot, int nslots, int W, int 
 // stays on the XCD its super-brick was dealt to): with few workgroups per CU
 // (a z-slab of an N-way split: ~2 rounds) the surface tiles, up to ~10x the
 // work of a free-space tile, otherwise land in the last round.
-//   tsdf_cost_kernel: per slot a cost bucket 0..63 from its tile's masks
-//     (4 x projected frames + free-space frames, over the 4 wave sub-tiles);
+//   tsdf_cull_kernel adds each tile's cost (4 x projected frames + free-space
+//     frames, over the 4 wave sub-tiles, before refinement) into a counter;
 //   tsdf_order_kernel: one workgroup per XCD class, stable counting sort of the
-//     class's slots by bucket, heaviest first: order[x + 8 k] = k-th slot.
+//     class's slots by cost bucket 0..63, heaviest first: order[x + 8 k] = k-th slot.
 constexpr int kOrderBuckets = 64;
-__global__ __launch_bounds__(256) void tsdf_cost_kernel(int nslots, int W, int H, int D, int z0, int z1, SuperBrick SB,
-                                                        int F, int nw, const unsigned* __restrict__ cull,
-                                                        const unsigned* __restrict__ freem,
-                                                        unsigned char* __restrict__ bucket) {
+__device__ __forceinline__ unsigned slot_bucket(int s, int nslots, int W, int H, int z0, int z1,
+                                                const SuperBrick& SB, int F, const unsigned* __restrict__ tcost) {
     const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
     const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
-    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += gridDim.x * blockDim.x) {
-        int bx, by, bz;
-        tsdf_slot_tile(s, nslots, W, H, SB, bx, by, bz);
-        unsigned cost = 0;
-        if (bx < ntx && by < nty && bz < ntz) {
-            const size_t base = ((((size_t)bz * nty + by) * ntx + bx) * kCullSub) * (size_t)nw;
-            for (int q = 0; q < kCullSub; ++q)
-                for (int w = 0; w < nw; ++w) {
-                    const unsigned live = F - 32 * w >= 32 ? ~0u : ((1u << (F - 32 * w)) - 1u);
-                    const unsigned c = cull[base + (size_t)q * nw + w], f = freem ? freem[base + (size_t)q * nw + w] : 0u;
-                    cost += 4u * __popc(live & ~c & ~f) + __popc(live & f & ~c);
-                }
-        }
-        bucket[s] = (unsigned char)min((unsigned)(kOrderBuckets - 1), cost * kOrderBuckets / (16u * F + 1u));
-    }
+    int bx, by, bz;
+    tsdf_slot_tile(s, nslots, W, H, SB, bx, by, bz);
+    const unsigned cost = bx < ntx && by < nty && bz < ntz ? tcost[((size_t)bz * nty + by) * ntx + bx] : 0u;
+    return min((unsigned)(kOrderBuckets - 1), cost * kOrderBuckets / (16u * F + 1u));
 }
 
-__global__ __launch_bounds__(256) void tsdf_order_kernel(int nslots, const unsigned char* __restrict__ bucket,
+// Dynamic LDS: one bucket byte per slot of the class (m <= 65535, host-checked).
+__global__ __launch_bounds__(256) void tsdf_order_kernel(int nslots, int W, int H, int z0, int z1, SuperBrick SB,
+                                                         int F, const unsigned* __restrict__ tcost,
                                                          unsigned* __restrict__ order) {
     __shared__ unsigned short hist[kOrderBuckets][256];
-    __shared__ unsigned part[256];
-    const int x = blockIdx.x, t = threadIdx.x;
+    __shared__ unsigned wsum[4];
+    extern __shared__ unsigned char bk[];
+    const int x = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int m = nslots > x ? (nslots - x + kNumXcd - 1) / kNumXcd : 0;   // slots x, x+8, ... of this class
     const int per = (m + 255) / 256, j0 = min(m, t * per), j1 = min(m, j0 + per);
     for (int b = 0; b < kOrderBuckets; ++b) hist[b][t] = 0;
-    for (int j = j0; j < j1; ++j) ++hist[bucket[x + kNumXcd * j]][t];
+    for (int j = t; j < m; j += 256)   // coalesced over the class: every cost load in flight
+        bk[j] = (unsigned char)slot_bucket(x + kNumXcd * j, nslots, W, H, z0, z1, SB, F, tcost);
+    __syncthreads();
+    for (int j = j0; j < j1; ++j) ++hist[bk[j]][t];
     __syncthreads();
     // exclusive scan over (bucket descending, thread): thread u owns entries [64u, 64u + 64)
     unsigned run = 0;
     for (int e = 64 * t; e < 64 * t + 64; ++e) run += hist[kOrderBuckets - 1 - e / 256][e % 256];
-    part[t] = run;
-    __syncthreads();
-    if (t == 0) {
-        unsigned acc = 0;
-        for (int u = 0; u < 256; ++u) { const unsigned v = part[u]; part[u] = acc; acc += v; }
+    unsigned incl = run;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned up = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += up;
     }
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    run = part[t];
+    unsigned base = 0;
+    for (int w = 0; w < wv; ++w) base += wsum[w];
+    run = base + incl - run;
     for (int e = 64 * t; e < 64 * t + 64; ++e) {
         unsigned short& h = hist[kOrderBuckets - 1 - e / 256][e % 256];
         const unsigned v = h;
@@ -1077,9 +1091,8 @@ __global__ __launch_bounds__(256) void tsdf_order_kernel(int nslots, const unsig
     }
     __syncthreads();
     for (int j = j0; j < j1; ++j) {
-        const int s = x + kNumXcd * j;
-        const unsigned pos = hist[bucket[s]][t]++;
-        order[x + kNumXcd * pos] = (unsigned)s;
+        const unsigned pos = hist[bk[j]][t]++;
+        order[x + kNumXcd * pos] = (unsigned)(x + kNumXcd * j);
     }
 }
 
@@ -1093,7 +1106,12 @@ __device__ __forceinline__ bool w_runs(float w) { return w >= 0.f && w <= 0x1p24
 // wave holds T = 1 and an integer weight, as W += k (each of the k updates would
 // compute (1 W + 1)/(W + 1) = 1 exactly and W + 1 exactly) — and every other
 // frame is projected and gathered.
-template <bool SWZ>
+// PIPE (latency mode only, no block table): the gather of the next projected frame
+// is issued before the current one's update and the free-space run between them,
+// so a thin slab's longest waves overlap one depth load with the previous frame's
+// arithmetic instead of waiting out each load in turn.  The order of the updates
+// per voxel is unchanged.
+template <bool SWZ, bool PIPE = false>
 __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float* __restrict__ Wt, int D, int H,
                                                    int W, int z0, int z1, const float* __restrict__ depth, int F,
                                                    int Hd, int Wd, const float* __restrict__ rec, Bounds B,
@@ -1146,6 +1164,110 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
         wv.y = g1 ? d.y : wv.y;
     };
 
+    if constexpr (PIPE) {
+        // frame cursor over the masks: events are free-space runs (k frames) and
+        // projected frames, in frame order
+        int cw = -1;
+        unsigned ctodo = 0u, cfre = 0u;
+        auto next = [&](int& val) -> int {   // 0 end, 1 free run of val frames, 2 projected frame val
+            while (ctodo == 0u) {
+                if (++cw >= nw) return 0;
+                const int w0 = cw << 5;
+                unsigned t = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u), fr = 0u;
+                if (cull) {
+                    t &= ~cull[slot + cw];
+                    if (freem) fr = freem[slot + cw] & t;
+                }
+                ctodo = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+                cfre = (unsigned)__builtin_amdgcn_readfirstlane((int)fr);
+            }
+            if (cfre & ctodo & (0u - ctodo)) {
+                const unsigned full = ctodo & ~cfre;
+                const unsigned run = ctodo & (full ? (full & (0u - full)) - 1u : ~0u);
+                ctodo &= ~run;
+                val = __builtin_popcount(run);
+                return 1;
+            }
+            val = (cw << 5) + __builtin_ctz(ctodo);
+            ctodo &= ctodo - 1u;
+            return 2;
+        };
+        struct Proj { f2 Zc, dep; bool ok0, ok1; };
+        auto project = [&](int f) -> Proj {   // projection + the (issued) depth gather
+            const float* r = rec + f * 16;
+            const f2 Q = (f2{r[0], r[1]} * f2s(vx) + f2{r[2], r[3]} * f2s(vz)) + f2{r[4], r[5]};
+            const float Qz = (r[6] * vx + r[7] * vz) + r[8];
+            const f2 Xc = f2s(r[9]) * vy + f2s(Q.x);
+            const f2 Yc = f2s(r[10]) * vy + f2s(Q.y);
+            Proj p;
+            p.Zc = f2s(r[11]) * vy + f2s(Qz);
+            const f2 iz = recip_rn(p.Zc);
+            const f2 uu = (f2s(r[12]) * Xc) * iz + f2s(r[14]);
+            const f2 vv = (f2s(r[13]) * Yc) * iz + f2s(r[15]);
+            const int iu0 = cvt_flr(uu.x), iv0 = cvt_flr(vv.x);
+            const int iu1 = cvt_flr(uu.y), iv1 = cvt_flr(vv.y);
+            p.ok0 = z_ok(p.Zc.x) && (unsigned)iu0 < (unsigned)Wd && (unsigned)iv0 < (unsigned)Hd;
+            p.ok1 = two && z_ok(p.Zc.y) && (unsigned)iu1 < (unsigned)Wd && (unsigned)iv1 < (unsigned)Hd;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(depth + (size_t)f * frame), (short)0, nbytes, 0x00020000);
+            p.dep = f2{0.f, 0.f};
+            if (p.ok0)
+                p.dep.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                        rs, (int)(__umul24(iv0, Wd4) + ((unsigned)iu0 << 2)), 0, 0));
+            if (p.ok1)
+                p.dep.y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                        rs, (int)(__umul24(iv1, Wd4) + ((unsigned)iu1 << 2)), 0, 0));
+            return p;
+        };
+        auto finish = [&](const Proj& p) {
+            const f2 sdf = p.dep - p.Zc;
+            const bool g0 = p.ok0 && p.dep.x > 0.f && !(sdf.x < -trunc);
+            const bool g1 = p.ok1 && p.dep.y > 0.f && !(sdf.y < -trunc);
+            const f2 sc = sdf * f2s(inv_trunc);
+            const f2 ts = {fminf(1.0f, sc.x), fminf(1.0f, sc.y)};
+            const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && w_runs(wv.x));
+            const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && w_runs(wv.y));
+            if (easy && __builtin_amdgcn_ballot_w64(!(easy0 && easy1)) == 0) {
+                wv.x = g0 ? wv.x + 1.f : wv.x;
+                wv.y = g1 ? wv.y + 1.f : wv.y;
+            } else {
+                update(ts, g0, g1);
+            }
+        };
+        auto free_run = [&](int k) {
+            const bool ones = tv.x == 1.f && tv.y == 1.f && w_runs(wv.x) && w_runs(wv.y);
+            if (free_ts == 1.f && __builtin_amdgcn_ballot_w64(!ones) == 0) {
+                wv = wv + f2s((float)k);
+            } else {
+                for (int i = 0; i < k; ++i) update(f2s(free_ts), true, two);
+            }
+        };
+        int val = 0, kind = next(val);
+        Proj pend;
+        bool have = false;
+        int run = 0;   // free frames between the pending projected frame and the next event
+        while (kind != 0) {
+            if (kind == 1) {
+                if (have) run += val;
+                else free_run(val);
+                kind = next(val);
+                continue;
+            }
+            const Proj p = project(val);   // its gather is in flight from here
+            if (have) {
+                finish(pend);
+                if (run) free_run(run);
+            }
+            pend = p;
+            have = true;
+            run = 0;
+            kind = next(val);
+        }
+        if (have) {
+            finish(pend);
+            if (run) free_run(run);
+        }
+    } else
     for (int w0 = 0; w0 < F; w0 += 32) {
         const int wd = w0 >> 5;
         unsigned todo = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u), fre = 0u;
@@ -1785,7 +1907,9 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         }
         if (cmask && want_free && scratch_alloc((void**)&cfree, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess)
             cfree = nullptr;   // free-space path off, culling unchanged
-        if (cmask && env_int("SFMHIP_TSDF_BRICK", 1) != 0) {
+        // brick pre-pass (SFMHIP_TSDF_BRICK; default off in latency mode, where a thin slab's
+        // cull pass is short and the two extra launches cost more than they save)
+        if (cmask && env_int("SFMHIP_TSDF_BRICK", latency_mode ? 0 : 1) != 0) {
             if (scratch_alloc((void**)&ctab, (size_t)cf * ncbu * ncbv * sizeof(float2) + (size_t)cull_bricks * cf, st) ==
                 hipSuccess)
                 bdec = reinterpret_cast<unsigned char*>(ctab + (size_t)cf * ncbu * ncbv);
@@ -1801,13 +1925,17 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const bool vox_test = cfree && env_int("SFMHIP_TSDF_VOXTEST", latency_mode ? 0 : 1) != 0;
     // division-free update of projected frames whose updates are all tsdf = 1 on T = 1 (SFMHIP_TSDF_EASY=0 off)
     const int easy = env_int("SFMHIP_TSDF_EASY", 1) != 0;
+    // latency mode without the block table: gathers one projected frame ahead (SFMHIP_TSDF_PIPE=0 off)
+    const bool pipe = !vox_test && latency_mode && env_int("SFMHIP_TSDF_PIPE", 1) != 0;
     // longest-first workgroup order (SFMHIP_TSDF_ORDER=0 off): needs the masks and the 1-D slot grid;
-    // bucket sort positions are 16-bit, so at most 65535 slots per XCD class
+    // at most 30000 slots per XCD class (16-bit sort positions; a bucket byte per slot in LDS
+    // next to the 32 KB histogram, within the default 64 KB)
     unsigned* ord = nullptr;
-    unsigned char* obucket = nullptr;
-    if (cmask && swz && !stats && env_int("SFMHIP_TSDF_ORDER", 1) != 0 && (int64_t)grid.x <= 65535LL * kNumXcd) {
-        if (scratch_alloc((void**)&ord, (size_t)grid.x * (sizeof(unsigned) + 1), st) == hipSuccess)
-            obucket = reinterpret_cast<unsigned char*>(ord + grid.x);
+    unsigned* tcost = nullptr;   // per-tile cost counters (after the order)
+    const int64_t ntiles = (int64_t)nbx * nby * nbz;
+    if (cmask && swz && !stats && env_int("SFMHIP_TSDF_ORDER", 1) != 0 && (int64_t)grid.x <= 30000LL * kNumXcd) {
+        if (scratch_alloc((void**)&ord, (size_t)(grid.x + ntiles) * sizeof(unsigned), st) == hipSuccess)
+            tcost = ord + grid.x;
         else
             ord = nullptr;
         (void)hipGetLastError();
@@ -1820,15 +1948,14 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         const float* dp = depth + (size_t)f0 * Hd * Wd;
         const float* pp = poses + (size_t)f0 * 12;
         const float* kp = Kf + (size_t)f0 * 4;
-        hipLaunchKernelGGL(tsdf_cam_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, pp, kp, nf, rec);
-        CullCam* ccam = reinterpret_cast<CullCam*>(rec + (size_t)cf * 16);
-        if (cmask) hipLaunchKernelGGL(cull_cam_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, pp, kp, nf, ccam);
+        CullCam* ccam = cmask ? reinterpret_cast<CullCam*>(rec + (size_t)cf * 16) : nullptr;
+        unsigned* pcount = plist ? plist + ntile_frames : nullptr;
+        const int nzero = tcost ? (int)ntiles : 0;
+        hipLaunchKernelGGL(tsdf_setup_kernel, dim3(ceil_div(nf, 64) + (nzero || pcount ? std::min(64, ceil_div(nzero, 1024) + 1) : 0)),
+                           dim3(64), 0, st, pp, kp, nf, rec, ccam, !cmask ? 0 : ext_table ? 1 : 2, H, W, z0, z1, Hd,
+                           Wd, cg, nbu, nbv, crange, tcost, nzero, pcount);
         const float2* tab = ext_table ? ext_table + (size_t)f0 * nbv * nbu : cbmm;
-        if (cmask && ext_table) {
-            hipLaunchKernelGGL(full_range_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, nf, nbu, nbv, crange);
-        } else if (cmask) {
-            hipLaunchKernelGGL(tsdf_footprint_kernel, dim3(ceil_div(nf, 64)), dim3(64), 0, st, H, W, z0, z1, nf, Hd,
-                               Wd, pp, kp, cg, nbu, nbv, crange);
+        if (cmask && !ext_table) {
             if (Wd % 4 == 0)
                 hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st,
                                    dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
@@ -1837,8 +1964,6 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                                    dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
         }
         if (cmask) {
-            unsigned* pcount = plist ? plist + ntile_frames : nullptr;
-            if (plist) (void)hipMemsetAsync(pcount, 0, sizeof(unsigned), st);
             if (bdec) {
                 const int64_t nc = (int64_t)nf * ncbu * ncbv, nd = (cull_bricks + 63) / 64 * 64 * nf;
                 hipLaunchKernelGGL(coarse_table_kernel, dim3((unsigned)ceil_div(nc, (int64_t)256)), dim3(256), 0, st,
@@ -1849,7 +1974,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             }
             hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nwf * 2)), dim3(1024), 0, st, H,
                                W, z0, z1, nf, Hd, Wd, ccam, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
-                               nwf, bdec, (unsigned short*)cmask, (unsigned short*)cfree, plist, pcount);
+                               nwf, bdec, (unsigned short*)cmask, (unsigned short*)cfree, plist, pcount, tcost);
             if (plist)
                 hipLaunchKernelGGL(tsdf_refine_kernel, dim3(2048), dim3(256), 0, st, H, W, z0, z1, nf, Hd, Wd, pp,
                                    kp, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, nwf, cmask, cfree, plist,
@@ -1896,11 +2021,13 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             fmask = nullptr;
         }
         if (ord) {   // longest-first workgroup order within each XCD class (bit-identical results)
-            hipLaunchKernelGGL(tsdf_cost_kernel, dim3((unsigned)std::min<int64_t>(ceil_div((int64_t)grid.x, 256), 1024)),
-                               dim3(256), 0, st, (int)grid.x, W, H, D, z0, z1, sb, nf, nwf, cmask, cfree, obucket);
-            hipLaunchKernelGGL(tsdf_order_kernel, dim3(kNumXcd), dim3(256), 0, st, (int)grid.x, obucket, ord);
+            hipLaunchKernelGGL(tsdf_order_kernel, dim3(kNumXcd), dim3(256), (size_t)ceil_div((int)grid.x, kNumXcd), st,
+                               (int)grid.x, W, H, z0, z1, sb, nf, tcost, ord);
         }
-        if (swz)
+        if (swz && pipe)
+            hipLaunchKernelGGL((tsdf_kernel<true, true>), grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
+                               Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, nullptr, nbu, nbv, ord, easy);
+        else if (swz)
             hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
                                bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, ord, easy);
         else

@@ -180,9 +180,10 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
                 dict(CULL="2", CULLSUB="4"), dict(CULL="2", CHUNK="3"), dict(CULL="2", VOXTEST="0"),
                 dict(CULL="2", CHUNK="512"), dict(CULL="2", REFINE="0"), dict(CULL="2", LATENCY="1"),
                 dict(CULL="2", LATENCY="0"), dict(CULL="2", ORDER="0"), dict(CULL="2", BRICK="0"),
-                dict(CULL="2", BRICK="0", CULLSUB="4")]
+                dict(CULL="2", BRICK="0", CULLSUB="4"), dict(CULL="2", LATENCY="1", PIPE="0"),
+                dict(CULL="2", LATENCY="1", EASY="0"), dict(CULL="2", EASY="0")]
     for v in variants:
-        for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST", "REFINE", "LATENCY", "ORDER", "BRICK"):
+        for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST", "REFINE", "LATENCY", "ORDER", "BRICK", "PIPE", "EASY"):
             monkeypatch.delenv("SFMHIP_TSDF_" + k, raising=False)
         for k, x in v.items():
             monkeypatch.setenv("SFMHIP_TSDF_" + k, x)
@@ -190,7 +191,7 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
         W = torch.zeros_like(T)
         sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95, z0=5, z1=90)
         out.append((T.cpu(), W.cpu()))
-    for i in (1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13):
+    for i in (1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16):
         assert torch.equal(out[0][0], out[i][0]) and torch.equal(out[0][1], out[i][1]), variants[i]
     assert (out[0][1] > 0).float().mean() > 0.3
     assert torch.equal(out[0][1], out[3][1])            # probe: same update pattern ...
