@@ -720,16 +720,23 @@ __device__ __forceinline__ void cull_test(const CullCam& cc, const CullGeom& G, 
         if (nb <= CAP && bu0 >= rg.x && bu1 <= rg.y && bv0 >= rg.z && bv1 <= rg.w) {
             const float2* bp = bmm + ((size_t)f * nbv + bv0) * nbu + bu0;
             float m = -__builtin_inff(), mn = __builtin_inff();
-            for (int bv = bv0; bv <= bv1; ++bv, bp += nbu) {
-                int i = 0;
-                for (; i + 4 <= nu; i += 4) {   // 4 independent loads in flight
-                    const float2 e0 = bp[i], e1 = bp[i + 1], e2 = bp[i + 2], e3 = bp[i + 3];
-                    m = fmaxf(fmaxf(m, fmaxf(e0.y, e1.y)), fmaxf(e2.y, e3.y));
-                    mn = fminf(fminf(mn, fminf(e0.x, e1.x)), fminf(e2.x, e3.x));
-                }
-                for (; i < nu; ++i) {
-                    m = fmaxf(m, bp[i].y);
-                    mn = fminf(mn, bp[i].x);   // never NaN (poisoned to -inf)
+            // rows in pairs, 8 predicated loads per row: up to 16 loads in flight per round
+            // (min / max are exact in any order; mins are never NaN, poisoned to -inf)
+            for (int bv = bv0; bv <= bv1; bv += 2, bp += 2 * nbu) {
+                const bool two_rows = bv + 1 <= bv1;
+                for (int i = 0; i < nu; i += 8) {
+                    float2 e[16];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        e[j] = i + j < nu ? bp[i + j] : make_float2(__builtin_inff(), -__builtin_inff());
+                        e[8 + j] = two_rows && i + j < nu ? bp[nbu + i + j]
+                                                          : make_float2(__builtin_inff(), -__builtin_inff());
+                    }
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        m = fmaxf(m, e[j].y);
+                        mn = fminf(mn, e[j].x);
+                    }
                 }
             }
             // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for the

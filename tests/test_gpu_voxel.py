@@ -120,7 +120,15 @@ def _tsdf_case(R=48, F=12, Hd=96, Wd=128, focal=110.0):
     return R, depth.numpy(), poses.numpy(), K.numpy()
 
 
-def test_tsdf_vs_oracle_bitexact(sfm, gpu):
+# "auto": small grids run in latency mode; "0" forces the whole-grid path (refinement
+# pass, per-voxel block test)
+LAT_MODES = ["auto", "0"]
+
+
+@pytest.mark.parametrize("lat", LAT_MODES)
+def test_tsdf_vs_oracle_bitexact(sfm, gpu, monkeypatch, lat):
+    if lat != "auto":
+        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", lat)
     R, depth, poses, K = _tsdf_case()
     T = torch.zeros((R, R, R), dtype=torch.float32, device=gpu)
     W = torch.zeros_like(T)
@@ -134,14 +142,17 @@ def test_tsdf_vs_oracle_bitexact(sfm, gpu):
     assert (Wg > 0).mean() > 0.2
 
 
+@pytest.mark.parametrize("lat", LAT_MODES)
 @pytest.mark.parametrize("Wd", [96, 97])
-def test_tsdf_edge_cases_bitexact(sfm, gpu, monkeypatch, Wd):
+def test_tsdf_edge_cases_bitexact(sfm, gpu, monkeypatch, Wd, lat):
     """Odd / non-cubic grid (a lane's second voxel off the grid), 30 frames (two
     frame-chunk launches), prior (T, W) state including values outside the fast
     division's range, depth holes / negative depth, a camera plane cutting the
     grid (Zc <= 0), and frames with a NaN pose, an infinite intrinsic and a
     >= 2^60 translation (skipped as a whole): bit-exact with the oracle."""
     monkeypatch.setenv("SFMHIP_TSDF_CHUNK", "7")  # several launches; Wd = 97: unaligned depth rows
+    if lat != "auto":
+        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", lat)
     D, H, W_ = 20, 33, 45
     F, Hd = 30, 72
     depth, poses, K = syn.tsdf_scene(F, Hd, Wd, focal=80.0, seed=11)
@@ -181,7 +192,8 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
                 dict(CULL="2", CHUNK="512"), dict(CULL="2", REFINE="0"), dict(CULL="2", LATENCY="1"),
                 dict(CULL="2", LATENCY="0"), dict(CULL="2", ORDER="0"), dict(CULL="2", BRICK="0"),
                 dict(CULL="2", BRICK="0", CULLSUB="4"), dict(CULL="2", LATENCY="1", PIPE="0"),
-                dict(CULL="2", LATENCY="1", EASY="0"), dict(CULL="2", EASY="0")]
+                dict(CULL="2", LATENCY="1", EASY="0"), dict(CULL="2", EASY="0"),
+                dict(CULL="2", LATENCY="0", REFINE="0"), dict(CULL="2", LATENCY="0", VOXTEST="0")]
     for v in variants:
         for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST", "REFINE", "LATENCY", "ORDER", "BRICK", "PIPE", "EASY"):
             monkeypatch.delenv("SFMHIP_TSDF_" + k, raising=False)
@@ -191,19 +203,22 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
         W = torch.zeros_like(T)
         sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95, z0=5, z1=90)
         out.append((T.cpu(), W.cpu()))
-    for i in (1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16):
+    for i in (1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18):
         assert torch.equal(out[0][0], out[i][0]) and torch.equal(out[0][1], out[i][1]), variants[i]
     assert (out[0][1] > 0).float().mean() > 0.3
     assert torch.equal(out[0][1], out[3][1])            # probe: same update pattern ...
     assert (out[3][0] != out[0][0]).float().mean() > 0.05  # ... and many free-space updates
 
 
+@pytest.mark.parametrize("lat", LAT_MODES)
 @pytest.mark.parametrize("trunc", [0.1, 0.3, 3 * 2.0 / 31, 0.0625])
-def test_tsdf_free_space_near_trunc_bitexact(sfm, gpu, monkeypatch, trunc):
+def test_tsdf_free_space_near_trunc_bitexact(sfm, gpu, monkeypatch, trunc, lat):
     """Frontal planes placed so that whole tiles sit just in front of depth - mu
     (the free-space proof's boundary), several truncation distances, prior
     (T, W) state: bit-exact with the oracle, with culling + free space forced."""
     monkeypatch.setenv("SFMHIP_TSDF_CULL", "2")
+    if lat != "auto":
+        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", lat)
     R, F, Hd, Wd = 32, 6, 64, 80
     rng = np.random.default_rng(int(trunc * 1000))
     zs = (np.float32(-1) + np.arange(R, dtype=np.float32) * (np.float32(2) / np.float32(R - 1)))
