@@ -1320,8 +1320,13 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
             if (bmm) {
                 const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
                     (void*)(bmm + (size_t)f * nbv * nbu), (short)0, nbv * nbu * 8, 0x00020000);
-                const auto e0 = __builtin_amdgcn_raw_buffer_load_b64(rb, ((iv0 >> 4) * nbu + (iu0 >> 4)) * 8, 0, 0);
-                const auto e1 = __builtin_amdgcn_raw_buffer_load_b64(rb, ((iv1 >> 4) * nbu + (iu1 >> 4)) * 8, 0, 0);
+                // 24-bit multiplies (v_mad_u32_u24, full rate; v_mul_lo_u32 is quarter rate): the
+                // block indices are < 2^20 when the pixel is in range, and out-of-range lanes'
+                // offsets only have to stay bounds-checked
+                const auto e0 = __builtin_amdgcn_raw_buffer_load_b64(
+                    rb, (int)((__umul24((unsigned)(iv0 >> 4) & 0xFFFFFFu, (unsigned)nbu) + ((unsigned)iu0 >> 4)) << 3), 0, 0);
+                const auto e1 = __builtin_amdgcn_raw_buffer_load_b64(
+                    rb, (int)((__umul24((unsigned)(iv1 >> 4) & 0xFFFFFFu, (unsigned)nbu) + ((unsigned)iu1 >> 4)) << 3), 0, 0);
                 const f2 bmn = {__builtin_bit_cast(float, (unsigned)e0[0]), __builtin_bit_cast(float, (unsigned)e1[0])};
                 const f2 bmx = {__builtin_bit_cast(float, (unsigned)e0[1]), __builtin_bit_cast(float, (unsigned)e1[1])};
                 const f2 scm = (bmn - Zc) * f2s(inv_trunc);
