@@ -291,7 +291,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
                                                          const int32_t* __restrict__ pair_of_obs,
                                                          const double* __restrict__ x0, const double* __restrict__ x1,
                                                          int64_t n, double* __restrict__ X4,
-                                                         unsigned* __restrict__ slots, unsigned* __restrict__ counts) {
+                                                         unsigned* __restrict__ slots, unsigned* __restrict__ counts,
+                                                         double4* __restrict__ recx, int* __restrict__ recpr) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t wave = i >> 6;   // global wave index (n_waves = ceil(n / 64) slots of 64)
     if (i >= n) return;
@@ -319,8 +320,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void d
     // wave cycles waiting)
     const unsigned long long m = __ballot(st != 0);
     const int lane = threadIdx.x & 63;
-    if (st != 0)
-        slots[(wave << 6) + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)i;
+    if (st != 0) {   // the slot carries the observation (index, pair, both image points): the list pass
+                     // then needs one dependent load level less
+        const int64_t pos = (wave << 6) + __popcll(m & ((1ull << lane) - 1ull));
+        slots[pos] = (unsigned)i;
+        recx[pos] = make_double4(xa, ya, xb, yb);
+        recpr[pos] = pr;
+    }
     if (lane == __ffsll((long long)__ballot(true)) - 1) counts[wave] = (unsigned)__popcll(m);
 }
 
@@ -332,7 +338,9 @@ __global__ __launch_bounds__(64) void dlt_list_kernel(const double* __restrict__
                                                       const double* __restrict__ x0, const double* __restrict__ x1,
                                                       int64_t n, double* __restrict__ X4,
                                                       const unsigned* __restrict__ slots,
-                                                      const unsigned* __restrict__ counts, int64_t n_waves) {
+                                                      const unsigned* __restrict__ counts,
+                                                      const double4* __restrict__ recx, const int* __restrict__ recpr,
+                                                      int64_t n_waves) {
     __shared__ unsigned items[64 * 64];
     const int lane = threadIdx.x;
     const int64_t w = (int64_t)blockIdx.x * 64 + lane;
@@ -345,13 +353,15 @@ __global__ __launch_bounds__(64) void dlt_list_kernel(const double* __restrict__
     }
     const unsigned total = __shfl(pre, 63);
     if (total == 0) return;
-    for (unsigned t = 0; t < c; ++t) items[pre - c + t] = slots[(w << 6) + t];
+    for (unsigned t = 0; t < c; ++t) items[pre - c + t] = (unsigned)((w << 6) + t);   // slot positions
     __syncthreads();
     for (unsigned k = lane; k < total; k += 64) {
-        const int64_t i = items[k];
-        const int pr = pair_of_obs ? pair_of_obs[i] : 0;
+        const unsigned pos = items[k];
+        const int64_t i = slots[pos];
+        const int pr = recpr[pos];
+        const double4 xr = recx[pos];
         double X[4];
-        const double *Pa = P + (size_t)pr * 24, xa = x0[i], ya = x0[n + i], xb = x1[i], yb = x1[n + i];
+        const double *Pa = P + (size_t)pr * 24, xa = xr.x, ya = xr.y, xb = xr.z, yb = xr.w;
         if (!dlt_point_qr3(Pa, Pa + 12, xa, ya, xb, yb, X)) dlt_point(Pa, Pa + 12, xa, ya, xb, yb, X);
 #pragma unroll
         for (int r = 0; r < 4; ++r) X4[(int64_t)r * n + i] = X[r];
@@ -483,14 +493,19 @@ extern "C" int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_ob
     const int64_t n_waves = ceil_div(n, 64);
     const char* qr = std::getenv("SFMHIP_DLT_QR");
     if (!(qr && std::atoi(qr) != 0) && n < ((int64_t)1 << 31) &&
-        scratch_alloc((void**)&slots, (size_t)n_waves * 65 * sizeof(unsigned), st) == hipSuccess) {
+        scratch_alloc((void**)&slots, (size_t)ceil_div(n_waves * 65, (int64_t)8) * 32 + (size_t)n_waves * 64 * 36, st) ==
+            hipSuccess) {
+        // [n_waves * 64] indices, [n_waves] counts, then (32-B aligned) the listed observations'
+        // points (double4) and pairs (int), at the same slot positions
         unsigned* counts = slots + n_waves * 64;
+        double4* recx = reinterpret_cast<double4*>(slots + ceil_div(n_waves * 65, (int64_t)8) * 8);
+        int* recpr = reinterpret_cast<int*>(recx + n_waves * 64);
         hipLaunchKernelGGL(dlt_normal_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, P, pair_of_obs, x0, x1, n,
-                           X4, slots, counts);
+                           X4, slots, counts, recx, recpr);
         int rc = check_launch("dlt_normal_kernel");
         if (rc == SFMHIP_OK) {
             hipLaunchKernelGGL(dlt_list_kernel, dim3((unsigned)ceil_div(n_waves, 64)), dim3(64), 0, st, P, pair_of_obs,
-                               x0, x1, n, X4, slots, counts, n_waves);
+                               x0, x1, n, X4, slots, counts, recx, recpr, n_waves);
             rc = check_launch("dlt_list_kernel");
         }
         (void)hipFreeAsync(slots, st);
