@@ -70,7 +70,7 @@ SIGNATURES = {
     "sfmhip_triangulate_dlt": [_p, _p, _p, _p, _i64, _p, _p],
     "sfmhip_reproj_residual": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "sfmhip_reproj_fd_jacobian": [_p, _p, _p, _p, _p, _i32, _i64, _p, _p, _p, _p],
-    "sfmhip_ba_solve": [_p, _p, _p, _p, _p, _i32, _f64, _f64, _f64, _i32, _p, _p, _p, _p, _p],
+    "sfmhip_ba_solve": [_p, _p, _p, _p, _p, _i32, _i64, _f64, _f64, _f64, _i32, _p, _p, _p, _p, _p],
     "sfmhip_voxel_traversal_count": [_p, _i64, _f32, _i32, _p, _p],
     "sfmhip_voxel_traversal": [_p, _i64, _f32, _i32, _p, _p],
     "sfmhip_grid_sample": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i64, _p, _p],
@@ -93,7 +93,6 @@ SIGNATURES = {
     "sfmhip_grid_from_voxel_major": [_p, _i32, _i32, _i32, _i32, _p, _p],
     "sfmhip_ray_aabb": [_p, _p, _i64, _p, _p, _p, _p, _p, _p],
     "sfmhip_stratified_samples": [_p, _p, _p, _i64, _i32, _i32, _p, _p],
-    "sfmhip_debug_ransac_prof": [_p],
     "sfmhip_comm_unique_id": [_p],
     "sfmhip_comm_init_rank": [_i32, _p, _i32, _p],
     "sfmhip_comm_init_all": [_i32, _p, _p],

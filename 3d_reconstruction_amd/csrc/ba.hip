@@ -145,7 +145,8 @@ __device__ __forceinline__ void resid(const double* R, const double* c, const do
 
 __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__ cam_io, const double* __restrict__ Kall,
                                                             double* __restrict__ X, const double* __restrict__ pts2d,
-                                                            const int64_t* __restrict__ off, double ftol, double xtol,
+                                                            const int64_t* __restrict__ off, int64_t n_obs,
+                                                            double ftol, double xtol,
                                                             double gtol, int max_nfev_arg, double* __restrict__ scratch,
                                                             double* __restrict__ cost_out, int32_t* __restrict__ nfev_out,
                                                             int32_t* __restrict__ njev_out,
@@ -153,6 +154,10 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
     __shared__ BaState S;
     const int p = blockIdx.x, tid = threadIdx.x;
     const int64_t o0 = off[p], o1 = off[p + 1];
+    if (!(0 <= o0 && o0 <= o1 && o1 <= n_obs && o1 - o0 <= INT_MAX)) {   // malformed offsets: touch nothing
+        if (tid == 0) { cost_out[p] = 0.0; nfev_out[p] = 0; njev_out[p] = 0; status_out[p] = -1; }
+        return;
+    }
     const int n = (int)(o1 - o0);
     const double* k = Kall + (size_t)p * 9;
     double* Xp = X + 3 * o0;
@@ -234,6 +239,7 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
     }
 
     while (true) {
+        __syncthreads();   // every wave has read the previous iteration's S.status / S.done
         if (tid == 0) {
             if (S.gmax < gtol) S.status = 1;
             S.done = S.status >= 0 || S.nfev == max_nfev;
@@ -544,28 +550,22 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
 using namespace sfmhip;
 
 extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const double* pts2d, const int64_t* pair_off,
-                               int n_pairs, double ftol, double xtol, double gtol, int max_nfev, double* cost,
-                               int32_t* nfev, int32_t* njev, int32_t* status, void* stream) {
+                               int n_pairs, int64_t n_obs, double ftol, double xtol, double gtol, int max_nfev,
+                               double* cost, int32_t* nfev, int32_t* njev, int32_t* status, void* stream) {
     SFMHIP_REQUIRE(cam && K && X && pts2d && pair_off && cost && nfev && njev && status,
                    "sfmhip_ba_solve: null pointer");
     SFMHIP_REQUIRE(n_pairs >= 0, "sfmhip_ba_solve: negative n_pairs");
+    SFMHIP_REQUIRE(n_obs >= 0, "sfmhip_ba_solve: negative n_obs");
     if (n_pairs == 0) return SFMHIP_OK;
     hipStream_t st = as_stream(stream);
-    int64_t n_obs = 0;
-    if (hipMemcpyAsync(&n_obs, pair_off + n_pairs, sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
-        set_error("sfmhip_ba_solve: reading the observation count failed");
-        return SFMHIP_E_HIP;
-    }
-    SFMHIP_REQUIRE(n_obs >= 0, "sfmhip_ba_solve: bad pair offsets");
     double* scratch = nullptr;
     if (scratch_alloc((void**)&scratch, (size_t)std::max<int64_t>(n_obs, 1) * kRec * sizeof(double), st) != hipSuccess) {
         (void)hipGetLastError();
         set_error("sfmhip_ba_solve: scratch allocation failed");
         return SFMHIP_E_HIP;
     }
-    hipLaunchKernelGGL(ba_trf_kernel, dim3(n_pairs), dim3(kBaThreads), 0, st, cam, K, X, pts2d, pair_off, ftol, xtol,
-                       gtol, max_nfev, scratch, cost, nfev, njev, status);
+    hipLaunchKernelGGL(ba_trf_kernel, dim3(n_pairs), dim3(kBaThreads), 0, st, cam, K, X, pts2d, pair_off, n_obs, ftol,
+                       xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
     const int rc = check_launch("ba_trf_kernel");
     (void)hipFreeAsync(scratch, st);
     return rc;

@@ -112,8 +112,8 @@ __device__ __forceinline__ void wave_sync_lds() { __builtin_amdgcn_fence(__ATOMI
 
 // Phase timers for tools/prof_ransac.py: build with -DSFMHIP_RANSAC_PROF
 // (make EXTRA=-DSFMHIP_RANSAC_PROF); compiled out otherwise.
-__device__ unsigned long long g_rprof[16];
 #ifdef SFMHIP_RANSAC_PROF
+__device__ unsigned long long g_rprof[16];
 #define SPROF(i) do { if (threadIdx.x == 0) { const unsigned long long t1 = wall_clock64(); atomicAdd(&g_rprof[i], t1 - st); st = t1; } } while (0)
 #define SPROF_INIT unsigned long long st = wall_clock64()
 #define RPROF(i, t0) do { if (tid == 0) { const unsigned long long t1 = wall_clock64(); atomicAdd(&g_rprof[i], t1 - t0); t0 = t1; } } while (0)
@@ -905,12 +905,16 @@ __global__ __launch_bounds__(kPThreads) void recover_pose_kernel(
 
 using namespace sfmhip;
 
+#ifdef SFMHIP_RANSAC_PROF
+// Phase timers of essential_ransac_kernel for tools/prof_ransac.py: exported only
+// by a profiling build (make EXTRA=-DSFMHIP_RANSAC_PROF), not part of the ABI.
 extern "C" int sfmhip_debug_ransac_prof(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rprof), sizeof(unsigned long long) * 16) != hipSuccess) return -2;
     unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), z, sizeof(z)) != hipSuccess) return -2;
     return 0;
 }
+#endif
 
 extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, const int64_t* offsets,
                                      int n_pairs, const double* cam, double prob, double threshold,

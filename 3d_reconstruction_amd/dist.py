@@ -19,6 +19,7 @@
 from __future__ import annotations
 
 import ctypes
+import sys
 
 import numpy as np
 import torch
@@ -92,11 +93,25 @@ class RcclComm:
                    DT_OF[send.dtype], st)
 
     def close(self) -> None:
+        """Destroy the communicator once every collective it enqueued has
+        finished: ``allgather`` returns without a host sync (the transfer runs on
+        a side stream), so the device is synchronised first."""
         if self.handle is not None and self.handle.value:
+            torch.cuda.synchronize()
             self._call("sfmhip_comm_destroy", self.handle)
         self.handle = None
 
+    def __enter__(self) -> "RcclComm":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
     def __del__(self):
+        # at interpreter shutdown the HIP runtime may already be gone: leave the
+        # communicator to process exit rather than call into a torn-down runtime
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

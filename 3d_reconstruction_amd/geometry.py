@@ -203,7 +203,7 @@ def residual_jacobian_batched(cam: torch.Tensor, K: torch.Tensor, X: torch.Tenso
 
 def ba_solve_batched(cam: torch.Tensor, K: torch.Tensor, X: torch.Tensor, pts2d: torch.Tensor,
                      pair_off: torch.Tensor, ftol: float = 1e-8, xtol: float = 1e-8, gtol: float = 1e-8,
-                     max_nfev: int | None = None) -> dict:
+                     max_nfev: int | None = None, validate: bool = True) -> dict:
     """The BA solve of sfm.py:37-38 for every pair at once, on the GPU (ba.hip):
     scipy ``least_squares(calculate_reprojection_error, [rvec, t, X], jac_sparsity=
     ba_sparse(...), x_scale='jac', ftol=ftol)`` restated (oracle/ba.py).
@@ -211,7 +211,12 @@ def ba_solve_batched(cam: torch.Tensor, K: torch.Tensor, X: torch.Tensor, pts2d:
     cam (P,6) and X (n,3) f64 device tensors are updated in place; K (P,3,3),
     pts2d (n,2) f64; pair_off (P+1) int64 (pair p owns observations
     [pair_off[p], pair_off[p+1])).  Returns device tensors cost (P,) f64 and
-    nfev, njev, status (P,) int32 (scipy's meanings)."""
+    nfev, njev, status (P,) int32 (scipy's meanings; -1 = malformed offsets).
+
+    ``validate`` checks pair_off on the device (off[0] = 0, non-decreasing,
+    off[P] = n) and raises ValueError — one reduction and a host sync; the
+    kernel itself never reads or writes outside [0, n) whatever the offsets
+    (a pair with bad offsets is skipped with status -1)."""
     require_gpu()
     P = int(cam.shape[0])
     for name, t, dt in (("cam", cam, torch.float64), ("K", K, torch.float64), ("X", X, torch.float64),
@@ -223,11 +228,15 @@ def ba_solve_batched(cam: torch.Tensor, K: torch.Tensor, X: torch.Tensor, pts2d:
             tuple(pts2d.shape) != (n, 2) or tuple(pair_off.shape) != (P + 1,):
         raise ValueError("shapes must be cam (P,6), K (P,3,3), X (n,3), pts2d (n,2), pair_off (P+1,)")
     dvc = cam.device
+    if validate and P > 0:
+        bad = (pair_off[0] != 0) | (pair_off[-1] != n) | (pair_off[1:] < pair_off[:-1]).any()
+        if bool(bad.item()):
+            raise ValueError("pair_off must start at 0, be non-decreasing and end at X.shape[0]")
     cost = torch.empty(P, dtype=torch.float64, device=dvc)
     nfev = torch.empty(P, dtype=torch.int32, device=dvc)
     njev = torch.empty(P, dtype=torch.int32, device=dvc)
     status = torch.empty(P, dtype=torch.int32, device=dvc)
-    call("sfmhip_ba_solve", ptr(cam), ptr(K), ptr(X), ptr(pts2d), ptr(pair_off), P, float(ftol), float(xtol),
+    call("sfmhip_ba_solve", ptr(cam), ptr(K), ptr(X), ptr(pts2d), ptr(pair_off), P, n, float(ftol), float(xtol),
          float(gtol), int(max_nfev or 0), ptr(cost), ptr(nfev), ptr(njev), ptr(status), stream_ptr())
     return {"cost": cost, "nfev": nfev, "njev": njev, "status": status}
 

@@ -218,14 +218,37 @@ def bf_match(desc0, desc1, ratio=0.75, mutual: bool = False, mode: int = MODE_FL
     return m0[0, :d0.shape[0]].cpu().numpy().astype(np.int64)
 
 
+def _exact_scores(x0: torch.Tensor, x1: torch.Tensor, m0: torch.Tensor) -> torch.Tensor:
+    """1 - sqrt(d1/d2) for the matched rows of x0 from f64 difference-form squared
+    distances (the exact mode's metric): d1 to the match, d2 the best other
+    row of x1; 0 for unmatched rows.  Only the matched rows are scored."""
+    sc = torch.zeros(x0.shape[0], dtype=torch.float32, device=x0.device)
+    rows = torch.nonzero(m0 >= 0).flatten()
+    if rows.numel() == 0:
+        return sc
+    a, b = x0[rows].double(), x1.double()
+    D = torch.cdist(a, b, compute_mode="donot_use_mm_for_euclid_dist").square()
+    j = m0[rows]
+    d1 = D[torch.arange(len(rows), device=D.device), j]
+    D[torch.arange(len(rows), device=D.device), j] = float("inf")
+    d2 = D.min(dim=1).values if b.shape[0] > 1 else torch.full_like(d1, float("inf"))
+    sc[rows] = (1.0 - torch.sqrt(d1 / d2.clamp_min(1e-300))).float()
+    return sc
+
+
 class Matcher(torch.nn.Module):
     """Brute-force L2 + ratio-test matcher with LightGlue's call/return contract.
 
     ``Matcher(ratio=0.75, mutual=True, mode=MODE_FLOAT)(data)`` where ``data`` is
     ``{'image0': {'descriptors': (1,M,d), ...}, 'image1': {...}}`` as built at
-    ``matching.py:107-120``.  ``matching_scores0`` = 1 - sqrt(d1/d2) (Lowe
-    margin of the int8 pass) for matched keypoints, 0 otherwise.  ``exact``
-    (default True): the exact float distance on the descriptors as given.
+    ``matching.py:107-120``.  ``matching_scores0`` = 1 - sqrt(d1/d2) (the Lowe
+    margin) for matched keypoints, 0 otherwise: from the f64 difference-form
+    distances of the descriptors as given in the exact mode, from the int8
+    distances otherwise (matching.py reads only ``matches``).  ``exact``
+    (default True): the exact float distance on the descriptors as given; it
+    needs finite descriptors and raises ValueError on NaN / inf, where
+    LightGlue would pass them through (``exact=False`` matches the int8
+    quantisation, which maps non-finite values like any out-of-range value).
     """
 
     default_conf = {"ratio": 0.75, "mutual": True, "mode": MODE_FLOAT, "exact": True}
@@ -258,9 +281,12 @@ class Matcher(torch.nn.Module):
             # matches1 from the forward result (first i claiming each j).
             i_idx = torch.nonzero(m0[0] >= 0).flatten()
             m1[0].scatter_reduce_(0, m0[0, i_idx], i_idx, reduce="amin", include_self=False)
-        d1f = d1[:, :M].double().clamp_min(0)
-        d2f = d2[:, :M].double().clamp_min(1e-12)
-        sc0 = torch.where(m0 >= 0, 1.0 - torch.sqrt(d1f / d2f), torch.zeros_like(d1f)).float()
+        if self.conf["exact"]:
+            sc0 = _exact_scores(desc0[0].detach(), desc1[0].detach(), m0[0].to(desc0.device))[None].to(m0.device)
+        else:
+            d1f = d1[:, :M].double().clamp_min(0)
+            d2f = d2[:, :M].double().clamp_min(1e-12)
+            sc0 = torch.where(m0 >= 0, 1.0 - torch.sqrt(d1f / d2f), torch.zeros_like(d1f)).float()
         sc1 = torch.zeros((1, N), dtype=torch.float32, device=m0.device)
         valid1 = m1[0] >= 0
         sc1[0, valid1] = sc0[0, m1[0, valid1]]

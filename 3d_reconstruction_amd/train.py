@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from ._abi import call, dev, ptr, require_gpu, stream_ptr
-from .voxel import MASK_PLENOXEL, MASK_SDF, _f3, _host_ptr
+from .voxel import MASK_PLENOXEL, MASK_SDF, _f3, _host_ptr, ray_aabb, sample_uniform
 
 
 class GridTrainer:
@@ -105,3 +105,23 @@ class GridTrainer:
         loss, _, B = self._backward(rays_o, rays_d, gt, z)
         self.optimizer_step()
         return float(loss.item()) / (3 * B) if B else float("nan")
+
+    def sdf_step(self, rays_o, rays_d, gt, num_samples: int = 160, t_rand=None):
+        """One iteration of sdf.py's training loop (sdf.py:427-438) on an SDF-mode
+        trainer: the sampler's ray-box test (sdf.py:154-165; rays that miss
+        are dropped, sdf.py:229-232), ``num_samples`` stratified depths with the
+        jitter ``t_rand`` (Bv, S) (torch.rand_like at sdf.py:176; drawn here
+        when omitted), forward, ``mse_loss(gt[valid], rgb)``, backward and
+        Adam.  Returns (loss.item(), valid (B,) bool device tensor)."""
+        if self.mask_mode != MASK_SDF:
+            raise ValueError("sdf_step needs an SDF-mode trainer (mask_mode=MASK_SDF)")
+        o = dev(rays_o, torch.float32).reshape(-1, 3)
+        d = dev(rays_d, torch.float32).reshape(-1, 3)
+        t = dev(gt, torch.float32).reshape(-1, 3)
+        tn, tf, valid = ray_aabb(o, d, self.bmin, self.bmax)
+        idx = torch.nonzero(valid).squeeze(1)
+        if idx.numel() == 0:
+            raise ValueError("No valid rays intersect the grid.")
+        z = sample_uniform(tn[idx].contiguous(), tf[idx].contiguous(), num_samples, t_rand)
+        loss = self.step(o[idx].contiguous(), d[idx].contiguous(), t[idx].contiguous(), z)
+        return loss, valid

@@ -55,6 +55,17 @@ DLT_FLOP_PER_OBS = 1200.0     # 6x4 f64 DLT null vector, ~1.2 kf
 FDJ_BYTES_PER_OBS = 200.0     # 40 B in + 16 B residual + 144 B Jacobian values
 DLT_BYTES_PER_OBS = 64.0      # 2 x 2 f64 pixels in, 4 f64 out
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2", "traffic.json")
+VERIFY_WORK_FILE = os.path.join(ROOT, "profiles", "r3", "verify_work.json")
+# Algorithmic fp64 flop counts of the secondary lines (DESIGN.md §5 derives each):
+F_5PT = 18_000.0        # one 5-point solve: 5x9 null space, 10x20 constraint matrix, 10x10 solve, degree-10 roots
+F_SAMPSON = 38.0        # one Sampson error (E x1, E^T x2, x2^T E x1, 4 squares, quotient) per model and point
+F_TRI_POSE = 1_250.0    # recoverPose: one DLT point (1.2 kflop) + two depth tests, per candidate pose
+F_EPNP = 90_000.0       # one EPnP hypothesis on 5 points (12x12 M^T M, Jacobi eigenvectors, 3 beta sets + GN, Procrustes)
+F_PNP_SCORE = 30.0      # one reprojection + squared error per hypothesis and point
+F_LM_OBS = 290.0        # one CvLevMarq pass per inlier: projection + analytic 2x6 Jacobian + J^T J / J^T e
+F_BA_J_OBS = 500.0      # one scipy 2-point FD Jacobian row pair per observation: 10 projections
+F_BA_STEP_OBS = 650.0   # the damped GN direction, the 2-D subspace products and one trial residual, per observation
+BA_BYTES_OBS = 64.0     # compulsory per solve: X (24 B) + pixel (16 B) read, X (24 B) written
 
 
 def pmc_traffic(kind: str, frac: float = 1.0):
@@ -65,6 +76,17 @@ def pmc_traffic(kind: str, frac: float = 1.0):
             t = json.load(f)
         return t[kind]["bytes_per_step"] * frac
     except (OSError, KeyError, ValueError):
+        return None
+
+
+def verify_work():
+    """Data-dependent work terms measured on the bench scenes by
+    tools/count_verify_work.py (mean 5-point models per RANSAC sample, LM
+    projection passes per PnP refinement)."""
+    try:
+        with open(VERIFY_WORK_FILE) as f:
+            return json.load(f)
+    except (OSError, ValueError):
         return None
 
 
@@ -106,12 +128,13 @@ def max_over_ranks(x: float, world: int, device) -> float:
 # ---------------------------------------------------------------------------
 # CPU baseline methodology: host threads, 1 warm-up + median of 3
 def host_threads() -> int:
-    """Threads this process may use on the host: OMP_NUM_THREADS (16 on the GPU
-    box: our share of its CPUs) or the affinity mask."""
+    """Threads this process may use on the host: OMP_NUM_THREADS when the
+    environment sets it (the GPU box sets 16, this job's share of the host: its
+    rules size worker pools to that share), else the whole affinity mask."""
     try:
         return max(1, int(os.environ["OMP_NUM_THREADS"]))
     except (KeyError, ValueError):
-        return max(1, min(16, len(os.sched_getaffinity(0))))
+        return max(1, len(os.sched_getaffinity(0)))
 
 
 def host_info() -> dict:
@@ -124,7 +147,8 @@ def host_info() -> dict:
                     break
     except OSError:
         pass
-    return {"cpu_count": os.cpu_count(), "threads_used": host_threads(), "model": model,
+    return {"cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "threads_used": host_threads(), "model": model,
             "numpy": np.__version__, "torch_threads": torch.get_num_threads()}
 
 
@@ -457,14 +481,28 @@ def verify_line(sfm, syn, device, args, barrier, cpu=True):
 
     wall, kms = timed(step, args.steps, 1, barrier)
     ms = wall / args.steps * 1e3
-    iters = holder["r"]["iters"].float().mean().item()
+    it_p = holder["r"]["iters"].double().cpu().numpy()
+    iters = float(it_p.mean())
+    n_p = np.array([len(x) for x in s["pts0"]], np.float64)
+    k_ms = float(np.mean(kms))
     line = {"metric": "geometric verification pairs/sec", "value": 256 / (ms * 1e-3), "unit": "pairs/s",
             "ms_per_step": ms,
             "config": {"workload": "findEssentialMat(RANSAC, 0.999, 1px) + recoverPose: 256 pairs x 2048 matches, "
                                    "30% outliers, 0.5 px noise (matching.py:134-139 / sfm.py:108-119)",
                        "mean_ransac_iters": iters},
             "roofline": {"bound": "fp64", "kernel": "essential_ransac_kernel+recover_pose_kernel",
-                         "kernel_ms": float(np.mean(kms))}}
+                         "kernel_ms": k_ms}}
+    vw = verify_work()
+    if vw is not None:
+        mps = vw["essential"]["models_per_sample"]
+        flops = float(np.sum(it_p * (F_5PT + mps * n_p * F_SAMPSON)) + np.sum(4.0 * n_p * F_TRI_POSE))
+        tf = flops / (k_ms * 1e-3) / 1e12
+        line["roofline"].update({
+            "unit": "TFLOP/s", "algorithmic_flop": flops, "achieved": tf, "peak": PEAK_FP64_TFLOPS,
+            "frac": tf / PEAK_FP64_TFLOPS,
+            "count": f"sum over pairs of iters x ({F_5PT:.0f} + {mps:.2f} models/sample x n x {F_SAMPSON:.0f}) "
+                     f"+ 4 poses x n x {F_TRI_POSE:.0f} (recoverPose); models/sample from "
+                     f"profiles/r3/verify_work.json"})
     if cpu:
         from oracle import ransac as orc
 
@@ -594,12 +632,25 @@ def pnp_line(sfm, syn, device, args, barrier, cpu=True):
 
     wall, kms = timed(step, args.steps, 1, barrier)
     ms = wall / args.steps * 1e3
+    k_ms = float(np.mean(kms))
+    it_p = holder["r"]["iters"].double().cpu().numpy()
+    inl_p = holder["r"]["n_inliers"].double().cpu().numpy()
     line = {"metric": "PnP registrations/sec", "value": P / (ms * 1e-3), "unit": "registrations/s",
             "ms_per_step": ms,
             "config": {"workload": "solvePnPRansac (sfm.py:116: 100 iters, 8 px, 0.99) + LM refine: 256 problems x "
                                    "2000 correspondences, 30% outliers",
-                       "mean_ransac_iters": holder["r"]["iters"].float().mean().item()},
-            "roofline": {"bound": "fp64", "kernel": "pnp_ransac_kernel", "kernel_ms": float(np.mean(kms))}}
+                       "mean_ransac_iters": float(it_p.mean())},
+            "roofline": {"bound": "fp64", "kernel": "pnp_ransac_kernel", "kernel_ms": k_ms}}
+    vw = verify_work()
+    if vw is not None:
+        lm_passes = vw["pnp"]["lm_projection_passes_per_problem"]
+        flops = float(np.sum(it_p * (F_EPNP + n * F_PNP_SCORE)) + np.sum(lm_passes * inl_p * F_LM_OBS))
+        tf = flops / (k_ms * 1e-3) / 1e12
+        line["roofline"].update({
+            "unit": "TFLOP/s", "algorithmic_flop": flops, "achieved": tf, "peak": PEAK_FP64_TFLOPS,
+            "frac": tf / PEAK_FP64_TFLOPS,
+            "count": f"sum over problems of iters x ({F_EPNP:.0f} + n x {F_PNP_SCORE:.0f}) + {lm_passes:.2f} LM "
+                     f"passes x inliers x {F_LM_OBS:.0f}; LM passes from profiles/r3/verify_work.json"})
     if cpu:
         from oracle import pnp as opnp
         line["cpu_baseline"] = cpu_leg(lambda k, nt: pool_map(lambda i: opnp.solve_pnp_ransac(Xs[i], uvs[i], K),
@@ -741,14 +792,15 @@ def ba_solve_line(sfm, syn, device, args, barrier, cpu=True):
     off = torch.arange(BA_PAIRS + 1, dtype=torch.int64, device=device) * BA_OBS
     cam, X = tt["cam"].clone(), tt["X"].clone()
     holder = {}
+    sfm.ba_solve_batched(cam, tt["K"], X, tt["pts2d"], off)     # validates the offsets once (host sync)
 
     def step(record):
         e0, e1 = events() if record else (None, None)
-        if record:
-            e0.record()
         cam.copy_(tt["cam"])
         X.copy_(tt["X"])
-        holder["r"] = sfm.ba_solve_batched(cam, tt["K"], X, tt["pts2d"], off)
+        if record:
+            e0.record()
+        holder["r"] = sfm.ba_solve_batched(cam, tt["K"], X, tt["pts2d"], off, validate=False)
         if record:
             e1.record()
         return (e0, e1)
@@ -756,13 +808,48 @@ def ba_solve_line(sfm, syn, device, args, barrier, cpu=True):
     wall, kms = timed(step, args.steps, 1, barrier)
     ms = wall / args.steps * 1e3
     r = holder["r"]
+    k_ms = float(np.mean(kms))
+    nfev = r["nfev"].double().cpu().numpy()
+    njev = r["njev"].double().cpu().numpy()
+    flops = float(np.sum(BA_OBS * (njev * F_BA_J_OBS + nfev * F_BA_STEP_OBS)))
+    tf = flops / (k_ms * 1e-3) / 1e12
     line = {"metric": "BA solves/sec (sfm.py:38 least_squares, on device)", "value": BA_PAIRS / (ms * 1e-3),
             "unit": "pairs/s", "ms_per_step": ms, "dtype": "f64",
             "config": {"workload": f"C3 BA: {BA_PAIRS} pairs x {BA_OBS} obs, scipy TRF (x_scale='jac', ftol 1e-8) "
-                                   f"restated, one workgroup per pair",
-                       "mean_nfev": float(r["nfev"].float().mean().item()),
+                                   f"restated on the device",
+                       "mean_nfev": float(nfev.mean()), "mean_njev": float(njev.mean()),
                        "status_ok": int((r["status"] > 0).sum().item())},
-            "kernel_ms": float(np.mean(kms))}
+            "kernel_ms": k_ms,
+            "roofline": {"bound": "fp64", "kernel": "ba_trf_kernel", "kernel_ms": k_ms, "unit": "TFLOP/s",
+                         "algorithmic_flop": flops, "achieved": tf, "peak": PEAK_FP64_TFLOPS,
+                         "frac": tf / PEAK_FP64_TFLOPS,
+                         "achieved_gbs": BA_PAIRS * BA_OBS * BA_BYTES_OBS / (k_ms * 1e-3) / 1e9,
+                         "count": f"sum over pairs of n_obs x (njev x {F_BA_J_OBS:.0f} + nfev x {F_BA_STEP_OBS:.0f}) "
+                                  f"fp64 flops; compulsory bytes {BA_BYTES_OBS:.0f} per observation per solve "
+                                  f"(achieved_gbs): the fp64 bound is the larger"}}
+    # sfm.py:37-38 left exactly as written (scipy least_squares, jac_sparsity=ba_sparse, 2-point FD) with
+    # only `import sfmhip as cv2`: every residual evaluation is one sfmhip.projectPoints call (host <->
+    # device round trip); scipy's TRF / LSMR stay on the host.  Wall time per pair on one C3 pair.
+    from scipy.optimize import least_squares as _ls
+    import sfmhip as cv2_alias
+    p0 = 0
+    sl0 = slice(p0 * BA_OBS, (p0 + 1) * BA_OBS)
+    x0_0 = np.concatenate([s["cam"][p0], s["X"][sl0].ravel()])
+    A0 = cv2_alias.ba_sparse(BA_OBS, len(x0_0), 6)
+
+    def sfm_py_residual(x, K, point_2D):
+        proj, _ = cv2_alias.projectPoints(x[6:].reshape((len(point_2D), 3)), x[:3], x[3:6], K, distCoeffs=None)
+        return (point_2D - proj[:, 0, :]).ravel()
+    hold = {}
+
+    def literal():
+        hold["r"] = _ls(sfm_py_residual, x0_0, jac_sparsity=A0, x_scale="jac", ftol=1e-8,
+                        args=(s["K"][p0], s["pts2d"][sl0]))
+    t_lit, ts_lit = cpu_median(literal)
+    line["unchanged_sfm_py"] = {
+        "s_per_pair": t_lit, "nfev": int(hold["r"].nfev),
+        "note": "sfm.py:38 unchanged, `import sfmhip as cv2`: scipy least_squares on the host, each residual "
+                "evaluation one sfmhip.projectPoints call; one C3 pair (4096 obs), median of 3 after 1 warm-up"}
     if cpu:
         from scipy.optimize import least_squares
         from oracle import geometry as og
@@ -840,6 +927,65 @@ def composite_line(result, match_cpu, ba, tsdf):
                                    "times are linear extrapolations of the timed samples"}}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``bench.py --gpus N`` (N > 1) without a torch.distributed launcher: start
+    N fresh child processes of this script, one per GPU, with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, and wait for them.  The parent
+    never touches the GPU (it only imported torch) and never exec's: the
+    children are new processes.  Rank 0 inherits stdout (the one JSON line);
+    the other ranks' stdout goes to stderr.  If any child fails, the others are
+    stopped (their exact PIDs) and its exit code is returned."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log(f"[launcher] rank {procs.index(p)} exited with {code}; stopping the other ranks")
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def dry_run(world: int, rank: int, backend: str) -> dict:
+    """--dry-run: the rank/world plumbing without any GPU work (CPU tests of
+    the launcher): every rank joins the process group and the world is
+    all-gathered."""
+    if world > 1:
+        dist.init_process_group(backend)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                                       "pid": os.getpid()})
+        dist.destroy_process_group()
+    else:
+        ranks = [{"rank": 0, "local_rank": 0, "pid": os.getpid()}]
+    return {"metric": "image-pairs matched/sec", "value": None, "unit": "pairs/s", "n_gpus": world,
+            "dry_run": True, "ranks": ranks}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -851,7 +997,24 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for rehearsal")
     ap.add_argument("--rehearse-overlap", action="store_true",
                     help="N=1 rehearsal of the N>1 path: a one-rank RCCL communicator + the overlapped all-gather")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/process-group plumbing only (no GPU work; CPU tests)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {args.gpus})")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # one process per GPU: this process only launches and waits (no GPU call here)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} does not match the launcher's WORLD_SIZE {world}")
+    if args.dry_run:
+        line = dry_run(world, rank, "gloo" if args.dist_backend == "nccl" else args.dist_backend)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        return
     # stdout carries exactly one JSON line: RCCL (version banner at communicator
     # init) and other libraries print to fd 1, so fd 1 becomes stderr for the run
     # and the result goes to a private copy of the original stdout
@@ -859,8 +1022,6 @@ def main():
     out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("SFMHIP_BENCH_SAME_DEVICE"):  # rehearsal: every rank on device 0
         local = 0

@@ -194,10 +194,12 @@ int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, const double* 
  * pair_off (n_pairs + 1) int64 device offsets (off[0] = 0, observations of a
  * pair contiguous); max_nfev <= 0: scipy's default 100 * len(x).  Outputs per
  * pair: final cost 0.5 |f|^2, nfev, njev, status (scipy's codes 0..4).
+ * n_obs = rows of X / pts2d: a pair whose offsets are not
+ * 0 <= off[p] <= off[p+1] <= n_obs touches nothing and gets status -1.
  * The Gauss-Newton direction is the exact damped least-squares solution where
  * scipy runs LSMR to 1e-6 (oracle/ba.py). */
 int sfmhip_ba_solve(double* cam, const double* K, double* X, const double* pts2d, const int64_t* pair_off,
-                    int n_pairs, double ftol, double xtol, double gtol, int max_nfev, double* cost,
+                    int n_pairs, int64_t n_obs, double ftol, double xtol, double gtol, int max_nfev, double* cost,
                     int32_t* nfev, int32_t* njev, int32_t* status, void* stream);
 
 /* ---- V1: voxel_traversal (voxel_travesal.py:1-73), quirks included -------
@@ -370,10 +372,6 @@ int sfmhip_ray_aabb(const float* rays_o, const float* rays_d, int64_t B, const f
  * + t_far t with t = linspace(0,1,S); perturb: lower + (upper-lower) t_rand.  */
 int sfmhip_stratified_samples(const float* t_near, const float* t_far, const float* t_rand, int64_t B,
                               int S, int perturb, float* z, void* stream);
-
-/* Debug: phase timers of essential_ransac_kernel (tools/prof_ransac.py); all
- * zero unless the library is built with -DSFMHIP_RANSAC_PROF.  out[16].       */
-int sfmhip_debug_ransac_prof(unsigned long long* out);
 
 /* ---- multi-GPU: the match-graph collective ---------
  * Thin C-ABI over RCCL (resolved with dlopen at first use: the RCCL already

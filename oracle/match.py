@@ -110,11 +110,17 @@ def bf_match(desc0, desc1, ratio=0.75, mutual=False, mode=MODE_FLOAT):
 def sq_dist_exact(xa, xb) -> np.ndarray:
     """Exact-float-mode distance (module docstring), f64 (M, N)."""
     A = np.asarray(xa, np.float32).astype(np.float64)
-    B = np.asarray(xb, np.float32).astype(np.float64)
-    D = np.zeros((A.shape[0], B.shape[0]))
-    for k in range(A.shape[1]):
-        t = A[:, k][:, None] - B[:, k][None, :]
-        D += t * t
+    BT = np.ascontiguousarray(np.asarray(xb, np.float32).astype(np.float64).T)
+    D = np.zeros((A.shape[0], BT.shape[1]))
+    rows = max(1, 65536 // max(1, BT.shape[1]))          # row blocks that stay in cache across the k loop
+    t = np.empty((rows, BT.shape[1]))
+    for r0 in range(0, A.shape[0], rows):
+        Dr = D[r0:r0 + rows]
+        tr = t[:Dr.shape[0]]
+        for k in range(A.shape[1]):                     # k order, one IEEE op per step
+            np.subtract(A[r0:r0 + rows, k][:, None], BT[k][None, :], out=tr)
+            np.multiply(tr, tr, out=tr)
+            np.add(Dr, tr, out=Dr)
     return D
 
 

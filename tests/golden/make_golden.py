@@ -475,6 +475,52 @@ def gen_sdf_sampler():
          valid=valid.numpy(), t_rand=t_rand.numpy(), pts=pts.detach().numpy(), rgb=c.detach().numpy())
 
 
+def gen_sdf_train():
+    """Two steps of sdf.py's training loop body (sdf.py:427-438): SDFGrid forward
+    (GradientBasedSampler, 160 perturbed stratified samples) -> mse_loss on the
+    valid rays -> zero_grad / backward -> Adam(lr=1e-2).step(), CPU torch, the
+    reference's own SDFGrid (stub cv2).  The jitter t_rand of each step
+    (torch.rand_like at sdf.py:176, the sampler's first draw) is captured by
+    re-seeding; Adam also holds SDFGrid's alpha / beta, which get no gradient."""
+    sys.modules.setdefault("cv2", types.ModuleType("cv2"))
+    sd = load("ref_sdf_train", os.path.join(REF, "sdf.py"))
+    torch.manual_seed(41)
+    res = (8, 9, 10)
+    mn, mx = (-1.0, -1.2, -0.9), (1.1, 1.0, 1.2)
+    model = sd.SDFGrid(res, mn, mx, "cpu")
+    with torch.no_grad():
+        model.grid.copy_(torch.randn_like(model.grid) * 0.3 + 0.15)
+    grid0 = model.grid.detach().numpy().copy()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+    rng = np.random.default_rng(41)
+    B = 40
+    out = dict(grid0=grid0, bmin=np.array(mn, np.float32), bmax=np.array(mx, np.float32))
+    for step in (1, 2):
+        ro = (rng.normal(0, 0.4, (B, 3)) + np.array([0, 0, -3.5])).astype(np.float32)
+        rd = (rng.normal(0, 0.25, (B, 3)) + np.array([0, 0, 1.0])).astype(np.float32)
+        rd[:3] = rng.normal(0, 1, (3, 3))                          # a few rays that may miss the box
+        rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+        gt = rng.uniform(0, 1, (B, 3)).astype(np.float32)
+        seed = 400 + step
+        ro_t, rd_t, gt_t = torch.from_numpy(ro), torch.from_numpy(rd), torch.from_numpy(gt)
+        torch.manual_seed(seed)
+        rgb, pts, valid = model(ro_t, rd_t)
+        loss = torch.nn.functional.mse_loss(gt_t[valid], rgb)
+        opt.zero_grad()
+        loss.backward()
+        grad = model.grid.grad.detach().numpy().copy()
+        opt.step()
+        torch.manual_seed(seed)
+        t_rand = torch.rand((int(valid.sum()), model.sampler.num_samples))
+        out.update({f"ro{step}": ro, f"rd{step}": rd, f"gt{step}": gt, f"t_rand{step}": t_rand.numpy(),
+                    f"valid{step}": valid.numpy(), f"rgb{step}": rgb.detach().numpy(),
+                    f"loss{step}": np.array(loss.item()), f"grad{step}": grad,
+                    f"grid{step}": model.grid.detach().numpy().copy()})
+    st = opt.state[model.grid]
+    out.update(exp_avg2=st["exp_avg"].numpy().copy(), exp_avg_sq2=st["exp_avg_sq"].numpy().copy())
+    save("sdf_train_golden.npz", **out)
+
+
 if __name__ == "__main__":
     gen_vq()
     gen_filter_matches()
@@ -487,3 +533,4 @@ if __name__ == "__main__":
     gen_sfm_triangulate()
     gen_train()
     gen_sdf_sampler()
+    gen_sdf_train()

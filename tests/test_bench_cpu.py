@@ -59,3 +59,47 @@ def test_composite_line_arithmetic():
     assert abs(c["cpu_s"] - (10.0 + 1.0 + 3.0)) < 1e-9
     assert abs(c["cpu_s_1thread"] - (100.0 + 1.0 + 6.0)) < 1e-9
     assert bench.composite_line(res, None, ba, tsdf) is None
+
+
+def _run_bench(args, env_extra=None, timeout=120):
+    import json
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR")}
+    env.update(env_extra or {})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    return p, [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """bench.py --gpus 2 (no torch.distributed launcher) starts two fresh rank
+    processes; rank 0 prints one JSON line with n_gpus 2 and both ranks."""
+    p, lines = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--dry-run"])
+    assert p.returncode == 0, p.stderr
+    assert len(lines) == 1
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["dry_run"] is True
+    assert [r["rank"] for r in ln["ranks"]] == [0, 1]
+    assert [r["local_rank"] for r in ln["ranks"]] == [0, 1]
+    assert len({r["pid"] for r in ln["ranks"]}) == 2
+
+
+def test_bench_gpus_must_match_world():
+    p, lines = _run_bench(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert p.returncode != 0 and not lines
+    assert "does not match" in p.stderr
+
+
+def test_bench_single_rank_default():
+    p, lines = _run_bench(["--dry-run"])
+    assert p.returncode == 0, p.stderr
+    assert lines[0]["n_gpus"] == 1
+
+
+def test_bench_launcher_propagates_rank_failure():
+    p, lines = _run_bench(["--gpus", "2", "--dist-backend", "no_such_backend", "--dry-run"])
+    assert p.returncode != 0 and not lines

@@ -67,7 +67,8 @@ def test_ba_solve_batched_vs_oracle(sfm, gpu, far):
         xo = np.concatenate([o["cam"], o["X"].ravel()])
         xg = np.concatenate([cam[p], X[off[p]:off[p + 1]].ravel()])
         assert np.abs(xg - xo).max() <= 1e-6 * np.abs(xo).max(), p
-        assert res["cost"][p] <= max(10 * o["cost"], 1e-16)
+        # the cost is flat along the solution manifold the point slides on: 1e-6 relative
+        assert abs(res["cost"][p] - o["cost"]) <= 1e-6 * o["cost"] + 1e-12, p
 
 
 def test_least_squares_ba_drop_in_vs_scipy(sfm, gpu):
@@ -80,7 +81,7 @@ def test_least_squares_ba_drop_in_vs_scipy(sfm, gpu):
     assert g.success and r.success
     assert abs(g.nfev - r.nfev) <= 1
     assert np.abs(g.x - r.x).max() <= 1e-6 * np.abs(r.x).max()
-    assert g.cost <= max(10 * r.cost, 1e-16)
+    assert abs(g.cost - r.cost) <= 1e-6 * r.cost + 1e-12
     np.testing.assert_allclose(g.fun, og.reprojection_error(g.x, Ks[0], ps[0]), rtol=1e-9, atol=1e-9)
 
 
@@ -93,3 +94,54 @@ def test_ba_solve_rejects_bad_shapes(sfm, gpu):
         sfm.ba_solve_batched(cam, K, X, P, torch.zeros(2, dtype=torch.int64, device=gpu))
     with pytest.raises(ValueError):
         sfm.ba_solve_batched(cam, K, X.float(), P, torch.zeros(3, dtype=torch.int64, device=gpu))
+
+
+def test_ba_solve_malformed_offsets(sfm, gpu):
+    """Offsets that are not 0 <= off[p] <= off[p+1] <= n: the wrapper raises, and
+    with validation off the kernel skips those pairs (status -1) without
+    touching X outside any valid range."""
+    cams, Ks, Xs, ps = _ragged_problem([40, 40, 40], seed=61)
+    cam = torch.tensor(np.stack(cams), device=gpu)
+    K = torch.tensor(np.stack(Ks), device=gpu)
+    X = torch.tensor(np.concatenate(Xs), device=gpu)
+    P = torch.tensor(np.concatenate(ps), device=gpu)
+    for off in ([0, 40, 30, 120], [0, 40, 80, 121], [5, 40, 80, 120], [0, 40, 200, 120]):
+        with pytest.raises(ValueError):
+            sfm.ba_solve_batched(cam, K, X, P, torch.tensor(off, dtype=torch.int64, device=gpu))
+    X0 = X.clone()
+    res = sfm.ba_solve_batched(cam, K, X, P, torch.tensor([0, 40, 200, 120], dtype=torch.int64, device=gpu),
+                               validate=False)
+    torch.cuda.synchronize()
+    st = res["status"].cpu().numpy()
+    assert st[0] > 0 and st[1] == -1 and st[2] == -1
+    assert torch.equal(X[40:], X0[40:])               # the skipped pairs' points are untouched
+
+
+def _sfm_py_residual(cv2):
+    """The residual sfm.py:87-91 hands to least_squares, written against a cv2
+    module: x = [rvec, t, X...] -> point_2D - projectPoints(X, rvec, t, K)."""
+    def residual(x, K, point_2D):
+        pts3d = x[6:].reshape((len(point_2D), 3))
+        proj, _ = cv2.projectPoints(pts3d, x[:3], x[3:6], K, distCoeffs=None)
+        return (point_2D - proj[:, 0, :]).ravel()
+    return residual
+
+
+def test_unchanged_sfm_py_least_squares_through_sfmhip(sfm, gpu):
+    """sfm.py:37-38 left exactly as written — scipy least_squares with
+    jac_sparsity=ba_sparse(...), x_scale='jac', ftol=1e-8 and the default
+    2-point FD — with only ``import sfmhip as cv2`` swapped in: every residual
+    evaluation goes through sfmhip.projectPoints on the device.  Same solution
+    as the oracle-driven run (the FD quantum of device vs glibc sin/cos is the
+    only difference in the Jacobian)."""
+    import sfmhip as cv2
+    cams, Ks, Xs, ps = _ragged_problem([500], seed=52, far=True)
+    x0 = np.concatenate([cams[0], Xs[0].ravel()])
+    A = cv2.ba_sparse(500, len(x0), 6)
+    got = least_squares(_sfm_py_residual(cv2), x0, jac_sparsity=A, x_scale="jac", ftol=1e-8, args=(Ks[0], ps[0]))
+    ref = least_squares(og.reprojection_error, x0, jac_sparsity=og.ba_sparse(500, len(x0), 6), x_scale="jac",
+                        ftol=1e-8, args=(Ks[0], ps[0]))
+    assert got.success and ref.success
+    assert abs(got.nfev - ref.nfev) <= 1
+    assert np.abs(got.x - ref.x).max() <= 1e-6 * np.abs(ref.x).max()
+    assert abs(got.cost - ref.cost) <= 1e-6 * ref.cost + 1e-12

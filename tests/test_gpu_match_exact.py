@@ -97,11 +97,20 @@ def test_exact_float_mutual_and_matcher_contract(sfm, gpu):
     r0, r1 = om.bf_match_exact_mutual_pair(x[0], x[1, :300], (3, 4))
     assert np.array_equal(pred["matches0"][0].cpu().numpy(), r0)
     assert np.array_equal(pred["matches1"][0].cpu().numpy(), r1)
+    # scores: the Lowe margin 1 - sqrt(d1/d2) of the f64 distances (> 1 - 0.75 for every accepted match)
+    sc = pred["matching_scores0"][0].cpu().numpy()
+    a, b = x[0].astype(np.float64), x[1, :300].astype(np.float64)
+    D = ((a[:, None, :] - b[None, :, :]) ** 2).sum(-1)
+    for i in np.nonzero(r0 >= 0)[0]:
+        d1 = D[i, r0[i]]
+        d2 = np.min(np.delete(D[i], r0[i]))
+        assert abs(sc[i] - (1 - np.sqrt(d1 / d2))) < 1e-6 and sc[i] > 0.25
+    assert (sc[r0 < 0] == 0).all()
 
 
 def test_exact_float_c3_full_size_sampled_rows(sfm, gpu):
-    """C3 at full size on float SuperPoint-like descriptors: 16 pairs spread
-    over the pair index space (near and far images), 128 rows each, bit-exact
+    """C3 at full size on float SuperPoint-like descriptors: 32 pairs spread
+    over the pair index space (near and far images), 384 rows each, bit-exact
     against the oracle; the exact pass touches a small share of the rows."""
     x = syn.superpoint_like(257, 4096, 256, seed=1, device=gpu)
     bank = sfm.DescriptorBank.from_float(x, mode=1, exact=True)
@@ -113,10 +122,10 @@ def test_exact_float_c3_full_size_sampled_rows(sfm, gpu):
     assert resolved < 0.01 * len(pairs) * 4096
     rng = np.random.default_rng(7)
     near = [p for p in range(len(pairs)) if pairs[p][1] - pairs[p][0] <= 2]
-    sample = list(rng.choice(near, 8, replace=False)) + list(rng.choice(len(pairs), 8, replace=False))
+    sample = list(rng.choice(near, 16, replace=False)) + list(rng.choice(len(pairs), 16, replace=False))
     for p in sample:
         a, b = pairs[p]
-        rows = np.sort(rng.choice(4096, 128, replace=False))
+        rows = np.sort(rng.choice(4096, 384, replace=False))
         xa = bank.x[a, rows].cpu().numpy()
         xb = bank.x[b].cpu().numpy()
         ref = om.bf_match_exact(xa, xb, (3, 4))

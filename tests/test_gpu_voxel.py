@@ -386,7 +386,9 @@ def test_tsdf_planned_uneven_slabs_bitexact(sfm, gpu):
     tot = sfm.tsdf_cull_stats((R, R, R), torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K), *args)
     assert st[:, 0].sum() == tot["tested"] and st[:, 1].sum() == tot["culled"] and st[:, 2].sum() == tot["free"]
     slabs = sdist.plan_slabs(sfm.tsdf_layer_cost(st), 3, layer=8, depth=R)
-    assert len({b - a for a, b in slabs}) > 1 or True        # uneven in general
+    # three contiguous slabs covering the grid, cut on the 8-layer tile boundaries
+    assert len(slabs) == 3 and slabs[0][0] == 0 and slabs[-1][1] == R
+    assert all(a < b and a % 8 == 0 for a, b in slabs) and all(slabs[i][1] == slabs[i + 1][0] for i in range(2))
     T0 = torch.zeros((R, R, R), dtype=torch.float32, device=gpu)
     W0 = torch.zeros_like(T0)
     sfm.tsdf_integrate(T0, W0, depth, poses, K, *args)

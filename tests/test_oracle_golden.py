@@ -228,3 +228,32 @@ def test_sdf_sampler_oracle_matches_reference():
     assert np.array_equal(pts, g["pts"])                                    # bit-exact incl. torch.linspace
     rgb = ov.render(g["grid"], g["bmin"], g["bmax"], 0, g["rays_o"][va], g["rays_d"][va], z)
     np.testing.assert_allclose(rgb, g["rgb"], rtol=1e-5, atol=1e-5)
+
+
+def test_sdf_train_oracle_matches_reference_torch():
+    """sdf.py's training-loop body (SDFGrid forward with its sampler + mse on the
+    valid rays + autograd + Adam, sdf.py:427-438) on CPU torch vs the restated
+    sampler, analytic backward and Adam."""
+    from oracle import train as ot
+    g = golden("sdf_train_golden.npz")
+    grid = g["grid0"][0]
+    m = np.zeros_like(grid)
+    v = np.zeros_like(grid)
+    for step in (1, 2):
+        tn, tf, va = ov.ray_aabb(g[f"ro{step}"], g[f"rd{step}"], g["bmin"], g["bmax"])
+        assert np.array_equal(va, g[f"valid{step}"])
+        z = ov.sample_uniform(tn[va], tf[va], 160, g[f"t_rand{step}"])
+        loss, rgb, grad = ot.render_loss_grad(grid, g["bmin"], g["bmax"], 0, g[f"ro{step}"][va], g[f"rd{step}"][va],
+                                              z, g[f"gt{step}"][va])
+        assert abs(loss - float(g[f"loss{step}"])) <= 1e-6 * float(g[f"loss{step}"])
+        np.testing.assert_allclose(rgb, g[f"rgb{step}"], rtol=0, atol=1e-6)
+        # f32 sums of up to 160 samples x 8 corners in another order: 1e-6 of the largest entry
+        np.testing.assert_allclose(grad, g[f"grad{step}"][0], rtol=1e-5, atol=1e-6 * np.abs(g[f"grad{step}"]).max())
+        grid, m, v = ot.adam_step(grid, grad, m, v, step)
+        # Adam's step g / (sqrt(v) + 1e-8) is ill-conditioned where |g| is near eps: there
+        # only its bound (lr per step) is checked
+        well = np.ones(grid.shape, bool)
+        for s_ in range(1, step + 1):
+            well &= np.abs(g[f"grad{s_}"][0]) > 1e-7
+        np.testing.assert_allclose(grid[well], g[f"grid{step}"][0][well], rtol=0, atol=1e-5)
+        assert np.abs(grid - g[f"grid{step}"][0]).max() <= 2e-2 * step
