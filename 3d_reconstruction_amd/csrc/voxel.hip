@@ -1179,7 +1179,7 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
         wv.y = g1 ? d.y : wv.y;
     };
 
-    if constexpr (MODE >= 2) {
+    if constexpr (MODE == 2) {
         // frame cursor over the masks: events are free-space runs (k frames) and
         // projected frames, in frame order
         int cw = -1;
@@ -1215,7 +1215,7 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
                 for (int i = 0; i < k; ++i) update(f2s(free_ts), true, two);
             }
         };
-        constexpr int NB = MODE == 2 ? kTsdfBatch : 2;
+        constexpr int NB = kTsdfBatch;
         int val = 0, kind = next(val);
         while (kind != 0) {
             // collect up to NB projected frames and the free-space runs in front of each
@@ -1303,40 +1303,28 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
                 }
             }
             // round 3: the updates in frame order, each projected frame after the free run in front of it
-            // (one copy of the update code: the slot's values are selected, the index is wave-uniform)
-            for (int i = 0; i < nb; ++i) {
-                int run = runs[0];
-                f2 zc = Zc[0], dp = dep[0];
-                bool a0 = ok0[0], a1 = ok1[0], b0 = fr0[0], b1 = fr1[0];
 #pragma unroll
-                for (int j = 1; j < NB; ++j)
-                    if (i == j) {
-                        run = runs[j];
-                        zc = Zc[j];
-                        dp = dep[j];
-                        a0 = ok0[j]; a1 = ok1[j]; b0 = fr0[j]; b1 = fr1[j];
+            for (int i = 0; i < NB; ++i) {
+                if (i < nb) {
+                    if (runs[i]) free_run(runs[i]);
+                    const f2 sdf = dep[i] - Zc[i];
+                    const bool g0 = fr0[i] || (ok0[i] && dep[i].x > 0.f && !(sdf.x < -trunc));
+                    const bool g1 = fr1[i] || (ok1[i] && dep[i].y > 0.f && !(sdf.y < -trunc));
+                    const f2 sc = sdf * f2s(inv_trunc);
+                    const f2 ts = {fr0[i] ? free_ts : fminf(1.0f, sc.x), fr1[i] ? free_ts : fminf(1.0f, sc.y)};
+                    const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && w_runs(wv.x));
+                    const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && w_runs(wv.y));
+                    if (easy && __builtin_amdgcn_ballot_w64(!(easy0 && easy1)) == 0) {
+                        wv.x = g0 ? wv.x + 1.f : wv.x;
+                        wv.y = g1 ? wv.y + 1.f : wv.y;
+                    } else {
+                        update(ts, g0, g1);
                     }
-                if (run) free_run(run);
-                const f2 sdf = dp - zc;
-                const bool g0 = b0 || (a0 && dp.x > 0.f && !(sdf.x < -trunc));
-                const bool g1 = b1 || (a1 && dp.y > 0.f && !(sdf.y < -trunc));
-                const f2 sc = sdf * f2s(inv_trunc);
-                const f2 ts = {b0 ? free_ts : fminf(1.0f, sc.x), b1 ? free_ts : fminf(1.0f, sc.y)};
-                const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && w_runs(wv.x));
-                const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && w_runs(wv.y));
-                if (easy && __builtin_amdgcn_ballot_w64(!(easy0 && easy1)) == 0) {
-                    wv.x = g0 ? wv.x + 1.f : wv.x;
-                    wv.y = g1 ? wv.y + 1.f : wv.y;
-                } else {
-                    update(ts, g0, g1);
                 }
             }
-            {
-                int run = runs[0];
 #pragma unroll
-                for (int j = 1; j <= NB; ++j) run = j == nb ? runs[j] : run;
-                if (run) free_run(run);   // free frames after the last projected one (end of the walk)
-            }
+            for (int i = 0; i <= NB; ++i)
+                if (i == nb && runs[i]) free_run(runs[i]);   // free frames after the last projected one (end of the walk)
         }
     } else if constexpr (MODE == 1) {
         // frame cursor over the masks: events are free-space runs (k frames) and
@@ -2107,7 +2095,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     // latency mode without the block table: gathers one projected frame ahead (SFMHIP_TSDF_PIPE=0 off)
     const bool pipe = !vox_test && latency_mode && env_int("SFMHIP_TSDF_PIPE", 1) != 0;
     // batched gathers (kTsdfBatch projected frames per round; SFMHIP_TSDF_BATCH=0: the one-at-a-time paths)
-    const int batch = env_int("SFMHIP_TSDF_BATCH", 1);   // 1: 4 frames per round, 2: 2 frames
+    const bool batch = env_int("SFMHIP_TSDF_BATCH", 1) != 0;
     // longest-first workgroup order (SFMHIP_TSDF_ORDER=0 off): needs the masks and the 1-D slot grid;
     // at most 30000 slots per XCD class (16-bit sort positions; a bucket byte per slot in LDS
     // next to the 32 KB histogram, within the default 64 KB)
@@ -2205,11 +2193,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             hipLaunchKernelGGL(tsdf_order_kernel, dim3(kNumXcd), dim3(256), (size_t)ceil_div((int)grid.x, kNumXcd), st,
                                (int)grid.x, W, H, z0, z1, sb, nf, tcost, ord);
         }
-        if (swz && batch == 2)
-            hipLaunchKernelGGL((tsdf_kernel<true, 3>), grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
-                               Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv,
-                               ord, easy);
-        else if (swz && batch)
+        if (swz && batch)
             hipLaunchKernelGGL((tsdf_kernel<true, 2>), grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
                                Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv,
                                ord, easy);
