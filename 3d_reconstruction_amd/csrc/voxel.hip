@@ -1118,15 +1118,7 @@ __device__ __forceinline__ bool w_runs(float w) { return w >= 0.f && w <= 0x1p24
 // so a thin slab's longest waves overlap one depth load with the previous frame's
 // arithmetic instead of waiting out each load in turn.  The order of the updates
 // per voxel is unchanged.
-// MODE 0: one projected frame at a time (table lookup, then its gather, then the
-// update: two dependent loads per frame in series).  MODE 1 (PIPE): one frame
-// ahead, no block table.  MODE 2 (BATCH): up to kTsdfBatch projected frames per
-// round — all their projections and table loads are issued, then all their depth
-// gathers, then the updates (and the free-space runs between them) in frame
-// order — so a wave waits out two load latencies per round instead of two per
-// frame.  The loads do not depend on (T, W): only the updates are ordered.
-constexpr int kTsdfBatch = 4;
-template <bool SWZ, int MODE = 0>
+template <bool SWZ, bool PIPE = false>
 __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float* __restrict__ Wt, int D, int H,
                                                    int W, int z0, int z1, const float* __restrict__ depth, int F,
                                                    int Hd, int Wd, const float* __restrict__ rec, Bounds B,
@@ -1179,154 +1171,7 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
         wv.y = g1 ? d.y : wv.y;
     };
 
-    if constexpr (MODE == 2) {
-        // frame cursor over the masks: events are free-space runs (k frames) and
-        // projected frames, in frame order
-        int cw = -1;
-        unsigned ctodo = 0u, cfre = 0u;
-        auto next = [&](int& val) -> int {   // 0 end, 1 free run of val frames, 2 projected frame val
-            while (ctodo == 0u) {
-                if (++cw >= nw) return 0;
-                const int w0 = cw << 5;
-                unsigned t = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u), fr = 0u;
-                if (cull) {
-                    t &= ~cull[slot + cw];
-                    if (freem) fr = freem[slot + cw] & t;
-                }
-                ctodo = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
-                cfre = (unsigned)__builtin_amdgcn_readfirstlane((int)fr);
-            }
-            if (cfre & ctodo & (0u - ctodo)) {
-                const unsigned full = ctodo & ~cfre;
-                const unsigned run = ctodo & (full ? (full & (0u - full)) - 1u : ~0u);
-                ctodo &= ~run;
-                val = __builtin_popcount(run);
-                return 1;
-            }
-            val = (cw << 5) + __builtin_ctz(ctodo);
-            ctodo &= ctodo - 1u;
-            return 2;
-        };
-        auto free_run = [&](int k) {
-            const bool ones = tv.x == 1.f && tv.y == 1.f && w_runs(wv.x) && w_runs(wv.y);
-            if (free_ts == 1.f && __builtin_amdgcn_ballot_w64(!ones) == 0) {
-                wv = wv + f2s((float)k);
-            } else {
-                for (int i = 0; i < k; ++i) update(f2s(free_ts), true, two);
-            }
-        };
-        constexpr int NB = kTsdfBatch;
-        int val = 0, kind = next(val);
-        while (kind != 0) {
-            // collect up to NB projected frames and the free-space runs in front of each
-            int fs[NB], runs[NB + 1];
-#pragma unroll
-            for (int i = 0; i < NB; ++i) { fs[i] = 0; runs[i] = 0; }
-            runs[NB] = 0;
-            int nb = 0;
-            while (kind != 0 && nb < NB) {
-                if (kind == 1) {
-#pragma unroll
-                    for (int i = 0; i <= NB; ++i) runs[i] += i == nb ? val : 0;
-                } else {
-#pragma unroll
-                    for (int i = 0; i < NB; ++i) fs[i] = i == nb ? val : fs[i];
-                    ++nb;
-                }
-                kind = next(val);
-            }
-            f2 Zc[NB], dep[NB];
-            int off0[NB], off1[NB];
-            bool ok0[NB], ok1[NB], fr0[NB], fr1[NB];
-            typedef unsigned u2v __attribute__((ext_vector_type(2)));
-            u2v e0[NB], e1[NB];
-            // round 1: projections and (with the block table) the table loads of every frame
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                ok0[i] = ok1[i] = fr0[i] = fr1[i] = false;
-                Zc[i] = f2{1.f, 1.f};
-                off0[i] = off1[i] = 0;
-                if (i < nb) {
-                    const int f = fs[i];
-                    const float* r = rec + f * 16;   // uniform: scalar loads
-                    const f2 Q = (f2{r[0], r[1]} * f2s(vx) + f2{r[2], r[3]} * f2s(vz)) + f2{r[4], r[5]};
-                    const float Qz = (r[6] * vx + r[7] * vz) + r[8];
-                    const f2 Xc = f2s(r[9]) * vy + f2s(Q.x);
-                    const f2 Yc = f2s(r[10]) * vy + f2s(Q.y);
-                    Zc[i] = f2s(r[11]) * vy + f2s(Qz);
-                    const f2 iz = recip_rn(Zc[i]);
-                    const f2 uu = (f2s(r[12]) * Xc) * iz + f2s(r[14]);
-                    const f2 vv = (f2s(r[13]) * Yc) * iz + f2s(r[15]);
-                    const int iu0 = cvt_flr(uu.x), iv0 = cvt_flr(vv.x);
-                    const int iu1 = cvt_flr(uu.y), iv1 = cvt_flr(vv.y);
-                    ok0[i] = z_ok(Zc[i].x) && (unsigned)iu0 < (unsigned)Wd && (unsigned)iv0 < (unsigned)Hd;
-                    ok1[i] = two && z_ok(Zc[i].y) && (unsigned)iu1 < (unsigned)Wd && (unsigned)iv1 < (unsigned)Hd;
-                    off0[i] = (int)(__umul24(iv0, Wd4) + ((unsigned)iu0 << 2));
-                    off1[i] = (int)(__umul24(iv1, Wd4) + ((unsigned)iu1 << 2));
-                    if (bmm) {
-                        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-                            (void*)(bmm + (size_t)f * nbv * nbu), (short)0, nbv * nbu * 8, 0x00020000);
-                        e0[i] = __builtin_amdgcn_raw_buffer_load_b64(
-                            rb, (int)((__umul24((unsigned)(iv0 >> 4) & 0xFFFFFFu, (unsigned)nbu) + ((unsigned)iu0 >> 4)) << 3),
-                            0, 0);
-                        e1[i] = __builtin_amdgcn_raw_buffer_load_b64(
-                            rb, (int)((__umul24((unsigned)(iv1 >> 4) & 0xFFFFFFu, (unsigned)nbu) + ((unsigned)iu1 >> 4)) << 3),
-                            0, 0);
-                    }
-                }
-            }
-            // round 2: the block test (free / no update without the depth), then the gathers
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                dep[i] = f2{0.f, 0.f};
-                if (i < nb) {
-                    bool need0 = ok0[i], need1 = ok1[i];
-                    if (bmm) {
-                        const f2 bmn = {__builtin_bit_cast(float, (unsigned)e0[i][0]),
-                                        __builtin_bit_cast(float, (unsigned)e1[i][0])};
-                        const f2 bmx = {__builtin_bit_cast(float, (unsigned)e0[i][1]),
-                                        __builtin_bit_cast(float, (unsigned)e1[i][1])};
-                        const f2 scm = (bmn - Zc[i]) * f2s(inv_trunc);
-                        const f2 smx = bmx - Zc[i];
-                        fr0[i] = ok0[i] && bmn.x > 0.f && scm.x >= 1.f;
-                        fr1[i] = ok1[i] && bmn.y > 0.f && scm.y >= 1.f;
-                        need0 = ok0[i] && !fr0[i] && bmx.x > 0.f && !(smx.x < -trunc);
-                        need1 = ok1[i] && !fr1[i] && bmx.y > 0.f && !(smx.y < -trunc);
-                    }
-                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                        (void*)(depth + (size_t)fs[i] * frame), (short)0, nbytes, 0x00020000);
-                    if (need0) dep[i].x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off0[i], 0, 0));
-                    if (need1) dep[i].y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off1[i], 0, 0));
-                    // no update without a gather: the lanes that did not gather keep dep = 0 (never > 0)
-                    ok0[i] = need0;
-                    ok1[i] = need1;
-                }
-            }
-            // round 3: the updates in frame order, each projected frame after the free run in front of it
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                if (i < nb) {
-                    if (runs[i]) free_run(runs[i]);
-                    const f2 sdf = dep[i] - Zc[i];
-                    const bool g0 = fr0[i] || (ok0[i] && dep[i].x > 0.f && !(sdf.x < -trunc));
-                    const bool g1 = fr1[i] || (ok1[i] && dep[i].y > 0.f && !(sdf.y < -trunc));
-                    const f2 sc = sdf * f2s(inv_trunc);
-                    const f2 ts = {fr0[i] ? free_ts : fminf(1.0f, sc.x), fr1[i] ? free_ts : fminf(1.0f, sc.y)};
-                    const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && w_runs(wv.x));
-                    const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && w_runs(wv.y));
-                    if (easy && __builtin_amdgcn_ballot_w64(!(easy0 && easy1)) == 0) {
-                        wv.x = g0 ? wv.x + 1.f : wv.x;
-                        wv.y = g1 ? wv.y + 1.f : wv.y;
-                    } else {
-                        update(ts, g0, g1);
-                    }
-                }
-            }
-#pragma unroll
-            for (int i = 0; i <= NB; ++i)
-                if (i == nb && runs[i]) free_run(runs[i]);   // free frames after the last projected one (end of the walk)
-        }
-    } else if constexpr (MODE == 1) {
+    if constexpr (PIPE) {
         // frame cursor over the masks: events are free-space runs (k frames) and
         // projected frames, in frame order
         int cw = -1;
@@ -2094,8 +1939,6 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const int easy = env_int("SFMHIP_TSDF_EASY", 1) != 0;
     // latency mode without the block table: gathers one projected frame ahead (SFMHIP_TSDF_PIPE=0 off)
     const bool pipe = !vox_test && latency_mode && env_int("SFMHIP_TSDF_PIPE", 1) != 0;
-    // batched gathers (kTsdfBatch projected frames per round; SFMHIP_TSDF_BATCH=0: the one-at-a-time paths)
-    const bool batch = env_int("SFMHIP_TSDF_BATCH", 1) != 0;
     // longest-first workgroup order (SFMHIP_TSDF_ORDER=0 off): needs the masks and the 1-D slot grid;
     // at most 30000 slots per XCD class (16-bit sort positions; a bucket byte per slot in LDS
     // next to the 32 KB histogram, within the default 64 KB)
@@ -2193,12 +2036,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             hipLaunchKernelGGL(tsdf_order_kernel, dim3(kNumXcd), dim3(256), (size_t)ceil_div((int)grid.x, kNumXcd), st,
                                (int)grid.x, W, H, z0, z1, sb, nf, tcost, ord);
         }
-        if (swz && batch)
-            hipLaunchKernelGGL((tsdf_kernel<true, 2>), grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
-                               Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv,
-                               ord, easy);
-        else if (swz && pipe)
-            hipLaunchKernelGGL((tsdf_kernel<true, 1>), grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
+        if (swz && pipe)
+            hipLaunchKernelGGL((tsdf_kernel<true, true>), grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
                                Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, nullptr, nbu, nbv, ord, easy);
         else if (swz)
             hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,

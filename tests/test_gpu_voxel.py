@@ -193,13 +193,9 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
                 dict(CULL="2", LATENCY="0"), dict(CULL="2", ORDER="0"), dict(CULL="2", BRICK="0"),
                 dict(CULL="2", BRICK="0", CULLSUB="4"), dict(CULL="2", LATENCY="1", PIPE="0"),
                 dict(CULL="2", LATENCY="1", EASY="0"), dict(CULL="2", EASY="0"),
-                dict(CULL="2", LATENCY="0", REFINE="0"), dict(CULL="2", LATENCY="0", VOXTEST="0"),
-                dict(CULL="2", BATCH="0"), dict(CULL="2", BATCH="0", LATENCY="1"),
-                dict(CULL="2", BATCH="0", LATENCY="0"), dict(CULL="2", BATCH="0", LATENCY="1", PIPE="0"),
-                dict(CULL="2", LATENCY="1", EASY="0", BATCH="1"), dict(CULL="2", CHUNK="3", BATCH="1")]
+                dict(CULL="2", LATENCY="0", REFINE="0"), dict(CULL="2", LATENCY="0", VOXTEST="0")]
     for v in variants:
-        for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST", "REFINE", "LATENCY", "ORDER", "BRICK", "PIPE", "EASY",
-                  "BATCH"):
+        for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST", "REFINE", "LATENCY", "ORDER", "BRICK", "PIPE", "EASY"):
             monkeypatch.delenv("SFMHIP_TSDF_" + k, raising=False)
         for k, x in v.items():
             monkeypatch.setenv("SFMHIP_TSDF_" + k, x)
@@ -207,7 +203,7 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
         W = torch.zeros_like(T)
         sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95, z0=5, z1=90)
         out.append((T.cpu(), W.cpu()))
-    for i in [1, 2] + list(range(4, len(variants))):
+    for i in (1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18):
         assert torch.equal(out[0][0], out[i][0]) and torch.equal(out[0][1], out[i][1]), variants[i]
     assert (out[0][1] > 0).float().mean() > 0.3
     assert torch.equal(out[0][1], out[3][1])            # probe: same update pattern ...
@@ -305,13 +301,6 @@ def test_tsdf_c5_full_size_slabs_bitexact(sfm, gpu, monkeypatch):
     # the latency mode of thin slabs (no block-table test, no refinement pass) on the full grid
     monkeypatch.setenv("SFMHIP_TSDF_CULL", "1")
     monkeypatch.setenv("SFMHIP_TSDF_LATENCY", "1")
-    T2.zero_()
-    W2.zero_()
-    sfm.tsdf_integrate(T2, W2, *args)
-    assert torch.equal(T, T2) and torch.equal(W, W2)
-    # the one-frame-at-a-time fusion (no batched gathers) on the full grid
-    monkeypatch.delenv("SFMHIP_TSDF_LATENCY")
-    monkeypatch.setenv("SFMHIP_TSDF_BATCH", "0")
     T2.zero_()
     W2.zero_()
     sfm.tsdf_integrate(T2, W2, *args)
