@@ -558,6 +558,19 @@ def train_line(sfm, syn, device, args, barrier, cpu=True):
     wall, kms = timed(step, args.steps, 1, barrier)
     ms = wall / args.steps * 1e3
     adam_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["a"]]))
+    # this box's streaming rate on the same buffers (a device copy of the parameter lines):
+    # Adam's time tracks it from box to box (tools/adam_probe.py)
+    tmp = torch.empty_like(tr.param)
+    cps = []
+    for _ in range(4):
+        a, b = events()
+        a.record()
+        tmp.copy_(tr.param)
+        b.record()
+        torch.cuda.synchronize()
+        cps.append(2 * tr.param.numel() * 4 / (a.elapsed_time(b) * 1e-3) / 1e9)
+    del tmp
+    copy_gbs = max(cps[1:])
     n_par = 28 * N ** 3
     tr.backward(ro, rd, gt, z)                    # the share of voxel lines one step's scatter touches
     touched = float(tr.touched.float().mean().item())
@@ -572,6 +585,8 @@ def train_line(sfm, syn, device, args, barrier, cpu=True):
                          "frac": n_par * 32 / (adam_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                          "touched_line_frac": touched,
                          "moved_gbs": n_par * 32 / 28 * moved / (adam_ms * 1e-3) / 1e9,
+                         "box_copy_gbs": copy_gbs,
+                         "moved_vs_copy": (n_par * 32 / 28 * moved / (adam_ms * 1e-3) / 1e9) / copy_gbs,
                          "note": "torch Adam's 32 B/param (p, g, m, v read; p, m, v, g written) is the algorithmic "
                                  "count; the kernel skips grad lines the step's scatter did not touch (known 0), and "
                                  "moves (24 + 8 x touched) B per slot of the voxel-major 32-channel layout "
