@@ -19,16 +19,16 @@
 #include "common.h"
 #include "geom_dev.h"
 #include <climits>
+#include <cstdlib>
 
 namespace sfmhip {
 namespace {
 
-constexpr int kBaThreads = 256;
 constexpr int kRec = 26;   // per observation: J (18: u row, v row), f (2), scale_inv of the point (3), X_new (3)
 
-// sum of K doubles over the workgroup; every thread receives the totals in out[]
-template <int K>
-__device__ void block_sum(double (&v)[K], double* red /* [4][K] */, double* out /* [K] */) {
+// sum of K doubles over the workgroup (NW waves); every thread receives the totals in out[]
+template <int NW, int K>
+__device__ void block_sum(double (&v)[K], double* red /* [NW][K] */, double* out /* [K] */) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -41,17 +41,29 @@ __device__ void block_sum(double (&v)[K], double* red /* [4][K] */, double* out 
 #pragma unroll
         for (int k = 0; k < K; ++k) red[wave * K + k] = v[k];
     __syncthreads();
-    if (threadIdx.x < K) out[threadIdx.x] = (red[threadIdx.x] + red[K + threadIdx.x]) + (red[2 * K + threadIdx.x] + red[3 * K + threadIdx.x]);
+    if (threadIdx.x < K) {   // pairwise over the waves, a fixed order
+        double t[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) t[w] = red[w * K + threadIdx.x];
+#pragma unroll
+        for (int h = NW / 2; h >= 1; h >>= 1)
+#pragma unroll
+            for (int w = 0; w < h; ++w) t[w] = t[w] + t[w + h];
+        out[threadIdx.x] = t[0];
+    }
     __syncthreads();
 }
 
+template <int NW>
 __device__ double block_max(double v, double* red) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
     if (lane == 0) red[wave] = v;
     __syncthreads();
-    const double m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    double m = red[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) m = fmax(m, red[w]);
     __syncthreads();
     return m;
 }
@@ -122,17 +134,39 @@ __device__ void tr_solve_2d(const double B[3] /* b00, b01, b11 */, const double 
     p[1] = Delta * sin(best);
 }
 
+template <int NW>
 struct BaState {   // LDS: the iteration's scalars, written by thread 0 or by block_sum
     double cam[6], cam_new[6], R[4][9], Rn[9];
     double gc[6], sic[6], dc[6], ghc[6], gnc[6], s1c[6], s2c[6], shc[6];
     double G[6][6], z[6];
-    double red[4 * 27], tot[27];
+    double red[NW * 27], tot[27];
     double Delta, mu, cost, cost_new, pS[2];
     double gmax, gh2, ghn, c12, s2n, BS[3], gS[2];
     int status, nfev, njev, done, accept;
 };
 
-__device__ __forceinline__ const double* rec_of(double* scratch, int64_t i) { return scratch + (size_t)i * kRec; }
+// A pair's observation records in the scratch block of kRec doubles per
+// observation: AoS (record i at i * kRec) or, SOA, field-major within the pair
+// (field f of record i at f * n + i: a wave's load of one field is 64
+// consecutive doubles).  Passes copy the fields they use into registers.
+template <bool SOA>
+struct Recs {
+    double* base;
+    int n;
+    __device__ __forceinline__ double* at(int i, int f) const {
+        return SOA ? base + (size_t)f * n + i : base + (size_t)i * kRec + f;
+    }
+    template <int LO, int HI>
+    __device__ __forceinline__ void load(int i, double* r) const {
+#pragma unroll
+        for (int f = LO; f < HI; ++f) r[f] = *at(i, f);
+    }
+    template <int LO, int HI>
+    __device__ __forceinline__ void store(int i, const double* r) const {
+#pragma unroll
+        for (int f = LO; f < HI; ++f) *at(i, f) = r[f];
+    }
+};
 
 // residual of one observation at (camera rotation R, c = [rvec, t], X)
 __device__ __forceinline__ void resid(const double* R, const double* c, const double* k, const double* X,
@@ -143,15 +177,16 @@ __device__ __forceinline__ void resid(const double* R, const double* c, const do
     rv = pts[1] - v;
 }
 
-__global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__ cam_io, const double* __restrict__ Kall,
-                                                            double* __restrict__ X, const double* __restrict__ pts2d,
-                                                            const int64_t* __restrict__ off, int64_t n_obs,
-                                                            double ftol, double xtol,
-                                                            double gtol, int max_nfev_arg, double* __restrict__ scratch,
-                                                            double* __restrict__ cost_out, int32_t* __restrict__ nfev_out,
-                                                            int32_t* __restrict__ njev_out,
-                                                            int32_t* __restrict__ status_out) {
-    __shared__ BaState S;
+template <int NT, bool SOA>
+__global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io, const double* __restrict__ Kall,
+                                                    double* __restrict__ X, const double* __restrict__ pts2d,
+                                                    const int64_t* __restrict__ off, int64_t n_obs, double ftol,
+                                                    double xtol, double gtol, int max_nfev_arg,
+                                                    double* __restrict__ scratch, double* __restrict__ cost_out,
+                                                    int32_t* __restrict__ nfev_out, int32_t* __restrict__ njev_out,
+                                                    int32_t* __restrict__ status_out) {
+    constexpr int NW = NT / 64;
+    __shared__ BaState<NW> S;
     const int p = blockIdx.x, tid = threadIdx.x;
     const int64_t o0 = off[p], o1 = off[p + 1];
     if (!(0 <= o0 && o0 <= o1 && o1 <= n_obs && o1 - o0 <= INT_MAX)) {   // malformed offsets: touch nothing
@@ -162,7 +197,7 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
     const double* k = Kall + (size_t)p * 9;
     double* Xp = X + 3 * o0;
     const double* pts = pts2d + 2 * o0;
-    double* rec = scratch + (size_t)o0 * kRec;
+    const Recs<SOA> rec{scratch + (size_t)o0 * kRec, n};
     if (tid < 6) S.cam[tid] = cam_io[(size_t)p * 6 + tid];
     __syncthreads();
     if (n == 0) {
@@ -181,9 +216,10 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
         __syncthreads();
         double acc[13] = {0};   // gc (6), column sums of squares (6), cost
         double gmax = 0.0;
-        for (int i = tid; i < n; i += kBaThreads) {
-            double* r = scratch + (size_t)(o0 + i) * kRec;
+        for (int i = tid; i < n; i += NT) {
+            double r[kRec];
             double f[2];
+            if (!first) rec.template load<20, 23>(i, r);
             fd_obs(&S.R[0][0], S.cam, k, Xp + 3 * i, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
             r[18] = f[0];
             r[19] = f[1];
@@ -202,9 +238,10 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
                 else si = fmax(si, r[20 + c]);
                 r[20 + c] = si;
             }
+            rec.template store<0, 23>(i, r);
         }
-        gmax = block_max(gmax, S.red);
-        block_sum<13>(acc, S.red, S.tot);
+        gmax = block_max<NW>(gmax, S.red);
+        block_sum<NW, 13>(acc, S.red, S.tot);
         if (tid == 0) {
             double gm = gmax;
             for (int c = 0; c < 6; ++c) {
@@ -223,11 +260,12 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
     // Delta = |x0 * scale_inv|
     {
         double acc[1] = {0.0};
-        for (int i = tid; i < n; i += kBaThreads) {
-            const double* r = rec_of(rec, i);
+        for (int i = tid; i < n; i += NT) {
+            double r[kRec];
+            rec.template load<20, 23>(i, r);
             for (int c = 0; c < 3; ++c) { const double t = Xp[3 * i + c] * r[20 + c]; acc[0] += t * t; }
         }
-        block_sum<1>(acc, S.red, S.tot);
+        block_sum<NW, 1>(acc, S.red, S.tot);
         if (tid == 0) {
             double d2 = S.tot[0];
             for (int c = 0; c < 6; ++c) d2 += (S.cam[c] * S.sic[c]) * (S.cam[c] * S.sic[c]);
@@ -250,8 +288,9 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
         // regularize: a = 0.5 |J_h (-g_h)|^2, |g_h|^2 (build_quadratic_1d along -g_h)
         {
             double acc[2] = {0.0, 0.0};
-            for (int i = tid; i < n; i += kBaThreads) {
-                const double* r = rec_of(rec, i);
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<0, 23>(i, r);
                 double vu = 0.0, vv = 0.0;
                 for (int c = 0; c < 6; ++c) { vu -= r[c] * S.dc[c] * S.ghc[c]; vv -= r[9 + c] * S.dc[c] * S.ghc[c]; }
                 for (int c = 0; c < 3; ++c) {
@@ -263,7 +302,7 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
                 }
                 acc[0] += vu * vu + vv * vv;
             }
-            block_sum<2>(acc, S.red, S.tot);
+            block_sum<NW, 2>(acc, S.red, S.tot);
             if (tid == 0) {
                 double gh2 = S.tot[1];
                 for (int c = 0; c < 6; ++c) gh2 += S.ghc[c] * S.ghc[c];
@@ -285,8 +324,9 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
             double acc[27];
 #pragma unroll
             for (int e = 0; e < 27; ++e) acc[e] = 0.0;
-            for (int i = tid; i < n; i += kBaThreads) {
-                const double* r = rec_of(rec, i);
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<0, 23>(i, r);
                 double C[2][6], Pp[2][3];
                 for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
                 for (int c = 0; c < 3; ++c) {
@@ -307,7 +347,7 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
                     for (int b = a; b < 6; ++b) acc[e++] += C[0][a] * Y[0][b] + C[1][a] * Y[1][b];
                 for (int a = 0; a < 6; ++a) acc[21 + a] += C[0][a] * u0 + C[1][a] * u1;
             }
-            block_sum<27>(acc, S.red, S.tot);
+            block_sum<NW, 27>(acc, S.red, S.tot);
             if (tid == 0) {
                 double G[6][6], h[6];
                 int e = 0;
@@ -322,8 +362,9 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
         // gn_h = J_h^T y, y = B^-1 f - B^-1 C z; g_h . gn_h and |gn_h|^2 (Gram-Schmidt of [g_h, gn_h])
         {
             double acc[7] = {0};   // gnc (6), point part of g_h . gn_h
-            for (int i = tid; i < n; i += kBaThreads) {
-                const double* r = rec_of(rec, i);
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<0, 23>(i, r);
                 double C[2][6], Pp[2][3];
                 for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
                 for (int c = 0; c < 3; ++c) {
@@ -346,7 +387,7 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
                     acc[6] += gh * gn;
                 }
             }
-            block_sum<7>(acc, S.red, S.tot);
+            block_sum<NW, 7>(acc, S.red, S.tot);
             if (tid == 0) {
                 const double ghn = sqrt(S.gh2);
                 double dot = S.tot[6];
@@ -388,12 +429,14 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
         };
         {
             double acc[1] = {0.0};
-            for (int i = tid; i < n; i += kBaThreads) {
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<0, 23>(i, r);
                 double s1[3], s2[3];
-                point_vecs(rec_of(rec, i), s1, s2);
+                point_vecs(r, s1, s2);
                 acc[0] += s2[0] * s2[0] + s2[1] * s2[1] + s2[2] * s2[2];
             }
-            block_sum<1>(acc, S.red, S.tot);
+            block_sum<NW, 1>(acc, S.red, S.tot);
             if (tid == 0) {
                 double n2 = S.tot[0];
                 for (int c = 0; c < 6; ++c) n2 += S.s2c[c] * S.s2c[c];
@@ -405,8 +448,9 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
         const double s2n = S.s2n;
         {
             double acc[5] = {0};   // JS1.JS1, JS1.JS2, JS2.JS2, s2 . g_h and s1 . g_h (point parts)
-            for (int i = tid; i < n; i += kBaThreads) {
-                const double* r = rec_of(rec, i);
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<0, 23>(i, r);
                 double s1[3], s2[3];
                 point_vecs(r, s1, s2);
                 double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
@@ -431,7 +475,7 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
                 acc[1] += a0 * b0 + a1 * b1;
                 acc[2] += b0 * b0 + b1 * b1;
             }
-            block_sum<5>(acc, S.red, S.tot);
+            block_sum<NW, 5>(acc, S.red, S.tot);
             if (tid == 0) {
                 double g0 = S.tot[4], g1 = S.tot[3];
                 for (int c = 0; c < 6; ++c) { g0 += S.s1c[c] * S.ghc[c]; g1 += S.s2c[c] * S.ghc[c]; }
@@ -459,8 +503,9 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
             if (S.done) break;
             // step, J_h step, f(x_new): predicted reduction, cost_new, |step_h|, |step|, |x|, finiteness
             double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
-            for (int i = tid; i < n; i += kBaThreads) {
-                double* r = scratch + (size_t)(o0 + i) * kRec;
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<0, 23>(i, r);
                 double s1[3], s2[3];
                 point_vecs(r, s1, s2);
                 double ju = 0, jv = 0;
@@ -480,13 +525,14 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
                     Xn[c] = x + st;
                     r[23 + c] = Xn[c];
                 }
+                rec.template store<23, 26>(i, r);
                 acc[0] += ju * ju + jv * jv;
                 double ru, rv;
                 resid(S.Rn, S.cam_new, k, Xn, pts + 2 * i, ru, rv);
                 acc[2] += ru * ru + rv * rv;
                 if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
             }
-            block_sum<7>(acc, S.red, S.tot);
+            block_sum<NW, 7>(acc, S.red, S.tot);
             if (tid == 0) {
                 double sg = S.tot[1], sh2 = S.tot[3], st2 = S.tot[4], x2 = S.tot[5];
                 for (int c = 0; c < 6; ++c) {
@@ -523,8 +569,9 @@ __global__ __launch_bounds__(kBaThreads) void ba_trf_kernel(double* __restrict__
             if (S.status >= 0 || S.accept == 1) break;
         }
         if (S.accept == 1) {   // x = x_new; J at the new point
-            for (int i = tid; i < n; i += kBaThreads) {
-                const double* r = rec_of(rec, i);
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<23, 26>(i, r);
                 for (int c = 0; c < 3; ++c) Xp[3 * i + c] = r[23 + c];
             }
             if (tid < 6) S.cam[tid] = S.cam_new[tid];
@@ -564,8 +611,26 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
         set_error("sfmhip_ba_solve: scratch allocation failed");
         return SFMHIP_E_HIP;
     }
-    hipLaunchKernelGGL(ba_trf_kernel, dim3(n_pairs), dim3(kBaThreads), 0, st, cam, K, X, pts2d, pair_off, n_obs, ftol,
-                       xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+    // SFMHIP_BA_VARIANT (A/B runs): 0 AoS records, 256 threads; 1 field-major records, 256 threads;
+    // 2 field-major, 512 threads; 3 AoS, 512 threads
+    static const int variant = [] { const char* e = std::getenv("SFMHIP_BA_VARIANT"); return e ? std::atoi(e) : 0; }();
+    switch (variant) {
+        case 1:
+            hipLaunchKernelGGL((ba_trf_kernel<256, true>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
+                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+            break;
+        case 2:
+            hipLaunchKernelGGL((ba_trf_kernel<512, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
+                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+            break;
+        case 3:
+            hipLaunchKernelGGL((ba_trf_kernel<512, false>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
+                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+            break;
+        default:
+            hipLaunchKernelGGL((ba_trf_kernel<256, false>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
+                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+    }
     const int rc = check_launch("ba_trf_kernel");
     (void)hipFreeAsync(scratch, st);
     return rc;
