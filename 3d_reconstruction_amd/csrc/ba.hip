@@ -591,6 +591,408 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     }
 }
 
+// The same iteration with the passes fused (4 per TRF iteration instead of 8):
+//   * the Jacobian pass (the first one and every accepted step; it also moves
+//     X to the accepted point) accumulates, besides J^T f / column norms / cost,
+//     sum Jc^T Jc and the point parts of J_h g_h, so regularize's a = |J_h g_h|^2 / 2
+//     comes out of the reductions: |Jc w + q|^2 = w^T (sum Jc^T Jc) w + 2 w . sum Jc^T q
+//     + sum |q|^2 with w = dc^2 gc;
+//   * ridge (G, h -> z) as before;
+//   * one pass gives gn_h and every product of the 2-D subspace: with a = J_h g_h
+//     and b = J_h gn_h = C gn_c + q (gn_c is that pass's own reduction), sum |b|^2
+//     and sum a . b are expanded over sum C^T C, sum C^T q, sum C^T a, so
+//     B_S = S^T J_h^T J_h S, g_S and |s2| follow from the reductions;
+//   * the trial step(s).
+// Records are field-major per pair (Recs<true>).  Same TRF decisions as the
+// unfused kernel; the expanded sums differ from the direct ones by rounding.
+template <int NW>
+struct BaStateF {
+    double cam[6], cam_new[6], R[4][9], Rn[9];
+    double gc[6], sic[6], dc[6], ghc[6], s1c[6], s2c[6], shc[6];
+    double JtJ[21], z[6];
+    double red[NW * 43], tot[43];
+    double Delta, mu, cost, cost_new, pS[2], aq, gh2;
+    double gmax, ghn, c12, s2n, BS[3], gS[2];
+    int status, nfev, njev, done, accept;
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ cam_io, const double* __restrict__ Kall,
+                                                          double* __restrict__ X, const double* __restrict__ pts2d,
+                                                          const int64_t* __restrict__ off, int64_t n_obs, double ftol,
+                                                          double xtol, double gtol, int max_nfev_arg,
+                                                          double* __restrict__ scratch, double* __restrict__ cost_out,
+                                                          int32_t* __restrict__ nfev_out,
+                                                          int32_t* __restrict__ njev_out,
+                                                          int32_t* __restrict__ status_out) {
+    constexpr int NW = NT / 64;
+    __shared__ BaStateF<NW> S;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int64_t o0 = off[p], o1 = off[p + 1];
+    if (!(0 <= o0 && o0 <= o1 && o1 <= n_obs && o1 - o0 <= INT_MAX)) {   // malformed offsets: touch nothing
+        if (tid == 0) { cost_out[p] = 0.0; nfev_out[p] = 0; njev_out[p] = 0; status_out[p] = -1; }
+        return;
+    }
+    const int n = (int)(o1 - o0);
+    const double* k = Kall + (size_t)p * 9;
+    double* Xp = X + 3 * o0;
+    const double* pts = pts2d + 2 * o0;
+    const Recs<true> rec{scratch + (size_t)o0 * kRec, n};
+    if (tid < 6) S.cam[tid] = cam_io[(size_t)p * 6 + tid];
+    __syncthreads();
+    if (n == 0) {
+        if (tid == 0) { cost_out[p] = 0.0; nfev_out[p] = 0; njev_out[p] = 0; status_out[p] = 1; }
+        return;
+    }
+    const int max_nfev = max_nfev_arg > 0 ? max_nfev_arg : (int)min((int64_t)INT_MAX, 100 * (6 + 3 * (int64_t)n));
+
+    // J, f at the current point (first: x0; moved: the accepted trial point, which it
+    // also writes to X); scale_inv; gc, cost, |g|_inf; sum Jc^T Jc; the regularize sums
+    auto jacobian = [&](bool first, bool moved) {
+        if (tid < 4) {   // R(rvec) and the three perturbed rotations of the FD
+            double q[3] = {S.cam[0], S.cam[1], S.cam[2]};
+            if (tid > 0) q[tid - 1] = q[tid - 1] + fd_step(q[tid - 1]);
+            rodrigues(q, S.R[tid]);
+        }
+        __syncthreads();
+        // gc (6), column sums of squares (6), cost, sum Jc^T Jc (21), sum Jc^T q (6), |q|^2, |g_h point|^2, |x0 s|^2
+        double acc[43];
+#pragma unroll
+        for (int e = 0; e < 43; ++e) acc[e] = 0.0;
+        double gmax = 0.0;
+        for (int i = tid; i < n; i += NT) {
+            double r[kRec];
+            double f[2], Xi[3];
+            if (moved) {
+                rec.template load<23, 26>(i, r);
+                for (int c = 0; c < 3; ++c) { Xi[c] = r[23 + c]; Xp[3 * i + c] = Xi[c]; }
+            } else {
+                for (int c = 0; c < 3; ++c) Xi[c] = Xp[3 * i + c];
+            }
+            if (!first) rec.template load<20, 23>(i, r);
+            fd_obs(&S.R[0][0], S.cam, k, Xi, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
+            r[18] = f[0];
+            r[19] = f[1];
+            acc[12] += f[0] * f[0] + f[1] * f[1];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                acc[c] += r[c] * f[0] + r[9 + c] * f[1];
+                acc[6 + c] += r[c] * r[c] + r[9 + c] * r[9 + c];
+            }
+            int e = 13;
+#pragma unroll
+            for (int a = 0; a < 6; ++a)
+#pragma unroll
+                for (int b = a; b < 6; ++b) acc[e++] += r[a] * r[b] + r[9 + a] * r[9 + b];
+            double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const double gp = r[6 + c] * f[0] + r[15 + c] * f[1];
+                gmax = fmax(gmax, fabs(gp));
+                double si = sqrt(r[6 + c] * r[6 + c] + r[15 + c] * r[15 + c]);
+                if (first) si = si == 0.0 ? 1.0 : si;
+                else si = fmax(si, r[20 + c]);
+                r[20 + c] = si;
+                const double d = 1.0 / si;
+                const double gh = d * gp;                     // g_h, point column c
+                q0 += r[6 + c] * d * gh;                      // (J_h g_h) point part
+                q1 += r[15 + c] * d * gh;
+                acc[41] += gh * gh;
+                if (first) { const double t = Xi[c] * si; acc[42] += t * t; }
+            }
+#pragma unroll
+            for (int c = 0; c < 6; ++c) acc[34 + c] += r[c] * q0 + r[9 + c] * q1;
+            acc[40] += q0 * q0 + q1 * q1;
+            rec.template store<0, 23>(i, r);
+        }
+        gmax = block_max<NW>(gmax, S.red);
+        block_sum<NW, 43>(acc, S.red, S.tot);
+        if (tid == 0) {
+            double gm = gmax;
+            for (int c = 0; c < 6; ++c) {
+                S.gc[c] = S.tot[c];
+                gm = fmax(gm, fabs(S.gc[c]));
+                const double si = sqrt(S.tot[6 + c]);
+                S.sic[c] = first ? (si == 0.0 ? 1.0 : si) : fmax(si, S.sic[c]);
+                S.dc[c] = 1.0 / S.sic[c];
+                S.ghc[c] = S.dc[c] * S.gc[c];
+            }
+            for (int e = 0; e < 21; ++e) S.JtJ[e] = S.tot[13 + e];
+            // |J_h g_h|^2 = w^T (Jc^T Jc) w + 2 w . (Jc^T q) + |q|^2, w = dc * ghc
+            double w[6], a2 = S.tot[40], gh2 = S.tot[41];
+            for (int c = 0; c < 6; ++c) { w[c] = S.dc[c] * S.ghc[c]; gh2 += S.ghc[c] * S.ghc[c]; }
+            int e = 0;
+            for (int a = 0; a < 6; ++a)
+                for (int b = a; b < 6; ++b) {
+                    const double t = w[a] * S.JtJ[e++] * w[b];
+                    a2 += a == b ? t : 2.0 * t;
+                }
+            for (int c = 0; c < 6; ++c) a2 += 2.0 * w[c] * S.tot[34 + c];
+            S.aq = 0.5 * a2;
+            S.gh2 = gh2;
+            S.gmax = gm;
+            S.cost = 0.5 * S.tot[12];
+            if (first) {
+                double d2 = S.tot[42];
+                for (int c = 0; c < 6; ++c) d2 += (S.cam[c] * S.sic[c]) * (S.cam[c] * S.sic[c]);
+                S.Delta = sqrt(d2);
+                if (S.Delta == 0.0) S.Delta = 1.0;
+                S.nfev = 1; S.njev = 1; S.status = -1; S.done = 0;
+            }
+        }
+        __syncthreads();
+    };
+
+    // per observation: the scaled blocks C = Jc dc, Pp = Jp d and (J_h J_h^T + mu)^-1's 2x2 point part
+    struct Blk { double C[2][6], Pp[2][3], d[3], i00, i01, i11; };
+    auto blocks = [&](const double* r, double mu, Blk& B) {
+        for (int c = 0; c < 6; ++c) { B.C[0][c] = r[c] * S.dc[c]; B.C[1][c] = r[9 + c] * S.dc[c]; }
+        for (int c = 0; c < 3; ++c) {
+            B.d[c] = 1.0 / r[20 + c];
+            B.Pp[0][c] = r[6 + c] * B.d[c];
+            B.Pp[1][c] = r[15 + c] * B.d[c];
+        }
+        const double b00 = B.Pp[0][0] * B.Pp[0][0] + B.Pp[0][1] * B.Pp[0][1] + B.Pp[0][2] * B.Pp[0][2] + mu;
+        const double b01 = B.Pp[0][0] * B.Pp[1][0] + B.Pp[0][1] * B.Pp[1][1] + B.Pp[0][2] * B.Pp[1][2];
+        const double b11 = B.Pp[1][0] * B.Pp[1][0] + B.Pp[1][1] * B.Pp[1][1] + B.Pp[1][2] * B.Pp[1][2] + mu;
+        const double idet = 1.0 / (b00 * b11 - b01 * b01);
+        B.i00 = b11 * idet; B.i01 = -b01 * idet; B.i11 = b00 * idet;
+    };
+
+    jacobian(true, false);
+
+    while (true) {
+        __syncthreads();   // every wave has read the previous iteration's S.status / S.done
+        if (tid == 0) {
+            if (S.gmax < gtol) S.status = 1;
+            S.done = S.status >= 0 || S.nfev == max_nfev;
+            // regularize (build_quadratic_1d along -g_h, minimize_quadratic_1d on [0, Delta / |g_h|])
+            const double a = S.aq, b = -S.gh2, to_tr = S.Delta / sqrt(S.gh2);
+            double ag = 0.0;
+            ag = fmin(ag, to_tr * (a * to_tr + b));
+            if (a != 0.0) {
+                const double ext = -0.5 * b / a;
+                if (0.0 < ext && ext < to_tr) ag = fmin(ag, ext * (a * ext + b));
+            }
+            S.mu = -ag / (S.Delta * S.Delta);
+        }
+        __syncthreads();
+        if (S.done) break;
+        const double mu = S.mu;
+        // ridge: G = I + sum C^T B^-1 C, h = sum C^T B^-1 f
+        {
+            double acc[27];
+#pragma unroll
+            for (int e = 0; e < 27; ++e) acc[e] = 0.0;
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<0, 23>(i, r);
+                Blk B;
+                blocks(r, mu, B);
+                const double u0 = B.i00 * r[18] + B.i01 * r[19], u1 = B.i01 * r[18] + B.i11 * r[19];
+                double Y[2][6];
+                for (int c = 0; c < 6; ++c) {
+                    Y[0][c] = B.i00 * B.C[0][c] + B.i01 * B.C[1][c];
+                    Y[1][c] = B.i01 * B.C[0][c] + B.i11 * B.C[1][c];
+                }
+                int e = 0;
+                for (int a = 0; a < 6; ++a)
+                    for (int b = a; b < 6; ++b) acc[e++] += B.C[0][a] * Y[0][b] + B.C[1][a] * Y[1][b];
+                for (int a = 0; a < 6; ++a) acc[21 + a] += B.C[0][a] * u0 + B.C[1][a] * u1;
+            }
+            block_sum<NW, 27>(acc, S.red, S.tot);
+            if (tid == 0) {
+                double G[6][6], h[6];
+                int e = 0;
+                for (int a = 0; a < 6; ++a)
+                    for (int b = a; b < 6; ++b) { G[a][b] = G[b][a] = S.tot[e++] + (a == b ? 1.0 : 0.0); }
+                for (int a = 0; a < 6; ++a) h[a] = S.tot[21 + a];
+                if (!chol6_solve(G, h)) S.status = -2;   // not expected: G = I + PSD
+                for (int a = 0; a < 6; ++a) S.z[a] = h[a];
+            }
+            __syncthreads();
+        }
+        // gn_h = J_h^T y (y = B^-1 (f - C z)) and the 2-D subspace products in one pass
+        {
+            double acc[23];   // gn_c (6), g_h.gn_h pts, |gn_h pts|^2, |a|^2, C^T a (6), a.q, C^T q (6), |q|^2
+#pragma unroll
+            for (int e = 0; e < 23; ++e) acc[e] = 0.0;
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<0, 23>(i, r);
+                Blk B;
+                blocks(r, mu, B);
+                double w0 = r[18], w1 = r[19];
+                for (int c = 0; c < 6; ++c) { w0 -= B.C[0][c] * S.z[c]; w1 -= B.C[1][c] * S.z[c]; }
+                const double y0 = B.i00 * w0 + B.i01 * w1, y1 = B.i01 * w0 + B.i11 * w1;
+                double a0 = 0.0, a1 = 0.0, q0 = 0.0, q1 = 0.0;   // a = J_h g_h, q = Pp gn_p
+                for (int c = 0; c < 6; ++c) {
+                    acc[c] += B.C[0][c] * y0 + B.C[1][c] * y1;
+                    a0 += B.C[0][c] * S.ghc[c];
+                    a1 += B.C[1][c] * S.ghc[c];
+                }
+                for (int c = 0; c < 3; ++c) {
+                    const double gn = B.Pp[0][c] * y0 + B.Pp[1][c] * y1;
+                    const double gh = B.Pp[0][c] * r[18] + B.Pp[1][c] * r[19];
+                    acc[6] += gh * gn;
+                    acc[7] += gn * gn;
+                    a0 += B.Pp[0][c] * gh;
+                    a1 += B.Pp[1][c] * gh;
+                    q0 += B.Pp[0][c] * gn;
+                    q1 += B.Pp[1][c] * gn;
+                }
+                acc[8] += a0 * a0 + a1 * a1;
+                acc[15] += a0 * q0 + a1 * q1;
+                for (int c = 0; c < 6; ++c) {
+                    acc[9 + c] += B.C[0][c] * a0 + B.C[1][c] * a1;
+                    acc[16 + c] += B.C[0][c] * q0 + B.C[1][c] * q1;
+                }
+                acc[22] += q0 * q0 + q1 * q1;
+            }
+            block_sum<NW, 23>(acc, S.red, S.tot);
+            if (tid == 0) {
+                const double ghn = sqrt(S.gh2);
+                double gnc[6], dot = S.tot[6], gn2 = S.tot[7];
+                for (int c = 0; c < 6; ++c) {
+                    gnc[c] = S.tot[c];
+                    dot += S.ghc[c] * gnc[c];
+                    gn2 += gnc[c] * gnc[c];
+                    S.s1c[c] = S.ghc[c] / ghn;
+                }
+                const double c12 = dot / ghn;
+                const double s2sq = gn2 - c12 * c12;   // |gn_h - (s1 . gn_h) s1|^2
+                const double s2n = sqrt(fmax(s2sq, 1e-300));
+                for (int c = 0; c < 6; ++c) S.s2c[c] = (gnc[c] - c12 * S.s1c[c]) / s2n;
+                // sum a.b and |b|^2 with b = C gn_c + q:  C^T C = dc (Jc^T Jc) dc
+                double ab = S.tot[15], bb = S.tot[22];
+                for (int c = 0; c < 6; ++c) { ab += gnc[c] * S.tot[9 + c]; bb += 2.0 * gnc[c] * S.tot[16 + c]; }
+                int e = 0;
+                for (int a = 0; a < 6; ++a)
+                    for (int b = a; b < 6; ++b) {
+                        const double t = gnc[a] * (S.dc[a] * S.JtJ[e++] * S.dc[b]) * gnc[b];
+                        bb += a == b ? t : 2.0 * t;
+                    }
+                const double aa = S.tot[8], rr = c12 / ghn;
+                // JS1 = a / |g_h|, JS2 = (b - c12 a / |g_h|) / |s2|
+                S.BS[0] = aa / S.gh2;
+                S.BS[1] = (ab - rr * aa) / (ghn * s2n);
+                S.BS[2] = (bb - 2.0 * rr * ab + rr * rr * aa) / (s2n * s2n);
+                S.gS[0] = S.gh2 / ghn;
+                S.gS[1] = (dot - c12 * ghn) / s2n;
+                S.ghn = ghn;
+                S.c12 = c12;
+                S.s2n = s2n;
+            }
+            __syncthreads();
+        }
+        const double ghn = S.ghn, c12 = S.c12, s2n = S.s2n;
+        // inner loop: trial steps until the cost decreases
+        if (tid == 0) S.accept = 0;
+        __syncthreads();
+        while (true) {
+            if (tid == 0) {
+                S.done = !(S.nfev < max_nfev);
+                if (!S.done) {
+                    tr_solve_2d(S.BS, S.gS, S.Delta, S.pS);
+                    for (int c = 0; c < 6; ++c) {
+                        S.shc[c] = S.pS[0] * S.s1c[c] + S.pS[1] * S.s2c[c];
+                        S.cam_new[c] = S.cam[c] + S.dc[c] * S.shc[c];
+                    }
+                    rodrigues(S.cam_new, S.Rn);
+                }
+            }
+            __syncthreads();
+            if (S.done) break;
+            double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
+            for (int i = tid; i < n; i += NT) {
+                double r[kRec];
+                rec.template load<0, 23>(i, r);
+                Blk B;
+                blocks(r, mu, B);
+                double w0 = r[18], w1 = r[19];
+                for (int c = 0; c < 6; ++c) { w0 -= B.C[0][c] * S.z[c]; w1 -= B.C[1][c] * S.z[c]; }
+                const double y0 = B.i00 * w0 + B.i01 * w1, y1 = B.i01 * w0 + B.i11 * w1;
+                double ju = 0, jv = 0;
+                for (int c = 0; c < 6; ++c) { ju += B.C[0][c] * S.shc[c]; jv += B.C[1][c] * S.shc[c]; }
+                double Xn[3];
+                for (int c = 0; c < 3; ++c) {
+                    const double gn = B.Pp[0][c] * y0 + B.Pp[1][c] * y1;
+                    const double gh = B.Pp[0][c] * r[18] + B.Pp[1][c] * r[19];
+                    const double s1 = gh / ghn;
+                    const double s2 = gn - c12 * s1;
+                    const double sh = S.pS[0] * s1 + S.pS[1] * (s2 / s2n);
+                    ju += B.Pp[0][c] * sh;
+                    jv += B.Pp[1][c] * sh;
+                    acc[1] += sh * gh;
+                    acc[3] += sh * sh;
+                    const double st = B.d[c] * sh;
+                    acc[4] += st * st;
+                    const double x = Xp[3 * i + c];
+                    acc[5] += x * x;
+                    Xn[c] = x + st;
+                    r[23 + c] = Xn[c];
+                }
+                rec.template store<23, 26>(i, r);
+                acc[0] += ju * ju + jv * jv;
+                double ru, rv;
+                resid(S.Rn, S.cam_new, k, Xn, pts + 2 * i, ru, rv);
+                acc[2] += ru * ru + rv * rv;
+                if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
+            }
+            block_sum<NW, 7>(acc, S.red, S.tot);
+            if (tid == 0) {
+                double sg = S.tot[1], sh2 = S.tot[3], st2 = S.tot[4], x2 = S.tot[5];
+                for (int c = 0; c < 6; ++c) {
+                    sg += S.shc[c] * S.ghc[c];
+                    sh2 += S.shc[c] * S.shc[c];
+                    st2 += (S.dc[c] * S.shc[c]) * (S.dc[c] * S.shc[c]);
+                    x2 += S.cam[c] * S.cam[c];
+                }
+                const double predicted = -(0.5 * S.tot[0] + sg);
+                S.nfev += 1;
+                const double sh_norm = sqrt(sh2);
+                if (S.tot[6] > 0.0) {   // non-finite residuals: shrink and retry
+                    S.Delta = 0.25 * sh_norm;
+                    S.accept = -1;
+                } else {
+                    S.cost_new = 0.5 * S.tot[2];
+                    const double actual = S.cost - S.cost_new;
+                    double ratio;
+                    if (predicted > 0.0) ratio = actual / predicted;
+                    else if (predicted == 0.0 && actual == 0.0) ratio = 1.0;
+                    else ratio = 0.0;
+                    double Dn = S.Delta;
+                    if (ratio < 0.25) Dn = 0.25 * sh_norm;
+                    else if (ratio > 0.75 && sh_norm > 0.95 * S.Delta) Dn = S.Delta * 2.0;
+                    const double step_norm = sqrt(st2), x_norm = sqrt(x2);
+                    const bool fok = actual < ftol * S.cost && ratio > 0.25;
+                    const bool xok = step_norm < xtol * (xtol + x_norm);
+                    S.status = (fok && xok) ? 4 : fok ? 2 : xok ? 3 : -1;
+                    S.accept = actual > 0.0 ? 1 : 0;
+                    if (S.status < 0) S.Delta = Dn;
+                }
+            }
+            __syncthreads();
+            if (S.status >= 0 || S.accept == 1) break;
+        }
+        if (S.accept == 1) {   // x = x_new (moved by the Jacobian pass); J at the new point
+            if (tid < 6) S.cam[tid] = S.cam_new[tid];
+            __syncthreads();
+            jacobian(false, true);
+            if (tid == 0) { S.njev += 1; }
+            __syncthreads();
+        }
+        if (S.done) break;
+    }
+    if (tid < 6) cam_io[(size_t)p * 6 + tid] = S.cam[tid];
+    if (tid == 0) {
+        cost_out[p] = S.cost;
+        nfev_out[p] = S.nfev;
+        njev_out[p] = S.njev;
+        status_out[p] = S.status < 0 ? 0 : S.status;
+    }
+}
+
 }  // namespace
 }  // namespace sfmhip
 
@@ -621,6 +1023,14 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
             break;
         case 2:
             hipLaunchKernelGGL((ba_trf_kernel<512, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
+                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+            break;
+        case 4:
+            hipLaunchKernelGGL((ba_trf_fused_kernel<256>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
+                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+            break;
+        case 5:
+            hipLaunchKernelGGL((ba_trf_fused_kernel<512>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
                                n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
             break;
         case 3:
