@@ -168,6 +168,22 @@ struct Recs {
     }
 };
 
+// for i = tid, tid + NT, ... < n: body(i, r) with r[LO, HI) = record i, the next
+// record's loads issued before the current one's arithmetic (one record ahead)
+template <int NT, int LO, int HI, bool SOA, typename F>
+__device__ __forceinline__ void stream_recs(const Recs<SOA>& rec, int n, F&& body) {
+    double nx[kRec];
+    int i = threadIdx.x;
+    if (i < n) rec.template load<LO, HI>(i, nx);
+    for (; i < n; i += NT) {
+        double r[kRec];
+#pragma unroll
+        for (int f = LO; f < HI; ++f) r[f] = nx[f];
+        if (i + NT < n) rec.template load<LO, HI>(i + NT, nx);
+        body(i, r);
+    }
+}
+
 // residual of one observation at (camera rotation R, c = [rvec, t], X)
 __device__ __forceinline__ void resid(const double* R, const double* c, const double* k, const double* X,
                                       const double* pts, double& ru, double& rv) {
@@ -784,9 +800,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
             double acc[27];
 #pragma unroll
             for (int e = 0; e < 27; ++e) acc[e] = 0.0;
-            for (int i = tid; i < n; i += NT) {
-                double r[kRec];
-                rec.template load<0, 23>(i, r);
+            stream_recs<NT, 0, 23>(rec, n, [&](int i, const double* r) {
                 Blk B;
                 blocks(r, mu, B);
                 const double u0 = B.i00 * r[18] + B.i01 * r[19], u1 = B.i01 * r[18] + B.i11 * r[19];
@@ -799,7 +813,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 for (int a = 0; a < 6; ++a)
                     for (int b = a; b < 6; ++b) acc[e++] += B.C[0][a] * Y[0][b] + B.C[1][a] * Y[1][b];
                 for (int a = 0; a < 6; ++a) acc[21 + a] += B.C[0][a] * u0 + B.C[1][a] * u1;
-            }
+            });
             block_sum<NW, 27>(acc, S.red, S.tot);
             if (tid == 0) {
                 double G[6][6], h[6];
@@ -817,9 +831,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
             double acc[23];   // gn_c (6), g_h.gn_h pts, |gn_h pts|^2, |a|^2, C^T a (6), a.q, C^T q (6), |q|^2
 #pragma unroll
             for (int e = 0; e < 23; ++e) acc[e] = 0.0;
-            for (int i = tid; i < n; i += NT) {
-                double r[kRec];
-                rec.template load<0, 23>(i, r);
+            stream_recs<NT, 0, 23>(rec, n, [&](int i, const double* r) {
                 Blk B;
                 blocks(r, mu, B);
                 double w0 = r[18], w1 = r[19];
@@ -848,7 +860,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                     acc[16 + c] += B.C[0][c] * q0 + B.C[1][c] * q1;
                 }
                 acc[22] += q0 * q0 + q1 * q1;
-            }
+            });
             block_sum<NW, 23>(acc, S.red, S.tot);
             if (tid == 0) {
                 const double ghn = sqrt(S.gh2);
@@ -904,9 +916,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
             __syncthreads();
             if (S.done) break;
             double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
-            for (int i = tid; i < n; i += NT) {
-                double r[kRec];
-                rec.template load<0, 23>(i, r);
+            stream_recs<NT, 0, 23>(rec, n, [&](int i, const double* r) {
                 Blk B;
                 blocks(r, mu, B);
                 double w0 = r[18], w1 = r[19];
@@ -915,6 +925,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 double ju = 0, jv = 0;
                 for (int c = 0; c < 6; ++c) { ju += B.C[0][c] * S.shc[c]; jv += B.C[1][c] * S.shc[c]; }
                 double Xn[3];
+                double xs[kRec];
                 for (int c = 0; c < 3; ++c) {
                     const double gn = B.Pp[0][c] * y0 + B.Pp[1][c] * y1;
                     const double gh = B.Pp[0][c] * r[18] + B.Pp[1][c] * r[19];
@@ -930,15 +941,15 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                     const double x = Xp[3 * i + c];
                     acc[5] += x * x;
                     Xn[c] = x + st;
-                    r[23 + c] = Xn[c];
+                    xs[23 + c] = Xn[c];
                 }
-                rec.template store<23, 26>(i, r);
+                rec.template store<23, 26>(i, xs);
                 acc[0] += ju * ju + jv * jv;
                 double ru, rv;
                 resid(S.Rn, S.cam_new, k, Xn, pts + 2 * i, ru, rv);
                 acc[2] += ru * ru + rv * rv;
                 if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
-            }
+            });
             block_sum<NW, 7>(acc, S.red, S.tot);
             if (tid == 0) {
                 double sg = S.tot[1], sh2 = S.tot[3], st2 = S.tot[4], x2 = S.tot[5];
