@@ -134,6 +134,49 @@ __device__ void tr_solve_2d(const double B[3] /* b00, b01, b11 */, const double 
     p[1] = Delta * sin(best);
 }
 
+// tr_solve_2d on a whole wave (every lane returns the same p): the interior point as
+// tr_solve_2d; on the circle, lane l evaluates angle 2 pi l / 64 (the serial scan's
+// points), the lowest-index minimum wins as in the serial loop, then the same Newton
+// refinement on every lane.
+__device__ void tr_solve_2d_wave(const double B[3], const double g[2], double Delta, double p[2]) {
+    const double b00 = B[0], b01 = B[1], b11 = B[2];
+    if (b00 > 0.0) {
+        const double l00 = sqrt(b00), l10 = b01 / l00, s = b11 - l10 * l10;
+        if (s > 0.0) {
+            const double l11 = sqrt(s);
+            const double y0 = g[0] / l00, y1 = (g[1] - l10 * y0) / l11;
+            const double x1 = y1 / l11, x0 = (y0 - l10 * x1) / l00;
+            if (x0 * x0 + x1 * x1 <= Delta * Delta) { p[0] = -x0; p[1] = -x1; return; }
+        }
+    }
+    auto val = [&](double ph) {
+        const double c = cos(ph), s = sin(ph);
+        return 0.5 * Delta * Delta * (b00 * c * c + 2.0 * b01 * c * s + b11 * s * s) + Delta * (g[0] * c + g[1] * s);
+    };
+    const int lane = threadIdx.x & 63;
+    constexpr int kScan = 64;
+    double bv = val(lane == 0 ? 0.0 : 6.283185307179586 * lane / kScan);
+    int bi = lane;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {   // (value, index) min, lowest index on ties
+        const double ov = __shfl_xor(bv, off);
+        const int oi = __shfl_xor(bi, off);
+        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    double best = bi == 0 ? 0.0 : 6.283185307179586 * bi / kScan;
+    for (int it = 0; it < 40; ++it) {   // Newton on dq/dphi
+        const double c = cos(best), s = sin(best);
+        const double d1 = Delta * Delta * ((b11 - b00) * c * s + b01 * (c * c - s * s)) + Delta * (g[1] * c - g[0] * s);
+        const double d2 = Delta * Delta * ((b11 - b00) * (c * c - s * s) - 4.0 * b01 * c * s) - Delta * (g[0] * c + g[1] * s);
+        if (!(d2 > 0.0)) break;
+        const double step = d1 / d2;
+        best -= step;
+        if (fabs(step) < 1e-16) break;
+    }
+    p[0] = Delta * cos(best);
+    p[1] = Delta * sin(best);
+}
+
 template <int NW>
 struct BaState {   // LDS: the iteration's scalars, written by thread 0 or by block_sum
     double cam[6], cam_new[6], R[4][9], Rn[9];
@@ -619,6 +662,8 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
 //     and sum a . b are expanded over sum C^T C, sum C^T q, sum C^T a, so
 //     B_S = S^T J_h^T J_h S, g_S and |s2| follow from the reductions;
 //   * the trial step(s).
+// The trust-region subproblem runs on wave 0 (tr_solve_2d_wave: the circle scan's
+// 64 angles one per lane).
 // Records are field-major per pair (Recs<true>).  Same TRF decisions as the
 // unfused kernel; the expanded sums differ from the direct ones by rounding.
 template <int NW>
@@ -902,15 +947,22 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
         if (tid == 0) S.accept = 0;
         __syncthreads();
         while (true) {
-            if (tid == 0) {
-                S.done = !(S.nfev < max_nfev);
-                if (!S.done) {
-                    tr_solve_2d(S.BS, S.gS, S.Delta, S.pS);
-                    for (int c = 0; c < 6; ++c) {
-                        S.shc[c] = S.pS[0] * S.s1c[c] + S.pS[1] * S.s2c[c];
-                        S.cam_new[c] = S.cam[c] + S.dc[c] * S.shc[c];
+            if (tid < 64) {   // wave 0: the 2-D subproblem (uniform: every lane computes the same p)
+                if (!(S.nfev < max_nfev)) {
+                    if (tid == 0) S.done = 1;
+                } else {
+                    double pS[2];
+                    tr_solve_2d_wave(S.BS, S.gS, S.Delta, pS);
+                    if (tid == 0) {
+                        S.done = 0;
+                        S.pS[0] = pS[0];
+                        S.pS[1] = pS[1];
+                        for (int c = 0; c < 6; ++c) {
+                            S.shc[c] = S.pS[0] * S.s1c[c] + S.pS[1] * S.s2c[c];
+                            S.cam_new[c] = S.cam[c] + S.dc[c] * S.shc[c];
+                        }
+                        rodrigues(S.cam_new, S.Rn);
                     }
-                    rodrigues(S.cam_new, S.Rn);
                 }
             }
             __syncthreads();
