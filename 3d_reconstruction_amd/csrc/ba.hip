@@ -24,6 +24,25 @@
 namespace sfmhip {
 namespace {
 
+#ifdef SFMHIP_BA_PROF
+// phase timing of the fused kernel (thread 0, wall clock at 100 MHz), a tool-only build
+// (make EXTRA=-DSFMHIP_BA_PROF; tools/ba_phase_prof.py): never in the product library
+constexpr int kProfPhases = 10;
+__device__ unsigned long long g_ba_prof[4096 * kProfPhases];
+#define BA_MARK(k)                                                   \
+    do {                                                             \
+        if (threadIdx.x == 0) {                                      \
+            const unsigned long long t_ = wall_clock64();            \
+            prof_acc[k] += t_ - prof_t;                              \
+            prof_t = t_;                                             \
+        }                                                            \
+    } while (0)
+#else
+#define BA_MARK(k) \
+    do {           \
+    } while (0)
+#endif
+
 constexpr int kRec = 26;   // per observation: J (18: u row, v row), f (2), scale_inv of the point (3), X_new (3)
 
 // sum of K doubles over the workgroup (NW waves); every thread receives the totals in out[]
@@ -706,6 +725,9 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
         return;
     }
     const int max_nfev = max_nfev_arg > 0 ? max_nfev_arg : (int)min((int64_t)INT_MAX, 100 * (6 + 3 * (int64_t)n));
+#ifdef SFMHIP_BA_PROF
+    unsigned long long prof_acc[kProfPhases] = {}, prof_t = wall_clock64();
+#endif
 
     // J, f at the current point (first: x0; moved: the accepted trial point, which it
     // also writes to X); scale_inv; gc, cost, |g|_inf; sum Jc^T Jc; the regularize sums
@@ -821,6 +843,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
     };
 
     jacobian(true, false);
+    BA_MARK(0);
 
     while (true) {
         __syncthreads();   // every wave has read the previous iteration's S.status / S.done
@@ -838,6 +861,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
             S.mu = -ag / (S.Delta * S.Delta);
         }
         __syncthreads();
+        BA_MARK(1);
         if (S.done) break;
         const double mu = S.mu;
         // ridge: G = I + sum C^T B^-1 C, h = sum C^T B^-1 f
@@ -860,6 +884,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 for (int a = 0; a < 6; ++a) acc[21 + a] += B.C[0][a] * u0 + B.C[1][a] * u1;
             });
             block_sum<NW, 27>(acc, S.red, S.tot);
+            BA_MARK(2);
             if (tid == 0) {
                 double G[6][6], h[6];
                 int e = 0;
@@ -870,6 +895,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 for (int a = 0; a < 6; ++a) S.z[a] = h[a];
             }
             __syncthreads();
+            BA_MARK(3);
         }
         // gn_h = J_h^T y (y = B^-1 (f - C z)) and the 2-D subspace products in one pass
         {
@@ -907,6 +933,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 acc[22] += q0 * q0 + q1 * q1;
             });
             block_sum<NW, 23>(acc, S.red, S.tot);
+            BA_MARK(4);
             if (tid == 0) {
                 const double ghn = sqrt(S.gh2);
                 double gnc[6], dot = S.tot[6], gn2 = S.tot[7];
@@ -941,6 +968,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 S.s2n = s2n;
             }
             __syncthreads();
+            BA_MARK(5);
         }
         const double ghn = S.ghn, c12 = S.c12, s2n = S.s2n;
         // inner loop: trial steps until the cost decreases
@@ -966,6 +994,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 }
             }
             __syncthreads();
+            BA_MARK(6);
             if (S.done) break;
             double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
             stream_recs<NT, 0, 23>(rec, n, [&](int i, const double* r) {
@@ -1003,6 +1032,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
             });
             block_sum<NW, 7>(acc, S.red, S.tot);
+            BA_MARK(7);
             if (tid == 0) {
                 double sg = S.tot[1], sh2 = S.tot[3], st2 = S.tot[4], x2 = S.tot[5];
                 for (int c = 0; c < 6; ++c) {
@@ -1036,6 +1066,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 }
             }
             __syncthreads();
+            BA_MARK(8);
             if (S.status >= 0 || S.accept == 1) break;
         }
         if (S.accept == 1) {   // x = x_new (moved by the Jacobian pass); J at the new point
@@ -1044,9 +1075,14 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
             jacobian(false, true);
             if (tid == 0) { S.njev += 1; }
             __syncthreads();
+            BA_MARK(0);
         }
         if (S.done) break;
     }
+#ifdef SFMHIP_BA_PROF
+    if (tid == 0 && p < 4096)
+        for (int k = 0; k < kProfPhases; ++k) g_ba_prof[p * kProfPhases + k] = prof_acc[k];
+#endif
     if (tid < 6) cam_io[(size_t)p * 6 + tid] = S.cam[tid];
     if (tid == 0) {
         cost_out[p] = S.cost;
@@ -1108,3 +1144,12 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
     (void)hipFreeAsync(scratch, st);
     return rc;
 }
+
+#ifdef SFMHIP_BA_PROF
+// tool-only build: the per-pair phase times of the last fused-kernel launch (wall-clock ticks)
+extern "C" int sfmhip_ba_prof_read(unsigned long long* host, int n_pairs) {
+    const int n = std::min(n_pairs, 4096) * kProfPhases;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ba_prof), (size_t)n * sizeof(unsigned long long)) == hipSuccess
+               ? 0 : -1;
+}
+#endif

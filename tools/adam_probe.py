@@ -4,10 +4,14 @@ per fresh process (python tools/adam_probe.py MODE):
   after   after the bench's C3 match + C5 TSDF + render/vq buffers were made and freed
   trim    as 'after', then sfmhip_scratch_trim(0) before the trainer
   copy    as 'after', plus a plain torch copy over the trainer's buffers (placement, not kernel)
+  warm    fresh, then ~1.5 s of back-to-back HBM copies right before the timed steps (clock ramp)
+  sleep   as 'after', then 3 s of GPU idle before the timed steps
+  iters   fresh, 200 timed steps instead of 10: does the time drift down as the process runs?
 Prints the Adam kernel time (HIP events, median of 10) and a copy bandwidth."""
 import importlib
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -44,7 +48,7 @@ def churn():
     torch.cuda.empty_cache()
 
 
-if mode != "fresh":
+if mode in ("after", "trim", "copy", "sleep"):
     churn()
 if mode == "trim":
     sfm.lib.sfmhip_scratch_trim(0)
@@ -61,8 +65,20 @@ mid = (t[:, :-1] + t[:, 1:]) / 2
 z = (torch.cat([t[:, :1], mid], 1) + (torch.cat([mid, t[:, -1:]], 1) - torch.cat([t[:, :1], mid], 1))
      * torch.rand((B, S), generator=g, device=dev)).contiguous()
 gt = torch.rand((B, 3), generator=g, device=dev)
+if mode == "warm":
+    wa = torch.empty(256 << 20, device=dev)
+    wb = torch.empty_like(wa)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 1.5:
+        for _ in range(20):
+            wb.copy_(wa)
+        torch.cuda.synchronize()
+    del wa, wb
+if mode == "sleep":
+    torch.cuda.synchronize()
+    time.sleep(3.0)
 ad = []
-for k in range(12):
+for k in range(202 if mode == "iters" else 12):
     tr._backward(ro, rd, gt, z)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -70,6 +86,8 @@ for k in range(12):
     e1.record()
     torch.cuda.synchronize()
     ad.append(e0.elapsed_time(e1))
+if mode == "iters":
+    print("iters: first 20", [round(a, 2) for a in ad[:20]], "last 20", [round(a, 2) for a in ad[-20:]], flush=True)
 ad = sorted(ad[2:])
 cp = []
 if mode == "copy":

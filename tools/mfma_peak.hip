@@ -2,7 +2,10 @@
 // random register operands, with and without the matcher's 3-op epilogue per
 // output element (no LDS, no global traffic in the loop).  Gives the practical
 // ceiling (clock under load) the match kernel is compared against.
+// KS = MFMA k-steps per epilogue: d = 256 (C3) is 8 steps of 32x32x32 or 4 of
+// 16x16x64; d = 128 (C2) half that, so the epilogue weighs twice as much.
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/mfma_peak tools/mfma_peak.hip
+// Run:   tools/mfma_peak ITERS MODES   (MODES 1: random operands only)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -10,6 +13,7 @@
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ int med3i(int a, int b, int c) {
     int r;
@@ -17,7 +21,7 @@ __device__ __forceinline__ int med3i(int a, int b, int c) {
     return r;
 }
 
-template <bool EPI>
+template <bool EPI, int KS>
 __global__ __launch_bounds__(256, 2) void kern(const int* __restrict__ seed, int iters, int* out) {
     const int lane = threadIdx.x & 63;
     i32x4 a[8], b[2][8];
@@ -32,7 +36,7 @@ __global__ __launch_bounds__(256, 2) void kern(const int* __restrict__ seed, int
     for (int it = 0; it < iters; ++it) {
         i32x16 acc0 = {0}, acc1 = {0};
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < KS; ++k) {
             acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[k], b[0][k], acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[k], b[1][k], acc1, 0, 0, 0);
         }
@@ -53,6 +57,43 @@ __global__ __launch_bounds__(256, 2) void kern(const int* __restrict__ seed, int
         kv += 1;
     }
     out[blockIdx.x * blockDim.x + threadIdx.x] = t1a + t2a + t1b + t2b;
+}
+
+// the matcher's default shape: v_mfma_i32_16x16x64_i8, 4 output tiles per wave
+// (4 independent chains), KS k-steps of 64 per epilogue (4: d = 256, 2: d = 128)
+template <bool EPI, int KS>
+__global__ __launch_bounds__(256, 2) void kern16(const int* __restrict__ seed, int iters, int* out) {
+    const int lane = threadIdx.x & 63;
+    i32x4 a[4], b[4][4];
+    for (int k = 0; k < 4; ++k)
+        for (int e = 0; e < 4; ++e) {
+            a[k][e] = seed[(blockIdx.x * 97 + lane * 13 + k * 7 + e) & 4095];
+            for (int t = 0; t < 4; ++t) b[t][k][e] = seed[(blockIdx.x * 31 + lane * 5 + k * 11 + e * 3 + t * 17) & 4095];
+        }
+    int t1[4] = {INT_MIN, INT_MIN, INT_MIN, INT_MIN}, t2[4] = {INT_MIN, INT_MIN, INT_MIN, INT_MIN};
+    int kv = seed[lane];
+    for (int it = 0; it < iters; ++it) {
+        i32x4 acc[4] = {{0}, {0}, {0}, {0}};
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[k], b[t][k], acc[t], 0, 0, 0);
+        if (EPI) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int ka = acc[t][q] * 256 + kv;
+                    t2[t] = med3i(t2[t], ka, t1[t]);
+                    t1[t] = max(t1[t], ka);
+                }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) t1[t] ^= acc[t][lane & 3];
+        }
+        kv += 1;
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = t1[0] + t2[0] + t1[1] + t2[1] + t1[2] + t2[2] + t1[3] + t2[3];
 }
 
 int main(int argc, char** argv) {
@@ -84,21 +125,36 @@ int main(int argc, char** argv) {
             h[i] = (int)w;
         }
         hipMemcpy(seed, h, sizeof(h), hipMemcpyHostToDevice);
+        // (shape, d): ops per launch = blocks x 4 waves x iters x (MFMAs per iter) x ops per MFMA
+        struct Cfg { const char* name; int id; double mfma_per_iter, ops_per_mfma; };
+        const Cfg cfgs[4] = {{"32x32x32 d=256", 0, 16, 65536.0}, {"32x32x32 d=128", 1, 8, 65536.0},
+                             {"16x16x64 d=256", 2, 16, 32768.0}, {"16x16x64 d=128", 3, 8, 32768.0}};
+        for (const Cfg& c : cfgs)
         for (int epi = 0; epi < 2; ++epi) {
             hipEvent_t e0, e1;
             hipEventCreate(&e0);
             hipEventCreate(&e1);
             for (int rep = 0; rep < 3; ++rep) {
                 hipEventRecord(e0);
-                if (epi) hipLaunchKernelGGL(kern<true>, dim3(blocks), dim3(256), 0, 0, seed, iters, out);
-                else hipLaunchKernelGGL(kern<false>, dim3(blocks), dim3(256), 0, 0, seed, iters, out);
+#define L(K) hipLaunchKernelGGL(K, dim3(blocks), dim3(256), 0, 0, seed, iters, out)
+                switch (c.id * 2 + epi) {
+                    case 0: L((kern<false, 8>)); break;
+                    case 1: L((kern<true, 8>)); break;
+                    case 2: L((kern<false, 4>)); break;
+                    case 3: L((kern<true, 4>)); break;
+                    case 4: L((kern16<false, 4>)); break;
+                    case 5: L((kern16<true, 4>)); break;
+                    case 6: L((kern16<false, 2>)); break;
+                    default: L((kern16<true, 2>)); break;
+                }
+#undef L
                 hipEventRecord(e1);
                 hipEventSynchronize(e1);
                 float ms;
                 hipEventElapsedTime(&ms, e0, e1);
-                const double ops = (double)blocks * 4 * iters * 16 * 65536.0;
+                const double ops = (double)blocks * 4 * iters * c.mfma_per_iter * c.ops_per_mfma;
                 if (rep == 2)
-                    printf("%s operands, %s epilogue: %.2f ms  %.0f TOPS (%.1f%% of 5000)\n", names[zero],
+                    printf("%s operands, %s, %s epilogue: %.2f ms  %.0f TOPS (%.1f%% of 5000)\n", names[zero], c.name,
                            epi ? "with" : "no", ms, ops / ms / 1e9, ops / ms / 1e9 / 50.0);
             }
         }
