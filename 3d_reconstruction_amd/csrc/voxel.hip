@@ -312,13 +312,18 @@ __device__ __forceinline__ void sh_colour(const float* k, float x, float y, floa
     }
 }
 
+// order (optional): wave w renders ray order[w] (rays sorted by where they cross the
+// grid, render_order below); rgb stays indexed by the caller's ray, so the result
+// is the same bits in any order.
 __global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ gvm, int D, int H, int W,
                                                      Bounds B, int mode, const float* __restrict__ ro,
                                                      const float* __restrict__ rd, const float* __restrict__ zv,
-                                                     int64_t nrays, int S, float* __restrict__ rgb) {
+                                                     int64_t nrays, int S, float* __restrict__ rgb,
+                                                     const unsigned* __restrict__ order) {
     const int lane = threadIdx.x & 63;
-    const int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (ray >= nrays) return;  // wave-uniform
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= nrays) return;  // wave-uniform
+    const int64_t ray = order ? (int64_t)order[w] : w;
     const float o[3] = {ro[3 * ray], ro[3 * ray + 1], ro[3 * ray + 2]};
     const float d[3] = {rd[3 * ray], rd[3 * ray + 1], rd[3 * ray + 2]};
     const float* z = zv + (size_t)ray * S;
@@ -1103,8 +1108,14 @@ __global__ __launch_bounds__(256) void tsdf_order_kernel(int nslots, int W, int 
     }
 }
 
-// W may take k more exact +1 steps with T = 1 fixed: an integer in [0, 2^24 - 512]
-__device__ __forceinline__ bool w_runs(float w) { return w >= 0.f && w <= 0x1p24f - 512.f && w == truncf(w); }
+// W may take k more exact +1 steps with T = 1 fixed when it is an integer in [0, 2^24 - 512].
+// Updates only add 1 to W (general or division-free; W + 1 is exact below 2^24), at most
+// kTsdfMaxFrames = 512 per launch, so a W that starts the launch an integer in
+// [0, 2^24 - 1024] stays in that range for every frame: tested once per voxel instead of
+// per projected frame.  (A lane outside the range takes the general update, which gives
+// the same bits.)
+static_assert(kTsdfMaxFrames <= 512, "w_runs_launch assumes at most 512 updates per launch");
+__device__ __forceinline__ bool w_runs_launch(float w) { return w >= 0.f && w <= 0x1p24f - 1024.f && w == truncf(w); }
 
 // One workgroup = one 8x8x8 tile; every frame of the launch is fused with the
 // tile's (T, W) in registers.  The (tile, frame) masks of the cull pass drive a
@@ -1155,6 +1166,7 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
     f2 wv = {Wt[idx], two ? Wt[idx + W] : 0.f};
     // lanes whose stored (T, W) lie outside the fast division's range divide exactly throughout
     const bool wild = !(tame(tv.x, wv.x) && tame(tv.y, wv.y));
+    const bool wi0 = w_runs_launch(wv.x), wi1 = w_runs_launch(wv.y);
     const size_t frame = (size_t)Hd * Wd;
     const int nbytes = (int)(frame * 4);   // host-checked < 2^31
     const int Wd4 = Wd * 4;                 // < 2^24: exact in v_mul_u32_u24
@@ -1232,8 +1244,8 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
             const bool g1 = p.ok1 && p.dep.y > 0.f && !(sdf.y < -trunc);
             const f2 sc = sdf * f2s(inv_trunc);
             const f2 ts = {fminf(1.0f, sc.x), fminf(1.0f, sc.y)};
-            const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && w_runs(wv.x));
-            const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && w_runs(wv.y));
+            const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && wi0);
+            const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && wi1);
             if (easy && __builtin_amdgcn_ballot_w64(!(easy0 && easy1)) == 0) {
                 wv.x = g0 ? wv.x + 1.f : wv.x;
                 wv.y = g1 ? wv.y + 1.f : wv.y;
@@ -1242,7 +1254,7 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
             }
         };
         auto free_run = [&](int k) {
-            const bool ones = tv.x == 1.f && tv.y == 1.f && w_runs(wv.x) && w_runs(wv.y);
+            const bool ones = tv.x == 1.f && tv.y == 1.f && wi0 && wi1;
             if (free_ts == 1.f && __builtin_amdgcn_ballot_w64(!ones) == 0) {
                 wv = wv + f2s((float)k);
             } else {
@@ -1290,7 +1302,7 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
                 const unsigned run = todo & (full ? (full & (0u - full)) - 1u : ~0u);
                 todo &= ~run;
                 const int k = __builtin_popcount(run);
-                const bool ones = tv.x == 1.f && tv.y == 1.f && w_runs(wv.x) && w_runs(wv.y);
+                const bool ones = tv.x == 1.f && tv.y == 1.f && wi0 && wi1;
                 if (free_ts == 1.f && __builtin_amdgcn_ballot_w64(!ones) == 0) {
                     wv = wv + f2s((float)k);
                 } else {
@@ -1353,8 +1365,8 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
             const f2 ts = {fr0 ? free_ts : fminf(1.0f, sc.x), fr1 ? free_ts : fminf(1.0f, sc.y)};
             // every updating voxel of the wave has tsdf = 1, T = 1 and an integer W: each
             // update is (1 W + 1)/(W + 1) = 1 and W + 1, exactly (no division)
-            const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && w_runs(wv.x));
-            const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && w_runs(wv.y));
+            const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && wi0);
+            const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && wi1);
             if (easy && __builtin_amdgcn_ballot_w64(!(easy0 && easy1)) == 0) {
                 wv.x = g0 ? wv.x + 1.f : wv.x;
                 wv.y = g1 ? wv.y + 1.f : wv.y;
@@ -1790,15 +1802,156 @@ extern "C" int sfmhip_grid_to_voxel_major(const float* grid, int C, int D, int H
     return check_launch("to_vm_kernel");
 }
 
+// ---------------------------------------------------------------------------
+// Ray order for the renderer: rays whose samples touch the same voxel lines should
+// run close together in time (and on one XCD), so a line fetched for one ray is
+// still in L2 for the next.  Key = Morton code of the cell (2^bits per axis of
+// the bounds) holding the ray's sample sidx; a counting sort over the 2^(3 bits)
+// keys (histogram with ranks, then the scatter, which prefixes the bucket counts itself).
+// Order inside a bucket follows the atomics (arbitrary), which cannot change any ray's
+// colour.
+__device__ __forceinline__ unsigned morton_spread(unsigned v) {   // 10 bits -> every third bit
+    v &= 0x3FFu;
+    v = (v | (v << 16)) & 0x30000FFu;
+    v = (v | (v << 8)) & 0x300F00Fu;
+    v = (v | (v << 4)) & 0x30C30C3u;
+    v = (v | (v << 2)) & 0x9249249u;
+    return v;
+}
+
+// Key of ray i: Morton code of the cell holding its sample sidx.  Ranks inside a bucket
+// come from an LDS histogram per workgroup plus one global atomic per (workgroup,
+// non-empty bucket) that reserves the workgroup's run: the hot buckets of a ray bundle
+// see one global atomic per workgroup instead of one per ray.
+constexpr int kRenderSortMaxBuckets = 4096;   // bits <= 4
+__global__ __launch_bounds__(256) void render_key_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
+                                                         const float* __restrict__ zv, int64_t nrays, int S, int sidx,
+                                                         Bounds B, int bits, unsigned* __restrict__ hist,
+                                                         unsigned* __restrict__ key, unsigned* __restrict__ rank) {
+    __shared__ unsigned cnt[kRenderSortMaxBuckets];
+    const int nb = 1 << (3 * bits);
+    for (int b = threadIdx.x; b < nb; b += 256) cnt[b] = 0u;
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned k = 0u, r = 0u;
+    if (i < nrays) {
+        const float zs = zv[(size_t)i * S + sidx];
+        const float n = (float)(1 << bits);
+        unsigned q[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float p = ro[3 * i + a] + rd[3 * i + a] * zs;
+            const float c = (p - B.mn[a]) / (B.mx[a] - B.mn[a]) * n;   // NaN -> cell 0
+            q[a] = c >= n ? (1u << bits) - 1u : (c > 0.f ? (unsigned)c : 0u);
+        }
+        k = morton_spread(q[0]) | (morton_spread(q[1]) << 1) | (morton_spread(q[2]) << 2);
+        r = atomicAdd(&cnt[k], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += 256) {
+        const unsigned c = cnt[b];
+        cnt[b] = c ? atomicAdd(&hist[b], c) : 0u;   // this workgroup's run inside bucket b
+    }
+    __syncthreads();
+    if (i < nrays) {
+        key[i] = k;
+        rank[i] = cnt[k] + r;
+    }
+}
+
+// order[pos] = ray, pos = (exclusive prefix of the bucket counts, recomputed per
+// workgroup from the L2-resident histogram) + rank; with xchunk > 0 the sorted positions
+// are laid out so that XCD x gets runs of xchunk consecutive 4-ray workgroups (blocks
+// are dealt round-robin over the XCDs)
+__global__ __launch_bounds__(256) void render_scatter_kernel(const unsigned* __restrict__ hist, int nb,
+                                                             const unsigned* __restrict__ key,
+                                                             const unsigned* __restrict__ rank, int64_t nrays,
+                                                             int xchunk, unsigned* __restrict__ order) {
+    __shared__ unsigned base[kRenderSortMaxBuckets];
+    __shared__ unsigned part[256];
+    const int t = threadIdx.x, per = (nb + 255) / 256, a = t * per, e = min(nb, a + per);
+    unsigned sum = 0;
+    for (int j = a; j < e; ++j) sum += hist[j];
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {   // Hillis-Steele over the 256 partial sums
+        const unsigned v = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    unsigned run = part[t] - sum;
+    for (int j = a; j < e; ++j) {
+        base[j] = run;
+        run += hist[j];
+    }
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrays) return;
+    int64_t pos = (int64_t)base[key[i]] + rank[i];
+    if (xchunk > 0) {
+        const int64_t grp = (int64_t)4 * kNumXcd * xchunk;   // rays per full round of runs
+        const int64_t full = nrays / grp * grp;
+        if (pos < full) {   // logical block L -> launch block: L = ((s / c) * 8 + x) * c + s % c
+            const int64_t L = pos >> 2, c = xchunk;
+            const int64_t rn = L / c, s_in = L % c, x = rn % kNumXcd, sq = (rn / kNumXcd) * c + s_in;
+            pos = ((sq * kNumXcd + x) << 2) | (pos & 3);
+        }
+    }
+    order[pos] = (unsigned)i;
+}
+
 extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, const float* bmin,
                                   const float* bmax, int mask_mode, const float* rays_o, const float* rays_d,
                                   const float* z, int64_t B, int S, float* rgb, void* stream) {
     SFMHIP_REQUIRE(grid_vm && bmin && bmax && rays_o && rays_d && z && rgb, "sfmhip_render_rays: null pointer");
     SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && B >= 0 && S >= 1, "sfmhip_render_rays: bad shape");
     SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_render_rays: mask_mode must be 0 or 1");
+    SFMHIP_REQUIRE(B < ((int64_t)1 << 32), "sfmhip_render_rays: more than 2^32 rays");
     if (B == 0) return SFMHIP_OK;
-    hipLaunchKernelGGL(render_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, as_stream(stream), grid_vm, D, H, W,
-                       make_bounds(bmin, bmax), mask_mode, rays_o, rays_d, z, B, S, rgb);
+    hipStream_t st = as_stream(stream);
+    const Bounds bb = make_bounds(bmin, bmax);
+    // ray ordering (SFMHIP_RENDER_SORT=0 off; _BITS cells per axis as a power of two, _SIDX the
+    // sample (default the last), _XCHUNK XCD runs of workgroups): batches below 8192 rays fill
+    // only a fraction of the chip's waves at once and are rendered as given.  Bench workload
+    // (tools/bench_render_order.py, profiles/r3/ab/render_order_r3j.txt): 0.627-0.648 ms as
+    // given, 0.598 ms with this ordering (sort kernels included); keys and cell sizes from
+    // 2^2 to 2^8 per axis, host-sorted, all give the same ~0.58 ms kernel
+    const int sort = env_int("SFMHIP_RENDER_SORT", 1);
+    const int bits = std::min(std::max(env_int("SFMHIP_RENDER_SORT_BITS", 3), 1), 4);
+    const int sidx = std::min(std::max(env_int("SFMHIP_RENDER_SORT_SIDX", S - 1), 0), S - 1);
+    const int xchunk = std::max(env_int("SFMHIP_RENDER_SORT_XCHUNK", 0), 0);
+    unsigned* scratch = nullptr;
+    const int nb = 1 << (3 * bits);
+    if (sort && B >= 8192) {
+        if (scratch_alloc((void**)&scratch, (size_t)(nb + 3 * B) * sizeof(unsigned), st) != hipSuccess) {
+            (void)hipGetLastError();
+            scratch = nullptr;   // render in the given order
+        }
+    }
+    if (scratch) {
+        unsigned *hist = scratch, *key = hist + nb, *rank = key + B, *order = rank + B;
+        int rc = hipMemsetAsync(hist, 0, (size_t)nb * sizeof(unsigned), st) == hipSuccess ? SFMHIP_OK : SFMHIP_E_HIP;
+        if (rc == SFMHIP_OK) {
+            hipLaunchKernelGGL(render_key_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, st, rays_o, rays_d, z, B, S,
+                               sidx, bb, bits, hist, key, rank);
+            rc = check_launch("render_key_kernel");
+        }
+        if (rc == SFMHIP_OK) {
+            hipLaunchKernelGGL(render_scatter_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, st, hist, nb, key, rank, B,
+                               xchunk, order);
+            rc = check_launch("render_scatter_kernel");
+        }
+        if (rc == SFMHIP_OK) {
+            hipLaunchKernelGGL(render_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb, mask_mode,
+                               rays_o, rays_d, z, B, S, rgb, order);
+            rc = check_launch("render_kernel");
+        }
+        (void)hipFreeAsync(scratch, st);
+        return rc;
+    }
+    hipLaunchKernelGGL(render_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb, mask_mode, rays_o,
+                       rays_d, z, B, S, rgb, nullptr);
     return check_launch("render_kernel");
 }
 

@@ -115,6 +115,29 @@ def test_render_long_rays_vs_oracle(sfm, gpu):
                                rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("cfg", [{}, {"SFMHIP_RENDER_SORT_BITS": "1"}, {"SFMHIP_RENDER_SORT_XCHUNK": "4"},
+                                 {"SFMHIP_RENDER_SORT_SIDX": "0", "SFMHIP_RENDER_SORT_BITS": "4"}])
+def test_render_ray_order_bitexact(sfm, gpu, monkeypatch, cfg):
+    """Batches >= 8192 rays are rendered in a device-sorted order (sfmhip_render_rays'
+    Morton key + counting sort, optional XCD runs); every ray's colour must be the same
+    bits as the unsorted launch (SFMHIP_RENDER_SORT=0), incl. a ragged tail and rays
+    that miss the grid.  Reference semantics: plenoxel.py:71-93."""
+    g = torch.Generator(device=gpu).manual_seed(5)
+    N, B, S = 64, 3 * 4096 + 37, 96
+    vg = sfm.VoxelGrid.plenoxel(torch.randn((28, N, N, N), generator=g, device=gpu) * 0.1, 1.5)
+    ro = torch.randn((B, 3), generator=g, device=gpu) * 0.4 + torch.tensor([0.0, 0.0, -3.0], device=gpu)
+    rd = torch.randn((B, 3), generator=g, device=gpu) * 0.3 + torch.tensor([0.0, 0.0, 1.0], device=gpu)
+    rd = rd / rd.norm(dim=1, keepdim=True)
+    z = torch.sort(torch.rand((B, S), generator=g, device=gpu) * 4 + 2, 1).values.contiguous()
+    monkeypatch.setenv("SFMHIP_RENDER_SORT", "0")
+    ref = vg.render(ro, rd, z)
+    monkeypatch.setenv("SFMHIP_RENDER_SORT", "1")
+    for k, v in cfg.items():
+        monkeypatch.setenv(k, v)
+    got = vg.render(ro, rd, z)
+    assert torch.equal(got, ref)
+
+
 def _tsdf_case(R=48, F=12, Hd=96, Wd=128, focal=110.0):
     depth, poses, K = syn.tsdf_scene(F, Hd, Wd, focal=focal, seed=8)
     return R, depth.numpy(), poses.numpy(), K.numpy()

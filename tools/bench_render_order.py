@@ -1,6 +1,8 @@
-"""Render-kernel time vs ray order on bench.py's V2+V4 workload (plenoxel 28x256^3,
-16 x 2048 rays x 192 bins): the launch as given, and the rays permuted (torch argsort,
-outside the timed region) by several spatial keys.  Colours are checked identical per ray."""
+"""Render time vs ray order on bench.py's V2+V4 workload (plenoxel 28x256^3,
+16 x 2048 rays x 192 bins): (1) the library's own ordering off (SFMHIP_RENDER_SORT=0) with
+the rays permuted by torch argsort outside the timed region under several spatial keys;
+(2) sfmhip_render_rays' device-side ordering (sort kernels inside the timed call) under
+its env knobs.  Colours are checked identical per ray."""
 import importlib
 import os
 import sys
@@ -58,9 +60,35 @@ def keys():
     return out
 
 
+os.environ["SFMHIP_RENDER_SORT"] = "0"
 ref = vg.render(ro, rd, z)
 res = {}
+
+
+def timed(o2, d2, z2):
+    ts = []
+    for _ in range(10):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        vg.render(o2, d2, z2)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts))
+
+
+dev_cfgs = {"dev b3": {}, "dev b2": {"BITS": "2"}, "dev b4": {"BITS": "4"}, "dev b3 x2": {"XCHUNK": "2"},
+            "dev b3 x8": {"XCHUNK": "8"}, "dev b3 s0": {"SIDX": "0"}, "dev b3 s191": {"SIDX": "191"}}
 for rep in range(2):
+    for nm, cfg in dev_cfgs.items():
+        os.environ["SFMHIP_RENDER_SORT"] = "1"
+        for k in ("BITS", "XCHUNK", "SIDX"):
+            os.environ.pop("SFMHIP_RENDER_SORT_" + k, None)
+        for k, v in cfg.items():
+            os.environ["SFMHIP_RENDER_SORT_" + k] = v
+        assert torch.equal(vg.render(ro, rd, z), ref), nm
+        res.setdefault(nm, []).append(timed(ro, rd, z))
+    os.environ["SFMHIP_RENDER_SORT"] = "0"
     for nm, key in keys().items():
         if key is None:
             perm = torch.arange(NB * B, device=dev)
@@ -69,14 +97,6 @@ for rep in range(2):
         o2, d2, z2 = ro[perm].contiguous(), rd[perm].contiguous(), z[perm].contiguous()
         out = vg.render(o2, d2, z2)
         assert torch.equal(out, ref[perm]), nm
-        ts = []
-        for _ in range(10):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            vg.render(o2, d2, z2)
-            e1.record()
-            torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1))
-        res.setdefault(nm, []).append(float(np.median(ts)))
+        res.setdefault(nm, []).append(timed(o2, d2, z2))
 for nm, v in res.items():
     print(f"{nm:24s} " + " ".join(f"{x:.3f}" for x in v) + " ms", flush=True)
