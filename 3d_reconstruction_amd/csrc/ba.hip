@@ -25,7 +25,7 @@ namespace sfmhip {
 namespace {
 
 #ifdef SFMHIP_BA_PROF
-// phase timing of the fused kernel (thread 0, wall clock at 100 MHz), a tool-only build
+// phase timing of the solve kernel (thread 0, wall clock at 100 MHz), a tool-only build
 // (make EXTRA=-DSFMHIP_BA_PROF; tools/ba_phase_prof.py): never in the product library
 constexpr int kProfPhases = 10;
 __device__ unsigned long long g_ba_prof[4096 * kProfPhases];
@@ -114,49 +114,12 @@ __device__ bool chol6_solve(double (&A)[6][6], double (&b)[6]) {
     return true;
 }
 
-// scipy solve_trust_region_2d: the interior Newton point if B is positive
-// definite and it fits, else the minimiser of the quadratic on the circle
-// |p| = Delta (scipy takes the best real root of its quartic; here the same
-// point from a scan of the circle refined by Newton on the angle).
-__device__ void tr_solve_2d(const double B[3] /* b00, b01, b11 */, const double g[2], double Delta, double p[2]) {
-    const double b00 = B[0], b01 = B[1], b11 = B[2];
-    if (b00 > 0.0) {
-        const double l00 = sqrt(b00), l10 = b01 / l00, s = b11 - l10 * l10;
-        if (s > 0.0) {
-            const double l11 = sqrt(s);
-            const double y0 = g[0] / l00, y1 = (g[1] - l10 * y0) / l11;
-            const double x1 = y1 / l11, x0 = (y0 - l10 * x1) / l00;
-            if (x0 * x0 + x1 * x1 <= Delta * Delta) { p[0] = -x0; p[1] = -x1; return; }
-        }
-    }
-    // q(phi) = 0.5 D^2 (b00 c^2 + 2 b01 c s + b11 s^2) + D (g0 c + g1 s)
-    auto val = [&](double ph) {
-        const double c = cos(ph), s = sin(ph);
-        return 0.5 * Delta * Delta * (b00 * c * c + 2.0 * b01 * c * s + b11 * s * s) + Delta * (g[0] * c + g[1] * s);
-    };
-    double best = 0.0, bv = val(0.0);
-    constexpr int kScan = 64;
-    for (int k = 1; k < kScan; ++k) {
-        const double ph = 6.283185307179586 * k / kScan, v = val(ph);
-        if (v < bv) { bv = v; best = ph; }
-    }
-    for (int it = 0; it < 40; ++it) {   // Newton on dq/dphi
-        const double c = cos(best), s = sin(best);
-        const double d1 = Delta * Delta * ((b11 - b00) * c * s + b01 * (c * c - s * s)) + Delta * (g[1] * c - g[0] * s);
-        const double d2 = Delta * Delta * ((b11 - b00) * (c * c - s * s) - 4.0 * b01 * c * s) - Delta * (g[0] * c + g[1] * s);
-        if (!(d2 > 0.0)) break;
-        const double step = d1 / d2;
-        best -= step;
-        if (fabs(step) < 1e-16) break;
-    }
-    p[0] = Delta * cos(best);
-    p[1] = Delta * sin(best);
-}
-
-// tr_solve_2d on a whole wave (every lane returns the same p): the interior point as
-// tr_solve_2d; on the circle, lane l evaluates angle 2 pi l / 64 (the serial scan's
-// points), the lowest-index minimum wins as in the serial loop, then the same Newton
-// refinement on every lane.
+// scipy solve_trust_region_2d on a whole wave (every lane returns the same p): the
+// interior Newton point if B is positive definite and it fits, else the minimiser of
+// the quadratic on the circle |p| = Delta (scipy takes the best real root of its
+// quartic; here the same point from a 64-angle scan, lane l at 2 pi l / 64, lowest
+// index on ties, refined by Newton on the angle).  On one thread the scan's 128
+// sin/cos took up to 150 us of a pair's solve (tools/ba_phase_prof.py).
 __device__ void tr_solve_2d_wave(const double B[3], const double g[2], double Delta, double p[2]) {
     const double b00 = B[0], b01 = B[1], b11 = B[2];
     if (b00 > 0.0) {
@@ -283,9 +246,14 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         return;
     }
     const int max_nfev = max_nfev_arg > 0 ? max_nfev_arg : (int)min((int64_t)INT_MAX, 100 * (6 + 3 * (int64_t)n));
+#ifdef SFMHIP_BA_PROF
+    unsigned long long prof_acc[kProfPhases] = {}, prof_t = wall_clock64();
+#endif
 
-    // J, f at the current point; scale_inv (max with the old unless first); gc, cost, |g|_inf
-    auto jacobian = [&](bool first) {
+    // J, f at the current point; scale_inv (max with the old unless first); gc, cost, |g|_inf.
+    // moved: the point is the accepted trial point, read from the records (fields 23-25)
+    // and written to X here (no separate pass to move X)
+    auto jacobian = [&](bool first, bool moved) {
         if (tid < 4) {   // R(rvec) and the three perturbed rotations of the FD
             double q[3] = {S.cam[0], S.cam[1], S.cam[2]};
             if (tid > 0) q[tid - 1] = q[tid - 1] + fd_step(q[tid - 1]);
@@ -296,9 +264,15 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         double gmax = 0.0;
         for (int i = tid; i < n; i += NT) {
             double r[kRec];
-            double f[2];
+            double f[2], Xi[3];
+            if (moved) {
+                rec.template load<23, 26>(i, r);
+                for (int c = 0; c < 3; ++c) { Xi[c] = r[23 + c]; Xp[3 * i + c] = Xi[c]; }
+            } else {
+                for (int c = 0; c < 3; ++c) Xi[c] = Xp[3 * i + c];
+            }
             if (!first) rec.template load<20, 23>(i, r);
-            fd_obs(&S.R[0][0], S.cam, k, Xp + 3 * i, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
+            fd_obs(&S.R[0][0], S.cam, k, Xi, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
             r[18] = f[0];
             r[19] = f[1];
             acc[12] += f[0] * f[0] + f[1] * f[1];
@@ -334,7 +308,8 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         __syncthreads();
     };
 
-    jacobian(true);
+    jacobian(true, false);
+    BA_MARK(0);
     // Delta = |x0 * scale_inv|
     {
         double acc[1] = {0.0};
@@ -395,6 +370,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 S.gh2 = gh2;
             }
             __syncthreads();
+            BA_MARK(1);
         }
         const double mu = S.mu;
         // ridge: G = I + sum C^T B^-1 C, h = sum C^T B^-1 f  (C = J_h camera block, B = Jp_h Jp_h^T + mu I)
@@ -436,6 +412,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 for (int a = 0; a < 6; ++a) S.z[a] = h[a];
             }
             __syncthreads();
+            BA_MARK(2);
         }
         // gn_h = J_h^T y, y = B^-1 f - B^-1 C z; g_h . gn_h and |gn_h|^2 (Gram-Schmidt of [g_h, gn_h])
         {
@@ -479,6 +456,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 S.ghn = ghn;
             }
             __syncthreads();
+            BA_MARK(3);
         }
         // |s2|^2 exactly; then JS (2 columns) -> B_S, g_S
         const double ghn = S.ghn, c12 = S.c12;
@@ -505,27 +483,11 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 s2[c] = gn - c12 * s1[c];
             }
         };
+        // one pass for |s2|^2 and the products of JS = J_h [s1, s2]: with the unnormalised s2
+        // (camera part S.s2c, point part from point_vecs) every product that involves s2 is
+        // divided by |s2| (or |s2|^2) once afterwards
         {
-            double acc[1] = {0.0};
-            for (int i = tid; i < n; i += NT) {
-                double r[kRec];
-                rec.template load<0, 23>(i, r);
-                double s1[3], s2[3];
-                point_vecs(r, s1, s2);
-                acc[0] += s2[0] * s2[0] + s2[1] * s2[1] + s2[2] * s2[2];
-            }
-            block_sum<NW, 1>(acc, S.red, S.tot);
-            if (tid == 0) {
-                double n2 = S.tot[0];
-                for (int c = 0; c < 6; ++c) n2 += S.s2c[c] * S.s2c[c];
-                S.s2n = sqrt(n2);
-                for (int c = 0; c < 6; ++c) S.s2c[c] /= S.s2n;
-            }
-            __syncthreads();
-        }
-        const double s2n = S.s2n;
-        {
-            double acc[5] = {0};   // JS1.JS1, JS1.JS2, JS2.JS2, s2 . g_h and s1 . g_h (point parts)
+            double acc[6] = {0};   // JS1.JS1, JS1.JS2u, JS2u.JS2u, s2u . g_h and s1 . g_h (point parts), |s2u pts|^2
             for (int i = tid; i < n; i += NT) {
                 double r[kRec];
                 rec.template load<0, 23>(i, r);
@@ -540,44 +502,62 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 }
                 for (int c = 0; c < 3; ++c) {
                     const double d = 1.0 / r[20 + c];
-                    const double s2c = s2[c] / s2n;
                     a0 += r[6 + c] * d * s1[c];
                     a1 += r[15 + c] * d * s1[c];
-                    b0 += r[6 + c] * d * s2c;
-                    b1 += r[15 + c] * d * s2c;
+                    b0 += r[6 + c] * d * s2[c];
+                    b1 += r[15 + c] * d * s2[c];
                     const double gh = d * (r[6 + c] * r[18] + r[15 + c] * r[19]);
-                    acc[3] += s2c * gh;
+                    acc[3] += s2[c] * gh;
                     acc[4] += s1[c] * gh;
+                    acc[5] += s2[c] * s2[c];
                 }
                 acc[0] += a0 * a0 + a1 * a1;
                 acc[1] += a0 * b0 + a1 * b1;
                 acc[2] += b0 * b0 + b1 * b1;
             }
-            block_sum<NW, 5>(acc, S.red, S.tot);
+            block_sum<NW, 6>(acc, S.red, S.tot);
             if (tid == 0) {
+                double n2 = S.tot[5];
+                for (int c = 0; c < 6; ++c) n2 += S.s2c[c] * S.s2c[c];
+                const double s2n = sqrt(n2);
                 double g0 = S.tot[4], g1 = S.tot[3];
                 for (int c = 0; c < 6; ++c) { g0 += S.s1c[c] * S.ghc[c]; g1 += S.s2c[c] * S.ghc[c]; }
-                S.BS[0] = S.tot[0]; S.BS[1] = S.tot[1]; S.BS[2] = S.tot[2];
-                S.gS[0] = g0; S.gS[1] = g1;
+                for (int c = 0; c < 6; ++c) S.s2c[c] /= s2n;
+                S.s2n = s2n;
+                S.BS[0] = S.tot[0];
+                S.BS[1] = S.tot[1] / s2n;
+                S.BS[2] = S.tot[2] / s2n / s2n;
+                S.gS[0] = g0;
+                S.gS[1] = g1 / s2n;
             }
             __syncthreads();
+            BA_MARK(4);
         }
+        const double s2n = S.s2n;
         // inner loop: trial steps until the cost decreases
         if (tid == 0) S.accept = 0;
         __syncthreads();
         while (true) {
-            if (tid == 0) {
-                S.done = !(S.nfev < max_nfev);
-                if (!S.done) {
-                    tr_solve_2d(S.BS, S.gS, S.Delta, S.pS);
-                    for (int c = 0; c < 6; ++c) {
-                        S.shc[c] = S.pS[0] * S.s1c[c] + S.pS[1] * S.s2c[c];
-                        S.cam_new[c] = S.cam[c] + S.dc[c] * S.shc[c];
+            if (tid < 64) {   // wave 0: the 2-D subproblem (the circle scan's 64 angles one per lane)
+                if (!(S.nfev < max_nfev)) {
+                    if (tid == 0) S.done = 1;
+                } else {
+                    double pS[2];
+                    tr_solve_2d_wave(S.BS, S.gS, S.Delta, pS);
+                    if (tid == 0) {
+                        S.done = 0;
+                        S.pS[0] = pS[0];
+                        S.pS[1] = pS[1];
+                        for (int c = 0; c < 6; ++c) {
+                            S.shc[c] = S.pS[0] * S.s1c[c] + S.pS[1] * S.s2c[c];
+                            S.cam_new[c] = S.cam[c] + S.dc[c] * S.shc[c];
+                        }
+                        rodrigues(S.cam_new, S.Rn);
                     }
-                    rodrigues(S.cam_new, S.Rn);
                 }
             }
             __syncthreads();
+            BA_MARK(5);
             if (S.done) break;
             // step, J_h step, f(x_new): predicted reduction, cost_new, |step_h|, |step|, |x|, finiteness
             double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
@@ -611,428 +591,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
             }
             block_sum<NW, 7>(acc, S.red, S.tot);
-            if (tid == 0) {
-                double sg = S.tot[1], sh2 = S.tot[3], st2 = S.tot[4], x2 = S.tot[5];
-                for (int c = 0; c < 6; ++c) {
-                    sg += S.shc[c] * S.ghc[c];
-                    sh2 += S.shc[c] * S.shc[c];
-                    st2 += (S.dc[c] * S.shc[c]) * (S.dc[c] * S.shc[c]);
-                    x2 += S.cam[c] * S.cam[c];
-                }
-                const double predicted = -(0.5 * S.tot[0] + sg);
-                S.nfev += 1;
-                const double sh_norm = sqrt(sh2);
-                if (S.tot[6] > 0.0) {   // non-finite residuals: shrink and retry
-                    S.Delta = 0.25 * sh_norm;
-                    S.accept = -1;
-                } else {
-                    S.cost_new = 0.5 * S.tot[2];
-                    const double actual = S.cost - S.cost_new;
-                    double ratio;
-                    if (predicted > 0.0) ratio = actual / predicted;
-                    else if (predicted == 0.0 && actual == 0.0) ratio = 1.0;
-                    else ratio = 0.0;
-                    double Dn = S.Delta;
-                    if (ratio < 0.25) Dn = 0.25 * sh_norm;
-                    else if (ratio > 0.75 && sh_norm > 0.95 * S.Delta) Dn = S.Delta * 2.0;
-                    const double step_norm = sqrt(st2), x_norm = sqrt(x2);
-                    const bool fok = actual < ftol * S.cost && ratio > 0.25;
-                    const bool xok = step_norm < xtol * (xtol + x_norm);
-                    S.status = (fok && xok) ? 4 : fok ? 2 : xok ? 3 : -1;
-                    S.accept = actual > 0.0 ? 1 : 0;
-                    if (S.status < 0) S.Delta = Dn;
-                }
-            }
-            __syncthreads();
-            if (S.status >= 0 || S.accept == 1) break;
-        }
-        if (S.accept == 1) {   // x = x_new; J at the new point
-            for (int i = tid; i < n; i += NT) {
-                double r[kRec];
-                rec.template load<23, 26>(i, r);
-                for (int c = 0; c < 3; ++c) Xp[3 * i + c] = r[23 + c];
-            }
-            if (tid < 6) S.cam[tid] = S.cam_new[tid];
-            __syncthreads();
-            jacobian(false);
-            if (tid == 0) { S.njev += 1; }
-            __syncthreads();
-        }
-        if (S.done) break;
-    }
-    if (tid < 6) cam_io[(size_t)p * 6 + tid] = S.cam[tid];
-    if (tid == 0) {
-        cost_out[p] = S.cost;
-        nfev_out[p] = S.nfev;
-        njev_out[p] = S.njev;
-        status_out[p] = S.status < 0 ? 0 : S.status;
-    }
-}
-
-// The same iteration with the passes fused (4 per TRF iteration instead of 8):
-//   * the Jacobian pass (the first one and every accepted step; it also moves
-//     X to the accepted point) accumulates, besides J^T f / column norms / cost,
-//     sum Jc^T Jc and the point parts of J_h g_h, so regularize's a = |J_h g_h|^2 / 2
-//     comes out of the reductions: |Jc w + q|^2 = w^T (sum Jc^T Jc) w + 2 w . sum Jc^T q
-//     + sum |q|^2 with w = dc^2 gc;
-//   * ridge (G, h -> z) as before;
-//   * one pass gives gn_h and every product of the 2-D subspace: with a = J_h g_h
-//     and b = J_h gn_h = C gn_c + q (gn_c is that pass's own reduction), sum |b|^2
-//     and sum a . b are expanded over sum C^T C, sum C^T q, sum C^T a, so
-//     B_S = S^T J_h^T J_h S, g_S and |s2| follow from the reductions;
-//   * the trial step(s).
-// The trust-region subproblem runs on wave 0 (tr_solve_2d_wave: the circle scan's
-// 64 angles one per lane).
-// Records are field-major per pair (Recs<true>).  Same TRF decisions as the
-// unfused kernel; the expanded sums differ from the direct ones by rounding.
-template <int NW>
-struct BaStateF {
-    double cam[6], cam_new[6], R[4][9], Rn[9];
-    double gc[6], sic[6], dc[6], ghc[6], s1c[6], s2c[6], shc[6];
-    double JtJ[21], z[6];
-    double red[NW * 43], tot[43];
-    double Delta, mu, cost, cost_new, pS[2], aq, gh2;
-    double gmax, ghn, c12, s2n, BS[3], gS[2];
-    int status, nfev, njev, done, accept;
-};
-
-template <int NT>
-__global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ cam_io, const double* __restrict__ Kall,
-                                                          double* __restrict__ X, const double* __restrict__ pts2d,
-                                                          const int64_t* __restrict__ off, int64_t n_obs, double ftol,
-                                                          double xtol, double gtol, int max_nfev_arg,
-                                                          double* __restrict__ scratch, double* __restrict__ cost_out,
-                                                          int32_t* __restrict__ nfev_out,
-                                                          int32_t* __restrict__ njev_out,
-                                                          int32_t* __restrict__ status_out) {
-    constexpr int NW = NT / 64;
-    __shared__ BaStateF<NW> S;
-    const int p = blockIdx.x, tid = threadIdx.x;
-    const int64_t o0 = off[p], o1 = off[p + 1];
-    if (!(0 <= o0 && o0 <= o1 && o1 <= n_obs && o1 - o0 <= INT_MAX)) {   // malformed offsets: touch nothing
-        if (tid == 0) { cost_out[p] = 0.0; nfev_out[p] = 0; njev_out[p] = 0; status_out[p] = -1; }
-        return;
-    }
-    const int n = (int)(o1 - o0);
-    const double* k = Kall + (size_t)p * 9;
-    double* Xp = X + 3 * o0;
-    const double* pts = pts2d + 2 * o0;
-    const Recs<true> rec{scratch + (size_t)o0 * kRec, n};
-    if (tid < 6) S.cam[tid] = cam_io[(size_t)p * 6 + tid];
-    __syncthreads();
-    if (n == 0) {
-        if (tid == 0) { cost_out[p] = 0.0; nfev_out[p] = 0; njev_out[p] = 0; status_out[p] = 1; }
-        return;
-    }
-    const int max_nfev = max_nfev_arg > 0 ? max_nfev_arg : (int)min((int64_t)INT_MAX, 100 * (6 + 3 * (int64_t)n));
-#ifdef SFMHIP_BA_PROF
-    unsigned long long prof_acc[kProfPhases] = {}, prof_t = wall_clock64();
-#endif
-
-    // J, f at the current point (first: x0; moved: the accepted trial point, which it
-    // also writes to X); scale_inv; gc, cost, |g|_inf; sum Jc^T Jc; the regularize sums
-    auto jacobian = [&](bool first, bool moved) {
-        if (tid < 4) {   // R(rvec) and the three perturbed rotations of the FD
-            double q[3] = {S.cam[0], S.cam[1], S.cam[2]};
-            if (tid > 0) q[tid - 1] = q[tid - 1] + fd_step(q[tid - 1]);
-            rodrigues(q, S.R[tid]);
-        }
-        __syncthreads();
-        // gc (6), column sums of squares (6), cost, sum Jc^T Jc (21), sum Jc^T q (6), |q|^2, |g_h point|^2, |x0 s|^2
-        double acc[43];
-#pragma unroll
-        for (int e = 0; e < 43; ++e) acc[e] = 0.0;
-        double gmax = 0.0;
-        for (int i = tid; i < n; i += NT) {
-            double r[kRec];
-            double f[2], Xi[3];
-            if (moved) {
-                rec.template load<23, 26>(i, r);
-                for (int c = 0; c < 3; ++c) { Xi[c] = r[23 + c]; Xp[3 * i + c] = Xi[c]; }
-            } else {
-                for (int c = 0; c < 3; ++c) Xi[c] = Xp[3 * i + c];
-            }
-            if (!first) rec.template load<20, 23>(i, r);
-            fd_obs(&S.R[0][0], S.cam, k, Xi, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
-            r[18] = f[0];
-            r[19] = f[1];
-            acc[12] += f[0] * f[0] + f[1] * f[1];
-#pragma unroll
-            for (int c = 0; c < 6; ++c) {
-                acc[c] += r[c] * f[0] + r[9 + c] * f[1];
-                acc[6 + c] += r[c] * r[c] + r[9 + c] * r[9 + c];
-            }
-            int e = 13;
-#pragma unroll
-            for (int a = 0; a < 6; ++a)
-#pragma unroll
-                for (int b = a; b < 6; ++b) acc[e++] += r[a] * r[b] + r[9 + a] * r[9 + b];
-            double q0 = 0.0, q1 = 0.0;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const double gp = r[6 + c] * f[0] + r[15 + c] * f[1];
-                gmax = fmax(gmax, fabs(gp));
-                double si = sqrt(r[6 + c] * r[6 + c] + r[15 + c] * r[15 + c]);
-                if (first) si = si == 0.0 ? 1.0 : si;
-                else si = fmax(si, r[20 + c]);
-                r[20 + c] = si;
-                const double d = 1.0 / si;
-                const double gh = d * gp;                     // g_h, point column c
-                q0 += r[6 + c] * d * gh;                      // (J_h g_h) point part
-                q1 += r[15 + c] * d * gh;
-                acc[41] += gh * gh;
-                if (first) { const double t = Xi[c] * si; acc[42] += t * t; }
-            }
-#pragma unroll
-            for (int c = 0; c < 6; ++c) acc[34 + c] += r[c] * q0 + r[9 + c] * q1;
-            acc[40] += q0 * q0 + q1 * q1;
-            rec.template store<0, 23>(i, r);
-        }
-        gmax = block_max<NW>(gmax, S.red);
-        block_sum<NW, 43>(acc, S.red, S.tot);
-        if (tid == 0) {
-            double gm = gmax;
-            for (int c = 0; c < 6; ++c) {
-                S.gc[c] = S.tot[c];
-                gm = fmax(gm, fabs(S.gc[c]));
-                const double si = sqrt(S.tot[6 + c]);
-                S.sic[c] = first ? (si == 0.0 ? 1.0 : si) : fmax(si, S.sic[c]);
-                S.dc[c] = 1.0 / S.sic[c];
-                S.ghc[c] = S.dc[c] * S.gc[c];
-            }
-            for (int e = 0; e < 21; ++e) S.JtJ[e] = S.tot[13 + e];
-            // |J_h g_h|^2 = w^T (Jc^T Jc) w + 2 w . (Jc^T q) + |q|^2, w = dc * ghc
-            double w[6], a2 = S.tot[40], gh2 = S.tot[41];
-            for (int c = 0; c < 6; ++c) { w[c] = S.dc[c] * S.ghc[c]; gh2 += S.ghc[c] * S.ghc[c]; }
-            int e = 0;
-            for (int a = 0; a < 6; ++a)
-                for (int b = a; b < 6; ++b) {
-                    const double t = w[a] * S.JtJ[e++] * w[b];
-                    a2 += a == b ? t : 2.0 * t;
-                }
-            for (int c = 0; c < 6; ++c) a2 += 2.0 * w[c] * S.tot[34 + c];
-            S.aq = 0.5 * a2;
-            S.gh2 = gh2;
-            S.gmax = gm;
-            S.cost = 0.5 * S.tot[12];
-            if (first) {
-                double d2 = S.tot[42];
-                for (int c = 0; c < 6; ++c) d2 += (S.cam[c] * S.sic[c]) * (S.cam[c] * S.sic[c]);
-                S.Delta = sqrt(d2);
-                if (S.Delta == 0.0) S.Delta = 1.0;
-                S.nfev = 1; S.njev = 1; S.status = -1; S.done = 0;
-            }
-        }
-        __syncthreads();
-    };
-
-    // per observation: the scaled blocks C = Jc dc, Pp = Jp d and (J_h J_h^T + mu)^-1's 2x2 point part
-    struct Blk { double C[2][6], Pp[2][3], d[3], i00, i01, i11; };
-    auto blocks = [&](const double* r, double mu, Blk& B) {
-        for (int c = 0; c < 6; ++c) { B.C[0][c] = r[c] * S.dc[c]; B.C[1][c] = r[9 + c] * S.dc[c]; }
-        for (int c = 0; c < 3; ++c) {
-            B.d[c] = 1.0 / r[20 + c];
-            B.Pp[0][c] = r[6 + c] * B.d[c];
-            B.Pp[1][c] = r[15 + c] * B.d[c];
-        }
-        const double b00 = B.Pp[0][0] * B.Pp[0][0] + B.Pp[0][1] * B.Pp[0][1] + B.Pp[0][2] * B.Pp[0][2] + mu;
-        const double b01 = B.Pp[0][0] * B.Pp[1][0] + B.Pp[0][1] * B.Pp[1][1] + B.Pp[0][2] * B.Pp[1][2];
-        const double b11 = B.Pp[1][0] * B.Pp[1][0] + B.Pp[1][1] * B.Pp[1][1] + B.Pp[1][2] * B.Pp[1][2] + mu;
-        const double idet = 1.0 / (b00 * b11 - b01 * b01);
-        B.i00 = b11 * idet; B.i01 = -b01 * idet; B.i11 = b00 * idet;
-    };
-
-    jacobian(true, false);
-    BA_MARK(0);
-
-    while (true) {
-        __syncthreads();   // every wave has read the previous iteration's S.status / S.done
-        if (tid == 0) {
-            if (S.gmax < gtol) S.status = 1;
-            S.done = S.status >= 0 || S.nfev == max_nfev;
-            // regularize (build_quadratic_1d along -g_h, minimize_quadratic_1d on [0, Delta / |g_h|])
-            const double a = S.aq, b = -S.gh2, to_tr = S.Delta / sqrt(S.gh2);
-            double ag = 0.0;
-            ag = fmin(ag, to_tr * (a * to_tr + b));
-            if (a != 0.0) {
-                const double ext = -0.5 * b / a;
-                if (0.0 < ext && ext < to_tr) ag = fmin(ag, ext * (a * ext + b));
-            }
-            S.mu = -ag / (S.Delta * S.Delta);
-        }
-        __syncthreads();
-        BA_MARK(1);
-        if (S.done) break;
-        const double mu = S.mu;
-        // ridge: G = I + sum C^T B^-1 C, h = sum C^T B^-1 f
-        {
-            double acc[27];
-#pragma unroll
-            for (int e = 0; e < 27; ++e) acc[e] = 0.0;
-            stream_recs<NT, 0, 23>(rec, n, [&](int i, const double* r) {
-                Blk B;
-                blocks(r, mu, B);
-                const double u0 = B.i00 * r[18] + B.i01 * r[19], u1 = B.i01 * r[18] + B.i11 * r[19];
-                double Y[2][6];
-                for (int c = 0; c < 6; ++c) {
-                    Y[0][c] = B.i00 * B.C[0][c] + B.i01 * B.C[1][c];
-                    Y[1][c] = B.i01 * B.C[0][c] + B.i11 * B.C[1][c];
-                }
-                int e = 0;
-                for (int a = 0; a < 6; ++a)
-                    for (int b = a; b < 6; ++b) acc[e++] += B.C[0][a] * Y[0][b] + B.C[1][a] * Y[1][b];
-                for (int a = 0; a < 6; ++a) acc[21 + a] += B.C[0][a] * u0 + B.C[1][a] * u1;
-            });
-            block_sum<NW, 27>(acc, S.red, S.tot);
-            BA_MARK(2);
-            if (tid == 0) {
-                double G[6][6], h[6];
-                int e = 0;
-                for (int a = 0; a < 6; ++a)
-                    for (int b = a; b < 6; ++b) { G[a][b] = G[b][a] = S.tot[e++] + (a == b ? 1.0 : 0.0); }
-                for (int a = 0; a < 6; ++a) h[a] = S.tot[21 + a];
-                if (!chol6_solve(G, h)) S.status = -2;   // not expected: G = I + PSD
-                for (int a = 0; a < 6; ++a) S.z[a] = h[a];
-            }
-            __syncthreads();
-            BA_MARK(3);
-        }
-        // gn_h = J_h^T y (y = B^-1 (f - C z)) and the 2-D subspace products in one pass
-        {
-            double acc[23];   // gn_c (6), g_h.gn_h pts, |gn_h pts|^2, |a|^2, C^T a (6), a.q, C^T q (6), |q|^2
-#pragma unroll
-            for (int e = 0; e < 23; ++e) acc[e] = 0.0;
-            stream_recs<NT, 0, 23>(rec, n, [&](int i, const double* r) {
-                Blk B;
-                blocks(r, mu, B);
-                double w0 = r[18], w1 = r[19];
-                for (int c = 0; c < 6; ++c) { w0 -= B.C[0][c] * S.z[c]; w1 -= B.C[1][c] * S.z[c]; }
-                const double y0 = B.i00 * w0 + B.i01 * w1, y1 = B.i01 * w0 + B.i11 * w1;
-                double a0 = 0.0, a1 = 0.0, q0 = 0.0, q1 = 0.0;   // a = J_h g_h, q = Pp gn_p
-                for (int c = 0; c < 6; ++c) {
-                    acc[c] += B.C[0][c] * y0 + B.C[1][c] * y1;
-                    a0 += B.C[0][c] * S.ghc[c];
-                    a1 += B.C[1][c] * S.ghc[c];
-                }
-                for (int c = 0; c < 3; ++c) {
-                    const double gn = B.Pp[0][c] * y0 + B.Pp[1][c] * y1;
-                    const double gh = B.Pp[0][c] * r[18] + B.Pp[1][c] * r[19];
-                    acc[6] += gh * gn;
-                    acc[7] += gn * gn;
-                    a0 += B.Pp[0][c] * gh;
-                    a1 += B.Pp[1][c] * gh;
-                    q0 += B.Pp[0][c] * gn;
-                    q1 += B.Pp[1][c] * gn;
-                }
-                acc[8] += a0 * a0 + a1 * a1;
-                acc[15] += a0 * q0 + a1 * q1;
-                for (int c = 0; c < 6; ++c) {
-                    acc[9 + c] += B.C[0][c] * a0 + B.C[1][c] * a1;
-                    acc[16 + c] += B.C[0][c] * q0 + B.C[1][c] * q1;
-                }
-                acc[22] += q0 * q0 + q1 * q1;
-            });
-            block_sum<NW, 23>(acc, S.red, S.tot);
-            BA_MARK(4);
-            if (tid == 0) {
-                const double ghn = sqrt(S.gh2);
-                double gnc[6], dot = S.tot[6], gn2 = S.tot[7];
-                for (int c = 0; c < 6; ++c) {
-                    gnc[c] = S.tot[c];
-                    dot += S.ghc[c] * gnc[c];
-                    gn2 += gnc[c] * gnc[c];
-                    S.s1c[c] = S.ghc[c] / ghn;
-                }
-                const double c12 = dot / ghn;
-                const double s2sq = gn2 - c12 * c12;   // |gn_h - (s1 . gn_h) s1|^2
-                const double s2n = sqrt(fmax(s2sq, 1e-300));
-                for (int c = 0; c < 6; ++c) S.s2c[c] = (gnc[c] - c12 * S.s1c[c]) / s2n;
-                // sum a.b and |b|^2 with b = C gn_c + q:  C^T C = dc (Jc^T Jc) dc
-                double ab = S.tot[15], bb = S.tot[22];
-                for (int c = 0; c < 6; ++c) { ab += gnc[c] * S.tot[9 + c]; bb += 2.0 * gnc[c] * S.tot[16 + c]; }
-                int e = 0;
-                for (int a = 0; a < 6; ++a)
-                    for (int b = a; b < 6; ++b) {
-                        const double t = gnc[a] * (S.dc[a] * S.JtJ[e++] * S.dc[b]) * gnc[b];
-                        bb += a == b ? t : 2.0 * t;
-                    }
-                const double aa = S.tot[8], rr = c12 / ghn;
-                // JS1 = a / |g_h|, JS2 = (b - c12 a / |g_h|) / |s2|
-                S.BS[0] = aa / S.gh2;
-                S.BS[1] = (ab - rr * aa) / (ghn * s2n);
-                S.BS[2] = (bb - 2.0 * rr * ab + rr * rr * aa) / (s2n * s2n);
-                S.gS[0] = S.gh2 / ghn;
-                S.gS[1] = (dot - c12 * ghn) / s2n;
-                S.ghn = ghn;
-                S.c12 = c12;
-                S.s2n = s2n;
-            }
-            __syncthreads();
-            BA_MARK(5);
-        }
-        const double ghn = S.ghn, c12 = S.c12, s2n = S.s2n;
-        // inner loop: trial steps until the cost decreases
-        if (tid == 0) S.accept = 0;
-        __syncthreads();
-        while (true) {
-            if (tid < 64) {   // wave 0: the 2-D subproblem (uniform: every lane computes the same p)
-                if (!(S.nfev < max_nfev)) {
-                    if (tid == 0) S.done = 1;
-                } else {
-                    double pS[2];
-                    tr_solve_2d_wave(S.BS, S.gS, S.Delta, pS);
-                    if (tid == 0) {
-                        S.done = 0;
-                        S.pS[0] = pS[0];
-                        S.pS[1] = pS[1];
-                        for (int c = 0; c < 6; ++c) {
-                            S.shc[c] = S.pS[0] * S.s1c[c] + S.pS[1] * S.s2c[c];
-                            S.cam_new[c] = S.cam[c] + S.dc[c] * S.shc[c];
-                        }
-                        rodrigues(S.cam_new, S.Rn);
-                    }
-                }
-            }
-            __syncthreads();
             BA_MARK(6);
-            if (S.done) break;
-            double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
-            stream_recs<NT, 0, 23>(rec, n, [&](int i, const double* r) {
-                Blk B;
-                blocks(r, mu, B);
-                double w0 = r[18], w1 = r[19];
-                for (int c = 0; c < 6; ++c) { w0 -= B.C[0][c] * S.z[c]; w1 -= B.C[1][c] * S.z[c]; }
-                const double y0 = B.i00 * w0 + B.i01 * w1, y1 = B.i01 * w0 + B.i11 * w1;
-                double ju = 0, jv = 0;
-                for (int c = 0; c < 6; ++c) { ju += B.C[0][c] * S.shc[c]; jv += B.C[1][c] * S.shc[c]; }
-                double Xn[3];
-                double xs[kRec];
-                for (int c = 0; c < 3; ++c) {
-                    const double gn = B.Pp[0][c] * y0 + B.Pp[1][c] * y1;
-                    const double gh = B.Pp[0][c] * r[18] + B.Pp[1][c] * r[19];
-                    const double s1 = gh / ghn;
-                    const double s2 = gn - c12 * s1;
-                    const double sh = S.pS[0] * s1 + S.pS[1] * (s2 / s2n);
-                    ju += B.Pp[0][c] * sh;
-                    jv += B.Pp[1][c] * sh;
-                    acc[1] += sh * gh;
-                    acc[3] += sh * sh;
-                    const double st = B.d[c] * sh;
-                    acc[4] += st * st;
-                    const double x = Xp[3 * i + c];
-                    acc[5] += x * x;
-                    Xn[c] = x + st;
-                    xs[23 + c] = Xn[c];
-                }
-                rec.template store<23, 26>(i, xs);
-                acc[0] += ju * ju + jv * jv;
-                double ru, rv;
-                resid(S.Rn, S.cam_new, k, Xn, pts + 2 * i, ru, rv);
-                acc[2] += ru * ru + rv * rv;
-                if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
-            });
-            block_sum<NW, 7>(acc, S.red, S.tot);
-            BA_MARK(7);
             if (tid == 0) {
                 double sg = S.tot[1], sh2 = S.tot[3], st2 = S.tot[4], x2 = S.tot[5];
                 for (int c = 0; c < 6; ++c) {
@@ -1066,7 +625,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
                 }
             }
             __syncthreads();
-            BA_MARK(8);
+            BA_MARK(7);
             if (S.status >= 0 || S.accept == 1) break;
         }
         if (S.accept == 1) {   // x = x_new (moved by the Jacobian pass); J at the new point
@@ -1081,7 +640,7 @@ __global__ __launch_bounds__(NT) void ba_trf_fused_kernel(double* __restrict__ c
     }
 #ifdef SFMHIP_BA_PROF
     if (tid == 0 && p < 4096)
-        for (int k = 0; k < kProfPhases; ++k) g_ba_prof[p * kProfPhases + k] = prof_acc[k];
+        for (int kk = 0; kk < kProfPhases; ++kk) g_ba_prof[p * kProfPhases + kk] = prof_acc[kk];
 #endif
     if (tid < 6) cam_io[(size_t)p * 6 + tid] = S.cam[tid];
     if (tid == 0) {
@@ -1112,24 +671,16 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
         set_error("sfmhip_ba_solve: scratch allocation failed");
         return SFMHIP_E_HIP;
     }
-    // SFMHIP_BA_VARIANT (A/B runs): 0 AoS records, 256 threads; 1 field-major records, 256 threads;
-    // 2 field-major, 512 threads; 3 AoS, 512 threads
-    static const int variant = [] { const char* e = std::getenv("SFMHIP_BA_VARIANT"); return e ? std::atoi(e) : 0; }();
+    // SFMHIP_BA_VARIANT (A/B runs): 2 (default) field-major records, 512 threads; 1 field-major, 256 threads;
+    // 0 AoS records, 256 threads; 3 AoS, 512 threads (profiles/r3/ba_variants_r3m.txt)
+    static const int variant = [] { const char* e = std::getenv("SFMHIP_BA_VARIANT"); return e ? std::atoi(e) : 2; }();
     switch (variant) {
+        case 0:
+            hipLaunchKernelGGL((ba_trf_kernel<256, false>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
+                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+            break;
         case 1:
             hipLaunchKernelGGL((ba_trf_kernel<256, true>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
-                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-            break;
-        case 2:
-            hipLaunchKernelGGL((ba_trf_kernel<512, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
-                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-            break;
-        case 4:
-            hipLaunchKernelGGL((ba_trf_fused_kernel<256>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
-                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-            break;
-        case 5:
-            hipLaunchKernelGGL((ba_trf_fused_kernel<512>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
                                n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
             break;
         case 3:
@@ -1137,7 +688,7 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
                                n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
             break;
         default:
-            hipLaunchKernelGGL((ba_trf_kernel<256, false>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
+            hipLaunchKernelGGL((ba_trf_kernel<512, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
                                n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
     }
     const int rc = check_launch("ba_trf_kernel");
@@ -1146,7 +697,7 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
 }
 
 #ifdef SFMHIP_BA_PROF
-// tool-only build: the per-pair phase times of the last fused-kernel launch (wall-clock ticks)
+// tool-only build: the per-pair phase times of the last solve launch (wall-clock ticks)
 extern "C" int sfmhip_ba_prof_read(unsigned long long* host, int n_pairs) {
     const int n = std::min(n_pairs, 4096) * kProfPhases;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ba_prof), (size_t)n * sizeof(unsigned long long)) == hipSuccess

@@ -1595,16 +1595,22 @@ __device__ __forceinline__ v4f adam4(v4f pp, v4f gg, v4f& mm, v4f& vv, float w1,
     return pp;
 }
 
-// Streams are touched once per step: non-temporal loads/stores, two float4
-// per thread per iteration (8 loads in flight) over a grid-stride loop.
+// Streams are touched once per step: non-temporal loads/stores.  Workgroup b owns the
+// contiguous float4 range [b * chunk, (b + 1) * chunk) of every stream, two float4 per
+// thread in flight (512 per round), so the resident workgroups sweep each buffer in a
+// compact front; a grid-stride assignment (the resident workgroups spread over 8-16
+// regions 134 MB apart in all four buffers) ran 4-8 % slower on the same box
+// (tools/adam_layout_micro.hip, profiles/r3/ab/adam_access_micro_r3l.txt).
+constexpr int64_t kAdamChunk4 = 16384;   // float4 per workgroup and stream (256 KB)
+
 __global__ __launch_bounds__(256) void adam_kernel(v4f* __restrict__ p, v4f* __restrict__ g, v4f* __restrict__ m,
                                                    v4f* __restrict__ v, int64_t n4, float w1, float b2, float s2,
                                                    float bc2s, float eps, float step, int zero_grad) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * kAdamChunk4, b1 = min(n4, b0 + kAdamChunk4);
     const v4f z4 = {0.f, 0.f, 0.f, 0.f};
-    for (; i + stride < n4; i += 2 * stride) {
-        const int64_t j = i + stride;
+    int64_t i = b0 + threadIdx.x;
+    for (; i + 256 < b1; i += 512) {
+        const int64_t j = i + 256;
         const v4f g0 = __builtin_nontemporal_load(g + i), g1 = __builtin_nontemporal_load(g + j);
         v4f m0 = __builtin_nontemporal_load(m + i), m1 = __builtin_nontemporal_load(m + j);
         v4f v0 = __builtin_nontemporal_load(v + i), v1 = __builtin_nontemporal_load(v + j);
@@ -1616,7 +1622,7 @@ __global__ __launch_bounds__(256) void adam_kernel(v4f* __restrict__ p, v4f* __r
         __builtin_nontemporal_store(q0, p + i); __builtin_nontemporal_store(q1, p + j);
         if (zero_grad) { __builtin_nontemporal_store(z4, g + i); __builtin_nontemporal_store(z4, g + j); }
     }
-    for (; i < n4; i += stride) {
+    for (; i < b1; i += 256) {
         v4f m0 = m[i], v0 = v[i];
         p[i] = adam4(p[i], g[i], m0, v0, w1, b2, s2, bc2s, eps, step);
         m[i] = m0;
@@ -1628,18 +1634,18 @@ __global__ __launch_bounds__(256) void adam_kernel(v4f* __restrict__ p, v4f* __r
 // The same step where a flag byte per 2^fshift parameters marks the ones whose
 // gradient can be non-zero (the trainer's scatter sets it per touched voxel):
 // elsewhere the gradient is known to be 0 and is neither read nor re-zeroed, so a
-// step touching ~1/5 of the voxels moves ~25.5 instead of 32 bytes per parameter.
+// step touching ~1/12 of the voxel lines moves ~24.7 instead of 32 bytes per parameter.
 // Results are those of adam_kernel (g = 0 exactly where the flag is 0).
 __global__ __launch_bounds__(256) void adam_flagged_kernel(v4f* __restrict__ p, v4f* __restrict__ g,
                                                            v4f* __restrict__ m, v4f* __restrict__ v, int64_t n4,
                                                            float w1, float b2, float s2, float bc2s, float eps,
                                                            float step, int zero_grad,
                                                            const unsigned char* __restrict__ flags, int fshift4) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * kAdamChunk4, b1 = min(n4, b0 + kAdamChunk4);
     const v4f z4 = {0.f, 0.f, 0.f, 0.f};
-    for (; i + stride < n4; i += 2 * stride) {
-        const int64_t j = i + stride;
+    int64_t i = b0 + threadIdx.x;
+    for (; i + 256 < b1; i += 512) {
+        const int64_t j = i + 256;
         const bool t0 = flags[i >> fshift4] != 0, t1 = flags[j >> fshift4] != 0;
         v4f m0 = __builtin_nontemporal_load(m + i), m1 = __builtin_nontemporal_load(m + j);
         v4f v0 = __builtin_nontemporal_load(v + i), v1 = __builtin_nontemporal_load(v + j);
@@ -1655,7 +1661,7 @@ __global__ __launch_bounds__(256) void adam_flagged_kernel(v4f* __restrict__ p, 
         if (zero_grad && t0) __builtin_nontemporal_store(z4, g + i);
         if (zero_grad && t1) __builtin_nontemporal_store(z4, g + j);
     }
-    for (; i < n4; i += stride) {
+    for (; i < b1; i += 256) {
         const bool t0 = flags[i >> fshift4] != 0;
         v4f m0 = m[i], v0 = v[i];
         p[i] = adam4(p[i], t0 ? g[i] : z4, m0, v0, w1, b2, s2, bc2s, eps, step);
@@ -2319,7 +2325,7 @@ extern "C" int sfmhip_adam_step(float* param, float* grad, float* exp_avg, float
     const float bc2s = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
     const float stp = (float)(-lr / (1.0 - std::pow(beta1, (double)step)));
     const int64_t n4 = n / 4;
-    const int blocks = (int)std::min<int64_t>(ceil_div(n4, 256), env_int("SFMHIP_ADAM_BLOCKS", 32768));
+    const int blocks = ceil_div(n4, kAdamChunk4);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), reinterpret_cast<v4f*>(param),
                        reinterpret_cast<v4f*>(grad), reinterpret_cast<v4f*>(exp_avg),
                        reinterpret_cast<v4f*>(exp_avg_sq), n4, w1, b2, s2, bc2s, (float)eps, stp, zero_grad);
@@ -2338,7 +2344,7 @@ extern "C" int sfmhip_adam_step_flagged(float* param, float* grad, float* exp_av
     const float bc2s = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
     const float stp = (float)(-lr / (1.0 - std::pow(beta1, (double)step)));
     const int64_t n4 = n / 4;
-    const int blocks = (int)std::min<int64_t>(ceil_div(n4, 256), env_int("SFMHIP_ADAM_BLOCKS", 32768));
+    const int blocks = ceil_div(n4, kAdamChunk4);
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(adam_flagged_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<v4f*>(param),
                        reinterpret_cast<v4f*>(grad), reinterpret_cast<v4f*>(exp_avg),

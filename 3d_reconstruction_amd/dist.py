@@ -334,3 +334,55 @@ def plan_slabs(layer_cost, world: int, layer: int = 8, depth: int | None = None)
         bounds.append(j)
     bounds = bounds[::-1]
     return [(min(D, bounds[r] * layer), min(D, bounds[r + 1] * layer)) for r in range(world)]
+
+
+def rebalance_slabs(slabs, times, depth: int, align: int = 1, fixed: float = 0.0) -> list[tuple[int, int]]:
+    """Re-cut contiguous z-slabs from each rank's MEASURED fusion time (feedback
+    balancing for repeated integrations of one scene: measure a call, re-cut,
+    repeat).  Rank r's time minus ``fixed`` (the per-call cost that does not
+    scale with thickness) is spread evenly over its layers; the cumulative cost
+    over z is then cut at equal quantiles (``align`` > 1: the exact min-max
+    partition at multiples of ``align`` voxels, :func:`plan_slabs`).
+    Any cut gives the same grid (tiles start at z0 and culling is exact:
+    tests/test_gpu_voxel.py, tests/test_dist.py); only the balance changes.
+    The layer costs of an orbit scene vary by ~+-15 % over z, so
+    2-3 rounds bring the slowest slab to the mean."""
+    slabs = [(int(a), int(b)) for a, b in slabs]
+    t = np.asarray(times, np.float64).ravel()
+    world, D = len(slabs), int(depth)
+    if len(t) != world or world < 1:
+        raise ValueError("one time per slab")
+    if slabs[0][0] != 0 or slabs[-1][1] != D or any(slabs[r][1] != slabs[r + 1][0] for r in range(world - 1)):
+        raise ValueError("slabs must tile [0, depth) in order")
+    dens = np.zeros(D, np.float64)
+    for (a, b), tr in zip(slabs, t):
+        if b > a:
+            dens[a:b] = max(float(tr) - fixed, 1e-12) / (b - a)
+    # an empty slab's layers have no measurement: give them the mean density of the measured ones
+    meas = dens[dens > 0]
+    dens[dens == 0] = meas.mean() if meas.size else 1.0
+    if align > 1:   # coarse grid: the exact min-max partition of the aligned layers' costs
+        L = -(-D // align)
+        return plan_slabs([dens[i * align:(i + 1) * align].sum() for i in range(L)], world, layer=align, depth=D)
+    cum = np.concatenate([[0.0], np.cumsum(dens)])
+    cuts = [0]
+    for r in range(1, world):
+        z = int(np.searchsorted(cum, cum[-1] * r / world))
+        # the nearer of the two layer boundaries around the quantile, on the align grid
+        if z > 0 and cum[z] - cum[-1] * r / world > cum[-1] * r / world - cum[z - 1]:
+            z -= 1
+        cuts.append(min(max(z, cuts[-1]), D))
+    cuts.append(D)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def allgather_times(t: float, group=None) -> list[float]:
+    """Every rank's float (e.g. its measured slab time) on every rank, over the
+    torch.distributed group (gloo or nccl; a host value, so a CPU tensor for
+    gloo and a device tensor for nccl)."""
+    world = dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    mine = torch.tensor([float(t)], dtype=torch.float64, device=dev)
+    out = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(out, mine, group=group)
+    return [float(x.item()) for x in out]

@@ -1008,6 +1008,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--skip-secondary", action="store_true")
+    ap.add_argument("--no-rebalance", action="store_true",
+                    help="N > 1: keep equal-thickness TSDF slabs (default: re-cut from measured fusion times)")
+    ap.add_argument("--rebalance-rounds", type=int, default=3)
     ap.add_argument("--n-img", type=int, default=N_IMG)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for rehearsal")
     ap.add_argument("--rehearse-overlap", action="store_true",
@@ -1136,13 +1139,14 @@ def main():
         torch.cuda.synchronize()
         log(f"[rank {rank}] depth maps ready ({time.perf_counter() - t0:.1f}s): {depth.numel() * 4 / 1e9:.2f} GB")
         R = TSDF_R
-        z0, z1 = sdist.shard_range(R, rank, world)
+        slabs = [sdist.shard_range(R, r, world) for r in range(world)]
+        z0, z1 = slabs[rank]
         T = torch.zeros((R, R, R), dtype=torch.float32, device=device)
         Wt = torch.zeros_like(T)
         trunc = 3 * 2.4 / (R - 1)
         bmin, bmax = (-1.2, -1.2, -1.2), (1.2, 1.2, 1.2)
 
-        def tsdf_step(record):
+        def tsdf_step(record, fusion_events=None):
             T[z0:z1].zero_()
             Wt[z0:z1].zero_()
             e0, e1 = events() if record else (None, None)
@@ -1150,13 +1154,29 @@ def main():
                 e0.record()
             if world > 1:   # each rank builds the block table of 1/N of the frames; one all-gather
                 tab = sdist.shared_block_table(depth, comm=comm)
+                if fusion_events:
+                    fusion_events[0].record()
                 sfm.tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0, z1, block_table=tab)
+                if fusion_events:
+                    fusion_events[1].record()
             else:
                 sfm.tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0, z1)
             if record:
                 e1.record()
             return (e0, e1)
 
+        rebalance = world > 1 and not args.no_rebalance
+        if rebalance:
+            # feedback balancing (dist.rebalance_slabs): the slab fusions of an orbit scene differ by
+            # up to ~35 % at equal thickness (the centre carries more surface), so each rank times its
+            # own fusion, the times are all-gathered and the slabs re-cut; the grid is the same for any
+            # cut.  Untimed, like the warm-up steps.
+            for _ in range(args.rebalance_rounds):
+                fe = events()
+                tsdf_step(False, fe)
+                torch.cuda.synchronize()
+                slabs = sdist.rebalance_slabs(slabs, sdist.allgather_times(fe[0].elapsed_time(fe[1])), R)
+                z0, z1 = slabs[rank]
         wall_t, kms_t = timed(tsdf_step, args.steps, args.warmup, barrier)
         wall_t = max_over_ranks(wall_t, world, device)
         t_ms = wall_t / args.steps * 1e3
@@ -1169,7 +1189,10 @@ def main():
             "ms_per_step": t_ms, "scaling": "strong", "dtype": "f32",
             "config": {"workload": f"C5: {R}^3 grid x {TSDF_F} depth maps {syn.IMG_W}x{syn.IMG_H}",
                        "parallelism": f"z-slabs/{world}" + (" + 1 all-gather of the depth block table" if world > 1
-                                                             else "")},
+                                                             else ""),
+                       "slabs": [list(ab) for ab in slabs],
+                       "slab_cut": (f"re-cut from measured fusion times ({args.rebalance_rounds} rounds, "
+                                    "dist.rebalance_slabs)" if rebalance else "equal thickness")},
             "roofline": {"bound": "valu", "kernel": "tsdf_kernel + pre-passes", "kernel_ms": tk_ms, "unit": "TFLOP/s",
                          "achieved": 32.0 * local_upd / (tk_ms * 1e-3) / 1e12, "peak": PEAK_FP32_TFLOPS,
                          "frac": (32.0 * local_upd / (tk_ms * 1e-3) / 1e12) / PEAK_FP32_TFLOPS,

@@ -281,3 +281,63 @@ def test_uneven_slabs_allgather_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert all(v is True for v in res.values()), res
+
+
+def test_rebalance_slabs_properties():
+    """dist.rebalance_slabs (bench.py --gpus N's TSDF feedback balancing): the cut tiles
+    [0, D) in order; equal times keep equal slabs; a heavier centre gets thinner slabs;
+    the align grid is respected; malformed input is refused."""
+    R = 256
+    even = [sdist.shard_range(R, r, 8) for r in range(8)]
+    assert sdist.rebalance_slabs(even, [1.0] * 8, R) == even
+    t = [0.311, 0.298, 0.391, 0.373, 0.373, 0.366, 0.283, 0.3]   # measured N = 8 slab times (DESIGN §6c)
+    for align in (1, 8):
+        s = sdist.rebalance_slabs(even, t, R, align=align)
+        assert s[0][0] == 0 and s[-1][1] == R and all(s[i][1] == s[i + 1][0] for i in range(7))
+        assert all(a % align == 0 for a, _ in s)
+        width = [b - a for a, b in s]
+        if align == 1:
+            assert width[2] < 32 < width[0] and width[6] > 32
+        # the re-cut predicts (piecewise-constant density) a max slab cost below the measured max
+        dens = np.concatenate([[t[r] / 32] * 32 for r in range(8)])
+        assert max(dens[a:b].sum() for a, b in s) < max(t) - (0.01 if align == 1 else 0.0)
+    # an empty slab (world > layers) still yields a valid tiling
+    s = sdist.rebalance_slabs([(0, 0), (0, 4), (4, 4)], [0.0, 1.0, 0.0], 4)
+    assert s[0][0] == 0 and s[-1][1] == 4 and all(s[i][1] == s[i + 1][0] for i in range(2))
+    with pytest.raises(ValueError):
+        sdist.rebalance_slabs(even, [1.0] * 7, R)
+    with pytest.raises(ValueError):
+        sdist.rebalance_slabs([(0, 10), (12, 256)], [1.0, 1.0], R)
+
+
+def _worker_times(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        got = sdist.allgather_times(0.5 + rank)
+        slabs = sdist.rebalance_slabs([sdist.shard_range(64, r, world) for r in range(world)], got, 64)
+        q.put((rank, (got, slabs)))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_allgather_times_rebalance_gloo():
+    """Every rank sees every rank's time and so computes the same re-cut (world 2, gloo)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_times, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(isinstance(v, tuple) for v in res.values()), res
+    assert res[0] == res[1]
+    times, slabs = res[0]
+    assert times == [0.5, 1.5] and slabs[0][1] > 32   # the faster rank takes the thicker slab

@@ -1,8 +1,8 @@
-"""Phase breakdown of the fused BA solve kernel (variant 5) on C3's 256 pairs x 4096 obs.
+"""Phase breakdown of the BA solve kernel on C3's 256 pairs x 4096 obs (SFMHIP_BA_VARIANT as given).
 Needs the tool-only build (the phase timers are compiled out of the product library):
   hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -DSFMHIP_BA_PROF -shared \
         3d_reconstruction_amd/csrc/{lib,ba}.hip -o ab/libba_prof.so
-python tools/ba_phase_prof.py [variant: 4|5]"""
+python tools/ba_phase_prof.py [variant: 0..3]"""
 import ctypes
 import importlib
 import os
@@ -14,7 +14,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 syn = importlib.import_module("3d_reconstruction_amd.synthetic")
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ.setdefault("SFMHIP_BA_VARIANT", sys.argv[1] if len(sys.argv) > 1 else "5")
+os.environ.setdefault("SFMHIP_BA_VARIANT", sys.argv[1] if len(sys.argv) > 1 else "1")
 lib = ctypes.CDLL(os.path.join(root, "ab", "libba_prof.so"))
 P = ctypes.c_void_p
 lib.sfmhip_ba_solve.argtypes = [P, P, P, P, P, ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
@@ -27,8 +27,8 @@ off = torch.arange(257, dtype=torch.int64, device=dev) * 4096
 n = int(off[-1])
 cost = torch.empty(256, dtype=torch.float64, device=dev)
 nfev, njev, st = (torch.empty(256, dtype=torch.int32, device=dev) for _ in range(3))
-names = ["jacobian", "regularize", "ridge pass", "ridge chol", "gn pass", "gn serial", "tr solve", "trial pass",
-         "trial serial", "-"]
+names = ["jacobian (+X move)", "regularize", "ridge + chol", "gn pass", "subspace pass", "tr solve", "trial pass",
+         "trial serial", "-", "-"]
 for rep in range(3):
     cam, X = tt["cam"].clone(), tt["X"].clone()
     torch.cuda.synchronize()
@@ -47,6 +47,6 @@ t = buf.reshape(256, 10).astype(np.float64) * 10e-3   # 100 MHz ticks -> us
 print(f"variant {os.environ['SFMHIP_BA_VARIANT']}: kernel {ms:.3f} ms; nfev mean {nfev.float().mean().item():.2f} "
       f"njev mean {njev.float().mean().item():.2f}; per-pair phase sums (us): mean / max over pairs")
 tot = t.sum(1)
-for k, nm in enumerate(names[:9]):
+for k, nm in enumerate(names[:8]):
     print(f"  {nm:13s} {t[:, k].mean():8.1f} {t[:, k].max():8.1f}")
 print(f"  {'total':13s} {tot.mean():8.1f} {tot.max():8.1f}")

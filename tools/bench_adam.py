@@ -15,4 +15,4 @@ for k in range(12):
     e1.record(); torch.cuda.synchronize()
     ts.append(e0.elapsed_time(e1))
 ts = sorted(ts[2:])
-print(f"blocks={os.environ.get('SFMHIP_ADAM_BLOCKS', 'default')} adam n={n}: min {ts[0]:.3f} ms median {ts[len(ts)//2]:.3f} ms -> {32*n/ts[0]/1e6:.0f} GB/s (actual bytes incl pads)")
+print(f"adam n={n}: min {ts[0]:.3f} ms median {ts[len(ts)//2]:.3f} ms -> {32*n/ts[0]/1e6:.0f} GB/s (actual bytes incl pads)")

@@ -51,8 +51,19 @@ for n in [int(a) for a in sys.argv[1:]] or [8]:
                      reps=3) for f0, f1 in f_parts)
     plans = {"equal": [sdist.shard_range(R, r, n) for r in range(n)],
              "planned": sdist.plan_slabs(cost, n, layer=8, depth=R)}
+    def slab_times(slabs):
+        return [timed(lambda: sfm.tsdf_integrate(T, W, *args, z0, z1, block_table=full_tab)) if z1 > z0 else 0.0
+                for z0, z1 in slabs]
+
     for name, slabs in plans.items():
-        ts = [timed(lambda: sfm.tsdf_integrate(T, W, *args, z0, z1, block_table=full_tab)) if z1 > z0 else 0.0
-              for z0, z1 in slabs]
+        ts = slab_times(slabs)
         print(f"N={n} {name:8s}: fusion max {max(ts):.3f} ms mean {np.mean(ts):.3f} (+ table {t_tab:.3f}, "
               f"+ stats/rank {t_st:.3f}) slabs {slabs} ms {[round(t, 3) for t in ts]}", flush=True)
+    # feedback balancing as bench.py --gpus N does it (dist.rebalance_slabs on measured times, 3 rounds)
+    slabs = plans["equal"]
+    ts = slab_times(slabs)
+    for rnd in range(1, 4):
+        slabs = sdist.rebalance_slabs(slabs, ts, R)
+        ts = slab_times(slabs)
+        print(f"N={n} rebal {rnd} : fusion max {max(ts):.3f} ms mean {np.mean(ts):.3f} slabs {slabs} "
+              f"ms {[round(t, 3) for t in ts]}", flush=True)
