@@ -1,4 +1,4 @@
-# Round-2 PMC passes (tools/pmc.sh: SQ, clock + L2, FETCH_SIZE, WRITE_SIZE, each its own run)
+# PMC passes (round 2 onwards; TAG names the run) (tools/pmc.sh: SQ, clock + L2, FETCH_SIZE, WRITE_SIZE, each its own run)
 # for the C3 match launch, the C5 TSDF call and the V2+V4 render launch; summaries per kind.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"

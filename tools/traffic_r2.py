@@ -1,6 +1,6 @@
-"""Derive profiles/r2/traffic.json (HBM bytes per step of the dominant kernels)
+"""Derive profiles/<round>/traffic.json (HBM bytes per step of the dominant kernels)
 from a tools/gpu_traffic_r2.sh run, and copy the PMC summaries next to it.
-usage: python tools/traffic_r2.py <tag>"""
+usage: python tools/traffic_r2.py <tag> [round dir, default r2]"""
 import csv
 import glob
 import json
@@ -10,7 +10,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r2"
-src, dst = os.path.join(ROOT, "gpurun_out"), os.path.join(ROOT, "profiles", "r2")
+rnd = sys.argv[2] if len(sys.argv) > 2 else "r2"
+src, dst = os.path.join(ROOT, "gpurun_out"), os.path.join(ROOT, "profiles", rnd)
 os.makedirs(dst, exist_ok=True)
 traffic = {}
 for kind in ("match", "tsdf", "render"):
