@@ -1136,7 +1136,7 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
                                                    float trunc, SuperBrick SB, const unsigned* __restrict__ cull,
                                                    const unsigned* __restrict__ freem, int nw, float free_ts,
                                                    const float2* __restrict__ bmm, int nbu, int nbv,
-                                                   const unsigned* __restrict__ order, int easy, int prio) {
+                                                   const unsigned* __restrict__ order, int easy) {
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (SWZ) tsdf_slot_tile(order ? (int)order[blockIdx.x] : (int)blockIdx.x, gridDim.x, W, H, SB, bx, by, bz);
     const int l = threadIdx.x & 63;
@@ -1157,23 +1157,9 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
     const size_t slot = ((((size_t)bz * nty + by) * ntx + bx) * kCullSub + wave) * (size_t)nw;
     if (cull) {   // every frame of the launch culled for this wave: the grid is not even read
         unsigned any = 0u;
-        int nproj = 0;   // frames this wave projects (neither culled nor free space)
-        for (int w0 = 0; w0 < F; w0 += 32) {
-            const unsigned live = ~cull[slot + (w0 >> 5)] & (F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u));
-            any |= live;
-            nproj += __builtin_popcount(live & (freem ? ~freem[slot + (w0 >> 5)] : ~0u));
-        }
+        for (int w0 = 0; w0 < F; w0 += 32)
+            any |= ~cull[slot + (w0 >> 5)] & (F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u));
         if (__builtin_amdgcn_readfirstlane((int)any) == 0) return;
-        // Issue priority by the wave's own work: a surface wave projects most frames, its
-        // neighbours in free space or behind the surface few, and the call ends with the
-        // heavy waves' frame loops (all resident waves of a SIMD share its issue slots);
-        // the heavy ones issue first and the light ones fill the gaps.  Order only.
-        if (prio) {
-            nproj = __builtin_amdgcn_readfirstlane(nproj);
-            if (4 * nproj >= F) __builtin_amdgcn_s_setprio(3);
-            else if (8 * nproj >= F) __builtin_amdgcn_s_setprio(2);
-            else if (16 * nproj >= F) __builtin_amdgcn_s_setprio(1);
-        }
     }
     const size_t idx = ((size_t)z * H + y) * W + x;
     f2 tv = {T[idx], two ? T[idx + W] : 1.f};   // the absent voxel reads as T = 1, W = 0 (never stored)
@@ -2110,8 +2096,6 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const bool vox_test = cfree && env_int("SFMHIP_TSDF_VOXTEST", latency_mode ? 0 : 1) != 0;
     // division-free update of projected frames whose updates are all tsdf = 1 on T = 1 (SFMHIP_TSDF_EASY=0 off)
     const int easy = env_int("SFMHIP_TSDF_EASY", 1) != 0;
-    // issue priority of each fusion wave from its projected-frame count (SFMHIP_TSDF_PRIO=0 off)
-    const int prio = env_int("SFMHIP_TSDF_PRIO", 1) != 0;
     // latency mode without the block table: gathers one projected frame ahead (SFMHIP_TSDF_PIPE=0 off)
     const bool pipe = !vox_test && latency_mode && env_int("SFMHIP_TSDF_PIPE", 1) != 0;
     // longest-first workgroup order (SFMHIP_TSDF_ORDER=0 off): needs the masks and the 1-D slot grid;
@@ -2213,14 +2197,13 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         }
         if (swz && pipe)
             hipLaunchKernelGGL((tsdf_kernel<true, true>), grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
-                               Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, nullptr, nbu, nbv, ord, easy, prio);
+                               Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, nullptr, nbu, nbv, ord, easy);
         else if (swz)
             hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, ord, easy, prio);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, ord, easy);
         else
             hipLaunchKernelGGL(tsdf_kernel<false>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, nullptr, easy,
-                               prio);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, nullptr, easy);
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }
