@@ -1108,6 +1108,13 @@ __global__ __launch_bounds__(256) void tsdf_order_kernel(int nslots, int W, int 
     }
 }
 
+#ifdef SFMHIP_TSDF_PROF
+// tool-only build (tools/tsdf_wave_prof.py): per fusion wave {start, end} wall clock (100 MHz)
+// and its projected-frame count; never in the product library
+constexpr int kTsdfProfWaves = 1 << 18;
+__device__ unsigned long long g_tsdf_prof[kTsdfProfWaves * 3];
+#endif
+
 // W may take k more exact +1 steps with T = 1 fixed when it is an integer in [0, 2^24 - 512].
 // Updates only add 1 to W (general or division-free; W + 1 is exact below 2^24), at most
 // kTsdfMaxFrames = 512 per launch, so a W that starts the launch an integer in
@@ -1137,6 +1144,12 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
                                                    const unsigned* __restrict__ freem, int nw, float free_ts,
                                                    const float2* __restrict__ bmm, int nbu, int nbv,
                                                    const unsigned* __restrict__ order, int easy) {
+#ifdef SFMHIP_TSDF_PROF
+    const unsigned long long prof_t0 = wall_clock64();
+    int prof_nproj = 0;
+    const int prof_w = (int)(((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 +
+                       (int)(threadIdx.x >> 6);
+#endif
     int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (SWZ) tsdf_slot_tile(order ? (int)order[blockIdx.x] : (int)blockIdx.x, gridDim.x, W, H, SB, bx, by, bz);
     const int l = threadIdx.x & 63;
@@ -1213,6 +1226,9 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
         };
         struct Proj { f2 Zc, dep; bool ok0, ok1; };
         auto project = [&](int f) -> Proj {   // projection + the (issued) depth gather
+#ifdef SFMHIP_TSDF_PROF
+            ++prof_nproj;
+#endif
             const float* r = rec + f * 16;
             const f2 Q = (f2{r[0], r[1]} * f2s(vx) + f2{r[2], r[3]} * f2s(vz)) + f2{r[4], r[5]};
             const float Qz = (r[6] * vx + r[7] * vz) + r[8];
@@ -1312,6 +1328,9 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
             }
             const int f = w0 + __builtin_ctz(todo);
             todo &= todo - 1u;
+#ifdef SFMHIP_TSDF_PROF
+            ++prof_nproj;
+#endif
             const float* r = rec + f * 16;   // uniform: scalar loads
             const f2 Q = (f2{r[0], r[1]} * f2s(vx) + f2{r[2], r[3]} * f2s(vz)) + f2{r[4], r[5]};
             const float Qz = (r[6] * vx + r[7] * vz) + r[8];
@@ -1381,6 +1400,13 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
         T[idx + W] = tv.y;
         Wt[idx + W] = wv.y;
     }
+#ifdef SFMHIP_TSDF_PROF
+    if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63)) && prof_w < kTsdfProfWaves) {
+        g_tsdf_prof[3 * prof_w] = prof_t0;
+        g_tsdf_prof[3 * prof_w + 1] = wall_clock64();
+        g_tsdf_prof[3 * prof_w + 2] = (unsigned long long)prof_nproj;
+    }
+#endif
 }
 
 static int env_int(const char* name, int dflt) {
@@ -2380,3 +2406,17 @@ extern "C" int sfmhip_stratified_samples(const float* t_near, const float* t_far
                        t_rand, B, S, perturb, z);
     return check_launch("stratified_kernel");
 }
+
+#ifdef SFMHIP_TSDF_PROF
+extern "C" int sfmhip_tsdf_prof_read(unsigned long long* host, int n_waves, int clear) {
+    const int n = std::min(n_waves, kTsdfProfWaves) * 3;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tsdf_prof), (size_t)n * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    if (clear) {
+        static std::vector<unsigned long long> z((size_t)kTsdfProfWaves * 3, 0ull);
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tsdf_prof), z.data(), z.size() * sizeof(unsigned long long)) != hipSuccess)
+            return -1;
+    }
+    return 0;
+}
+#endif
