@@ -2221,8 +2221,14 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             hipLaunchKernelGGL(tsdf_order_kernel, dim3(kNumXcd), dim3(256), (size_t)ceil_div((int)grid.x, kNumXcd), st,
                                (int)grid.x, W, H, z0, z1, sb, nf, tcost, ord);
         }
+#ifdef SFMHIP_TSDF_PROF
+        // probe build: dynamic LDS per fusion workgroup to cap the resident waves (occupancy experiments)
+        const size_t prof_lds = (size_t)env_int("SFMHIP_TSDF_PROF_LDS", 0);
+#else
+        constexpr size_t prof_lds = 0;
+#endif
         if (swz && pipe)
-            hipLaunchKernelGGL((tsdf_kernel<true, true>), grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
+            hipLaunchKernelGGL((tsdf_kernel<true, true>), grid, dim3(256), prof_lds, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
                                Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, nullptr, nbu, nbv, ord, easy);
         else if (swz)
             hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,

@@ -4,7 +4,8 @@ grid and for N = 8 slabs 2 (heavy) and 6 (light).  Shows whether a call is bound
 throughput (waves end evenly) or by its longest waves' frame loops.
   hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -DSFMHIP_TSDF_PROF -shared \\
         -c voxel.hip -o voxel_prof.o, linked with the other objects of the Makefile into ab/libtsdf_prof.so
-python tools/tsdf_wave_prof.py"""
+python tools/tsdf_wave_prof.py   (SFMHIP_TSDF_PROF_LDS=bytes: dynamic LDS per slab fusion workgroup,
+                                  capping the resident waves, to tell latency- from issue-bound waves)"""
 import ctypes
 import importlib
 import os
@@ -67,7 +68,8 @@ def run(label, fn):
           + " / ".join(str(int(((st <= f * span) & (en > f * span)).sum())) for f in (0.5, 0.75, 0.9)), flush=True)
 
 
-run("whole grid", lambda: sfm.tsdf_integrate(T, W, *args))
+if os.environ.get("SFMHIP_TSDF_PROF_LDS", "0") == "0":
+    run("whole grid", lambda: sfm.tsdf_integrate(T, W, *args))
 for r in (2, 6):
     z0, z1 = sdist.shard_range(R, r, 8)
     run(f"N=8 slab {r} [{z0},{z1})", lambda: sfm.tsdf_integrate(T, W, *args, z0, z1, block_table=tab))
