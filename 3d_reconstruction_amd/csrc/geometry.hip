@@ -247,7 +247,8 @@ __device__ inline bool dlt_point_qr3(const double* P0, const double* P1, double 
 #pragma unroll
             for (int q = p + 1; q < 3; ++q) {
                 const double gpq = G[p][q];
-                if (fabs(gpq) <= 1e-18 * sqrt_nr(fabs(G[p][p] * G[q][q])) || gpq == 0.0) continue;
+                // |g_pq| <= 1e-18 sqrt(|g_pp g_qq|), squared: no square root on the rotation chain
+                if (gpq * gpq <= 1e-36 * fabs(G[p][p] * G[q][q])) continue;
                 rotated = true;
                 const double zeta = (G[q][q] - G[p][p]) * (0.5 * rcp_nr(gpq));
                 const double t = (zeta >= 0.0 ? 1.0 : -1.0) * rcp_nr(fabs(zeta) + sqrt_nr(fma(zeta, zeta, 1.0)));
