@@ -12,10 +12,11 @@
 //   * image b streams through LDS in 128-row blocks (XOR-swizzled, double
 //     buffered); v_mfma_i32_32x32x32_i8 computes C'[j][i] = <b_j, a_i>, so a
 //     lane owns ONE query row i and sixteen candidate rows j per tile.
-//   * fused epilogue, 3 VALU ops per distance: packed key
+//   * fused epilogue, <= 2.5 VALU ops per distance: packed key
 //        k = (dot << 8) + keys[j],  keys[j] = (-|b_j|^2 << 7) | (127 - j%128)
 //     i.e. k = ((2 dot - |b_j|^2) << 7) | (127 - j%128); larger k = smaller
-//     distance, lower index on ties.  top-2 per lane via max + med3; blocks
+//     distance, lower index on ties.  top-2 per lane via max3 + med3 + max per
+//     two candidates; blocks
 //     merge into (best key, best index, second key) with explicit index order.
 //   * nothing of the M x N distance matrix is ever written.
 #include "common.h"
@@ -39,6 +40,11 @@ __device__ __forceinline__ int swz_off(int r, int c) {
     return r * D + ((c ^ ((r / RPB) % CPR)) << 4);
 }
 
+__device__ __forceinline__ int max3i(int a, int b, int c) {
+    int r;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __device__ __forceinline__ int med3i(int a, int b, int c) {
     int r;
     asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -296,13 +302,18 @@ __global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
 #pragma unroll
             for (int g = 0; g < M::NREG / 4; ++g) {
                 const i32x4 kv = *reinterpret_cast<const i32x4*>(kl + jt * MF + M::row(4 * g, grp));
+                // two candidates per step: with t1 >= t2 the top two of {t1, t2, ka, kb} (distinct
+                // keys) are max3(t1, ka, kb) and max(t2, med3(t1, ka, kb)) — 5 VALU per 2 distances
+                // (2 packings + med3 + max3 + max) instead of 6; the same keys, so the same result
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < 4; e += 2) {
 #pragma unroll
                     for (int s = 0; s < NS; ++s) {
-                        const int kx = acc[s][4 * g + e] * 256 + kv[e];
-                        t2[s] = med3i(t2[s], kx, t1[s]);
-                        t1[s] = max(t1[s], kx);
+                        const int ka = acc[s][4 * g + e] * 256 + kv[e];
+                        const int kb = acc[s][4 * g + e + 1] * 256 + kv[e + 1];
+                        const int m = med3i(t1[s], ka, kb);
+                        t1[s] = max3i(t1[s], ka, kb);
+                        t2[s] = max(t2[s], m);
                     }
                 }
             }
