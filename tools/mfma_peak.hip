@@ -1,7 +1,9 @@
 // mfma_peak.hip — diagnostic: the int8 MFMA rate this MI355X sustains on
 // random register operands, with and without the matcher's 3-op epilogue per
 // output element (no LDS, no global traffic in the loop).  Gives the practical
-// ceiling (clock under load) the match kernel is compared against.
+// ceiling (clock under load) the match kernel is compared against.  The 16x16x64
+// epilogue is the matcher's current one (two candidates per top-2 step, ~2.5 VALU per
+// distance); the 32x32x32 kernel keeps the older 3-op form (max + med3 per candidate).
 // KS = MFMA k-steps per epilogue: d = 256 (C3) is 8 steps of 32x32x32 or 4 of
 // 16x16x64; d = 128 (C2) half that, so the epilogue weighs twice as much.
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/mfma_peak tools/mfma_peak.hip
@@ -15,6 +17,11 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
+__device__ __forceinline__ int max3i(int a, int b, int c) {
+    int r;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __device__ __forceinline__ int med3i(int a, int b, int c) {
     int r;
     asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -78,14 +85,15 @@ __global__ __launch_bounds__(256, 2) void kern16(const int* __restrict__ seed, i
         for (int k = 0; k < KS; ++k)
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[k], b[t][k], acc[t], 0, 0, 0);
-        if (EPI) {
+        if (EPI) {   // the matcher's epilogue: two candidates per top-2 step (max3 + med3 + max)
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int ka = acc[t][q] * 256 + kv;
-                    t2[t] = med3i(t2[t], ka, t1[t]);
-                    t1[t] = max(t1[t], ka);
+                for (int q = 0; q < 4; q += 2) {
+                    const int ka = acc[t][q] * 256 + kv, kb = acc[t][q + 1] * 256 + kv + 1;
+                    const int m = med3i(t1[t], ka, kb);
+                    t1[t] = max3i(t1[t], ka, kb);
+                    t2[t] = max(t2[t], m);
                 }
         } else {
 #pragma unroll
