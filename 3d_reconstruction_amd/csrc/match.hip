@@ -917,7 +917,7 @@ __global__ __launch_bounds__(WAVES * 64) void vq_f32r_kernel(const double* __res
             const double xr = __shfl(xn, 4 * kq + g);   // lane 4kq+g holds |x|^2 of that row
             const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax) +
                                vq_eps_abs(DP, sqrt(xr), cmax);
-            win[g] = ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
+            win[g] = PROBE == 4 ? (4 * kq + g) % n_codes : ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
         }
         int w = -1;   // row r16's verdict: group r16 >> 2, entry r16 & 3
 #pragma unroll
@@ -934,6 +934,204 @@ __global__ __launch_bounds__(WAVES * 64) void vq_f32r_kernel(const double* __res
             part = __builtin_fma(d0, d0, part);
             part = __builtin_fma(d1, d1, part);
             if ((s2 & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // 4 codeword loads in flight (VGPRs)
+        }
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+        if (kq == 0 && o < n_obs) {
+            if (w >= 0) {
+                codes[o] = w;
+                dist[o] = sqrt(part);
+            } else {
+                amb[atomicAdd(namb, 1u)] = (unsigned)o;
+            }
+        }
+    }
+}
+
+// vq, d = 128, <= 256 codewords: the same exact decision with the filter's products on the
+// f16 matrix cores (v_mfma_f32_16x16x32_f16, 16x the f32 matrix rate).  Each input is split
+// v = v_hi + v_lo, v_hi = fl16(v), v_lo = fl16(v - v_hi), and x.c is taken as
+// x_hi.c_hi + x_hi.c_lo + x_lo.c_hi (three MFMAs per k-block, f32 accumulation; f16 x f16
+// products are exact in f32).  Error of the score s_j = fl32(|c_j|^2) - 2 (x.c_j)~ against
+// |c_j|^2 - 2 x.c_j, with u = 2^-24 and |v - v_hi - v_lo| <= 2^-22 |v| + 2^-25 (the two
+// roundings to f16, f64 -> f32 -> f16 rounding twice, 2^-25 the f16 subnormal half-ulp):
+//   dropped x_hi.c_e + x_lo.c_lo + x_lo.c_e + x_e.c (c_e, x_e the split remainders):
+//   <= 2 (3 2^-22 |x| cmax + 2^-25 sqrt(d) (|x| + cmax) + d 2^-48); the f32 accumulation of 3d
+//   products (any order, truncating or not) <= 2 3d 2u |x| cmax (1 + 2^-9); the norm and the
+//   final subtraction: 2u (cmax^2 + 2 |x| cmax);
+// so eps16 = 1.01 (2 |x| cmax (3 2^-22 + 6d u + 4u) + 4u cmax^2 + 2^-24 sqrt(d) (|x| + cmax)
+// + 2 d 2^-48) + the subnormal term of the f32 path.  Inputs of magnitude >= 2^15 (f16
+// overflow) decide nothing: such an observation, or every observation when the codebook
+// holds one, goes to the exact pass.  Layout as vq_f32r_kernel: a wave owns 16 observations,
+// lane (r, q) holds row r's f64 values k = 8 t + 2 q + {0, 1} (64 contiguous bytes per row
+// per load); fragment b element j of the MFMA is k = 8 (4 b + j / 2) + 2 q + j % 2 (the dot
+// product's k order is free), and the codebook sits in LDS in that order
+// ([block][k-block][hi/lo][lane], 8 halves per lane: one ds_read_b128 per operand).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kVqhWaves = 8;
+__device__ __forceinline__ double vq_eps16(int DP, double xn, double cmax) {
+    const double u = 0x1p-24;
+    return 1.01 * (2.0 * xn * cmax * (0x1.8p-21 + 6.0 * DP * u + 4.0 * u) + 4.0 * u * cmax * cmax +
+                   0x1p-24 * sqrt((double)DP) * (xn + cmax) + 2.0 * DP * 0x1p-48) +
+           vq_eps_abs(DP, xn, cmax);
+}
+template <int PROBE, int WAVES = kVqhWaves>   // WAVES > 8: no prefetch (A/B); timing ablations only, never the product: 1 no HBM loads, 2 no winner codeword
+                      // loads, 4 no matrix-core pass (every row takes codeword r % n_codes)
+__global__ __launch_bounds__(WAVES * 64) void vq_f16s_kernel(const double* __restrict__ obs, int64_t n_obs,
+                                                                  const double* __restrict__ code, int n_codes,
+                                                                  int32_t* __restrict__ codes,
+                                                                  double* __restrict__ dist,
+                                                                  unsigned* __restrict__ amb,
+                                                                  unsigned* __restrict__ namb) {
+    constexpr int DP = 128, KB = 4, KS = 32;
+    extern __shared__ f32x4 smh[];
+    const int ncb = (n_codes + 15) >> 4;           // codeword blocks of 16
+    const int ncp = (ncb + 1) & ~1;                // LDS blocks (even count)
+    f16x8* sc = reinterpret_cast<f16x8*>(smh);     // [ncp][KB][2 (hi, lo)][64]
+    float* sn = reinterpret_cast<float*>(smh + ncp * KB * 2 * 64);   // [ncp * 16] squared norms
+    __shared__ unsigned s_cmax, s_big;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r16 = lane & 15, kq = lane >> 4;
+    if (threadIdx.x == 0) { s_cmax = 0u; s_big = 0u; }
+    __syncthreads();
+    for (int t = threadIdx.x; t < ncp * KB * 64; t += blockDim.x) {
+        const int ln = t & 63, kb = (t >> 6) % KB, cb = t / (KB * 64);
+        const int j = cb * 16 + (ln & 15), k0 = 32 * kb + 2 * (ln >> 4);
+        f16x8 hi, lo;
+        bool big = false;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {   // fragment element e <-> k = 8 (4 kb + e / 2) + 2 q + e % 2
+            const double v = j < n_codes ? code[(size_t)j * DP + k0 + 8 * (e >> 1) + (e & 1)] : 0.0;
+            big |= !(fabs(v) < 32768.0);
+            const _Float16 h = (_Float16)(float)v;
+            hi[e] = h;
+            lo[e] = (_Float16)(float)(v - (double)h);
+        }
+        if (big) s_big = 1u;
+        sc[((cb * KB + kb) * 2 + 0) * 64 + ln] = hi;
+        sc[((cb * KB + kb) * 2 + 1) * 64 + ln] = lo;
+    }
+    for (int r = threadIdx.x; r < ncp * 16; r += blockDim.x) {
+        double q = 0.0;
+        if (r < n_codes)
+            for (int k = 0; k < DP; ++k) q = __builtin_fma(code[(size_t)r * DP + k], code[(size_t)r * DP + k], q);
+        sn[r] = r < n_codes ? (float)q : __builtin_inff();   // padded codewords never win
+        if (r < n_codes) atomicMax(&s_cmax, __float_as_uint((float)sqrt(q) * 1.001f));
+    }
+    __syncthreads();
+    const double cmax = (double)__uint_as_float(s_cmax);
+    const bool book_big = s_big != 0u;
+    const int64_t n_units = (n_obs + 15) >> 4;
+    constexpr bool kPre = WAVES <= 8;   // the prefetch needs the VGPRs of 2 waves per SIMD
+    const int64_t ustep = (int64_t)gridDim.x * WAVES;
+    f64x2 nx[KS / 2];   // the next unit's observations, in flight while this unit computes
+    auto fetch = [&](int64_t un) {
+        const f64x2* xp = reinterpret_cast<const f64x2*>(obs + min(un * 16 + r16, n_obs - 1) * DP) + kq;
+#pragma unroll
+        for (int t = 0; t < KS / 2; ++t)   // 64 B per row
+            nx[t] = PROBE == 1 ? f64x2{(double)(lane + un) * 0x1p-10, (double)t * 0x1p-10}
+                               : __builtin_nontemporal_load(xp + 4 * t);
+    };
+    if (kPre) fetch(min((int64_t)blockIdx.x * WAVES + wave, n_units - 1));
+    for (int64_t un = (int64_t)blockIdx.x * WAVES + wave; un < n_units; un += ustep) {
+        if (!kPre) fetch(un);
+        const int64_t o = un * 16 + r16;
+        double x[KS];   // x[2 t + e] = row r16, k = 8 t + 2 kq + e (fragment b, element j: x[8 b + j])
+#pragma unroll
+        for (int s2 = 0; s2 < KS / 2; ++s2) {
+            x[2 * s2] = nx[s2].x;
+            x[2 * s2 + 1] = nx[s2].y;
+        }
+        if (kPre) fetch(min(un + ustep, n_units - 1));
+        double xn = 0.0;
+        bool big = book_big;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            xn = __builtin_fma(x[s], x[s], xn);
+            big |= !(fabs(x[s]) < 32768.0);
+        }
+        xn += __shfl_xor(xn, 16);
+        xn += __shfl_xor(xn, 32);   // |x|^2 of row r16, in every lane group
+        f16x8 ah[KB], al[KB];
+#pragma unroll
+        for (int b = 0; b < KB; ++b)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const _Float16 h = (_Float16)(float)x[8 * b + e];
+                ah[b][e] = h;
+                al[b][e] = (_Float16)(float)(x[8 * b + e] - (double)h);
+            }
+        float b1[4], b2[4];
+        int i1[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) { b1[g] = b2[g] = __builtin_inff(); i1[g] = INT_MAX; }
+        auto take = [&](int g, float dd, int j) {   // branch-free top-2 (selects)
+            const bool l = dd < b1[g];
+            b2[g] = l ? b1[g] : fminf(dd, b2[g]);
+            i1[g] = l ? j : i1[g];
+            b1[g] = l ? dd : b1[g];
+        };
+        for (int cb = 0; cb < (PROBE == 4 ? 0 : ncb); cb += 2) {   // two blocks per pass (the odd last one's partner is padding)
+            const f16x8* bp = sc + cb * KB * 2 * 64 + lane;
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+            for (int b = 0; b < KB; ++b) {
+                const f16x8 c0h = bp[(b * 2 + 0) * 64], c0l = bp[(b * 2 + 1) * 64];
+                const f16x8 c1h = bp[((KB + b) * 2 + 0) * 64], c1l = bp[((KB + b) * 2 + 1) * 64];
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c0h, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c1h, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c0l, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c1l, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[b], c0h, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[b], c1h, acc1, 0, 0, 0);
+            }
+            const int j0 = cb * 16 + r16;
+            const float cn0 = sn[j0], cn1 = sn[j0 + 16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {   // C row 4 kq + g (observation), columns j0, j0 + 16
+                take(g, cn0 - 2.f * acc0[g], j0);
+                take(g, cn1 - 2.f * acc1[g], j0 + 16);
+            }
+        }
+        int win[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            float v1 = b1[g], v2 = b2[g];
+            int x1 = i1[g];
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) {   // top-2 over the 16 codeword lanes
+                const float o1 = __shfl_xor(v1, off, 16), o2 = __shfl_xor(v2, off, 16);
+                const int ox = __shfl_xor(x1, off, 16);
+                const bool t = o1 < v1 || (o1 == v1 && ox < x1);
+                v2 = t ? fminf(v1, o2) : fminf(o1, v2);
+                v1 = t ? o1 : v1;
+                x1 = t ? ox : x1;
+            }
+            const double xr = __shfl(xn, 4 * kq + g);   // lane 4kq+g holds |x|^2 of that row
+            const double eps = vq_eps16(DP, sqrt(xr), cmax);
+            win[g] = PROBE == 4 ? (4 * kq + g) % n_codes : ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
+        }
+        int w = -1;   // row r16's verdict: group r16 >> 2, entry r16 & 3
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int t = __shfl(win[g], (r16 >> 2) << 4);
+            if ((r16 & 3) == g) w = t;
+        }
+        // an out-of-range input anywhere in the row (any lane group) decides nothing
+        const bool rbig = __shfl_xor((int)big, 16) | __shfl_xor((int)big, 32) | __shfl_xor((int)big, 48) | big;
+        if (rbig) w = -1;
+        const f64x2* cp = reinterpret_cast<const f64x2*>(code + (size_t)max(w, 0) * DP) + kq;
+        double part = 0.0;
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const f64x2 c = PROBE == 2 ? f64x2{x[8 * b + 2 * t + 1], x[8 * b + 2 * t]} : cp[4 * (4 * b + t)];
+                const double d0 = x[8 * b + 2 * t] - c.x, d1 = x[8 * b + 2 * t + 1] - c.y;
+                part = __builtin_fma(d0, d0, part);
+                part = __builtin_fma(d1, d1, part);
+            }
+            __builtin_amdgcn_sched_barrier(0);   // 4 codeword loads in flight (VGPRs)
         }
         part += __shfl_xor(part, 16);
         part += __shfl_xor(part, 32);
@@ -1308,12 +1506,13 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
     SFMHIP_REQUIRE(n_obs >= 0 && n_codes > 0 && d > 0 && d <= 256, "sfmhip_vq: bad shape (d <= 256)");
     if (n_obs == 0) return SFMHIP_OK;
     const char* venv = std::getenv("SFMHIP_VQ_VARIANT");    // 1: the FMA difference-form kernel (A/B runs)
-    const int variant = venv ? std::atoi(venv) : 0;          // 3: the f64-MFMA GEMM-form kernel (A/B runs)
-    if (d == 128 && n_codes <= 256 && (variant == 0 || variant == 4)) {   // 4: vq_f32f_kernel (A/B runs)
-        const bool reg = variant == 0;
+    const int variant = venv ? std::atoi(venv) : 6;          // 3: the f64-MFMA GEMM-form kernel (A/B runs)
+    if (d == 128 && n_codes <= 256 && (variant == 0 || variant == 4 || variant == 6)) {   // 6 (default): vq_f16s_kernel
+        const bool reg = variant == 0, half = variant == 6;   // 0: vq_f32r_kernel, 4: vq_f32f_kernel (A/B runs)
         const int ncb = ceil_div(n_codes, 16), ncp = ceil_div(n_codes, 32) * 2;
-        const size_t shm = reg ? (size_t)ncp * 16 * (128 + 1) * sizeof(float)
-                               : (size_t)ncb * 16 * (128 + 4 + 1) * sizeof(float);
+        const size_t shm = half ? (size_t)ncp * 4 * 2 * 64 * 16 + (size_t)ncp * 16 * sizeof(float)
+                           : reg ? (size_t)ncp * 16 * (128 + 1) * sizeof(float)
+                                 : (size_t)ncb * 16 * (128 + 4 + 1) * sizeof(float);
         hipStream_t s = as_stream(stream);
         unsigned* amb = nullptr;
         if (scratch_alloc((void**)&amb, (size_t)(n_obs + 1) * sizeof(unsigned), s) == hipSuccess &&
@@ -1324,7 +1523,22 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
             if (hipGetDevice(&dev) == hipSuccess)
                 (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
             int rc;
-            if (reg) {
+            if (half) {
+                const char* penv = std::getenv("SFMHIP_VQ_PROBE");   // timing ablations (tools/bench_vq.py)
+                const int probe = penv ? std::atoi(penv) : 0;
+                const int waves = probe == 5 ? 12 : probe == 6 ? 16 : kVqhWaves;
+                const int64_t n_wg = ((n_obs + 15) / 16 + waves - 1) / waves;
+                auto kern = probe == 1   ? vq_f16s_kernel<1>
+                            : probe == 2 ? vq_f16s_kernel<2>
+                            : probe == 4 ? vq_f16s_kernel<4>
+                            : probe == 5 ? vq_f16s_kernel<0, 12>
+                            : probe == 6 ? vq_f16s_kernel<0, 16> : vq_f16s_kernel<0>;
+                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+                hipLaunchKernelGGL(kern, dim3((unsigned)std::min<int64_t>(n_wg, n_cu)),
+                                   dim3(waves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
+                                   namb);
+                rc = check_launch("vq_f16s_kernel");
+            } else if (reg) {
                 const char* penv = std::getenv("SFMHIP_VQ_PROBE");   // timing ablations (tools/bench_vq.py)
                 const int probe = penv ? std::atoi(penv) : 0;
                 const int waves = probe == 5 ? 16 : kVqrWaves;

@@ -440,10 +440,15 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
     fl = 2 * obs.shape[0] * 200 * 128 / (np.mean(kms) * 1e-3) / 1e12
     line = {"metric": "vq obs/sec", "value": obs.shape[0] / (ms * 1e-3), "unit": "obs/s", "ms_per_step": ms,
             "config": {"workload": "M2 vq (matching.py:27): 257x4096 obs x 200 codes x 128-d, f64"},
-            # GEMM form: 2 flops per (obs, codeword, dim) on v_mfma_f32_16x16x4_f32 (f32 filter
-            # with a proven error bound; undecided observations settled in f64)
-            "roofline": {"bound": "mfma", "kernel": "vq_f32r_kernel+vq_exact_kernel", "kernel_ms": float(np.mean(kms)),
-                         "unit": "TFLOP/s", "achieved": fl, "peak": PEAK_FP32_TFLOPS, "frac": fl / PEAK_FP32_TFLOPS}}
+            # f16-split filter on v_mfma_f32_16x16x32_f16 (3 MFMAs per product, proven error bound;
+            # undecided observations settled in f64): the f64 observation stream (n*d*8 B, read once)
+            # plus codes + distances written is the bound — 3 x 2nkd f16 flops take 0.07 ms at the
+            # dense f16 peak, the stream 0.14 ms at 8 TB/s
+            "roofline": {"bound": "hbm", "kernel": "vq_f16s_kernel+vq_exact_kernel", "kernel_ms": float(np.mean(kms)),
+                         "unit": "GB/s", "compulsory_bytes": obs.shape[0] * (128 * 8 + 12),
+                         "achieved": obs.shape[0] * (128 * 8 + 12) / (np.mean(kms) * 1e-3) / 1e9,
+                         "peak": PEAK_HBM_GBS, "frac": obs.shape[0] * (128 * 8 + 12) / (np.mean(kms) * 1e-3) / 1e9
+                         / PEAK_HBM_GBS, "gemm_tflops_2nkd": fl}}
     if cpu:
         from scipy.cluster.vq import vq as scipy_vq
         oo, bb = obs[:65536].cpu().numpy(), book.cpu().numpy()
