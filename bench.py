@@ -448,7 +448,8 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
                          "unit": "GB/s", "compulsory_bytes": obs.shape[0] * (128 * 8 + 12),
                          "achieved": obs.shape[0] * (128 * 8 + 12) / (np.mean(kms) * 1e-3) / 1e9,
                          "peak": PEAK_HBM_GBS, "frac": obs.shape[0] * (128 * 8 + 12) / (np.mean(kms) * 1e-3) / 1e9
-                         / PEAK_HBM_GBS, "gemm_tflops_2nkd": fl}}
+                         / PEAK_HBM_GBS, "gemm_tflops_2nkd": fl, "traffic": pmc_traffic("vq"),
+                         "traffic_unit": "bytes per call (FETCH_SIZE*2 + WRITE_SIZE, profiles/r3/traffic.json)"}}
     if cpu:
         from scipy.cluster.vq import vq as scipy_vq
         oo, bb = obs[:65536].cpu().numpy(), book.cpu().numpy()
@@ -846,7 +847,13 @@ def ba_solve_line(sfm, syn, device, args, barrier, cpu=True):
                          "achieved_gbs": BA_PAIRS * BA_OBS * BA_BYTES_OBS / (k_ms * 1e-3) / 1e9,
                          "count": f"sum over pairs of n_obs x (njev x {F_BA_J_OBS:.0f} + nfev x {F_BA_STEP_OBS:.0f}) "
                                   f"fp64 flops; compulsory bytes {BA_BYTES_OBS:.0f} per observation per solve "
-                                  f"(achieved_gbs): the fp64 bound is the larger"}}
+                                  f"(achieved_gbs): the fp64 bound is the larger",
+                         # the record passes re-read each observation's 26-double scratch record ~20 times
+                         # per solve: measured L2-miss traffic, the rate the kernel actually moves
+                         "traffic": pmc_traffic("ba"),
+                         "traffic_gbs": (pmc_traffic("ba") or 0.0) / (k_ms * 1e-3) / 1e9,
+                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r3/traffic.json, "
+                                         "pmc_ba.txt)"}}
     # sfm.py:37-38 left exactly as written (scipy least_squares, jac_sparsity=ba_sparse, 2-point FD) with
     # only `import sfmhip as cv2`: every residual evaluation is one sfmhip.projectPoints call (host <->
     # device round trip); scipy's TRF / LSMR stay on the host.  Wall time per pair on one C3 pair.
