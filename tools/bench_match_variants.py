@@ -18,8 +18,9 @@ n_img = int(os.environ.get("N_IMG", "257"))
 d = int(os.environ.get("DIM", "256"))
 m = int(os.environ.get("MKPT", "4096"))
 dev = torch.device("cuda", 0)
-x = syn.superpoint_like(n_img, m, d, seed=1, device=dev)
-bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_FLOAT)
+sift = os.environ.get("DATA", "float") == "sift"   # DATA=sift: bench.py's C2 operands (MODE_SIFT)
+x = (syn.sift_like if sift else syn.superpoint_like)(n_img, m, d, seed=0 if sift else 1, device=dev)
+bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_SIFT if sift else sfm.MODE_FLOAT)
 del x
 pairs = torch.from_numpy(sfm.all_pairs(n_img)).to(dev)
 P = pairs.shape[0]
