@@ -917,7 +917,7 @@ __global__ __launch_bounds__(WAVES * 64) void vq_f32r_kernel(const double* __res
             const double xr = __shfl(xn, 4 * kq + g);   // lane 4kq+g holds |x|^2 of that row
             const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax) +
                                vq_eps_abs(DP, sqrt(xr), cmax);
-            win[g] = PROBE == 4 ? (4 * kq + g) % n_codes : ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
+            win[g] = PROBE == 4 || PROBE >= 7 ? (4 * kq + g) % n_codes : ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
         }
         int w = -1;   // row r16's verdict: group r16 >> 2, entry r16 & 3
 #pragma unroll
@@ -951,33 +951,48 @@ __global__ __launch_bounds__(WAVES * 64) void vq_f32r_kernel(const double* __res
 // vq, d = 128, <= 256 codewords: the same exact decision with the filter's products on the
 // f16 matrix cores (v_mfma_f32_16x16x32_f16, 16x the f32 matrix rate).  Each input is split
 // v = v_hi + v_lo, v_hi = fl16(v), v_lo = fl16(v - v_hi), and x.c is taken as
-// x_hi.c_hi + x_hi.c_lo + x_lo.c_hi (three MFMAs per k-block, f32 accumulation; f16 x f16
-// products are exact in f32).  Error of the score s_j = fl32(|c_j|^2) - 2 (x.c_j)~ against
+// x_hi.c_hi + (x_hi.c_lo + x_lo.c_hi): the main products in one f32 accumulator, the two
+// correction products (each <= 2^-11 of a main one) in a second, added at the end; f16 x f16
+// products are exact in f32.  Error of the score s_j = fl32(|c_j|^2) - 2 (x.c_j)~ against
 // |c_j|^2 - 2 x.c_j, with u = 2^-24 and |v - v_hi - v_lo| <= 2^-22 |v| + 2^-25 (the two
 // roundings to f16, f64 -> f32 -> f16 rounding twice, 2^-25 the f16 subnormal half-ulp):
 //   dropped x_hi.c_e + x_lo.c_lo + x_lo.c_e + x_e.c (c_e, x_e the split remainders):
-//   <= 2 (3 2^-22 |x| cmax + 2^-25 sqrt(d) (|x| + cmax) + d 2^-48); the f32 accumulation of 3d
-//   products (any order, truncating or not) <= 2 3d 2u |x| cmax (1 + 2^-9); the norm and the
-//   final subtraction: 2u (cmax^2 + 2 |x| cmax);
-// so eps16 = 1.01 (2 |x| cmax (3 2^-22 + 6d u + 4u) + 4u cmax^2 + 2^-24 sqrt(d) (|x| + cmax)
-// + 2 d 2^-48) + the subnormal term of the f32 path.  Inputs of magnitude >= 2^15 (f16
-// overflow) decide nothing: such an observation, or every observation when the codebook
-// holds one, goes to the exact pass.  Layout as vq_f32r_kernel: a wave owns 16 observations,
-// lane (r, q) holds row r's f64 values k = 8 t + 2 q + {0, 1} (64 contiguous bytes per row
-// per load); fragment b element j of the MFMA is k = 8 (4 b + j / 2) + 2 q + j % 2 (the dot
-// product's k order is free), and the codebook sits in LDS in that order
-// ([block][k-block][hi/lo][lane], 8 halves per lane: one ds_read_b128 per operand).
+//   <= 2 (3 2^-22 |x| cmax + 2^-25 sqrt(d) (|x| + cmax) + d 2^-48); the main accumulator's d
+//   products in any order, truncating or not: <= 2 d 2u |x| cmax (1 + 2^-10); the correction
+//   accumulator's 2d products of <= 2^-10 |x| cmax in sum: <= 2 2d 2u 2^-10 |x| cmax; their sum:
+//   2u |x| cmax; the norm and the final subtraction: 2u (cmax^2 + 2 |x| cmax);
+// so eps16 = 1.01 (2 |x| cmax (3 2^-22 + 2.02 d u + 4u) + 4u cmax^2 + 2^-24 sqrt(d) (|x| + cmax)
+// + 2 d 2^-48) + the subnormal term of the f32 path (one accumulator for all 3d products would
+// need 6d u: the split cuts the bound, and with it the exact pass's share, ~3x).  Inputs of
+// magnitude >= 2^15 (f16 overflow) decide nothing: such an observation, or every observation
+// when the codebook holds one, goes to the exact pass.
+// Layout: a wave owns 16 observations (rows).  Loads: instruction j (< 16) reads rows
+// (l & 7) + 8 (j >> 3), 128 contiguous bytes of each (lane l takes f64 pair 8 (j & 7) +
+// 2 (l >> 4) + ((l >> 3) & 1)): whole cache lines, where 16 rows x 64 B per instruction ran the
+// stream at half the rate.  One exchange between lanes l and l ^ 8 (DPP row_ror:8) then leaves
+// lane (r = l & 15, q = l >> 4) with row r's pairs 8m + 2q + c in register 8c + m — the MFMA's
+// A-fragment order (fragment b element j = register 4b + j/2, half j%2; the dot product's k
+// order is free), and the codebook sits in LDS in that order ([block][k-block][hi/lo][lane],
+// 8 halves per lane: one ds_read_b128 per operand).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 constexpr int kVqhWaves = 8;
 __device__ __forceinline__ double vq_eps16(int DP, double xn, double cmax) {
     const double u = 0x1p-24;
-    return 1.01 * (2.0 * xn * cmax * (0x1.8p-21 + 6.0 * DP * u + 4.0 * u) + 4.0 * u * cmax * cmax +
+    return 1.01 * (2.0 * xn * cmax * (0x1.8p-21 + 2.02 * DP * u + 4.0 * u) + 4.0 * u * cmax * cmax +
                    0x1p-24 * sqrt((double)DP) * (xn + cmax) + 2.0 * DP * 0x1p-48) +
            vq_eps_abs(DP, xn, cmax);
 }
-template <int PROBE, int WAVES = kVqhWaves>   // WAVES > 8: no prefetch (A/B); timing ablations only, never the product: 1 no HBM loads, 2 no winner codeword
-                      // loads, 4 no matrix-core pass (every row takes codeword r % n_codes)
-__global__ __launch_bounds__(WAVES * 64) void vq_f16s_kernel(const double* __restrict__ obs, int64_t n_obs,
+// k of register j (< 16), half e, for lane group q: pair 8 (j & 7) + 2q + (j >> 3)
+__device__ __forceinline__ int vqh_k(int j, int e, int q) { return 16 * (j & 7) + 4 * q + 2 * (j >> 3) + e; }
+// lanes l and l ^ 8 of each 16-lane row swap a value (row_ror:8)
+__device__ __forceinline__ double vqh_xor8(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp((int)__double2loint(v), 0x128, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)__double2hiint(v), 0x128, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+template <int PROBE>   // timing ablations only, never the product: 1 no HBM loads, 2 no winner codeword
+                       // loads, 4 no matrix-core pass (every row takes codeword r % n_codes)
+__global__ __launch_bounds__(kVqhWaves * 64) void vq_f16s_kernel(const double* __restrict__ obs, int64_t n_obs,
                                                                   const double* __restrict__ code, int n_codes,
                                                                   int32_t* __restrict__ codes,
                                                                   double* __restrict__ dist,
@@ -992,16 +1007,17 @@ __global__ __launch_bounds__(WAVES * 64) void vq_f16s_kernel(const double* __res
     __shared__ unsigned s_cmax, s_big;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r16 = lane & 15, kq = lane >> 4;
+    const bool b3 = (lane >> 3) & 1;
     if (threadIdx.x == 0) { s_cmax = 0u; s_big = 0u; }
     __syncthreads();
     for (int t = threadIdx.x; t < ncp * KB * 64; t += blockDim.x) {
         const int ln = t & 63, kb = (t >> 6) % KB, cb = t / (KB * 64);
-        const int j = cb * 16 + (ln & 15), k0 = 32 * kb + 2 * (ln >> 4);
+        const int j = cb * 16 + (ln & 15);
         f16x8 hi, lo;
         bool big = false;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {   // fragment element e <-> k = 8 (4 kb + e / 2) + 2 q + e % 2
-            const double v = j < n_codes ? code[(size_t)j * DP + k0 + 8 * (e >> 1) + (e & 1)] : 0.0;
+        for (int e = 0; e < 8; ++e) {   // fragment element e of k-block kb = register 4 kb + e / 2, half e % 2
+            const double v = j < n_codes ? code[(size_t)j * DP + vqh_k(4 * kb + (e >> 1), e & 1, ln >> 4)] : 0.0;
             big |= !(fabs(v) < 32768.0);
             const _Float16 h = (_Float16)(float)v;
             hi[e] = h;
@@ -1022,27 +1038,32 @@ __global__ __launch_bounds__(WAVES * 64) void vq_f16s_kernel(const double* __res
     const double cmax = (double)__uint_as_float(s_cmax);
     const bool book_big = s_big != 0u;
     const int64_t n_units = (n_obs + 15) >> 4;
-    constexpr bool kPre = WAVES <= 8;   // the prefetch needs the VGPRs of 2 waves per SIMD
-    const int64_t ustep = (int64_t)gridDim.x * WAVES;
-    f64x2 nx[KS / 2];   // the next unit's observations, in flight while this unit computes
+    const int64_t ustep = (int64_t)gridDim.x * kVqhWaves;
+    f64x2 nx[KS / 2];   // the next unit's observations (load order), in flight while this unit computes
     auto fetch = [&](int64_t un) {
-        const f64x2* xp = reinterpret_cast<const f64x2*>(obs + min(un * 16 + r16, n_obs - 1) * DP) + kq;
 #pragma unroll
-        for (int t = 0; t < KS / 2; ++t)   // 64 B per row
-            nx[t] = PROBE == 1 ? f64x2{(double)(lane + un) * 0x1p-10, (double)t * 0x1p-10}
-                               : __builtin_nontemporal_load(xp + 4 * t);
-    };
-    if (kPre) fetch(min((int64_t)blockIdx.x * WAVES + wave, n_units - 1));
-    for (int64_t un = (int64_t)blockIdx.x * WAVES + wave; un < n_units; un += ustep) {
-        if (!kPre) fetch(un);
-        const int64_t o = un * 16 + r16;
-        double x[KS];   // x[2 t + e] = row r16, k = 8 t + 2 kq + e (fragment b, element j: x[8 b + j])
-#pragma unroll
-        for (int s2 = 0; s2 < KS / 2; ++s2) {
-            x[2 * s2] = nx[s2].x;
-            x[2 * s2 + 1] = nx[s2].y;
+        for (int j = 0; j < KS / 2; ++j) {   // rows (l & 7) + 8 (j >> 3), 128 B each
+            const f64x2* xp = reinterpret_cast<const f64x2*>(
+                                  obs + min(un * 16 + (lane & 7) + 8 * (j >> 3), n_obs - 1) * DP) +
+                              8 * (j & 7) + 2 * kq + b3;
+            nx[j] = PROBE == 1 ? f64x2{(double)(lane + un) * 0x1p-10, (double)j * 0x1p-10}
+                               : __builtin_nontemporal_load(xp);
         }
-        if (kPre) fetch(min(un + ustep, n_units - 1));
+    };
+    fetch(min((int64_t)blockIdx.x * kVqhWaves + wave, n_units - 1));
+    for (int64_t un = (int64_t)blockIdx.x * kVqhWaves + wave; un < n_units; un += ustep) {
+        const int64_t o = un * 16 + r16;
+        double x[KS];   // x[2 j + e] = row r16, k = vqh_k(j, e, kq) (fragment b, element i: x[8 b + i])
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {   // load order -> row order: swap registers m / 8 + m across lanes l, l ^ 8
+            const f64x2 a0 = nx[m], a1 = nx[8 + m];
+            const double s0 = vqh_xor8(b3 ? a0.x : a1.x), s1 = vqh_xor8(b3 ? a0.y : a1.y);
+            x[2 * m] = b3 ? s0 : a0.x;
+            x[2 * m + 1] = b3 ? s1 : a0.y;
+            x[16 + 2 * m] = b3 ? a1.x : s0;
+            x[16 + 2 * m + 1] = b3 ? a1.y : s1;
+        }
+        fetch(min(un + ustep, n_units - 1));
         double xn = 0.0;
         bool big = book_big;
 #pragma unroll
@@ -1073,24 +1094,24 @@ __global__ __launch_bounds__(WAVES * 64) void vq_f16s_kernel(const double* __res
         };
         for (int cb = 0; cb < (PROBE == 4 ? 0 : ncb); cb += 2) {   // two blocks per pass (the odd last one's partner is padding)
             const f16x8* bp = sc + cb * KB * 2 * 64 + lane;
-            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+            f32x4 m0 = {0.f, 0.f, 0.f, 0.f}, m1 = m0, c0 = m0, c1 = m0;   // main / correction accumulators
 #pragma unroll
             for (int b = 0; b < KB; ++b) {
                 const f16x8 c0h = bp[(b * 2 + 0) * 64], c0l = bp[(b * 2 + 1) * 64];
                 const f16x8 c1h = bp[((KB + b) * 2 + 0) * 64], c1l = bp[((KB + b) * 2 + 1) * 64];
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c0h, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c1h, acc1, 0, 0, 0);
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c0l, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c1l, acc1, 0, 0, 0);
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[b], c0h, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[b], c1h, acc1, 0, 0, 0);
+                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c0h, m0, 0, 0, 0);
+                m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c1h, m1, 0, 0, 0);
+                c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c0l, c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[b], c1l, c1, 0, 0, 0);
+                c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[b], c0h, c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[b], c1h, c1, 0, 0, 0);
             }
             const int j0 = cb * 16 + r16;
             const float cn0 = sn[j0], cn1 = sn[j0 + 16];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {   // C row 4 kq + g (observation), columns j0, j0 + 16
-                take(g, cn0 - 2.f * acc0[g], j0);
-                take(g, cn1 - 2.f * acc1[g], j0 + 16);
+                take(g, cn0 - 2.f * (m0[g] + c0[g]), j0);
+                take(g, cn1 - 2.f * (m1[g] + c1[g]), j0 + 16);
             }
         }
         int win[4];
@@ -1120,14 +1141,15 @@ __global__ __launch_bounds__(WAVES * 64) void vq_f16s_kernel(const double* __res
         // an out-of-range input anywhere in the row (any lane group) decides nothing
         const bool rbig = __shfl_xor((int)big, 16) | __shfl_xor((int)big, 32) | __shfl_xor((int)big, 48) | big;
         if (rbig) w = -1;
-        const f64x2* cp = reinterpret_cast<const f64x2*>(code + (size_t)max(w, 0) * DP) + kq;
+        const f64x2* cp = reinterpret_cast<const f64x2*>(code + (size_t)max(w, 0) * DP) + 2 * kq;
         double part = 0.0;
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const f64x2 c = PROBE == 2 ? f64x2{x[8 * b + 2 * t + 1], x[8 * b + 2 * t]} : cp[4 * (4 * b + t)];
-                const double d0 = x[8 * b + 2 * t] - c.x, d1 = x[8 * b + 2 * t + 1] - c.y;
+                const int j = 4 * b + t;   // register j: pair 8 (j & 7) + 2 kq + (j >> 3)
+                const f64x2 c = PROBE == 2 ? f64x2{x[2 * j + 1], x[2 * j]} : cp[8 * (j & 7) + (j >> 3)];
+                const double d0 = x[2 * j] - c.x, d1 = x[2 * j + 1] - c.y;
                 part = __builtin_fma(d0, d0, part);
                 part = __builtin_fma(d1, d1, part);
             }
@@ -1526,16 +1548,13 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
             if (half) {
                 const char* penv = std::getenv("SFMHIP_VQ_PROBE");   // timing ablations (tools/bench_vq.py)
                 const int probe = penv ? std::atoi(penv) : 0;
-                const int waves = probe == 5 ? 12 : probe == 6 ? 16 : kVqhWaves;
-                const int64_t n_wg = ((n_obs + 15) / 16 + waves - 1) / waves;
+                const int64_t n_wg = ((n_obs + 15) / 16 + kVqhWaves - 1) / kVqhWaves;
                 auto kern = probe == 1   ? vq_f16s_kernel<1>
                             : probe == 2 ? vq_f16s_kernel<2>
-                            : probe == 4 ? vq_f16s_kernel<4>
-                            : probe == 5 ? vq_f16s_kernel<0, 12>
-                            : probe == 6 ? vq_f16s_kernel<0, 16> : vq_f16s_kernel<0>;
+                            : probe == 4 ? vq_f16s_kernel<4> : vq_f16s_kernel<0>;
                 (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
                 hipLaunchKernelGGL(kern, dim3((unsigned)std::min<int64_t>(n_wg, n_cu)),
-                                   dim3(waves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
+                                   dim3(kVqhWaves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
                                    namb);
                 rc = check_launch("vq_f16s_kernel");
             } else if (reg) {
