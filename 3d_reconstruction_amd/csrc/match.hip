@@ -1174,24 +1174,37 @@ __global__ __launch_bounds__(256) void vq_exact_kernel(const double* __restrict_
                                                        int n_codes, int d, const unsigned* __restrict__ amb,
                                                        const unsigned* __restrict__ namb, int32_t* __restrict__ codes,
                                                        double* __restrict__ dist) {
-    const int lane = threadIdx.x & 63;
+    // one wave per listed observation: four 16-lane groups take four codewords at a time, lane
+    // k16 of a group the dims 8 k16 .. 8 k16 + 7 of each 128-dim chunk (a codeword row is read as
+    // contiguous 1 KB pieces); partial sums of squared differences, then a 16-lane sum.  On
+    // integer data every partial sum is exact, so any order gives the same q.
+    const int lane = threadIdx.x & 63, cg = lane >> 4, k16 = lane & 15;
     const unsigned n = *namb;
     for (unsigned e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
         const int64_t o = amb[e];
         const double* xp = obs + o * d;
         double best = __builtin_inf();
         int bi = INT_MAX;
-        for (int j = lane; j < n_codes; j += 64) {
-            const double* cp = code + (size_t)j * d;
+        for (int j0 = 0; j0 < n_codes; j0 += 4) {
+            const int j = j0 + cg;
+            const double* cp = code + (size_t)min(j, n_codes - 1) * d;
             double q = 0.0;
-            for (int k = 0; k < d; ++k) {
-                const double df = xp[k] - cp[k];
-                q = __builtin_fma(df, df, q);
+            for (int k0 = 8 * k16; k0 < d; k0 += 128) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int k = k0 + t;
+                    if (k < d) {
+                        const double df = xp[k] - cp[k];
+                        q = __builtin_fma(df, df, q);
+                    }
+                }
             }
-            if (q < best) { best = q; bi = j; }   // j increasing per lane: first (lowest) kept
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) q += __shfl_xor(q, off, 16);
+            if (j < n_codes && q < best) { best = q; bi = j; }   // j increasing per group: the lowest kept
         }
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
+        for (int off = 32; off >= 16; off >>= 1) {   // across the four groups, lowest index on ties
             const double ob = __shfl_xor(best, off);
             const int oi = __shfl_xor(bi, off);
             if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
