@@ -50,11 +50,12 @@ __device__ __forceinline__ void ray_setup(const float* rr, float bin, Ray& R) {
 }
 
 // voxel_travesal.py:32-37 get_maskt: any axis with cur==cur and step*cur < step*last
+// (bitwise, not short-circuit: no exec-mask branches on the walk's critical path)
 __device__ __forceinline__ bool ray_active(const Ray& R) {
     bool m = false;
 #pragma unroll
     for (int a = 0; a < 3; ++a)
-        m = m || ((R.cur[a] == R.cur[a]) && (R.step[a] * R.cur[a] < R.step[a] * R.last[a]));
+        m = m | ((R.cur[a] == R.cur[a]) & (R.step[a] * R.cur[a] < R.step[a] * R.last[a]));
     return m;
 }
 
@@ -1769,8 +1770,8 @@ extern "C" int sfmhip_voxel_traversal_count(const float* rays, int64_t N, float 
     SFMHIP_REQUIRE(rays && n_steps, "sfmhip_voxel_traversal_count: null pointer");
     SFMHIP_REQUIRE(N >= 0 && max_steps > 0 && max_steps < INT_MAX, "sfmhip_voxel_traversal_count: bad args");
     if (N == 0) return SFMHIP_OK;
-    hipLaunchKernelGGL(dda_count_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, as_stream(stream), rays, N, bin,
-                       max_steps, n_steps);
+    hipLaunchKernelGGL(dda_count_kernel, dim3(ceil_div(N, 64)), dim3(64), 0, as_stream(stream), rays, N, bin,
+                       max_steps, n_steps);   // one wave per workgroup: the waves spread over the CUs
     return check_launch("dda_count_kernel");
 }
 
