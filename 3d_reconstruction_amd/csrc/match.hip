@@ -271,9 +271,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
         for (int kk = 0; kk < KK; ++kk) bq[s][kk] = *reinterpret_cast<const i32x4*>(rp + kk * M::KB);
     }
 
-    int g1k[NS], g1i[NS], g2k[NS];
+    int g1k[NS], g1i[NS], g2k[NS], g1w[NS], g1b[NS];   // best key, its packed word and block; second key
 #pragma unroll
-    for (int s = 0; s < NS; ++s) { g1k[s] = INT_MIN; g1i[s] = 0; g2k[s] = INT_MIN; }
+    for (int s = 0; s < NS; ++s) { g1k[s] = INT_MIN; g1i[s] = 0; g1w[s] = 127; g1b[s] = 0; g2k[s] = INT_MIN; }
 
     __syncthreads();
 
@@ -318,16 +318,33 @@ __global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
                 }
             }
         }
-        // merge this block's top-2 into the running (key, index, second key)
+        // merge this block's top-2 into the running (key, packed word + block, second key): the
+        // second of {g1, g2, k1, k2} is max3(min(g1, k1), g2, k2); an equal key from a later
+        // block never replaces the best (lower index on ties); the index is formed once at the end
+        // (d <= 128, where a block has half the MFMAs per merge; at d = 256 the branchy form below
+        // measured ~1 % faster: profiles/r3/ab/match_merge_ab_r3as.txt)
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            const int k1 = t1[s] >> 7, k2 = t2[s] >> 7, ix = blk * kJB + 127 - (t1[s] & 127);
-            if (k1 > g1k[s]) { g2k[s] = max(g1k[s], k2); g1k[s] = k1; g1i[s] = ix; }
-            else             { g2k[s] = max(g2k[s], k1); }
+            if constexpr (D <= 128) {
+                const int k1 = t1[s] >> 7, k2 = t2[s] >> 7;
+                const bool up = k1 > g1k[s];
+                g2k[s] = max3i(min(g1k[s], k1), g2k[s], k2);
+                g1w[s] = up ? t1[s] : g1w[s];
+                g1b[s] = up ? blk : g1b[s];
+                g1k[s] = max(g1k[s], k1);
+            } else {
+                const int k1 = t1[s] >> 7, k2 = t2[s] >> 7, ix = blk * kJB + 127 - (t1[s] & 127);
+                if (k1 > g1k[s]) { g2k[s] = max(g1k[s], k2); g1k[s] = k1; g1i[s] = ix; }
+                else             { g2k[s] = max(g2k[s], k1); }
+            }
         }
         __syncthreads();  // drains this wave's DMA; next block visible to all waves
     }
 
+    if constexpr (D <= 128) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) g1i[s] = g1b[s] * kJB + 127 - (g1w[s] & 127);
+    }
     // lanes of the NG groups hold the same query row, disjoint candidate rows.
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
