@@ -692,7 +692,7 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
                                n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
     }
     const int rc = check_launch("ba_trf_kernel");
-    (void)hipFreeAsync(scratch, st);
+    scratch_free(scratch, st);
     return rc;
 }
 

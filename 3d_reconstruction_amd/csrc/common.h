@@ -45,8 +45,13 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // Stream-ordered scratch from a library-owned memory pool per device (lib.hip):
 // freed scratch (up to 1 GiB) stays mapped between calls instead of going back
 // to the driver at every synchronisation (C5 TSDF: 2.32 -> 2.14 ms per call;
-// tools/tsdf_call_gap.py); sfmhip_scratch_trim releases it.
+// tools/tsdf_call_gap.py), and buffers up to 256 MB are cached per (device, stream)
+// so a call re-uses the previous call's scratch without waiting for it;
+// sfmhip_scratch_trim releases both.
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
+// Return scratch from scratch_alloc (stream-ordered: the next call on the same stream may
+// reuse it at once, its kernels run after this call's).
+void scratch_free(void* p, hipStream_t s);
 
 }  // namespace sfmhip
 

@@ -515,7 +515,7 @@ extern "C" int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_ob
                                x0, x1, n, X4, slots, counts, recx, recpr, n_waves, probe);
             rc = check_launch("dlt_list_kernel");
         }
-        (void)hipFreeAsync(slots, st);
+        scratch_free(slots, st);
         return rc;
     }
     (void)hipGetLastError();
@@ -552,6 +552,6 @@ extern "C" int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, con
     hipLaunchKernelGGL(fdjac_kernel, dim3(ceil_div(n, kFdThreads)), dim3(kFdThreads), 0, st, Rt, cam, K, X,
                        pts2d, pair_of_obs, n, f0, r, jvals);
     const int rc = check_launch("fdjac_kernel");
-    (void)hipFreeAsync(Rt, st);
+    scratch_free(Rt, st);
     return rc;
 }

@@ -43,13 +43,78 @@ static hipMemPool_t scratch_pool(int dev) {
     return g_pool[dev];
 }
 
-hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess) {
+static hipError_t pool_alloc(void** p, size_t bytes, hipStream_t s, int dev, bool have_dev) {
+    if (have_dev) {
         if (hipMemPool_t pool = scratch_pool(dev)) return hipMallocFromPoolAsync(p, bytes, pool, s);
     }
     (void)hipGetLastError();
     return hipMallocAsync(p, bytes, s);
+}
+
+// Per-stream scratch cache: a pool allocation + free per call made the host wait for the
+// previous call's kernels (hipMallocFromPoolAsync re-using memory freed on the stream: the
+// enqueue cost of the BA-obs step equalled its GPU time, tools/ba_host_overhead.py).  Buffers
+// up to kCacheMax bytes are kept per (device, stream) and handed out again to a later call on
+// the same stream — stream order makes that safe with no wait; sfmhip_scratch_trim releases
+// them.  Larger ones go straight back to the pool.
+constexpr int kCacheSlots = 32;
+constexpr size_t kCacheMax = 256ull << 20;
+struct CacheSlot {
+    void* p;
+    size_t bytes;
+    hipStream_t s;
+    int dev;
+    bool busy;
+};
+static CacheSlot g_cache[kCacheSlots];
+static std::mutex g_cache_mu;
+
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
+    int dev = 0;
+    const bool have_dev = hipGetDevice(&dev) == hipSuccess;
+    if (!have_dev) (void)hipGetLastError();
+    if (bytes == 0) bytes = 1;
+    if (bytes > kCacheMax || !have_dev) return pool_alloc(p, bytes, s, dev, have_dev);
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    int best = -1, empty = -1;
+    for (int i = 0; i < kCacheSlots; ++i) {
+        CacheSlot& c = g_cache[i];
+        if (!c.p) {
+            if (empty < 0) empty = i;
+        } else if (!c.busy && c.s == s && c.dev == dev && c.bytes >= bytes &&
+                   (best < 0 || c.bytes < g_cache[best].bytes)) {
+            best = i;
+        }
+    }
+    if (best >= 0) {
+        g_cache[best].busy = true;
+        *p = g_cache[best].p;
+        return hipSuccess;
+    }
+    if (empty < 0) {   // table full: drop this stream's smallest idle buffer, else allocate uncached
+        for (int i = 0; i < kCacheSlots; ++i)
+            if (!g_cache[i].busy && (empty < 0 || g_cache[i].bytes < g_cache[empty].bytes)) empty = i;
+        if (empty >= 0) {
+            (void)hipFreeAsync(g_cache[empty].p, g_cache[empty].s);
+            g_cache[empty] = CacheSlot{};
+        }
+    }
+    const hipError_t e = pool_alloc(p, bytes, s, dev, true);
+    if (e == hipSuccess && empty >= 0) g_cache[empty] = CacheSlot{*p, bytes, s, dev, true};
+    return e;
+}
+
+void scratch_free(void* p, hipStream_t s) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        for (int i = 0; i < kCacheSlots; ++i)
+            if (g_cache[i].p == p) {
+                g_cache[i].busy = false;
+                return;
+            }
+    }
+    (void)hipFreeAsync(p, s);
 }
 }  // namespace sfmhip
 
@@ -64,6 +129,15 @@ extern "C" int sfmhip_scratch_trim(uint64_t keep) {
         sfmhip::set_error("sfmhip_scratch_trim: no current HIP device");
         return SFMHIP_E_HIP;
     }
+    {   // the idle cached buffers of this device go back to the pool first
+        std::lock_guard<std::mutex> lk(sfmhip::g_cache_mu);
+        for (auto& c : sfmhip::g_cache)
+            if (c.p && !c.busy && c.dev == dev) {
+                (void)hipFreeAsync(c.p, c.s);
+                c = sfmhip::CacheSlot{};
+            }
+    }
+    (void)hipDeviceSynchronize();
     hipMemPool_t pool = sfmhip::scratch_pool(dev);
     if (!pool) return SFMHIP_OK;
     const hipError_t e = hipMemPoolTrimTo(pool, (size_t)keep);

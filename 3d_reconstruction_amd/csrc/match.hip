@@ -1614,7 +1614,7 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
                                    namb, codes, dist);
                 rc = check_launch("vq_exact_kernel");
             }
-            (void)hipFreeAsync(amb, s);
+            scratch_free(amb, s);
             return rc;
         }
         (void)hipGetLastError();   // no scratch: the f64 kernels below

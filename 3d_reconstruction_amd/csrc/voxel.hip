@@ -1980,7 +1980,7 @@ extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, con
                                rays_o, rays_d, z, B, S, rgb, order);
             rc = check_launch("render_kernel");
         }
-        (void)hipFreeAsync(scratch, st);
+        scratch_free(scratch, st);
         return rc;
     }
     hipLaunchKernelGGL(render_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb, mask_mode, rays_o,
@@ -2097,8 +2097,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         else if (scratch_alloc((void**)&cbmm, nblk * sizeof(float2), st) != hipSuccess) cbmm = nullptr;
         if (cbmm && (scratch_alloc((void**)&cmask, (size_t)nsub * nw * sizeof(unsigned), st) != hipSuccess ||
                      scratch_alloc((void**)&crange, (size_t)cf * sizeof(int4), st) != hipSuccess)) {
-            if (cmask) (void)hipFreeAsync(cmask, st);
-            if (!ext_table) (void)hipFreeAsync(cbmm, st);
+            if (cmask) scratch_free(cmask, st);
+            if (!ext_table) scratch_free(cbmm, st);
             cbmm = nullptr;
             cmask = nullptr;
             crange = nullptr;
@@ -2240,14 +2240,14 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }
-    (void)hipFreeAsync(rec, st);
-    if (ord) (void)hipFreeAsync(ord, st);
-    if (crange) (void)hipFreeAsync(crange, st);
-    if (cmask) (void)hipFreeAsync(cmask, st);
-    if (plist) (void)hipFreeAsync(plist, st);
-    if (ctab) (void)hipFreeAsync(ctab, st);
-    if (cbmm && !ext_table) (void)hipFreeAsync(cbmm, st);
-    if (cfree) (void)hipFreeAsync(cfree, st);
+    scratch_free(rec, st);
+    if (ord) scratch_free(ord, st);
+    if (crange) scratch_free(crange, st);
+    if (cmask) scratch_free(cmask, st);
+    if (plist) scratch_free(plist, st);
+    if (ctab) scratch_free(ctab, st);
+    if (cbmm && !ext_table) scratch_free(cbmm, st);
+    if (cfree) scratch_free(cfree, st);
     return rc;
 }
 
@@ -2293,7 +2293,7 @@ extern "C" int sfmhip_tsdf_block_table(const float* depth, int F, int Hd, int Wd
         hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st, dp, nf,
                            Hd, Wd, nbu, nbv, rg, tp);
     const int rc = check_launch("depth_blockmax_kernel");
-    (void)hipFreeAsync(rg, st);
+    scratch_free(rg, st);
     return rc;
 }
 
