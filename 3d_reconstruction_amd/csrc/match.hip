@@ -239,7 +239,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
     const int pair = wg / n_iblk, ib = wg % n_iblk;
     const int a = pairs[2 * pair], b = pairs[2 * pair + 1];
     const int na_rows = nk[a], nb_rows = nk[b];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the LDS-DMA M0 addresses stay scalar
     const int grp = lane / MF, lr = lane % MF;
     const int ibase = ib * IB + wave * IW;
     int32_t* out_m = m0 + (size_t)pair * m_pad;
