@@ -1023,7 +1023,7 @@ __global__ __launch_bounds__(kVqhWaves * 64) void vq_f16s_kernel(const double* _
     f16x8* sc = reinterpret_cast<f16x8*>(smh);     // [ncp][KB][2 (hi, lo)][64]
     float* sn = reinterpret_cast<float*>(smh + ncp * KB * 2 * 64);   // [ncp * 16] squared norms
     __shared__ unsigned s_cmax, s_big;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r16 = lane & 15, kq = lane >> 4;
     const bool b3 = (lane >> 3) & 1;
     if (threadIdx.x == 0) { s_cmax = 0u; s_big = 0u; }
@@ -1198,7 +1198,7 @@ __global__ __launch_bounds__(256) void vq_exact_kernel(const double* __restrict_
     // integer data every partial sum is exact, so any order gives the same q.
     const int lane = threadIdx.x & 63, cg = lane >> 4, k16 = lane & 15;
     const unsigned n = *namb;
-    for (unsigned e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
+    for (unsigned e = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
         const int64_t o = amb[e];
         const double* xp = obs + o * d;
         double best = __builtin_inf();

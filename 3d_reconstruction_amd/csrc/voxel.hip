@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ g
                                                      int64_t nrays, int S, float* __restrict__ rgb,
                                                      const unsigned* __restrict__ order) {
     const int lane = threadIdx.x & 63;
-    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (w >= nrays) return;  // wave-uniform
     const int64_t ray = order ? (int64_t)order[w] : w;
     const float o[3] = {ro[3 * ray], ro[3 * ray + 1], ro[3 * ray + 2]};
@@ -1447,7 +1447,7 @@ __global__ __launch_bounds__(256) void render_train_kernel(
     __shared__ int s_cv[4][64 * 8];
     __shared__ float s_cw[4][64 * 8];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (ray >= nrays) return;  // wave-uniform
     const float o[3] = {ro[3 * ray], ro[3 * ray + 1], ro[3 * ray + 2]};
     const float d[3] = {rd[3 * ray], rd[3 * ray + 1], rd[3 * ray + 2]};
