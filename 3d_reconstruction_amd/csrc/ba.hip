@@ -48,7 +48,7 @@ constexpr int kRec = 26;   // per observation: J (18: u row, v row), f (2), scal
 // sum of K doubles over the workgroup (NW waves); every thread receives the totals in out[]
 template <int NW, int K>
 __device__ void block_sum(double (&v)[K], double* red /* [NW][K] */, double* out /* [K] */) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         double x = v[k];
@@ -75,7 +75,7 @@ __device__ void block_sum(double (&v)[K], double* red /* [NW][K] */, double* out
 
 template <int NW>
 __device__ double block_max(double v, double* red) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
     if (lane == 0) red[wave] = v;
