@@ -495,6 +495,23 @@ __device__ __forceinline__ void project_f(const double* R, const double* t, doub
     v = (float)(y * z * fy + cy);
 }
 
+// K sums at once: the same per-value wave reduction and cross-wave order as block_sum
+// (the same bits), one barrier pair instead of K
+template <int K>
+__device__ __forceinline__ void block_sum_n(double (&v)[K], double* red /* [K * 4] */) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[k * 4 + w] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = ((red[k * 4] + red[k * 4 + 1]) + red[k * 4 + 2]) + red[k * 4 + 3];
+}
+
 __device__ __forceinline__ double block_sum(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     const int w = threadIdx.x >> 6;
@@ -723,13 +740,13 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
             }
         }
         double e2 = 0;
-        const int nk = with_j ? 28 : 1;
-        for (int k = 0; k < nk; ++k) {
-            const int kk = with_j ? k : 27;
-            const double s = block_sum(acc[kk], s_red);
-            if (kk == 27) e2 = s;
-            else if (kk < 21) jtj[kk] = s;
-            else jte[kk - 21] = s;
+        if (with_j) {   // all 28 sums behind one barrier pair
+            block_sum_n<28>(acc, s_red);
+            for (int k = 0; k < 21; ++k) jtj[k] = acc[k];
+            for (int k = 21; k < 27; ++k) jte[k - 21] = acc[k];
+            e2 = acc[27];
+        } else {
+            e2 = block_sum(acc[27], s_red);
         }
         return sqrt(e2);
     };
