@@ -58,7 +58,8 @@ static hipError_t pool_alloc(void** p, size_t bytes, hipStream_t s, int dev, boo
 // the same stream — stream order makes that safe with no wait; sfmhip_scratch_trim releases
 // them.  Larger ones go straight back to the pool.
 constexpr int kCacheSlots = 32;
-constexpr size_t kCacheMax = 256ull << 20;
+constexpr size_t kCacheMax = 256ull << 20;     // larger buffers are not cached
+constexpr size_t kCacheTotal = 1ull << 30;     // bytes held by the cache at most
 struct CacheSlot {
     void* p;
     size_t bytes;
@@ -100,7 +101,20 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
         }
     }
     const hipError_t e = pool_alloc(p, bytes, s, dev, true);
-    if (e == hipSuccess && empty >= 0) g_cache[empty] = CacheSlot{*p, bytes, s, dev, true};
+    if (e == hipSuccess && empty >= 0) {
+        g_cache[empty] = CacheSlot{*p, bytes, s, dev, true};
+        size_t held = 0;   // keep at most kCacheTotal bytes cached: drop idle buffers, largest first
+        for (const auto& c : g_cache) held += c.bytes;
+        while (held > kCacheTotal) {
+            int big = -1;
+            for (int i = 0; i < kCacheSlots; ++i)
+                if (g_cache[i].p && !g_cache[i].busy && (big < 0 || g_cache[i].bytes > g_cache[big].bytes)) big = i;
+            if (big < 0) break;
+            held -= g_cache[big].bytes;
+            (void)hipFreeAsync(g_cache[big].p, g_cache[big].s);
+            g_cache[big] = CacheSlot{};
+        }
+    }
     return e;
 }
 
