@@ -50,7 +50,10 @@ int         sfmhip_device_arch(char* buf, int len); /* "gfx950" of device 0   */
 
 /* Stream-ordered scratch comes from a library-owned memory pool per device
  * (never the device's default pool); up to 1 GiB of freed scratch stays
- * mapped between calls.  Trim the current device's pool to `keep` bytes.    */
+ * mapped between calls, and buffers up to 256 MB (1 GiB in all) are cached
+ * per (device, stream) so the next call on that stream re-uses them without
+ * waiting.  Releases the idle cached buffers of the current device (after a
+ * device synchronisation), then trims its pool to `keep` bytes.             */
 int         sfmhip_scratch_trim(uint64_t keep);
 
 /* ---- M1: brute-force L2 matching + ratio test --------------------------
