@@ -73,6 +73,8 @@ SIGNATURES = {
     "sfmhip_ba_solve": [_p, _p, _p, _p, _p, _i32, _i64, _f64, _f64, _f64, _i32, _p, _p, _p, _p, _p],
     "sfmhip_voxel_traversal_count": [_p, _i64, _f32, _i32, _p, _p],
     "sfmhip_voxel_traversal": [_p, _i64, _f32, _i32, _p, _p],
+    "sfmhip_voxel_traversal_capped": [_p, _i64, _f32, _i32, _p, _p, _p],
+    "sfmhip_voxel_traversal_rows": [_p, _i32, _p, _i64, _i32, _p, _p],
     "sfmhip_grid_sample": [_p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _i64, _p, _p],
     "sfmhip_nerf_forward": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _i64, _p, _p, _p],
     "sfmhip_grid_to_voxel_major": [_p, _i32, _i32, _i32, _i32, _p, _p],

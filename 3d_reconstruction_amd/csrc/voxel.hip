@@ -166,8 +166,11 @@ __global__ __launch_bounds__(256) void dda_fill_kernel(const float* __restrict__
 // each lane stores its own row directly, one 12-B store per step, no LDS
 // staging; lanes whose rays have ended store NaN rows, and a wave whose rays
 // have all ended stores the remaining padding in 64-lane runs and exits.
+// n_steps (optional, the capped one-walk form): each lane's step count, S when its ray is
+// still active after the row is full.
 __global__ __launch_bounds__(64) void dda_fill_direct_kernel(const float* __restrict__ rays, int64_t N, float bin,
-                                                             int S, float* __restrict__ out) {
+                                                             int S, float* __restrict__ out,
+                                                             int32_t* __restrict__ n_steps) {
     const int lane = threadIdx.x;
     const int64_t ray0 = (int64_t)blockIdx.x * 64, i = ray0 + lane;
     const float nan = __builtin_nanf("");
@@ -180,8 +183,11 @@ __global__ __launch_bounds__(64) void dda_fill_direct_kernel(const float* __rest
     }
     const int nrows = (int)min((int64_t)64, N - ray0);
     float* row = out + (size_t)min(i, N - 1) * S * 3;
+    int k = 0;   // steps walked
     for (int s = 0; s < S; ++s) {
         if (s >= 2 && !__any(act)) {
+            if (n_steps && i < N) n_steps[i] = k;
+            if (n_steps) return;   // capped form: dda_rows_kernel pads each row from its step count
             const int rest = (S - s) * 3;
             for (int r = 0; r < nrows; ++r) {
                 float* o = out + ((size_t)(ray0 + r) * S + s) * 3;
@@ -194,6 +200,7 @@ __global__ __launch_bounds__(64) void dda_fill_direct_kernel(const float* __rest
             v0 = R.cur[0]; v1 = R.cur[1]; v2 = R.cur[2];
         } else if (act) {
             ray_step(R);
+            ++k;
             v0 = R.cur[0]; v1 = R.cur[1]; v2 = R.cur[2];
             act = ray_active(R);
         }
@@ -203,6 +210,7 @@ __global__ __launch_bounds__(64) void dda_fill_direct_kernel(const float* __rest
             row[3 * s + 2] = v2;
         }
     }
+    if (n_steps && i < N) n_steps[i] = act ? S : k;
 }
 
 // ---------------------------------------------------------------------------
@@ -1786,12 +1794,47 @@ extern "C" int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, i
     const bool direct = denv ? std::atoi(denv) != 0 : N < 65536;
     if (direct) {
         hipLaunchKernelGGL(dda_fill_direct_kernel, dim3(ceil_div(N, 64)), dim3(64), 0, as_stream(stream), rays, N,
-                           bin, S, out);
+                           bin, S, out, nullptr);
         return check_launch("dda_fill_direct_kernel");
     }
     hipLaunchKernelGGL(dda_fill_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, as_stream(stream), rays, N, bin, S,
                        out);  // 4 waves x 64 rays per workgroup
     return check_launch("dda_fill_kernel");
+}
+
+// The capped form's rows -> out [N][S][3]: entries past a row's own length are NaN (length
+// k + 1, or 2 for a ray inactive from the start — k == 0 — whose start voxel is emitted twice).
+__global__ __launch_bounds__(256) void dda_rows_kernel(const float* __restrict__ buf, int cap,
+                                                       const int32_t* __restrict__ n_steps, int64_t N, int S,
+                                                       float* __restrict__ out) {
+    const int64_t total = N * (int64_t)S * 3;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e / (3 * (int64_t)S);
+        const int rem = (int)(e - i * 3 * (int64_t)S), s = rem / 3, c = rem - 3 * s;
+        const int k = n_steps[i], len = k == 0 ? 2 : k + 1;
+        out[e] = s < len ? buf[(i * cap + s) * 3 + c] : __builtin_nanf("");
+    }
+}
+
+extern "C" int sfmhip_voxel_traversal_rows(const float* buf, int32_t cap, const int32_t* n_steps, int64_t N,
+                                           int32_t S, float* out, void* stream) {
+    SFMHIP_REQUIRE(buf && n_steps && out, "sfmhip_voxel_traversal_rows: null pointer");
+    SFMHIP_REQUIRE(N >= 0 && S >= 1 && S <= cap, "sfmhip_voxel_traversal_rows: bad args (1 <= S <= cap)");
+    if (N == 0) return SFMHIP_OK;
+    const int64_t total = N * (int64_t)S * 3;
+    hipLaunchKernelGGL(dda_rows_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(total, 256), 8192)), dim3(256), 0,
+                       as_stream(stream), buf, cap, n_steps, N, S, out);
+    return check_launch("dda_rows_kernel");
+}
+
+extern "C" int sfmhip_voxel_traversal_capped(const float* rays, int64_t N, float bin, int32_t cap, float* out,
+                                             int32_t* n_steps, void* stream) {
+    SFMHIP_REQUIRE(rays && out && n_steps, "sfmhip_voxel_traversal_capped: null pointer");
+    SFMHIP_REQUIRE(N >= 0 && cap >= 2, "sfmhip_voxel_traversal_capped: bad args (cap >= 2)");
+    if (N == 0) return SFMHIP_OK;
+    hipLaunchKernelGGL(dda_fill_direct_kernel, dim3(ceil_div(N, 64)), dim3(64), 0, as_stream(stream), rays, N, bin,
+                       cap, out, n_steps);
+    return check_launch("dda_fill_direct_kernel");
 }
 
 static Bounds make_bounds(const float* bmin, const float* bmax) {

@@ -16,6 +16,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -42,6 +44,17 @@ def voxel_traversal(rays: torch.Tensor, _bin_size, max_steps: int = 1 << 20) -> 
     N = r.shape[0]
     b = float(_bin_size)
     steps = torch.empty(N, dtype=torch.int32, device=r.device)
+    # one walk into rows of width `cap` when they fit a bounded buffer (DDA_CAP; 0 = always two passes):
+    # the prefix of the rows is the two-pass result whenever every ray ends within cap - 1 steps
+    cap = min(int(os.environ.get("SFMHIP_DDA_CAP", "1024")), int(max_steps) + 1)
+    if N > 0 and cap >= 2 and N * cap * 12 <= (256 << 20):
+        buf = torch.empty((N, cap, 3), dtype=torch.float32, device=r.device)
+        call("sfmhip_voxel_traversal_capped", ptr(r), N, b, cap, ptr(buf), ptr(steps), stream_ptr())
+        longest = int(steps.max().item())
+        if longest < cap:
+            out = torch.empty((N, 1 + longest, 3), dtype=torch.float32, device=r.device)
+            call("sfmhip_voxel_traversal_rows", ptr(buf), cap, ptr(steps), N, 1 + longest, ptr(out), stream_ptr())
+            return out
     call("sfmhip_voxel_traversal_count", ptr(r), N, b, int(max_steps), ptr(steps), stream_ptr())
     longest = int(steps.max().item()) if N > 0 else 0
     if longest > max_steps:

@@ -213,6 +213,16 @@ int sfmhip_voxel_traversal_count(const float* rays, int64_t N, float bin,
                                  int32_t max_steps, int32_t* n_steps, void* stream);
 int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, int32_t S,
                            float* out, void* stream);
+/* One walk instead of two: each ray's visited voxels into rows of width `cap`
+ * (buf [N][cap][3]; entries past a row's end are left unwritten) and its step
+ * count (n_steps[N]; cap when the ray is still active after cap - 1 steps).
+ * When every n_steps < cap, sfmhip_voxel_traversal_rows with S = 1 + max
+ * n_steps writes exactly the two-pass form's out [N][S][3] (NaN padded);
+ * otherwise the caller falls back to the two-pass form.                    */
+int sfmhip_voxel_traversal_capped(const float* rays, int64_t N, float bin, int32_t cap,
+                                  float* buf, int32_t* n_steps, void* stream);
+int sfmhip_voxel_traversal_rows(const float* buf, int32_t cap, const int32_t* n_steps,
+                                int64_t N, int32_t S, float* out, void* stream);
 
 /* ---- V2: trilinear grid sample (sdf.py:284-342, plenoxel.py:31-43) -------
  * grid in the reference layout (1,C,D,H,W) f32.  pts [P][3] world coords.

@@ -37,11 +37,13 @@ def test_voxel_traversal_random_vs_oracle(sfm, gpu):
     np.testing.assert_array_equal(out, ov.voxel_traversal(rays, 1.0))
 
 
-@pytest.mark.parametrize("direct", ["0", "1"])
+@pytest.mark.parametrize("direct", ["capped", "0", "1"])
 def test_voxel_traversal_padding_early_exit_vs_oracle(sfm, gpu, monkeypatch, direct):
     """One long ray sets S for the whole batch, so most waves end long before S
     and store their NaN padding without walking the remaining steps; a ragged
-    last wave (N = 1000) and rays inactive from the start (emitted twice)."""
+    last wave (N = 1000) and rays inactive from the start (emitted twice).
+    "capped": the one-walk form (default); "0" / "1": the two-pass form with
+    either fill kernel."""
     rng = np.random.default_rng(5)
     N = 1000
     o = rng.uniform(-20, 20, (N, 3)).astype(np.float32)
@@ -51,7 +53,9 @@ def test_voxel_traversal_padding_early_exit_vs_oracle(sfm, gpu, monkeypatch, dir
     far[::13] = near[::13]                         # inactive from the start
     far[131] = near[131] + 150.0                   # the longest ray, in the third wave
     rays = np.concatenate([o, d, near, far], 1)
-    monkeypatch.setenv("SFMHIP_DDA_DIRECT", direct)   # both fill kernels
+    if direct != "capped":
+        monkeypatch.setenv("SFMHIP_DDA_CAP", "0")       # the two-pass form ...
+        monkeypatch.setenv("SFMHIP_DDA_DIRECT", direct)  # ... with both fill kernels
     out = sfm.voxel_traversal(torch.from_numpy(rays).to(gpu), 1.0).cpu().numpy()
     ref = ov.voxel_traversal(rays, 1.0)
     assert out.shape == ref.shape and out.shape[1] > 100
@@ -136,6 +140,27 @@ def test_render_ray_order_bitexact(sfm, gpu, monkeypatch, cfg):
         monkeypatch.setenv(k, v)
     got = vg.render(ro, rd, z)
     assert torch.equal(got, ref)
+
+
+def test_voxel_traversal_cap_boundary(sfm, gpu, monkeypatch):
+    """The one-walk form at the edge of its row width: cap = S (every ray fits:
+    the rows' prefix is returned) and cap = S - 1 (the longest ray does not fit:
+    the two-pass fallback) both give the reference's array."""
+    rng = np.random.default_rng(9)
+    N = 700
+    o = rng.uniform(-10, 10, (N, 3)).astype(np.float32)
+    d = rng.standard_normal((N, 3)).astype(np.float32)
+    near = rng.uniform(0, 1, (N, 1)).astype(np.float32)
+    far = near + rng.uniform(0, 12, (N, 1)).astype(np.float32)
+    far[::11] = near[::11]
+    rays = np.concatenate([o, d, near, far], 1)
+    ref = ov.voxel_traversal(rays, 1.0)
+    S = ref.shape[1]
+    for cap in (S, S - 1, 2):
+        monkeypatch.setenv("SFMHIP_DDA_CAP", str(cap))
+        out = sfm.voxel_traversal(torch.from_numpy(rays).to(gpu), 1.0).cpu().numpy()
+        assert out.shape == ref.shape
+        np.testing.assert_array_equal(out, ref)
 
 
 def _tsdf_case(R=48, F=12, Hd=96, Wd=128, focal=110.0):
