@@ -299,8 +299,22 @@ __device__ double epnp_R_t(const EpnpData& D, const double* G, const int* vi, co
     return sum / 5;
 }
 
+// Phase timers for tools/prof_pnp.py: build with -DSFMHIP_PNP_PROF (make EXTRA=-DSFMHIP_PNP_PROF);
+// compiled out otherwise.
+#ifdef SFMHIP_PNP_PROF
+__device__ unsigned long long g_pprof[16];
+#define PPROF(i) do { if (threadIdx.x == 0) { const unsigned long long t1_ = wall_clock64(); atomicAdd(&g_pprof[i], t1_ - pp_t); pp_t = t1_; } } while (0)
+#define PPROF_INIT unsigned long long pp_t = wall_clock64()
+#define PPROF_ADD(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_pprof[i], (unsigned long long)(v)); } while (0)
+#else
+#define PPROF(i) do {} while (0)
+#define PPROF_INIT do {} while (0)
+#define PPROF_ADD(i, v) do {} while (0)
+#endif
+
 // EPnP on 5 correspondences by a 16-lane group; writes (rvec, tvec) to out[6].
 __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
+    PPROF_INIT;
     // M^T M (12x12) into A, V = I
     for (int e = gl; e < 144; e += kPnGL) {
         const int i = e / 12, j = e % 12;
@@ -319,61 +333,83 @@ __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
         G[gV + e] = (i == j) ? 1.0 : 0.0;
     }
     lds_fence();
+    PPROF(7);
     // parallel-ordered two-sided Jacobi: 11 rounds of 6 disjoint pairs per sweep
+    auto pair_of = [](int rnd, int k, int& p, int& q) {
+        if (k == 0) { p = 11; q = rnd; } else { p = (rnd + k) % 11; q = (rnd - k + 11) % 11; }
+        if (p > q) { const int t = p; p = q; q = t; }
+    };
+    double* A = G + gA;
+    double* V = G + gV;
     for (int sweep = 0; sweep < 15; ++sweep) {
-        // convergence: off-diagonal vs diagonal mass (group reduction)
+        // convergence: off-diagonal vs diagonal mass (group reduction; 9 elements per lane,
+        // all loads issued before the sums)
+        double av[9];
+#pragma unroll
+        for (int it = 0; it < 9; ++it) av[it] = A[gl + kPnGL * it];
         double off = 0, dg = 0;
-        for (int e = gl; e < 144; e += kPnGL) {
-            const double a = G[gA + e];
-            if (e / 12 == e % 12) dg += a * a; else off += a * a;
+#pragma unroll
+        for (int it = 0; it < 9; ++it) {
+            const int e = gl + kPnGL * it;
+            if (e / 12 == e % 12) dg += av[it] * av[it]; else off += av[it] * av[it];
         }
         for (int o = 8; o > 0; o >>= 1) { off += __shfl_xor(off, o, kPnGL); dg += __shfl_xor(dg, o, kPnGL); }
         if (off <= 1e-30 * dg) break;
+        PPROF_ADD(15, 1);
         for (int rnd = 0; rnd < 11; ++rnd) {
             if (gl < 6) {
                 int p, q;
-                if (gl == 0) { p = 11; q = rnd; } else { p = (rnd + gl) % 11; q = (rnd - gl + 11) % 11; }
-                if (p > q) { const int t = p; p = q; q = t; }
-                const double apq = G[gA + p * 12 + q];
-                double c = 1.0, s = 0.0;
-                if (apq != 0.0) {
-                    const double tau = (G[gA + q * 12 + q] - G[gA + p * 12 + p]) / (2.0 * apq);
-                    const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
-                    c = 1.0 / sqrt(1.0 + t * t);
-                    s = t * c;
-                }
-                G[gRot + 2 * gl] = c;
-                G[gRot + 2 * gl + 1] = s;
+                pair_of(rnd, gl, p, q);
+                const double apq = A[p * 12 + q], aqq = A[q * 12 + q], app = A[p * 12 + p];
+                const double tau = (aqq - app) / (2.0 * apq);
+                const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+                const double c = 1.0 / sqrt(1.0 + t * t);
+                const bool rot = apq != 0.0;
+                G[gRot + 2 * gl] = rot ? c : 1.0;
+                G[gRot + 2 * gl + 1] = rot ? t * c : 0.0;
             }
             lds_fence();
-            // rows: A <- J^T A (row pairs (p, q) of all 12 columns): 6 x 12 updates
-            for (int u = gl; u < 72; u += kPnGL) {
-                const int k = u / 12, col = u % 12;
-                int p, q;
-                if (k == 0) { p = 11; q = rnd; } else { p = (rnd + k) % 11; q = (rnd - k + 11) % 11; }
-                if (p > q) { const int t = p; p = q; q = t; }
-                const double c = G[gRot + 2 * k], s = G[gRot + 2 * k + 1];
-                const double ap = G[gA + p * 12 + col], aq = G[gA + q * 12 + col];
-                G[gA + p * 12 + col] = c * ap - s * aq;
-                G[gA + q * 12 + col] = s * ap + c * aq;
+            // A <- J^T A J and V <- V J fused per 2x2 block: block (bi, bj) of A is rows
+            // pair bi x columns pair bj, rotated by rows then by columns (the same operations,
+            // in the same order, as two separate passes); V block = rows 2bi, 2bi+1 x pair bj.
+            // The 36 blocks are disjoint: a lane loads its 3 blocks, then rotates and stores them.
+            int ia[3][4], iv[3][4];
+            double ld[3][12];
+#pragma unroll
+            for (int it = 0; it < 3; ++it) {
+                const int b = min(gl + kPnGL * it, 35);
+                const int bi = b / 6, bj = b - 6 * bi;
+                int pi, qi, pj, qj;
+                pair_of(rnd, bi, pi, qi);
+                pair_of(rnd, bj, pj, qj);
+                ia[it][0] = pi * 12 + pj; ia[it][1] = pi * 12 + qj; ia[it][2] = qi * 12 + pj; ia[it][3] = qi * 12 + qj;
+                iv[it][0] = 24 * bi + pj; iv[it][1] = 24 * bi + qj; iv[it][2] = 24 * bi + 12 + pj; iv[it][3] = 24 * bi + 12 + qj;
+                ld[it][0] = G[gRot + 2 * bi]; ld[it][1] = G[gRot + 2 * bi + 1];
+                ld[it][2] = G[gRot + 2 * bj]; ld[it][3] = G[gRot + 2 * bj + 1];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { ld[it][4 + k] = A[ia[it][k]]; ld[it][8 + k] = V[iv[it][k]]; }
             }
-            lds_fence();
-            // columns: A <- A J and V <- V J
-            for (int u = gl; u < 144; u += kPnGL) {
-                const int k = (u % 72) / 12, row = u % 12;
-                const bool isV = u >= 72;
-                int p, q;
-                if (k == 0) { p = 11; q = rnd; } else { p = (rnd + k) % 11; q = (rnd - k + 11) % 11; }
-                if (p > q) { const int t = p; p = q; q = t; }
-                const double c = G[gRot + 2 * k], s = G[gRot + 2 * k + 1];
-                double* M = G + (isV ? gV : gA);
-                const double ap = M[row * 12 + p], aq = M[row * 12 + q];
-                M[row * 12 + p] = c * ap - s * aq;
-                M[row * 12 + q] = s * ap + c * aq;
+#pragma unroll
+            for (int it = 0; it < 3; ++it) {
+                if (gl + kPnGL * it >= 36) break;
+                const double ci = ld[it][0], si = ld[it][1], cj = ld[it][2], sj = ld[it][3];
+                const double a00 = ld[it][4], a01 = ld[it][5], a10 = ld[it][6], a11 = ld[it][7];
+                const double v0p = ld[it][8], v0q = ld[it][9], v1p = ld[it][10], v1q = ld[it][11];
+                const double r00 = ci * a00 - si * a10, r10 = si * a00 + ci * a10;
+                const double r01 = ci * a01 - si * a11, r11 = si * a01 + ci * a11;
+                A[ia[it][0]] = cj * r00 - sj * r01;
+                A[ia[it][1]] = sj * r00 + cj * r01;
+                A[ia[it][2]] = cj * r10 - sj * r11;
+                A[ia[it][3]] = sj * r10 + cj * r11;
+                V[iv[it][0]] = cj * v0p - sj * v0q;
+                V[iv[it][1]] = sj * v0p + cj * v0q;
+                V[iv[it][2]] = cj * v1p - sj * v1q;
+                V[iv[it][3]] = sj * v1p + cj * v1q;
             }
             lds_fence();
         }
     }
+    PPROF(8);
     // the 4 smallest eigenvalues (ascending), canonical signs
     int vi[4];
     {
@@ -417,6 +453,7 @@ __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
                        (ca[2] - cb[2]) * (ca[2] - cb[2]);
     }
     lds_fence();
+    PPROF(9);
     // three beta approximations (lane 0: B11 B12 B13 B14, 1: B11 B12 B22, 2: B11 B12 B22 B13 B23)
     if (gl < 3) {
         double L[6][10], rho[6];
@@ -472,6 +509,7 @@ __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
         sol[12] = err;
     }
     lds_fence();
+    PPROF(10);
     if (gl == 0) {
         int N = 0;
         if (G[gSol + 13 + 12] < G[gSol + 12]) N = 1;
@@ -481,6 +519,7 @@ __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
         out[3] = sol[9]; out[4] = sol[10]; out[5] = sol[11];
     }
     lds_fence();
+    PPROF(11);
 }
 
 // projection of a float object point (converted to double) with R, t, K;
@@ -621,6 +660,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
     }
     CvRng rng{~0ULL};
     const double inv_n = 1.0 / (double)n;
+    PPROF_INIT;
     for (;;) {
         const int k0 = s_k0, niters = s_niters;
         if (tid == 0) {
@@ -639,16 +679,20 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         }
         if (tid < kPnH) s_cnt[tid] = 0;
         __syncthreads();
+        PPROF(0);
         const bool live = k0 + h < niters;
         if (live) {
             EpnpData D;
+            PPROF_INIT;
             load_sample(s_sub + h * 5, D);
             double* G = s_grp + h * kPnGS;
             prepare(D, G);
+            PPROF(6);
             epnp_group(D, gl, G, s_models[h]);
             if (gl == 0) rodrigues(s_models[h], s_models[h] + 6);
         }
         __syncthreads();
+        PPROF(1);
         for (int i0 = 0; i0 < n; i0 += kPnThreads) {
             const int i = i0 + tid;
             const bool valid = i < n;
@@ -665,6 +709,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
             }
         }
         __syncthreads();
+        PPROF(2);
         if (tid == 0) {
             int nit = niters, maxgood = s_maxgood, last = s_last;
             for (int hh = 0; hh < kPnH; ++hh) {
@@ -683,6 +728,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         __syncthreads();
         if (s_k0 >= s_niters) break;
     }
+    PPROF(3);
     const int maxgood = s_maxgood;
     if (maxgood <= 0) {
         if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = s_last + 1; }
@@ -704,6 +750,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
     double* Rm = s_lm + 39;   // R (9)
     if (tid < 6) prm[tid] = s_best[tid];
     __syncthreads();
+    PPROF(4);
     auto eval = [&](bool with_j, double* jtj, double* jte) -> double {
         if (tid == 0) {
             rodrigues(prm, Rm);
@@ -807,6 +854,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         prev_err = err_norm;
         err = eval(true, jtj, jte);
     }
+    PPROF(5);
     if (tid == 0) {
         for (int k = 0; k < 3; ++k) { rvec_out[3 * p + k] = prm[k]; tvec_out[3 * p + k] = prm[3 + k]; }
         ok_out[p] = 1; ninl_out[p] = maxgood; iters_out[p] = s_last + 1;
@@ -818,6 +866,17 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
 }  // namespace sfmhip
 
 using namespace sfmhip;
+
+#ifdef SFMHIP_PNP_PROF
+// Phase timers of pnp_ransac_kernel for tools/prof_pnp.py: exported only by a profiling build
+// (make EXTRA=-DSFMHIP_PNP_PROF), not part of the ABI.
+extern "C" int sfmhip_debug_pnp_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sfmhip::g_pprof), sizeof(unsigned long long) * 16) != hipSuccess) return -2;
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sfmhip::g_pprof), z, sizeof(z)) != hipSuccess) return -2;
+    return 0;
+}
+#endif
 
 extern "C" int sfmhip_pnp_ransac(const double* obj, const double* img, const int64_t* offsets, int n_problems,
                                  const double* cam, int iterations, double reprojection_error, double confidence,

@@ -1,0 +1,49 @@
+"""Phase profile of pnp_ransac_kernel on bench.py's PnP workload (256 x 2000).
+Needs the library built with: make -C 3d_reconstruction_amd/csrc clean all EXTRA=-DSFMHIP_PNP_PROF"""
+import ctypes
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sfm = importlib.import_module("3d_reconstruction_amd")
+syn = importlib.import_module("3d_reconstruction_amd.synthetic")
+from oracle import geometry as og   # noqa: E402  (workload generation only)
+
+dev = torch.device("cuda", 0)
+v = sfm.verify
+rng = np.random.default_rng(12)
+K = np.diag([syn.FOCAL, syn.FOCAL, 1.0])
+P, n = 256, 2000
+Xs, uvs = [], []
+for _ in range(P):
+    rv = rng.normal(0, 0.2, 3)
+    t = np.array([rng.normal(0, 0.3), rng.normal(0, 0.3), 5.0 + rng.random()])
+    X = rng.uniform(-1, 1, (n, 3))
+    uv = og.project_points(X, rv, t, K) + rng.normal(0, 0.5, (n, 2))
+    bad = rng.random(n) < 0.3
+    uv[bad] = rng.uniform(-900, 900, (int(bad.sum()), 2))
+    Xs.append(X)
+    uvs.append(uv)
+Xd = torch.tensor(np.concatenate(Xs), device=dev)
+ud = torch.tensor(np.concatenate(uvs), device=dev)
+of = torch.tensor(np.arange(P + 1, dtype=np.int64) * n, device=dev)
+cam = torch.tensor(v._cam(K), device=dev).expand(P, 4).contiguous()
+r = v.pnp_ransac_batched(Xd, ud, of, cam)
+torch.cuda.synchronize()
+buf = (ctypes.c_ulonglong * 16)()
+sfm.lib.sfmhip_debug_pnp_prof(buf)
+r = v.pnp_ransac_batched(Xd, ud, of, cam)
+torch.cuda.synchronize()
+sfm.lib.sfmhip_debug_pnp_prof(buf)
+names = ["sample draw", "EPnP solve", "score", "replay", "inlier mask", "LM refine"]
+tot = sum(buf[:6])
+print("per-problem mean (us, wall clock 100 MHz):", {nm: round(buf[i] / P / 100, 1) for i, nm in enumerate(names)})
+print("fractions:", {nm: round(buf[i] / max(tot, 1), 3) for i, nm in enumerate(names)})
+sub = ["load+prepare", "MtM", "Jacobi", "signs+L/rho", "betas+GN+R_t", "select+rodrigues_inv"]
+print("EPnP sub-phases of group 0 (us per problem):", {nm: round(buf[6 + i] / P / 100, 1) for i, nm in enumerate(sub)})
+print("Jacobi sweeps per problem (group 0):", buf[15] / P)
+print("mean ransac iters", r["iters"].float().mean().item())
