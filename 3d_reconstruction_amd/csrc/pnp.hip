@@ -8,8 +8,9 @@
 //
 // One workgroup (4 waves) per registration problem:
 //   * points are converted to float (solvePnPRansac's CV_32F conversion);
-//   * RANSAC: lane 0 draws 16 five-point samples per chunk from cv::RNG(-1);
-//     each sample is solved by EPnP in a 16-lane group (M^T M eigenvectors by
+//   * RANSAC: lane 0 draws 32 five-point samples per chunk from cv::RNG(-1)
+//     (OpenCV's ~25 iterations at 30 % outliers fit one chunk);
+//     each sample is solved by EPnP in an 8-lane group (M^T M eigenvectors by
 //     a parallel-ordered two-sided Jacobi in LDS, the three beta
 //     approximations + Gauss-Newton in lanes 0..2, Procrustes), scored by all
 //     lanes (float squared reprojection error <= 64, wave ballots) and
@@ -24,15 +25,19 @@ namespace sfmhip {
 namespace {
 
 constexpr int kPnThreads = 256;
-constexpr int kPnGL = 16;
+constexpr int kPnGL = 8;                   // lanes per EPnP group
 constexpr int kPnH = kPnThreads / kPnGL;  // hypotheses per chunk
+constexpr int kJcN = 144 / kPnGL;          // convergence-check elements per lane
+constexpr int kJbN = (36 + kPnGL - 1) / kPnGL;  // 2x2 rotation blocks per lane
+static_assert(144 % kPnGL == 0 && kPnGL >= 6, "EPnP group width");
 constexpr int kPnGS = 448;                // LDS doubles per group
 constexpr double kEps64 = 2.220446049250313e-16;
 constexpr double kDblMin64 = 2.2250738585072014e-308;
 
 // group scratch map (doubles)
 constexpr int gA = 0, gV = 144, gRot = 288 /* 6 x (c, s) */, gL = 300, gRho = 360, gSol = 366 /* 3 x 13 */,
-              gCws = 405 /* 12 */;
+              gCws = 405 /* 12 */, gAl = 417 /* 5 x 4 alphas */, gUd = 437 /* 5 x (uc - u, vc - v) */;
+static_assert(gUd + 10 <= kPnGS, "group scratch map");
 
 struct CvRng {
     uint64_t s;
@@ -94,22 +99,30 @@ __device__ void eig3_desc(double A[3][3], double w[3], double E[3][3]) {
                 }
             }
     }
-    int o[3] = {0, 1, 2};
-    for (int i = 0; i < 2; ++i)
-        for (int j = 0; j < 2 - i; ++j)
-            if (A[o[j]][o[j]] < A[o[j + 1]][o[j + 1]]) { const int t = o[j]; o[j] = o[j + 1]; o[j + 1] = t; }
+    // bubble sort (descending) of (diagonal, eigenvector column) pairs; static indices only
+    double d[3] = {A[0][0], A[1][1], A[2][2]};
+    double C[3][3];  // C[c] = column c of V
+    for (int c = 0; c < 3; ++c)
+        for (int k = 0; k < 3; ++k) C[c][k] = V[k][c];
+    auto cswap = [&](int j) {
+        if (d[j] < d[j + 1]) {
+            const double t = d[j]; d[j] = d[j + 1]; d[j + 1] = t;
+            for (int k = 0; k < 3; ++k) { const double u = C[j][k]; C[j][k] = C[j + 1][k]; C[j + 1][k] = u; }
+        }
+    };
+    cswap(0); cswap(1); cswap(0);
     for (int i = 0; i < 3; ++i) {
-        w[i] = A[o[i]][o[i]];
-        int im = 0;
+        w[i] = d[i];
+        double big = C[i][0];
         for (int k = 1; k < 3; ++k)
-            if (fabs(V[k][o[i]]) > fabs(V[im][o[i]])) im = k;
-        const double sg = V[im][o[i]] >= 0 ? 1.0 : -1.0;
-        for (int k = 0; k < 3; ++k) E[i][k] = sg * V[k][o[i]];
+            if (fabs(C[i][k]) > fabs(big)) big = C[i][k];
+        const double sg = big >= 0 ? 1.0 : -1.0;
+        for (int k = 0; k < 3; ++k) E[i][k] = sg * C[i][k];
     }
 }
 
 // SVD of a 3x3 (row-major A) by one-sided Jacobi: A = U diag(s) V^T, s descending.
-__device__ void svd3(const double* A, double U[3][3], double s[3], double V[3][3]) {
+__device__ __forceinline__ void svd3(const double* A, double U[3][3], double s[3], double V[3][3]) {
     double B[3][3];  // B[col][row]
     double W[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};  // W[col][row]
     for (int c = 0; c < 3; ++c)
@@ -141,19 +154,26 @@ __device__ void svd3(const double* A, double U[3][3], double s[3], double V[3][3
         if (!rot) break;
     }
     double sg[3];
-    int o[3] = {0, 1, 2};
     for (int c = 0; c < 3; ++c) sg[c] = sqrt(B[c][0] * B[c][0] + B[c][1] * B[c][1] + B[c][2] * B[c][2]);
-    for (int i = 0; i < 2; ++i)
-        for (int j = 0; j < 2 - i; ++j)
-            if (sg[o[j]] < sg[o[j + 1]]) { const int t = o[j]; o[j] = o[j + 1]; o[j + 1] = t; }
+    // bubble sort (descending) of (sigma, B column, W column); static indices only
+    auto cswap = [&](int j) {
+        if (sg[j] < sg[j + 1]) {
+            const double t = sg[j]; sg[j] = sg[j + 1]; sg[j + 1] = t;
+            for (int r = 0; r < 3; ++r) {
+                const double b = B[j][r]; B[j][r] = B[j + 1][r]; B[j + 1][r] = b;
+                const double w = W[j][r]; W[j][r] = W[j + 1][r]; W[j + 1][r] = w;
+            }
+        }
+    };
+    cswap(0); cswap(1); cswap(0);
     for (int i = 0; i < 3; ++i) {
-        s[i] = sg[o[i]];
-        for (int r = 0; r < 3; ++r) V[r][i] = W[o[i]][r];
+        s[i] = sg[i];
+        for (int r = 0; r < 3; ++r) V[r][i] = W[i][r];
     }
     for (int i = 0; i < 2; ++i)
-        for (int r = 0; r < 3; ++r) U[r][i] = s[i] > 0 ? B[o[i]][r] / s[i] : (r == i ? 1.0 : 0.0);
+        for (int r = 0; r < 3; ++r) U[r][i] = s[i] > 0 ? B[i][r] / s[i] : (r == i ? 1.0 : 0.0);
     if (s[2] > 1e-300 * s[0] && s[2] > 0) {
-        for (int r = 0; r < 3; ++r) U[r][2] = B[o[2]][r] / s[2];
+        for (int r = 0; r < 3; ++r) U[r][2] = B[2][r] / s[2];
     } else {  // rank-deficient: complete the basis
         U[0][2] = U[1][0] * U[2][1] - U[2][0] * U[1][1];
         U[1][2] = U[2][0] * U[0][1] - U[0][0] * U[2][1];
@@ -256,7 +276,7 @@ struct EpnpData {
 };
 
 // compute_R_and_t for one beta vector (epnp.cpp); returns the mean reprojection error.
-__device__ double epnp_R_t(const EpnpData& D, const double* G, const int* vi, const double* betas, double* R,
+__device__ __forceinline__ double epnp_R_t(const EpnpData& D, const double* G, const int* vi, const double* betas, double* R,
                            double* t) {
     double ccs[4][3] = {};
     for (int i = 0; i < 4; ++i) {
@@ -303,30 +323,37 @@ __device__ double epnp_R_t(const EpnpData& D, const double* G, const int* vi, co
 // compiled out otherwise.
 #ifdef SFMHIP_PNP_PROF
 __device__ unsigned long long g_pprof[16];
+__device__ unsigned long long g_wgt[2 * 1024];  // per-workgroup start / end
 #define PPROF(i) do { if (threadIdx.x == 0) { const unsigned long long t1_ = wall_clock64(); atomicAdd(&g_pprof[i], t1_ - pp_t); pp_t = t1_; } } while (0)
 #define PPROF_INIT unsigned long long pp_t = wall_clock64()
 #define PPROF_ADD(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_pprof[i], (unsigned long long)(v)); } while (0)
+#define PPROF_WG(k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_wgt[2 * blockIdx.x + (k)] = wall_clock64(); } while (0)
 #else
 #define PPROF(i) do {} while (0)
 #define PPROF_INIT do {} while (0)
+#define PPROF_WG(k) do {} while (0)
 #define PPROF_ADD(i, v) do {} while (0)
 #endif
 
-// EPnP on 5 correspondences by a 16-lane group; writes (rvec, tvec) to out[6].
-__device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
+// EPnP on 5 correspondences by a kPnGL-lane group; writes (rvec, tvec) to out[6].
+__device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
     PPROF_INIT;
     // M^T M (12x12) into A, V = I
+    // (alphas and uc - u, vc - v were staged in G by prepare: a dynamic index into D would put
+    // it in scratch memory)
     for (int e = gl; e < 144; e += kPnGL) {
         const int i = e / 12, j = e % 12;
         double acc = 0;
+#pragma unroll
         for (int p = 0; p < 5; ++p) {
             // M rows 2p (u) and 2p+1 (v): col 3c -> a*fu / 0, col 3c+1 -> 0 / a*fv, col 3c+2 -> a*(uc-u) / a*(vc-v)
             const int ci = i / 3, ki = i % 3, cj = j / 3, kj = j % 3;
-            const double ai = D.al[p][ci], aj = D.al[p][cj];
-            const double mu_i = ki == 0 ? ai * D.fu : ki == 1 ? 0.0 : ai * (D.uc - D.us[p][0]);
-            const double mu_j = kj == 0 ? aj * D.fu : kj == 1 ? 0.0 : aj * (D.uc - D.us[p][0]);
-            const double mv_i = ki == 0 ? 0.0 : ki == 1 ? ai * D.fv : ai * (D.vc - D.us[p][1]);
-            const double mv_j = kj == 0 ? 0.0 : kj == 1 ? aj * D.fv : aj * (D.vc - D.us[p][1]);
+            const double ai = G[gAl + 4 * p + ci], aj = G[gAl + 4 * p + cj];
+            const double du = G[gUd + 2 * p], dv = G[gUd + 2 * p + 1];
+            const double mu_i = ki == 0 ? ai * D.fu : ki == 1 ? 0.0 : ai * du;
+            const double mu_j = kj == 0 ? aj * D.fu : kj == 1 ? 0.0 : aj * du;
+            const double mv_i = ki == 0 ? 0.0 : ki == 1 ? ai * D.fv : ai * dv;
+            const double mv_j = kj == 0 ? 0.0 : kj == 1 ? aj * D.fv : aj * dv;
             acc += mu_i * mu_j + mv_i * mv_j;
         }
         G[gA + e] = acc;
@@ -344,19 +371,20 @@ __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
     for (int sweep = 0; sweep < 15; ++sweep) {
         // convergence: off-diagonal vs diagonal mass (group reduction; 9 elements per lane,
         // all loads issued before the sums)
-        double av[9];
+        double av[kJcN];
 #pragma unroll
-        for (int it = 0; it < 9; ++it) av[it] = A[gl + kPnGL * it];
+        for (int it = 0; it < kJcN; ++it) av[it] = A[gl + kPnGL * it];
         double off = 0, dg = 0;
 #pragma unroll
-        for (int it = 0; it < 9; ++it) {
+        for (int it = 0; it < kJcN; ++it) {
             const int e = gl + kPnGL * it;
             if (e / 12 == e % 12) dg += av[it] * av[it]; else off += av[it] * av[it];
         }
-        for (int o = 8; o > 0; o >>= 1) { off += __shfl_xor(off, o, kPnGL); dg += __shfl_xor(dg, o, kPnGL); }
+        for (int o = kPnGL / 2; o > 0; o >>= 1) { off += __shfl_xor(off, o, kPnGL); dg += __shfl_xor(dg, o, kPnGL); }
         if (off <= 1e-30 * dg) break;
         PPROF_ADD(15, 1);
         for (int rnd = 0; rnd < 11; ++rnd) {
+            PPROF(8);
             if (gl < 6) {
                 int p, q;
                 pair_of(rnd, gl, p, q);
@@ -369,14 +397,15 @@ __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
                 G[gRot + 2 * gl + 1] = rot ? t * c : 0.0;
             }
             lds_fence();
+            PPROF(13);
             // A <- J^T A J and V <- V J fused per 2x2 block: block (bi, bj) of A is rows
             // pair bi x columns pair bj, rotated by rows then by columns (the same operations,
             // in the same order, as two separate passes); V block = rows 2bi, 2bi+1 x pair bj.
-            // The 36 blocks are disjoint: a lane loads its 3 blocks, then rotates and stores them.
-            int ia[3][4], iv[3][4];
-            double ld[3][12];
+            // The 36 blocks are disjoint: a lane loads its kJbN blocks, then rotates and stores them.
+            int ia[kJbN][4], iv[kJbN][4];
+            double ld[kJbN][12];
 #pragma unroll
-            for (int it = 0; it < 3; ++it) {
+            for (int it = 0; it < kJbN; ++it) {
                 const int b = min(gl + kPnGL * it, 35);
                 const int bi = b / 6, bj = b - 6 * bi;
                 int pi, qi, pj, qj;
@@ -390,7 +419,7 @@ __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
                 for (int k = 0; k < 4; ++k) { ld[it][4 + k] = A[ia[it][k]]; ld[it][8 + k] = V[iv[it][k]]; }
             }
 #pragma unroll
-            for (int it = 0; it < 3; ++it) {
+            for (int it = 0; it < kJbN; ++it) {
                 if (gl + kPnGL * it >= 36) break;
                 const double ci = ld[it][0], si = ld[it][1], cj = ld[it][2], sj = ld[it][3];
                 const double a00 = ld[it][4], a01 = ld[it][5], a10 = ld[it][6], a11 = ld[it][7];
@@ -407,6 +436,7 @@ __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
                 V[iv[it][3]] = sj * v1p + cj * v1q;
             }
             lds_fence();
+            PPROF(14);
         }
     }
     PPROF(8);
@@ -414,19 +444,23 @@ __device__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
     int vi[4];
     {
         double ev[12];
+#pragma unroll
         for (int i = 0; i < 12; ++i) ev[i] = G[gA + i * 13];
-        bool used[12] = {};
+        unsigned used = 0;  // bit mask: no dynamically indexed arrays
+#pragma unroll
         for (int k = 0; k < 4; ++k) {
             int b = -1;
+            double eb = 0.0;
+#pragma unroll
             for (int i = 0; i < 12; ++i)
-                if (!used[i] && (b < 0 || ev[i] < ev[b])) b = i;
-            used[b] = true;
+                if (!((used >> i) & 1u) && (b < 0 || ev[i] < eb)) { b = i; eb = ev[i]; }
+            used |= 1u << b;
             vi[k] = b;
         }
     }
     lds_fence();
     if (gl < 4) {
-        const int col = vi[gl];
+        const int col = gl == 0 ? vi[0] : gl == 1 ? vi[1] : gl == 2 ? vi[2] : vi[3];
         int im = 0;
         for (int r = 1; r < 12; ++r)
             if (fabs(G[gV + r * 12 + col]) > fabs(G[gV + im * 12 + col])) im = r;
@@ -576,6 +610,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
 
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int h = tid / kPnGL, gl = tid % kPnGL;
+    PPROF_WG(0);
     const int64_t off = offs[p];
     const int n = (int)(offs[p + 1] - off);
     const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
@@ -640,6 +675,12 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
             for (int a = 0; a < 3; ++a) D.al[j][1 + a] = ci[a][0] * d0 + ci[a][1] * d1 + ci[a][2] * d2;
             D.al[j][0] = 1.0 - D.al[j][1] - D.al[j][2] - D.al[j][3];
         }
+        if (gl == 0)
+            for (int j = 0; j < 5; ++j) {
+                for (int a = 0; a < 4; ++a) G[gAl + 4 * j + a] = D.al[j][a];
+                G[gUd + 2 * j] = D.uc - D.us[j][0];
+                G[gUd + 2 * j + 1] = D.vc - D.us[j][1];
+            }
         lds_fence();
     };
     if (n == 5) {  // model_points == npoints: solvePnP(EPnP) on all points, no refinement
@@ -806,15 +847,23 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
                 for (int b = a; b < 6; ++b) { A[a][b] = jtj[k]; A[b][a] = jtj[k]; ++k; }
             const double l = exp(lam * log(10.0));
             for (int a = 0; a < 6; ++a) { A[a][a] *= 1.0 + l; A[a][6] = jte[a]; }
-            for (int c = 0; c < 6; ++c) {  // Gaussian elimination, partial pivoting
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {  // Gaussian elimination, partial pivoting (static indices)
                 int pv = c;
+                double best = fabs(A[c][c]);
+#pragma unroll
                 for (int r = c + 1; r < 6; ++r)
-                    if (fabs(A[r][c]) > fabs(A[pv][c])) pv = r;
-                if (pv != c)
-                    for (int j = 0; j < 7; ++j) { const double t = A[c][j]; A[c][j] = A[pv][j]; A[pv][j] = t; }
+                    if (fabs(A[r][c]) > best) { pv = r; best = fabs(A[r][c]); }
+#pragma unroll
+                for (int r = c + 1; r < 6; ++r)
+                    if (pv == r)
+#pragma unroll
+                        for (int j = 0; j < 7; ++j) { const double t = A[c][j]; A[c][j] = A[r][j]; A[r][j] = t; }
                 if (A[c][c] == 0.0) continue;
+#pragma unroll
                 for (int r = c + 1; r < 6; ++r) {
                     const double fct = A[r][c] / A[c][c];
+#pragma unroll
                     for (int j = c; j < 7; ++j) A[r][j] -= fct * A[c][j];
                 }
             }
@@ -855,6 +904,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         err = eval(true, jtj, jte);
     }
     PPROF(5);
+    PPROF_WG(1);
     if (tid == 0) {
         for (int k = 0; k < 3; ++k) { rvec_out[3 * p + k] = prm[k]; tvec_out[3 * p + k] = prm[3 + k]; }
         ok_out[p] = 1; ninl_out[p] = maxgood; iters_out[p] = s_last + 1;
@@ -875,6 +925,9 @@ extern "C" int sfmhip_debug_pnp_prof(unsigned long long* out) {
     unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(sfmhip::g_pprof), z, sizeof(z)) != hipSuccess) return -2;
     return 0;
+}
+extern "C" int sfmhip_debug_pnp_wg(unsigned long long* out /* [2 * 1024] */) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfmhip::g_wgt), sizeof(unsigned long long) * 2048) == hipSuccess ? 0 : -2;
 }
 #endif
 

@@ -46,4 +46,15 @@ print("fractions:", {nm: round(buf[i] / max(tot, 1), 3) for i, nm in enumerate(n
 sub = ["load+prepare", "MtM", "Jacobi", "signs+L/rho", "betas+GN+R_t", "select+rodrigues_inv"]
 print("EPnP sub-phases of group 0 (us per problem):", {nm: round(buf[6 + i] / P / 100, 1) for i, nm in enumerate(sub)})
 print("Jacobi sweeps per problem (group 0):", buf[15] / P)
+print("Jacobi rounds: rotation / blocks (us per problem, group 0):", round(buf[13] / P / 100, 1), round(buf[14] / P / 100, 1))
+wg = (ctypes.c_ulonglong * 2048)()
+sfm.lib.sfmhip_debug_pnp_wg(wg)
+w = np.array(wg[:2 * P], dtype=np.int64).reshape(P, 2)
+st = (w[:, 0] - w[:, 0].min()) / 100.0
+dur = (w[:, 1] - w[:, 0]) / 100.0
+print("workgroup start offsets (us): min/median/max", st.min(), np.median(st), st.max(), " n started > 50 us late:", int((st > 50).sum()))
+print("workgroup durations (us): min/median/mean/max", dur.min(), np.median(dur), dur.mean().round(1), dur.max())
+print("span first start -> last end (us):", (w[:, 1].max() - w[:, 0].min()) / 100.0)
+it = r["iters"].cpu().numpy()
+print("slowest 5 problems (us, iters):", [(round(float(dur[i]), 1), int(it[i])) for i in np.argsort(dur)[-5:]])
 print("mean ransac iters", r["iters"].float().mean().item())
