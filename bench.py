@@ -290,6 +290,12 @@ def exact_line(sfm, syn, device, args, barrier, cpu=True, int8_ms=None):
             "config": {"workload": f"C3 float descriptors, exact f64 BF-L2 + ratio 0.75 (Matcher(exact=True)): "
                                    f"{N_IMG} imgs x {M_KPT} x {DIM}, all {P} pairs"},
             "kernel_ms": float(np.mean(kms)),
+            "roofline": {"bound": "mfma", "kernel": "match_kernel<256> exact + match_resolve_kernel", "unit": "TOPS",
+                         "achieved": 2.0 * M_KPT * M_KPT * DIM * P / (float(np.mean(kms)) * 1e-3) / 1e12,
+                         "peak": PEAK_INT8_TOPS,
+                         "frac": 2.0 * M_KPT * M_KPT * DIM * P / (float(np.mean(kms)) * 1e-3) / 1e12 / PEAK_INT8_TOPS,
+                         "algorithmic": "2*M*N*d int8 ops per pair (the f64 re-score of the uncertified rows "
+                                        "is counted as overhead, not work)"},
             "rows_rescored": res, "rows_rescored_frac": (res / (P * M_KPT)) if res is not None else None,
             "cost_vs_int8": (ms / int8_ms) if int8_ms else None}
     del bank
@@ -350,9 +356,19 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
 
     wall, _ = timed(dda_step, args.steps, 1, barrier)
     ms = wall / args.steps * 1e3
+    vt = sfm.voxel_traversal(rays, 1.0)
+    # algorithmic bytes of one call: the rays read once + the (N, S_max, 3) array written once
+    dda_bytes = rays.numel() * rays.element_size() + vt.numel() * vt.element_size()
     line = {"metric": "voxel_traversal rays/sec", "value": nr / (ms * 1e-3), "unit": "rays/s", "ms_per_step": ms,
             "config": {"workload": "V1 DDA (voxel_travesal.py semantics): 4096 rays, bin 1, far U(0,64) "
-                                   "(count pass + host S_max + fill pass)"}}
+                                   "(walk into capped rows + host S_max + row-building pass)",
+                       "s_max": int(vt.shape[1])},
+            "roofline": {"bound": "hbm", "kernel": "dda_walk + dda_rows", "unit": "GB/s",
+                         "algorithmic_bytes": dda_bytes, "achieved": dda_bytes / (ms * 1e-3) / 1e9,
+                         "peak": PEAK_HBM_GBS, "frac": dda_bytes / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                         "note": "whole call (two launches + the one S_max read-back) per step: a 4096-ray call "
+                                 "is launch / sync bound, not HBM bound"}}
+    del vt
     if cpu:
         from oracle import voxel as ov
         rr = rays.cpu().numpy()
