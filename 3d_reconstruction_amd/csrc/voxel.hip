@@ -2181,6 +2181,10 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             ord = nullptr;
         (void)hipGetLastError();
     }
+    // refine pass grid (grid-stride over the device-side count; atomic ORs, any grid gives the same masks):
+    // 8192 x 256 threads fill the 6 waves per SIMD its 79 VGPRs allow, where 2048 gave 2 (C5 call
+    // 1.93 -> 1.90 ms, profiles/r3/ab/tsdf_refine_wg_r3bp.txt)
+    const int refine_wg = std::max(1, env_int("SFMHIP_TSDF_REFINE_WG", 8192));
     // frame chunks run in order on the stream, so per-voxel update order is kept
     int rc = SFMHIP_OK;
     for (int f0 = 0; f0 < F; f0 += chunk) {
@@ -2217,7 +2221,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                                W, z0, z1, nf, Hd, Wd, ccam, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
                                nwf, bdec, (unsigned short*)cmask, (unsigned short*)cfree, plist, pcount, tcost);
             if (plist)
-                hipLaunchKernelGGL(tsdf_refine_kernel, dim3(2048), dim3(256), 0, st, H, W, z0, z1, nf, Hd, Wd, pp,
+                hipLaunchKernelGGL(tsdf_refine_kernel, dim3(refine_wg), dim3(256), 0, st, H, W, z0, z1, nf, Hd, Wd, pp,
                                    kp, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, nwf, cmask, cfree, plist,
                                    pcount);
         }

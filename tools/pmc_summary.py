@@ -31,5 +31,5 @@ for k, c in vals.items():
         print(f"   L2 hit    ~ {avg['TCC_HIT_sum'] / (avg['TCC_HIT_sum'] + avg['TCC_MISS_sum']):.1%}")
     if "SQ_ACTIVE_INST_VALU" in avg and "SQ_WAVE_CYCLES" in avg:
         print(f"   VALU-active / wave-cycles {avg['SQ_ACTIVE_INST_VALU'] / avg['SQ_WAVE_CYCLES']:.1%}, "
-              f"wait_any {avg['SQ_WAIT_ANY'] / avg['SQ_WAVE_CYCLES']:.1%}, "
-              f"wait_inst {avg['SQ_WAIT_INST_ANY'] / avg['SQ_WAVE_CYCLES']:.1%}")
+              + (f"wait_any {avg['SQ_WAIT_ANY'] / avg['SQ_WAVE_CYCLES']:.1%}, " if "SQ_WAIT_ANY" in avg else "")
+              + (f"wait_inst {avg['SQ_WAIT_INST_ANY'] / avg['SQ_WAVE_CYCLES']:.1%}" if "SQ_WAIT_INST_ANY" in avg else ""))
