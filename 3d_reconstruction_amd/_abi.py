@@ -54,6 +54,7 @@ SIGNATURES = {
     "sfmhip_last_error": [],
     "sfmhip_device_arch": [ctypes.c_char_p, _i32],
     "sfmhip_scratch_trim": [_u64],
+    "sfmhip_scratch_release_stream": [_p],
     "sfmhip_desc_quantize": [_p, _i32, _i32, _i32, _p, _i32, _p, _p],
     "sfmhip_desc_prepare": [_p, _i32, _i32, _i32, _p, _p, _p, _p],
     "sfmhip_desc_prepare_shifted": [_p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p],
@@ -69,6 +70,7 @@ SIGNATURES = {
     "sfmhip_track_merge": [_p, _i64, _p, _i64, _p, _p, _i64, _p, _p],
     "sfmhip_triangulate_dlt": [_p, _p, _p, _p, _i64, _p, _p],
     "sfmhip_reproj_residual": [_p, _p, _p, _p, _p, _i64, _p, _p],
+    "sfmhip_reproj_residual_host": [_p, _p, _p, _p, _i64, _p, _p],
     "sfmhip_reproj_fd_jacobian": [_p, _p, _p, _p, _p, _i32, _i64, _p, _p, _p, _p],
     "sfmhip_ba_solve": [_p, _p, _p, _p, _p, _i32, _i64, _f64, _f64, _f64, _i32, _p, _p, _p, _p, _p],
     "sfmhip_voxel_traversal_count": [_p, _i64, _f32, _i32, _p, _p],

@@ -9,6 +9,8 @@
 //     -> scipy/optimize/_numdiff.py _compute_absolute_step / _sparse_difference
 // Restated in oracle/geometry.py; the kernels follow the same op order.
 #include "common.h"
+#include <cstring>
+#include <mutex>
 #include "geom_dev.h"
 #include <climits>
 
@@ -510,7 +512,11 @@ extern "C" int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_ob
                            X4, slots, counts, recx, recpr);
         int rc = check_launch("dlt_normal_kernel");
         if (rc == SFMHIP_OK) {
+#ifdef SFMHIP_PROBES   // timing probes (tool-only builds: make EXTRA=-DSFMHIP_PROBES); they return fake triangulations
             static const int probe = [] { const char* e = std::getenv("SFMHIP_DLT_LISTPROBE"); return e ? std::atoi(e) : 0; }();
+#else
+            constexpr int probe = 0;
+#endif
             hipLaunchKernelGGL(dlt_list_kernel, dim3((unsigned)ceil_div(n_waves, 64)), dim3(64), 0, st, P, pair_of_obs,
                                x0, x1, n, X4, slots, counts, recx, recpr, n_waves, probe);
             rc = check_launch("dlt_list_kernel");
@@ -532,6 +538,78 @@ extern "C" int sfmhip_reproj_residual(const double* cam, const double* K, const 
     hipLaunchKernelGGL(residual_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), cam,
                        K, X, pts2d, pair_of_obs, n, r);
     return check_launch("residual_kernel");
+}
+
+// Host-array form of sfmhip_reproj_residual for the cv2/scipy contract (sfm.py:87-91 called by
+// least_squares ~40 times per pair): the inputs are packed into one pinned staging buffer (one
+// H2D copy), the kernel runs, one D2H copy, one stream synchronisation — no per-call device
+// allocation.  The staging buffers are library-owned per device and grow on demand.
+namespace {
+struct HostStage {
+    std::mutex mu;
+    double* h = nullptr;   // pinned: [cam 6 | K 9 | pad 1 | X 3n | pts 2n | r 2n]
+    double* d = nullptr;   // device, same layout
+    size_t cap = 0;        // doubles
+};
+HostStage g_stage[64];
+}  // namespace
+
+extern "C" int sfmhip_reproj_residual_host(const double* cam, const double* K, const double* X,
+                                           const double* pts2d, int64_t n, double* r, void* stream) {
+    SFMHIP_REQUIRE(cam && K && X && r, "sfmhip_reproj_residual_host: null pointer");
+    SFMHIP_REQUIRE(n >= 0 && n < ((int64_t)1 << 40), "sfmhip_reproj_residual_host: bad n");
+    if (n == 0) return SFMHIP_OK;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        set_error("sfmhip_reproj_residual_host: no current HIP device");
+        return SFMHIP_E_HIP;
+    }
+    HostStage& st = g_stage[dev];
+    std::lock_guard<std::mutex> lk(st.mu);
+    const size_t need = 16 + 7 * (size_t)n;
+    if (st.cap < need) {
+        if (st.h) (void)hipHostFree(st.h);
+        if (st.d) (void)hipFree(st.d);
+        st.h = st.d = nullptr;
+        st.cap = 0;
+        const size_t cap = need + need / 2;
+        if (hipHostMalloc((void**)&st.h, cap * sizeof(double), hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void**)&st.d, cap * sizeof(double)) != hipSuccess) {
+            (void)hipGetLastError();
+            if (st.h) (void)hipHostFree(st.h);
+            st.h = st.d = nullptr;
+            set_error("sfmhip_reproj_residual_host: staging allocation failed");
+            return SFMHIP_E_HIP;
+        }
+        st.cap = cap;
+    }
+    double* h = st.h;
+    std::memcpy(h, cam, 6 * sizeof(double));
+    std::memcpy(h + 6, K, 9 * sizeof(double));
+    h[15] = 0.0;
+    std::memcpy(h + 16, X, 3 * (size_t)n * sizeof(double));
+    if (pts2d) std::memcpy(h + 16 + 3 * n, pts2d, 2 * (size_t)n * sizeof(double));
+    else std::memset(h + 16 + 3 * n, 0, 2 * (size_t)n * sizeof(double));
+    hipStream_t s = as_stream(stream);
+    const size_t in_bytes = (16 + 5 * (size_t)n) * sizeof(double);
+    double* d = st.d;
+    hipError_t e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(residual_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, d, d + 6, d + 16,
+                           d + 16 + 3 * n, nullptr, n, d + 16 + 5 * n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(h + 16 + 5 * n, d + 16 + 5 * n, 2 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("sfmhip_reproj_residual_host: %s", hipGetErrorString(e));
+        return SFMHIP_E_HIP;
+    }
+    std::memcpy(r, h + 16 + 5 * n, 2 * (size_t)n * sizeof(double));
+    return SFMHIP_OK;
 }
 
 extern "C" int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, const double* X,

@@ -70,6 +70,21 @@ struct CacheSlot {
 static CacheSlot g_cache[kCacheSlots];
 static std::mutex g_cache_mu;
 
+// Return one idle cached buffer to the pool.  The slot's stream may have been destroyed by the
+// caller since it was cached (sfmhip_scratch_release_stream is the clean way out): HIP then
+// refuses the stream-ordered free, so the buffer is freed after a device synchronisation (all
+// work of a destroyed stream has been issued already) and the error is cleared, so that the
+// caller's next launch check does not report it.
+static void release_slot(CacheSlot& c) {
+    if (hipFreeAsync(c.p, c.s) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipDeviceSynchronize();
+        (void)hipFree(c.p);
+    }
+    (void)hipGetLastError();
+    c = CacheSlot{};
+}
+
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
     int dev = 0;
     const bool have_dev = hipGetDevice(&dev) == hipSuccess;
@@ -92,13 +107,10 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
         *p = g_cache[best].p;
         return hipSuccess;
     }
-    if (empty < 0) {   // table full: drop this stream's smallest idle buffer, else allocate uncached
+    if (empty < 0) {   // table full: drop the smallest idle buffer of any stream, else allocate uncached
         for (int i = 0; i < kCacheSlots; ++i)
             if (!g_cache[i].busy && (empty < 0 || g_cache[i].bytes < g_cache[empty].bytes)) empty = i;
-        if (empty >= 0) {
-            (void)hipFreeAsync(g_cache[empty].p, g_cache[empty].s);
-            g_cache[empty] = CacheSlot{};
-        }
+        if (empty >= 0) release_slot(g_cache[empty]);
     }
     const hipError_t e = pool_alloc(p, bytes, s, dev, true);
     if (e == hipSuccess && empty >= 0) {
@@ -111,8 +123,7 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
                 if (g_cache[i].p && !g_cache[i].busy && (big < 0 || g_cache[i].bytes > g_cache[big].bytes)) big = i;
             if (big < 0) break;
             held -= g_cache[big].bytes;
-            (void)hipFreeAsync(g_cache[big].p, g_cache[big].s);
-            g_cache[big] = CacheSlot{};
+            release_slot(g_cache[big]);
         }
     }
     return e;
@@ -132,7 +143,8 @@ void scratch_free(void* p, hipStream_t s) {
 }
 }  // namespace sfmhip
 
-extern "C" int sfmhip_version(void) { return (0 << 16) | (1 << 8) | 0; }
+// 0.2.0: sfmhip_ba_solve takes n_obs (between n_pairs and ftol); sfmhip_scratch_release_stream
+extern "C" int sfmhip_version(void) { return (0 << 16) | (2 << 8) | 0; }
 
 extern "C" const char* sfmhip_last_error(void) { return sfmhip::g_err; }
 
@@ -146,10 +158,7 @@ extern "C" int sfmhip_scratch_trim(uint64_t keep) {
     {   // the idle cached buffers of this device go back to the pool first
         std::lock_guard<std::mutex> lk(sfmhip::g_cache_mu);
         for (auto& c : sfmhip::g_cache)
-            if (c.p && !c.busy && c.dev == dev) {
-                (void)hipFreeAsync(c.p, c.s);
-                c = sfmhip::CacheSlot{};
-            }
+            if (c.p && !c.busy && c.dev == dev) sfmhip::release_slot(c);
     }
     (void)hipDeviceSynchronize();
     hipMemPool_t pool = sfmhip::scratch_pool(dev);
@@ -172,5 +181,15 @@ extern "C" int sfmhip_device_arch(char* buf, int len) {
     }
     std::strncpy(buf, prop.gcnArchName, (size_t)len - 1);
     buf[len - 1] = '\0';
+    return SFMHIP_OK;
+}
+
+// Release the idle scratch cached for `stream` (call before destroying a stream that was passed
+// to the library; buffers of a destroyed stream are otherwise freed at the next eviction or trim).
+extern "C" int sfmhip_scratch_release_stream(void* stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(sfmhip::g_cache_mu);
+    for (auto& c : sfmhip::g_cache)
+        if (c.p && !c.busy && c.s == s) sfmhip::release_slot(c);
     return SFMHIP_OK;
 }

@@ -1577,8 +1577,12 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
                 (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
             int rc;
             if (half) {
-                const char* penv = std::getenv("SFMHIP_VQ_PROBE");   // timing ablations (tools/bench_vq.py)
+#ifdef SFMHIP_PROBES   // timing ablations (tool-only builds: make EXTRA=-DSFMHIP_PROBES); they return wrong codes
+                const char* penv = std::getenv("SFMHIP_VQ_PROBE");
                 const int probe = penv ? std::atoi(penv) : 0;
+#else
+                constexpr int probe = 0;
+#endif
                 const int64_t n_wg = ((n_obs + 15) / 16 + kVqhWaves - 1) / kVqhWaves;
                 auto kern = probe == 1   ? vq_f16s_kernel<1>
                             : probe == 2 ? vq_f16s_kernel<2>
@@ -1589,8 +1593,12 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
                                    namb);
                 rc = check_launch("vq_f16s_kernel");
             } else if (reg) {
-                const char* penv = std::getenv("SFMHIP_VQ_PROBE");   // timing ablations (tools/bench_vq.py)
+#ifdef SFMHIP_PROBES   // timing ablations (tool-only builds: make EXTRA=-DSFMHIP_PROBES); they return wrong codes
+                const char* penv = std::getenv("SFMHIP_VQ_PROBE");
                 const int probe = penv ? std::atoi(penv) : 0;
+#else
+                constexpr int probe = 0;
+#endif
                 const int waves = probe == 5 ? 16 : kVqrWaves;
                 const int64_t n_wg = ((n_obs + 15) / 16 + waves - 1) / waves;
                 auto kern = probe == 1 ? vq_f32r_kernel<1>

@@ -369,7 +369,7 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
     double* A = G + gA;
     double* V = G + gV;
     for (int sweep = 0; sweep < 15; ++sweep) {
-        // convergence: off-diagonal vs diagonal mass (group reduction; 9 elements per lane,
+        // convergence: off-diagonal vs diagonal mass (group reduction; kJcN (18) elements per lane,
         // all loads issued before the sums)
         double av[kJcN];
 #pragma unroll

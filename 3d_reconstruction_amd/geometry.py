@@ -135,18 +135,29 @@ def projectPoints(objectPoints, rvec, tvec, cameraMatrix, distCoeffs=None):
         raise NotImplementedError("distortion coefficients are not supported (sfm.py passes None)")
     X = np.asarray(objectPoints, np.float64).reshape(-1, 3)
     cam = np.concatenate([np.asarray(rvec, np.float64).ravel(), np.asarray(tvec, np.float64).ravel()])
-    r = _residual(cam, _K_of(cameraMatrix), X, np.zeros((X.shape[0], 2)))
+    r = _residual(cam, _K_of(cameraMatrix), X, None)
     return (-r).reshape(-1, 1, 2), None
 
 
 def _residual(cam, K, X, pts2d):
+    """Host arrays in, host (n,2) out, through sfmhip_reproj_residual_host: one pinned
+    staging buffer, one copy each way and a stream synchronisation per call (scipy's
+    least_squares calls this ~40 times per pair at sfm.py:38).  pts2d None = zeros."""
+    require_gpu()
     n = X.shape[0]
-    camt, Kt = dev(cam.reshape(1, 6), torch.float64), dev(K, torch.float64)
-    Xt, pt = dev(X, torch.float64), dev(pts2d, torch.float64)
-    r = torch.empty((n, 2), dtype=torch.float64, device=Xt.device)
-    call("sfmhip_reproj_residual", ptr(camt), ptr(Kt), ptr(Xt), ptr(pt), None, n, ptr(r), stream_ptr())
-    torch.cuda.synchronize()
-    return r.cpu().numpy()
+    cam = np.ascontiguousarray(cam, np.float64)
+    K = np.ascontiguousarray(K, np.float64)
+    X = np.ascontiguousarray(X, np.float64)
+    r = np.empty((n, 2), np.float64)
+    if pts2d is not None:
+        pts2d = np.ascontiguousarray(pts2d, np.float64)
+        if pts2d.shape != (n, 2):
+            raise ValueError("point_2D must have one (x, y) row per 3D point")
+    if cam.size != 6 or K.size != 9 or X.shape != (n, 3):
+        raise ValueError("cam (6,), K (3,3) and X (n,3) expected")
+    call("sfmhip_reproj_residual_host", cam.ctypes.data, K.ctypes.data, X.ctypes.data,
+         None if pts2d is None else pts2d.ctypes.data, n, r.ctypes.data, stream_ptr())
+    return r
 
 
 def calculate_reprojection_error(x, K, point_2D):

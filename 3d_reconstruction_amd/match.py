@@ -219,20 +219,32 @@ def bf_match(desc0, desc1, ratio=0.75, mutual: bool = False, mode: int = MODE_FL
 
 
 def _exact_scores(x0: torch.Tensor, x1: torch.Tensor, m0: torch.Tensor) -> torch.Tensor:
-    """1 - sqrt(d1/d2) for the matched rows of x0 from f64 difference-form squared
-    distances (the exact mode's metric): d1 to the match, d2 the best other
-    row of x1; 0 for unmatched rows.  Only the matched rows are scored."""
+    """1 - sqrt(d1/d2) for the matched rows of x0 from the exact mode's metric:
+    d = sum_k (f64(a_k) - f64(b_k))^2 summed in k order, one IEEE op per step
+    (oracle/match.py:sq_dist_exact, bit for bit); d1 to the match, d2 the best
+    other row of x1; 0 for unmatched rows.  Only the matched rows are scored, in
+    row chunks of <= 32 MB of f64 distances."""
     sc = torch.zeros(x0.shape[0], dtype=torch.float32, device=x0.device)
     rows = torch.nonzero(m0 >= 0).flatten()
     if rows.numel() == 0:
         return sc
-    a, b = x0[rows].double(), x1.double()
-    D = torch.cdist(a, b, compute_mode="donot_use_mm_for_euclid_dist").square()
-    j = m0[rows]
-    d1 = D[torch.arange(len(rows), device=D.device), j]
-    D[torch.arange(len(rows), device=D.device), j] = float("inf")
-    d2 = D.min(dim=1).values if b.shape[0] > 1 else torch.full_like(d1, float("inf"))
-    sc[rows] = (1.0 - torch.sqrt(d1 / d2.clamp_min(1e-300))).float()
+    a, bt = x0[rows].float().double(), x1.float().double().t().contiguous()
+    n, d = bt.shape[1], bt.shape[0]
+    step = max(1, (32 << 20) // (8 * max(1, n)))
+    for r0 in range(0, a.shape[0], step):
+        ar = a[r0:r0 + step]
+        D = torch.zeros((ar.shape[0], n), dtype=torch.float64, device=a.device)
+        t = torch.empty_like(D)
+        for k in range(d):   # k order, one IEEE op per step (sub, mul, add: no fused form)
+            torch.sub(ar[:, k:k + 1], bt[k][None, :], out=t)
+            t.mul_(t)
+            D.add_(t)
+        ri = torch.arange(ar.shape[0], device=a.device)
+        j = m0[rows[r0:r0 + step]]
+        d1 = D[ri, j]
+        D[ri, j] = float("inf")
+        d2 = D.min(dim=1).values if n > 1 else torch.full_like(d1, float("inf"))
+        sc[rows[r0:r0 + step]] = (1.0 - torch.sqrt(d1 / d2.clamp_min(1e-300))).float()
     return sc
 
 

@@ -55,6 +55,10 @@ int         sfmhip_device_arch(char* buf, int len); /* "gfx950" of device 0   */
  * waiting.  Releases the idle cached buffers of the current device (after a
  * device synchronisation), then trims its pool to `keep` bytes.             */
 int         sfmhip_scratch_trim(uint64_t keep);
+/* Releases the idle scratch cached for `stream`.  Call it before destroying a
+ * stream that was passed to the library (a destroyed stream's buffers are
+ * otherwise freed at the next eviction or trim, after a device sync).      */
+int         sfmhip_scratch_release_stream(void* stream);
 
 /* ---- M1: brute-force L2 matching + ratio test --------------------------
  * Replaces the matcher call site matching.py:20,122-128 (LightGlue forward,
@@ -183,6 +187,14 @@ int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_obs,
 int sfmhip_reproj_residual(const double* cam, const double* K, const double* X,
                            const double* pts2d, const int32_t* pair_of_obs,
                            int64_t n, double* r, void* stream);
+/* HOST arrays (the cv2.projectPoints / calculate_reprojection_error contract
+ * sfm.py:87-91, called by scipy's least_squares ~40 times per pair at sfm.py:38):
+ * cam[6], K[9], X[n][3], pts2d[n][2] (NULL = zeros, i.e. -projectPoints) and
+ * r[n][2] are host memory.  One pinned staging buffer per device (library-owned,
+ * grows on demand): one H2D copy, the kernel, one D2H copy, a synchronisation
+ * of `stream`.  Blocking; thread-safe (the staging is locked per device).     */
+int sfmhip_reproj_residual_host(const double* cam, const double* K, const double* X,
+                                const double* pts2d, int64_t n, double* r, void* stream);
 int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, const double* X,
                               const double* pts2d, const int32_t* pair_of_obs,
                               int n_pairs, int64_t n, const double* f0,

@@ -97,14 +97,14 @@ def test_exact_float_mutual_and_matcher_contract(sfm, gpu):
     r0, r1 = om.bf_match_exact_mutual_pair(x[0], x[1, :300], (3, 4))
     assert np.array_equal(pred["matches0"][0].cpu().numpy(), r0)
     assert np.array_equal(pred["matches1"][0].cpu().numpy(), r1)
-    # scores: the Lowe margin 1 - sqrt(d1/d2) of the f64 distances (> 1 - 0.75 for every accepted match)
+    # scores: the Lowe margin 1 - sqrt(d1/d2) of the oracle's k-ordered f64 distances, bit for bit
+    # (> 1 - 0.75 for every accepted match)
     sc = pred["matching_scores0"][0].cpu().numpy()
-    a, b = x[0].astype(np.float64), x[1, :300].astype(np.float64)
-    D = ((a[:, None, :] - b[None, :, :]) ** 2).sum(-1)
+    D = om.sq_dist_exact(x[0], x[1, :300])
     for i in np.nonzero(r0 >= 0)[0]:
         d1 = D[i, r0[i]]
         d2 = np.min(np.delete(D[i], r0[i]))
-        assert abs(sc[i] - (1 - np.sqrt(d1 / d2))) < 1e-6 and sc[i] > 0.25
+        assert sc[i] == np.float32(1 - np.sqrt(d1 / d2)) and sc[i] > 0.25
     assert (sc[r0 < 0] == 0).all()
 
 

@@ -61,3 +61,35 @@ def test_scratch_dlt_back_to_back_matches_single(sfm, gpu):
     again = sfm.triangulate_batched(tt["P"], tt["pair_of_obs"], tt["x0"], tt["x1"])
     torch.cuda.synchronize()
     assert torch.equal(again, single)
+
+
+def test_scratch_destroyed_stream_then_eviction(sfm, gpu):
+    """A caller-created stream that is destroyed while the library still caches its scratch:
+    a later eviction / trim must not leave a HIP error behind that the next launch check
+    would report, and sfmhip_scratch_release_stream frees a live stream's slots."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    obs, code = _vq_inputs(7)
+    ref_c, ref_d = _vq_on(obs, code, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    for release_first in (False, True):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        ext = torch.cuda.ExternalStream(s.value)
+        c, d = _vq_on(obs, code, ext)   # caches a scratch buffer keyed on s
+        assert hip.hipStreamSynchronize(s) == 0
+        assert torch.equal(c, ref_c) and torch.equal(d, ref_d)
+        if release_first:
+            assert abi.lib.sfmhip_scratch_release_stream(s.value) == 0
+        assert hip.hipStreamDestroy(s) == 0
+        # fill the 32-slot table from another stream so the dead stream's slot is evicted
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            for k in range(40):
+                o2, c2 = _vq_inputs(100 + k, n=1000 + 17 * k)
+                _vq_on(o2, c2, st)
+        torch.cuda.synchronize()
+        assert abi.lib.sfmhip_scratch_trim(0) == 0
+        c, d = _vq_on(obs, code, torch.cuda.current_stream())   # the next launch check is clean
+        torch.cuda.synchronize()
+        assert torch.equal(c, ref_c) and torch.equal(d, ref_d)
