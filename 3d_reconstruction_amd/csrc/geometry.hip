@@ -541,14 +541,14 @@ extern "C" int sfmhip_reproj_residual(const double* cam, const double* K, const 
 }
 
 // Host-array form of sfmhip_reproj_residual for the cv2/scipy contract (sfm.py:87-91 called by
-// least_squares ~40 times per pair): the inputs are packed into one pinned staging buffer (one
-// H2D copy), the kernel runs, one D2H copy, one stream synchronisation — no per-call device
-// allocation.  The staging buffers are library-owned per device and grow on demand.
+// least_squares ~60 times per pair at sfm.py:38): the inputs are packed into one pinned staging
+// buffer that the kernel reads over PCIe and writes the residual back into (zero-copy, ~224 B per
+// observation), then one stream synchronisation — no copies, no per-call device allocation.  The
+// staging buffer is library-owned per device and grows on demand.
 namespace {
 struct HostStage {
     std::mutex mu;
-    double* h = nullptr;   // pinned: [cam 6 | K 9 | pad 1 | X 3n | pts 2n | r 2n]
-    double* d = nullptr;   // device, same layout
+    double* h = nullptr;   // pinned, device-accessible: [cam 6 | K 9 | pad 1 | X 3n | pts 2n | r 2n]
     size_t cap = 0;        // doubles
 };
 HostStage g_stage[64];
@@ -570,15 +570,12 @@ extern "C" int sfmhip_reproj_residual_host(const double* cam, const double* K, c
     const size_t need = 16 + 7 * (size_t)n;
     if (st.cap < need) {
         if (st.h) (void)hipHostFree(st.h);
-        if (st.d) (void)hipFree(st.d);
-        st.h = st.d = nullptr;
+        st.h = nullptr;
         st.cap = 0;
         const size_t cap = need + need / 2;
-        if (hipHostMalloc((void**)&st.h, cap * sizeof(double), hipHostMallocDefault) != hipSuccess ||
-            hipMalloc((void**)&st.d, cap * sizeof(double)) != hipSuccess) {
+        if (hipHostMalloc((void**)&st.h, cap * sizeof(double), hipHostMallocMapped) != hipSuccess) {
             (void)hipGetLastError();
-            if (st.h) (void)hipHostFree(st.h);
-            st.h = st.d = nullptr;
+            st.h = nullptr;
             set_error("sfmhip_reproj_residual_host: staging allocation failed");
             return SFMHIP_E_HIP;
         }
@@ -592,16 +589,13 @@ extern "C" int sfmhip_reproj_residual_host(const double* cam, const double* K, c
     if (pts2d) std::memcpy(h + 16 + 3 * n, pts2d, 2 * (size_t)n * sizeof(double));
     else std::memset(h + 16 + 3 * n, 0, 2 * (size_t)n * sizeof(double));
     hipStream_t s = as_stream(stream);
-    const size_t in_bytes = (16 + 5 * (size_t)n) * sizeof(double);
-    double* d = st.d;
-    hipError_t e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s);
+    double* d = nullptr;
+    hipError_t e = hipHostGetDevicePointer((void**)&d, h, 0);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(residual_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, d, d + 6, d + 16,
                            d + 16 + 3 * n, nullptr, n, d + 16 + 5 * n);
         e = hipGetLastError();
     }
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(h + 16 + 5 * n, d + 16 + 5 * n, 2 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
         (void)hipGetLastError();

@@ -99,14 +99,20 @@ class GridTrainer:
              self.param.numel(), self.lr, self.betas[0], self.betas[1], self.eps, self.step_count,
              1 if zero_grad else 0, ptr(self.touched), 5, stream_ptr())
 
-    def step(self, rays_o, rays_d, gt, z) -> float:
+    def step(self, rays_o, rays_d, gt, z, events=None) -> float:
         """One training iteration; returns loss.item() (plenoxel.py:105-111 reads it
-        every step).  The host waits once, after the Adam step is enqueued."""
+        every step).  The host waits once, after the Adam step is enqueued.
+        ``events``: optional (start, end) torch.cuda.Event pair recorded around the
+        Adam launch on the current stream (timing only)."""
         loss, _, B = self._backward(rays_o, rays_d, gt, z)
+        if events is not None:
+            events[0].record()
         self.optimizer_step()
+        if events is not None:
+            events[1].record()
         return float(loss.item()) / (3 * B) if B else float("nan")
 
-    def sdf_step(self, rays_o, rays_d, gt, num_samples: int = 160, t_rand=None):
+    def sdf_step(self, rays_o, rays_d, gt, num_samples: int = 160, t_rand=None, events=None):
         """One iteration of sdf.py's training loop (sdf.py:427-438) on an SDF-mode
         trainer: the sampler's ray-box test (sdf.py:154-165; rays that miss
         are dropped, sdf.py:229-232), ``num_samples`` stratified depths with the
@@ -123,5 +129,5 @@ class GridTrainer:
         if idx.numel() == 0:
             raise ValueError("No valid rays intersect the grid.")
         z = sample_uniform(tn[idx].contiguous(), tf[idx].contiguous(), num_samples, t_rand)
-        loss = self.step(o[idx].contiguous(), d[idx].contiguous(), t[idx].contiguous(), z)
+        loss = self.step(o[idx].contiguous(), d[idx].contiguous(), t[idx].contiguous(), z, events)
         return loss, valid

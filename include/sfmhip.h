@@ -191,7 +191,7 @@ int sfmhip_reproj_residual(const double* cam, const double* K, const double* X,
  * sfm.py:87-91, called by scipy's least_squares ~40 times per pair at sfm.py:38):
  * cam[6], K[9], X[n][3], pts2d[n][2] (NULL = zeros, i.e. -projectPoints) and
  * r[n][2] are host memory.  One pinned staging buffer per device (library-owned,
- * grows on demand): one H2D copy, the kernel, one D2H copy, a synchronisation
+ * grows on demand) that the kernel reads and writes over PCIe (zero-copy), then a synchronisation
  * of `stream`.  Blocking; thread-safe (the staging is locked per device).     */
 int sfmhip_reproj_residual_host(const double* cam, const double* K, const double* X,
                                 const double* pts2d, int64_t n, double* r, void* stream);
