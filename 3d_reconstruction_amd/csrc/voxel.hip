@@ -4,6 +4,7 @@
 // render_rays) and V5 TSDF integration (build-defined).
 // All fp32 with -ffp-contract=off so the op order matches oracle/voxel.py.
 #include "common.h"
+#include <mutex>
 #include <climits>
 #include <cstdlib>
 #include <algorithm>
@@ -1124,6 +1125,69 @@ constexpr int kTsdfProfWaves = 1 << 18;
 __device__ unsigned long long g_tsdf_prof[kTsdfProfWaves * 3];
 #endif
 
+// One projected frame of one lane's voxel pair (tsdf_kernel's non-PIPE loop and the heavy-tile
+// producers): projection, the per-voxel block test against the pixel's 16x16 {min, max} (exact, with
+// this kernel's own f32 Zc: every depth d of the block has fl(d - Zc) between fl(min - Zc) and
+// fl(max - Zc)) when bmm is given, the bounds-checked depth gather where the test did not decide,
+// and the update inputs: ts and whether each voxel updates (g0, g1).
+__device__ __forceinline__ void tsdf_frame_eval(const float* __restrict__ rec, int f, float vx, f2 vy, float vz,
+                                                bool two, const float* __restrict__ depth, size_t frame, int nbytes,
+                                                int Wd4, int Hd, int Wd, float trunc, float inv_trunc, float free_ts,
+                                                const float2* __restrict__ bmm, int nbu, int nbv, f2& ts, bool& g0,
+                                                bool& g1) {
+    const float* r = rec + f * 16;   // uniform: scalar loads
+    const f2 Q = (f2{r[0], r[1]} * f2s(vx) + f2{r[2], r[3]} * f2s(vz)) + f2{r[4], r[5]};
+    const float Qz = (r[6] * vx + r[7] * vz) + r[8];
+    const f2 Xc = f2s(r[9]) * vy + f2s(Q.x);
+    const f2 Yc = f2s(r[10]) * vy + f2s(Q.y);
+    const f2 Zc = f2s(r[11]) * vy + f2s(Qz);
+    const f2 iz = recip_rn(Zc);
+    const f2 uu = (f2s(r[12]) * Xc) * iz + f2s(r[14]);
+    const f2 vv = (f2s(r[13]) * Yc) * iz + f2s(r[15]);
+    const int iu0 = cvt_flr(uu.x), iv0 = cvt_flr(vv.x);
+    const int iu1 = cvt_flr(uu.y), iv1 = cvt_flr(vv.y);
+    const bool ok0 = z_ok(Zc.x) && (unsigned)iu0 < (unsigned)Wd && (unsigned)iv0 < (unsigned)Hd;
+    const bool ok1 = two && z_ok(Zc.y) && (unsigned)iu1 < (unsigned)Wd && (unsigned)iv1 < (unsigned)Hd;
+    // Per-voxel test against the pixel's 16x16 block {min, max} (exact, with this
+    // kernel's own f32 Zc: every depth d of the block has fl(d - Zc) between
+    // fl(min - Zc) and fl(max - Zc)): free (tsdf = 1) or no update without the depth.
+    bool fr0 = false, fr1 = false, need0 = ok0, need1 = ok1;
+    if (bmm) {
+        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(bmm + (size_t)f * nbv * nbu), (short)0, nbv * nbu * 8, 0x00020000);
+        // 24-bit multiplies (v_mad_u32_u24, full rate; v_mul_lo_u32 is quarter rate): the
+        // block indices are < 2^20 when the pixel is in range, and out-of-range lanes'
+        // offsets only have to stay bounds-checked
+        const auto e0 = __builtin_amdgcn_raw_buffer_load_b64(
+            rb, (int)((__umul24((unsigned)(iv0 >> 4) & 0xFFFFFFu, (unsigned)nbu) + ((unsigned)iu0 >> 4)) << 3), 0, 0);
+        const auto e1 = __builtin_amdgcn_raw_buffer_load_b64(
+            rb, (int)((__umul24((unsigned)(iv1 >> 4) & 0xFFFFFFu, (unsigned)nbu) + ((unsigned)iu1 >> 4)) << 3), 0, 0);
+        const f2 bmn = {__builtin_bit_cast(float, (unsigned)e0[0]), __builtin_bit_cast(float, (unsigned)e1[0])};
+        const f2 bmx = {__builtin_bit_cast(float, (unsigned)e0[1]), __builtin_bit_cast(float, (unsigned)e1[1])};
+        const f2 scm = (bmn - Zc) * f2s(inv_trunc);
+        const f2 smx = bmx - Zc;
+        fr0 = ok0 && bmn.x > 0.f && scm.x >= 1.f;
+        fr1 = ok1 && bmn.y > 0.f && scm.y >= 1.f;
+        need0 = ok0 && !fr0 && bmx.x > 0.f && !(smx.x < -trunc);
+        need1 = ok1 && !fr1 && bmx.y > 0.f && !(smx.y < -trunc);
+    }
+    // bounds-checked gather, only where the block test did not decide
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(depth + (size_t)f * frame), (short)0, nbytes, 0x00020000);
+    f2 dep = {0.f, 0.f};
+    if (need0)
+        dep.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             rs, (int)(__umul24(iv0, Wd4) + ((unsigned)iu0 << 2)), 0, 0));
+    if (need1)
+        dep.y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             rs, (int)(__umul24(iv1, Wd4) + ((unsigned)iu1 << 2)), 0, 0));
+    const f2 sdf = dep - Zc;
+    g0 = fr0 || (need0 && dep.x > 0.f && !(sdf.x < -trunc));
+    g1 = fr1 || (need1 && dep.y > 0.f && !(sdf.y < -trunc));
+    const f2 sc = sdf * f2s(inv_trunc);
+    ts = f2{fr0 ? free_ts : fminf(1.0f, sc.x), fr1 ? free_ts : fminf(1.0f, sc.y)};
+}
+
 // W may take k more exact +1 steps with T = 1 fixed when it is an integer in [0, 2^24 - 512].
 // Updates only add 1 to W (general or division-free; W + 1 is exact below 2^24), at most
 // kTsdfMaxFrames = 512 per launch, so a W that starts the launch an integer in
@@ -1152,7 +1216,8 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
                                                    float trunc, SuperBrick SB, const unsigned* __restrict__ cull,
                                                    const unsigned* __restrict__ freem, int nw, float free_ts,
                                                    const float2* __restrict__ bmm, int nbu, int nbv,
-                                                   const unsigned* __restrict__ order, int easy) {
+                                                   const unsigned* __restrict__ order, int easy,
+                                                   const unsigned char* __restrict__ skip) {
 #ifdef SFMHIP_TSDF_PROF
     const unsigned long long prof_t0 = wall_clock64();
     int prof_nproj = 0;
@@ -1176,7 +1241,9 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
     const float vz = B.mn[2] + (float)z * sz;
     const float inv_trunc = 1.0f / trunc;
     const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
-    const size_t slot = ((((size_t)bz * nty + by) * ntx + bx) * kCullSub + wave) * (size_t)nw;
+    const size_t sub = (((size_t)bz * nty + by) * ntx + bx) * kCullSub + wave;
+    const size_t slot = sub * (size_t)nw;
+    if (skip && skip[sub]) return;   // a heavy sub-tile: tsdf_heavy_kernel fuses it
     if (cull) {   // every frame of the launch culled for this wave: the grid is not even read
         unsigned any = 0u;
         for (int w0 = 0; w0 < F; w0 += 32)
@@ -1340,57 +1407,10 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
 #ifdef SFMHIP_TSDF_PROF
             ++prof_nproj;
 #endif
-            const float* r = rec + f * 16;   // uniform: scalar loads
-            const f2 Q = (f2{r[0], r[1]} * f2s(vx) + f2{r[2], r[3]} * f2s(vz)) + f2{r[4], r[5]};
-            const float Qz = (r[6] * vx + r[7] * vz) + r[8];
-            const f2 Xc = f2s(r[9]) * vy + f2s(Q.x);
-            const f2 Yc = f2s(r[10]) * vy + f2s(Q.y);
-            const f2 Zc = f2s(r[11]) * vy + f2s(Qz);
-            const f2 iz = recip_rn(Zc);
-            const f2 uu = (f2s(r[12]) * Xc) * iz + f2s(r[14]);
-            const f2 vv = (f2s(r[13]) * Yc) * iz + f2s(r[15]);
-            const int iu0 = cvt_flr(uu.x), iv0 = cvt_flr(vv.x);
-            const int iu1 = cvt_flr(uu.y), iv1 = cvt_flr(vv.y);
-            const bool ok0 = z_ok(Zc.x) && (unsigned)iu0 < (unsigned)Wd && (unsigned)iv0 < (unsigned)Hd;
-            const bool ok1 = two && z_ok(Zc.y) && (unsigned)iu1 < (unsigned)Wd && (unsigned)iv1 < (unsigned)Hd;
-            // Per-voxel test against the pixel's 16x16 block {min, max} (exact, with this
-            // kernel's own f32 Zc: every depth d of the block has fl(d - Zc) between
-            // fl(min - Zc) and fl(max - Zc)): free (tsdf = 1) or no update without the depth.
-            bool fr0 = false, fr1 = false, need0 = ok0, need1 = ok1;
-            if (bmm) {
-                const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-                    (void*)(bmm + (size_t)f * nbv * nbu), (short)0, nbv * nbu * 8, 0x00020000);
-                // 24-bit multiplies (v_mad_u32_u24, full rate; v_mul_lo_u32 is quarter rate): the
-                // block indices are < 2^20 when the pixel is in range, and out-of-range lanes'
-                // offsets only have to stay bounds-checked
-                const auto e0 = __builtin_amdgcn_raw_buffer_load_b64(
-                    rb, (int)((__umul24((unsigned)(iv0 >> 4) & 0xFFFFFFu, (unsigned)nbu) + ((unsigned)iu0 >> 4)) << 3), 0, 0);
-                const auto e1 = __builtin_amdgcn_raw_buffer_load_b64(
-                    rb, (int)((__umul24((unsigned)(iv1 >> 4) & 0xFFFFFFu, (unsigned)nbu) + ((unsigned)iu1 >> 4)) << 3), 0, 0);
-                const f2 bmn = {__builtin_bit_cast(float, (unsigned)e0[0]), __builtin_bit_cast(float, (unsigned)e1[0])};
-                const f2 bmx = {__builtin_bit_cast(float, (unsigned)e0[1]), __builtin_bit_cast(float, (unsigned)e1[1])};
-                const f2 scm = (bmn - Zc) * f2s(inv_trunc);
-                const f2 smx = bmx - Zc;
-                fr0 = ok0 && bmn.x > 0.f && scm.x >= 1.f;
-                fr1 = ok1 && bmn.y > 0.f && scm.y >= 1.f;
-                need0 = ok0 && !fr0 && bmx.x > 0.f && !(smx.x < -trunc);
-                need1 = ok1 && !fr1 && bmx.y > 0.f && !(smx.y < -trunc);
-            }
-            // bounds-checked gather, only where the block test did not decide
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc((void*)(depth + (size_t)f * frame), (short)0, nbytes, 0x00020000);
-            f2 dep = {0.f, 0.f};
-            if (need0)
-                dep.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                     rs, (int)(__umul24(iv0, Wd4) + ((unsigned)iu0 << 2)), 0, 0));
-            if (need1)
-                dep.y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                     rs, (int)(__umul24(iv1, Wd4) + ((unsigned)iu1 << 2)), 0, 0));
-            const f2 sdf = dep - Zc;
-            const bool g0 = fr0 || (need0 && dep.x > 0.f && !(sdf.x < -trunc));
-            const bool g1 = fr1 || (need1 && dep.y > 0.f && !(sdf.y < -trunc));
-            const f2 sc = sdf * f2s(inv_trunc);
-            const f2 ts = {fr0 ? free_ts : fminf(1.0f, sc.x), fr1 ? free_ts : fminf(1.0f, sc.y)};
+            f2 ts;
+            bool g0, g1;
+            tsdf_frame_eval(rec, f, vx, vy, vz, two, depth, frame, nbytes, Wd4, Hd, Wd, trunc, inv_trunc, free_ts,
+                            bmm, nbu, nbv, ts, g0, g1);
             // every updating voxel of the wave has tsdf = 1, T = 1 and an integer W: each
             // update is (1 W + 1)/(W + 1) = 1 and W + 1, exactly (no division)
             const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && wi0);
@@ -1416,6 +1436,209 @@ __global__ __launch_bounds__(256) void tsdf_kernel(float* __restrict__ T, float*
         g_tsdf_prof[3 * prof_w + 2] = (unsigned long long)prof_nproj;
     }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// Heavy sub-tiles (surface bands: up to ~225 projected frames of one 8x2x8 sub-tile): the
+// per-voxel update T <- (T W + ts)/(W + 1) must run in frame order (bit-exact with the oracle), but
+// the projection, block test, gather and ts of a frame do not depend on T or W.  tsdf_kernel keeps
+// all of it on the sub-tile's one wave, ~1 us per projected frame of dependent work, which bounds a
+// thin z-slab.  Here one 512-thread workgroup owns one heavy sub-tile: waves 1..7
+// (producers) evaluate the projected frames, interleaved, kHvyK per wave per round, into an LDS
+// round buffer (ts per voxel, NaN = no update); wave 0 (the consumer) holds (T, W) and applies the
+// rounds in frame order — free-space runs from the masks and the projected frames from the buffer,
+// with tsdf_kernel's own update and division-free paths — while the producers fill the next round
+// (double buffer, one barrier per round).  Same updates in the same order: the same bits.
+//   tsdf_heavy_list_kernel: per sub-tile projected-frame count from the final masks; sub-tiles at
+//     or above the threshold are listed (wave-aggregated append) and flagged so tsdf_kernel skips
+//     them; the heavy kernel runs concurrently with tsdf_kernel on a side stream (tsdf_run).
+constexpr int kHvyWaves = 8, kHvyProd = kHvyWaves - 1, kHvyK = 4;   // K: frames per producer per round
+
+__global__ __launch_bounds__(256) void tsdf_heavy_list_kernel(const unsigned* __restrict__ cull,
+                                                              const unsigned* __restrict__ freem, int nw, int F,
+                                                              int64_t nsub, unsigned thr,
+                                                              unsigned char* __restrict__ skip,
+                                                              unsigned* __restrict__ hlist,
+                                                              unsigned* __restrict__ hcount) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned cnt = 0u;
+    if (i < nsub) {
+        for (int w = 0; w < nw; ++w) {
+            const int w0 = w << 5;
+            const unsigned live = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u);
+            const unsigned c = cull[i * nw + w], fr = freem ? freem[i * nw + w] : 0u;
+            cnt += __builtin_popcount(live & ~c & ~fr);
+        }
+        skip[i] = cnt >= thr ? 1 : 0;
+    }
+    const bool heavy = i < nsub && cnt >= thr;
+    const uint64_t b = __builtin_amdgcn_ballot_w64(heavy);
+    if (b == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int first = __builtin_ctzll(b);
+    unsigned base = 0;
+    if (lane == first) base = atomicAdd(hcount, (unsigned)__builtin_popcountll(b));
+    base = __shfl(base, first, 64);
+    if (heavy) hlist[base + __builtin_popcountll(b & ((1ull << lane) - 1ull))] = (unsigned)i;
+}
+
+template <int K>
+__global__ __launch_bounds__(kHvyWaves * 64) void tsdf_heavy_kernel(
+    float* __restrict__ T, float* __restrict__ Wt, int D, int H, int W, int z0, int z1, const float* __restrict__ depth,
+    int F, int Hd, int Wd, const float* __restrict__ rec, Bounds B, float trunc, const unsigned* __restrict__ cull,
+    const unsigned* __restrict__ freem, int nw, float free_ts, const float2* __restrict__ bmm, int nbu, int nbv,
+    int easy, const unsigned* __restrict__ hlist, const unsigned* __restrict__ hcount) {
+    constexpr int R = kHvyProd * K;   // projected frames per round
+    __shared__ f2 buf[2][R][64];
+    __shared__ unsigned short plist[kTsdfMaxFrames];
+    __shared__ int s_np;
+    const int l = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const unsigned count = *hcount;
+    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
+    const float sx = (B.mx[0] - B.mn[0]) / (float)(W - 1);
+    const float sy = (B.mx[1] - B.mn[1]) / (float)(H - 1);
+    const float sz = (B.mx[2] - B.mn[2]) / (float)(D - 1);
+    const float inv_trunc = 1.0f / trunc;
+    const size_t frame = (size_t)Hd * Wd;
+    const int nbytes = (int)(frame * 4);
+    const int Wd4 = Wd * 4;
+    const float no_upd = __builtin_bit_cast(float, 0x7FC00000u);
+    for (unsigned item = blockIdx.x; item < count; item += gridDim.x) {
+        const unsigned sub = __builtin_amdgcn_readfirstlane((int)hlist[item]);
+        const unsigned tile = sub / kCullSub;
+        const int ws = (int)(sub % kCullSub);
+        const int bx = (int)(tile % ntx), by = (int)((tile / ntx) % nty), bz = (int)(tile / ((unsigned)ntx * nty));
+        const int x = bx * kTsdfTX + (l & 3) + 4 * ((l >> 4) & 1);
+        const int z = z0 + bz * kTsdfTZ + ((l >> 2) & 3) + 4 * (l >> 5);
+        const int y = by * kTsdfTY + 2 * ws;
+        const bool inb = x < W && y < H && z < z1;
+        const bool two = inb && y + 1 < H;
+        const float vx = B.mn[0] + (float)x * sx;
+        const f2 vy = {B.mn[1] + (float)y * sy, B.mn[1] + (float)(y + 1) * sy};
+        const float vz = B.mn[2] + (float)z * sz;
+        const size_t slot = (size_t)sub * nw;
+        if (wave == 0) {   // the projected frames in order: lane w < nw takes mask word w
+            unsigned pw = 0u;
+            if (l < nw) {
+                const int w0 = l << 5;
+                pw = (F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u)) & ~cull[slot + l];
+                if (freem) pw &= ~freem[slot + l];
+            }
+            const int c = __builtin_popcount(pw);
+            int incl = c;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                const int up = __shfl_up(incl, off, 64);
+                if (l >= off) incl += up;
+            }
+            int pos = incl - c;
+            while (pw) {
+                plist[pos++] = (unsigned short)((l << 5) + __builtin_ctz(pw));
+                pw &= pw - 1u;
+            }
+            if (l == 15) s_np = incl;
+        }
+        __syncthreads();
+        const int np = s_np;
+        const int nr = (np + R - 1) / R;
+        auto produce = [&](int r) {   // producer wave p: projected frames r R + (p - 1) + kHvyProd j
+            for (int j = wave - 1; j < R; j += kHvyProd) {
+                const int k = r * R + j;
+                if (k >= np) break;
+                const int f = plist[k];
+                f2 ts;
+                bool g0, g1;
+                tsdf_frame_eval(rec, f, vx, vy, vz, two, depth, frame, nbytes, Wd4, Hd, Wd, trunc, inv_trunc,
+                                free_ts, bmm, nbu, nbv, ts, g0, g1);
+                buf[r & 1][j][l] = f2{g0 && inb ? ts.x : no_upd, g1 ? ts.y : no_upd};
+            }
+        };
+        // consumer state (wave 0): (T, W) in registers, tsdf_kernel's update paths, events in frame order
+        const size_t idx = ((size_t)z * H + y) * W + x;
+        f2 tv = f2{1.f, 1.f}, wv = f2{0.f, 0.f};
+        if (wave == 0) {
+            tv = f2{inb ? T[idx] : 1.f, two ? T[idx + W] : 1.f};
+            wv = f2{inb ? Wt[idx] : 0.f, two ? Wt[idx + W] : 0.f};
+        }
+        const bool wild = !(tame(tv.x, wv.x) && tame(tv.y, wv.y));
+        const bool wi0 = w_runs_launch(wv.x), wi1 = w_runs_launch(wv.y);
+        auto update = [&](f2 ts, bool g0, bool g1) {
+            const f2 n = tv * wv + ts;
+            const f2 d = wv + f2s(1.0f);
+            f2 q = div_rn(n, d);
+            if (wild || !(fabsf(n.x) >= 0x1p-100f)) q.x = n.x / d.x;
+            if (wild || !(fabsf(n.y) >= 0x1p-100f)) q.y = n.y / d.y;
+            tv.x = g0 ? q.x : tv.x;
+            wv.x = g0 ? d.x : wv.x;
+            tv.y = g1 ? q.y : tv.y;
+            wv.y = g1 ? d.y : wv.y;
+        };
+        auto free_run = [&](int k) {
+            const bool ones = tv.x == 1.f && tv.y == 1.f && wi0 && wi1;
+            if (free_ts == 1.f && __builtin_amdgcn_ballot_w64(!ones) == 0) {
+                wv = wv + f2s((float)k);
+            } else {
+                for (int i = 0; i < k; ++i) update(f2s(free_ts), inb, two);
+            }
+        };
+        int cw = -1;
+        unsigned ctodo = 0u, cfre = 0u;
+        int done = 0;   // projected frames applied
+        // apply every event before projected frame `upto` (its free-space run included)
+        auto consume = [&](int upto, int r) {
+            while (true) {
+                while (ctodo == 0u) {
+                    if (++cw >= nw) return;
+                    const int w0 = cw << 5;
+                    unsigned t = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u), fr = 0u;
+                    t &= ~cull[slot + cw];
+                    if (freem) fr = freem[slot + cw] & t;
+                    ctodo = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+                    cfre = (unsigned)__builtin_amdgcn_readfirstlane((int)fr);
+                }
+                if (cfre & ctodo & (0u - ctodo)) {   // lowest pending frame is free space: its run
+                    const unsigned full = ctodo & ~cfre;
+                    const unsigned run = ctodo & (full ? (full & (0u - full)) - 1u : ~0u);
+                    ctodo &= ~run;
+                    free_run(__builtin_popcount(run));
+                    continue;
+                }
+                if (done >= upto) return;   // the next projected frame belongs to a later round
+                ctodo &= ctodo - 1u;
+                const f2 ts = buf[r & 1][done - r * R][l];
+                ++done;
+                const bool g0 = ts.x == ts.x, g1 = ts.y == ts.y;   // NaN: no update
+                const bool easy0 = !g0 || (ts.x == 1.f && tv.x == 1.f && wi0);
+                const bool easy1 = !g1 || (ts.y == 1.f && tv.y == 1.f && wi1);
+                if (easy && __builtin_amdgcn_ballot_w64(!(easy0 && easy1)) == 0) {
+                    wv.x = g0 ? wv.x + 1.f : wv.x;
+                    wv.y = g1 ? wv.y + 1.f : wv.y;
+                } else {
+                    update(ts, g0, g1);
+                }
+            }
+        };
+        if (wave != 0) produce(0);
+        __syncthreads();   // round 0 produced
+        for (int r = 0; r < nr; ++r) {   // the consumer applies round r while the producers fill round r + 1
+            if (wave == 0) consume(min(np, (r + 1) * R), r);
+            else if (r + 1 < nr) produce(r + 1);
+            __syncthreads();
+        }
+        if (wave == 0) {
+            consume(np, nr);   // the free-space runs after the last projected frame
+            if (inb) {
+                T[idx] = tv.x;
+                Wt[idx] = wv.x;
+            }
+            if (two) {
+                T[idx + W] = tv.y;
+                Wt[idx + W] = wv.y;
+            }
+        }
+        __syncthreads();   // plist / s_np reused by the next item
+    }
 }
 
 static int env_int(const char* name, int dflt) {
@@ -2035,6 +2258,29 @@ extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, con
 // (wave sub-tile, frame) pairs: stats[0] tested, [1] culled, [2] free space.
 // ext_table != nullptr: the caller's {min, max} block table of every frame over the
 // whole image ([F][nbv][nbu] float2, sfmhip_tsdf_block_table); the block pass is skipped.
+// Library-owned side stream per device (created once): tsdf_heavy_kernel runs on it beside
+// tsdf_kernel on the caller's stream, forked and joined with events, so the call stays ordered on
+// the caller's stream.  The mutex keeps one fork/join sequence at a time per device.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    std::mutex mu;
+};
+static SideStream g_side[64];
+static std::once_flag g_side_once[64];
+static SideStream* side_stream(int dev) {
+    if (dev < 0 || dev >= 64) return nullptr;
+    std::call_once(g_side_once[dev], [dev] {
+        SideStream& ss = g_side[dev];
+        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
+            ss.s = nullptr;
+        (void)hipGetLastError();
+    });
+    return g_side[dev].s ? &g_side[dev] : nullptr;
+}
+
 static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, const float* depth, int F, int Hd,
                     int Wd, const float* poses, const float* Kf, const float* bmin, const float* bmax, float trunc,
                     void* stream, int64_t* stats, const float2* ext_table, int64_t* layer_stats = nullptr) {
@@ -2181,6 +2427,21 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             ord = nullptr;
         (void)hipGetLastError();
     }
+    // heavy sub-tiles (tsdf_heavy_kernel, frame-split over 7 producer waves): the projected-frame
+    // threshold, SFMHIP_TSDF_HEAVY (0 off; default on in latency mode, where a slab is bound by its
+    // surface waves' frame chains), and the persistent grid SFMHIP_TSDF_HEAVY_WG
+    const int heavy_thr = env_int("SFMHIP_TSDF_HEAVY", latency_mode ? 96 : 0);
+    unsigned* hbuf = nullptr;   // [count][list nsub][skip nsub bytes]
+    int dev_id = 0;
+    (void)hipGetDevice(&dev_id);
+    (void)hipGetLastError();
+    SideStream* side = heavy_thr > 0 && cmask && !stats && swz ? side_stream(dev_id) : nullptr;
+    if (side && scratch_alloc((void**)&hbuf, (size_t)(nsub + 1) * sizeof(unsigned) + (size_t)nsub, st) != hipSuccess) {
+        (void)hipGetLastError();
+        hbuf = nullptr;
+    }
+    const int heavy_wg = std::max(1, std::min<int>((int)std::min<int64_t>(nsub, INT_MAX),
+                                                   env_int("SFMHIP_TSDF_HEAVY_WG", 2048)));
     // refine pass grid (grid-stride over the device-side count; atomic ORs, any grid gives the same masks):
     // 8192 x 256 threads fill the 6 waves per SIMD its 79 VGPRs allow, where 2048 gave 2 (C5 call
     // 1.93 -> 1.90 ms, profiles/r3/ab/tsdf_refine_wg_r3bp.txt)
@@ -2275,19 +2536,41 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
 #else
         constexpr size_t prof_lds = 0;
 #endif
+        const unsigned char* skip = nullptr;
+        std::unique_lock<std::mutex> side_lock;
+        if (hbuf) {   // list the heavy sub-tiles, then fork tsdf_heavy_kernel onto the side stream
+            unsigned* hcount = hbuf;
+            unsigned* hlist = hbuf + 1;
+            unsigned char* hskip = reinterpret_cast<unsigned char*>(hbuf + 1 + nsub);
+            (void)hipMemsetAsync(hcount, 0, sizeof(unsigned), st);
+            hipLaunchKernelGGL(tsdf_heavy_list_kernel, dim3((unsigned)ceil_div(nsub, (int64_t)256)), dim3(256), 0, st,
+                               cmask, fmask, nwf, nf, nsub, (unsigned)heavy_thr, hskip, hlist, hcount);
+            side_lock = std::unique_lock<std::mutex>(side->mu);
+            (void)hipEventRecord(side->fork, st);
+            (void)hipStreamWaitEvent(side->s, side->fork, 0);
+            hipLaunchKernelGGL(tsdf_heavy_kernel<kHvyK>, dim3((unsigned)heavy_wg), dim3(kHvyWaves * 64), 0, side->s, T,
+                               Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec, bb, trunc, cmask, fmask, nwf, free_ts,
+                               vox_test ? tab : nullptr, nbu, nbv, easy, hlist, hcount);
+            (void)hipEventRecord(side->join, side->s);
+            skip = hskip;
+        }
         if (swz && pipe)
             hipLaunchKernelGGL((tsdf_kernel<true, true>), grid, dim3(256), prof_lds, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd,
-                               Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, nullptr, nbu, nbv, ord, easy);
+                               Wd, rec, bb, trunc, sb, cmask, fmask, nwf, free_ts, nullptr, nbu, nbv, ord, easy, skip);
         else if (swz)
             hipLaunchKernelGGL(tsdf_kernel<true>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, ord, easy);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, ord, easy,
+                               skip);
         else
             hipLaunchKernelGGL(tsdf_kernel<false>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
-                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, nullptr, easy);
+                               bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, nullptr, easy,
+                               nullptr);
+        if (skip) (void)hipStreamWaitEvent(st, side->join, 0);   // join: the call stays ordered on st
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }
     scratch_free(rec, st);
+    if (hbuf) scratch_free(hbuf, st);
     if (ord) scratch_free(ord, st);
     if (crange) scratch_free(crange, st);
     if (cmask) scratch_free(cmask, st);

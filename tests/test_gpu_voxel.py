@@ -169,14 +169,25 @@ def _tsdf_case(R=48, F=12, Hd=96, Wd=128, focal=110.0):
 
 
 # "auto": small grids run in latency mode; "0" forces the whole-grid path (refinement
-# pass, per-voxel block test)
-LAT_MODES = ["auto", "0"]
+# pass, per-voxel block test); "heavy*": every sub-tile with a projected frame goes through
+# tsdf_heavy_kernel (frame-split producers + ordered consumer), in either mode, and with a
+# 3-workgroup grid so each workgroup takes several sub-tiles
+LAT_MODES = ["auto", "0", "heavy", "heavy0"]
+
+
+def _set_lat(monkeypatch, lat):
+    if lat in ("auto", "heavy"):
+        pass
+    else:
+        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", "0")
+    if lat.startswith("heavy"):
+        monkeypatch.setenv("SFMHIP_TSDF_HEAVY", "1")
+        monkeypatch.setenv("SFMHIP_TSDF_HEAVY_WG", "3")
 
 
 @pytest.mark.parametrize("lat", LAT_MODES)
 def test_tsdf_vs_oracle_bitexact(sfm, gpu, monkeypatch, lat):
-    if lat != "auto":
-        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", lat)
+    _set_lat(monkeypatch, lat)
     R, depth, poses, K = _tsdf_case()
     T = torch.zeros((R, R, R), dtype=torch.float32, device=gpu)
     W = torch.zeros_like(T)
@@ -199,8 +210,7 @@ def test_tsdf_edge_cases_bitexact(sfm, gpu, monkeypatch, Wd, lat):
     grid (Zc <= 0), and frames with a NaN pose, an infinite intrinsic and a
     >= 2^60 translation (skipped as a whole): bit-exact with the oracle."""
     monkeypatch.setenv("SFMHIP_TSDF_CHUNK", "7")  # several launches; Wd = 97: unaligned depth rows
-    if lat != "auto":
-        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", lat)
+    _set_lat(monkeypatch, lat)
     D, H, W_ = 20, 33, 45
     F, Hd = 30, 72
     depth, poses, K = syn.tsdf_scene(F, Hd, Wd, focal=80.0, seed=11)
@@ -241,9 +251,13 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
                 dict(CULL="2", LATENCY="0"), dict(CULL="2", ORDER="0"), dict(CULL="2", BRICK="0"),
                 dict(CULL="2", BRICK="0", CULLSUB="4"), dict(CULL="2", LATENCY="1", PIPE="0"),
                 dict(CULL="2", LATENCY="1", EASY="0"), dict(CULL="2", EASY="0"),
-                dict(CULL="2", LATENCY="0", REFINE="0"), dict(CULL="2", LATENCY="0", VOXTEST="0")]
+                dict(CULL="2", LATENCY="0", REFINE="0"), dict(CULL="2", LATENCY="0", VOXTEST="0"),
+                dict(CULL="2", HEAVY="1"), dict(CULL="2", HEAVY="1", LATENCY="0"),
+                dict(CULL="2", HEAVY="2", HEAVY_WG="5", CHUNK="17"), dict(CULL="2", HEAVY="1", EASY="0"),
+                dict(CULL="2", HEAVY="0", LATENCY="1")]
     for v in variants:
-        for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST", "REFINE", "LATENCY", "ORDER", "BRICK", "PIPE", "EASY"):
+        for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST", "REFINE", "LATENCY", "ORDER", "BRICK", "PIPE", "EASY",
+                  "HEAVY", "HEAVY_WG"):
             monkeypatch.delenv("SFMHIP_TSDF_" + k, raising=False)
         for k, x in v.items():
             monkeypatch.setenv("SFMHIP_TSDF_" + k, x)
@@ -251,7 +265,7 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
         W = torch.zeros_like(T)
         sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95, z0=5, z1=90)
         out.append((T.cpu(), W.cpu()))
-    for i in (1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18):
+    for i in [1, 2] + list(range(4, len(variants))):
         assert torch.equal(out[0][0], out[i][0]) and torch.equal(out[0][1], out[i][1]), variants[i]
     assert (out[0][1] > 0).float().mean() > 0.3
     assert torch.equal(out[0][1], out[3][1])            # probe: same update pattern ...
@@ -265,8 +279,7 @@ def test_tsdf_free_space_near_trunc_bitexact(sfm, gpu, monkeypatch, trunc, lat):
     (the free-space proof's boundary), several truncation distances, prior
     (T, W) state: bit-exact with the oracle, with culling + free space forced."""
     monkeypatch.setenv("SFMHIP_TSDF_CULL", "2")
-    if lat != "auto":
-        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", lat)
+    _set_lat(monkeypatch, lat)
     R, F, Hd, Wd = 32, 6, 64, 80
     rng = np.random.default_rng(int(trunc * 1000))
     zs = (np.float32(-1) + np.arange(R, dtype=np.float32) * (np.float32(2) / np.float32(R - 1)))
@@ -346,13 +359,17 @@ def test_tsdf_c5_full_size_slabs_bitexact(sfm, gpu, monkeypatch):
     monkeypatch.setenv("SFMHIP_TSDF_CULL", "0")
     sfm.tsdf_integrate(T2, W2, *args)
     assert torch.equal(T, T2) and torch.equal(W, W2)
-    # the latency mode of thin slabs (no block-table test, no refinement pass) on the full grid
+    # the latency mode of thin slabs (no block-table test, no refinement pass; heavy sub-tiles
+    # frame-split) on the full grid, and the whole-grid mode with the heavy path
     monkeypatch.setenv("SFMHIP_TSDF_CULL", "1")
-    monkeypatch.setenv("SFMHIP_TSDF_LATENCY", "1")
-    T2.zero_()
-    W2.zero_()
-    sfm.tsdf_integrate(T2, W2, *args)
-    assert torch.equal(T, T2) and torch.equal(W, W2)
+    for lat, heavy in (("1", None), ("0", "48")):
+        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", lat)
+        if heavy:
+            monkeypatch.setenv("SFMHIP_TSDF_HEAVY", heavy)
+        T2.zero_()
+        W2.zero_()
+        sfm.tsdf_integrate(T2, W2, *args)
+        assert torch.equal(T, T2) and torch.equal(W, W2), (lat, heavy)
 
 
 def test_tsdf_zslab_split_equals_whole(sfm, gpu):
