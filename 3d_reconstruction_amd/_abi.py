@@ -81,6 +81,7 @@ SIGNATURES = {
     "sfmhip_nerf_forward": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _i64, _p, _p, _p],
     "sfmhip_grid_to_voxel_major": [_p, _i32, _i32, _i32, _i32, _p, _p],
     "sfmhip_render_rays": [_p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _i64, _i32, _p, _p],
+    "sfmhip_render_rays_sdf": [_p, _p, _i32, _i32, _i32, _p, _p, _i32, _p, _p, _p, _i64, _i32, _p, _p],
     "sfmhip_tsdf_integrate": [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p,
                               _f32, _p],
     "sfmhip_tsdf_block_table": [_p, _i32, _i32, _i32, _i32, _i32, _p, _p],

@@ -325,11 +325,18 @@ __device__ __forceinline__ void sh_colour(const float* k, float x, float y, floa
 // order (optional): wave w renders ray order[w] (rays sorted by where they cross the
 // grid, render_order below); rgb stays indexed by the caller's ray, so the result
 // is the same bits in any order.
+// SIG (sdfp = the reference layout's channel-0 plane (D,H,W), the caller guarantees a finite
+// grid): the sample's sdf is interpolated from that compact plane first (same corners, weights
+// and order: the same value), and the 28-channel voxel lines are fetched only for samples whose
+// alpha is non-zero.  Where alpha = 0, w = T alpha = 0 and the finite colour adds +-0 to sums that
+// end in + 1: the same bits.  Rays with a non-finite direction take the full path.
+template <bool SIG>
 __global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ gvm, int D, int H, int W,
                                                      Bounds B, int mode, const float* __restrict__ ro,
                                                      const float* __restrict__ rd, const float* __restrict__ zv,
                                                      int64_t nrays, int S, float* __restrict__ rgb,
-                                                     const unsigned* __restrict__ order) {
+                                                     const unsigned* __restrict__ order,
+                                                     const float* __restrict__ sdfp) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (w >= nrays) return;  // wave-uniform
@@ -337,6 +344,7 @@ __global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ g
     const float o[3] = {ro[3 * ray], ro[3 * ray + 1], ro[3 * ray + 2]};
     const float d[3] = {rd[3 * ray], rd[3 * ray + 1], rd[3 * ray + 2]};
     const float* z = zv + (size_t)ray * S;
+    const bool sig = SIG && isfinite(d[0]) && isfinite(d[1]) && isfinite(d[2]);
     float carry = 1.f;  // transmittance entering this chunk
     float cr = 0.f, cg = 0.f, cb = 0.f, ws = 0.f;
     for (int s0 = 0; s0 < S; s0 += 64) {
@@ -350,29 +358,41 @@ __global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ g
             float k[27];
 #pragma unroll
             for (int c = 0; c < 27; ++c) k[c] = 0.f;
+            const float delta = (s + 1 < S) ? (z[s + 1] - zs) : 1e10f;
             if (normalise(p, B, mode, g)) {
                 Corners cn;
                 corners(g, D, H, W, cn);
+                bool lines = true;
+                if (sig) {   // sdf from the compact plane; the voxel lines only where alpha != 0
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    int x, y, zz;
-                    if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
-                    const float w = cn.w[q];
-                    const float4* v = reinterpret_cast<const float4*>(gvm + ((((size_t)zz * H + y) * W + x) << 5));
-                    float vv[28];
-#pragma unroll
-                    for (int t = 0; t < 7; ++t) {
-                        const float4 f = v[t];
-                        vv[4 * t] = f.x; vv[4 * t + 1] = f.y; vv[4 * t + 2] = f.z; vv[4 * t + 3] = f.w;
+                    for (int q = 0; q < 8; ++q) {
+                        int x, y, zz;
+                        if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
+                        sdf = sdf + sdfp[((size_t)zz * H + y) * W + x] * cn.w[q];
                     }
-                    sdf = sdf + vv[0] * w;
+                    lines = 1.f - expf((-fmaxf(sdf, 0.f)) * delta) != 0.f;
+                }
+                if (lines) {
 #pragma unroll
-                    for (int c = 0; c < 27; ++c) k[c] = k[c] + vv[1 + c] * w;
+                    for (int q = 0; q < 8; ++q) {
+                        int x, y, zz;
+                        if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
+                        const float w = cn.w[q];
+                        const float4* v = reinterpret_cast<const float4*>(gvm + ((((size_t)zz * H + y) * W + x) << 5));
+                        float vv[28];
+#pragma unroll
+                        for (int t = 0; t < 7; ++t) {
+                            const float4 f = v[t];
+                            vv[4 * t] = f.x; vv[4 * t + 1] = f.y; vv[4 * t + 2] = f.z; vv[4 * t + 3] = f.w;
+                        }
+                        if (!sig) sdf = sdf + vv[0] * w;
+#pragma unroll
+                        for (int c = 0; c < 27; ++c) k[c] = k[c] + vv[1 + c] * w;
+                    }
                 }
             }
             sh_colour(k, d[0], d[1], d[2], col);
             const float sigma = fmaxf(sdf, 0.f);
-            const float delta = (s + 1 < S) ? (z[s + 1] - zs) : 1e10f;
             alpha = 1.f - expf((-sigma) * delta);
         }
         // exclusive multiplicative scan of (1 - alpha) across the wave
@@ -2200,9 +2220,9 @@ __global__ __launch_bounds__(256) void render_scatter_kernel(const unsigned* __r
     order[pos] = (unsigned)i;
 }
 
-extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, const float* bmin,
-                                  const float* bmax, int mask_mode, const float* rays_o, const float* rays_d,
-                                  const float* z, int64_t B, int S, float* rgb, void* stream) {
+static int render_run(const float* grid_vm, const float* sdfp, int D, int H, int W, const float* bmin,
+                      const float* bmax, int mask_mode, const float* rays_o, const float* rays_d, const float* z,
+                      int64_t B, int S, float* rgb, void* stream) {
     SFMHIP_REQUIRE(grid_vm && bmin && bmax && rays_o && rays_d && z && rgb, "sfmhip_render_rays: null pointer");
     SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && B >= 0 && S >= 1, "sfmhip_render_rays: bad shape");
     SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_render_rays: mask_mode must be 0 or 1");
@@ -2242,16 +2262,38 @@ extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, con
             rc = check_launch("render_scatter_kernel");
         }
         if (rc == SFMHIP_OK) {
-            hipLaunchKernelGGL(render_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb, mask_mode,
-                               rays_o, rays_d, z, B, S, rgb, order);
+            if (sdfp)
+                hipLaunchKernelGGL(render_kernel<true>, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb,
+                                   mask_mode, rays_o, rays_d, z, B, S, rgb, order, sdfp);
+            else
+                hipLaunchKernelGGL(render_kernel<false>, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb,
+                                   mask_mode, rays_o, rays_d, z, B, S, rgb, order, nullptr);
             rc = check_launch("render_kernel");
         }
         scratch_free(scratch, st);
         return rc;
     }
-    hipLaunchKernelGGL(render_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb, mask_mode, rays_o,
-                       rays_d, z, B, S, rgb, nullptr);
+    if (sdfp)
+        hipLaunchKernelGGL(render_kernel<true>, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb, mask_mode,
+                           rays_o, rays_d, z, B, S, rgb, nullptr, sdfp);
+    else
+        hipLaunchKernelGGL(render_kernel<false>, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb,
+                           mask_mode, rays_o, rays_d, z, B, S, rgb, nullptr, nullptr);
     return check_launch("render_kernel");
+}
+
+extern "C" int sfmhip_render_rays(const float* grid_vm, int D, int H, int W, const float* bmin,
+                                  const float* bmax, int mask_mode, const float* rays_o, const float* rays_d,
+                                  const float* z, int64_t B, int S, float* rgb, void* stream) {
+    return render_run(grid_vm, nullptr, D, H, W, bmin, bmax, mask_mode, rays_o, rays_d, z, B, S, rgb, stream);
+}
+
+extern "C" int sfmhip_render_rays_sdf(const float* grid_vm, const float* sdf_plane, int D, int H, int W,
+                                      const float* bmin, const float* bmax, int mask_mode, const float* rays_o,
+                                      const float* rays_d, const float* z, int64_t B, int S, float* rgb,
+                                      void* stream) {
+    SFMHIP_REQUIRE(sdf_plane, "sfmhip_render_rays_sdf: null sdf plane");
+    return render_run(grid_vm, sdf_plane, D, H, W, bmin, bmax, mask_mode, rays_o, rays_d, z, B, S, rgb, stream);
 }
 
 // stats != nullptr: run only the culling pre-passes (forced on) and count

@@ -114,6 +114,7 @@ class VoxelGrid:
         self.bmax = _f3(max_bound)
         self.mask_mode = int(mask_mode)
         self._vm = None
+        self._finite = None
 
     @classmethod
     def plenoxel(cls, voxel_grid: torch.Tensor, scale: float = 1.5) -> "VoxelGrid":
@@ -182,9 +183,21 @@ class VoxelGrid:
         zz = dev(z, torch.float32)
         B, S = zz.shape
         rgb = torch.empty((B, 3), dtype=torch.float32, device=o.device)
-        call("sfmhip_render_rays", ptr(self.voxel_major()), self.D, self.H, self.W, _host_ptr(self.bmin),
-             _host_ptr(self.bmax), self.mask_mode, ptr(o), ptr(d), ptr(zz), B, S, ptr(rgb), stream_ptr())
+        vm = self.voxel_major()
+        if self.finite():   # sdf from the compact channel-0 plane, voxel lines only where alpha != 0
+            call("sfmhip_render_rays_sdf", ptr(vm), ptr(self.grid[0]), self.D, self.H, self.W, _host_ptr(self.bmin),
+                 _host_ptr(self.bmax), self.mask_mode, ptr(o), ptr(d), ptr(zz), B, S, ptr(rgb), stream_ptr())
+        else:
+            call("sfmhip_render_rays", ptr(vm), self.D, self.H, self.W, _host_ptr(self.bmin),
+                 _host_ptr(self.bmax), self.mask_mode, ptr(o), ptr(d), ptr(zz), B, S, ptr(rgb), stream_ptr())
         return rgb
+
+    def finite(self) -> bool:
+        """Whether every grid value is finite (cached with the voxel-major copy): the render
+        may then skip the colour lines of samples with alpha = 0, bit-identically."""
+        if getattr(self, "_finite", None) is None:
+            self._finite = bool(torch.isfinite(self.grid).all().item())
+        return self._finite
 
 
 def tsdf_integrate(T: torch.Tensor, Wt: torch.Tensor, depth: torch.Tensor, poses: torch.Tensor,

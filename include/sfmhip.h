@@ -267,6 +267,15 @@ int sfmhip_render_rays(const float* grid_vm, int D, int H, int W,
                        const float* bmin, const float* bmax, int mask_mode,
                        const float* rays_o, const float* rays_d, const float* z,
                        int64_t B, int S, float* rgb, void* stream);
+/* The same render with the SDF (channel 0) also given as the compact reference
+ * plane (D,H,W) f32 (grid channel 0 of the (C,D,H,W) layout): each sample's sdf
+ * is read from it and the 28-channel voxel lines are fetched only for samples
+ * with alpha != 0 (w = T*alpha = 0 otherwise).  The caller guarantees a finite
+ * grid; the result is then bit-identical to sfmhip_render_rays.              */
+int sfmhip_render_rays_sdf(const float* grid_vm, const float* sdf_plane, int D, int H, int W,
+                           const float* bmin, const float* bmax, int mask_mode,
+                           const float* rays_o, const float* rays_d, const float* z,
+                           int64_t B, int S, float* rgb, void* stream);
 
 /* ---- V5: TSDF integration (build-defined) --------------
  * T, Wt: (D,H,W) f32 grids updated in place for z-slices [z0, z1).

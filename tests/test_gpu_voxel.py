@@ -142,6 +142,46 @@ def test_render_ray_order_bitexact(sfm, gpu, monkeypatch, cfg):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("sort", ["0", "1"])
+def test_render_sdf_plane_skip_bitexact(sfm, gpu, monkeypatch, sort):
+    """sfmhip_render_rays_sdf (sdf from the compact channel-0 plane, colour lines only for
+    samples with alpha != 0) gives the same bits as sfmhip_render_rays on a finite grid whose
+    sdf is negative for about half the samples, incl. rays that miss the grid, a ray with a
+    non-finite direction (full path) and a ragged tail; a grid with a non-finite SH value
+    renders through the full path (VoxelGrid.finite() False).  plenoxel.py:71-93, sdf.py:376."""
+    monkeypatch.setenv("SFMHIP_RENDER_SORT", sort)
+    abi = importlib.import_module("3d_reconstruction_amd._abi")
+    g = torch.Generator(device=gpu).manual_seed(9)
+    N, B, S = 48, 8192 + 77, 100
+    grid = torch.randn((28, N, N + 3, N + 5), generator=g, device=gpu) * 0.1
+    vg = sfm.VoxelGrid.plenoxel(grid, 1.5)
+    ro = torch.randn((B, 3), generator=g, device=gpu) * 0.6 + torch.tensor([0.0, 0.0, -3.0], device=gpu)
+    rd = torch.randn((B, 3), generator=g, device=gpu) * 0.4 + torch.tensor([0.0, 0.0, 1.0], device=gpu)
+    rd = rd / rd.norm(dim=1, keepdim=True)
+    rd[5] = torch.tensor([float("nan"), 0.0, 1.0], device=gpu)
+    z = torch.sort(torch.rand((B, S), generator=g, device=gpu) * 4 + 2, 1).values.contiguous()
+    bmin, bmax = np.full(3, -1.5, np.float32), np.full(3, 1.5, np.float32)
+    outs = []
+    for name, extra in (("sfmhip_render_rays", ()), ("sfmhip_render_rays_sdf", (vg.grid[0].data_ptr(),))):
+        rgb = torch.empty((B, 3), dtype=torch.float32, device=gpu)
+        abi.call(name, vg.voxel_major().data_ptr(), *extra, N, N + 3, N + 5, bmin.ctypes.data, bmax.ctypes.data, 1,
+                 ro.data_ptr(), rd.data_ptr(), z.data_ptr(), B, S, rgb.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        outs.append(rgb)
+    assert vg.finite()
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(vg.render(ro, rd, z), outs[0])
+    assert torch.isnan(outs[0][5]).all()
+    grid2 = grid.clone()
+    grid2[5, 10, 10, 10] = float("inf")
+    vg2 = sfm.VoxelGrid.plenoxel(grid2, 1.5)
+    assert not vg2.finite()
+    r2 = vg2.render(ro, rd, z)
+    rgb = torch.empty((B, 3), dtype=torch.float32, device=gpu)
+    abi.call("sfmhip_render_rays", vg2.voxel_major().data_ptr(), N, N + 3, N + 5, bmin.ctypes.data, bmax.ctypes.data, 1,
+             ro.data_ptr(), rd.data_ptr(), z.data_ptr(), B, S, rgb.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(r2, rgb)
+
+
 def test_voxel_traversal_cap_boundary(sfm, gpu, monkeypatch):
     """The one-walk form at the edge of its row width: cap = S (every ray fits:
     the rows' prefix is returned) and cap = S - 1 (the longest ray does not fit:
