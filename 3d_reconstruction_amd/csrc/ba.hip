@@ -44,6 +44,7 @@ __device__ unsigned long long g_ba_prof[4096 * kProfPhases];
 #endif
 
 constexpr int kRec = 26;   // per observation: J (18: u row, v row), f (2), scale_inv of the point (3), X_new (3)
+constexpr int kRecRC = 6;  // RC records: scale_inv of the point (3) at fields 20-22 of the pass view, X_new (3)
 
 // sum of K doubles over the workgroup (NW waves); every thread receives the totals in out[]
 template <int NW, int K>
@@ -174,12 +175,13 @@ struct BaState {   // LDS: the iteration's scalars, written by thread 0 or by bl
 // observation: AoS (record i at i * kRec) or, SOA, field-major within the pair
 // (field f of record i at f * n + i: a wave's load of one field is 64
 // consecutive doubles).  Passes copy the fields they use into registers.
-template <bool SOA>
+template <bool SOA, bool RC = false>
 struct Recs {
     double* base;
     int n;
     __device__ __forceinline__ double* at(int i, int f) const {
-        return SOA ? base + (size_t)f * n + i : base + (size_t)i * kRec + f;
+        if (RC) f -= 20;   // only fields 20-25 are stored
+        return SOA ? base + (size_t)f * n + i : base + (size_t)i * (RC ? kRecRC : kRec) + f;
     }
     template <int LO, int HI>
     __device__ __forceinline__ void load(int i, double* r) const {
@@ -196,7 +198,7 @@ struct Recs {
 // for i = tid, tid + NT, ... < n: body(i, r) with r[LO, HI) = record i, the next
 // record's loads issued before the current one's arithmetic (one record ahead)
 template <int NT, int LO, int HI, bool SOA, typename F>
-__device__ __forceinline__ void stream_recs(const Recs<SOA>& rec, int n, F&& body) {
+__device__ __forceinline__ void stream_recs(const Recs<SOA, false>& rec, int n, F&& body) {
     double nx[kRec];
     int i = threadIdx.x;
     if (i < n) rec.template load<LO, HI>(i, nx);
@@ -218,7 +220,12 @@ __device__ __forceinline__ void resid(const double* R, const double* c, const do
     rv = pts[1] - v;
 }
 
-template <int NT, bool SOA>
+// RC (recompute): the records hold only the point column scales (3) and the trial point (3);
+// every pass re-derives the observation's J (18) and f (2) from X, pts and the pair's camera
+// (fd_obs: the same function, the same values as the Jacobian pass) instead of re-reading a
+// 23-double record written by it — ~450 f64 flops per observation and pass against 184 B of
+// record traffic (5.5 GB per launch at 23 % L2 hits).
+template <int NT, bool SOA, bool RC = false>
 __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io, const double* __restrict__ Kall,
                                                     double* __restrict__ X, const double* __restrict__ pts2d,
                                                     const int64_t* __restrict__ off, int64_t n_obs, double ftol,
@@ -238,7 +245,20 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     const double* k = Kall + (size_t)p * 9;
     double* Xp = X + 3 * o0;
     const double* pts = pts2d + 2 * o0;
-    const Recs<SOA> rec{scratch + (size_t)o0 * kRec, n};
+    const Recs<SOA, RC> rec{scratch + (size_t)o0 * (RC ? kRecRC : kRec), n};
+    // the pass view of observation i: r[0..17] J, r[18..19] f, r[20..22] point scale_inv
+    auto pass_rec = [&](int i, double* r) {
+        if constexpr (RC) {
+            const double Xi[3] = {Xp[3 * i], Xp[3 * i + 1], Xp[3 * i + 2]};
+            double f[2];
+            rec.template load<20, 23>(i, r);
+            fd_obs(&S.R[0][0], S.cam, k, Xi, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
+            r[18] = f[0];
+            r[19] = f[1];
+        } else {
+            rec.template load<0, 23>(i, r);
+        }
+    };
     if (tid < 6) S.cam[tid] = cam_io[(size_t)p * 6 + tid];
     __syncthreads();
     if (n == 0) {
@@ -290,7 +310,8 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 else si = fmax(si, r[20 + c]);
                 r[20 + c] = si;
             }
-            rec.template store<0, 23>(i, r);
+            if (RC) rec.template store<20, 23>(i, r);
+            else rec.template store<0, 23>(i, r);
         }
         gmax = block_max<NW>(gmax, S.red);
         block_sum<NW, 13>(acc, S.red, S.tot);
@@ -343,7 +364,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             double acc[2] = {0.0, 0.0};
             for (int i = tid; i < n; i += NT) {
                 double r[kRec];
-                rec.template load<0, 23>(i, r);
+                pass_rec(i, r);
                 double vu = 0.0, vv = 0.0;
                 for (int c = 0; c < 6; ++c) { vu -= r[c] * S.dc[c] * S.ghc[c]; vv -= r[9 + c] * S.dc[c] * S.ghc[c]; }
                 for (int c = 0; c < 3; ++c) {
@@ -380,7 +401,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             for (int e = 0; e < 27; ++e) acc[e] = 0.0;
             for (int i = tid; i < n; i += NT) {
                 double r[kRec];
-                rec.template load<0, 23>(i, r);
+                pass_rec(i, r);
                 double C[2][6], Pp[2][3];
                 for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
                 for (int c = 0; c < 3; ++c) {
@@ -419,7 +440,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             double acc[7] = {0};   // gnc (6), point part of g_h . gn_h
             for (int i = tid; i < n; i += NT) {
                 double r[kRec];
-                rec.template load<0, 23>(i, r);
+                pass_rec(i, r);
                 double C[2][6], Pp[2][3];
                 for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
                 for (int c = 0; c < 3; ++c) {
@@ -490,7 +511,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             double acc[6] = {0};   // JS1.JS1, JS1.JS2u, JS2u.JS2u, s2u . g_h and s1 . g_h (point parts), |s2u pts|^2
             for (int i = tid; i < n; i += NT) {
                 double r[kRec];
-                rec.template load<0, 23>(i, r);
+                pass_rec(i, r);
                 double s1[3], s2[3];
                 point_vecs(r, s1, s2);
                 double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
@@ -563,7 +584,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
             for (int i = tid; i < n; i += NT) {
                 double r[kRec];
-                rec.template load<0, 23>(i, r);
+                pass_rec(i, r);
                 double s1[3], s2[3];
                 point_vecs(r, s1, s2);
                 double ju = 0, jv = 0;
@@ -673,7 +694,8 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
     }
     // SFMHIP_BA_VARIANT (A/B runs): 2 (default) field-major records, 512 threads; 1 field-major, 256 threads;
     // 0 AoS records, 256 threads; 3 AoS, 512 threads (profiles/r3/ba_variants_r3m.txt)
-    static const int variant = [] { const char* e = std::getenv("SFMHIP_BA_VARIANT"); return e ? std::atoi(e) : 2; }();
+    // 4 / 5 / 6: the recompute form (RC) at 512 / 256 / 1024 threads
+    const int variant = [] { const char* e = std::getenv("SFMHIP_BA_VARIANT"); return e ? std::atoi(e) : 2; }();
     switch (variant) {
         case 0:
             hipLaunchKernelGGL((ba_trf_kernel<256, false>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
@@ -686,6 +708,18 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
         case 3:
             hipLaunchKernelGGL((ba_trf_kernel<512, false>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
                                n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+            break;
+        case 4:
+            hipLaunchKernelGGL((ba_trf_kernel<512, true, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d,
+                               pair_off, n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+            break;
+        case 5:
+            hipLaunchKernelGGL((ba_trf_kernel<256, true, true>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d,
+                               pair_off, n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+            break;
+        case 6:
+            hipLaunchKernelGGL((ba_trf_kernel<1024, true, true>), dim3(n_pairs), dim3(1024), 0, st, cam, K, X, pts2d,
+                               pair_off, n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
             break;
         default:
             hipLaunchKernelGGL((ba_trf_kernel<512, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,

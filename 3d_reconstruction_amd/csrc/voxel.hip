@@ -2304,7 +2304,7 @@ extern "C" int sfmhip_render_rays_sdf(const float* grid_vm, const float* sdf_pla
 // tsdf_kernel on the caller's stream, forked and joined with events, so the call stays ordered on
 // the caller's stream.  The mutex keeps one fork/join sequence at a time per device.
 struct SideStream {
-    hipStream_t s = nullptr;
+    hipStream_t s = nullptr, hi = nullptr;   // hi: the device's greatest stream priority
     hipEvent_t fork = nullptr, join = nullptr;
     std::mutex mu;
 };
@@ -2314,6 +2314,10 @@ static SideStream* side_stream(int dev) {
     if (dev < 0 || dev >= 64) return nullptr;
     std::call_once(g_side_once[dev], [dev] {
         SideStream& ss = g_side[dev];
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&ss.hi, hipStreamNonBlocking, hi) != hipSuccess)
+            ss.hi = nullptr;
         if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
@@ -2470,9 +2474,10 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         (void)hipGetLastError();
     }
     // heavy sub-tiles (tsdf_heavy_kernel, frame-split over 7 producer waves): the projected-frame
-    // threshold, SFMHIP_TSDF_HEAVY (0 off; default on in latency mode, where a slab is bound by its
-    // surface waves' frame chains), and the persistent grid SFMHIP_TSDF_HEAVY_WG
-    const int heavy_thr = env_int("SFMHIP_TSDF_HEAVY", latency_mode ? 96 : 0);
+    // threshold SFMHIP_TSDF_HEAVY (0 = off, the default) and the persistent grid SFMHIP_TSDF_HEAVY_WG.
+    // Measured slower at every threshold and launch form (N = 8 centre slab 0.35 ms off,
+    // 0.47-0.54 ms on; whole grid 1.93 vs 2.42-2.90 ms): kept as a tested A/B form only
+    const int heavy_thr = env_int("SFMHIP_TSDF_HEAVY", 0);
     unsigned* hbuf = nullptr;   // [count][list nsub][skip nsub bytes]
     int dev_id = 0;
     (void)hipGetDevice(&dev_id);
@@ -2579,6 +2584,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         constexpr size_t prof_lds = 0;
 #endif
         const unsigned char* skip = nullptr;
+        bool joined = true;
         std::unique_lock<std::mutex> side_lock;
         if (hbuf) {   // list the heavy sub-tiles, then fork tsdf_heavy_kernel onto the side stream
             unsigned* hcount = hbuf;
@@ -2587,13 +2593,20 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             (void)hipMemsetAsync(hcount, 0, sizeof(unsigned), st);
             hipLaunchKernelGGL(tsdf_heavy_list_kernel, dim3((unsigned)ceil_div(nsub, (int64_t)256)), dim3(256), 0, st,
                                cmask, fmask, nwf, nf, nsub, (unsigned)heavy_thr, hskip, hlist, hcount);
-            side_lock = std::unique_lock<std::mutex>(side->mu);
-            (void)hipEventRecord(side->fork, st);
-            (void)hipStreamWaitEvent(side->s, side->fork, 0);
-            hipLaunchKernelGGL(tsdf_heavy_kernel<kHvyK>, dim3((unsigned)heavy_wg), dim3(kHvyWaves * 64), 0, side->s, T,
+            // SFMHIP_TSDF_HEAVY_MODE (A/B): 0 side stream, 1 high-priority side stream, 2 before
+            // tsdf_kernel on the caller's stream
+            const int hmode = env_int("SFMHIP_TSDF_HEAVY_MODE", 1);
+            hipStream_t hs = hmode == 2 ? st : hmode == 1 && side->hi ? side->hi : side->s;
+            if (hs != st) {
+                side_lock = std::unique_lock<std::mutex>(side->mu);
+                (void)hipEventRecord(side->fork, st);
+                (void)hipStreamWaitEvent(hs, side->fork, 0);
+            }
+            hipLaunchKernelGGL(tsdf_heavy_kernel<kHvyK>, dim3((unsigned)heavy_wg), dim3(kHvyWaves * 64), 0, hs, T,
                                Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec, bb, trunc, cmask, fmask, nwf, free_ts,
                                vox_test ? tab : nullptr, nbu, nbv, easy, hlist, hcount);
-            (void)hipEventRecord(side->join, side->s);
+            if (hs != st) (void)hipEventRecord(side->join, hs);
+            joined = hs == st;
             skip = hskip;
         }
         if (swz && pipe)
@@ -2607,7 +2620,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             hipLaunchKernelGGL(tsdf_kernel<false>, grid, dim3(256), 0, st, T, Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec,
                                bb, trunc, sb, cmask, fmask, nwf, free_ts, vox_test ? tab : nullptr, nbu, nbv, nullptr, easy,
                                nullptr);
-        if (skip) (void)hipStreamWaitEvent(st, side->join, 0);   // join: the call stays ordered on st
+        if (!joined) (void)hipStreamWaitEvent(st, side->join, 0);   // join: the call stays ordered on st
         rc = check_launch("tsdf_kernel");
         if (rc != SFMHIP_OK) break;
     }

@@ -36,7 +36,7 @@ def timed(fn, reps=5):
 
 
 def setenv(**kw):
-    for k in ("HEAVY", "HEAVY_WG", "LATENCY"):
+    for k in ("HEAVY", "HEAVY_WG", "LATENCY", "HEAVY_MODE"):
         os.environ.pop("SFMHIP_TSDF_" + k, None)
     for k, v in kw.items():
         os.environ["SFMHIP_TSDF_" + k] = str(v)
@@ -51,25 +51,27 @@ def run_whole():
 setenv()
 run_whole()
 Tref, Wref = T.clone(), W.clone()
-whole_variants = [dict(), dict(HEAVY=160), dict(HEAVY=128), dict(HEAVY=96), dict(HEAVY=64)]
+whole_variants = [dict(), dict(HEAVY=128, HEAVY_MODE=1), dict(HEAVY=128, HEAVY_MODE=2), dict(HEAVY=128, HEAVY_MODE=0)]
 for rep in range(2):
     for v in whole_variants:
         setenv(**v)
         t = timed(run_whole)
         same = torch.equal(T, Tref) and torch.equal(W, Wref)
         print(f"whole grid {v or 'default'}: {t:.3f} ms  identical={same}", flush=True)
+slab_variants = [dict(HEAVY=0), dict(HEAVY=96, HEAVY_MODE=0), dict(HEAVY=96, HEAVY_MODE=1), dict(HEAVY=96, HEAVY_MODE=2),
+                 dict(HEAVY=160, HEAVY_MODE=1), dict(HEAVY=160, HEAVY_MODE=2), dict(HEAVY=64, HEAVY_MODE=2)]
 for n in [int(a) for a in sys.argv[1:]] or [8]:
     slabs = [sdist.shard_range(R, r, n) for r in range(n)]
     f_parts = [sdist.shard_range(depth.shape[0], r, n) for r in range(n)]
     t_tab = max(timed(lambda: sfm.tsdf_block_table(depth, f0, f1, out=tab)) for f0, f1 in f_parts)
     for rep in range(2):
-        for v in [dict(HEAVY=0), dict(), dict(HEAVY=160), dict(HEAVY=128), dict(HEAVY=64), dict(HEAVY=48),
-                  dict(HEAVY=96, HEAVY_WG=512), dict(HEAVY=96, HEAVY_WG=8192)]:
+        for v in slab_variants:
             setenv(**v)
+            ts = [timed(lambda: sfm.tsdf_integrate(T, W, *args, z0, z1, block_table=tab)) for z0, z1 in slabs]
             T.zero_()
             W.zero_()
-            ts = [timed(lambda: sfm.tsdf_integrate(T, W, *args, z0, z1, block_table=tab)) for z0, z1 in slabs]
+            for z0, z1 in slabs:
+                sfm.tsdf_integrate(T, W, *args, z0, z1, block_table=tab)
             same = torch.equal(T, Tref) and torch.equal(W, Wref)
-            print(f"N={n} {str(v):32s} slab max {max(ts):.3f} ms mean {np.mean(ts):.3f} + table {t_tab:.3f}; "
-                  f"whole/(max+table) = {timed(run_whole) if False else 0:.0f} identical={same} "
-                  f"[{' '.join(f'{t:.3f}' for t in ts)}]", flush=True)
+            print(f"N={n} {str(v):36s} slab max {max(ts):.3f} ms mean {np.mean(ts):.3f} + table {t_tab:.3f} "
+                  f"identical={same} [{' '.join(f'{t:.3f}' for t in ts)}]", flush=True)
