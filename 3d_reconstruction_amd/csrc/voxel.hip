@@ -2602,7 +2602,10 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                 (void)hipEventRecord(side->fork, st);
                 (void)hipStreamWaitEvent(hs, side->fork, 0);
             }
-            hipLaunchKernelGGL(tsdf_heavy_kernel<kHvyK>, dim3((unsigned)heavy_wg), dim3(kHvyWaves * 64), 0, hs, T,
+            const int hk = env_int("SFMHIP_TSDF_HEAVY_K", kHvyK);   // frames per producer and round (A/B)
+            auto hkern = hk <= 1 ? tsdf_heavy_kernel<1> : hk == 2 ? tsdf_heavy_kernel<2>
+                         : hk >= 8 ? tsdf_heavy_kernel<8> : tsdf_heavy_kernel<kHvyK>;
+            hipLaunchKernelGGL(hkern, dim3((unsigned)heavy_wg), dim3(kHvyWaves * 64), 0, hs, T,
                                Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec, bb, trunc, cmask, fmask, nwf, free_ts,
                                vox_test ? tab : nullptr, nbu, nbv, easy, hlist, hcount);
             if (hs != st) (void)hipEventRecord(side->join, hs);
