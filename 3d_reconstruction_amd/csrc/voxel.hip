@@ -331,7 +331,7 @@ __device__ __forceinline__ void sh_colour(const float* k, float x, float y, floa
 // alpha is non-zero.  Where alpha = 0, w = T alpha = 0 and the finite colour adds +-0 to sums that
 // end in + 1: the same bits.  Rays with a non-finite direction take the full path.
 template <bool SIG>
-__global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ gvm, int D, int H, int W,
+__device__ __forceinline__ void render_body(const float* __restrict__ gvm, int D, int H, int W,
                                                      Bounds B, int mode, const float* __restrict__ ro,
                                                      const float* __restrict__ rd, const float* __restrict__ zv,
                                                      int64_t nrays, int S, float* __restrict__ rgb,
@@ -422,6 +422,17 @@ __global__ __launch_bounds__(256) void render_kernel(const float* __restrict__ g
         rgb[3 * ray + 1] = (cg + 1.f) - ws;
         rgb[3 * ray + 2] = (cb + 1.f) - ws;
     }
+}
+
+// OCC: amdgpu_waves_per_eu floor (register budget) for the occupancy A/B (SFMHIP_RENDER_OCC);
+// 0 = the compiler's choice (130 VGPRs: 3 waves per SIMD)
+template <bool SIG, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
+void render_kernel(const float* __restrict__ gvm, int D, int H, int W, Bounds B, int mode,
+                   const float* __restrict__ ro, const float* __restrict__ rd, const float* __restrict__ zv,
+                   int64_t nrays, int S, float* __restrict__ rgb, const unsigned* __restrict__ order,
+                   const float* __restrict__ sdfp) {
+    render_body<SIG>(gvm, D, H, W, B, mode, ro, rd, zv, nrays, S, rgb, order, sdfp);
 }
 
 // NerfModel.forward (plenoxel.py:31-43): the 28 channels at each point
@@ -2220,6 +2231,29 @@ __global__ __launch_bounds__(256) void render_scatter_kernel(const unsigned* __r
     order[pos] = (unsigned)i;
 }
 
+static void launch_render(const float* sdfp, dim3 grid, hipStream_t st, const float* gvm, int D, int H, int W,
+                          const Bounds& bb, int mode, const float* ro, const float* rd, const float* z, int64_t B, int S,
+                          float* rgb, const unsigned* order) {
+    const int occ = env_int("SFMHIP_RENDER_OCC", 0);
+#define SFMHIP_RENDER_LAUNCH(SIG, OCC)                                                                        \
+    hipLaunchKernelGGL((render_kernel<SIG, OCC>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd, z, B, S, \
+                       rgb, order, SIG ? sdfp : nullptr)
+    if (sdfp) {
+        if (occ == 4) SFMHIP_RENDER_LAUNCH(true, 4);
+        else if (occ == 5) SFMHIP_RENDER_LAUNCH(true, 5);
+        else if (occ == 6) SFMHIP_RENDER_LAUNCH(true, 6);
+        else if (occ == 8) SFMHIP_RENDER_LAUNCH(true, 8);
+        else SFMHIP_RENDER_LAUNCH(true, 0);
+    } else {
+        if (occ == 4) SFMHIP_RENDER_LAUNCH(false, 4);
+        else if (occ == 5) SFMHIP_RENDER_LAUNCH(false, 5);
+        else if (occ == 6) SFMHIP_RENDER_LAUNCH(false, 6);
+        else if (occ == 8) SFMHIP_RENDER_LAUNCH(false, 8);
+        else SFMHIP_RENDER_LAUNCH(false, 0);
+    }
+#undef SFMHIP_RENDER_LAUNCH
+}
+
 static int render_run(const float* grid_vm, const float* sdfp, int D, int H, int W, const float* bmin,
                       const float* bmax, int mask_mode, const float* rays_o, const float* rays_d, const float* z,
                       int64_t B, int S, float* rgb, void* stream) {
@@ -2262,23 +2296,15 @@ static int render_run(const float* grid_vm, const float* sdfp, int D, int H, int
             rc = check_launch("render_scatter_kernel");
         }
         if (rc == SFMHIP_OK) {
-            if (sdfp)
-                hipLaunchKernelGGL(render_kernel<true>, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb,
-                                   mask_mode, rays_o, rays_d, z, B, S, rgb, order, sdfp);
-            else
-                hipLaunchKernelGGL(render_kernel<false>, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb,
-                                   mask_mode, rays_o, rays_d, z, B, S, rgb, order, nullptr);
+            launch_render(sdfp, dim3(ceil_div(B, 4)), st, grid_vm, D, H, W, bb, mask_mode, rays_o, rays_d, z, B, S,
+                          rgb, order);
             rc = check_launch("render_kernel");
         }
         scratch_free(scratch, st);
         return rc;
     }
-    if (sdfp)
-        hipLaunchKernelGGL(render_kernel<true>, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb, mask_mode,
-                           rays_o, rays_d, z, B, S, rgb, nullptr, sdfp);
-    else
-        hipLaunchKernelGGL(render_kernel<false>, dim3(ceil_div(B, 4)), dim3(256), 0, st, grid_vm, D, H, W, bb,
-                           mask_mode, rays_o, rays_d, z, B, S, rgb, nullptr, nullptr);
+    launch_render(sdfp, dim3(ceil_div(B, 4)), st, grid_vm, D, H, W, bb, mask_mode, rays_o, rays_d, z, B, S, rgb,
+                  nullptr);
     return check_launch("render_kernel");
 }
 

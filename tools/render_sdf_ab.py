@@ -39,7 +39,8 @@ def run(sdf):
 
 ref = run(False)
 for rep in range(3):
-    for sdf in (False, True):
+    for sdf, occ in ((False, "0"), (True, "0"), (True, "4"), (True, "5"), (True, "6"), (True, "8"), (False, "6")):
+        os.environ["SFMHIP_RENDER_OCC"] = occ
         ts = []
         for _ in range(10):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -48,5 +49,5 @@ for rep in range(3):
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
-        print(f"sdf_plane={sdf}: {np.median(ts):.3f} ms (min {min(ts):.3f})  identical={torch.equal(out, ref)}",
+        print(f"sdf_plane={sdf} occ={occ}: {np.median(ts):.3f} ms (min {min(ts):.3f})  identical={torch.equal(out, ref)}",
               flush=True)
