@@ -2234,7 +2234,9 @@ __global__ __launch_bounds__(256) void render_scatter_kernel(const unsigned* __r
 static void launch_render(const float* sdfp, dim3 grid, hipStream_t st, const float* gvm, int D, int H, int W,
                           const Bounds& bb, int mode, const float* ro, const float* rd, const float* z, int64_t B, int S,
                           float* rgb, const unsigned* order) {
-    const int occ = env_int("SFMHIP_RENDER_OCC", 0);
+    // 4 waves per SIMD for the sdf-plane form (128 VGPRs): 0.524 vs 0.538 ms on the bench workload; 5, 6
+    // and 8 spill (0.69 / 0.84 / 3.8 ms), profiles/r4/ab_render_occ_heavy_trace_r4g.log
+    const int occ = env_int("SFMHIP_RENDER_OCC", sdfp ? 4 : 0);
 #define SFMHIP_RENDER_LAUNCH(SIG, OCC)                                                                        \
     hipLaunchKernelGGL((render_kernel<SIG, OCC>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd, z, B, S, \
                        rgb, order, SIG ? sdfp : nullptr)
