@@ -131,3 +131,43 @@ def test_exact_float_c3_full_size_sampled_rows(sfm, gpu):
         ref = om.bf_match_exact(xa, xb, (3, 4))
         assert np.array_equal(m0[p, rows].cpu().numpy(), ref), p
     assert (m0[near[:50]] >= 0).float().mean().item() > 0.03
+
+
+def _sq_dist_exact_torch(xa, xb):
+    """oracle/match.py:sq_dist_exact restated with torch on the device, op for op (f32 -> f64,
+    then per k: subtract, square, add — separate IEEE ops, k order): the test's fast checker
+    for whole C3 pairs, pinned bit for bit to the numpy oracle below."""
+    a = xa.float().double()
+    bt = xb.float().double().t().contiguous()
+    D = torch.zeros((a.shape[0], bt.shape[1]), dtype=torch.float64, device=a.device)
+    t = torch.empty_like(D)
+    for k in range(a.shape[1]):
+        torch.sub(a[:, k:k + 1], bt[k][None, :], out=t)
+        t.mul_(t)
+        D.add_(t)
+    return D
+
+
+def test_exact_float_c3_whole_pairs(sfm, gpu):
+    """C3 at full size, exact float mode: 24 WHOLE pairs (every one of the 4096 rows; near and
+    far images) against the oracle's decision rules (top2_f, ratio_accept_exact) on the
+    oracle's distance, computed by its device restatement (bit-identical to sq_dist_exact,
+    checked here on a slice)."""
+    x = syn.superpoint_like(257, 4096, 256, seed=1, device=gpu)
+    bank = sfm.DescriptorBank.from_float(x, mode=1, exact=True)
+    del x
+    pairs = sfm.all_pairs(257)
+    m0 = bank.match(pairs)
+    torch.cuda.synchronize()
+    xa, xb = bank.x[3, :48], bank.x[200, :333]
+    assert np.array_equal(_sq_dist_exact_torch(xa, xb).cpu().numpy(),
+                          om.sq_dist_exact(xa.cpu().numpy(), xb.cpu().numpy()))
+    rng = np.random.default_rng(11)
+    near = [p for p in range(len(pairs)) if pairs[p][1] - pairs[p][0] <= 2]
+    sample = list(rng.choice(near, 12, replace=False)) + list(rng.choice(len(pairs), 12, replace=False))
+    for p in sample:
+        a, b = pairs[p]
+        D = _sq_dist_exact_torch(bank.x[a], bank.x[b]).cpu().numpy()
+        j1, d1, d2 = om.top2_f(D)
+        ref = np.where(om.ratio_accept_exact(d1, d2, 3, 4), j1, -1)
+        assert np.array_equal(m0[p, :4096].cpu().numpy(), ref), p
