@@ -1518,7 +1518,7 @@ __global__ __launch_bounds__(kHvyWaves * 64) void tsdf_heavy_kernel(
     float* __restrict__ T, float* __restrict__ Wt, int D, int H, int W, int z0, int z1, const float* __restrict__ depth,
     int F, int Hd, int Wd, const float* __restrict__ rec, Bounds B, float trunc, const unsigned* __restrict__ cull,
     const unsigned* __restrict__ freem, int nw, float free_ts, const float2* __restrict__ bmm, int nbu, int nbv,
-    int easy, const unsigned* __restrict__ hlist, const unsigned* __restrict__ hcount) {
+    int easy, const unsigned* __restrict__ hlist, const unsigned* __restrict__ hcount, int hprobe) {
     constexpr int R = kHvyProd * K;   // projected frames per round
     __shared__ f2 buf[2][R][64];
     __shared__ unsigned short plist[kTsdfMaxFrames];
@@ -1580,6 +1580,12 @@ __global__ __launch_bounds__(kHvyWaves * 64) void tsdf_heavy_kernel(
                 const int f = plist[k];
                 f2 ts;
                 bool g0, g1;
+#ifdef SFMHIP_PROBES   // timing probe 1: no frame evaluation (a constant partial update)
+                if (hprobe & 1) {
+                    ts = f2{0.5f, 0.5f};
+                    g0 = g1 = (f & 1) == 0;
+                } else
+#endif
                 tsdf_frame_eval(rec, f, vx, vy, vz, two, depth, frame, nbytes, Wd4, Hd, Wd, trunc, inv_trunc,
                                 free_ts, bmm, nbu, nbv, ts, g0, g1);
                 buf[r & 1][j][l] = f2{g0 && inb ? ts.x : no_upd, g1 ? ts.y : no_upd};
@@ -1653,6 +1659,10 @@ __global__ __launch_bounds__(kHvyWaves * 64) void tsdf_heavy_kernel(
         if (wave != 0) produce(0);
         __syncthreads();   // round 0 produced
         for (int r = 0; r < nr; ++r) {   // the consumer applies round r while the producers fill round r + 1
+#ifdef SFMHIP_PROBES   // timing probe 2: the consumer skips the application
+            if (wave == 0 && (hprobe & 2)) done = min(np, (r + 1) * R);
+            else
+#endif
             if (wave == 0) consume(min(np, (r + 1) * R), r);
             else if (r + 1 < nr) produce(r + 1);
             __syncthreads();
@@ -2631,11 +2641,16 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                 (void)hipStreamWaitEvent(hs, side->fork, 0);
             }
             const int hk = env_int("SFMHIP_TSDF_HEAVY_K", kHvyK);   // frames per producer and round (A/B)
+#ifdef SFMHIP_PROBES
+            const int hprobe = env_int("SFMHIP_TSDF_HEAVY_PROBE", 0);   // tool-only builds: timing probes
+#else
+            constexpr int hprobe = 0;
+#endif
             auto hkern = hk <= 1 ? tsdf_heavy_kernel<1> : hk == 2 ? tsdf_heavy_kernel<2>
                          : hk >= 8 ? tsdf_heavy_kernel<8> : tsdf_heavy_kernel<kHvyK>;
             hipLaunchKernelGGL(hkern, dim3((unsigned)heavy_wg), dim3(kHvyWaves * 64), 0, hs, T,
                                Wt, D, H, W, z0, z1, dp, nf, Hd, Wd, rec, bb, trunc, cmask, fmask, nwf, free_ts,
-                               vox_test ? tab : nullptr, nbu, nbv, easy, hlist, hcount);
+                               vox_test ? tab : nullptr, nbu, nbv, easy, hlist, hcount, hprobe);
             if (hs != st) (void)hipEventRecord(side->join, hs);
             joined = hs == st;
             skip = hskip;
