@@ -31,6 +31,10 @@ constexpr int kJcN = 144 / kPnGL;          // convergence-check elements per lan
 constexpr int kJbN = (36 + kPnGL - 1) / kPnGL;  // 2x2 rotation blocks per lane
 static_assert(144 % kPnGL == 0 && kPnGL >= 6, "EPnP group width");
 constexpr int kPnGS = 448;                // LDS doubles per group
+#ifndef SFMHIP_PNP_FAST_ROT
+#define SFMHIP_PNP_FAST_ROT 1
+#endif
+constexpr bool kPnFastRot = SFMHIP_PNP_FAST_ROT != 0;   // EPnP Jacobi rotations without IEEE div / sqrt
 constexpr double kEps64 = 2.220446049250313e-16;
 constexpr double kDblMin64 = 2.2250738585072014e-308;
 
@@ -389,10 +393,18 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
                 int p, q;
                 pair_of(rnd, gl, p, q);
                 const double apq = A[p * 12 + q], aqq = A[q * 12 + q], app = A[p * 12 + p];
-                const double tau = (aqq - app) / (2.0 * apq);
-                const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
-                const double c = 1.0 / sqrt(1.0 + t * t);
                 const bool rot = apq != 0.0;
+                double t, c;
+                if (kPnFastRot) {   // Newton-refined v_rcp / v_rsq (a few ulps): any rotation this close keeps
+                                    // the sweep convergent, and the chain has no IEEE division / sqrt
+                    const double tau = (aqq - app) * (0.5 * rcp_nr(rot ? apq : 1.0));
+                    t = (tau >= 0 ? 1.0 : -1.0) * rcp_nr(fabs(tau) + sqrt_nr(fma(tau, tau, 1.0)));
+                    c = rsq_nr(fma(t, t, 1.0));
+                } else {
+                    const double tau = (aqq - app) / (2.0 * apq);
+                    t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+                    c = 1.0 / sqrt(1.0 + t * t);
+                }
                 G[gRot + 2 * gl] = rot ? c : 1.0;
                 G[gRot + 2 * gl + 1] = rot ? t * c : 0.0;
             }
