@@ -44,6 +44,10 @@ constexpr int kRWaves = kRThreads / 64;
 constexpr int kPThreads = 256;          // recover_pose kernel
 constexpr double kDblEps = 2.220446049250313e-16;
 constexpr double kDblMin = 2.2250738585072014e-308;
+#ifndef SFMHIP_ABERTH_FAST
+#define SFMHIP_ABERTH_FAST 1
+#endif
+constexpr bool kAberthFast = SFMHIP_ABERTH_FAST != 0;   // Aberth steps on rcp_nr (A/B: -DSFMHIP_ABERTH_FAST=0)
 
 // cv::RNG: multiply-with-carry, uniform(a, b) = a + next() % (b - a).
 struct CvRng {
@@ -383,12 +387,15 @@ __device__ int five_point_group(const double (&q)[5][4], int gl, int gsh, double
                     const double npi = __builtin_fma(pr, zi, pim * zr);
                     dr = ndr; di = ndi; pr = npr; pim = npi;
                 }
-            // N = p / p'
+            // N = p / p'.  The iteration's quotients use Newton-refined reciprocals (rcp_nr, within
+            // an ulp): the roots are fixed points of the iteration whatever the rounding of its
+            // steps, and real roots are polished below with IEEE Newton steps.
             const double dd = dr * dr + di * di;
             double nr_ = 0, ni_ = 0;
             if (dd > 0) {
-                nr_ = (pr * dr + pim * di) / dd;
-                ni_ = (pim * dr - pr * di) / dd;
+                const double idd = kAberthFast ? rcp_nr(dd) : 1.0 / dd;
+                nr_ = (pr * dr + pim * di) * idd;
+                ni_ = (pim * dr - pr * di) * idd;
             }
             double sr = 0, si = 0;  // S = sum_{j != i} 1 / (z - z_j)
 #pragma unroll
@@ -396,21 +403,32 @@ __device__ int five_point_group(const double (&q)[5][4], int gl, int gsh, double
                 if (j < n && j != gl) {
                     const double xr = zr - Z[2 * j], xi = zi - Z[2 * j + 1];
                     const double m = xr * xr + xi * xi;
-                    if (m > 0) { sr += xr / m; si -= xi / m; }
+                    if (m > 0) {
+                        if (kAberthFast) {
+                            const double im = rcp_nr(m);
+                            sr += xr * im;
+                            si -= xi * im;
+                        } else {
+                            sr += xr / m;
+                            si -= xi / m;
+                        }
+                    }
                 }
             // w = N / (1 - N S)
             const double qr = 1.0 - (nr_ * sr - ni_ * si), qi = -(nr_ * si + ni_ * sr);
             const double qq = qr * qr + qi * qi;
             double wr = nr_, wi = ni_;
             if (qq > 0) {
-                wr = (nr_ * qr + ni_ * qi) / qq;
-                wi = (ni_ * qr - nr_ * qi) / qq;
+                const double iqq = kAberthFast ? rcp_nr(qq) : 1.0 / qq;
+                wr = (nr_ * qr + ni_ * qi) * iqq;
+                wi = (ni_ * qr - nr_ * qi) * iqq;
             }
             zr -= wr;
             zi -= wi;
             // converged: step at rounding level, or |p(z)| within the rounding noise of Horner
-            conv = sqrt(wr * wr + wi * wi) <= 4 * kDblEps * sqrt(zr * zr + zi * zi) ||
-                   sqrt(pr * pr + pim * pim) <= 16 * kDblEps * pabs;
+            // (compared squared: no square roots on the chain)
+            conv = (wr * wr + wi * wi) <= (16 * kDblEps * kDblEps) * (zr * zr + zi * zi) ||
+                   (pr * pr + pim * pim) <= (256 * kDblEps * kDblEps) * (pabs * pabs);
         }
         wave_sync_lds();
         if ((((unsigned)(__ballot(!conv) >> gsh)) & 0xFFFFu) == 0u) {
