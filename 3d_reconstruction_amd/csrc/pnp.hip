@@ -31,8 +31,8 @@ constexpr int kJcN = 144 / kPnGL;          // convergence-check elements per lan
 constexpr int kJbN = (36 + kPnGL - 1) / kPnGL;  // 2x2 rotation blocks per lane
 static_assert(144 % kPnGL == 0 && kPnGL >= 6, "EPnP group width");
 constexpr int kPnGS = 448;                // LDS doubles per group
-#ifndef SFMHIP_PNP_FAST_ROT
-#define SFMHIP_PNP_FAST_ROT 1
+#ifndef SFMHIP_PNP_FAST_ROT   // 1: measured 0.705 vs 0.713 ms (noise level, profiles/r4/ab_pnp_verify_heavyprobe_r4j.log)
+#define SFMHIP_PNP_FAST_ROT 0
 #endif
 constexpr bool kPnFastRot = SFMHIP_PNP_FAST_ROT != 0;   // EPnP Jacobi rotations without IEEE div / sqrt
 constexpr double kEps64 = 2.220446049250313e-16;
