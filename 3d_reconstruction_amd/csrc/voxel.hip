@@ -424,15 +424,137 @@ __device__ __forceinline__ void render_body(const float* __restrict__ gvm, int D
     }
 }
 
+// Two-phase form of render_body<true> (SFMHIP_RENDER_2PH): per group of NCH chunks of 64 samples,
+// phase 1 issues every chunk's depth and sdf-plane gathers together and composites the alphas
+// (the transmittance scan in chunk order), phase 2 fetches the colour lines of the alpha != 0
+// samples chunk by chunk.  Each chunk's scan, weights and sums are the same operations in the same
+// order as render_body's, so the colours are the same bits; the plane gathers of all chunks are in
+// flight at once instead of one chunk's per round trip.
+template <int NCH>
+__device__ __forceinline__ void render_body_2ph(const float* __restrict__ gvm, int D, int H, int W, Bounds B, int mode,
+                                                const float* __restrict__ ro, const float* __restrict__ rd,
+                                                const float* __restrict__ zv, int64_t nrays, int S,
+                                                float* __restrict__ rgb, const unsigned* __restrict__ order,
+                                                const float* __restrict__ sdfp) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (w >= nrays) return;  // wave-uniform
+    const int64_t ray = order ? (int64_t)order[w] : w;
+    const float o[3] = {ro[3 * ray], ro[3 * ray + 1], ro[3 * ray + 2]};
+    const float d[3] = {rd[3 * ray], rd[3 * ray + 1], rd[3 * ray + 2]};
+    if (!(isfinite(d[0]) && isfinite(d[1]) && isfinite(d[2]))) {   // the full path (wave-uniform)
+        render_body<true>(gvm, D, H, W, B, mode, ro, rd, zv, nrays, S, rgb, order, sdfp);
+        return;
+    }
+    const float* z = zv + (size_t)ray * S;
+    float carry = 1.f;
+    float cr = 0.f, cg = 0.f, cb = 0.f, ws = 0.f;
+    for (int g0 = 0; g0 < S; g0 += 64 * NCH) {
+        float alpha[NCH], wgt[NCH], zsv[NCH];
+        bool lines[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {   // phase 1: depths, plane sdf, alpha
+            const int s = g0 + 64 * c + lane;
+            alpha[c] = 0.f;
+            lines[c] = false;
+            zsv[c] = 0.f;
+            if (s < S) {
+                const float zs = z[s];
+                zsv[c] = zs;
+                const float p[3] = {o[0] + d[0] * zs, o[1] + d[1] * zs, o[2] + d[2] * zs};
+                const float delta = (s + 1 < S) ? (z[s + 1] - zs) : 1e10f;
+                float g[3], sdf = 0.f;
+                if (normalise(p, B, mode, g)) {
+                    Corners cn;
+                    corners(g, D, H, W, cn);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        int x, y, zz;
+                        if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
+                        sdf = sdf + sdfp[((size_t)zz * H + y) * W + x] * cn.w[q];
+                    }
+                }
+                alpha[c] = 1.f - expf((-fmaxf(sdf, 0.f)) * delta);
+                lines[c] = alpha[c] != 0.f;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {   // transmittance in chunk order (render_body's scan)
+            wgt[c] = 0.f;
+            if (g0 + 64 * c >= S) continue;   // wave-uniform
+            float incl = 1.f - alpha[c];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const float up = __shfl_up(incl, off, 64);
+                if (lane >= off) incl = incl * up;
+            }
+            float excl = __shfl_up(incl, 1, 64);
+            if (lane == 0) excl = 1.f;
+            wgt[c] = (carry * excl) * alpha[c];
+            carry = carry * __shfl(incl, 63, 64);
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {   // phase 2: colour lines where alpha != 0, sums in chunk order
+            if (g0 + 64 * c >= S) continue;   // wave-uniform
+            float k[27];
+#pragma unroll
+            for (int q = 0; q < 27; ++q) k[q] = 0.f;
+            if (lines[c]) {
+                const float zs = zsv[c];
+                const float p[3] = {o[0] + d[0] * zs, o[1] + d[1] * zs, o[2] + d[2] * zs};
+                float g[3];
+                normalise(p, B, mode, g);   // true: alpha != 0 needs a sample inside the mask
+                Corners cn;
+                corners(g, D, H, W, cn);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    int x, y, zz;
+                    if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
+                    const float cw = cn.w[q];
+                    const float4* v = reinterpret_cast<const float4*>(gvm + ((((size_t)zz * H + y) * W + x) << 5));
+                    float vv[28];
+#pragma unroll
+                    for (int t = 0; t < 7; ++t) {
+                        const float4 f = v[t];
+                        vv[4 * t] = f.x; vv[4 * t + 1] = f.y; vv[4 * t + 2] = f.z; vv[4 * t + 3] = f.w;
+                    }
+#pragma unroll
+                    for (int q2 = 0; q2 < 27; ++q2) k[q2] = k[q2] + vv[1 + q2] * cw;
+                }
+            }
+            float col[3];
+            sh_colour(k, d[0], d[1], d[2], col);
+            const float wc = wgt[c];
+            float pr = wc * col[0], pg = wc * col[1], pb = wc * col[2], pw = wc;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                pr += __shfl_xor(pr, off, 64);
+                pg += __shfl_xor(pg, off, 64);
+                pb += __shfl_xor(pb, off, 64);
+                pw += __shfl_xor(pw, off, 64);
+            }
+            cr += pr; cg += pg; cb += pb; ws += pw;
+        }
+    }
+    if (lane == 0) {
+        rgb[3 * ray] = (cr + 1.f) - ws;
+        rgb[3 * ray + 1] = (cg + 1.f) - ws;
+        rgb[3 * ray + 2] = (cb + 1.f) - ws;
+    }
+}
+
 // OCC: amdgpu_waves_per_eu floor (register budget) for the occupancy A/B (SFMHIP_RENDER_OCC);
 // 0 = the compiler's choice (130 VGPRs: 3 waves per SIMD)
-template <bool SIG, int OCC>
+template <bool SIG, int OCC, int NCH = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void render_kernel(const float* __restrict__ gvm, int D, int H, int W, Bounds B, int mode,
                    const float* __restrict__ ro, const float* __restrict__ rd, const float* __restrict__ zv,
                    int64_t nrays, int S, float* __restrict__ rgb, const unsigned* __restrict__ order,
                    const float* __restrict__ sdfp) {
-    render_body<SIG>(gvm, D, H, W, B, mode, ro, rd, zv, nrays, S, rgb, order, sdfp);
+    if constexpr (SIG && NCH > 0)
+        render_body_2ph<NCH>(gvm, D, H, W, B, mode, ro, rd, zv, nrays, S, rgb, order, sdfp);
+    else
+        render_body<SIG>(gvm, D, H, W, B, mode, ro, rd, zv, nrays, S, rgb, order, sdfp);
 }
 
 // NerfModel.forward (plenoxel.py:31-43): the 28 channels at each point
@@ -2250,7 +2372,20 @@ static void launch_render(const float* sdfp, dim3 grid, hipStream_t st, const fl
 #define SFMHIP_RENDER_LAUNCH(SIG, OCC)                                                                        \
     hipLaunchKernelGGL((render_kernel<SIG, OCC>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd, z, B, S, \
                        rgb, order, SIG ? sdfp : nullptr)
-    if (sdfp) {
+    const int two = env_int("SFMHIP_RENDER_2PH", 0);   // A/B: two-phase sdf-plane form, chunks per group
+    if (sdfp && two > 0) {
+        if (two >= 4) {
+            if (occ == 4) hipLaunchKernelGGL((render_kernel<true, 4, 4>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode,
+                                             ro, rd, z, B, S, rgb, order, sdfp);
+            else hipLaunchKernelGGL((render_kernel<true, 0, 4>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd,
+                                    z, B, S, rgb, order, sdfp);
+        } else {
+            if (occ == 4) hipLaunchKernelGGL((render_kernel<true, 4, 3>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode,
+                                             ro, rd, z, B, S, rgb, order, sdfp);
+            else hipLaunchKernelGGL((render_kernel<true, 0, 3>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd,
+                                    z, B, S, rgb, order, sdfp);
+        }
+    } else if (sdfp) {
         if (occ == 4) SFMHIP_RENDER_LAUNCH(true, 4);
         else if (occ == 5) SFMHIP_RENDER_LAUNCH(true, 5);
         else if (occ == 6) SFMHIP_RENDER_LAUNCH(true, 6);

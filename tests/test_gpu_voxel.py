@@ -142,17 +142,19 @@ def test_render_ray_order_bitexact(sfm, gpu, monkeypatch, cfg):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("two", ["0", "3", "4"])
 @pytest.mark.parametrize("sort", ["0", "1"])
-def test_render_sdf_plane_skip_bitexact(sfm, gpu, monkeypatch, sort):
+def test_render_sdf_plane_skip_bitexact(sfm, gpu, monkeypatch, sort, two):
     """sfmhip_render_rays_sdf (sdf from the compact channel-0 plane, colour lines only for
     samples with alpha != 0) gives the same bits as sfmhip_render_rays on a finite grid whose
     sdf is negative for about half the samples, incl. rays that miss the grid, a ray with a
     non-finite direction (full path) and a ragged tail; a grid with a non-finite SH value
     renders through the full path (VoxelGrid.finite() False).  plenoxel.py:71-93, sdf.py:376."""
     monkeypatch.setenv("SFMHIP_RENDER_SORT", sort)
+    monkeypatch.setenv("SFMHIP_RENDER_2PH", two)   # the two-phase form: groups of 3 or 4 chunks
     abi = importlib.import_module("3d_reconstruction_amd._abi")
     g = torch.Generator(device=gpu).manual_seed(9)
-    N, B, S = 48, 8192 + 77, 100
+    N, B, S = 48, 8192 + 77, 100 if two == "0" else 300   # S = 300: two groups, a ragged last chunk
     grid = torch.randn((28, N, N + 3, N + 5), generator=g, device=gpu) * 0.1
     vg = sfm.VoxelGrid.plenoxel(grid, 1.5)
     ro = torch.randn((B, 3), generator=g, device=gpu) * 0.6 + torch.tensor([0.0, 0.0, -3.0], device=gpu)

@@ -39,8 +39,10 @@ def run(sdf):
 
 ref = run(False)
 for rep in range(3):
-    for sdf, occ in ((False, "0"), (True, "0"), (True, "4"), (True, "5"), (True, "6"), (True, "8"), (False, "6")):
+    for sdf, occ, two in ((False, "0", "0"), (True, "4", "0"), (True, "0", "3"), (True, "4", "3"), (True, "4", "4"),
+                          (True, "0", "4")):
         os.environ["SFMHIP_RENDER_OCC"] = occ
+        os.environ["SFMHIP_RENDER_2PH"] = two
         ts = []
         for _ in range(10):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -49,5 +51,5 @@ for rep in range(3):
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
-        print(f"sdf_plane={sdf} occ={occ}: {np.median(ts):.3f} ms (min {min(ts):.3f})  identical={torch.equal(out, ref)}",
+        print(f"sdf_plane={sdf} occ={occ} 2ph={two}: {np.median(ts):.3f} ms (min {min(ts):.3f})  identical={torch.equal(out, ref)}",
               flush=True)
