@@ -43,8 +43,11 @@ __device__ unsigned long long g_ba_prof[4096 * kProfPhases];
     } while (0)
 #endif
 
-constexpr int kRec = 26;   // per observation: J (18: u row, v row), f (2), scale_inv of the point (3), X_new (3)
-constexpr int kRecRC = 6;  // RC records: scale_inv of the point (3) at fields 20-22 of the pass view, X_new (3)
+// per observation: J (18: u row, v row), f (2), the point's column scales d = 1 / scale_inv (3), X_new (3),
+// scale_inv (3: the column norms, max'ed across Jacobian evaluations); d is stored so that no pass
+// divides (the same IEEE quotient once per Jacobian instead of once per pass)
+constexpr int kRec = 29;
+constexpr int kRecRC = 9;  // RC records: fields 20-28 only (d, X_new, scale_inv)
 
 // sum of K doubles over the workgroup (NW waves); every thread receives the totals in out[]
 template <int NW, int K>
@@ -220,7 +223,7 @@ __device__ __forceinline__ void resid(const double* R, const double* c, const do
     rv = pts[1] - v;
 }
 
-// RC (recompute): the records hold only the point column scales (3) and the trial point (3);
+// RC (recompute): the records hold only the point column scales (d and scale_inv, 3 each) and the trial point (3);
 // every pass re-derives the observation's J (18) and f (2) from X, pts and the pair's camera
 // (fd_obs: the same function, the same values as the Jacobian pass) instead of re-reading a
 // 23-double record written by it — ~450 f64 flops per observation and pass against 184 B of
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     double* Xp = X + 3 * o0;
     const double* pts = pts2d + 2 * o0;
     const Recs<SOA, RC> rec{scratch + (size_t)o0 * (RC ? kRecRC : kRec), n};
-    // the pass view of observation i: r[0..17] J, r[18..19] f, r[20..22] point scale_inv
+    // the pass view of observation i: r[0..17] J, r[18..19] f, r[20..22] the point column scales d
     auto pass_rec = [&](int i, double* r) {
         if constexpr (RC) {
             const double Xi[3] = {Xp[3 * i], Xp[3 * i + 1], Xp[3 * i + 2]};
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             } else {
                 for (int c = 0; c < 3; ++c) Xi[c] = Xp[3 * i + c];
             }
-            if (!first) rec.template load<20, 23>(i, r);
+            if (!first) rec.template load<26, 29>(i, r);
             fd_obs(&S.R[0][0], S.cam, k, Xi, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
             r[18] = f[0];
             r[19] = f[1];
@@ -307,11 +310,13 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 gmax = fmax(gmax, fabs(gp));
                 double si = sqrt(r[6 + c] * r[6 + c] + r[15 + c] * r[15 + c]);
                 if (first) si = si == 0.0 ? 1.0 : si;
-                else si = fmax(si, r[20 + c]);
-                r[20 + c] = si;
+                else si = fmax(si, r[26 + c]);
+                r[26 + c] = si;
+                r[20 + c] = 1.0 / si;
             }
             if (RC) rec.template store<20, 23>(i, r);
             else rec.template store<0, 23>(i, r);
+            rec.template store<26, 29>(i, r);
         }
         gmax = block_max<NW>(gmax, S.red);
         block_sum<NW, 13>(acc, S.red, S.tot);
@@ -336,8 +341,8 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         double acc[1] = {0.0};
         for (int i = tid; i < n; i += NT) {
             double r[kRec];
-            rec.template load<20, 23>(i, r);
-            for (int c = 0; c < 3; ++c) { const double t = Xp[3 * i + c] * r[20 + c]; acc[0] += t * t; }
+            rec.template load<26, 29>(i, r);
+            for (int c = 0; c < 3; ++c) { const double t = Xp[3 * i + c] * r[26 + c]; acc[0] += t * t; }
         }
         block_sum<NW, 1>(acc, S.red, S.tot);
         if (tid == 0) {
@@ -368,7 +373,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 double vu = 0.0, vv = 0.0;
                 for (int c = 0; c < 6; ++c) { vu -= r[c] * S.dc[c] * S.ghc[c]; vv -= r[9 + c] * S.dc[c] * S.ghc[c]; }
                 for (int c = 0; c < 3; ++c) {
-                    const double d = 1.0 / r[20 + c];
+                    const double d = r[20 + c];
                     const double gh = d * (r[6 + c] * r[18] + r[15 + c] * r[19]);
                     vu -= r[6 + c] * d * gh;
                     vv -= r[15 + c] * d * gh;
@@ -405,7 +410,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 double C[2][6], Pp[2][3];
                 for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
                 for (int c = 0; c < 3; ++c) {
-                    const double d = 1.0 / r[20 + c];
+                    const double d = r[20 + c];
                     Pp[0][c] = r[6 + c] * d;
                     Pp[1][c] = r[15 + c] * d;
                 }
@@ -444,7 +449,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 double C[2][6], Pp[2][3];
                 for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
                 for (int c = 0; c < 3; ++c) {
-                    const double d = 1.0 / r[20 + c];
+                    const double d = r[20 + c];
                     Pp[0][c] = r[6 + c] * d;
                     Pp[1][c] = r[15 + c] * d;
                 }
@@ -485,7 +490,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             double C[2][6], Pp[2][3];
             for (int c = 0; c < 6; ++c) { C[0][c] = r[c] * S.dc[c]; C[1][c] = r[9 + c] * S.dc[c]; }
             for (int c = 0; c < 3; ++c) {
-                const double d = 1.0 / r[20 + c];
+                const double d = r[20 + c];
                 Pp[0][c] = r[6 + c] * d;
                 Pp[1][c] = r[15 + c] * d;
             }
@@ -522,7 +527,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                     b1 += r[9 + c] * S.dc[c] * S.s2c[c];
                 }
                 for (int c = 0; c < 3; ++c) {
-                    const double d = 1.0 / r[20 + c];
+                    const double d = r[20 + c];
                     a0 += r[6 + c] * d * s1[c];
                     a1 += r[15 + c] * d * s1[c];
                     b0 += r[6 + c] * d * s2[c];
@@ -591,7 +596,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 for (int c = 0; c < 6; ++c) { ju += r[c] * S.dc[c] * S.shc[c]; jv += r[9 + c] * S.dc[c] * S.shc[c]; }
                 double Xn[3];
                 for (int c = 0; c < 3; ++c) {
-                    const double d = 1.0 / r[20 + c];
+                    const double d = r[20 + c];
                     const double sh = S.pS[0] * s1[c] + S.pS[1] * (s2[c] / s2n);
                     ju += r[6 + c] * d * sh;
                     jv += r[15 + c] * d * sh;
