@@ -1014,14 +1014,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                                                          unsigned short* __restrict__ cull,
                                                          unsigned short* __restrict__ freem,
                                                          unsigned* __restrict__ plist, unsigned* __restrict__ pcount,
-                                                         unsigned* __restrict__ tcost) {
+                                                         unsigned* __restrict__ tcost, int h_off, int nhs) {
     __shared__ unsigned char bits[kCullFrames][64];
     const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
     const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
     const int nsy = nty * per_tile;                        // sub-tile rows in y
     const int nqx = (ntx + 3) >> 2, nqy = (nsy + 3) >> 2;  // 4x4x4 bricks of boxes
-    const int nh = 2 * nw;                                 // 16-frame halves per launch
-    const int hf = blockIdx.x % nh, brick = blockIdx.x / nh;
+    // 16-frame halves [h_off, h_off + nhs) of the launch's 2 nw (the pre-pass pipeline runs the
+    // pass per group of frames; mask halves are addressed by the absolute half index)
+    const int hf = h_off + (int)(blockIdx.x % nhs), brick = (int)(blockIdx.x / nhs);
+    const int nh = nhs;
     const int l = threadIdx.x & 63, j = threadIdx.x >> 6;
     const int f = hf * kCullFrames + j;
     const int tx = (brick % nqx) * 4 + (l & 3);
@@ -2476,9 +2478,11 @@ extern "C" int sfmhip_render_rays_sdf(const float* grid_vm, const float* sdf_pla
 // Library-owned side stream per device (created once): tsdf_heavy_kernel runs on it beside
 // tsdf_kernel on the caller's stream, forked and joined with events, so the call stays ordered on
 // the caller's stream.  The mutex keeps one fork/join sequence at a time per device.
+constexpr int kPrePipeMax = 8;   // frame groups of the pre-pass pipeline
 struct SideStream {
     hipStream_t s = nullptr, hi = nullptr;   // hi: the device's greatest stream priority
     hipEvent_t fork = nullptr, join = nullptr;
+    hipEvent_t grp[kPrePipeMax] = {};        // pre-pass pipeline: block tables of frame groups ready
     std::mutex mu;
 };
 static SideStream g_side[64];
@@ -2491,10 +2495,12 @@ static SideStream* side_stream(int dev) {
         if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
             hipStreamCreateWithPriority(&ss.hi, hipStreamNonBlocking, hi) != hipSuccess)
             ss.hi = nullptr;
-        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
-            ss.s = nullptr;
+        bool ok = hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) == hipSuccess;
+        for (int k = 0; ok && k < kPrePipeMax; ++k)
+            ok = hipEventCreateWithFlags(&ss.grp[k], hipEventDisableTiming) == hipSuccess;
+        if (!ok) ss.s = nullptr;
         (void)hipGetLastError();
     });
     return g_side[dev].s ? &g_side[dev] : nullptr;
@@ -2599,7 +2605,9 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     unsigned char* bdec = nullptr;
     const int ncbu = ceil_div(nbu, kCoarse), ncbv = ceil_div(nbv, kCoarse);
     int4* crange = nullptr;
-    const int64_t ntile_frames = (int64_t)nbx * nby * nbz * std::min(chunk, F);
+    // refinement list capacity: one entry per (tile, frame) of whole 32-frame words (the pre-pass
+    // pipeline gives each frame group its own region), then the counters
+    const int64_t plist_cap = (int64_t)nbx * nby * nbz * 32 * ceil_div(std::min(chunk, F), 32);
     if (want_cull) {
         if (ext_table) cbmm = const_cast<float2*>(ext_table);
         else if (scratch_alloc((void**)&cbmm, nblk * sizeof(float2), st) != hipSuccess) cbmm = nullptr;
@@ -2622,8 +2630,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             else
                 ctab = nullptr;   // no brick pre-pass
         }
-        if (cmask && want_refine && ntile_frames < (int64_t)1 << 30 && nbx * nby * nbz < (1 << 23) &&
-            scratch_alloc((void**)&plist, (size_t)(ntile_frames + 1) * sizeof(unsigned), st) != hipSuccess)
+        if (cmask && want_refine && plist_cap < (int64_t)1 << 30 && nbx * nby * nbz < (1 << 23) &&
+            scratch_alloc((void**)&plist, (size_t)(plist_cap + kPrePipeMax) * sizeof(unsigned), st) != hipSuccess)
             plist = nullptr;   // no second pass
         (void)hipGetLastError();
     }
@@ -2666,6 +2674,18 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     // 8192 x 256 threads fill the 6 waves per SIMD its 79 VGPRs allow, where 2048 gave 2 (C5 call
     // 1.93 -> 1.90 ms, profiles/r3/ab/tsdf_refine_wg_r3bp.txt)
     const int refine_wg = std::max(1, env_int("SFMHIP_TSDF_REFINE_WG", 8192));
+    // Pre-pass pipeline (SFMHIP_TSDF_PREPIPE = frame groups, 0/1 off): the block pass of frame group
+    // k + 1 (HBM-bound) runs on the library's side stream while the cull and refinement passes of
+    // group k (latency-bound f64 tests) run on the caller's stream; every mask word is written by
+    // the group that owns its frames, the refinement list has a region per group, and the fusion
+    // waits for all of them.  Whole-grid mode with the call's own table; the brick pre-pass is
+    // off in it (its coarse table needs every frame's blocks first).
+    int pre_groups = 1;
+    SideStream* pside = nullptr;
+    if (cmask && !ext_table && !stats && !latency_mode) {
+        pre_groups = std::min(kPrePipeMax, std::max(1, env_int("SFMHIP_TSDF_PREPIPE", 1)));
+        if (pre_groups > 1 && !(pside = side_stream(dev_id))) pre_groups = 1;
+    }
     // frame chunks run in order on the stream, so per-voxel update order is kept
     int rc = SFMHIP_OK;
     for (int f0 = 0; f0 < F; f0 += chunk) {
@@ -2675,13 +2695,49 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         const float* pp = poses + (size_t)f0 * 12;
         const float* kp = Kf + (size_t)f0 * 4;
         CullCam* ccam = cmask ? reinterpret_cast<CullCam*>(rec + (size_t)cf * 16) : nullptr;
-        unsigned* pcount = plist ? plist + ntile_frames : nullptr;
+        unsigned* pcount = plist ? plist + plist_cap : nullptr;
         const int nzero = tcost ? (int)ntiles : 0;
         hipLaunchKernelGGL(tsdf_setup_kernel, dim3(ceil_div(nf, 64) + (nzero || pcount ? std::min(64, ceil_div(nzero, 1024) + 1) : 0)),
                            dim3(64), 0, st, pp, kp, nf, rec, ccam, !cmask ? 0 : ext_table ? 1 : 2, H, W, z0, z1, Hd,
                            Wd, cg, nbu, nbv, crange, tcost, nzero, pcount);
         const float2* tab = ext_table ? ext_table + (size_t)f0 * nbv * nbu : cbmm;
-        if (cmask && !ext_table) {
+        const int nh_all = 2 * nwf;
+        const int groups = std::min(pre_groups, nh_all);
+        if (groups > 1) {   // the pre-pass pipeline (above)
+            std::lock_guard<std::mutex> lk(pside->mu);
+            if (plist) (void)hipMemsetAsync(plist + plist_cap, 0, kPrePipeMax * sizeof(unsigned), st);
+            (void)hipEventRecord(pside->fork, st);
+            (void)hipStreamWaitEvent(pside->s, pside->fork, 0);
+            for (int k = 0; k < groups; ++k) {
+                const int h0 = nh_all * k / groups, h1 = nh_all * (k + 1) / groups;
+                const int fa = h0 * kCullFrames, fb = std::min(nf, h1 * kCullFrames);
+                if (fb > fa) {
+                    if (Wd % 4 == 0)
+                        hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, fb - fa), dim3(256),
+                                           0, pside->s, dp + (size_t)fa * Hd * Wd, fb - fa, Hd, Wd, nbu, nbv,
+                                           crange + fa, cbmm + (size_t)fa * nbv * nbu);
+                    else
+                        hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, fb - fa), dim3(256),
+                                           0, pside->s, dp + (size_t)fa * Hd * Wd, fb - fa, Hd, Wd, nbu, nbv,
+                                           crange + fa, cbmm + (size_t)fa * nbv * nbu);
+                }
+                (void)hipEventRecord(pside->grp[k], pside->s);
+            }
+            for (int k = 0; k < groups; ++k) {
+                const int h0 = nh_all * k / groups, h1 = nh_all * (k + 1) / groups;
+                (void)hipStreamWaitEvent(st, pside->grp[k], 0);
+                unsigned* pl = plist ? plist + (int64_t)nbx * nby * nbz * kCullFrames * h0 : nullptr;
+                unsigned* pc = plist ? plist + plist_cap + k : nullptr;
+                hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * (h1 - h0))), dim3(1024), 0, st, H,
+                                   W, z0, z1, nf, Hd, Wd, ccam, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
+                                   nwf, nullptr, (unsigned short*)cmask, (unsigned short*)cfree, pl, pc, tcost, h0,
+                                   h1 - h0);
+                if (plist)
+                    hipLaunchKernelGGL(tsdf_refine_kernel, dim3(refine_wg), dim3(256), 0, st, H, W, z0, z1, nf, Hd, Wd,
+                                       pp, kp, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, nwf, cmask, cfree, pl,
+                                       pc);
+            }
+        } else if (cmask && !ext_table) {
             if (Wd % 4 == 0)
                 hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st,
                                    dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
@@ -2689,7 +2745,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                 hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st,
                                    dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
         }
-        if (cmask) {
+        if (cmask && groups <= 1) {
             if (bdec) {
                 const int64_t nc = (int64_t)nf * ncbu * ncbv, nd = (cull_bricks + 63) / 64 * 64 * nf;
                 hipLaunchKernelGGL(coarse_table_kernel, dim3((unsigned)ceil_div(nc, (int64_t)256)), dim3(256), 0, st,
@@ -2700,7 +2756,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             }
             hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nwf * 2)), dim3(1024), 0, st, H,
                                W, z0, z1, nf, Hd, Wd, ccam, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
-                               nwf, bdec, (unsigned short*)cmask, (unsigned short*)cfree, plist, pcount, tcost);
+                               nwf, bdec, (unsigned short*)cmask, (unsigned short*)cfree, plist, pcount, tcost, 0,
+                               2 * nwf);
             if (plist)
                 hipLaunchKernelGGL(tsdf_refine_kernel, dim3(refine_wg), dim3(256), 0, st, H, W, z0, z1, nf, Hd, Wd, pp,
                                    kp, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, nwf, cmask, cfree, plist,

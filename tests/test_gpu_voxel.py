@@ -217,7 +217,7 @@ def _tsdf_case(R=48, F=12, Hd=96, Wd=128, focal=110.0):
 # pass, per-voxel block test); "heavy*": every sub-tile with a projected frame goes through
 # tsdf_heavy_kernel (frame-split producers + ordered consumer), in either mode, and with a
 # 3-workgroup grid so each workgroup takes several sub-tiles
-LAT_MODES = ["auto", "0", "heavy", "heavy0"]
+LAT_MODES = ["auto", "0", "heavy", "heavy0", "pre0"]
 
 
 def _set_lat(monkeypatch, lat):
@@ -225,6 +225,8 @@ def _set_lat(monkeypatch, lat):
         pass
     else:
         monkeypatch.setenv("SFMHIP_TSDF_LATENCY", "0")
+    if lat == "pre0":   # the pre-pass pipeline: block tables of frame groups on the side stream
+        monkeypatch.setenv("SFMHIP_TSDF_PREPIPE", "3")
     if lat.startswith("heavy"):
         monkeypatch.setenv("SFMHIP_TSDF_HEAVY", "1")
         monkeypatch.setenv("SFMHIP_TSDF_HEAVY_WG", "3")
@@ -299,10 +301,12 @@ def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
                 dict(CULL="2", LATENCY="0", REFINE="0"), dict(CULL="2", LATENCY="0", VOXTEST="0"),
                 dict(CULL="2", HEAVY="1"), dict(CULL="2", HEAVY="1", LATENCY="0"),
                 dict(CULL="2", HEAVY="2", HEAVY_WG="5", CHUNK="17"), dict(CULL="2", HEAVY="1", EASY="0"),
-                dict(CULL="2", HEAVY="0", LATENCY="1")]
+                dict(CULL="2", HEAVY="0", LATENCY="1"),
+                dict(CULL="2", LATENCY="0", PREPIPE="4"), dict(CULL="2", LATENCY="0", PREPIPE="3", CHUNK="17"),
+                dict(CULL="2", LATENCY="0", PREPIPE="8", FREE="0"), dict(CULL="2", LATENCY="0", PREPIPE="2", REFINE="0")]
     for v in variants:
         for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST", "REFINE", "LATENCY", "ORDER", "BRICK", "PIPE", "EASY",
-                  "HEAVY", "HEAVY_WG"):
+                  "HEAVY", "HEAVY_WG", "PREPIPE"):
             monkeypatch.delenv("SFMHIP_TSDF_" + k, raising=False)
         for k, x in v.items():
             monkeypatch.setenv("SFMHIP_TSDF_" + k, x)
@@ -407,10 +411,12 @@ def test_tsdf_c5_full_size_slabs_bitexact(sfm, gpu, monkeypatch):
     # the latency mode of thin slabs (no block-table test, no refinement pass; heavy sub-tiles
     # frame-split) on the full grid, and the whole-grid mode with the heavy path
     monkeypatch.setenv("SFMHIP_TSDF_CULL", "1")
-    for lat, heavy in (("1", None), ("0", "48")):
+    for lat, heavy, pre in (("1", None, None), ("0", "48", None), ("0", "0", "4")):
         monkeypatch.setenv("SFMHIP_TSDF_LATENCY", lat)
         if heavy:
             monkeypatch.setenv("SFMHIP_TSDF_HEAVY", heavy)
+        if pre:
+            monkeypatch.setenv("SFMHIP_TSDF_PREPIPE", pre)
         T2.zero_()
         W2.zero_()
         sfm.tsdf_integrate(T2, W2, *args)

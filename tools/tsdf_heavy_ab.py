@@ -36,7 +36,7 @@ def timed(fn, reps=5):
 
 
 def setenv(**kw):
-    for k in ("HEAVY", "HEAVY_WG", "LATENCY", "HEAVY_MODE"):
+    for k in ("HEAVY", "HEAVY_WG", "LATENCY", "HEAVY_MODE", "PREPIPE"):
         os.environ.pop("SFMHIP_TSDF_" + k, None)
     for k, v in kw.items():
         os.environ["SFMHIP_TSDF_" + k] = str(v)
@@ -51,7 +51,7 @@ def run_whole():
 setenv()
 run_whole()
 Tref, Wref = T.clone(), W.clone()
-whole_variants = [dict(), dict(HEAVY=128, HEAVY_MODE=1), dict(HEAVY=128, HEAVY_MODE=2), dict(HEAVY=128, HEAVY_MODE=0)]
+whole_variants = [dict(), dict(PREPIPE=2), dict(PREPIPE=3), dict(PREPIPE=4), dict(PREPIPE=6), dict(PREPIPE=8)]
 for rep in range(2):
     for v in whole_variants:
         setenv(**v)
@@ -60,7 +60,7 @@ for rep in range(2):
         print(f"whole grid {v or 'default'}: {t:.3f} ms  identical={same}", flush=True)
 slab_variants = [dict(HEAVY=0), dict(HEAVY=96, HEAVY_MODE=0), dict(HEAVY=96, HEAVY_MODE=1), dict(HEAVY=96, HEAVY_MODE=2),
                  dict(HEAVY=160, HEAVY_MODE=1), dict(HEAVY=160, HEAVY_MODE=2), dict(HEAVY=64, HEAVY_MODE=2)]
-for n in [int(a) for a in sys.argv[1:]] or [8]:
+for n in [int(a) for a in sys.argv[1:]]:
     slabs = [sdist.shard_range(R, r, n) for r in range(n)]
     f_parts = [sdist.shard_range(depth.shape[0], r, n) for r in range(n)]
     t_tab = max(timed(lambda: sfm.tsdf_block_table(depth, f0, f1, out=tab)) for f0, f1 in f_parts)
