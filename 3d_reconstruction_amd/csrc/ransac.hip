@@ -28,6 +28,9 @@
 //      replaces the best iff count > max(best, 4), niters shrinks by
 //      RANSACUpdateNumIters — so the chosen model and the iteration count are
 //      exactly those of the sequential loop over the same models.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "geom_dev.h"
 
@@ -574,6 +577,71 @@ __device__ __forceinline__ int wave_sum(int v) {
 }
 
 
+// Scores every listed model of a chunk on all n points: each wave's ballot counts go to
+// s_cnt[model][wave] (no atomics).  Branch-free margin tests for two models x kPB points at a
+// time, so the chains interleave; the exact division only where a test is ambiguous.
+__device__ __forceinline__ void score_chunk(const double* __restrict__ q, int n, const int* s_list, int nlist,
+                                            const double* s_models, int (*s_cnt)[kRWaves], float tf, double tlo,
+                                            double thi, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int b0 = 0; b0 < n; b0 += kRThreads * kPB) {
+        double pt[kPB][4];
+        bool val[kPB];
+#pragma unroll
+        for (int u = 0; u < kPB; ++u) {
+            const int i = b0 + u * kRThreads + tid;
+            val[u] = i < n;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) pt[u][c] = val[u] ? q[4 * i + c] : 0.0;
+        }
+        for (int j = 0; j < nlist; j += 2) {   // two models per step: independent chains
+            const int ma = s_list[j], mb = s_list[min(j + 1, nlist - 1)];
+            double Ea[9], Eb[9];
+#pragma unroll
+            for (int e = 0; e < 9; ++e) {
+                Ea[e] = s_models[ma * 9 + e];
+                Eb[e] = s_models[mb * 9 + e];
+            }
+            // branch-free margin tests for all 2 x kPB (model, point) pairs, so the
+            // chains interleave; the exact division only where a test is ambiguous
+            double nm[2][kPB], dn[2][kPB];
+            bool in[2][kPB], amb = false;
+#pragma unroll
+            for (int u = 0; u < kPB; ++u) {
+                sampson_nd(Ea, pt[u][0], pt[u][1], pt[u][2], pt[u][3], nm[0][u], dn[0][u]);
+                sampson_nd(Eb, pt[u][0], pt[u][1], pt[u][2], pt[u][3], nm[1][u], dn[1][u]);
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int u = 0; u < kPB; ++u) {
+                    in[k][u] = nm[k][u] <= dn[k][u] * tlo;
+                    amb = amb || !(in[k][u] || nm[k][u] > dn[k][u] * thi) || !(dn[k][u] > 0);
+                }
+            if (amb) {   // rare: near the threshold (2^-40 relative) or a degenerate denominator
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+#pragma unroll
+                    for (int u = 0; u < kPB; ++u) {
+                        const double n_ = nm[k][u], d_ = dn[k][u];
+                        const bool sure = d_ > 0 && (n_ <= d_ * tlo || n_ > d_ * thi);
+                        if (!sure) in[k][u] = (float)(n_ / d_) <= tf;
+                    }
+            }
+            int ca = 0, cb = 0;  // wave-uniform: ballots + scalar popcounts
+#pragma unroll
+            for (int u = 0; u < kPB; ++u) {
+                ca += wave_count(val[u] && in[0][u]);
+                cb += wave_count(val[u] && in[1][u]);
+            }
+            if (lane == 0) {
+                s_cnt[ma][wave] += ca;
+                if (j + 1 < nlist) s_cnt[mb][wave] += cb;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
     const double* __restrict__ pts0, const double* __restrict__ pts1, const int64_t* __restrict__ offs,
     const double* __restrict__ cam, double prob, double threshold, int max_iters, double* __restrict__ qn,
@@ -684,63 +752,7 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
         }
         __syncthreads();
         RPROF(1, tp);
-        const int nlist = s_nlist, wave = tid >> 6;
-        for (int b0 = 0; b0 < n; b0 += kRThreads * kPB) {
-            double pt[kPB][4];
-            bool val[kPB];
-#pragma unroll
-            for (int u = 0; u < kPB; ++u) {
-                const int i = b0 + u * kRThreads + tid;
-                val[u] = i < n;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) pt[u][c] = val[u] ? q[4 * i + c] : 0.0;
-            }
-            for (int j = 0; j < nlist; j += 2) {   // two models per step: independent chains
-                const int ma = s_list[j], mb = s_list[min(j + 1, nlist - 1)];
-                double Ea[9], Eb[9];
-#pragma unroll
-                for (int e = 0; e < 9; ++e) {
-                    Ea[e] = s_models[ma * 9 + e];
-                    Eb[e] = s_models[mb * 9 + e];
-                }
-                // branch-free margin tests for all 2 x kPB (model, point) pairs, so the
-                // chains interleave; the exact division only where a test is ambiguous
-                double nm[2][kPB], dn[2][kPB];
-                bool in[2][kPB], amb = false;
-#pragma unroll
-                for (int u = 0; u < kPB; ++u) {
-                    sampson_nd(Ea, pt[u][0], pt[u][1], pt[u][2], pt[u][3], nm[0][u], dn[0][u]);
-                    sampson_nd(Eb, pt[u][0], pt[u][1], pt[u][2], pt[u][3], nm[1][u], dn[1][u]);
-                }
-#pragma unroll
-                for (int k = 0; k < 2; ++k)
-#pragma unroll
-                    for (int u = 0; u < kPB; ++u) {
-                        in[k][u] = nm[k][u] <= dn[k][u] * tlo;
-                        amb = amb || !(in[k][u] || nm[k][u] > dn[k][u] * thi) || !(dn[k][u] > 0);
-                    }
-                if (amb) {   // rare: near the threshold (2^-40 relative) or a degenerate denominator
-#pragma unroll
-                    for (int k = 0; k < 2; ++k)
-#pragma unroll
-                        for (int u = 0; u < kPB; ++u) {
-                            const double n_ = nm[k][u], d_ = dn[k][u];
-                            const bool sure = d_ > 0 && (n_ <= d_ * tlo || n_ > d_ * thi);
-                            if (!sure) in[k][u] = (float)(n_ / d_) <= tf;
-                        }
-                }
-                int ca = 0, cb = 0;  // wave-uniform: ballots + scalar popcounts
-#pragma unroll
-                for (int u = 0; u < kPB; ++u) {
-                    ca += wave_count(val[u] && in[0][u]);
-                    cb += wave_count(val[u] && in[1][u]);
-                }
-                if (lane == 0) {
-                    s_cnt[ma][wave] += ca;
-                    if (j + 1 < nlist) s_cnt[mb][wave] += cb;
-                }
-            }
-        }
+        score_chunk(q, n, s_list, s_nlist, s_models, s_cnt, tf, tlo, thi, tid);
         __syncthreads();
         RPROF(2, tp);
         if (tid == 0) {
@@ -778,6 +790,403 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
     if (maxgood > 0)
         for (int i = tid; i < n; i += kRThreads)
             mask[off + i] = sampson(s_best, q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]) <= tf ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Load-balanced form (default).  essential_ransac_kernel runs a pair's chunks one after another on
+// one CU, so a call lasts as long as its pair with the most chunks: on the bench scene (256 pairs
+// x 2048 matches) 2-8 chunks of 32 hypotheses, mean 2.9, and the call ~2.6x the mean pair.  Here a
+// chunk is a work item that any CU may take, and the sequential parts are separate passes:
+//   ess_init_kernel    normalised points, per-pair state (EssState), outputs of n < 5 pairs;
+//   ess_gen            one lane per pair draws the pair's samples from cv::RNG(-1) in draw order up
+//                      to a target hypothesis count (below) and appends the chunks that cover them to a work list;
+//   ess_chunk_kernel   persistent 512-thread workgroups take (pair, chunk) items from the list:
+//                      the chunk's 32 samples solved by 16-lane groups and its models scored on
+//                      every point (essential_ransac_kernel's own solver and scoring), then its
+//                      records: the models whose count exceeds max(4, every earlier count of the
+//                      chunk), in replay order;
+//   ess_replay_kernel  one lane per pair replays the records in OpenCV's order (a model replaces
+//                      the best iff count > max(best, 4); RANSACUpdateNumIters shrinks niters),
+//                      then runs ess_gen for the next round (round 0: ess_gen_kernel).
+// Only a record can ever replace the best (a model at or below an earlier count of its chunk was
+// either beaten by that model's acceptance or is <= max(best, 4) already), and niters never grows,
+// so the last round — every chunk below the niters the previous replay left, an upper bound of the
+// final one — completes every pair; rounds 0 and 1 list chunks up to 2 and 4 per pair (bounded
+// speculation: a chunk a later replay finds unneeded is wasted work, never a different result).
+// The same best model, inlier count and iteration count as the sequential loop over the same
+// models.  ess_final_kernel writes E (kept with the record, or re-solved from its sample) and the
+// mask.
+constexpr int kSpecChunks = 2;     // round r lists chunks up to kSpecChunks << r (last round: all)
+constexpr int kEssRounds = 3;
+constexpr int kRecMax = kRH * kMaxModels;
+constexpr int kRecE = 16;          // records per chunk whose E is kept (later ones: re-solved)
+constexpr int kEssFive = 1, kEssDone = 2;
+
+struct EssState {
+    uint64_t rng;
+    int n, flags, niters, maxgood;
+    int gen_upto, eval_upto, rc, cur_k;   // samples drawn, hypotheses listed, replay cursor (chunk, hyp)
+    int kp, best_c, best_i, best_k, best_m, last;
+};
+
+struct EssBufs {
+    EssState* st;
+    int* samp;       // [P][hcap][5]
+    int2* rec;       // [P][cmax][kRecMax]: {count, h * 16 + m}
+    int* nrec;       // [P][cmax]
+    double* recE;    // [P][cmax][kRecE][9]
+    int2* list;      // [kEssRounds][P * cmax]: {pair, chunk (-1: the n == 5 call)}
+    int* ctr;        // [2 kEssRounds]: (count, head) per round
+    int cmax, hcap, rece;
+};
+
+__global__ __launch_bounds__(256) void ess_init_kernel(const double* __restrict__ pts0, const double* __restrict__ pts1,
+                                                       const int64_t* __restrict__ offs, const double* __restrict__ cam,
+                                                       int max_iters, double* __restrict__ qn, uint8_t* __restrict__ mask,
+                                                       int32_t* __restrict__ nmodels_out,
+                                                       int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out,
+                                                       EssBufs B) {
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int64_t off = offs[p];
+    const int n = (int)(offs[p + 1] - off);
+    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
+    double* q = qn + off * 4;
+    for (int i = tid; i < n; i += 256) {
+        q[4 * i + 0] = (pts0[2 * (off + i)] - cx) / fx;
+        q[4 * i + 1] = (pts0[2 * (off + i) + 1] - cy) / fy;
+        q[4 * i + 2] = (pts1[2 * (off + i)] - cx) / fx;
+        q[4 * i + 3] = (pts1[2 * (off + i) + 1] - cy) / fy;
+        mask[off + i] = 0;
+    }
+    if (tid == 0) {
+        EssState s;
+        s.rng = ~0ULL;
+        s.n = n;
+        s.flags = n < 5 ? kEssDone : n == 5 ? kEssFive : 0;
+        s.niters = max(max_iters, 1);
+        s.maxgood = 0;
+        s.gen_upto = s.eval_upto = s.rc = 0;
+        s.cur_k = s.kp = -1;
+        s.best_c = s.best_i = s.best_k = s.best_m = -1;
+        s.last = -1;
+        B.st[p] = s;
+        if (n < 5) { nmodels_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
+        if (p == 0)
+            for (int i = 0; i < 2 * kEssRounds; ++i) B.ctr[i] = 0;
+    }
+}
+
+// One lane per pair: draws samples [gen_upto, target) exactly as essential_ransac_kernel's lane 0
+// does (5 distinct indices per sample, redrawing duplicates), then lists the chunks covering them.
+__device__ void ess_gen(EssState& s, int p, int P, int round, const EssBufs& B) {
+    int2* list = B.list + (size_t)round * P * B.cmax;
+    int* cnt = B.ctr + 2 * round;
+    const int target = round + 1 < kEssRounds ? min(s.niters, (kSpecChunks << round) * kRH) : s.niters;
+    const unsigned n = (unsigned)s.n;
+    const double inv_n = 1.0 / (double)n;
+    CvRng rng{s.rng};
+    int* smp = B.samp + (size_t)p * B.hcap * 5;
+    const uint64_t A = 4164903690ULL;
+    const unsigned mg = (unsigned)((1ULL << 32) / n);   // n > 5
+    for (int k = s.gen_upto; k < target; ++k) {
+        // five draws at once (the state chain is one multiply-add per draw; the reductions and
+        // the duplicate tests run beside it); a duplicate (~0.5 % of samples at n = 2048) redraws
+        // sequentially from the state after it, exactly as the one-at-a-time loop does
+        uint64_t st[5];
+        unsigned x[5];
+        uint64_t sv = rng.s;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            sv = (uint64_t)(unsigned)sv * A + (unsigned)(sv >> 32);
+            st[i] = sv;
+            x[i] = (unsigned)sv;
+        }
+        int d[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {   // x mod n: umulhi(x, floor(2^32 / n)) is q or q - 1
+            const unsigned r = x[i] - __umulhi(x[i], mg) * n;
+            d[i] = (int)(r >= n ? r - n : r);
+        }
+        int j = 5;   // first draw that repeats an earlier one
+#pragma unroll
+        for (int i = 4; i >= 1; --i) {
+            bool dup = false;
+#pragma unroll
+            for (int t = 0; t < i; ++t) dup = dup || d[t] == d[i];
+            if (dup) j = i;
+        }
+        if (j == 5) {
+            rng.s = st[4];
+        } else {
+            rng.s = st[j];   // the duplicate draw is consumed; slot j onward one draw at a time
+            for (int i = j; i < 5; ++i) {
+                int idx;
+                for (;;) {
+                    idx = rng.uniform0(n, inv_n);
+                    bool dup = false;
+                    for (int t = 0; t < i; ++t) dup = dup || d[t] == idx;
+                    if (!dup) break;
+                }
+                d[i] = idx;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) smp[5 * k + i] = d[i];
+    }
+    if (target > s.gen_upto) {
+        s.gen_upto = target;
+        s.rng = rng.s;
+    }
+    const int c0 = s.eval_upto / kRH, c1 = (target + kRH - 1) / kRH;
+    if (c1 > c0) {
+        const int base = atomicAdd(cnt, c1 - c0);
+        for (int c = c0; c < c1; ++c) list[base + c - c0] = make_int2(p, c);
+        s.eval_upto = c1 * kRH;
+    }
+}
+
+// Round 0's samples and work list (later rounds: ess_replay_kernel, after its replay).
+__global__ __launch_bounds__(64) void ess_gen_kernel(int P, EssBufs B) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= P) return;
+    EssState s = B.st[p];
+    if (s.flags & kEssFive) {
+        B.list[atomicAdd(B.ctr, 1)] = make_int2(p, -1);
+        return;
+    }
+    if (s.flags & kEssDone) return;
+    ess_gen(s, p, P, 0, B);
+    B.st[p] = s;
+}
+
+// Persistent: each workgroup takes items until the list is exhausted (the count is final: the
+// list was written by the previous launch), so every wave reaches the exit.
+__global__ __launch_bounds__(kRThreads) void ess_chunk_kernel(int P, int round, const int64_t* __restrict__ offs,
+                                                              const double* __restrict__ cam, double threshold,
+                                                              const double* __restrict__ qn,
+                                                              double* __restrict__ E_out,
+                                                              int32_t* __restrict__ nmodels_out,
+                                                              uint8_t* __restrict__ mask,
+                                                              int32_t* __restrict__ ninl_out,
+                                                              int32_t* __restrict__ iters_out, EssBufs B) {
+    __shared__ double s_grp[kRH * kGS];
+    __shared__ double s_models[kRH * kMaxModels * 9];
+    __shared__ int s_nmod[kRH];
+    __shared__ int s_cnt[kRH * kMaxModels][kRWaves];
+    __shared__ int s_list[kRH * kMaxModels];
+    __shared__ int s_good[kRH * kMaxModels];
+    __shared__ int s_nlist, s_item;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int h = tid / kGL, gl = tid % kGL, gsh = (lane / kGL) * kGL;
+    const int2* list = B.list + (size_t)round * P * B.cmax;
+    const int count = B.ctr[2 * round];
+    for (;;) {
+        if (tid == 0) s_item = atomicAdd(B.ctr + 2 * round + 1, 1);
+        __syncthreads();
+        const int it = s_item;
+        if (it >= count) break;
+        const int2 item = list[it];
+        const int p = item.x, c = item.y;
+        const int64_t off = offs[p];
+        const int n = (int)(offs[p + 1] - off);
+        const double* q = qn + off * 4;
+        if (c < 0) {   // count == modelPoints: one kernel call on all points, mask all ones
+            if (h == 0) {
+                double qq[5][4];
+#pragma unroll
+                for (int j = 0; j < 5; ++j)
+#pragma unroll
+                    for (int cc = 0; cc < 4; ++cc) qq[j][cc] = q[4 * j + cc];
+                const int nm = five_point_group(qq, gl, gsh, s_grp, s_models);
+                if (gl == 0) {
+                    double* Eo = E_out + (int64_t)p * kMaxModels * 9;
+                    for (int e = 0; e < nm * 9; ++e) Eo[e] = s_models[e];
+                    nmodels_out[p] = nm;
+                    ninl_out[p] = nm > 0 ? 5 : 0;
+                    iters_out[p] = 1;
+                    for (int i = 0; i < 5; ++i) mask[off + i] = nm > 0 ? 1 : 0;
+                }
+            }
+            __syncthreads();
+            continue;
+        }
+        const double fx = cam[4 * p], fy = cam[4 * p + 1];
+        const double thresh = threshold / ((fx + fy) / 2);
+        const float tf = (float)(thresh * thresh);
+        const float tfu = nextafterf(tf, INFINITY);
+        const double mid = 0.5 * ((double)tf + (double)tfu);
+        const double Tmax = ((__float_as_uint(tf) & 1u) == 0u) ? mid : nextafter(mid, 0.0);
+        const double tlo = Tmax * (1.0 - 0x1p-40), thi = Tmax * (1.0 + 0x1p-40);
+        const int gen = B.st[p].gen_upto;
+        const int k = c * kRH + h;
+        for (int i = tid; i < kRH * kMaxModels * kRWaves; i += kRThreads) (&s_cnt[0][0])[i] = 0;
+        {
+            int nm = 0;
+            if (k < gen) {
+                const int* smp = B.samp + ((size_t)p * B.hcap + k) * 5;
+                double qq[5][4];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const int idx = smp[j];
+#pragma unroll
+                    for (int cc = 0; cc < 4; ++cc) qq[j][cc] = q[4 * idx + cc];
+                }
+                nm = five_point_group(qq, gl, gsh, s_grp + h * kGS, s_models + h * kMaxModels * 9);
+            }
+            if (gl == 0) s_nmod[h] = nm;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int cn = 0;
+            for (int hh = 0; hh < kRH; ++hh)
+                for (int m = 0; m < s_nmod[hh]; ++m) s_list[cn++] = hh * kMaxModels + m;
+            s_nlist = cn;
+        }
+        __syncthreads();
+        const int nlist = s_nlist;
+        score_chunk(q, n, s_list, nlist, s_models, s_cnt, tf, tlo, thi, tid);
+        __syncthreads();
+        for (int e = tid; e < nlist; e += kRThreads) {
+            int g = 0;
+#pragma unroll
+            for (int w = 0; w < kRWaves; ++w) g += s_cnt[s_list[e]][w];
+            s_good[e] = g;
+        }
+        __syncthreads();
+        if (tid < 64) {   // records: strict prefix maxima above 4, by a running max over 64-entry blocks
+            int2* rec = B.rec + ((size_t)p * B.cmax + c) * kRecMax;
+            double* recE = B.recE + ((size_t)p * B.cmax + c) * kRecE * 9;
+            int carry = 4, nr = 0;
+            for (int b0 = 0; b0 < nlist; b0 += 64) {
+                const int e = b0 + lane;
+                const int g = e < nlist ? s_good[e] : -1;
+                int pm = g;   // inclusive prefix max
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t = __shfl_up(pm, o);
+                    if (lane >= o) pm = max(pm, t);
+                }
+                int ex = __shfl_up(pm, 1);
+                ex = lane == 0 ? carry : max(carry, ex);
+                const bool isr = e < nlist && g > ex;
+                const unsigned long long bm = __ballot(isr);
+                if (isr) {
+                    const int r = nr + __popcll(bm & ((1ULL << lane) - 1ULL));
+                    const int code = s_list[e];
+                    const int hh = code / kMaxModels, m = code % kMaxModels;
+                    rec[r] = make_int2(g, hh * 16 + m);
+                    if (r < B.rece)
+                        for (int q9 = 0; q9 < 9; ++q9) recE[r * 9 + q9] = s_models[code * 9 + q9];
+                }
+                nr += __popcll(bm);
+                carry = max(carry, __shfl(pm, 63));
+            }
+            if (lane == 0) B.nrec[(size_t)p * B.cmax + c] = nr;
+        }
+        __syncthreads();
+    }
+}
+
+// One lane per pair: the records of the listed chunks in order (essential_ransac_kernel's replay),
+// then, unless the pair is complete, the next round's samples and work items.  A chunk's record
+// count and its first kPre records are loaded together (one round trip per chunk, not per record).
+constexpr int kPre = 6;
+__global__ __launch_bounds__(64) void ess_replay_kernel(int P, int round, double prob, EssBufs B) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= P) return;
+    EssState s = B.st[p];
+    if (s.flags & (kEssFive | kEssDone)) return;
+    int nit = s.niters;
+    bool done = false;
+    int c = s.rc;
+    const int cend = s.eval_upto / kRH;
+    for (; c < cend && !done; ++c) {
+        const int2* rec = B.rec + ((size_t)p * B.cmax + c) * kRecMax;
+        const int nr = B.nrec[(size_t)p * B.cmax + c];
+        int2 pre[kPre];
+#pragma unroll
+        for (int i = 0; i < kPre; ++i) pre[i] = rec[i];   // may read past nr: scratch, unused then
+        for (int i = 0; i < nr; ++i) {
+            int2 r = pre[0];
+#pragma unroll
+            for (int t = 1; t < kPre; ++t)
+                if (i == t) r = pre[t];
+            if (i >= kPre) r = rec[i];
+            const int k = c * kRH + (r.y >> 4), m = r.y & 15;
+            if (k != s.cur_k) {
+                if (k >= nit) { done = true; break; }
+                s.cur_k = k;
+            }
+            s.kp = k;
+            if (r.x > max(s.maxgood, 4)) {
+                s.maxgood = r.x;
+                s.best_c = c;
+                s.best_i = i;
+                s.best_k = k;
+                s.best_m = m;
+                nit = update_num_iters(prob, (double)(s.n - r.x) / s.n, 5, nit);
+            }
+        }
+    }
+    s.rc = c;
+    s.niters = nit;
+    if (done || nit <= s.eval_upto) {
+        s.flags |= kEssDone;
+        s.last = max(nit, s.kp + 1) - 1;
+    } else if (round + 1 < kEssRounds) {
+        ess_gen(s, p, P, round + 1, B);
+    }
+    B.st[p] = s;
+}
+
+__global__ __launch_bounds__(256) void ess_final_kernel(const int64_t* __restrict__ offs,
+                                                        const double* __restrict__ cam, double threshold,
+                                                        const double* __restrict__ qn, double* __restrict__ E_out,
+                                                        int32_t* __restrict__ nmodels_out,
+                                                        uint8_t* __restrict__ mask, int32_t* __restrict__ ninl_out,
+                                                        int32_t* __restrict__ iters_out, EssBufs B) {
+    __shared__ double s_grp[kGS];
+    __shared__ double s_models[kMaxModels * 9];
+    __shared__ double s_E[9];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const EssState s = B.st[p];
+    if (s.n <= 5) return;   // n < 5: written by ess_init_kernel; n == 5: by ess_chunk_kernel
+    const int64_t off = offs[p];
+    const int n = s.n;
+    const double* q = qn + off * 4;
+    const int maxgood = s.maxgood;
+    if (maxgood > 0) {
+        if (s.best_i < B.rece) {
+            if (tid < 9) s_E[tid] = B.recE[(((size_t)p * B.cmax + s.best_c) * kRecE + s.best_i) * 9 + tid];
+        } else if (tid < kGL) {   // the record's E was not kept: re-solve its sample (the same bits)
+            const int* smp = B.samp + ((size_t)p * B.hcap + s.best_k) * 5;
+            double qq[5][4];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int idx = smp[j];
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) qq[j][cc] = q[4 * idx + cc];
+            }
+            five_point_group(qq, tid, 0, s_grp, s_models);
+            wave_sync_lds();
+            if (tid < 9) s_E[tid] = s_models[s.best_m * 9 + tid];
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        nmodels_out[p] = maxgood > 0 ? 1 : 0;
+        ninl_out[p] = maxgood;
+        iters_out[p] = s.last + 1;
+        if (maxgood > 0)
+            for (int e = 0; e < 9; ++e) E_out[(int64_t)p * kMaxModels * 9 + e] = s_E[e];
+    }
+    if (maxgood > 0) {
+        const double fx = cam[4 * p], fy = cam[4 * p + 1];
+        const double thresh = threshold / ((fx + fy) / 2);
+        const float tf = (float)(thresh * thresh);
+        for (int i = tid; i < n; i += 256)
+            mask[off + i] = sampson(s_E, q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]) <= tf ? 1 : 0;
+    }
 }
 
 // cv::decomposeEssentialMat: SVD by one-sided Jacobi on E's columns, U's third
@@ -943,9 +1352,71 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
     SFMHIP_REQUIRE(pts0 && pts1 && offsets && cam && work && E && n_models && mask && n_inliers && iters,
                    "find_essential: null pointer");
     SFMHIP_REQUIRE(prob >= 0 && prob <= 1 && threshold > 0, "find_essential: prob in [0,1], threshold > 0");
-    hipLaunchKernelGGL(essential_ransac_kernel, dim3(n_pairs), dim3(kRThreads), 0, as_stream(stream), pts0, pts1,
-                       offsets, cam, prob, threshold, max_iters, work, E, n_models, mask, n_inliers, iters);
-    return check_launch("essential_ransac_kernel");
+    hipStream_t st = as_stream(stream);
+    auto env = [](const char* name, int dflt) {
+        const char* v = getenv(name);
+        return v && *v ? atoi(v) : dflt;
+    };
+    const int mono = env("SFMHIP_ESS_MONO", 0);   // A/B: the one-workgroup-per-pair kernel
+    if (mono) {
+        hipLaunchKernelGGL(essential_ransac_kernel, dim3(n_pairs), dim3(kRThreads), 0, st, pts0, pts1, offsets, cam,
+                           prob, threshold, max_iters, work, E, n_models, mask, n_inliers, iters);
+        return check_launch("essential_ransac_kernel");
+    }
+    // load-balanced form: per-pair scratch, pairs in batches of at most ~192 MB of it
+    const int cmax = ceil_div(std::max(max_iters, 1), kRH), hcap = cmax * kRH;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t per_pair = sizeof(EssState) + (size_t)hcap * 5 * sizeof(int) + (size_t)cmax * kRecMax * sizeof(int2) +
+                            (size_t)cmax * sizeof(int) + (size_t)cmax * kRecE * 9 * sizeof(double) +
+                            kEssRounds * (size_t)cmax * sizeof(int2);
+    const int batch = (int)std::max<int64_t>(1, std::min<int64_t>(n_pairs, ((size_t)192 << 20) / per_pair));
+    const size_t bytes = al(batch * sizeof(EssState)) + al((size_t)batch * hcap * 5 * sizeof(int)) +
+                         al((size_t)batch * cmax * kRecMax * sizeof(int2)) + al((size_t)batch * cmax * sizeof(int)) +
+                         al((size_t)batch * cmax * kRecE * 9 * sizeof(double)) +
+                         al(kEssRounds * (size_t)batch * cmax * sizeof(int2)) + al(2 * kEssRounds * sizeof(int));
+    char* base = nullptr;
+    if (scratch_alloc((void**)&base, bytes, st) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("find_essential: scratch allocation of %zu bytes failed", bytes);
+        return SFMHIP_E_HIP;
+    }
+    EssBufs B;
+    char* cur = base;
+    auto carve = [&](size_t b) { char* r = cur; cur += al(b); return r; };
+    B.st = (EssState*)carve(batch * sizeof(EssState));
+    B.samp = (int*)carve((size_t)batch * hcap * 5 * sizeof(int));
+    B.rec = (int2*)carve((size_t)batch * cmax * kRecMax * sizeof(int2));
+    B.nrec = (int*)carve((size_t)batch * cmax * sizeof(int));
+    B.recE = (double*)carve((size_t)batch * cmax * kRecE * 9 * sizeof(double));
+    B.list = (int2*)carve(kEssRounds * (size_t)batch * cmax * sizeof(int2));
+    B.ctr = (int*)carve(2 * kEssRounds * sizeof(int));
+    B.cmax = cmax;
+    B.hcap = hcap;
+    // records whose E is kept (tests: 0 re-solves every chosen model from its sample)
+    B.rece = std::min(kRecE, std::max(0, env("SFMHIP_ESS_RECE", kRecE)));
+    int rc = SFMHIP_OK;
+    for (int p0 = 0; p0 < n_pairs && rc == SFMHIP_OK; p0 += batch) {
+        const int PB = std::min(batch, n_pairs - p0);
+        const int64_t* of = offsets + p0;
+        const double* cm = cam + 4 * (size_t)p0;
+        double* Eb = E + (size_t)p0 * kMaxModels * 9;
+        int32_t *nmb = n_models + p0, *nib = n_inliers + p0, *itb = iters + p0;
+        const int lanes = ceil_div(PB, 64);
+        hipLaunchKernelGGL(ess_init_kernel, dim3(PB), dim3(256), 0, st, pts0, pts1, of, cm, max_iters, work, mask, nmb,
+                           nib, itb, B);
+        for (int round = 0; round < kEssRounds; ++round) {
+            if (round == 0) hipLaunchKernelGGL(ess_gen_kernel, dim3(lanes), dim3(64), 0, st, PB, B);
+            const int g = (int)std::min<int64_t>(512, (int64_t)PB * std::min(cmax, round + 1 < kEssRounds ? kSpecChunks << round : cmax));
+            hipLaunchKernelGGL(ess_chunk_kernel, dim3(g), dim3(kRThreads), 0, st, PB, round, of, cm, threshold, work,
+                               Eb, nmb, mask, nib, itb, B);
+            hipLaunchKernelGGL(ess_replay_kernel, dim3(lanes), dim3(64), 0, st, PB, round, prob, B);
+        }
+        hipLaunchKernelGGL(ess_final_kernel, dim3(PB), dim3(256), 0, st, of, cm, threshold, work, Eb, nmb, mask, nib,
+                           itb, B);
+        rc = check_launch("ess_*_kernel");
+    }
+    scratch_free(base, st);
+    return rc;
 }
 
 extern "C" int sfmhip_recover_pose(const double* E, int64_t e_stride, const double* pts0, const double* pts1,

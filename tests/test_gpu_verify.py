@@ -119,3 +119,63 @@ def test_essential_inliers_is_matching_py_count(sfm, gpu, scene):
         keep = mo.ravel() > 0
         ngo, _, _, _ = orc.recover_pose(Eo[:3], scene["pts0"][p][keep], scene["pts1"][p][keep], scene["K"])
         assert got[p] == ngo, p
+
+
+def _ess_run(sfm, pts0, pts1, K, max_iters=1000, prob=0.999, **env):
+    import os
+    keys = ("SFMHIP_ESS_MONO", "SFMHIP_ESS_RECE")
+    old = {k: os.environ.pop(k, None) for k in keys}
+    try:
+        for k, v in env.items():
+            os.environ["SFMHIP_ESS_" + k] = str(v)
+        v = sfm.verify
+        a, b, of = v.pack_pairs(pts0, pts1)
+        r = v.find_essential_batched(a, b, of, v._cam(K), prob=prob, max_iters=max_iters)
+        torch.cuda.synchronize()
+        return {k: t.cpu().numpy() for k, t in r.items()}
+    finally:
+        for k in keys:
+            os.environ.pop(k, None)
+            if old[k] is not None:
+                os.environ[k] = old[k]
+
+
+def _ess_mixed_scene():
+    """Ragged pairs: n < 5, n == 5, tiny n, high outlier fractions (many chunks, a round-1
+    work list), all-inlier pairs (niters collapses), and bench-sized pairs."""
+    sizes = [3, 5, 6, 9, 40, 300, 2048, 1000, 0, 700, 2048, 5, 120, 64]
+    out_fr = [0.3, 0.0, 0.0, 0.2, 0.6, 0.7, 0.3, 0.0, 0.3, 0.55, 0.45, 0.3, 0.8, 0.5]
+    pts0, pts1 = [], []
+    K = None
+    for i, (n, f) in enumerate(zip(sizes, out_fr)):
+        s = syn.two_view_pairs(1, max(n, 1), outlier_frac=f, noise_px=0.5, seed=100 + i)
+        K = s["K"]
+        pts0.append(s["pts0"][0][:n])
+        pts1.append(s["pts1"][0][:n])
+    return pts0, pts1, K
+
+
+@pytest.mark.parametrize("max_iters", [1000, 1, 40, 77])
+def test_balanced_equals_monolithic(sfm, gpu, max_iters):
+    """The load-balanced form (chunks as work items, records replayed per pair) gives the same
+    bits as the one-workgroup-per-pair kernel: E, model counts, masks, inlier and iteration
+    counts; also with every chosen E re-solved from its sample (SFMHIP_ESS_RECE=0)."""
+    pts0, pts1, K = _ess_mixed_scene()
+    mono = _ess_run(sfm, pts0, pts1, K, max_iters, MONO=1)
+    for env in ({}, {"RECE": 0}, {"RECE": 1}):
+        bal = _ess_run(sfm, pts0, pts1, K, max_iters, **env)
+        for k in ("n_models", "n_inliers", "iters", "mask"):
+            assert np.array_equal(bal[k], mono[k]), (env, k, bal[k], mono[k])
+        nm = mono["n_models"]
+        for p in range(len(nm)):
+            assert np.array_equal(bal["E"][p, :nm[p]], mono["E"][p, :nm[p]]), (env, p)
+
+
+def test_balanced_bench_scene_matches_monolithic(sfm, gpu):
+    """The bench workload's first 64 pairs (2-7 chunks each, oracle-counted): same bits."""
+    s = syn.two_view_pairs(64, 2048, outlier_frac=0.3, noise_px=0.5, seed=6)
+    mono = _ess_run(sfm, s["pts0"], s["pts1"], s["K"], MONO=1)
+    bal = _ess_run(sfm, s["pts0"], s["pts1"], s["K"])
+    for k in ("E", "n_models", "n_inliers", "iters", "mask"):
+        assert np.array_equal(bal[k], mono[k]), k
+    assert mono["iters"].max() > 64 and mono["iters"].min() >= 1   # round 1 exercised
