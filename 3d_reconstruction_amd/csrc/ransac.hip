@@ -44,7 +44,7 @@ constexpr int kMaxModels = 10;
 constexpr int kGS = 224;                // LDS doubles per group
 constexpr int kPB = 4;                  // points per lane per scoring block
 constexpr int kRWaves = kRThreads / 64;
-constexpr int kPThreads = 256;          // recover_pose kernel
+constexpr int kPThreads = 768;          // recover_pose kernel: 3 waves per SIMD (156 VGPRs), one workgroup per CU
 constexpr double kDblEps = 2.220446049250313e-16;
 constexpr double kDblMin = 2.2250738585072014e-308;
 #ifndef SFMHIP_ABERTH_FAST
