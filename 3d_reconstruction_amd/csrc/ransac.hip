@@ -580,16 +580,17 @@ __device__ __forceinline__ int wave_sum(int v) {
 // Scores every listed model of a chunk on all n points: each wave's ballot counts go to
 // s_cnt[model][wave] (no atomics).  Branch-free margin tests for two models x kPB points at a
 // time, so the chains interleave; the exact division only where a test is ambiguous.
+template <int NT = kRThreads>
 __device__ __forceinline__ void score_chunk(const double* __restrict__ q, int n, const int* s_list, int nlist,
-                                            const double* s_models, int (*s_cnt)[kRWaves], float tf, double tlo,
+                                            const double* s_models, int (*s_cnt)[NT / 64], float tf, double tlo,
                                             double thi, int tid) {
     const int lane = tid & 63, wave = tid >> 6;
-    for (int b0 = 0; b0 < n; b0 += kRThreads * kPB) {
+    for (int b0 = 0; b0 < n; b0 += NT * kPB) {
         double pt[kPB][4];
         bool val[kPB];
 #pragma unroll
         for (int u = 0; u < kPB; ++u) {
-            const int i = b0 + u * kRThreads + tid;
+            const int i = b0 + u * NT + tid;
             val[u] = i < n;
 #pragma unroll
             for (int c = 0; c < 4; ++c) pt[u][c] = val[u] ? q[4 * i + c] : 0.0;
@@ -807,7 +808,7 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
 //                      chunk), in replay order;
 //   ess_replay_kernel  one lane per pair replays the records in OpenCV's order (a model replaces
 //                      the best iff count > max(best, 4); RANSACUpdateNumIters shrinks niters),
-//                      then runs ess_gen for the next round (round 0: ess_gen_kernel).
+//                      then runs ess_gen for the next round (round 0: ess_init_kernel).
 // Only a record can ever replace the best (a model at or below an earlier count of its chunk was
 // either beaten by that model's acceptance or is <= max(best, 4) already), and niters never grows,
 // so the last round — every chunk below the niters the previous replay left, an upper bound of the
@@ -816,9 +817,8 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
 // The same best model, inlier count and iteration count as the sequential loop over the same
 // models.  ess_final_kernel writes E (kept with the record, or re-solved from its sample) and the
 // mask.
-constexpr int kSpecChunks = 2;     // round r lists chunks up to kSpecChunks << r (last round: all)
+constexpr int kSpecHyps = 64;      // round r lists chunks up to kSpecHyps << r hypotheses (last round: all)
 constexpr int kEssRounds = 3;
-constexpr int kRecMax = kRH * kMaxModels;
 constexpr int kRecE = 16;          // records per chunk whose E is kept (later ones: re-solved)
 constexpr int kEssFive = 1, kEssDone = 2;
 
@@ -832,56 +832,21 @@ struct EssState {
 struct EssBufs {
     EssState* st;
     int* samp;       // [P][hcap][5]
-    int2* rec;       // [P][cmax][kRecMax]: {count, h * 16 + m}
+    int2* rec;       // [P][cmax][ch * kMaxModels]: {count, h * 16 + m}
     int* nrec;       // [P][cmax]
     double* recE;    // [P][cmax][kRecE][9]
     int2* list;      // [kEssRounds][P * cmax]: {pair, chunk (-1: the n == 5 call)}
     int* ctr;        // [2 kEssRounds]: (count, head) per round
     int cmax, hcap, rece;
+    int ch;          // hypotheses per chunk (16-lane groups of the chunk kernel)
 };
-
-__global__ __launch_bounds__(256) void ess_init_kernel(const double* __restrict__ pts0, const double* __restrict__ pts1,
-                                                       const int64_t* __restrict__ offs, const double* __restrict__ cam,
-                                                       int max_iters, double* __restrict__ qn, uint8_t* __restrict__ mask,
-                                                       int32_t* __restrict__ nmodels_out,
-                                                       int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out,
-                                                       EssBufs B) {
-    const int p = blockIdx.x, tid = threadIdx.x;
-    const int64_t off = offs[p];
-    const int n = (int)(offs[p + 1] - off);
-    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
-    double* q = qn + off * 4;
-    for (int i = tid; i < n; i += 256) {
-        q[4 * i + 0] = (pts0[2 * (off + i)] - cx) / fx;
-        q[4 * i + 1] = (pts0[2 * (off + i) + 1] - cy) / fy;
-        q[4 * i + 2] = (pts1[2 * (off + i)] - cx) / fx;
-        q[4 * i + 3] = (pts1[2 * (off + i) + 1] - cy) / fy;
-        mask[off + i] = 0;
-    }
-    if (tid == 0) {
-        EssState s;
-        s.rng = ~0ULL;
-        s.n = n;
-        s.flags = n < 5 ? kEssDone : n == 5 ? kEssFive : 0;
-        s.niters = max(max_iters, 1);
-        s.maxgood = 0;
-        s.gen_upto = s.eval_upto = s.rc = 0;
-        s.cur_k = s.kp = -1;
-        s.best_c = s.best_i = s.best_k = s.best_m = -1;
-        s.last = -1;
-        B.st[p] = s;
-        if (n < 5) { nmodels_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
-        if (p == 0)
-            for (int i = 0; i < 2 * kEssRounds; ++i) B.ctr[i] = 0;
-    }
-}
 
 // One lane per pair: draws samples [gen_upto, target) exactly as essential_ransac_kernel's lane 0
 // does (5 distinct indices per sample, redrawing duplicates), then lists the chunks covering them.
 __device__ void ess_gen(EssState& s, int p, int P, int round, const EssBufs& B) {
     int2* list = B.list + (size_t)round * P * B.cmax;
     int* cnt = B.ctr + 2 * round;
-    const int target = round + 1 < kEssRounds ? min(s.niters, (kSpecChunks << round) * kRH) : s.niters;
+    const int target = round + 1 < kEssRounds ? min(s.niters, kSpecHyps << round) : s.niters;
     const unsigned n = (unsigned)s.n;
     const double inv_n = 1.0 / (double)n;
     CvRng rng{s.rng};
@@ -937,31 +902,54 @@ __device__ void ess_gen(EssState& s, int p, int P, int round, const EssBufs& B) 
         s.gen_upto = target;
         s.rng = rng.s;
     }
-    const int c0 = s.eval_upto / kRH, c1 = (target + kRH - 1) / kRH;
+    const int c0 = s.eval_upto / B.ch, c1 = (target + B.ch - 1) / B.ch;
     if (c1 > c0) {
         const int base = atomicAdd(cnt, c1 - c0);
         for (int c = c0; c < c1; ++c) list[base + c - c0] = make_int2(p, c);
-        s.eval_upto = c1 * kRH;
+        s.eval_upto = c1 * B.ch;
     }
 }
 
-// Round 0's samples and work list (later rounds: ess_replay_kernel, after its replay).
-__global__ __launch_bounds__(64) void ess_gen_kernel(int P, EssBufs B) {
-    const int p = blockIdx.x * 64 + threadIdx.x;
-    if (p >= P) return;
-    EssState s = B.st[p];
-    if (s.flags & kEssFive) {
-        B.list[atomicAdd(B.ctr, 1)] = make_int2(p, -1);
-        return;
+__global__ __launch_bounds__(256) void ess_init_kernel(const double* __restrict__ pts0, const double* __restrict__ pts1,
+                                                       const int64_t* __restrict__ offs, const double* __restrict__ cam,
+                                                       int max_iters, double* __restrict__ qn, uint8_t* __restrict__ mask,
+                                                       int32_t* __restrict__ nmodels_out,
+                                                       int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out,
+                                                       int P, EssBufs B) {
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int64_t off = offs[p];
+    const int n = (int)(offs[p + 1] - off);
+    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
+    double* q = qn + off * 4;
+    for (int i = tid; i < n; i += 256) {
+        q[4 * i + 0] = (pts0[2 * (off + i)] - cx) / fx;
+        q[4 * i + 1] = (pts0[2 * (off + i) + 1] - cy) / fy;
+        q[4 * i + 2] = (pts1[2 * (off + i)] - cx) / fx;
+        q[4 * i + 3] = (pts1[2 * (off + i) + 1] - cy) / fy;
+        mask[off + i] = 0;
     }
-    if (s.flags & kEssDone) return;
-    ess_gen(s, p, P, 0, B);
-    B.st[p] = s;
+    if (tid == 0) {
+        EssState s;
+        s.rng = ~0ULL;
+        s.n = n;
+        s.flags = n < 5 ? kEssDone : n == 5 ? kEssFive : 0;
+        s.niters = max(max_iters, 1);
+        s.maxgood = 0;
+        s.gen_upto = s.eval_upto = s.rc = 0;
+        s.cur_k = s.kp = -1;
+        s.best_c = s.best_i = s.best_k = s.best_m = -1;
+        s.last = -1;
+        if (n < 5) { nmodels_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
+        if (n == 5) B.list[atomicAdd(B.ctr, 1)] = make_int2(p, -1);   // the one kernel call on all points
+        if (n > 5) ess_gen(s, p, P, 0, B);                               // round 0's samples and items
+        B.st[p] = s;
+    }
 }
 
 // Persistent: each workgroup takes items until the list is exhausted (the count is final: the
 // list was written by the previous launch), so every wave reaches the exit.
-__global__ __launch_bounds__(kRThreads) void ess_chunk_kernel(int P, int round, const int64_t* __restrict__ offs,
+template <int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void ess_chunk_kernel(int P, int round, const int64_t* __restrict__ offs,
                                                               const double* __restrict__ cam, double threshold,
                                                               const double* __restrict__ qn,
                                                               double* __restrict__ E_out,
@@ -969,12 +957,13 @@ __global__ __launch_bounds__(kRThreads) void ess_chunk_kernel(int P, int round, 
                                                               uint8_t* __restrict__ mask,
                                                               int32_t* __restrict__ ninl_out,
                                                               int32_t* __restrict__ iters_out, EssBufs B) {
-    __shared__ double s_grp[kRH * kGS];
-    __shared__ double s_models[kRH * kMaxModels * 9];
-    __shared__ int s_nmod[kRH];
-    __shared__ int s_cnt[kRH * kMaxModels][kRWaves];
-    __shared__ int s_list[kRH * kMaxModels];
-    __shared__ int s_good[kRH * kMaxModels];
+    constexpr int CH = NT / kGL, NW = NT / 64;
+    __shared__ double s_grp[CH * kGS];
+    __shared__ double s_models[CH * kMaxModels * 9];
+    __shared__ int s_nmod[CH];
+    __shared__ int s_cnt[CH * kMaxModels][NW];
+    __shared__ int s_list[CH * kMaxModels];
+    __shared__ int s_good[CH * kMaxModels];
     __shared__ int s_nlist, s_item;
     const int tid = threadIdx.x, lane = tid & 63;
     const int h = tid / kGL, gl = tid % kGL, gsh = (lane / kGL) * kGL;
@@ -1018,8 +1007,8 @@ __global__ __launch_bounds__(kRThreads) void ess_chunk_kernel(int P, int round, 
         const double Tmax = ((__float_as_uint(tf) & 1u) == 0u) ? mid : nextafter(mid, 0.0);
         const double tlo = Tmax * (1.0 - 0x1p-40), thi = Tmax * (1.0 + 0x1p-40);
         const int gen = B.st[p].gen_upto;
-        const int k = c * kRH + h;
-        for (int i = tid; i < kRH * kMaxModels * kRWaves; i += kRThreads) (&s_cnt[0][0])[i] = 0;
+        const int k = c * CH + h;
+        for (int i = tid; i < CH * kMaxModels * NW; i += NT) (&s_cnt[0][0])[i] = 0;
         {
             int nm = 0;
             if (k < gen) {
@@ -1038,23 +1027,23 @@ __global__ __launch_bounds__(kRThreads) void ess_chunk_kernel(int P, int round, 
         __syncthreads();
         if (tid == 0) {
             int cn = 0;
-            for (int hh = 0; hh < kRH; ++hh)
+            for (int hh = 0; hh < CH; ++hh)
                 for (int m = 0; m < s_nmod[hh]; ++m) s_list[cn++] = hh * kMaxModels + m;
             s_nlist = cn;
         }
         __syncthreads();
         const int nlist = s_nlist;
-        score_chunk(q, n, s_list, nlist, s_models, s_cnt, tf, tlo, thi, tid);
+        score_chunk<NT>(q, n, s_list, nlist, s_models, s_cnt, tf, tlo, thi, tid);
         __syncthreads();
-        for (int e = tid; e < nlist; e += kRThreads) {
+        for (int e = tid; e < nlist; e += NT) {
             int g = 0;
 #pragma unroll
-            for (int w = 0; w < kRWaves; ++w) g += s_cnt[s_list[e]][w];
+            for (int w = 0; w < NW; ++w) g += s_cnt[s_list[e]][w];
             s_good[e] = g;
         }
         __syncthreads();
         if (tid < 64) {   // records: strict prefix maxima above 4, by a running max over 64-entry blocks
-            int2* rec = B.rec + ((size_t)p * B.cmax + c) * kRecMax;
+            int2* rec = B.rec + ((size_t)p * B.cmax + c) * (CH * kMaxModels);
             double* recE = B.recE + ((size_t)p * B.cmax + c) * kRecE * 9;
             int carry = 4, nr = 0;
             for (int b0 = 0; b0 < nlist; b0 += 64) {
@@ -1087,47 +1076,71 @@ __global__ __launch_bounds__(kRThreads) void ess_chunk_kernel(int P, int round, 
     }
 }
 
-// One lane per pair: the records of the listed chunks in order (essential_ransac_kernel's replay),
-// then, unless the pair is complete, the next round's samples and work items.  A chunk's record
-// count and its first kPre records are loaded together (one round trip per chunk, not per record).
-constexpr int kPre = 6;
+// One wave per pair: the records of the listed chunks in order (essential_ransac_kernel's replay),
+// then, unless the pair is complete, the next round's samples and work items (lane 0).  The lanes
+// first stage a window of chunks' records in LDS — lane t loads chunk t's count and then its
+// records, all loads independent — so lane 0's replay waits on memory once per window, not once
+// per record.
+constexpr int kRpCap = 2048;   // records staged per window
 __global__ __launch_bounds__(64) void ess_replay_kernel(int P, int round, double prob, EssBufs B) {
-    const int p = blockIdx.x * 64 + threadIdx.x;
-    if (p >= P) return;
+    __shared__ int2 s_rec[kRpCap];
+    __shared__ int s_off[65], s_cnt[64];
+    const int p = blockIdx.x, lane = threadIdx.x;
     EssState s = B.st[p];
-    if (s.flags & (kEssFive | kEssDone)) return;
+    if (s.flags & (kEssFive | kEssDone)) return;   // uniform
+    const int recmax = B.ch * kMaxModels;
     int nit = s.niters;
     bool done = false;
     int c = s.rc;
-    const int cend = s.eval_upto / kRH;
-    for (; c < cend && !done; ++c) {
-        const int2* rec = B.rec + ((size_t)p * B.cmax + c) * kRecMax;
-        const int nr = B.nrec[(size_t)p * B.cmax + c];
-        int2 pre[kPre];
+    const int cend = s.eval_upto / B.ch;
+    while (c < cend && !done) {   // uniform: done is broadcast below
+        const int t_n = c + lane < cend ? B.nrec[(size_t)p * B.cmax + c + lane] : 0;
+        int pre = t_n;   // inclusive scan
 #pragma unroll
-        for (int i = 0; i < kPre; ++i) pre[i] = rec[i];   // may read past nr: scratch, unused then
-        for (int i = 0; i < nr; ++i) {
-            int2 r = pre[0];
-#pragma unroll
-            for (int t = 1; t < kPre; ++t)
-                if (i == t) r = pre[t];
-            if (i >= kPre) r = rec[i];
-            const int k = c * kRH + (r.y >> 4), m = r.y & 15;
-            if (k != s.cur_k) {
-                if (k >= nit) { done = true; break; }
-                s.cur_k = k;
-            }
-            s.kp = k;
-            if (r.x > max(s.maxgood, 4)) {
-                s.maxgood = r.x;
-                s.best_c = c;
-                s.best_i = i;
-                s.best_k = k;
-                s.best_m = m;
-                nit = update_num_iters(prob, (double)(s.n - r.x) / s.n, 5, nit);
-            }
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(pre, d);
+            if (lane >= d) pre += t;
         }
+        // window: the leading chunks whose records fit (a chunk holds at most recmax <= kRpCap)
+        const unsigned long long fit = __ballot(c + lane < cend && pre <= kRpCap);
+        const int nwin = __popcll(fit);   // fit is a prefix of the lanes (pre grows with lane)
+        if (lane < nwin) {
+            const int2* rec = B.rec + ((size_t)p * B.cmax + c + lane) * recmax;
+            for (int i = 0; i < t_n; ++i) s_rec[pre - t_n + i] = rec[i];
+            s_off[lane] = pre - t_n;
+            s_cnt[lane] = t_n;
+        }
+        __syncthreads();
+        if (lane == 0) {
+            int w = 0;
+            for (; w < nwin && !done; ++w) {
+                const int cc = c + w;
+                for (int i = 0; i < s_cnt[w]; ++i) {
+                    const int2 r = s_rec[s_off[w] + i];
+                    const int k = cc * B.ch + (r.y >> 4), m = r.y & 15;
+                    if (k != s.cur_k) {
+                        if (k >= nit) { done = true; break; }
+                        s.cur_k = k;
+                    }
+                    s.kp = k;
+                    if (r.x > max(s.maxgood, 4)) {
+                        s.maxgood = r.x;
+                        s.best_c = cc;
+                        s.best_i = i;
+                        s.best_k = k;
+                        s.best_m = m;
+                        nit = update_num_iters(prob, (double)(s.n - r.x) / s.n, 5, nit);
+                    }
+                }
+            }
+            s_off[64] = (done ? 1 : 0) | (w << 1);
+        }
+        __syncthreads();
+        done = s_off[64] & 1;
+        c += done ? (s_off[64] >> 1) : nwin;
+        __syncthreads();
     }
+    if (lane != 0) return;
     s.rc = c;
     s.niters = nit;
     if (done || nit <= s.eval_upto) {
@@ -1363,15 +1376,19 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
                            prob, threshold, max_iters, work, E, n_models, mask, n_inliers, iters);
         return check_launch("essential_ransac_kernel");
     }
-    // load-balanced form: per-pair scratch, pairs in batches of at most ~192 MB of it
-    const int cmax = ceil_div(std::max(max_iters, 1), kRH), hcap = cmax * kRH;
+    // load-balanced form: per-pair scratch, pairs in batches of at most ~192 MB of it.  Chunk
+    // kernel: 256 threads (16 hypotheses per item, two workgroups per CU so one's scoring overlaps
+    // the other's solve) or 512 (SFMHIP_ESS_CT=512: 32 per item, one per CU)
+    const int ct = env("SFMHIP_ESS_CT", 256) == 512 ? 512 : 256;
+    const int ch = ct / kGL, recmax = ch * kMaxModels;
+    const int cmax = ceil_div(std::max(max_iters, 1), ch), hcap = cmax * ch;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t per_pair = sizeof(EssState) + (size_t)hcap * 5 * sizeof(int) + (size_t)cmax * kRecMax * sizeof(int2) +
+    const size_t per_pair = sizeof(EssState) + (size_t)hcap * 5 * sizeof(int) + (size_t)cmax * recmax * sizeof(int2) +
                             (size_t)cmax * sizeof(int) + (size_t)cmax * kRecE * 9 * sizeof(double) +
                             kEssRounds * (size_t)cmax * sizeof(int2);
     const int batch = (int)std::max<int64_t>(1, std::min<int64_t>(n_pairs, ((size_t)192 << 20) / per_pair));
     const size_t bytes = al(batch * sizeof(EssState)) + al((size_t)batch * hcap * 5 * sizeof(int)) +
-                         al((size_t)batch * cmax * kRecMax * sizeof(int2)) + al((size_t)batch * cmax * sizeof(int)) +
+                         al((size_t)batch * cmax * recmax * sizeof(int2)) + al((size_t)batch * cmax * sizeof(int)) +
                          al((size_t)batch * cmax * kRecE * 9 * sizeof(double)) +
                          al(kEssRounds * (size_t)batch * cmax * sizeof(int2)) + al(2 * kEssRounds * sizeof(int));
     char* base = nullptr;
@@ -1385,13 +1402,14 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
     auto carve = [&](size_t b) { char* r = cur; cur += al(b); return r; };
     B.st = (EssState*)carve(batch * sizeof(EssState));
     B.samp = (int*)carve((size_t)batch * hcap * 5 * sizeof(int));
-    B.rec = (int2*)carve((size_t)batch * cmax * kRecMax * sizeof(int2));
+    B.rec = (int2*)carve((size_t)batch * cmax * recmax * sizeof(int2));
     B.nrec = (int*)carve((size_t)batch * cmax * sizeof(int));
     B.recE = (double*)carve((size_t)batch * cmax * kRecE * 9 * sizeof(double));
     B.list = (int2*)carve(kEssRounds * (size_t)batch * cmax * sizeof(int2));
     B.ctr = (int*)carve(2 * kEssRounds * sizeof(int));
     B.cmax = cmax;
     B.hcap = hcap;
+    B.ch = ch;
     // records whose E is kept (tests: 0 re-solves every chosen model from its sample)
     B.rece = std::min(kRecE, std::max(0, env("SFMHIP_ESS_RECE", kRecE)));
     int rc = SFMHIP_OK;
@@ -1401,15 +1419,19 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
         const double* cm = cam + 4 * (size_t)p0;
         double* Eb = E + (size_t)p0 * kMaxModels * 9;
         int32_t *nmb = n_models + p0, *nib = n_inliers + p0, *itb = iters + p0;
-        const int lanes = ceil_div(PB, 64);
+        (void)hipMemsetAsync(B.ctr, 0, 2 * kEssRounds * sizeof(int), st);
         hipLaunchKernelGGL(ess_init_kernel, dim3(PB), dim3(256), 0, st, pts0, pts1, of, cm, max_iters, work, mask, nmb,
-                           nib, itb, B);
+                           nib, itb, PB, B);
         for (int round = 0; round < kEssRounds; ++round) {
-            if (round == 0) hipLaunchKernelGGL(ess_gen_kernel, dim3(lanes), dim3(64), 0, st, PB, B);
-            const int g = (int)std::min<int64_t>(512, (int64_t)PB * std::min(cmax, round + 1 < kEssRounds ? kSpecChunks << round : cmax));
-            hipLaunchKernelGGL(ess_chunk_kernel, dim3(g), dim3(kRThreads), 0, st, PB, round, of, cm, threshold, work,
-                               Eb, nmb, mask, nib, itb, B);
-            hipLaunchKernelGGL(ess_replay_kernel, dim3(lanes), dim3(64), 0, st, PB, round, prob, B);
+            const int items = round + 1 < kEssRounds ? ceil_div(kSpecHyps << round, ch) : cmax;
+            const int g = (int)std::min<int64_t>(ct == 512 ? 512 : 1024, (int64_t)PB * std::min(cmax, items));
+            if (ct == 512)
+                hipLaunchKernelGGL(ess_chunk_kernel<512>, dim3(g), dim3(512), 0, st, PB, round, of, cm, threshold,
+                                   work, Eb, nmb, mask, nib, itb, B);
+            else
+                hipLaunchKernelGGL(ess_chunk_kernel<256>, dim3(g), dim3(256), 0, st, PB, round, of, cm, threshold,
+                                   work, Eb, nmb, mask, nib, itb, B);
+            hipLaunchKernelGGL(ess_replay_kernel, dim3(PB), dim3(64), 0, st, PB, round, prob, B);
         }
         hipLaunchKernelGGL(ess_final_kernel, dim3(PB), dim3(256), 0, st, of, cm, threshold, work, Eb, nmb, mask, nib,
                            itb, B);
