@@ -37,124 +37,7 @@ namespace sfmhip {
 // the SVD where lambda4/lambda3 -> 1 from M's rounding, and a two-vector block,
 // 2e-7 off where sigma2 ~ sigma3), and with geom_dev.h's dlt_point (inverse
 // iteration + 4x4 Jacobi) what that cannot decide.
-constexpr int kDltNormalIters = 6;
-constexpr double kDltLam3Floor = 1e-7;
-
 typedef const double __attribute__((address_space(4))) const_f64;   // constant space: uniform -> s_load
-
-// M = A^T A: m = {00, 01, 02, 03, 11, 12, 13, 22, 23, 33}
-template <class PT>
-__device__ __forceinline__ void dlt_normal_matrix(PT Pa, double xa, double ya, double xb, double yb, double (&m)[10]) {
-#pragma unroll
-    for (int k = 0; k < 10; ++k) m[k] = 0.0;
-    auto acc = [&](double r0, double r1, double r2, double r3) {
-        m[0] = fma(r0, r0, m[0]); m[1] = fma(r0, r1, m[1]); m[2] = fma(r0, r2, m[2]); m[3] = fma(r0, r3, m[3]);
-        m[4] = fma(r1, r1, m[4]); m[5] = fma(r1, r2, m[5]); m[6] = fma(r1, r3, m[6]);
-        m[7] = fma(r2, r2, m[7]); m[8] = fma(r2, r3, m[8]); m[9] = fma(r3, r3, m[9]);
-    };
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-        const PT Q = Pa + 12 * v;
-        const double x = v ? xb : xa, y = v ? yb : ya;
-        // rows x p2 - p0, y p2 - p1, x p1 - y p0 (cvTriangulatePoints matrA)
-        acc(fma(x, Q[8], -Q[0]), fma(x, Q[9], -Q[1]), fma(x, Q[10], -Q[2]), fma(x, Q[11], -Q[3]));
-        acc(fma(y, Q[8], -Q[4]), fma(y, Q[9], -Q[5]), fma(y, Q[10], -Q[6]), fma(y, Q[11], -Q[7]));
-        acc(fma(x, Q[4], -y * Q[0]), fma(x, Q[5], -y * Q[1]), fma(x, Q[6], -y * Q[2]), fma(x, Q[7], -y * Q[3]));
-        // the sums are complete here: without this the compiler sinks the off-diagonal
-        // sums to their first use and keeps all 24 row entries live (110 VGPRs)
-        asm volatile("" : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]), "+v"(m[3]), "+v"(m[4]), "+v"(m[5]), "+v"(m[6]),
-                     "+v"(m[7]), "+v"(m[8]), "+v"(m[9]));
-    }
-}
-
-// L D L^T of M - shift I (unit lower L: l10 l20 l30 l21 l31 l32; inverse pivots i0..i3)
-struct Ldl {
-    double l10, l20, l30, l21, l31, l32, i0, i1, i2, i3;
-    bool pd3;      // the leading 3x3 pivots are positive
-    double t3;     // trace of the leading 3x3 block's inverse (bounds its smallest eigenvalue)
-};
-
-__device__ __forceinline__ Ldl dlt_ldl(const double (&m)[10], double shift, double floor3) {
-    Ldl f;
-    const double d0 = m[0] - shift;
-    f.i0 = rcp_nr(d0);
-    f.l10 = m[1] * f.i0; f.l20 = m[2] * f.i0; f.l30 = m[3] * f.i0;
-    const double d1 = fma(-f.l10, m[1], m[4] - shift);
-    f.i1 = rcp_nr(d1);
-    const double a21 = fma(-f.l20, m[1], m[5]), a31 = fma(-f.l30, m[1], m[6]);
-    f.l21 = a21 * f.i1; f.l31 = a31 * f.i1;
-    const double d2 = fma(-f.l21, a21, fma(-f.l20, m[2], m[7] - shift));
-    f.i2 = rcp_nr(d2);
-    const double a32 = fma(-f.l31, a21, fma(-f.l30, m[2], m[8]));
-    f.l32 = a32 * f.i2;
-    const double d3 = fma(-f.l32, a32, fma(-f.l31, a31, fma(-f.l30, m[3], m[9] - shift)));
-    // d3 ~ lambda4 - shift may round to ~0: keep its sign, floor its size at the rounding level of M
-    f.i3 = rcp_nr(d3 < 0.0 ? fmin(d3, -floor3) : fmax(d3, floor3));
-    f.pd3 = d0 > 0.0 && d1 > 0.0 && d2 > 0.0;
-    const double g = fma(f.l10, f.l21, -f.l20);
-    f.t3 = fma(fma(g, g, fma(f.l21, f.l21, 1.0)), f.i2, fma(fma(f.l10, f.l10, 1.0), f.i1, f.i0));
-    return f;
-}
-
-// One inverse-iteration step on a unit iterate: y <- (M - shift I)^-1 y, renormalised
-// (sign aligned with the old y: an indefinite shifted matrix may flip it);
-// returns |y_new - y_old|^2.
-__device__ __forceinline__ double dlt_inv_step(const Ldl& f, double& y0, double& y1, double& y2, double& y3) {
-    const double o0 = y0, o1 = y1, o2 = y2, o3 = y3;
-    // L w = o, w /= d, L^T z = w
-    const double w0 = o0 * f.i0;
-    const double u1 = fma(-f.l10, o0, o1);
-    const double w1 = u1 * f.i1;
-    const double v2 = fma(-f.l21, u1, fma(-f.l20, o0, o2));
-    const double w2 = v2 * f.i2;
-    const double z3 = fma(-f.l32, v2, fma(-f.l31, u1, fma(-f.l30, o0, o3))) * f.i3;
-    const double z2 = fma(-f.l32, z3, w2);
-    const double z1 = fma(-f.l31, z3, fma(-f.l21, z2, w1));
-    const double z0 = fma(-f.l30, z3, fma(-f.l20, z2, fma(-f.l10, z1, w0)));
-    double s2 = rsq_nr(fma(z0, z0, fma(z1, z1, fma(z2, z2, z3 * z3))));
-    if (fma(z0, o0, fma(z1, o1, fma(z2, o2, z3 * o3))) < 0.0) s2 = -s2;
-    y0 = z0 * s2;
-    y1 = z1 * s2;
-    y2 = z2 * s2;
-    y3 = z3 * s2;
-    const double e0 = y0 - o0, e1 = y1 - o1, e2 = y2 - o2, e3 = y3 - o3;
-    return fma(e0, e0, fma(e1, e1, fma(e2, e2, e3 * e3)));
-}
-
-__device__ __forceinline__ bool dlt_store_unit(double y0, double y1, double y2, double y3, double* Xout) {
-    const double nn = fma(y0, y0, fma(y1, y1, fma(y2, y2, y3 * y3)));
-    if (!(nn > 0.0) || !(nn < 1e300)) return false;
-    const double sc = (y3 < 0 ? -1.0 : 1.0) / sqrt(nn);
-    Xout[0] = y0 * sc;
-    Xout[1] = y1 * sc;
-    Xout[2] = y2 * sc;
-    Xout[3] = y3 * sc;
-    return true;
-}
-
-// 0: decided (Xout written); 1: lambda3 bound met but not converged; 2: the QR path decides
-__device__ __forceinline__ int dlt_point_normal(const const_f64* __restrict__ Pa, double xa, double ya, double xb,
-                                                double yb, double* Xout) {
-    double m[10];
-    dlt_normal_matrix(Pa, xa, ya, xb, yb, m);
-    // branch-free up to the iteration (an early exit lets the compiler sink the
-    // off-diagonal sums past it and keep all 24 row entries live)
-    const double tr = (m[0] + m[4]) + (m[7] + m[9]);
-    const Ldl f = dlt_ldl(m, 0.0, 1e-30 * tr);
-    const bool good = f.pd3 && tr < 1e300 && f.t3 * (kDltLam3Floor * tr) <= 1.0;
-    double y0, y1, y2, y3 = 1.0;                        // L^T y = e4, normalised
-    y2 = -f.l32;
-    y1 = fma(-f.l21, y2, -f.l31);
-    y0 = fma(-f.l10, y1, fma(-f.l20, y2, -f.l30));
-    const double s0 = rsq_nr(fma(y0, y0, fma(y1, y1, fma(y2, y2, 1.0))));
-    y0 *= s0; y1 *= s0; y2 *= s0; y3 = s0;
-    bool done = false;
-#pragma unroll 1
-    for (int it = 0; it < kDltNormalIters && good && !done; ++it) done = dlt_inv_step(f, y0, y1, y2, y3) <= 1e-26;
-    if (!good) return 2;
-    if (!done) return 1;
-    return dlt_store_unit(y0, y1, y2, y3, Xout) ? 0 : 2;
-}
 
 // Listed observations: Householder QR of A (backward stable: no squaring of the
 // condition), then a three-vector block inverse iteration with R's triangular

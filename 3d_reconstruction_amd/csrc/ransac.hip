@@ -29,6 +29,7 @@
 //      RANSACUpdateNumIters — so the chosen model and the iteration count are
 //      exactly those of the sequential loop over the same models.
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 
 #include "common.h"
@@ -583,9 +584,10 @@ __device__ __forceinline__ int wave_sum(int v) {
 template <int NT = kRThreads>
 __device__ __forceinline__ void score_chunk(const double* __restrict__ q, int n, const int* s_list, int nlist,
                                             const double* s_models, int (*s_cnt)[NT / 64], float tf, double tlo,
-                                            double thi, int tid) {
+                                            double thi, int tid, int p_lo = 0, int p_hi = INT_MAX) {
     const int lane = tid & 63, wave = tid >> 6;
-    for (int b0 = 0; b0 < n; b0 += NT * kPB) {
+    n = min(n, p_hi);   // points [p_lo, p_hi): p_lo a multiple of NT * kPB
+    for (int b0 = p_lo; b0 < n; b0 += NT * kPB) {
         double pt[kPB][4];
         bool val[kPB];
 #pragma unroll
@@ -964,7 +966,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
     __shared__ int s_cnt[CH * kMaxModels][NW];
     __shared__ int s_list[CH * kMaxModels];
     __shared__ int s_good[CH * kMaxModels];
-    __shared__ int s_nlist, s_item;
+    __shared__ int s_act[CH * kMaxModels];
+    __shared__ int s_nlist, s_item, s_nact;
     const int tid = threadIdx.x, lane = tid & 63;
     const int h = tid / kGL, gl = tid % kGL, gsh = (lane / kGL) * kGL;
     const int2* list = B.list + (size_t)round * P * B.cmax;
@@ -1033,13 +1036,53 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
         }
         __syncthreads();
         const int nlist = s_nlist;
-        score_chunk<NT>(q, n, s_list, nlist, s_models, s_cnt, tf, tlo, thi, tid);
-        __syncthreads();
-        for (int e = tid; e < nlist; e += NT) {
-            int g = 0;
+        // Rounds >= 1: every model of this chunk is replayed after the previous rounds' replays, so
+        // one whose count cannot exceed max(their best, 4) never replaces the best and need not be
+        // counted exactly: after the first block of points, models whose count plus the points left
+        // is at most that bound drop out (s_good = -1: never a record; a later model it would have
+        // shadowed is recorded instead and rejected by the replay's own test).
+        const int bound = round > 0 ? max(B.st[p].maxgood, 4) : 4;
+        constexpr int blk = NT * kPB;
+        if (bound > 4 && n > blk && n - blk < bound) {
+            score_chunk<NT>(q, n, s_list, nlist, s_models, s_cnt, tf, tlo, thi, tid, 0, blk);
+            __syncthreads();
+            if (tid < 64) {   // wave 0: compact the live models (order kept) into s_act
+                int na = 0;
+                for (int b0 = 0; b0 < nlist; b0 += 64) {
+                    const int e = b0 + tid;
+                    bool live = false;
+                    if (e < nlist) {
+                        int g = 0;
 #pragma unroll
-            for (int w = 0; w < NW; ++w) g += s_cnt[s_list[e]][w];
-            s_good[e] = g;
+                        for (int w = 0; w < NW; ++w) g += s_cnt[s_list[e]][w];
+                        live = g + (n - blk) > bound;
+                        s_good[e] = live ? 0 : -1;
+                    }
+                    const unsigned long long bm = __ballot(live);
+                    if (live) s_act[na + __popcll(bm & ((1ULL << tid) - 1ULL))] = s_list[e];
+                    na += __popcll(bm);
+                }
+                if (tid == 0) s_nact = na;
+            }
+            __syncthreads();
+            score_chunk<NT>(q, n, s_act, s_nact, s_models, s_cnt, tf, tlo, thi, tid, blk);
+            __syncthreads();
+            for (int e = tid; e < nlist; e += NT) {
+                if (s_good[e] < 0) continue;
+                int g = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) g += s_cnt[s_list[e]][w];
+                s_good[e] = g;
+            }
+        } else {
+            score_chunk<NT>(q, n, s_list, nlist, s_models, s_cnt, tf, tlo, thi, tid);
+            __syncthreads();
+            for (int e = tid; e < nlist; e += NT) {
+                int g = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) g += s_cnt[s_list[e]][w];
+                s_good[e] = g;
+            }
         }
         __syncthreads();
         if (tid < 64) {   // records: strict prefix maxima above 4, by a running max over 64-entry blocks
@@ -1273,8 +1316,9 @@ __global__ __launch_bounds__(kPThreads) void recover_pose_kernel(
     const double* __restrict__ Ein, int64_t e_stride, const double* __restrict__ pts0,
     const double* __restrict__ pts1, const int64_t* __restrict__ offs, const double* __restrict__ cam,
     const uint8_t* __restrict__ mask_in, double dist, double* __restrict__ R_out, double* __restrict__ t_out,
-    uint8_t* __restrict__ mask_out, int32_t* __restrict__ good_out) {
+    uint8_t* __restrict__ mask_out, int32_t* __restrict__ good_out, int fast) {
     __shared__ double sP[4][12];
+    __shared__ double sPP[4][24];   // [P0 | P_k] contiguous, for dlt_point_normal
     __shared__ int s_cnt[4];
     __shared__ int s_sel;
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -1290,6 +1334,10 @@ __global__ __launch_bounds__(kPThreads) void recover_pose_kernel(
                 for (int c = 0; c < 3; ++c) sP[k][4 * r + c] = R[3 * r + c];
                 sP[k][4 * r + 3] = sg * t[r];
             }
+            for (int e = 0; e < 12; ++e) {
+                sPP[k][e] = (e % 5 == 0) ? 1.0 : 0.0;   // [I | 0]
+                sPP[k][12 + e] = sP[k][e];
+            }
             s_cnt[k] = 0;
         }
     }
@@ -1303,14 +1351,37 @@ __global__ __launch_bounds__(kPThreads) void recover_pose_kernel(
             const double x1 = (pts0[2 * (off + i)] - cx) / fx, y1 = (pts0[2 * (off + i) + 1] - cy) / fy;
             const double x2 = (pts1[2 * (off + i)] - cx) / fx, y2 = (pts1[2 * (off + i) + 1] - cy) / fy;
             for (int k = 0; k < 4; ++k) {
-                double Q[4];
-                dlt_point(P0, sP[k], x1, y1, x2, y2, Q);
-                bool ok = Q[2] * Q[3] > 0;
-                const double X = Q[0] / Q[3], Y = Q[1] / Q[3], Z = Q[2] / Q[3], W = Q[3] / Q[3];
-                ok = ok && Z < dist;
                 const double* P = sP[k];
-                const double z2 = ((P[8] * X + P[9] * Y) + P[10] * Z) + P[11] * W;
-                ok = ok && z2 > 0 && z2 < dist;
+                auto test = [&](const double* Q, bool& ok, double& scale) {
+                    ok = Q[2] * Q[3] > 0;
+                    const double X = Q[0] / Q[3], Y = Q[1] / Q[3], Z = Q[2] / Q[3], W = Q[3] / Q[3];
+                    ok = ok && Z < dist;
+                    const double z2 = ((P[8] * X + P[9] * Y) + P[10] * Z) + P[11] * W;
+                    ok = ok && z2 > 0 && z2 < dist;
+                    // distance of every tested quantity from its decision boundary, relative to
+                    // what a 1e-6 change of the unit null vector could move it
+                    const double aq3 = fabs(Q[3]);
+                    const double m = 4e-6 * (1.0 + fabs(X) + fabs(Y) + fabs(Z)) / fmax(aq3, 1e-300) *
+                                     (1.0 + fabs(P[8]) + fabs(P[9]) + fabs(P[10]) + fabs(P[11]));
+                    scale = fmin(fmin(fmin(fabs(Q[2]), aq3) * 1e6, fmin(fabs(Z), fabs(Z - dist)) / m),
+                                 fmin(fabs(z2), fabs(z2 - dist)) / m);
+                };
+                // the normal-equation fast path (geom_dev.h dlt_point_normal: null vector within
+                // ~1e-9 of the SVD's when it decides); dlt_point where it cannot decide or where a
+                // cheirality test lies within the fast path's error bound of its boundary, so the
+                // decisions are dlt_point's
+                double Q[4];
+                bool ok = false, sure = false;
+                if (fast && dlt_point_normal(sPP[k], x1, y1, x2, y2, Q) == 0) {
+                    double sc;
+                    test(Q, ok, sc);
+                    sure = sc > 1.0;
+                }
+                if (!sure) {
+                    double sc;
+                    dlt_point(P0, P, x1, y1, x2, y2, Q);
+                    test(Q, ok, sc);
+                }
                 code |= ok ? (1 << k) : 0;
             }
         }
@@ -1450,7 +1521,9 @@ extern "C" int sfmhip_recover_pose(const double* E, int64_t e_stride, const doub
     SFMHIP_REQUIRE(E && pts0 && pts1 && offsets && cam && R && t && mask_out && n_good,
                    "recover_pose: null pointer");
     SFMHIP_REQUIRE(e_stride >= 9, "recover_pose: e_stride >= 9");
+    const char* rpf = getenv("SFMHIP_RP_FAST");   // A/B: 0 = dlt_point for every triangulation
+    const int rp_fast = rpf && *rpf ? atoi(rpf) : 1;
     hipLaunchKernelGGL(recover_pose_kernel, dim3(n_pairs), dim3(kPThreads), 0, as_stream(stream), E, e_stride,
-                       pts0, pts1, offsets, cam, mask_in, distance_thresh, R, t, mask_out, n_good);
+                       pts0, pts1, offsets, cam, mask_in, distance_thresh, R, t, mask_out, n_good, rp_fast);
     return check_launch("recover_pose_kernel");
 }

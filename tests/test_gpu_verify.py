@@ -180,3 +180,27 @@ def test_balanced_bench_scene_matches_monolithic(sfm, gpu):
         for k in ("E", "n_models", "n_inliers", "iters", "mask"):
             assert np.array_equal(bal[k], mono[k]), (env, k)
     assert mono["iters"].max() > 64 and mono["iters"].min() >= 1   # round 1 exercised
+
+
+def test_recover_pose_fast_path_equals_dlt_point(sfm, gpu):
+    """recoverPose's normal-equation triangulations (certified against the cheirality boundaries,
+    dlt_point otherwise) give dlt_point's decisions: same R, t, masks and counts with
+    SFMHIP_RP_FAST=1 (default) and 0, on the bench scene's first 64 pairs and on noise-free pairs."""
+    import os
+    v = sfm.verify
+    for s in (syn.two_view_pairs(64, 2048, outlier_frac=0.3, noise_px=0.5, seed=6),
+              syn.two_view_pairs(8, 500, outlier_frac=0.0, noise_px=0.0, seed=12)):
+        a, b, of = v.pack_pairs(s["pts0"], s["pts1"])
+        cam = v._cam(s["K"])
+        r = v.find_essential_batched(a, b, of, cam)
+        outs = []
+        for fast in ("0", "1"):
+            os.environ["SFMHIP_RP_FAST"] = fast
+            try:
+                rp = v.recover_pose_batched(r["E"], a, b, of, cam, mask=r["mask"])
+                torch.cuda.synchronize()
+                outs.append({k: t.cpu().numpy() for k, t in rp.items()})
+            finally:
+                os.environ.pop("SFMHIP_RP_FAST", None)
+        for k in outs[0]:
+            assert np.array_equal(outs[0][k], outs[1][k]), k
