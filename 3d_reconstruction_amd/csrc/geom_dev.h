@@ -3,6 +3,7 @@
 // the cvTriangulatePoints DLT for one correspondence.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 
 namespace sfmhip {
 
@@ -500,5 +501,53 @@ __device__ __forceinline__ int dlt_point_normal(PT Pa, double xa, double ya, dou
     return dlt_store_unit(y0, y1, y2, y3, Xout) ? 0 : 2;
 }
 
+
+// ---------------------------------------------------------------------------
+// One RANSAC sample of 5 distinct indices in [0, n) from cv::RNG (multiply-with-carry
+// state s; uniform(0, n) = next() % n; a repeated index is redrawn), exactly as the
+// one-draw-at-a-time loop (ptsetreg.cpp getSubset) gives it.  The five draws are taken at
+// once — the state chain is one v_mad_u64_u32 per draw, x mod n is umulhi(x, mg) * n off by
+// at most one n (mg = floor(2^32 / n), n >= 2) — and only a duplicate (~0.5 % of samples at
+// n = 2048) falls back to drawing one at a time from the state after it.
+__device__ __forceinline__ unsigned cv_rng_mod(unsigned x, unsigned n, unsigned mg) {
+    const unsigned r = x - __umulhi(x, mg) * n;
+    return r >= n ? r - n : r;
+}
+__device__ __forceinline__ void cv_rng_sample5(uint64_t& s, unsigned n, unsigned mg, int (&d)[5]) {
+    constexpr uint64_t A = 4164903690ULL;
+    uint64_t st[5];
+    uint64_t sv = s;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        sv = (uint64_t)(unsigned)sv * A + (unsigned)(sv >> 32);
+        st[i] = sv;
+        d[i] = (int)cv_rng_mod((unsigned)sv, n, mg);
+    }
+    int j = 5;   // first draw that repeats an earlier one
+#pragma unroll
+    for (int i = 4; i >= 1; --i) {
+        bool dup = false;
+#pragma unroll
+        for (int t = 0; t < i; ++t) dup = dup || d[t] == d[i];
+        if (dup) j = i;
+    }
+    if (j == 5) {
+        s = st[4];
+        return;
+    }
+    sv = st[j];   // the duplicate draw is consumed; slot j onward one draw at a time
+    for (int i = j; i < 5; ++i) {
+        int idx;
+        for (;;) {
+            sv = (uint64_t)(unsigned)sv * A + (unsigned)(sv >> 32);
+            idx = (int)cv_rng_mod((unsigned)sv, n, mg);
+            bool dup = false;
+            for (int t = 0; t < i; ++t) dup = dup || d[t] == idx;
+            if (!dup) break;
+        }
+        d[i] = idx;
+    }
+    s = sv;
+}
 
 }  // namespace sfmhip

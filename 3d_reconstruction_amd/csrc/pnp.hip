@@ -18,6 +18,8 @@
 //   * the RANSAC pose is refined on the inliers by Levenberg-Marquardt with
 //     CvLevMarq's control flow; J^T J / J^T e are block reductions in a fixed
 //     order, the 6x6 damped system is solved by thread 0.
+#include <cstdlib>
+
 #include "common.h"
 #include "geom_dev.h"
 
@@ -339,8 +341,178 @@ __device__ unsigned long long g_wgt[2 * 1024];  // per-workgroup start / end
 #define PPROF_ADD(i, v) do {} while (0)
 #endif
 
+// Round-robin pair schedule of the 12x12 parallel Jacobi: round r pairs (11, r) and
+// ((r + k) mod 11, (r - k) mod 11), k = 1..5, each ordered p < q; entry r * 6 + k = p | q << 8.
+__device__ __forceinline__ void pnp_pair_table(unsigned short* pq, int tid) {
+    if (tid < 66) {
+        const int r = tid / 6, k = tid % 6;
+        int p, q;
+        if (k == 0) { p = 11; q = r; } else { p = (r + k) % 11; q = (r - k + 11) % 11; }
+        if (p > q) { const int t = p; p = q; q = t; }
+        pq[tid] = (unsigned short)(p | (q << 8));
+    }
+}
+
+// EPnP eigen-decomposition of M^T M (12x12, symmetric) by Householder tridiagonalisation and
+// the implicit QL iteration (EISPACK tred2 / tql2 form), on a kPnGL-lane group.  A (G[gA]) is
+// reduced in LDS, each lane owning rows gl and gl + 8; the reflector v and the update vector q
+// go through LDS (G[gRot], G[gL]); Q = H_0 ... H_9 is kept in registers (the lane's two rows).
+// The QL iteration runs on every lane of the group (d, e in registers, the same operations on
+// the same values) and each lane rotates its own rows of Q, so no rotation is broadcast.
+// Result as the Jacobi's: eigenvalues on A's diagonal, eigenvectors as the columns of V (G[gV]).
+__device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
+    double* A = G + gA;
+    double* vv = G + gRot;   // 12 doubles
+    double* qv = G + gL;     // 12 doubles
+    const int r0 = gl, r1 = gl + kPnGL;
+    const bool h1 = r1 < 12;
+    double z0[12], z1[12];   // rows r0 and r1 of Q
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        z0[j] = j == r0 ? 1.0 : 0.0;
+        z1[j] = j == r1 ? 1.0 : 0.0;
+    }
+    double d[12], e[12];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        // x = A[k+1..11][k]; |x|^2 over the group
+        const double a0 = r0 > k ? A[r0 * 12 + k] : 0.0;
+        const double a1 = h1 && r1 > k ? A[r1 * 12 + k] : 0.0;
+        double n2 = fma(a0, a0, a1 * a1);
+#pragma unroll
+        for (int o = kPnGL / 2; o > 0; o >>= 1) n2 += __shfl_xor(n2, o, kPnGL);
+        const double x0 = A[(k + 1) * 12 + k];
+        const double s2 = n2 - x0 * x0;
+        if (!(s2 > 1e-300 * n2) || !(n2 > 0.0)) {   // column already reduced (uniform in the group)
+            e[k] = x0;
+            continue;
+        }
+        const double alpha = x0 >= 0.0 ? -sqrt_nr(n2) : sqrt_nr(n2);
+        const double vk = x0 - alpha;
+        const double beta = 2.0 * rcp_nr(fma(vk, vk, s2));
+        e[k] = alpha;
+        const double v0 = r0 == k + 1 ? vk : a0;   // rows <= k: 0 (a0 = 0 there)
+        const double v1 = r1 == k + 1 ? vk : a1;
+        vv[r0] = v0;
+        if (h1) vv[r1] = v1;
+        lds_fence();
+        // p = beta A v on the trailing block; K = beta / 2 v.p
+        double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+        for (int j = k + 1; j < 12; ++j) {
+            const double vj = vv[j];
+            p0 = fma(A[r0 * 12 + j], vj, p0);
+            if (h1) p1 = fma(A[r1 * 12 + j], vj, p1);
+        }
+        p0 = r0 > k ? beta * p0 : 0.0;
+        p1 = h1 && r1 > k ? beta * p1 : 0.0;
+        double kk = fma(v0, p0, v1 * p1);
+#pragma unroll
+        for (int o = kPnGL / 2; o > 0; o >>= 1) kk += __shfl_xor(kk, o, kPnGL);
+        kk *= 0.5 * beta;
+        const double q0 = fma(-kk, v0, p0), q1 = fma(-kk, v1, p1);
+        qv[r0] = q0;
+        if (h1) qv[r1] = q1;
+        lds_fence();
+        // A <- A - v q^T - q v^T on the trailing block (own rows); Q <- Q H (own rows)
+        double w0 = 0.0, w1 = 0.0;
+#pragma unroll
+        for (int j = k + 1; j < 12; ++j) {
+            const double vj = vv[j], qj = qv[j];
+            if (r0 > k) A[r0 * 12 + j] = A[r0 * 12 + j] - fma(v0, qj, q0 * vj);
+            if (h1 && r1 > k) A[r1 * 12 + j] = A[r1 * 12 + j] - fma(v1, qj, q1 * vj);
+            w0 = fma(z0[j], vj, w0);
+            w1 = fma(z1[j], vj, w1);
+        }
+        w0 *= beta;
+        w1 *= beta;
+#pragma unroll
+        for (int j = k + 1; j < 12; ++j) {
+            const double vj = vv[j];
+            z0[j] = fma(-w0, vj, z0[j]);
+            z1[j] = fma(-w1, vj, z1[j]);
+        }
+        lds_fence();
+    }
+    e[10] = A[11 * 12 + 10];
+    e[11] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) d[i] = A[i * 13];
+    // implicit QL (tql2): e[i] couples d[i] and d[i + 1]
+    for (int l = 0; l < 12; ++l) {
+        for (int iter = 0; iter < 40; ++iter) {
+            int m = 11;
+#pragma unroll
+            for (int j = 10; j >= 0; --j) {
+                const double dd = fabs(d[j]) + fabs(d[j + 1]);
+                if (j >= l && fabs(e[j]) + dd == dd) m = j;
+            }
+            if (m <= l) break;
+            double dl = 0.0, dl1 = 0.0, el = 0.0, dm = 0.0;
+#pragma unroll
+            for (int j = 0; j < 12; ++j) {
+                if (j == l) { dl = d[j]; el = e[j]; }
+                if (j == l + 1) dl1 = d[j];
+                if (j == m) dm = d[j];
+            }
+            double g = (dl1 - dl) * (0.5 * rcp_nr(el));
+            double r = sqrt_nr(fma(g, g, 1.0));
+            g = dm - dl + el * rcp_nr(g + (g >= 0.0 ? r : -r));
+            double s = 1.0, c = 1.0, p = 0.0;
+            bool live = true;
+#pragma unroll
+            for (int i = 10; i >= 0; --i) {
+                if (!(live && i >= l && i < m)) continue;
+                const double f = s * e[i], b = c * e[i];
+                r = sqrt_nr(fma(f, f, g * g));
+                e[i + 1] = r;
+                if (r == 0.0) {   // underflow: deflate and restart this l
+                    d[i + 1] -= p;
+#pragma unroll
+                    for (int j = 0; j < 12; ++j)
+                        if (j == m) e[j] = 0.0;
+                    live = false;
+                    continue;
+                }
+                const double ir = rcp_nr(r);
+                s = f * ir;
+                c = g * ir;
+                g = d[i + 1] - p;
+                r = fma(d[i] - g, s, 2.0 * c * b);
+                p = s * r;
+                d[i + 1] = g + p;
+                g = fma(c, r, -b);
+                const double f0 = z0[i + 1], f1 = z1[i + 1];
+                z0[i + 1] = fma(s, z0[i], c * f0);
+                z0[i] = fma(c, z0[i], -s * f0);
+                z1[i + 1] = fma(s, z1[i], c * f1);
+                z1[i] = fma(c, z1[i], -s * f1);
+            }
+            if (live) {
+#pragma unroll
+                for (int j = 0; j < 12; ++j) {
+                    if (j == l) { d[j] -= p; e[j] = g; }
+                    if (j == m) e[j] = 0.0;
+                }
+            }
+        }
+    }
+    lds_fence();
+    if (gl == 0) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) A[i * 13] = d[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        G[gV + r0 * 12 + j] = z0[j];
+        if (h1) G[gV + r1 * 12 + j] = z1[j];
+    }
+    lds_fence();
+}
+
 // EPnP on 5 correspondences by a kPnGL-lane group; writes (rvec, tvec) to out[6].
-__device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
+__device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G, double* out,
+                                           const unsigned short* __restrict__ pq, bool ql) {
     PPROF_INIT;
     // M^T M (12x12) into A, V = I
     // (alphas and uc - u, vc - v were staged in G by prepare: a dynamic index into D would put
@@ -366,13 +538,17 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
     lds_fence();
     PPROF(7);
     // parallel-ordered two-sided Jacobi: 11 rounds of 6 disjoint pairs per sweep
-    auto pair_of = [](int rnd, int k, int& p, int& q) {
-        if (k == 0) { p = 11; q = rnd; } else { p = (rnd + k) % 11; q = (rnd - k + 11) % 11; }
-        if (p > q) { const int t = p; p = q; q = t; }
+    // the round's pairs from the workgroup's LDS table (pnp_pair_table: p | q << 8), not two
+    // modulo-11 divisions per block and round
+    auto pair_of = [&](int rnd, int k, int& p, int& q) {
+        const unsigned e = pq[rnd * 6 + k];
+        p = (int)(e & 255u);
+        q = (int)(e >> 8);
     };
     double* A = G + gA;
     double* V = G + gV;
-    for (int sweep = 0; sweep < 15; ++sweep) {
+    if (ql) epnp_eig_ql(gl, G);   // default (SFMHIP_PNP_EIG=0: the Jacobi below)
+    for (int sweep = 0; sweep < (ql ? 0 : 15); ++sweep) {
         // convergence: off-diagonal vs diagonal mass (group reduction; kJcN (18) elements per lane,
         // all loads issued before the sums)
         double av[kJcN];
@@ -610,7 +786,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
     const double* __restrict__ obj, const double* __restrict__ img, const int64_t* __restrict__ offs,
     const double* __restrict__ cam, int max_iters, double reproj, double confidence, float* __restrict__ wf,
     double* __restrict__ rvec_out, double* __restrict__ tvec_out, uint8_t* __restrict__ mask,
-    int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out) {
+    int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out, int eig_ql) {
     __shared__ double s_grp[kPnH * kPnGS];
     __shared__ double s_models[kPnH][6 + 9];  // rvec, tvec, R
     __shared__ int s_cnt[kPnH];
@@ -619,6 +795,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
     __shared__ double s_red[4 * 28];
     __shared__ double s_lm[6 + 6 + 27 + 9];   // param, prev, dRdr, R
     __shared__ int s_niters, s_maxgood, s_k0, s_last, s_flag;
+    __shared__ unsigned short s_pq[66];
 
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int h = tid / kPnGL, gl = tid % kPnGL;
@@ -634,6 +811,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         mask[off + i] = 0;
     }
     if (tid == 0) { s_niters = max(max_iters, 1); s_maxgood = 0; s_k0 = 0; s_last = -1; }
+    pnp_pair_table(s_pq, tid);
     __syncthreads();
     if (n < 5) {
         if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
@@ -701,7 +879,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
             EpnpData D;
             load_sample(idx, D);
             prepare(D, s_grp);
-            epnp_group(D, gl, s_grp, s_best);
+            epnp_group(D, gl, s_grp, s_best, s_pq, eig_ql != 0);
         }
         __syncthreads();
         if (tid == 0) {
@@ -712,23 +890,18 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         return;
     }
     CvRng rng{~0ULL};
-    const double inv_n = 1.0 / (double)n;
+    const unsigned mg = (unsigned)((1ULL << 32) / (unsigned)n);   // n > 5 here
     PPROF_INIT;
     for (;;) {
         const int k0 = s_k0, niters = s_niters;
-        if (tid == 0) {
+        if (tid == 0) {   // samples in registers (geom_dev.h cv_rng_sample5), then to LDS
             const int nh = min(kPnH, niters - k0);
-            for (int hh = 0; hh < nh; ++hh)
-                for (int i = 0; i < 5; ++i) {
-                    int idx;
-                    for (;;) {
-                        idx = rng.uniform0((unsigned)n, inv_n);
-                        int j = 0;
-                        while (j < i && s_sub[hh * 5 + j] != idx) ++j;
-                        if (j == i) break;
-                    }
-                    s_sub[hh * 5 + i] = idx;
-                }
+            for (int hh = 0; hh < nh; ++hh) {
+                int d[5];
+                cv_rng_sample5(rng.s, (unsigned)n, mg, d);
+#pragma unroll
+                for (int i = 0; i < 5; ++i) s_sub[hh * 5 + i] = d[i];
+            }
         }
         if (tid < kPnH) s_cnt[tid] = 0;
         __syncthreads();
@@ -741,7 +914,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
             double* G = s_grp + h * kPnGS;
             prepare(D, G);
             PPROF(6);
-            epnp_group(D, gl, G, s_models[h]);
+            epnp_group(D, gl, G, s_models[h], s_pq, eig_ql != 0);
             if (gl == 0) rodrigues(s_models[h], s_models[h] + 6);
         }
         __syncthreads();
@@ -953,8 +1126,11 @@ extern "C" int sfmhip_pnp_ransac(const double* obj, const double* img, const int
                    "pnp_ransac: null pointer");
     SFMHIP_REQUIRE(reprojection_error > 0 && confidence >= 0 && confidence <= 1,
                    "pnp_ransac: reprojection_error > 0, confidence in [0, 1]");
+    // EPnP's 12x12 eigen-decomposition: tridiagonal QL (default) or the parallel Jacobi (A/B)
+    const char* eg = getenv("SFMHIP_PNP_EIG");
+    const int eig_ql = eg && *eg ? atoi(eg) : 1;
     hipLaunchKernelGGL(pnp_ransac_kernel, dim3(n_problems), dim3(kPnThreads), 0, as_stream(stream), obj, img,
                        offsets, cam, iterations, reprojection_error, confidence, work, rvec, tvec, inlier_mask,
-                       n_inliers, iters, ok);
+                       n_inliers, iters, ok, eig_ql);
     return check_launch("pnp_ransac_kernel");
 }

@@ -850,59 +850,18 @@ __device__ void ess_gen(EssState& s, int p, int P, int round, const EssBufs& B) 
     int* cnt = B.ctr + 2 * round;
     const int target = round + 1 < kEssRounds ? min(s.niters, kSpecHyps << round) : s.niters;
     const unsigned n = (unsigned)s.n;
-    const double inv_n = 1.0 / (double)n;
-    CvRng rng{s.rng};
+    uint64_t rs = s.rng;
     int* smp = B.samp + (size_t)p * B.hcap * 5;
-    const uint64_t A = 4164903690ULL;
     const unsigned mg = (unsigned)((1ULL << 32) / n);   // n > 5
     for (int k = s.gen_upto; k < target; ++k) {
-        // five draws at once (the state chain is one multiply-add per draw; the reductions and
-        // the duplicate tests run beside it); a duplicate (~0.5 % of samples at n = 2048) redraws
-        // sequentially from the state after it, exactly as the one-at-a-time loop does
-        uint64_t st[5];
-        unsigned x[5];
-        uint64_t sv = rng.s;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            sv = (uint64_t)(unsigned)sv * A + (unsigned)(sv >> 32);
-            st[i] = sv;
-            x[i] = (unsigned)sv;
-        }
         int d[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {   // x mod n: umulhi(x, floor(2^32 / n)) is q or q - 1
-            const unsigned r = x[i] - __umulhi(x[i], mg) * n;
-            d[i] = (int)(r >= n ? r - n : r);
-        }
-        int j = 5;   // first draw that repeats an earlier one
-#pragma unroll
-        for (int i = 4; i >= 1; --i) {
-            bool dup = false;
-#pragma unroll
-            for (int t = 0; t < i; ++t) dup = dup || d[t] == d[i];
-            if (dup) j = i;
-        }
-        if (j == 5) {
-            rng.s = st[4];
-        } else {
-            rng.s = st[j];   // the duplicate draw is consumed; slot j onward one draw at a time
-            for (int i = j; i < 5; ++i) {
-                int idx;
-                for (;;) {
-                    idx = rng.uniform0(n, inv_n);
-                    bool dup = false;
-                    for (int t = 0; t < i; ++t) dup = dup || d[t] == idx;
-                    if (!dup) break;
-                }
-                d[i] = idx;
-            }
-        }
+        cv_rng_sample5(rs, n, mg, d);
 #pragma unroll
         for (int i = 0; i < 5; ++i) smp[5 * k + i] = d[i];
     }
     if (target > s.gen_upto) {
         s.gen_upto = target;
-        s.rng = rng.s;
+        s.rng = rs;
     }
     const int c0 = s.eval_upto / B.ch, c1 = (target + B.ch - 1) / B.ch;
     if (c1 > c0) {
