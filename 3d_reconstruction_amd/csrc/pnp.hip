@@ -919,19 +919,28 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         }
         __syncthreads();
         PPROF(1);
+        const int nh = min(kPnH, niters - k0);   // uniform
         for (int i0 = 0; i0 < n; i0 += kPnThreads) {
             const int i = i0 + tid;
             const bool valid = i < n;
             float X = 0, Y = 0, Z = 0, u = 0, v = 0;
             if (valid) { X = f[5 * i]; Y = f[5 * i + 1]; Z = f[5 * i + 2]; u = f[5 * i + 3]; v = f[5 * i + 4]; }
-            for (int hh = 0; hh < kPnH; ++hh) {
-                if (k0 + hh >= niters) break;
-                float pu, pv;
-                project_f(s_models[hh] + 6, s_models[hh] + 3, fx, fy, cx, cy, X, Y, Z, pu, pv);
-                const float du = u - pu, dv = v - pv;
-                const float e = du * du + dv * dv;
-                const int c = __popcll(__ballot(valid && e <= thr));
-                if (lane == 0 && c) atomicAdd(&s_cnt[hh], c);
+            // four models per step: independent projection chains (each with its IEEE division)
+            for (int h0 = 0; h0 < nh; h0 += 4) {
+                float e4[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int hh = min(h0 + q, nh - 1);
+                    float pu, pv;
+                    project_f(s_models[hh] + 6, s_models[hh] + 3, fx, fy, cx, cy, X, Y, Z, pu, pv);
+                    const float du = u - pu, dv = v - pv;
+                    e4[q] = du * du + dv * dv;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int c = __popcll(__ballot(valid && e4[q] <= thr));
+                    if (lane == 0 && c && h0 + q < nh) atomicAdd(&s_cnt[h0 + q], c);
+                }
             }
         }
         __syncthreads();
