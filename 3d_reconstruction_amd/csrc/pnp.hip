@@ -18,6 +18,7 @@
 //   * the RANSAC pose is refined on the inliers by Levenberg-Marquardt with
 //     CvLevMarq's control flow; J^T J / J^T e are block reductions in a fixed
 //     order, the 6x6 damped system is solved by thread 0.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -782,191 +783,82 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
     return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-__global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
-    const double* __restrict__ obj, const double* __restrict__ img, const int64_t* __restrict__ offs,
-    const double* __restrict__ cam, int max_iters, double reproj, double confidence, float* __restrict__ wf,
-    double* __restrict__ rvec_out, double* __restrict__ tvec_out, uint8_t* __restrict__ mask,
-    int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out, int eig_ql) {
-    __shared__ double s_grp[kPnH * kPnGS];
-    __shared__ double s_models[kPnH][6 + 9];  // rvec, tvec, R
-    __shared__ int s_cnt[kPnH];
-    __shared__ int s_sub[kPnH * 5];
-    __shared__ double s_best[6];
-    __shared__ double s_red[4 * 28];
-    __shared__ double s_lm[6 + 6 + 27 + 9];   // param, prev, dRdr, R
-    __shared__ int s_niters, s_maxgood, s_k0, s_last, s_flag;
-    __shared__ unsigned short s_pq[66];
+// One sample's correspondences (the float copies, as solvePnPRansac casts them) and intrinsics.
+__device__ __forceinline__ void pnp_load_sample(const float* __restrict__ f, const int* idx, double fx, double fy,
+                                                double cx, double cy, EpnpData& D) {
+    D.fu = fx; D.fv = fy; D.uc = cx; D.vc = cy;
+    for (int j = 0; j < 5; ++j) {
+        for (int k = 0; k < 3; ++k) D.pw[j][k] = (double)f[5 * idx[j] + k];
+        for (int k = 0; k < 2; ++k) D.us[j][k] = (double)f[5 * idx[j] + 3 + k];
+    }
+}
 
-    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const int h = tid / kPnGL, gl = tid % kPnGL;
-    PPROF_WG(0);
-    const int64_t off = offs[p];
-    const int n = (int)(offs[p + 1] - off);
-    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
-    const float thr = (float)(reproj * reproj);
-    float* f = wf + off * 5;  // float copies: X, Y, Z, u, v
-    for (int i = tid; i < n; i += kPnThreads) {
-        for (int k = 0; k < 3; ++k) f[5 * i + k] = (float)obj[3 * (off + i) + k];
-        for (int k = 0; k < 2; ++k) f[5 * i + 3 + k] = (float)img[2 * (off + i) + k];
-        mask[off + i] = 0;
+// EPnP control points and barycentric alphas (every lane of the group; lane 0 stages them in G).
+__device__ __forceinline__ void pnp_prepare(EpnpData& D, double* G, int gl) {
+    double c0[3] = {0, 0, 0};
+    for (int j = 0; j < 5; ++j)
+        for (int k = 0; k < 3; ++k) c0[k] += D.pw[j][k];
+    for (int k = 0; k < 3; ++k) c0[k] /= 5;
+    double A[3][3] = {}, w[3], E[3][3];
+    for (int j = 0; j < 5; ++j)
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) A[a][b] += (D.pw[j][a] - c0[a]) * (D.pw[j][b] - c0[b]);
+    eig3_desc(A, w, E);
+    double cws[4][3];
+    for (int k = 0; k < 3; ++k) cws[0][k] = c0[k];
+    for (int i = 1; i < 4; ++i) {
+        const double kk = sqrt(fmax(w[i - 1], 0.0) / 5);
+        for (int k = 0; k < 3; ++k) cws[i][k] = c0[k] + kk * E[i - 1][k];
     }
-    if (tid == 0) { s_niters = max(max_iters, 1); s_maxgood = 0; s_k0 = 0; s_last = -1; }
-    pnp_pair_table(s_pq, tid);
-    __syncthreads();
-    if (n < 5) {
-        if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
-        return;
+    if (gl == 0)
+        for (int i = 0; i < 4; ++i)
+            for (int k = 0; k < 3; ++k) G[gCws + 3 * i + k] = cws[i][k];
+    double CC[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 1; j < 4; ++j) CC[i][j - 1] = cws[j][i] - cws[0][i];
+    const double det = CC[0][0] * (CC[1][1] * CC[2][2] - CC[1][2] * CC[2][1]) -
+                       CC[0][1] * (CC[1][0] * CC[2][2] - CC[1][2] * CC[2][0]) +
+                       CC[0][2] * (CC[1][0] * CC[2][1] - CC[1][1] * CC[2][0]);
+    const double id = det != 0.0 ? 1.0 / det : 0.0;
+    double ci[3][3];
+    ci[0][0] = (CC[1][1] * CC[2][2] - CC[1][2] * CC[2][1]) * id;
+    ci[0][1] = (CC[0][2] * CC[2][1] - CC[0][1] * CC[2][2]) * id;
+    ci[0][2] = (CC[0][1] * CC[1][2] - CC[0][2] * CC[1][1]) * id;
+    ci[1][0] = (CC[1][2] * CC[2][0] - CC[1][0] * CC[2][2]) * id;
+    ci[1][1] = (CC[0][0] * CC[2][2] - CC[0][2] * CC[2][0]) * id;
+    ci[1][2] = (CC[0][2] * CC[1][0] - CC[0][0] * CC[1][2]) * id;
+    ci[2][0] = (CC[1][0] * CC[2][1] - CC[1][1] * CC[2][0]) * id;
+    ci[2][1] = (CC[0][1] * CC[2][0] - CC[0][0] * CC[2][1]) * id;
+    ci[2][2] = (CC[0][0] * CC[1][1] - CC[0][1] * CC[1][0]) * id;
+    for (int j = 0; j < 5; ++j) {
+        const double d0 = D.pw[j][0] - cws[0][0], d1 = D.pw[j][1] - cws[0][1], d2 = D.pw[j][2] - cws[0][2];
+        for (int a = 0; a < 3; ++a) D.al[j][1 + a] = ci[a][0] * d0 + ci[a][1] * d1 + ci[a][2] * d2;
+        D.al[j][0] = 1.0 - D.al[j][1] - D.al[j][2] - D.al[j][3];
     }
-    auto load_sample = [&](const int* idx, EpnpData& D) {
-        D.fu = fx; D.fv = fy; D.uc = cx; D.vc = cy;
+    if (gl == 0)
         for (int j = 0; j < 5; ++j) {
-            for (int k = 0; k < 3; ++k) D.pw[j][k] = (double)f[5 * idx[j] + k];
-            for (int k = 0; k < 2; ++k) D.us[j][k] = (double)f[5 * idx[j] + 3 + k];
+            for (int a = 0; a < 4; ++a) G[gAl + 4 * j + a] = D.al[j][a];
+            G[gUd + 2 * j] = D.uc - D.us[j][0];
+            G[gUd + 2 * j + 1] = D.vc - D.us[j][1];
         }
-    };
-    auto prepare = [&](EpnpData& D, double* G) {  // control points + alphas (every lane of the group)
-        double c0[3] = {0, 0, 0};
-        for (int j = 0; j < 5; ++j)
-            for (int k = 0; k < 3; ++k) c0[k] += D.pw[j][k];
-        for (int k = 0; k < 3; ++k) c0[k] /= 5;
-        double A[3][3] = {}, w[3], E[3][3];
-        for (int j = 0; j < 5; ++j)
-            for (int a = 0; a < 3; ++a)
-                for (int b = 0; b < 3; ++b) A[a][b] += (D.pw[j][a] - c0[a]) * (D.pw[j][b] - c0[b]);
-        eig3_desc(A, w, E);
-        double cws[4][3];
-        for (int k = 0; k < 3; ++k) cws[0][k] = c0[k];
-        for (int i = 1; i < 4; ++i) {
-            const double kk = sqrt(fmax(w[i - 1], 0.0) / 5);
-            for (int k = 0; k < 3; ++k) cws[i][k] = c0[k] + kk * E[i - 1][k];
-        }
-        if (gl == 0)
-            for (int i = 0; i < 4; ++i)
-                for (int k = 0; k < 3; ++k) G[gCws + 3 * i + k] = cws[i][k];
-        double CC[3][3];
-        for (int i = 0; i < 3; ++i)
-            for (int j = 1; j < 4; ++j) CC[i][j - 1] = cws[j][i] - cws[0][i];
-        const double det = CC[0][0] * (CC[1][1] * CC[2][2] - CC[1][2] * CC[2][1]) -
-                           CC[0][1] * (CC[1][0] * CC[2][2] - CC[1][2] * CC[2][0]) +
-                           CC[0][2] * (CC[1][0] * CC[2][1] - CC[1][1] * CC[2][0]);
-        const double id = det != 0.0 ? 1.0 / det : 0.0;
-        double ci[3][3];
-        ci[0][0] = (CC[1][1] * CC[2][2] - CC[1][2] * CC[2][1]) * id;
-        ci[0][1] = (CC[0][2] * CC[2][1] - CC[0][1] * CC[2][2]) * id;
-        ci[0][2] = (CC[0][1] * CC[1][2] - CC[0][2] * CC[1][1]) * id;
-        ci[1][0] = (CC[1][2] * CC[2][0] - CC[1][0] * CC[2][2]) * id;
-        ci[1][1] = (CC[0][0] * CC[2][2] - CC[0][2] * CC[2][0]) * id;
-        ci[1][2] = (CC[0][2] * CC[1][0] - CC[0][0] * CC[1][2]) * id;
-        ci[2][0] = (CC[1][0] * CC[2][1] - CC[1][1] * CC[2][0]) * id;
-        ci[2][1] = (CC[0][1] * CC[2][0] - CC[0][0] * CC[2][1]) * id;
-        ci[2][2] = (CC[0][0] * CC[1][1] - CC[0][1] * CC[1][0]) * id;
-        for (int j = 0; j < 5; ++j) {
-            const double d0 = D.pw[j][0] - cws[0][0], d1 = D.pw[j][1] - cws[0][1], d2 = D.pw[j][2] - cws[0][2];
-            for (int a = 0; a < 3; ++a) D.al[j][1 + a] = ci[a][0] * d0 + ci[a][1] * d1 + ci[a][2] * d2;
-            D.al[j][0] = 1.0 - D.al[j][1] - D.al[j][2] - D.al[j][3];
-        }
-        if (gl == 0)
-            for (int j = 0; j < 5; ++j) {
-                for (int a = 0; a < 4; ++a) G[gAl + 4 * j + a] = D.al[j][a];
-                G[gUd + 2 * j] = D.uc - D.us[j][0];
-                G[gUd + 2 * j + 1] = D.vc - D.us[j][1];
-            }
-        lds_fence();
-    };
-    if (n == 5) {  // model_points == npoints: solvePnP(EPnP) on all points, no refinement
-        if (h == 0) {
-            const int idx[5] = {0, 1, 2, 3, 4};
-            EpnpData D;
-            load_sample(idx, D);
-            prepare(D, s_grp);
-            epnp_group(D, gl, s_grp, s_best, s_pq, eig_ql != 0);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            for (int k = 0; k < 3; ++k) { rvec_out[3 * p + k] = s_best[k]; tvec_out[3 * p + k] = s_best[3 + k]; }
-            ok_out[p] = 1; ninl_out[p] = 5; iters_out[p] = 1;
-        }
-        if (tid < 5) mask[off + tid] = 1;
-        return;
-    }
-    CvRng rng{~0ULL};
-    const unsigned mg = (unsigned)((1ULL << 32) / (unsigned)n);   // n > 5 here
-    PPROF_INIT;
-    for (;;) {
-        const int k0 = s_k0, niters = s_niters;
-        if (tid == 0) {   // samples in registers (geom_dev.h cv_rng_sample5), then to LDS
-            const int nh = min(kPnH, niters - k0);
-            for (int hh = 0; hh < nh; ++hh) {
-                int d[5];
-                cv_rng_sample5(rng.s, (unsigned)n, mg, d);
-#pragma unroll
-                for (int i = 0; i < 5; ++i) s_sub[hh * 5 + i] = d[i];
-            }
-        }
-        if (tid < kPnH) s_cnt[tid] = 0;
-        __syncthreads();
-        PPROF(0);
-        const bool live = k0 + h < niters;
-        if (live) {
-            EpnpData D;
-            PPROF_INIT;
-            load_sample(s_sub + h * 5, D);
-            double* G = s_grp + h * kPnGS;
-            prepare(D, G);
-            PPROF(6);
-            epnp_group(D, gl, G, s_models[h], s_pq, eig_ql != 0);
-            if (gl == 0) rodrigues(s_models[h], s_models[h] + 6);
-        }
-        __syncthreads();
-        PPROF(1);
-        const int nh = min(kPnH, niters - k0);   // uniform
-        for (int i0 = 0; i0 < n; i0 += kPnThreads) {
-            const int i = i0 + tid;
-            const bool valid = i < n;
-            float X = 0, Y = 0, Z = 0, u = 0, v = 0;
-            if (valid) { X = f[5 * i]; Y = f[5 * i + 1]; Z = f[5 * i + 2]; u = f[5 * i + 3]; v = f[5 * i + 4]; }
-            // four models per step: independent projection chains (each with its IEEE division)
-            for (int h0 = 0; h0 < nh; h0 += 4) {
-                float e4[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int hh = min(h0 + q, nh - 1);
-                    float pu, pv;
-                    project_f(s_models[hh] + 6, s_models[hh] + 3, fx, fy, cx, cy, X, Y, Z, pu, pv);
-                    const float du = u - pu, dv = v - pv;
-                    e4[q] = du * du + dv * dv;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int c = __popcll(__ballot(valid && e4[q] <= thr));
-                    if (lane == 0 && c && h0 + q < nh) atomicAdd(&s_cnt[h0 + q], c);
-                }
-            }
-        }
-        __syncthreads();
-        PPROF(2);
-        if (tid == 0) {
-            int nit = niters, maxgood = s_maxgood, last = s_last;
-            for (int hh = 0; hh < kPnH; ++hh) {
-                const int k = k0 + hh;
-                if (k >= nit) break;
-                const int good = s_cnt[hh];
-                if (good > max(maxgood, 4)) {
-                    for (int e = 0; e < 6; ++e) s_best[e] = s_models[hh][e];
-                    maxgood = good;
-                    nit = update_num_iters(confidence, (double)(n - good) / n, 5, nit);
-                }
-                last = k;
-            }
-            s_niters = nit; s_maxgood = maxgood; s_last = last; s_k0 = k0 + kPnH;
-        }
-        __syncthreads();
-        if (s_k0 >= s_niters) break;
-    }
-    PPROF(3);
-    const int maxgood = s_maxgood;
+    lds_fence();
+}
+
+// After the RANSAC loop (best model s_best, maxgood inliers, last hypothesis run): the inlier mask
+// of the best model, CvLevMarq on the inliers (cvProjectPoints2's analytic Jacobian, J^T J / J^T e
+// as fixed-order block reductions), the outputs.  Every thread of the kPnThreads workgroup.
+__device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const float* __restrict__ f, double fx,
+                                           double fy, double cx, double cy, float thr, int maxgood, int last,
+                                           const double* s_best, double* s_lm, double* s_red,
+                                           uint8_t* __restrict__ mask, double* __restrict__ rvec_out,
+                                           double* __restrict__ tvec_out, int32_t* __restrict__ ninl_out,
+                                           int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out) {
+    const int tid = threadIdx.x;
+#ifdef SFMHIP_PNP_PROF
+    unsigned long long pp_t = wall_clock64();
+#endif
     if (maxgood <= 0) {
-        if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = s_last + 1; }
+        if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = last + 1; }
         return;
     }
     // inlier mask of the best model
@@ -1101,9 +993,400 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
     PPROF_WG(1);
     if (tid == 0) {
         for (int k = 0; k < 3; ++k) { rvec_out[3 * p + k] = prm[k]; tvec_out[3 * p + k] = prm[3 + k]; }
-        ok_out[p] = 1; ninl_out[p] = maxgood; iters_out[p] = s_last + 1;
+        ok_out[p] = 1; ninl_out[p] = maxgood; iters_out[p] = last + 1;
     }
+}
+
+__global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
+    const double* __restrict__ obj, const double* __restrict__ img, const int64_t* __restrict__ offs,
+    const double* __restrict__ cam, int max_iters, double reproj, double confidence, float* __restrict__ wf,
+    double* __restrict__ rvec_out, double* __restrict__ tvec_out, uint8_t* __restrict__ mask,
+    int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out, int eig_ql) {
+    __shared__ double s_grp[kPnH * kPnGS];
+    __shared__ double s_models[kPnH][6 + 9];  // rvec, tvec, R
+    __shared__ int s_cnt[kPnH];
+    __shared__ int s_sub[kPnH * 5];
+    __shared__ double s_best[6];
+    __shared__ double s_red[4 * 28];
+    __shared__ double s_lm[6 + 6 + 27 + 9];   // param, prev, dRdr, R
+    __shared__ int s_niters, s_maxgood, s_k0, s_last, s_flag;
+    __shared__ unsigned short s_pq[66];
+
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int h = tid / kPnGL, gl = tid % kPnGL;
+    PPROF_WG(0);
+    const int64_t off = offs[p];
+    const int n = (int)(offs[p + 1] - off);
+    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
+    const float thr = (float)(reproj * reproj);
+    float* f = wf + off * 5;  // float copies: X, Y, Z, u, v
+    for (int i = tid; i < n; i += kPnThreads) {
+        for (int k = 0; k < 3; ++k) f[5 * i + k] = (float)obj[3 * (off + i) + k];
+        for (int k = 0; k < 2; ++k) f[5 * i + 3 + k] = (float)img[2 * (off + i) + k];
+        mask[off + i] = 0;
+    }
+    if (tid == 0) { s_niters = max(max_iters, 1); s_maxgood = 0; s_k0 = 0; s_last = -1; }
+    pnp_pair_table(s_pq, tid);
+    __syncthreads();
+    if (n < 5) {
+        if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
+        return;
+    }
+    auto load_sample = [&](const int* idx, EpnpData& D) { pnp_load_sample(f, idx, fx, fy, cx, cy, D); };
+    auto prepare = [&](EpnpData& D, double* G) { pnp_prepare(D, G, gl); };
+    if (n == 5) {  // model_points == npoints: solvePnP(EPnP) on all points, no refinement
+        if (h == 0) {
+            const int idx[5] = {0, 1, 2, 3, 4};
+            EpnpData D;
+            load_sample(idx, D);
+            prepare(D, s_grp);
+            epnp_group(D, gl, s_grp, s_best, s_pq, eig_ql != 0);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int k = 0; k < 3; ++k) { rvec_out[3 * p + k] = s_best[k]; tvec_out[3 * p + k] = s_best[3 + k]; }
+            ok_out[p] = 1; ninl_out[p] = 5; iters_out[p] = 1;
+        }
+        if (tid < 5) mask[off + tid] = 1;
+        return;
+    }
+    CvRng rng{~0ULL};
+    const unsigned mg = (unsigned)((1ULL << 32) / (unsigned)n);   // n > 5 here
+    PPROF_INIT;
+    for (;;) {
+        const int k0 = s_k0, niters = s_niters;
+        if (tid == 0) {   // samples in registers (geom_dev.h cv_rng_sample5), then to LDS
+            const int nh = min(kPnH, niters - k0);
+            for (int hh = 0; hh < nh; ++hh) {
+                int d[5];
+                cv_rng_sample5(rng.s, (unsigned)n, mg, d);
+#pragma unroll
+                for (int i = 0; i < 5; ++i) s_sub[hh * 5 + i] = d[i];
+            }
+        }
+        if (tid < kPnH) s_cnt[tid] = 0;
+        __syncthreads();
+        PPROF(0);
+        const bool live = k0 + h < niters;
+        if (live) {
+            EpnpData D;
+            PPROF_INIT;
+            load_sample(s_sub + h * 5, D);
+            double* G = s_grp + h * kPnGS;
+            prepare(D, G);
+            PPROF(6);
+            epnp_group(D, gl, G, s_models[h], s_pq, eig_ql != 0);
+            if (gl == 0) rodrigues(s_models[h], s_models[h] + 6);
+        }
+        __syncthreads();
+        PPROF(1);
+        const int nh = min(kPnH, niters - k0);   // uniform
+        for (int i0 = 0; i0 < n; i0 += kPnThreads) {
+            const int i = i0 + tid;
+            const bool valid = i < n;
+            float X = 0, Y = 0, Z = 0, u = 0, v = 0;
+            if (valid) { X = f[5 * i]; Y = f[5 * i + 1]; Z = f[5 * i + 2]; u = f[5 * i + 3]; v = f[5 * i + 4]; }
+            // four models per step: independent projection chains (each with its IEEE division)
+            for (int h0 = 0; h0 < nh; h0 += 4) {
+                float e4[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int hh = min(h0 + q, nh - 1);
+                    float pu, pv;
+                    project_f(s_models[hh] + 6, s_models[hh] + 3, fx, fy, cx, cy, X, Y, Z, pu, pv);
+                    const float du = u - pu, dv = v - pv;
+                    e4[q] = du * du + dv * dv;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int c = __popcll(__ballot(valid && e4[q] <= thr));
+                    if (lane == 0 && c && h0 + q < nh) atomicAdd(&s_cnt[h0 + q], c);
+                }
+            }
+        }
+        __syncthreads();
+        PPROF(2);
+        if (tid == 0) {
+            int nit = niters, maxgood = s_maxgood, last = s_last;
+            for (int hh = 0; hh < kPnH; ++hh) {
+                const int k = k0 + hh;
+                if (k >= nit) break;
+                const int good = s_cnt[hh];
+                if (good > max(maxgood, 4)) {
+                    for (int e = 0; e < 6; ++e) s_best[e] = s_models[hh][e];
+                    maxgood = good;
+                    nit = update_num_iters(confidence, (double)(n - good) / n, 5, nit);
+                }
+                last = k;
+            }
+            s_niters = nit; s_maxgood = maxgood; s_last = last; s_k0 = k0 + kPnH;
+        }
+        __syncthreads();
+        if (s_k0 >= s_niters) break;
+    }
+    PPROF(3);
+    pnp_refine(p, n, off, f, fx, fy, cx, cy, thr, s_maxgood, s_last, s_best, s_lm, s_red, mask, rvec_out,
+               tvec_out, ninl_out, iters_out, ok_out);
     (void)s_flag;
+}
+
+
+// ---------------------------------------------------------------------------
+// Load-balanced form (default; SFMHIP_PNP_MONO=1 runs pnp_ransac_kernel).  With one workgroup per
+// problem the call lasts as long as its slowest problem: one that needs a second 32-hypothesis
+// chunk (33-37 iterations on the bench scene) runs the EPnP solves twice in a row, at one wave per
+// SIMD (the whole kernel's 454 VGPRs), scoring included.  Here the phases are separate kernels:
+//   pnp_init_kernel    float copies, per-problem state, outputs of n < 5, round 0's samples
+//                      (hypotheses up to min(niters, 32): one chunk);
+//   pnp_solve_kernel   persistent workgroups take (problem, chunk) items: the chunk's EPnP solves
+//                      (one workgroup per CU: 454 VGPRs and 115 KB of LDS per 32 hypotheses, so a
+//                      second chunk cannot run beside the first without halving both);
+//   pnp_score_kernel   each item's hypotheses scored on every correspondence (96 VGPRs: full
+//                      occupancy, where the one-workgroup kernel scored at one wave per SIMD);
+//   pnp_replay_kernel  one wave per problem replays the counts in OpenCV's order (a model
+//                      replaces the best iff count > max(best, 4); niters shrinks) and, unless the
+//                      problem is complete, draws round 1's samples up to the niters it left;
+//   pnp_final_kernel   the best model's inlier mask, CvLevMarq and the outputs (pnp_refine).
+// The same samples, solver, counts and replay as pnp_ransac_kernel: the same outputs; a
+// hypothesis past the final niters costs work, never a different result.
+constexpr int kPnSpecHyps = 32;   // round 0: one chunk per problem (the solve kernel holds one workgroup per CU)
+constexpr int kPnRounds = 2;
+constexpr int kPnFive = 1, kPnDone = 2;
+
+struct PnpState {
+    uint64_t rng;
+    int n, flags, niters, maxgood, gen_upto, eval_upto, rk, last, best_k;
+};
+
+struct PnpBufs {
+    PnpState* st;
+    int* samp;        // [P][hcap][5]
+    double* models;   // [P][hcap][15]: rvec, tvec, R
+    int* cnt;         // [P][hcap]
+    int2* list;       // [kPnRounds][P * cmax]: {problem, chunk (-1: the n == 5 call)}
+    int* ctr;         // [2 kPnRounds]: (count, head) per round
+    int cmax, hcap;
+};
+
+// One lane per problem: samples [gen_upto, target) in cv::RNG order, then the chunks covering them.
+__device__ void pnp_gen(PnpState& s, int p, int P, int round, const PnpBufs& B) {
+    const int target = round + 1 < kPnRounds ? min(s.niters, kPnSpecHyps) : s.niters;
+    const unsigned n = (unsigned)s.n;
+    const unsigned mg = (unsigned)((1ULL << 32) / n);   // n > 5
+    int* smp = B.samp + (size_t)p * B.hcap * 5;
+    for (int k = s.gen_upto; k < target; ++k) {
+        int d[5];
+        cv_rng_sample5(s.rng, n, mg, d);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) smp[5 * k + i] = d[i];
+    }
+    s.gen_upto = max(s.gen_upto, target);
+    const int c0 = s.eval_upto / kPnH, c1 = (target + kPnH - 1) / kPnH;
+    if (c1 > c0) {
+        int2* list = B.list + (size_t)round * P * B.cmax;
+        const int base = atomicAdd(B.ctr + 2 * round, c1 - c0);
+        for (int c = c0; c < c1; ++c) list[base + c - c0] = make_int2(p, c);
+        s.eval_upto = c1 * kPnH;
+    }
+}
+
+__global__ __launch_bounds__(kPnThreads) void pnp_init_kernel(const double* __restrict__ obj,
+                                                              const double* __restrict__ img,
+                                                              const int64_t* __restrict__ offs, int max_iters,
+                                                              float* __restrict__ wf, uint8_t* __restrict__ mask,
+                                                              int32_t* __restrict__ ninl_out,
+                                                              int32_t* __restrict__ iters_out,
+                                                              int32_t* __restrict__ ok_out, int P, PnpBufs B) {
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int64_t off = offs[p];
+    const int n = (int)(offs[p + 1] - off);
+    float* f = wf + off * 5;
+    for (int i = tid; i < n; i += kPnThreads) {
+        for (int k = 0; k < 3; ++k) f[5 * i + k] = (float)obj[3 * (off + i) + k];
+        for (int k = 0; k < 2; ++k) f[5 * i + 3 + k] = (float)img[2 * (off + i) + k];
+        mask[off + i] = 0;
+    }
+    if (tid == 0) {
+        PnpState s;
+        s.rng = ~0ULL;
+        s.n = n;
+        s.flags = n < 5 ? kPnDone : n == 5 ? kPnFive : 0;
+        s.niters = max(max_iters, 1);
+        s.maxgood = 0;
+        s.gen_upto = s.eval_upto = s.rk = 0;
+        s.last = s.best_k = -1;
+        if (n < 5) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
+        if (n == 5) B.list[atomicAdd(B.ctr, 1)] = make_int2(p, -1);
+        if (n > 5) pnp_gen(s, p, P, 0, B);
+        B.st[p] = s;
+    }
+}
+
+__global__ __launch_bounds__(kPnThreads) void pnp_solve_kernel(
+    int P, int round, const int64_t* __restrict__ offs, const double* __restrict__ cam,
+    const float* __restrict__ wf, double* __restrict__ rvec_out, double* __restrict__ tvec_out,
+    uint8_t* __restrict__ mask, int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out,
+    int32_t* __restrict__ ok_out, int eig_ql, PnpBufs B) {
+    __shared__ double s_grp[kPnH * kPnGS];
+    __shared__ double s_models[kPnH][6 + 9];
+    __shared__ unsigned short s_pq[66];
+    __shared__ int s_item, s_five[5];
+    const int tid = threadIdx.x, h = tid / kPnGL, gl = tid % kPnGL;
+    pnp_pair_table(s_pq, tid);
+    if (tid < 5) s_five[tid] = tid;
+    const int2* list = B.list + (size_t)round * P * B.cmax;
+    const int count = B.ctr[2 * round];
+    for (;;) {
+        if (tid == 0) s_item = atomicAdd(B.ctr + 2 * round + 1, 1);
+        __syncthreads();
+        const int it = s_item;
+        if (it >= count) break;
+        const int p = list[it].x, c = list[it].y;
+        const int64_t off = offs[p];
+        const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
+        const float* f = wf + off * 5;
+        // c < 0: model_points == npoints, solvePnP(EPnP) on all points (group 0), no refinement.
+        // One call site of the solver for both kinds of item (one inlined copy of it).
+        const bool five = c < 0;
+        const int k = five ? 0 : c * kPnH + h;
+        if (five ? h == 0 : k < B.st[p].gen_upto) {
+            EpnpData D;
+            pnp_load_sample(f, five ? s_five : B.samp + ((size_t)p * B.hcap + k) * 5, fx, fy, cx, cy, D);
+            double* G = s_grp + h * kPnGS;
+            pnp_prepare(D, G, gl);
+            epnp_group(D, gl, G, s_models[h], s_pq, eig_ql != 0);
+            if (gl == 0 && !five) rodrigues(s_models[h], s_models[h] + 6);
+            lds_fence();
+            if (!five) {
+                double* mo = B.models + ((size_t)p * B.hcap + k) * 15;
+                mo[gl] = s_models[h][gl];
+                if (gl + kPnGL < 15) mo[gl + kPnGL] = s_models[h][gl + kPnGL];
+            }
+        }
+        __syncthreads();
+        if (five) {
+            if (tid == 0) {
+                for (int q = 0; q < 3; ++q) { rvec_out[3 * p + q] = s_models[0][q]; tvec_out[3 * p + q] = s_models[0][3 + q]; }
+                ok_out[p] = 1; ninl_out[p] = 5; iters_out[p] = 1;
+            }
+            if (tid < 5) mask[off + tid] = 1;
+            __syncthreads();
+        }
+    }
+}
+
+// One item per workgroup pass: the chunk's models against every correspondence, four per step.
+__global__ __launch_bounds__(kPnThreads) void pnp_score_kernel(int P, int round, const int64_t* __restrict__ offs,
+                                                               const double* __restrict__ cam, double reproj,
+                                                               const float* __restrict__ wf, PnpBufs B) {
+    __shared__ double s_m[kPnH][15];
+    __shared__ int s_cnt[kPnH];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int2* list = B.list + (size_t)round * P * B.cmax;
+    const int count = B.ctr[2 * round];
+    const float thr = (float)(reproj * reproj);
+    for (int it = blockIdx.x; it < count; it += gridDim.x) {
+        const int p = list[it].x, c = list[it].y;
+        if (c < 0) continue;   // uniform
+        const int64_t off = offs[p];
+        const int n = B.st[p].n;
+        const int nh = min(kPnH, B.st[p].gen_upto - c * kPnH);
+        const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
+        const float* f = wf + off * 5;
+        const double* mo = B.models + ((size_t)p * B.hcap + c * kPnH) * 15;
+        for (int e = tid; e < nh * 15; e += kPnThreads) s_m[e / 15][e % 15] = mo[e];
+        if (tid < kPnH) s_cnt[tid] = 0;
+        __syncthreads();
+        for (int i0 = 0; i0 < n; i0 += kPnThreads) {
+            const int i = i0 + tid;
+            const bool valid = i < n;
+            float X = 0, Y = 0, Z = 0, u = 0, v = 0;
+            if (valid) { X = f[5 * i]; Y = f[5 * i + 1]; Z = f[5 * i + 2]; u = f[5 * i + 3]; v = f[5 * i + 4]; }
+            for (int h0 = 0; h0 < nh; h0 += 4) {
+                float e4[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int hh = min(h0 + q, nh - 1);
+                    float pu, pv;
+                    project_f(s_m[hh] + 6, s_m[hh] + 3, fx, fy, cx, cy, X, Y, Z, pu, pv);
+                    const float du = u - pu, dv = v - pv;
+                    e4[q] = du * du + dv * dv;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int cq = __popcll(__ballot(valid && e4[q] <= thr));
+                    if (lane == 0 && cq && h0 + q < nh) atomicAdd(&s_cnt[h0 + q], cq);
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < nh) B.cnt[(size_t)p * B.hcap + c * kPnH + tid] = s_cnt[tid];
+        __syncthreads();
+    }
+}
+
+// One wave per problem: the counts of the listed hypotheses staged in LDS, lane 0 replays them.
+__global__ __launch_bounds__(64) void pnp_replay_kernel(int P, int round, double confidence, PnpBufs B) {
+    __shared__ int s_c[256];
+    const int p = blockIdx.x, lane = threadIdx.x;
+    PnpState s = B.st[p];
+    if (s.flags & (kPnFive | kPnDone)) return;   // uniform
+    int nit = s.niters, k = s.rk;
+    bool done = false;
+    while (k < s.eval_upto && k < nit && !done) {   // windows of 256 hypotheses
+        const int w = min(256, s.eval_upto - k);
+        for (int t = lane; t < w; t += 64) s_c[t] = B.cnt[(size_t)p * B.hcap + k + t];
+        __syncthreads();
+        if (lane == 0) {
+            int t = 0;
+            for (; t < w; ++t) {
+                if (k + t >= nit) { done = true; break; }
+                const int good = s_c[t];
+                if (good > max(s.maxgood, 4)) {
+                    s.best_k = k + t;
+                    s.maxgood = good;
+                    nit = update_num_iters(confidence, (double)(s.n - good) / s.n, 5, nit);
+                }
+                s.last = k + t;
+            }
+            s_c[0] = t | (done ? 1 << 30 : 0);
+        }
+        __syncthreads();
+        const int r = s_c[0];
+        done = (r >> 30) & 1;
+        k += r & ((1 << 30) - 1);
+        nit = __shfl(nit, 0);
+        __syncthreads();
+    }
+    if (lane != 0) return;
+    s.rk = k;
+    s.niters = nit;
+    if (done || k >= nit) s.flags |= kPnDone;
+    else if (round + 1 < kPnRounds) pnp_gen(s, p, P, round + 1, B);
+    B.st[p] = s;
+}
+
+__global__ __launch_bounds__(kPnThreads) void pnp_final_kernel(const int64_t* __restrict__ offs,
+                                                               const double* __restrict__ cam, double reproj,
+                                                               const float* __restrict__ wf,
+                                                               double* __restrict__ rvec_out,
+                                                               double* __restrict__ tvec_out,
+                                                               uint8_t* __restrict__ mask,
+                                                               int32_t* __restrict__ ninl_out,
+                                                               int32_t* __restrict__ iters_out,
+                                                               int32_t* __restrict__ ok_out, PnpBufs B) {
+    __shared__ double s_best[6];
+    __shared__ double s_red[4 * 28];
+    __shared__ double s_lm[6 + 6 + 27 + 9];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const PnpState s = B.st[p];
+    if (s.n <= 5) return;   // n < 5: ess_init; n == 5: the solve kernel
+    if (s.maxgood > 0 && tid < 6) s_best[tid] = B.models[((size_t)p * B.hcap + s.best_k) * 15 + tid];
+    __syncthreads();
+    const int64_t off = offs[p];
+    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
+    pnp_refine(p, s.n, off, wf + off * 5, fx, fy, cx, cy, (float)(reproj * reproj), s.maxgood, s.last, s_best,
+               s_lm, s_red, mask, rvec_out, tvec_out, ninl_out, iters_out, ok_out);
 }
 
 }  // namespace
@@ -1138,8 +1421,61 @@ extern "C" int sfmhip_pnp_ransac(const double* obj, const double* img, const int
     // EPnP's 12x12 eigen-decomposition: tridiagonal QL (default) or the parallel Jacobi (A/B)
     const char* eg = getenv("SFMHIP_PNP_EIG");
     const int eig_ql = eg && *eg ? atoi(eg) : 1;
-    hipLaunchKernelGGL(pnp_ransac_kernel, dim3(n_problems), dim3(kPnThreads), 0, as_stream(stream), obj, img,
-                       offsets, cam, iterations, reprojection_error, confidence, work, rvec, tvec, inlier_mask,
-                       n_inliers, iters, ok, eig_ql);
-    return check_launch("pnp_ransac_kernel");
+    hipStream_t st = as_stream(stream);
+    const char* mo = getenv("SFMHIP_PNP_MONO");   // A/B: one workgroup per problem
+    if (mo && *mo && atoi(mo) != 0) {
+        hipLaunchKernelGGL(pnp_ransac_kernel, dim3(n_problems), dim3(kPnThreads), 0, st, obj, img, offsets, cam,
+                           iterations, reprojection_error, confidence, work, rvec, tvec, inlier_mask, n_inliers, iters,
+                           ok, eig_ql);
+        return check_launch("pnp_ransac_kernel");
+    }
+    const int cmax = ceil_div(std::max(iterations, 1), kPnH), hcap = cmax * kPnH;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t per = sizeof(PnpState) + (size_t)hcap * (5 * sizeof(int) + 15 * sizeof(double) + sizeof(int)) +
+                       kPnRounds * (size_t)cmax * sizeof(int2);
+    const int batch = (int)std::max<int64_t>(1, std::min<int64_t>(n_problems, ((size_t)192 << 20) / per));
+    const size_t bytes = al(batch * sizeof(PnpState)) + al((size_t)batch * hcap * 5 * sizeof(int)) +
+                         al((size_t)batch * hcap * 15 * sizeof(double)) + al((size_t)batch * hcap * sizeof(int)) +
+                         al(kPnRounds * (size_t)batch * cmax * sizeof(int2)) + al(2 * kPnRounds * sizeof(int));
+    char* base = nullptr;
+    if (scratch_alloc((void**)&base, bytes, st) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("pnp_ransac: scratch allocation of %zu bytes failed", bytes);
+        return SFMHIP_E_HIP;
+    }
+    PnpBufs B;
+    char* cur = base;
+    auto carve = [&](size_t b) { char* r = cur; cur += al(b); return r; };
+    B.st = (PnpState*)carve(batch * sizeof(PnpState));
+    B.samp = (int*)carve((size_t)batch * hcap * 5 * sizeof(int));
+    B.models = (double*)carve((size_t)batch * hcap * 15 * sizeof(double));
+    B.cnt = (int*)carve((size_t)batch * hcap * sizeof(int));
+    B.list = (int2*)carve(kPnRounds * (size_t)batch * cmax * sizeof(int2));
+    B.ctr = (int*)carve(2 * kPnRounds * sizeof(int));
+    B.cmax = cmax;
+    B.hcap = hcap;
+    int rc = SFMHIP_OK;
+    for (int p0 = 0; p0 < n_problems && rc == SFMHIP_OK; p0 += batch) {
+        const int PB = std::min(batch, n_problems - p0);
+        const int64_t* of = offsets + p0;
+        const double* cm = cam + 4 * (size_t)p0;
+        double *rv = rvec + 3 * (size_t)p0, *tv = tvec + 3 * (size_t)p0;
+        int32_t *nib = n_inliers + p0, *itb = iters + p0, *okb = ok + p0;
+        (void)hipMemsetAsync(B.ctr, 0, 2 * kPnRounds * sizeof(int), st);
+        hipLaunchKernelGGL(pnp_init_kernel, dim3(PB), dim3(kPnThreads), 0, st, obj, img, of, iterations, work,
+                           inlier_mask, nib, itb, okb, PB, B);
+        for (int round = 0; round < kPnRounds; ++round) {
+            const int items = (int)std::min<int64_t>((int64_t)PB * (round == 0 ? std::min(cmax, ceil_div(kPnSpecHyps, kPnH)) : cmax), 1 << 30);
+            hipLaunchKernelGGL(pnp_solve_kernel, dim3(std::min(items, 512)), dim3(kPnThreads), 0, st, PB, round, of,
+                               cm, work, rv, tv, inlier_mask, nib, itb, okb, eig_ql, B);
+            hipLaunchKernelGGL(pnp_score_kernel, dim3(std::min(items, 2048)), dim3(kPnThreads), 0, st, PB, round, of,
+                               cm, reprojection_error, work, B);
+            hipLaunchKernelGGL(pnp_replay_kernel, dim3(PB), dim3(64), 0, st, PB, round, confidence, B);
+        }
+        hipLaunchKernelGGL(pnp_final_kernel, dim3(PB), dim3(kPnThreads), 0, st, of, cm, reprojection_error, work, rv,
+                           tv, inlier_mask, nib, itb, okb, B);
+        rc = check_launch("pnp_*_kernel");
+    }
+    scratch_free(base, st);
+    return rc;
 }
