@@ -1132,7 +1132,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
 
 
 // ---------------------------------------------------------------------------
-// Load-balanced form (default; SFMHIP_PNP_MONO=1 runs pnp_ransac_kernel).  With one workgroup per
+// Phase-split form (SFMHIP_PNP_MONO=0; the default is pnp_ransac_kernel).  With one workgroup per
 // problem the call lasts as long as its slowest problem: one that needs a second 32-hypothesis
 // chunk (33-37 iterations on the bench scene) runs the EPnP solves twice in a row, at one wave per
 // SIMD (the whole kernel's 454 VGPRs), scoring included.  Here the phases are separate kernels:
@@ -1422,8 +1422,8 @@ extern "C" int sfmhip_pnp_ransac(const double* obj, const double* img, const int
     const char* eg = getenv("SFMHIP_PNP_EIG");
     const int eig_ql = eg && *eg ? atoi(eg) : 1;
     hipStream_t st = as_stream(stream);
-    const char* mo = getenv("SFMHIP_PNP_MONO");   // A/B: one workgroup per problem
-    if (mo && *mo && atoi(mo) != 0) {
+    const char* mo = getenv("SFMHIP_PNP_MONO");   // 1 (default): one workgroup per problem; 0: phase-split
+    if (!(mo && *mo && atoi(mo) == 0)) {
         hipLaunchKernelGGL(pnp_ransac_kernel, dim3(n_problems), dim3(kPnThreads), 0, st, obj, img, offsets, cam,
                            iterations, reprojection_error, confidence, work, rvec, tvec, inlier_mask, n_inliers, iters,
                            ok, eig_ql);

@@ -105,7 +105,7 @@ def test_pnp_eigensolvers_same_outcome(sfm, gpu):
 
 def test_pnp_balanced_equals_monolithic(sfm, gpu):
     """The phase-split form (solve / score / replay / refine kernels over (problem, chunk) items)
-    gives the same bits as the one-workgroup-per-problem kernel (SFMHIP_PNP_MONO=1): ragged
+    (SFMHIP_PNP_MONO=0) gives the same bits as the one-workgroup-per-problem kernel: ragged
     problems incl. n < 5, n == 5, all-outlier and bench-sized ones, and iteration caps."""
     import os
     import torch
