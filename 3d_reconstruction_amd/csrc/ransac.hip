@@ -645,6 +645,113 @@ __device__ __forceinline__ void score_chunk(const double* __restrict__ q, int n,
     }
 }
 
+// The f64 decision of one (model, point) pair: essential_ransac_kernel's margin tests around the
+// largest double that rounds to a float <= t, and the exact division where they cannot decide.
+__device__ __forceinline__ bool sampson_in_f64(const double* E, const double (&pt)[4], float tf, double tlo,
+                                               double thi) {
+    double nm, dn;
+    sampson_nd(E, pt[0], pt[1], pt[2], pt[3], nm, dn);
+    if (dn > 0 && nm <= dn * tlo) return true;
+    if (dn > 0 && nm > dn * thi) return false;
+    return (float)(nm / dn) <= tf;
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v f2b(float a) { return f2v{a, a}; }
+__device__ __forceinline__ f2v fma2v(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+
+// score_chunk with a packed-f32 pre-test (the load-balanced chunk kernel).  Two points per
+// instruction: Ex1, E^T x2, d = x2^T E x1 and den in f32 FMA arithmetic from the f32-rounded
+// points and model (|E_ij| <= 1: unit Frobenius norm).  With a = 1 + |x1| + |y1|, b = 1 + |x2| + |y2|
+// (u = 2^-24) every f32 ex/et is within 4.01 u a (b) of its exact value, d within 7.1 u a b and
+// den within 24.2 u (a^2 + b^2); the bounds used are 12 u a b and 32 u (a^2 + b^2).  A point is
+// surely in when (|d| + dd)^2 <= T (1 - 2^-20) (den - dden) and surely out when
+// (|d| - dd)^2 > T (1 + 2^-20) (den + dden), T the largest double rounding to a float <= t: the
+// margins cover the test's own f32 rounding (< 2^-22) and the f64 path's (~1e-15), so a sure
+// decision is the f64 decision.  Every other pair takes sampson_in_f64 (its own lanes only).
+template <int NT>
+__device__ __forceinline__ void score_chunk_f32(const double* __restrict__ q, int n, const int* s_list, int nlist,
+                                                const double* s_models, const float* s_models32,
+                                                int (*s_cnt)[NT / 64], float tf, double Tmax, double tlo,
+                                                double thi, int tid, int p_lo = 0, int p_hi = INT_MAX) {
+    static_assert(kPB % 2 == 0, "points are processed in pairs");
+    constexpr int NP = kPB / 2;
+    constexpr float u24 = 0x1p-24f;
+    const float Tl = (float)(Tmax * (1.0 - 0x1p-20)), Th = (float)(Tmax * (1.0 + 0x1p-20));
+    const int lane = tid & 63, wave = tid >> 6;
+    n = min(n, p_hi);
+    for (int b0 = p_lo; b0 < n; b0 += NT * kPB) {
+        double pt[kPB][4];
+        bool val[kPB];
+#pragma unroll
+        for (int u = 0; u < kPB; ++u) {
+            const int i = b0 + u * NT + tid;
+            val[u] = i < n;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) pt[u][c] = val[u] ? q[4 * i + c] : 0.0;
+        }
+        f2v X1[NP], Y1[NP], X2[NP], Y2[NP], DD[NP], DN[NP];
+#pragma unroll
+        for (int v = 0; v < NP; ++v) {
+            X1[v] = f2v{(float)pt[2 * v][0], (float)pt[2 * v + 1][0]};
+            Y1[v] = f2v{(float)pt[2 * v][1], (float)pt[2 * v + 1][1]};
+            X2[v] = f2v{(float)pt[2 * v][2], (float)pt[2 * v + 1][2]};
+            Y2[v] = f2v{(float)pt[2 * v][3], (float)pt[2 * v + 1][3]};
+            const f2v a = f2b(1.0f) + __builtin_elementwise_abs(X1[v]) + __builtin_elementwise_abs(Y1[v]);
+            const f2v b = f2b(1.0f) + __builtin_elementwise_abs(X2[v]) + __builtin_elementwise_abs(Y2[v]);
+            DD[v] = f2b(12.0f * u24) * (a * b);
+            DN[v] = f2b(32.0f * u24) * fma2v(a, a, b * b);
+        }
+        for (int j = 0; j < nlist; j += 2) {   // two models per step: independent chains
+            const int mm[2] = {s_list[j], s_list[min(j + 1, nlist - 1)]};
+            bool in[2][kPB], amb[2][kPB];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                float E[9];
+#pragma unroll
+                for (int e = 0; e < 9; ++e) E[e] = s_models32[mm[k] * 9 + e];
+#pragma unroll
+                for (int v = 0; v < NP; ++v) {
+                    const f2v ex0 = fma2v(f2b(E[0]), X1[v], fma2v(f2b(E[1]), Y1[v], f2b(E[2])));
+                    const f2v ex1 = fma2v(f2b(E[3]), X1[v], fma2v(f2b(E[4]), Y1[v], f2b(E[5])));
+                    const f2v ex2 = fma2v(f2b(E[6]), X1[v], fma2v(f2b(E[7]), Y1[v], f2b(E[8])));
+                    const f2v et0 = fma2v(f2b(E[0]), X2[v], fma2v(f2b(E[3]), Y2[v], f2b(E[6])));
+                    const f2v et1 = fma2v(f2b(E[1]), X2[v], fma2v(f2b(E[4]), Y2[v], f2b(E[7])));
+                    const f2v d = fma2v(X2[v], ex0, fma2v(Y2[v], ex1, ex2));
+                    const f2v den = fma2v(ex0, ex0, fma2v(ex1, ex1, fma2v(et0, et0, et1 * et1)));
+                    const f2v ad = __builtin_elementwise_abs(d);
+                    const f2v up = ad + DD[v], lo = ad - DD[v];
+                    const f2v dl = den - DN[v], dh = den + DN[v];
+                    const f2v lhs_in = up * up, rhs_in = f2b(Tl) * dl;
+                    const f2v lhs_out = lo * lo, rhs_out = f2b(Th) * dh;
+#pragma unroll
+                    for (int w = 0; w < 2; ++w) {
+                        const bool sin = dl[w] > 0.0f && lhs_in[w] <= rhs_in[w];
+                        const bool sout = lo[w] > 0.0f && lhs_out[w] > rhs_out[w];
+                        in[k][2 * v + w] = sin;
+                        amb[k][2 * v + w] = !(sin || sout);
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int u = 0; u < kPB; ++u)
+                    if (amb[k][u]) in[k][u] = sampson_in_f64(s_models + mm[k] * 9, pt[u], tf, tlo, thi);
+            int ca = 0, cb = 0;  // wave-uniform: ballots + scalar popcounts
+#pragma unroll
+            for (int u = 0; u < kPB; ++u) {
+                ca += wave_count(val[u] && in[0][u]);
+                cb += wave_count(val[u] && in[1][u]);
+            }
+            if (lane == 0) {
+                s_cnt[mm[0]][wave] += ca;
+                if (j + 1 < nlist) s_cnt[mm[1]][wave] += cb;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
     const double* __restrict__ pts0, const double* __restrict__ pts1, const int64_t* __restrict__ offs,
     const double* __restrict__ cam, double prob, double threshold, int max_iters, double* __restrict__ qn,
@@ -917,10 +1024,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
                                                               int32_t* __restrict__ nmodels_out,
                                                               uint8_t* __restrict__ mask,
                                                               int32_t* __restrict__ ninl_out,
-                                                              int32_t* __restrict__ iters_out, EssBufs B) {
+                                                              int32_t* __restrict__ iters_out, int f32pre, EssBufs B) {
     constexpr int CH = NT / kGL, NW = NT / 64;
     __shared__ double s_grp[CH * kGS];
     __shared__ double s_models[CH * kMaxModels * 9];
+    __shared__ float s_models32[CH * kMaxModels * 9];   // f32 copies for the packed pre-test
     __shared__ int s_nmod[CH];
     __shared__ int s_cnt[CH * kMaxModels][NW];
     __shared__ int s_list[CH * kMaxModels];
@@ -993,8 +1101,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
                 for (int m = 0; m < s_nmod[hh]; ++m) s_list[cn++] = hh * kMaxModels + m;
             s_nlist = cn;
         }
+        for (int e = tid; e < CH * kMaxModels * 9; e += NT) s_models32[e] = (float)s_models[e];
         __syncthreads();
         const int nlist = s_nlist;
+        auto score = [&](const int* lst, int nl, int lo, int hi) {
+            if (f32pre)
+                score_chunk_f32<NT>(q, n, lst, nl, s_models, s_models32, s_cnt, tf, Tmax, tlo, thi, tid, lo, hi);
+            else
+                score_chunk<NT>(q, n, lst, nl, s_models, s_cnt, tf, tlo, thi, tid, lo, hi);
+        };
         // Rounds >= 1: every model of this chunk is replayed after the previous rounds' replays, so
         // one whose count cannot exceed max(their best, 4) never replaces the best and need not be
         // counted exactly: after the first block of points, models whose count plus the points left
@@ -1003,7 +1118,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
         const int bound = round > 0 ? max(B.st[p].maxgood, 4) : 4;
         constexpr int blk = NT * kPB;
         if (bound > 4 && n > blk && n - blk < bound) {
-            score_chunk<NT>(q, n, s_list, nlist, s_models, s_cnt, tf, tlo, thi, tid, 0, blk);
+            score(s_list, nlist, 0, blk);
             __syncthreads();
             if (tid < 64) {   // wave 0: compact the live models (order kept) into s_act
                 int na = 0;
@@ -1024,7 +1139,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
                 if (tid == 0) s_nact = na;
             }
             __syncthreads();
-            score_chunk<NT>(q, n, s_act, s_nact, s_models, s_cnt, tf, tlo, thi, tid, blk);
+            score(s_act, s_nact, blk, INT_MAX);
             __syncthreads();
             for (int e = tid; e < nlist; e += NT) {
                 if (s_good[e] < 0) continue;
@@ -1034,7 +1149,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
                 s_good[e] = g;
             }
         } else {
-            score_chunk<NT>(q, n, s_list, nlist, s_models, s_cnt, tf, tlo, thi, tid);
+            score(s_list, nlist, 0, INT_MAX);
             __syncthreads();
             for (int e = tid; e < nlist; e += NT) {
                 int g = 0;
@@ -1410,6 +1525,7 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
     // kernel: 256 threads (16 hypotheses per item, two workgroups per CU so one's scoring overlaps
     // the other's solve) or 512 (SFMHIP_ESS_CT=512: 32 per item, one per CU)
     const int ct = env("SFMHIP_ESS_CT", 256) == 512 ? 512 : 256;
+    const int f32pre = env("SFMHIP_ESS_F32", 1);   // packed-f32 Sampson pre-test (0: f64 throughout)
     const int ch = ct / kGL, recmax = ch * kMaxModels;
     const int cmax = ceil_div(std::max(max_iters, 1), ch), hcap = cmax * ch;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1457,10 +1573,10 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
             const int g = (int)std::min<int64_t>(ct == 512 ? 512 : 1024, (int64_t)PB * std::min(cmax, items));
             if (ct == 512)
                 hipLaunchKernelGGL(ess_chunk_kernel<512>, dim3(g), dim3(512), 0, st, PB, round, of, cm, threshold,
-                                   work, Eb, nmb, mask, nib, itb, B);
+                                   work, Eb, nmb, mask, nib, itb, f32pre, B);
             else
                 hipLaunchKernelGGL(ess_chunk_kernel<256>, dim3(g), dim3(256), 0, st, PB, round, of, cm, threshold,
-                                   work, Eb, nmb, mask, nib, itb, B);
+                                   work, Eb, nmb, mask, nib, itb, f32pre, B);
             hipLaunchKernelGGL(ess_replay_kernel, dim3(PB), dim3(64), 0, st, PB, round, prob, B);
         }
         hipLaunchKernelGGL(ess_final_kernel, dim3(PB), dim3(256), 0, st, of, cm, threshold, work, Eb, nmb, mask, nib,
