@@ -1525,7 +1525,7 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
     // kernel: 256 threads (16 hypotheses per item, two workgroups per CU so one's scoring overlaps
     // the other's solve) or 512 (SFMHIP_ESS_CT=512: 32 per item, one per CU)
     const int ct = env("SFMHIP_ESS_CT", 256) == 512 ? 512 : 256;
-    const int f32pre = env("SFMHIP_ESS_F32", 0);   // 1: packed-f32 Sampson pre-test (default: f64 throughout)
+    const int f32pre = env("SFMHIP_ESS_F32", 1);   // packed-f32 Sampson pre-test (0: f64 throughout)
     const int ch = ct / kGL, recmax = ch * kMaxModels;
     const int cmax = ceil_div(std::max(max_iters, 1), ch), hcap = cmax * ch;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
