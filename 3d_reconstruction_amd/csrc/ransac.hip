@@ -1078,6 +1078,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
         const double tlo = Tmax * (1.0 - 0x1p-40), thi = Tmax * (1.0 + 0x1p-40);
         const int gen = B.st[p].gen_upto;
         const int k = c * CH + h;
+        RPROF_INIT;
+        PROF_COUNT(14, 1);
         for (int i = tid; i < CH * kMaxModels * NW; i += NT) (&s_cnt[0][0])[i] = 0;
         {
             int nm = 0;
@@ -1104,6 +1106,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
         for (int e = tid; e < CH * kMaxModels * 9; e += NT) s_models32[e] = (float)s_models[e];
         __syncthreads();
         const int nlist = s_nlist;
+        RPROF(9, tp);
         auto score = [&](const int* lst, int nl, int lo, int hi) {
             if (f32pre)
                 score_chunk_f32<NT>(q, n, lst, nl, s_models, s_models32, s_cnt, tf, Tmax, tlo, thi, tid, lo, hi);
@@ -1159,6 +1162,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
             }
         }
         __syncthreads();
+        RPROF(10, tp);
         if (tid < 64) {   // records: strict prefix maxima above 4, by a running max over 64-entry blocks
             int2* rec = B.rec + ((size_t)p * B.cmax + c) * (CH * kMaxModels);
             double* recE = B.recE + ((size_t)p * B.cmax + c) * kRecE * 9;
