@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <mutex>
 
 #include "common.h"
 #include "geom_dev.h"
@@ -936,6 +937,7 @@ struct EssState {
     int n, flags, niters, maxgood;
     int gen_upto, eval_upto, rc, cur_k;   // samples drawn, hypotheses listed, replay cursor (chunk, hyp)
     int kp, best_c, best_i, best_k, best_m, last;
+    int solve_upto;   // hypotheses below this are solved (the listing target; samples may run ahead)
 };
 
 struct EssBufs {
@@ -948,6 +950,8 @@ struct EssBufs {
     int* ctr;        // [2 kEssRounds]: (count, head) per round
     int cmax, hcap, rece;
     int ch;          // hypotheses per chunk (16-lane groups of the chunk kernel)
+    uint64_t* spec_rng;   // [P]: the side stream's pre-drawn samples run to spec_upto with this state
+    int* spec_upto;       // [P]
 };
 
 // One lane per pair: draws samples [gen_upto, target) exactly as essential_ransac_kernel's lane 0
@@ -956,6 +960,11 @@ __device__ void ess_gen(EssState& s, int p, int P, int round, const EssBufs& B) 
     int2* list = B.list + (size_t)round * P * B.cmax;
     int* cnt = B.ctr + 2 * round;
     const int target = round + 1 < kEssRounds ? min(s.niters, kSpecHyps << round) : s.niters;
+    if (round > 0 && B.spec_upto && B.spec_upto[p] > s.gen_upto) {   // samples drawn ahead (ess_pregen_kernel)
+        s.gen_upto = B.spec_upto[p];
+        s.rng = B.spec_rng[p];
+    }
+    s.solve_upto = target;
     const unsigned n = (unsigned)s.n;
     uint64_t rs = s.rng;
     int* smp = B.samp + (size_t)p * B.hcap * 5;
@@ -976,6 +985,33 @@ __device__ void ess_gen(EssState& s, int p, int P, int round, const EssBufs& B) 
         for (int c = c0; c < c1; ++c) list[base + c - c0] = make_int2(p, c);
         s.eval_upto = c1 * B.ch;
     }
+}
+
+// Side stream, beside round 0's chunk kernel: each pair's samples drawn ahead from where round 0's
+// stopped up to min(niters, kPreHyps), into the sample table past what round 0 solves, with the
+// state they leave in spec_rng / spec_upto (the pair state itself is left alone: round 0 reads
+// it).  The draws do not depend on any model, so round 1's replay only adopts them (ess_gen).
+constexpr int kPreHyps = 256;
+__global__ __launch_bounds__(64) void ess_pregen_kernel(int P, EssBufs B) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= P) return;
+    const EssState s = B.st[p];
+    int upto = s.gen_upto;
+    uint64_t rng = s.rng;
+    if (!(s.flags & (kEssFive | kEssDone))) {
+        const unsigned n = (unsigned)s.n;
+        const unsigned mg = (unsigned)((1ULL << 32) / n);   // n > 5
+        int* smp = B.samp + (size_t)p * B.hcap * 5;
+        const int target = min(min(s.niters, kPreHyps), B.hcap);
+        for (; upto < target; ++upto) {
+            int d[5];
+            cv_rng_sample5(rng, n, mg, d);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) smp[5 * upto + i] = d[i];
+        }
+    }
+    B.spec_rng[p] = rng;
+    B.spec_upto[p] = upto;
 }
 
 __global__ __launch_bounds__(256) void ess_init_kernel(const double* __restrict__ pts0, const double* __restrict__ pts1,
@@ -1007,6 +1043,7 @@ __global__ __launch_bounds__(256) void ess_init_kernel(const double* __restrict_
         s.cur_k = s.kp = -1;
         s.best_c = s.best_i = s.best_k = s.best_m = -1;
         s.last = -1;
+        s.solve_upto = 0;
         if (n < 5) { nmodels_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
         if (n == 5) B.list[atomicAdd(B.ctr, 1)] = make_int2(p, -1);   // the one kernel call on all points
         if (n > 5) ess_gen(s, p, P, 0, B);                               // round 0's samples and items
@@ -1076,7 +1113,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
         const double mid = 0.5 * ((double)tf + (double)tfu);
         const double Tmax = ((__float_as_uint(tf) & 1u) == 0u) ? mid : nextafter(mid, 0.0);
         const double tlo = Tmax * (1.0 - 0x1p-40), thi = Tmax * (1.0 + 0x1p-40);
-        const int gen = B.st[p].gen_upto;
+        const int gen = B.st[p].solve_upto;
         const int k = c * CH + h;
         RPROF_INIT;
         PROF_COUNT(14, 1);
@@ -1505,6 +1542,29 @@ extern "C" int sfmhip_debug_ransac_prof(unsigned long long* out) {
 }
 #endif
 
+// Library-owned side stream per device for ess_pregen_kernel (created once; events fork it from
+// and join it to the caller's stream, so the call stays ordered on that stream).  The mutex keeps
+// one fork/join sequence at a time per device.
+struct EssSide {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    std::mutex mu;
+};
+static EssSide g_ess_side[64];
+static std::once_flag g_ess_side_once[64];
+static EssSide* ess_side(int dev) {
+    if (dev < 0 || dev >= 64) return nullptr;
+    std::call_once(g_ess_side_once[dev], [dev] {
+        EssSide& e = g_ess_side[dev];
+        if (hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.join, hipEventDisableTiming) != hipSuccess)
+            e.s = nullptr;
+        (void)hipGetLastError();
+    });
+    return g_ess_side[dev].s ? &g_ess_side[dev] : nullptr;
+}
+
 extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, const int64_t* offsets,
                                      int n_pairs, const double* cam, double prob, double threshold,
                                      int max_iters, double* work, double* E, int32_t* n_models,
@@ -1540,7 +1600,8 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
     const size_t bytes = al(batch * sizeof(EssState)) + al((size_t)batch * hcap * 5 * sizeof(int)) +
                          al((size_t)batch * cmax * recmax * sizeof(int2)) + al((size_t)batch * cmax * sizeof(int)) +
                          al((size_t)batch * cmax * kRecE * 9 * sizeof(double)) +
-                         al(kEssRounds * (size_t)batch * cmax * sizeof(int2)) + al(2 * kEssRounds * sizeof(int));
+                         al(kEssRounds * (size_t)batch * cmax * sizeof(int2)) + al(2 * kEssRounds * sizeof(int)) +
+                         al(batch * sizeof(uint64_t)) + al(batch * sizeof(int));
     char* base = nullptr;
     if (scratch_alloc((void**)&base, bytes, st) != hipSuccess) {
         (void)hipGetLastError();
@@ -1557,9 +1618,18 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
     B.recE = (double*)carve((size_t)batch * cmax * kRecE * 9 * sizeof(double));
     B.list = (int2*)carve(kEssRounds * (size_t)batch * cmax * sizeof(int2));
     B.ctr = (int*)carve(2 * kEssRounds * sizeof(int));
+    B.spec_rng = (uint64_t*)carve(batch * sizeof(uint64_t));
+    B.spec_upto = (int*)carve(batch * sizeof(int));
     B.cmax = cmax;
     B.hcap = hcap;
     B.ch = ch;
+    // samples drawn ahead on a side stream while round 0 runs (SFMHIP_ESS_PREGEN=0: off)
+    int dev = -1;
+    EssSide* side = env("SFMHIP_ESS_PREGEN", 1) && hipGetDevice(&dev) == hipSuccess ? ess_side(dev) : nullptr;
+    (void)hipGetLastError();
+    std::unique_lock<std::mutex> side_lock;
+    if (side) side_lock = std::unique_lock<std::mutex>(side->mu);
+    else B.spec_upto = nullptr;
     // records whose E is kept (tests: 0 re-solves every chosen model from its sample)
     B.rece = std::min(kRecE, std::max(0, env("SFMHIP_ESS_RECE", kRecE)));
     int rc = SFMHIP_OK;
@@ -1572,6 +1642,12 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
         (void)hipMemsetAsync(B.ctr, 0, 2 * kEssRounds * sizeof(int), st);
         hipLaunchKernelGGL(ess_init_kernel, dim3(PB), dim3(256), 0, st, pts0, pts1, of, cm, max_iters, work, mask, nmb,
                            nib, itb, PB, B);
+        if (side) {   // fork: the side stream draws ahead once the init kernel has run
+            (void)hipEventRecord(side->fork, st);
+            (void)hipStreamWaitEvent(side->s, side->fork, 0);
+            hipLaunchKernelGGL(ess_pregen_kernel, dim3(ceil_div(PB, 64)), dim3(64), 0, side->s, PB, B);
+            (void)hipEventRecord(side->join, side->s);
+        }
         for (int round = 0; round < kEssRounds; ++round) {
             const int items = round + 1 < kEssRounds ? ceil_div(kSpecHyps << round, ch) : cmax;
             const int g = (int)std::min<int64_t>(ct == 512 ? 512 : 1024, (int64_t)PB * std::min(cmax, items));
@@ -1581,6 +1657,7 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
             else
                 hipLaunchKernelGGL(ess_chunk_kernel<256>, dim3(g), dim3(256), 0, st, PB, round, of, cm, threshold,
                                    work, Eb, nmb, mask, nib, itb, f32pre, B);
+            if (side && round == 0) (void)hipStreamWaitEvent(st, side->join, 0);   // join before round 1's draws
             hipLaunchKernelGGL(ess_replay_kernel, dim3(PB), dim3(64), 0, st, PB, round, prob, B);
         }
         hipLaunchKernelGGL(ess_final_kernel, dim3(PB), dim3(256), 0, st, of, cm, threshold, work, Eb, nmb, mask, nib,
