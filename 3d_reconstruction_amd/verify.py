@@ -30,6 +30,16 @@ def _cam(K) -> np.ndarray:
     K = np.asarray(K, np.float64).reshape(3, 3)
     return np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]])
 
+def _cam_rows(cam, P: int) -> torch.Tensor:
+    """[fx, fy, cx, cy] per problem as a contiguous (P, 4) f64 device tensor.  A device tensor stays
+    on the device (one row is broadcast there): no host round trip, so a batched call never waits
+    for the work queued before it."""
+    if isinstance(cam, torch.Tensor):
+        t = dev(cam, torch.float64).reshape(-1, 4)
+        return (t.expand(P, 4) if t.shape[0] == 1 else t).contiguous()
+    return dev(np.broadcast_to(np.asarray(cam, np.float64).reshape(-1, 4), (P, 4)).copy(), torch.float64)
+
+
 
 def pack_pairs(pts0_list, pts1_list):
     """Lists of (n_p, 2) arrays -> (pts0 (N,2) f64 device, pts1, offsets (P+1,) int64 device)."""
@@ -52,8 +62,7 @@ def find_essential_batched(pts0: torch.Tensor, pts1: torch.Tensor, offsets: torc
     of = dev(offsets, torch.int64)
     P = of.numel() - 1
     N = p0.shape[0]
-    c = dev(np.broadcast_to(np.asarray(cam.cpu() if isinstance(cam, torch.Tensor) else cam, np.float64),
-                            (P, 4)).copy(), torch.float64)
+    c = _cam_rows(cam, P)
     d = p0.device
     out = dict(E=torch.zeros((P, MAX_MODELS, 9), dtype=torch.float64, device=d),
                n_models=torch.empty(P, dtype=torch.int32, device=d),
@@ -77,8 +86,7 @@ def recover_pose_batched(E: torch.Tensor, pts0: torch.Tensor, pts1: torch.Tensor
     P = of.numel() - 1
     N = p0.shape[0]
     Et = dev(E, torch.float64).reshape(P, -1)
-    c = dev(np.broadcast_to(np.asarray(cam.cpu() if isinstance(cam, torch.Tensor) else cam, np.float64),
-                            (P, 4)).copy(), torch.float64)
+    c = _cam_rows(cam, P)
     mk = None if mask is None else dev(mask, torch.uint8)
     d = p0.device
     out = dict(R=torch.empty((P, 3, 3), dtype=torch.float64, device=d),
@@ -186,8 +194,7 @@ def pnp_ransac_batched(obj: torch.Tensor, img: torch.Tensor, offsets: torch.Tens
     of = dev(offsets, torch.int64)
     P = of.numel() - 1
     N = X.shape[0]
-    c = dev(np.broadcast_to(np.asarray(cam.cpu() if isinstance(cam, torch.Tensor) else cam, np.float64),
-                            (P, 4)).copy(), torch.float64)
+    c = _cam_rows(cam, P)
     d = X.device
     out = dict(rvec=torch.empty((P, 3), dtype=torch.float64, device=d),
                tvec=torch.empty((P, 3), dtype=torch.float64, device=d),
