@@ -512,7 +512,7 @@ def verify_line(sfm, syn, device, args, barrier, cpu=True):
             "config": {"workload": "findEssentialMat(RANSAC, 0.999, 1px) + recoverPose: 256 pairs x 2048 matches, "
                                    "30% outliers, 0.5 px noise (matching.py:134-139 / sfm.py:108-119)",
                        "mean_ransac_iters": iters},
-            "roofline": {"bound": "fp64", "kernel": "essential_ransac_kernel+recover_pose_kernel",
+            "roofline": {"bound": "fp64", "kernel": "ess_init/chunk/replay/final + recover_pose_kernel",
                          "kernel_ms": k_ms}}
     vw = verify_work()
     if vw is not None:
