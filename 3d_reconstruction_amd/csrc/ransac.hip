@@ -922,12 +922,13 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
 // Only a record can ever replace the best (a model at or below an earlier count of its chunk was
 // either beaten by that model's acceptance or is <= max(best, 4) already), and niters never grows,
 // so the last round — every chunk below the niters the previous replay left, an upper bound of the
-// final one — completes every pair; rounds 0 and 1 list chunks up to 2 and 4 per pair (bounded
-// speculation: a chunk a later replay finds unneeded is wasted work, never a different result).
+// final one — completes every pair; rounds 0 and 1 list hypotheses up to 64 and up to cap1 (default
+// 256, as far as the side stream draws ahead) per pair (bounded speculation: a chunk a later replay
+// finds unneeded is wasted work, never a different result).
 // The same best model, inlier count and iteration count as the sequential loop over the same
 // models.  ess_final_kernel writes E (kept with the record, or re-solved from its sample) and the
 // mask.
-constexpr int kSpecHyps = 64;      // round r lists chunks up to kSpecHyps << r hypotheses (last round: all)
+constexpr int kSpecHyps = 64;      // round 0 lists hypotheses up to kSpecHyps (round 1: cap1; last round: all)
 constexpr int kEssRounds = 3;
 constexpr int kRecE = 16;          // records per chunk whose E is kept (later ones: re-solved)
 constexpr int kEssFive = 1, kEssDone = 2;
@@ -950,6 +951,7 @@ struct EssBufs {
     int* ctr;        // [2 kEssRounds]: (count, head) per round
     int cmax, hcap, rece;
     int ch;          // hypotheses per chunk (16-lane groups of the chunk kernel)
+    int cap1;        // round 1 lists hypotheses up to min(niters, cap1)
     uint64_t* spec_rng;   // [P]: the side stream's pre-drawn samples run to spec_upto with this state
     int* spec_upto;       // [P]
 };
@@ -959,7 +961,7 @@ struct EssBufs {
 __device__ void ess_gen(EssState& s, int p, int P, int round, const EssBufs& B) {
     int2* list = B.list + (size_t)round * P * B.cmax;
     int* cnt = B.ctr + 2 * round;
-    const int target = round + 1 < kEssRounds ? min(s.niters, kSpecHyps << round) : s.niters;
+    const int target = round == 0 ? min(s.niters, kSpecHyps) : round + 1 < kEssRounds ? min(s.niters, B.cap1) : s.niters;
     if (round > 0 && B.spec_upto && B.spec_upto[p] > s.gen_upto) {   // samples drawn ahead (ess_pregen_kernel)
         s.gen_upto = B.spec_upto[p];
         s.rng = B.spec_rng[p];
@@ -1632,6 +1634,9 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
     else B.spec_upto = nullptr;
     // records whose E is kept (tests: 0 re-solves every chosen model from its sample)
     B.rece = std::min(kRecE, std::max(0, env("SFMHIP_ESS_RECE", kRecE)));
+    // round 1's speculation cap (SFMHIP_ESS_CAP1, >= 2 kSpecHyps): the pre-drawn samples' reach by
+    // default, so round 1 is the last round a pair needs unless its niters exceeds kPreHyps
+    B.cap1 = std::max(2 * kSpecHyps, env("SFMHIP_ESS_CAP1", kPreHyps));
     int rc = SFMHIP_OK;
     for (int p0 = 0; p0 < n_pairs && rc == SFMHIP_OK; p0 += batch) {
         const int PB = std::min(batch, n_pairs - p0);
@@ -1649,7 +1654,7 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
             (void)hipEventRecord(side->join, side->s);
         }
         for (int round = 0; round < kEssRounds; ++round) {
-            const int items = round + 1 < kEssRounds ? ceil_div(kSpecHyps << round, ch) : cmax;
+            const int items = round == 0 ? ceil_div(kSpecHyps, ch) : round + 1 < kEssRounds ? ceil_div(B.cap1, ch) : cmax;
             const int g = (int)std::min<int64_t>(ct == 512 ? 512 : 1024, (int64_t)PB * std::min(cmax, items));
             if (ct == 512)
                 hipLaunchKernelGGL(ess_chunk_kernel<512>, dim3(g), dim3(512), 0, st, PB, round, of, cm, threshold,

@@ -101,8 +101,9 @@ def test_records_replay_equals_sequential(seed):
     ref = sequential(models, n, max_iters)
     for ch in (16, 32):
         for drop in (0, 1, 2):
-            got = balanced(models, n, max_iters, ch, caps=(64, 128), drop=drop)
-            assert got == ref, (seed, ch, drop, got, ref)
+            for caps in ((64, 128), (64, 256), (64, 1000)):
+                got = balanced(models, n, max_iters, ch, caps=caps, drop=drop)
+                assert got == ref, (seed, ch, drop, caps, got, ref)
 
 
 def test_records_replay_adversarial_increasing_counts():
@@ -114,4 +115,5 @@ def test_records_replay_adversarial_increasing_counts():
         ref = sequential(models, n, 1000)
         for ch in (16, 32):
             for drop in (0, 1, 2):
-                assert balanced(models, n, 1000, ch, caps=(64, 128), drop=drop) == ref
+                for caps in ((64, 128), (64, 256)):
+                    assert balanced(models, n, 1000, ch, caps=caps, drop=drop) == ref
