@@ -2678,8 +2678,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     // k + 1 (HBM-bound) runs on the library's side stream while the cull and refinement passes of
     // group k (latency-bound f64 tests) run on the caller's stream; every mask word is written by
     // the group that owns its frames, the refinement list has a region per group, and the fusion
-    // waits for all of them.  Whole-grid mode with the call's own table; the brick pre-pass is
-    // off in it (its coarse table needs every frame's blocks first).
+    // waits for all of them.  Whole-grid mode with the call's own table; the brick pre-pass runs per
+    // group too (coarse table and brick decisions are per frame).
     int pre_groups = 1;
     SideStream* pside = nullptr;
     if (cmask && !ext_table && !stats && !latency_mode) {
@@ -2726,11 +2726,22 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             for (int k = 0; k < groups; ++k) {
                 const int h0 = nh_all * k / groups, h1 = nh_all * (k + 1) / groups;
                 (void)hipStreamWaitEvent(st, pside->grp[k], 0);
+                const int fa = h0 * kCullFrames, fb = std::min(nf, h1 * kCullFrames);
+                if (bdec && fb > fa) {   // the group's coarse table and brick decisions (per frame)
+                    const int gn = fb - fa;
+                    const int64_t nc = (int64_t)gn * ncbu * ncbv, nd = (cull_bricks + 63) / 64 * 64 * gn;
+                    float2* gtab = ctab + (size_t)fa * ncbu * ncbv;
+                    hipLaunchKernelGGL(coarse_table_kernel, dim3((unsigned)ceil_div(nc, (int64_t)256)), dim3(256), 0, st,
+                                       tab + (size_t)fa * nbv * nbu, gn, nbu, nbv, ncbu, ncbv, crange + fa, gtab);
+                    hipLaunchKernelGGL(tsdf_brick_kernel, dim3((unsigned)ceil_div(nd, (int64_t)256)), dim3(256), 0, st,
+                                       H, W, z0, z1, gn, Hd, Wd, ccam + fa, cg, trunc, gtab, cfree ? 1 : 0, ncbu, ncbv,
+                                       per_tile, (int)cull_bricks, bdec + (size_t)fa * cull_bricks);
+                }
                 unsigned* pl = plist ? plist + (int64_t)nbx * nby * nbz * kCullFrames * h0 : nullptr;
                 unsigned* pc = plist ? plist + plist_cap + k : nullptr;
                 hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * (h1 - h0))), dim3(1024), 0, st, H,
                                    W, z0, z1, nf, Hd, Wd, ccam, cg, trunc, tab, cfree ? 1 : 0, nbu, nbv, crange, per_tile,
-                                   nwf, nullptr, (unsigned short*)cmask, (unsigned short*)cfree, pl, pc, tcost, h0,
+                                   nwf, bdec, (unsigned short*)cmask, (unsigned short*)cfree, pl, pc, tcost, h0,
                                    h1 - h0);
                 if (plist)
                     hipLaunchKernelGGL(tsdf_refine_kernel, dim3(refine_wg), dim3(256), 0, st, H, W, z0, z1, nf, Hd, Wd,
