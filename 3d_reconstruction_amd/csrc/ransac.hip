@@ -928,7 +928,7 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
 // The same best model, inlier count and iteration count as the sequential loop over the same
 // models.  ess_final_kernel writes E (kept with the record, or re-solved from its sample) and the
 // mask.
-constexpr int kSpecHyps = 64;      // round 0 lists hypotheses up to kSpecHyps (round 1: cap1; last round: all)
+constexpr int kSpecHyps = 64;      // round 0 lists hypotheses up to cap0 (default kSpecHyps; round 1: cap1; last: all)
 constexpr int kEssRounds = 3;
 constexpr int kRecE = 16;          // records per chunk whose E is kept (later ones: re-solved)
 constexpr int kEssFive = 1, kEssDone = 2;
@@ -951,7 +951,7 @@ struct EssBufs {
     int* ctr;        // [2 kEssRounds]: (count, head) per round
     int cmax, hcap, rece;
     int ch;          // hypotheses per chunk (16-lane groups of the chunk kernel)
-    int cap1;        // round 1 lists hypotheses up to min(niters, cap1)
+    int cap0, cap1;  // rounds 0 and 1 list hypotheses up to min(niters, cap)
     uint64_t* spec_rng;   // [P]: the side stream's pre-drawn samples run to spec_upto with this state
     int* spec_upto;       // [P]
 };
@@ -961,7 +961,7 @@ struct EssBufs {
 __device__ void ess_gen(EssState& s, int p, int P, int round, const EssBufs& B) {
     int2* list = B.list + (size_t)round * P * B.cmax;
     int* cnt = B.ctr + 2 * round;
-    const int target = round == 0 ? min(s.niters, kSpecHyps) : round + 1 < kEssRounds ? min(s.niters, B.cap1) : s.niters;
+    const int target = round == 0 ? min(s.niters, B.cap0) : round + 1 < kEssRounds ? min(s.niters, B.cap1) : s.niters;
     if (round > 0 && B.spec_upto && B.spec_upto[p] > s.gen_upto) {   // samples drawn ahead (ess_pregen_kernel)
         s.gen_upto = B.spec_upto[p];
         s.rng = B.spec_rng[p];
@@ -1634,9 +1634,12 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
     else B.spec_upto = nullptr;
     // records whose E is kept (tests: 0 re-solves every chosen model from its sample)
     B.rece = std::min(kRecE, std::max(0, env("SFMHIP_ESS_RECE", kRecE)));
-    // round 1's speculation cap (SFMHIP_ESS_CAP1, >= 2 kSpecHyps): the pre-drawn samples' reach by
-    // default, so round 1 is the last round a pair needs unless its niters exceeds kPreHyps
-    B.cap1 = std::max(2 * kSpecHyps, env("SFMHIP_ESS_CAP1", kPreHyps));
+    // speculation caps: round 0 (SFMHIP_ESS_CAP0, default kSpecHyps) and round 1 (SFMHIP_ESS_CAP1, at
+    // least cap0): the pre-drawn samples' reach by default, so round 1 is the last round a pair needs
+    // unless its niters exceeds kPreHyps.  Whole chunks: a listed chunk counts as evaluated, and the
+    // chunk kernel solves only below the listing target, so a target short of niters must end a chunk
+    B.cap0 = ceil_div(std::max(1, env("SFMHIP_ESS_CAP0", kSpecHyps)), ch) * ch;
+    B.cap1 = std::max(B.cap0, ceil_div(std::max(1, env("SFMHIP_ESS_CAP1", kPreHyps)), ch) * ch);
     int rc = SFMHIP_OK;
     for (int p0 = 0; p0 < n_pairs && rc == SFMHIP_OK; p0 += batch) {
         const int PB = std::min(batch, n_pairs - p0);
@@ -1654,7 +1657,7 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
             (void)hipEventRecord(side->join, side->s);
         }
         for (int round = 0; round < kEssRounds; ++round) {
-            const int items = round == 0 ? ceil_div(kSpecHyps, ch) : round + 1 < kEssRounds ? ceil_div(B.cap1, ch) : cmax;
+            const int items = round == 0 ? ceil_div(B.cap0, ch) : round + 1 < kEssRounds ? ceil_div(B.cap1, ch) : cmax;
             const int g = (int)std::min<int64_t>(ct == 512 ? 512 : 1024, (int64_t)PB * std::min(cmax, items));
             if (ct == 512)
                 hipLaunchKernelGGL(ess_chunk_kernel<512>, dim3(g), dim3(512), 0, st, PB, round, of, cm, threshold,

@@ -124,7 +124,7 @@ def test_essential_inliers_is_matching_py_count(sfm, gpu, scene):
 def _ess_run(sfm, pts0, pts1, K, max_iters=1000, prob=0.999, **env):
     import os
     keys = ("SFMHIP_ESS_MONO", "SFMHIP_ESS_RECE", "SFMHIP_ESS_CT", "SFMHIP_ESS_F32", "SFMHIP_ESS_PREGEN",
-            "SFMHIP_ESS_CAP1")
+            "SFMHIP_ESS_CAP0", "SFMHIP_ESS_CAP1")
     old = {k: os.environ.pop(k, None) for k in keys}
     try:
         for k, v in env.items():
@@ -164,7 +164,8 @@ def test_balanced_equals_monolithic(sfm, gpu, max_iters):
     pts0, pts1, K = _ess_mixed_scene()
     mono = _ess_run(sfm, pts0, pts1, K, max_iters, MONO=1)
     for env in ({}, {"RECE": 0}, {"RECE": 1}, {"CT": 512}, {"CT": 512, "RECE": 0}, {"F32": 0}, {"PREGEN": 0},
-                {"CAP1": 128}, {"CAP1": 1000}, {"CAP1": 1000, "PREGEN": 0}):
+                {"CAP1": 128}, {"CAP1": 1000}, {"CAP1": 1000, "PREGEN": 0}, {"CAP0": 16}, {"CAP0": 48},
+                {"CAP0": 96, "CAP1": 96}, {"CAP0": 300, "PREGEN": 0}):
         bal = _ess_run(sfm, pts0, pts1, K, max_iters, **env)
         for k in ("n_models", "n_inliers", "iters", "mask"):
             assert np.array_equal(bal[k], mono[k]), (env, k, bal[k], mono[k])
@@ -177,7 +178,7 @@ def test_balanced_bench_scene_matches_monolithic(sfm, gpu):
     """The bench workload's first 64 pairs (2-7 chunks each, oracle-counted): same bits."""
     s = syn.two_view_pairs(64, 2048, outlier_frac=0.3, noise_px=0.5, seed=6)
     mono = _ess_run(sfm, s["pts0"], s["pts1"], s["K"], MONO=1)
-    for env in ({}, {"CT": 512}, {"F32": 0}, {"PREGEN": 0}, {"CAP1": 128}):
+    for env in ({}, {"CT": 512}, {"F32": 0}, {"PREGEN": 0}, {"CAP1": 128}, {"CAP0": 32}, {"CAP0": 48}):
         bal = _ess_run(sfm, s["pts0"], s["pts1"], s["K"], **env)
         for k in ("E", "n_models", "n_inliers", "iters", "mask"):
             assert np.array_equal(bal[k], mono[k]), (env, k)

@@ -29,6 +29,7 @@ def sequential(models, n, max_iters):
 
 def balanced(models, n, max_iters, ch, caps, drop):
     """The ess_* schedule: gen / chunk / replay rounds (caps in hypotheses, last round: all)."""
+    caps = tuple(-(-c // ch) * ch for c in caps)   # whole chunks, as the host rounds them
     st = dict(niters=max(max_iters, 1), maxgood=0, eval_upto=0, rc=0, cur_k=-1, kp=-1, best=None, done=False)
     recs = {}
     for rnd in range(len(caps) + 1):
@@ -101,7 +102,7 @@ def test_records_replay_equals_sequential(seed):
     ref = sequential(models, n, max_iters)
     for ch in (16, 32):
         for drop in (0, 1, 2):
-            for caps in ((64, 128), (64, 256), (64, 1000)):
+            for caps in ((64, 128), (64, 256), (64, 1000), (16, 256), (32, 256), (48, 256), (96, 96), (40, 300)):
                 got = balanced(models, n, max_iters, ch, caps=caps, drop=drop)
                 assert got == ref, (seed, ch, drop, caps, got, ref)
 
