@@ -34,6 +34,7 @@ constexpr int kJcN = 144 / kPnGL;          // convergence-check elements per lan
 constexpr int kJbN = (36 + kPnGL - 1) / kPnGL;  // 2x2 rotation blocks per lane
 static_assert(144 % kPnGL == 0 && kPnGL >= 6, "EPnP group width");
 constexpr int kPnGS = 448;                // LDS doubles per group
+constexpr int kPnStageCap = kPnH * kPnGS * 8 / 21;   // LM points staged in the group scratch (5 floats + a flag)
 #ifndef SFMHIP_PNP_FAST_ROT   // 1: measured 0.705 vs 0.713 ms (noise level, profiles/r4/ab_pnp_verify_heavyprobe_r4j.log)
 #define SFMHIP_PNP_FAST_ROT 0
 #endif
@@ -847,12 +848,16 @@ __device__ __forceinline__ void pnp_prepare(EpnpData& D, double* G, int gl) {
 // After the RANSAC loop (best model s_best, maxgood inliers, last hypothesis run): the inlier mask
 // of the best model, CvLevMarq on the inliers (cvProjectPoints2's analytic Jacobian, J^T J / J^T e
 // as fixed-order block reductions), the outputs.  Every thread of the kPnThreads workgroup.
-__device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const float* __restrict__ f, double fx,
+// stage (LDS the caller no longer needs, cap points): the problem's points and inlier flags are
+// copied there when they fit, so the LM passes read LDS instead of global memory (the same values
+// and per-thread order: the same bits); null or n > cap reads global memory.
+__device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const float* __restrict__ fg, double fx,
                                            double fy, double cx, double cy, float thr, int maxgood, int last,
                                            const double* s_best, double* s_lm, double* s_red,
                                            uint8_t* __restrict__ mask, double* __restrict__ rvec_out,
                                            double* __restrict__ tvec_out, int32_t* __restrict__ ninl_out,
-                                           int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out) {
+                                           int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out,
+                                           float* stage = nullptr, int cap = 0) {
     const int tid = threadIdx.x;
 #ifdef SFMHIP_PNP_PROF
     unsigned long long pp_t = wall_clock64();
@@ -861,6 +866,11 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
         if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = last + 1; }
         return;
     }
+    const bool staged = stage && n <= cap;
+    uint8_t* inl = staged ? reinterpret_cast<uint8_t*>(stage + 5 * cap) : mask + off;
+    if (staged)
+        for (int t = tid; t < 5 * n; t += kPnThreads) stage[t] = fg[t];
+    const float* f = staged ? stage : fg;
     // inlier mask of the best model
     if (tid == 0) rodrigues(s_best, s_lm + 39);
     __syncthreads();
@@ -868,7 +878,9 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
         float pu, pv;
         project_f(s_lm + 39, s_best + 3, fx, fy, cx, cy, f[5 * i], f[5 * i + 1], f[5 * i + 2], pu, pv);
         const float du = f[5 * i + 3] - pu, dv = f[5 * i + 4] - pv;
-        mask[off + i] = (du * du + dv * dv <= thr) ? 1 : 0;
+        const uint8_t m = (du * du + dv * dv <= thr) ? 1 : 0;
+        mask[off + i] = m;
+        if (staged) inl[i] = m;
     }
     // Levenberg-Marquardt refinement on the inliers (CvLevMarq control flow)
     double* prm = s_lm;       // param[6]
@@ -887,7 +899,7 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
         double acc[28];
         for (int k = 0; k < 28; ++k) acc[k] = 0;
         for (int i = tid; i < n; i += kPnThreads) {
-            if (!mask[off + i]) continue;
+            if (!inl[i]) continue;
             const double X = f[5 * i], Y = f[5 * i + 1], Z = f[5 * i + 2];
             const double xc = Rm[0] * X + Rm[1] * Y + Rm[2] * Z + prm[3];
             const double yc = Rm[3] * X + Rm[4] * Y + Rm[5] * Z + prm[4];
@@ -1125,8 +1137,9 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         if (s_k0 >= s_niters) break;
     }
     PPROF(3);
+    // the EPnP group scratch is free now: the LM stages the points there
     pnp_refine(p, n, off, f, fx, fy, cx, cy, thr, s_maxgood, s_last, s_best, s_lm, s_red, mask, rvec_out,
-               tvec_out, ninl_out, iters_out, ok_out);
+               tvec_out, ninl_out, iters_out, ok_out, reinterpret_cast<float*>(s_grp), kPnStageCap);
     (void)s_flag;
 }
 
