@@ -911,9 +911,10 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
 //   ess_init_kernel    normalised points, per-pair state (EssState), outputs of n < 5 pairs;
 //   ess_gen            one lane per pair draws the pair's samples from cv::RNG(-1) in draw order up
 //                      to a target hypothesis count (below) and appends the chunks that cover them to a work list;
-//   ess_chunk_kernel   persistent 512-thread workgroups take (pair, chunk) items from the list:
-//                      the chunk's 32 samples solved by 16-lane groups and its models scored on
-//                      every point (essential_ransac_kernel's own solver and scoring), then its
+//   ess_chunk_kernel   persistent workgroups (256 threads by default, SFMHIP_ESS_CT=512) take
+//                      (pair, chunk) items from the list: the chunk's 16 (32) samples solved by
+//                      16-lane groups and its models scored on every point (essential_ransac_kernel's
+//                      own solver and scoring, with the packed-f32 Sampson pre-test), then its
 //                      records: the models whose count exceeds max(4, every earlier count of the
 //                      chunk), in replay order;
 //   ess_replay_kernel  one lane per pair replays the records in OpenCV's order (a model replaces
@@ -922,7 +923,7 @@ __global__ __launch_bounds__(kRThreads) void essential_ransac_kernel(
 // Only a record can ever replace the best (a model at or below an earlier count of its chunk was
 // either beaten by that model's acceptance or is <= max(best, 4) already), and niters never grows,
 // so the last round — every chunk below the niters the previous replay left, an upper bound of the
-// final one — completes every pair; rounds 0 and 1 list hypotheses up to 64 and up to cap1 (default
+// final one — completes every pair; rounds 0 and 1 list hypotheses up to cap0 (default 64) and cap1 (default
 // 256, as far as the side stream draws ahead) per pair (bounded speculation: a chunk a later replay
 // finds unneeded is wasted work, never a different result).
 // The same best model, inlier count and iteration count as the sequential loop over the same
