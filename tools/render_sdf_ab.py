@@ -39,8 +39,8 @@ def run(sdf):
 
 ref = run(False)
 for rep in range(3):
-    for sdf, occ, two in ((False, "0", "0"), (True, "4", "0"), (True, "0", "3"), (True, "4", "3"), (True, "4", "4"),
-                          (True, "0", "4")):
+    for sdf, occ, two in ((False, "0", "0"), (True, "4", "0"), (True, "0", "0"), (True, "0", "3"), (True, "4", "3"),
+                          (True, "4", "4"), (True, "0", "4")):
         os.environ["SFMHIP_RENDER_OCC"] = occ
         os.environ["SFMHIP_RENDER_2PH"] = two
         ts = []
