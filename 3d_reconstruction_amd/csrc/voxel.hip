@@ -364,12 +364,22 @@ __device__ __forceinline__ void render_body(const float* __restrict__ gvm, int D
                 corners(g, D, H, W, cn);
                 bool lines = true;
                 if (sig) {   // sdf from the compact plane; the voxel lines only where alpha != 0
+                    // the 8 plane gathers in flight together: an out-of-range corner reads its clamped
+                    // neighbour with weight 0 (finite grid: v * 0 = +-0 leaves a sum that starts at +0
+                    // unchanged, the same bits as skipping it)
+                    float pv[8], wq[8];
 #pragma unroll
                     for (int q = 0; q < 8; ++q) {
                         int x, y, zz;
-                        if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
-                        sdf = sdf + sdfp[((size_t)zz * H + y) * W + x] * cn.w[q];
+                        const bool in = corner_in(cn, q, D, H, W, x, y, zz);
+                        x = min(max(x, 0), W - 1);
+                        y = min(max(y, 0), H - 1);
+                        zz = min(max(zz, 0), D - 1);
+                        wq[q] = in ? cn.w[q] : 0.f;
+                        pv[q] = sdfp[((size_t)zz * H + y) * W + x];
                     }
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) sdf = sdf + pv[q] * wq[q];
                     lines = 1.f - expf((-fmaxf(sdf, 0.f)) * delta) != 0.f;
                 }
                 if (lines) {
