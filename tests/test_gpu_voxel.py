@@ -187,6 +187,34 @@ def test_render_sdf_plane_skip_bitexact(sfm, gpu, monkeypatch, sort, two):
     assert same(r2, rgb)
 
 
+def test_render_sdf_plane_grid_faces_bitexact(sfm, gpu):
+    """Samples exactly on the grid's upper faces (sdf.py's inclusive mask, mode 0): their +1 corners
+    are out of range, which the sdf-plane path reads clamped with weight 0 and the full path skips;
+    both must give the same bits.  Axis-aligned rays on the x = max and y = max faces, and depths
+    that put the last sample on z = max."""
+    abi = importlib.import_module("3d_reconstruction_amd._abi")
+    g = torch.Generator(device=gpu).manual_seed(11)
+    N, S = 20, 64
+    grid = torch.randn((28, N, N + 1, N + 2), generator=g, device=gpu) * 0.1 + 0.05
+    vg = sfm.VoxelGrid.plenoxel(grid, 1.5)
+    xs = torch.tensor([1.5, 1.5, -1.5, 0.3, 1.5, 0.0], device=gpu)
+    ys = torch.tensor([0.2, 1.5, 1.5, 1.5, -0.7, 0.0], device=gpu)
+    B = xs.numel()
+    ro = torch.stack([xs, ys, torch.full_like(xs, -3.0)], 1).contiguous()
+    rd = torch.tensor([0.0, 0.0, 1.0], device=gpu).expand(B, 3).contiguous()
+    z = torch.linspace(1.5, 4.5, S, device=gpu).expand(B, S).contiguous()   # last sample: z = 1.5 exactly
+    assert float(z[0, -1]) == 4.5
+    bmin, bmax = np.full(3, -1.5, np.float32), np.full(3, 1.5, np.float32)
+    outs = []
+    for name, extra in (("sfmhip_render_rays", ()), ("sfmhip_render_rays_sdf", (vg.grid[0].data_ptr(),))):
+        rgb = torch.empty((B, 3), dtype=torch.float32, device=gpu)
+        abi.call(name, vg.voxel_major().data_ptr(), *extra, N, N + 1, N + 2, bmin.ctypes.data, bmax.ctypes.data, 0,
+                 ro.data_ptr(), rd.data_ptr(), z.data_ptr(), B, S, rgb.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        outs.append(rgb)
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()
+
+
 def test_voxel_traversal_cap_boundary(sfm, gpu, monkeypatch):
     """The one-walk form at the edge of its row width: cap = S (every ray fits:
     the rows' prefix is returned) and cap = S - 1 (the longest ray does not fit:
