@@ -10,7 +10,7 @@ functions) are top-level, so ``import sfmhip as cv2`` binds them.
 Every compute entry point runs a HIP kernel from ``libsfmhip.so``; there is no
 CPU fallback.
 """
-from ._abi import LIB_PATH, SfmHipError, lib, require_gpu  # noqa: F401  (fails loudly if the .so is missing)
+from ._abi import LIB_PATH, SfmHipError, knobs_reload, lib, require_gpu  # noqa: F401  (fails loudly if the .so is missing)
 from .match import (MODE_FLOAT, MODE_SIFT, DescriptorBank, Matcher, all_pairs,  # noqa: F401
                     bf_match, vq)
 from .geometry import (Rodrigues, ba_sparse, calculate_reprojection_error,  # noqa: F401

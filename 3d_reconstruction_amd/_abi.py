@@ -55,6 +55,7 @@ SIGNATURES = {
     "sfmhip_device_arch": [ctypes.c_char_p, _i32],
     "sfmhip_scratch_trim": [_u64],
     "sfmhip_scratch_release_stream": [_p],
+    "sfmhip_knobs_reload": [],
     "sfmhip_desc_quantize": [_p, _i32, _i32, _i32, _p, _i32, _p, _p],
     "sfmhip_desc_prepare": [_p, _i32, _i32, _i32, _p, _p, _p, _p],
     "sfmhip_desc_prepare_shifted": [_p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p],
@@ -132,6 +133,12 @@ def call(name: str, *args) -> None:
     if rc != SFMHIP_OK:
         msg = lib.sfmhip_last_error().decode(errors="replace")
         raise SfmHipError(name, rc, msg)
+
+
+def knobs_reload() -> None:
+    """Re-read the library's runtime knobs (SFMHIP_*) from the
+    environment; the library reads them once, at its first call."""
+    call("sfmhip_knobs_reload")
 
 
 def require_gpu() -> torch.device:

@@ -53,6 +53,15 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 // reuse it at once, its kernels run after this call's).
 void scratch_free(void* p, hipStream_t s);
 
+// Runtime knobs (INTEGRATION.md "Runtime knobs"): read from the environment once, at
+// the first call; sfmhip_knobs_reload() re-reads them (tests).  Every other choice is
+// fixed in the code.
+struct Knobs {
+    int tsdf_latency;   // SFMHIP_TSDF_LATENCY: -1 auto, 0 whole-grid mode, 1 latency mode
+    int tsdf_slots;     // SFMHIP_TSDF_SLOTS: fusion partial-slot capacity (0: 4 per wave sub-tile)
+};
+const Knobs& knobs();
+
 }  // namespace sfmhip
 
 #define SFMHIP_REQUIRE(cond, ...)                                   \

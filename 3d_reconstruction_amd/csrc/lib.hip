@@ -1,6 +1,7 @@
 // lib.hip — library-level entry points: version, thread-local error, arch probe.
 #include "common.h"
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 
 namespace sfmhip {
@@ -78,8 +79,12 @@ static std::mutex g_cache_mu;
 static void release_slot(CacheSlot& c) {
     if (hipFreeAsync(c.p, c.s) != hipSuccess) {
         (void)hipGetLastError();
+        int cur = -1;
+        const bool have = hipGetDevice(&cur) == hipSuccess;
+        if (!have || cur != c.dev) (void)hipSetDevice(c.dev);   // the buffer's own device
         (void)hipDeviceSynchronize();
         (void)hipFree(c.p);
+        if (have && cur != c.dev) (void)hipSetDevice(cur);
     }
     (void)hipGetLastError();
     c = CacheSlot{};
@@ -107,9 +112,10 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
         *p = g_cache[best].p;
         return hipSuccess;
     }
-    if (empty < 0) {   // table full: drop the smallest idle buffer of any stream, else allocate uncached
+    if (empty < 0) {   // table full: drop the smallest idle buffer of this device, else allocate uncached
         for (int i = 0; i < kCacheSlots; ++i)
-            if (!g_cache[i].busy && (empty < 0 || g_cache[i].bytes < g_cache[empty].bytes)) empty = i;
+            if (!g_cache[i].busy && g_cache[i].dev == dev && (empty < 0 || g_cache[i].bytes < g_cache[empty].bytes))
+                empty = i;
         if (empty >= 0) release_slot(g_cache[empty]);
     }
     const hipError_t e = pool_alloc(p, bytes, s, dev, true);
@@ -120,7 +126,9 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
         while (held > kCacheTotal) {
             int big = -1;
             for (int i = 0; i < kCacheSlots; ++i)
-                if (g_cache[i].p && !g_cache[i].busy && (big < 0 || g_cache[i].bytes > g_cache[big].bytes)) big = i;
+                if (g_cache[i].p && !g_cache[i].busy && g_cache[i].dev == dev &&
+                    (big < 0 || g_cache[i].bytes > g_cache[big].bytes))
+                    big = i;
             if (big < 0) break;
             held -= g_cache[big].bytes;
             release_slot(g_cache[big]);
@@ -141,7 +149,34 @@ void scratch_free(void* p, hipStream_t s) {
     }
     (void)hipFreeAsync(p, s);
 }
+
+static int env_knob(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e && *e ? std::atoi(e) : dflt;
+}
+static Knobs read_knobs() {
+    Knobs k;
+    k.tsdf_latency = env_knob("SFMHIP_TSDF_LATENCY", -1);
+    k.tsdf_slots = env_knob("SFMHIP_TSDF_SLOTS", 0);
+    return k;
+}
+static Knobs g_knobs;
+static std::once_flag g_knobs_once;
+static std::mutex g_knobs_mu;
+const Knobs& knobs() {
+    std::call_once(g_knobs_once, [] { g_knobs = read_knobs(); });
+    return g_knobs;
+}
 }  // namespace sfmhip
+
+// Re-read the runtime knobs from the environment (tests that switch a knob between
+// calls; not thread-safe against concurrent library calls).
+extern "C" int sfmhip_knobs_reload(void) {
+    (void)sfmhip::knobs();
+    std::lock_guard<std::mutex> lk(sfmhip::g_knobs_mu);
+    sfmhip::g_knobs = sfmhip::read_knobs();
+    return SFMHIP_OK;
+}
 
 // 0.2.0: sfmhip_ba_solve takes n_obs (between n_pairs and ftol); sfmhip_scratch_release_stream
 extern "C" int sfmhip_version(void) { return (0 << 16) | (2 << 8) | 0; }

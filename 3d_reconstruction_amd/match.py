@@ -18,13 +18,16 @@ ratio test ``den^2 * d1 < num^2 * d2`` evaluated exactly, optional mutual
 check with LightGlue's ``filter_matches`` semantics
 (``lightglue/lightglue.py:235-254``).  Two distance definitions:
 
-* quantised (default for ``DescriptorBank``): exact integer squared L2 of the
-  int8 quantisation (SIFT: q = x - 128; float: q = rint(127 x));
-* exact float (``exact=True``; default for :class:`Matcher`, which receives
-  the float DISK / SuperPoint descriptors of matching.py:111-122): squared L2
-  of the f32 descriptors summed in f64 in k order.  The int8 MFMA pass runs
-  with a proven bound on the quantisation residual and certifies most rows;
-  the rest are re-scored exactly (DESIGN.md "exact float mode").
+* exact float (the default for float descriptors -- ``MODE_FLOAT``, the DISK /
+  SuperPoint descriptors of matching.py:111-122 -- in :class:`Matcher`,
+  :meth:`DescriptorBank.from_float`, :func:`bf_match` and so in
+  ``pipeline.matching_stage`` / ``dist.match_all_pairs_sharded``): squared L2 of
+  the f32 descriptors summed in f64 in k order.  The int8 MFMA pass runs with a
+  proven bound on the quantisation residual and certifies most rows; the rest
+  are re-scored exactly (DESIGN.md "exact float mode");
+* quantised (``exact=False``; and ``MODE_SIFT``, whose integer 0..255 values
+  quantise exactly): exact integer squared L2 of the int8 quantisation (SIFT:
+  q = x - 128; float: q = rint(127 x)).
 """
 from __future__ import annotations
 
@@ -121,11 +124,14 @@ class DescriptorBank:
 
     # -- construction -------------------------------------------------------
     @classmethod
-    def from_float(cls, desc, n_kpts=None, mode: int = MODE_FLOAT, exact: bool = False) -> "DescriptorBank":
+    def from_float(cls, desc, n_kpts=None, mode: int = MODE_FLOAT, exact: bool | None = None) -> "DescriptorBank":
         """``desc``: f32 [n_img, M, d] array/tensor or a list of (K_i, d) arrays
         (the ``all_descriptors.npy`` object-array format, ``feature_extraction.py:50``).
         ``exact``: keep the f32 descriptors for the exact float mode (finite
-        values required; padding rows are zeroed)."""
+        values required; padding rows are zeroed); default: True for
+        ``MODE_FLOAT``, False for ``MODE_SIFT`` (integer values: the int8
+        distances are the exact ones)."""
+        exact = (mode == MODE_FLOAT) if exact is None else bool(exact)
         d0 = require_gpu()
         if isinstance(desc, (list, tuple)) or (isinstance(desc, np.ndarray) and desc.dtype == object):
             rows = [dev(r, torch.float32) for r in desc]
@@ -207,7 +213,7 @@ def all_pairs(n_img: int) -> np.ndarray:
     return np.stack([a, b], 1).astype(np.int32)
 
 
-def bf_match(desc0, desc1, ratio=0.75, mutual: bool = False, mode: int = MODE_FLOAT, exact: bool = False):
+def bf_match(desc0, desc1, ratio=0.75, mutual: bool = False, mode: int = MODE_FLOAT, exact: bool | None = None):
     """One pair, numpy in / numpy out: ``matches0`` int64 (M,), -1 = no match."""
     d0 = np.asarray(desc0, dtype=np.float32)
     d1 = np.asarray(desc1, dtype=np.float32)

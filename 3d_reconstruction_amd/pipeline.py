@@ -15,11 +15,14 @@ from .match import MODE_FLOAT, DescriptorBank, all_pairs
 
 
 def matching_stage(all_descriptors, codebook, ratio=0.75, mode: int = MODE_FLOAT, top_k: int = 10,
-                   verify=None, min_matches: int = 500, all_points=None, focal: float = 2378.98305085):
-    """Returns dict(img_pairs, all_matches, connection, start, matches0, matches1)."""
+                   verify=None, min_matches: int = 500, all_points=None, focal: float = 2378.98305085,
+                   exact: bool | None = None):
+    """Returns dict(img_pairs, all_matches, connection, start, matches0, matches1).
+    ``exact`` (default: True for float descriptors): the matcher's distance semantics
+    (match.py module docstring); False selects the quantised int8 mode."""
     descs = [np.asarray(d, np.float32) for d in all_descriptors]
     _, conn, start = bow.retrieval_graph(descs, codebook, top_k=top_k)
-    bank = DescriptorBank.from_float(descs, mode=mode)
+    bank = DescriptorBank.from_float(descs, mode=mode, exact=exact)
     pairs = all_pairs(len(descs))
     m0, m1 = bank.match(pairs, ratio=ratio, mutual=True)
     torch.cuda.synchronize()

@@ -219,6 +219,24 @@ def match_cpu_leg(qcpu, pairs, sample, n_one=3):
                    f"pairs (1 thread), spread over the pair list")
 
 
+def match_cpu_leg_exact(xcpu, pairs, sample, n_one=2):
+    """The exact-float oracle (oracle.match.bf_match_exact: f32 descriptors, squared L2
+    summed in f64 in k order, top-2, exact ratio) on a spread sample of the same pairs,
+    pairs over a thread pool with one BLAS thread per worker."""
+    from oracle import match as om
+
+    def one(i):
+        a, b = (int(v) for v in pairs[i])
+        om.bf_match_exact(xcpu[a], xcpu[b], (3, 4))
+
+    def run(k, nt):
+        with blas_limit(1):
+            pool_map(one, sample[:k], nt)
+    return cpu_leg(run, len(sample), n_one, "pairs/s", "port",
+                   f"oracle.match.bf_match_exact on {len(sample)} pairs over a thread pool (all threads) / {n_one} "
+                   f"pairs (1 thread), spread over the pair list")
+
+
 def spread(n_total: int, n: int):
     return [(i * 997) % n_total for i in range(n)]
 
@@ -262,42 +280,45 @@ def c2_line(sfm, syn, device, args, barrier, cpu=True):
     return line
 
 
-def exact_line(sfm, syn, device, args, barrier, cpu=True, int8_ms=None):
-    """The exact float matching mode (Matcher default for float DISK/SuperPoint
-    descriptors, matching.py:111-122) on all C3 pairs: int8 MFMA pass with a
-    proven bound on the quantisation residual, uncertified rows re-scored in
-    f64.  Reported as its cost relative to the int8 path."""
+def int8_line(sfm, syn, device, args, barrier, cpu=True, exact_ms=None):
+    """The quantised mode (DescriptorBank.from_float(..., exact=False)): exact integer
+    squared L2 of the int8 quantisation q = rint(127 x), the int8 MFMA kernel alone, on
+    all C3 pairs.  Reported with its speed relative to the exact-float headline."""
     sdist = importlib.import_module("3d_reconstruction_amd.dist")
     x = syn.superpoint_like(N_IMG, M_KPT, DIM, seed=1, device=device)
-    bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_FLOAT, exact=True)
+    bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_FLOAT, exact=False)
     del x
-    pdev = torch.from_numpy(sfm.all_pairs(N_IMG)).to(device)
+    pairs = sfm.all_pairs(N_IMG)
+    pdev = torch.from_numpy(pairs).to(device)
     P = pdev.shape[0]
 
     def step(record):
         e0, e1 = events() if record else (None, None)
         if record:
             e0.record()
-        sdist.match_all_pairs_sharded(bank, pdev, exact=True, chunks=1,
+        sdist.match_all_pairs_sharded(bank, pdev, exact=False, chunks=1,
                                       after_compute=(e1.record if record else None))
         return (e0, e1)
 
     wall, kms = timed(step, args.steps, 1, barrier)
     ms = wall / args.steps * 1e3
-    res = int(bank.last_resolved.item()) if bank.last_resolved is not None else None
-    line = {"metric": "exact-float image-pairs matched/sec", "value": P / (ms * 1e-3), "unit": "pairs/s",
-            "ms_per_step": ms, "dtype": "int8 filter + f64 re-score",
-            "config": {"workload": f"C3 float descriptors, exact f64 BF-L2 + ratio 0.75 (Matcher(exact=True)): "
-                                   f"{N_IMG} imgs x {M_KPT} x {DIM}, all {P} pairs"},
-            "kernel_ms": float(np.mean(kms)),
-            "roofline": {"bound": "mfma", "kernel": "match_kernel<256> exact + match_resolve_kernel", "unit": "TOPS",
-                         "achieved": 2.0 * M_KPT * M_KPT * DIM * P / (float(np.mean(kms)) * 1e-3) / 1e12,
-                         "peak": PEAK_INT8_TOPS,
-                         "frac": 2.0 * M_KPT * M_KPT * DIM * P / (float(np.mean(kms)) * 1e-3) / 1e12 / PEAK_INT8_TOPS,
-                         "algorithmic": "2*M*N*d int8 ops per pair (the f64 re-score of the uncertified rows "
-                                        "is counted as overhead, not work)"},
-            "rows_rescored": res, "rows_rescored_frac": (res / (P * M_KPT)) if res is not None else None,
-            "cost_vs_int8": (ms / int8_ms) if int8_ms else None}
+    k_ms = float(np.mean(kms))
+    ops = 2.0 * M_KPT * M_KPT * DIM * P
+    line = {"metric": "quantised-int8 image-pairs matched/sec", "value": P / (ms * 1e-3), "unit": "pairs/s",
+            "ms_per_step": ms, "dtype": "int8",
+            "config": {"workload": f"C3 float descriptors quantised q = rint(127 x), exact int8 BF-L2 + ratio 0.75 "
+                                   f"(DescriptorBank.from_float(exact=False)): {N_IMG} imgs x {M_KPT} x {DIM}, "
+                                   f"all {P} pairs"},
+            "roofline": {"bound": "mfma", "kernel": "match_kernel<256>", "kernel_ms": k_ms, "unit": "TOPS",
+                         "achieved": ops / (k_ms * 1e-3) / 1e12, "peak": PEAK_INT8_TOPS,
+                         "frac": ops / (k_ms * 1e-3) / 1e12 / PEAK_INT8_TOPS,
+                         "traffic": pmc_traffic("match"),
+                         "algorithmic": "2*M*N*d int8 ops per pair"},
+            "speed_vs_exact": (exact_ms / ms) if exact_ms else None}
+    if cpu:
+        sample = spread(P, 16)
+        qcpu = {int(k): bank.q[int(k)].cpu().numpy() for i in sample for k in pairs[i]}
+        line["cpu_baseline"] = match_cpu_leg(qcpu, pairs, sample)
     del bank
     torch.cuda.empty_cache()
     return line
@@ -1240,12 +1261,17 @@ def main():
     n_img = args.n_img
     t0 = time.perf_counter()
     x = syn.superpoint_like(n_img, M_KPT, DIM, seed=1, device=device)
-    bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_FLOAT)
+    # the float descriptors' own semantics (exact f32-input BF-L2, Matcher's default): the int8
+    # MFMA pass certifies most rows with a proven residual bound, the rest are re-scored in f64
+    bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_FLOAT, exact=True)
+    pairs_all = sfm.all_pairs(n_img)
+    if cpu:
+        sample = spread(len(pairs_all), 12)
+        xcpu = {int(k): x[int(k)].cpu().numpy() for i in sample for k in pairs_all[i]}
     del x
     torch.cuda.synchronize()
     log(f"[rank {rank}] descriptors ready ({time.perf_counter() - t0:.1f}s): "
-        f"{n_img}x{M_KPT}x{DIM} int8 = {bank.q.numel() / 1e6:.0f} MB")
-    pairs_all = sfm.all_pairs(n_img)
+        f"{n_img}x{M_KPT}x{DIM} int8 = {bank.q.numel() / 1e6:.0f} MB + f32 = {bank.x.numel() * 4 / 1e6:.0f} MB")
     P = len(pairs_all)
     pairs_dev = torch.from_numpy(pairs_all).to(device)
     chunks = MATCH_CHUNKS if (world > 1 or comm is not None) else 1
@@ -1255,7 +1281,7 @@ def main():
         e0, e1 = events() if record else (None, None)
         if record:
             e0.record()
-        holder["g"] = sdist.match_all_pairs_sharded(bank, pairs_dev, ratio=(3, 4), exact=False, comm=comm,
+        holder["g"] = sdist.match_all_pairs_sharded(bank, pairs_dev, ratio=(3, 4), exact=True, comm=comm,
                                                     chunks=chunks, after_compute=(e1.record if record else None))
         return (e0, e1)
 
@@ -1268,6 +1294,7 @@ def main():
     achieved_tops = ops_per_launch / (kern_ms * 1e-3) / 1e12
     graph = holder["g"]
     n_matched = int((graph >= 0).sum().item())
+    rescored = int(bank.last_resolved.item()) if bank.last_resolved is not None else None
     log(f"[rank {rank}] match: {ms_per_step:.2f} ms/step, kernel {kern_ms:.2f} ms, "
         f"{achieved_tops:.0f} TOPS, {n_matched} matches in the gathered graph {tuple(graph.shape)} {graph.dtype}")
 
@@ -1282,10 +1309,12 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "int8",
+        "dtype": "f32 descriptors: int8 MFMA certified filter + f64 re-score",
         "data": "synthetic (SuperPoint-like unit-norm descriptors, 40% cross-view overlap, seed 1)",
-        "config": {"workload": f"C3/C4 all-pairs BF-L2 + ratio 0.75: {n_img} imgs x {M_KPT} kpts x {DIM}-d",
-                   "pairs": P, "api": "dist.match_all_pairs_sharded",
+        "config": {"workload": f"C3/C4 all-pairs BF-L2 + ratio 0.75: {n_img} imgs x {M_KPT} kpts x {DIM}-d, "
+                               "exact f32-input semantics (oracle.match.bf_match_exact, bit for bit)",
+                   "pairs": P, "api": "dist.match_all_pairs_sharded(exact=True)", "match_mode": "exact-float",
+                   "rows_rescored_per_step": rescored,
                    "parallelism": f"pairs/{world}" + (
                        f" + {chunks} RCCL all-gathers (int16, sfmhip_allgather) overlapped with the match launches"
                        if comm is not None else (" + torch.distributed all-gather (rehearsal)" if world > 1 else ""))},
@@ -1293,13 +1322,11 @@ def main():
                      "frac": achieved_tops / PEAK_INT8_TOPS,
                      "traffic": pmc_traffic("match", pairs_per_launch / P) if n_img == N_IMG else None,
                      "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r4/traffic.json)",
-                     "kernel": "match_kernel<256>", "kernel_ms": kern_ms,
-                     "algorithmic": "2*M*N*d int8 ops per pair x pairs per launch"},
+                     "kernel": "match_kernel<256> (exact mode) + match_resolve_kernel", "kernel_ms": kern_ms,
+                     "algorithmic": "2*M*N*d int8 ops per pair x pairs per launch (the f64 re-score of the "
+                                    "uncertified rows is overhead, not work)"},
     }
     match_cpu = None
-    if cpu:
-        sample = spread(P, 16)
-        qcpu = {int(k): bank.q[int(k)].cpu().numpy() for i in sample for k in pairs_all[i]}
     del bank, holder["g"], graph
     torch.cuda.empty_cache()
 
@@ -1391,7 +1418,7 @@ def main():
         if world == 1:
             result["secondary"].append(ba_solve_line(sfm, syn, device, args, barrier, cpu=cpu))
             result["secondary"].append(c2_line(sfm, syn, device, args, barrier, cpu=cpu))
-            result["secondary"].append(exact_line(sfm, syn, device, args, barrier, cpu=cpu, int8_ms=ms_per_step))
+            result["secondary"].append(int8_line(sfm, syn, device, args, barrier, cpu=cpu, exact_ms=ms_per_step))
             result["secondary"].extend(voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=cpu))
             result["secondary"].append(verify_line(sfm, syn, device, args, barrier, cpu=cpu))
             result["secondary"].append(pnp_line(sfm, syn, device, args, barrier, cpu=cpu))
@@ -1400,7 +1427,7 @@ def main():
 
     # ---------------- CPU baseline (rank 0, N=1 only) ------------------------
     if cpu:
-        match_cpu = match_cpu_leg(qcpu, pairs_all, sample)
+        match_cpu = match_cpu_leg_exact(xcpu, pairs_all, sample)
         match_cpu["sample"] += f"; linear extrapolation to all {P} pairs = {P / match_cpu['value']:.0f} s"
         result["cpu_baseline"] = match_cpu
         result["host"] = host_info()
@@ -1411,7 +1438,10 @@ def main():
 
     if rank == 0:
         if "tsdf_value" in result:   # last key: the end of the line is what a truncated tail keeps
-            result["headline"] = {"pairs_per_s": result["value"], "match_ms_per_step": result["ms_per_step"],
+            int8 = next((x for x in result.get("secondary", []) if x.get("metric", "").startswith("quantised")), {})
+            result["headline"] = {"match_mode": "exact-float", "pairs_per_s": result["value"],
+                                  "match_ms_per_step": result["ms_per_step"],
+                                  "int8_mode_ms_per_step": int8.get("ms_per_step"),
                                   "match_frac": result["roofline"]["frac"], "tsdf_mvoxel_per_s": result["tsdf_value"],
                                   "tsdf_ms_per_step": result["tsdf_ms_per_step"],
                                   "tsdf_frac": result["tsdf_roofline"]["frac"], "n_gpus": world}

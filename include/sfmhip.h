@@ -59,6 +59,9 @@ int         sfmhip_scratch_trim(uint64_t keep);
  * stream that was passed to the library (a destroyed stream's buffers are
  * otherwise freed at the next eviction or trim, after a device sync).      */
 int         sfmhip_scratch_release_stream(void* stream);
+/* Runtime knobs (INTEGRATION.md "Runtime knobs") are read from the environment
+ * once, at the first call; this re-reads them (tests switching a knob).      */
+int         sfmhip_knobs_reload(void);
 
 /* ---- M1: brute-force L2 matching + ratio test --------------------------
  * Replaces the matcher call site matching.py:20,122-128 (LightGlue forward,
@@ -278,10 +281,14 @@ int sfmhip_render_rays_sdf(const float* grid_vm, const float* sdf_plane, int D, 
                            int64_t B, int S, float* rgb, void* stream);
 
 /* ---- V5: TSDF integration (build-defined) --------------
- * T, Wt: (D,H,W) f32 grids updated in place for z-slices [z0, z1).
+ * T, Wt: (D,H,W) f32 grids updated in place for z-slices [z0, z1), laid out
+ * like the sdf.py grid (sdf.py:284-304: x -> W, align_corners).
  * depth [F][Hd][Wd] f32 (<= 0 invalid); poses [F][3][4] world->camera;
  * Kf [F][4] = fx, fy, cx, cy; bmin/bmax are HOST float[3] grid bounds;
- * trunc = truncation distance mu (world units).                               */
+ * trunc = truncation distance mu (world units).  The frames of one integration
+ * step (the call, in steps of at most 512 frames) are fused order-free: per
+ * voxel S = sum rint(tsdf * 2^21) and n updates, then W' = W + n,
+ * T' = f32((f64 T * W + S 2^-21) / (W + n))  (oracle/voxel.py tsdf_integrate).  */
 int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, int z0, int z1,
                           const float* depth, int F, int Hd, int Wd,
                           const float* poses, const float* Kf,

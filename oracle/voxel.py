@@ -7,7 +7,8 @@ float32 restatements with the reference's op order:
                    (bilinear, zeros padding, align_corners=True)
   sh_colour        sdf.py:361-369 / plenoxel.py:9-16
   composite        sdf.py:391-406 / plenoxel.py:71-93
-  tsdf_integrate   build-defined, parity unpinned.
+  tsdf_integrate   build-defined, parity unpinned; order-free
+                   fixed-point fusion (tsdf_integrate_seq: the sequential form).
   block_table      the TSDF pre-pass table (build-defined): {min, max} per 16x16
                    depth block, min poisoned by NaN, max ignoring NaN.
 """
@@ -150,32 +151,14 @@ def render(grid, bmin, bmax, mask_mode, rays_o, rays_d, z) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------
-def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None, grid_depth=None):
-    """Build-defined TSDF update, in place on copies; returns (T, Wt).
+TSDF_STEP = 512        # frames per integration step (tsdf.hip kTsdfMaxFrames)
+TSDF_QBITS = 21        # tsdf fixed point (tsdf.hip kTsdfQBits)
 
-    ``grid_depth``: when given, T/Wt hold only the z-slices [z0, z1) of a grid
-    of that depth (the slab a CPU worker thread owns), else the whole grid.
 
-    Every f32 operation below is one IEEE round-to-nearest step, in the order
-    written (the HIP kernel tsdf_kernel computes exactly these, two voxels per
-    lane in packed f32):
-      voxel (z,y,x) -> v = bmin + idx*(bmax-bmin)/(R-1)  (align_corners, x->W)
-      Q = (P[r,0] vx + P[r,2] vz) + P[r,3];  c_r = P[r,1] vy + Q      (r = X, Y, Z rows)
-      frames with any non-finite or |.| >= 2^60 pose/intrinsic are skipped
-      skip unless 2^-60 <= Zc < 2^60;  iz = 1/Zc
-      pixel = floor((fx Xc) iz + (cx + 0.5)), floor((fy Yc) iz + (cy + 0.5))
-      skip off-image or depth <= 0; sdf = depth - Zc; skip sdf < -mu
-      tsdf = min(1, sdf * (1/mu)); T = (T W + tsdf)/(W + 1); W += 1."""
-    T = np.array(T, F32, copy=True)
-    Wt = np.array(Wt, F32, copy=True)
-    D, H, W = T.shape
-    slab_only = grid_depth is not None
-    if slab_only:
-        z1 = z0 + D if z1 is None else z1
-        if z1 - z0 != D:
-            raise ValueError("slab arrays must hold z1 - z0 slices")
-        D = int(grid_depth)
-    z1 = D if z1 is None else z1
+def _tsdf_frames(Ts, Ws, depth, poses, K, bmin, bmax, trunc, z0, z1, D, step):
+    """Per frame: (ok, ts) of every voxel of the slab [z0, z1) -- the projection and skip
+    rules of the definition, every f32 op one IEEE RN step in the order written."""
+    Dz, H, W = Ts.shape
     mn = np.asarray(bmin, F32).ravel()
     mx = np.asarray(bmax, F32).ravel()
     sx = (mx[0] - mn[0]) / F32(W - 1)
@@ -191,11 +174,11 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None, gri
     tr = F32(trunc)
     inv_tr = F32(1) / tr
     big, zlo, zhi = F32(2.0 ** 60), F32(2.0 ** -60), F32(2.0 ** 60)
-    Ts, Ws = (T, Wt) if slab_only else (T[z0:z1], Wt[z0:z1])
     for f in range(F):
         P = poses[f]
         with np.errstate(invalid="ignore"):
             if not (np.abs(np.concatenate([P, K[f]])) < big).all():
+                yield f, None, None
                 continue
         Xc = P[1] * vy + ((P[0] * vx + P[2] * vz) + P[3])
         Yc = P[5] * vy + ((P[4] * vx + P[6] * vz) + P[7])
@@ -211,11 +194,92 @@ def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None, gri
         ui = np.where(ok, fu, 0).astype(np.int64)
         vi = np.where(ok, fv, 0).astype(np.int64)
         dep = dep_all[f][vi, ui]
-        ok &= dep > 0
-        sdf = dep - Zc
-        ok &= ~(sdf < -tr)
-        ts = np.minimum(F32(1), sdf * inv_tr)
-        Tn = (Ts * Ws + ts) / (Ws + F32(1))
+        with np.errstate(invalid="ignore", over="ignore"):
+            ok &= dep > 0
+            sdf = dep - Zc
+            ok &= ~(sdf < -tr)
+            ts = np.minimum(F32(1), sdf * inv_tr)
+        yield f, ok, ts
+
+
+def _slab_views(T, Wt, z0, z1, grid_depth):
+    T = np.array(T, F32, copy=True)
+    Wt = np.array(Wt, F32, copy=True)
+    D = T.shape[0]
+    slab_only = grid_depth is not None
+    if slab_only:
+        z1 = z0 + D if z1 is None else z1
+        if z1 - z0 != D:
+            raise ValueError("slab arrays must hold z1 - z0 slices")
+        D = int(grid_depth)
+    z1 = D if z1 is None else z1
+    return T, Wt, D, z1, slab_only
+
+
+def tsdf_integrate(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None, grid_depth=None):
+    """Build-defined TSDF integration, on copies; returns (T, Wt).
+    The HIP path (tsdf.hip) computes exactly this, bit for bit.
+
+    ``grid_depth``: when given, T/Wt hold only the z-slices [z0, z1) of a grid
+    of that depth (the slab a CPU worker thread owns), else the whole grid.
+
+    Per voxel and frame (every f32 operation one IEEE round-to-nearest step, in
+    the order written):
+      voxel (z,y,x) -> v = bmin + idx*(bmax-bmin)/(R-1)  (align_corners, x->W: sdf.py:284-304)
+      Q = (P[r,0] vx + P[r,2] vz) + P[r,3];  c_r = P[r,1] vy + Q      (r = X, Y, Z rows)
+      frames with any non-finite or |.| >= 2^60 pose/intrinsic are skipped
+      skip unless 2^-60 <= Zc < 2^60;  iz = 1/Zc
+      pixel = floor((fx Xc) iz + (cx + 0.5)), floor((fy Yc) iz + (cy + 0.5))
+      skip off-image or depth <= 0; sdf = depth - Zc; skip sdf < -mu
+      tsdf = min(1, sdf * (1/mu))
+    The frames of one integration step (512 frames; longer inputs are consecutive
+    steps) are fused order-free:
+      q = rint(tsdf * 2^21) (exact integer);  S = sum q;  n = number of updates
+      where n > 0:  T = f32((f64(T) f64(W) + f64(S) 2^-21) / (f64(W) + n));  W = W + f32(n)
+    which telescopes the running average T = (T W + tsdf)/(W + 1), W += 1 of
+    :func:`tsdf_integrate_seq` (2^-22 per update of the exact mean)."""
+    T, Wt, D, z1, slab_only = _slab_views(T, Wt, z0, z1, grid_depth)
+    Ts, Ws = (T, Wt) if slab_only else (T[z0:z1], Wt[z0:z1])
+    F = np.asarray(depth).shape[0]
+    for s0 in range(0, F, TSDF_STEP):
+        s1 = min(F, s0 + TSDF_STEP)
+        S = np.zeros(Ts.shape, np.int64)
+        n = np.zeros(Ts.shape, np.int64)
+        sl = (np.asarray(depth, F32)[s0:s1], np.asarray(poses, F32).reshape(-1, 12)[s0:s1],
+              np.asarray(K, F32).reshape(-1, 4)[s0:s1])
+        for _, ok, ts in _tsdf_frames(Ts, Ws, *sl, bmin, bmax, trunc, z0, z1, D, s0):
+            if ok is None:
+                continue
+            with np.errstate(invalid="ignore"):
+                q = np.rint(np.where(ok, ts, F32(0)) * F32(2.0 ** TSDF_QBITS))
+            S += q.astype(np.int64)
+            n += ok
+        upd = n > 0
+        with np.errstate(invalid="ignore", over="ignore", divide="ignore"):
+            num = Ts.astype(np.float64) * Ws.astype(np.float64) + S.astype(np.float64) * 2.0 ** -TSDF_QBITS
+            den = Ws.astype(np.float64) + n.astype(np.float64)
+            Tn = (num / den).astype(F32)
+            Wn = (Ws + n.astype(F32)).astype(F32)
+        Ts = np.where(upd, Tn, Ts).astype(F32)
+        Ws = np.where(upd, Wn, Ws).astype(F32)
+    if slab_only:
+        return Ts, Ws
+    T[z0:z1] = Ts
+    Wt[z0:z1] = Ws
+    return T, Wt
+
+
+def tsdf_integrate_seq(T, Wt, depth, poses, K, bmin, bmax, trunc, z0=0, z1=None, grid_depth=None):
+    """The sequential running-average form of the same definition (rounds 1-4 of the
+    build): per frame in order, T = (T W + tsdf)/(W + 1), W += 1, each f32 op one RN
+    step.  tsdf_integrate equals it within the accumulated roundings (tests)."""
+    T, Wt, D, z1, slab_only = _slab_views(T, Wt, z0, z1, grid_depth)
+    Ts, Ws = (T, Wt) if slab_only else (T[z0:z1], Wt[z0:z1])
+    for _, ok, ts in _tsdf_frames(Ts, Ws, depth, poses, K, bmin, bmax, trunc, z0, z1, D, 0):
+        if ok is None:
+            continue
+        with np.errstate(invalid="ignore", over="ignore"):
+            Tn = (Ts * Ws + ts) / (Ws + F32(1))
         Ts = np.where(ok, Tn, Ts).astype(F32)
         Ws = np.where(ok, Ws + F32(1), Ws).astype(F32)
     if slab_only:

@@ -25,6 +25,26 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 
 
+@pytest.fixture(autouse=True)
+def _knobs_follow_env():
+    """Library knobs are read once per process (sfmhip_knobs_reload re-reads them).
+    Autouse and independent of monkeypatch, so this teardown runs after
+    monkeypatch has restored the environment: the next test sees the defaults."""
+    yield
+    abi = sys.modules.get("3d_reconstruction_amd._abi")
+    if abi is not None:
+        abi.knobs_reload()
+
+
+@pytest.fixture
+def knob(monkeypatch):
+    """knob(name, value): set SFMHIP_<name> for this test and reload the library's knobs."""
+    def set_knob(name, value):
+        monkeypatch.setenv("SFMHIP_" + name, str(value))
+        sys.modules["3d_reconstruction_amd._abi"].knobs_reload()
+    return set_knob
+
+
 @pytest.fixture(scope="session")
 def sfm():
     """The product package (directory name is not an identifier)."""

@@ -28,7 +28,7 @@ def test_overlapped_allgather_nccl_single_rank(sfm, gpu):
     try:
         syn = importlib.import_module("3d_reconstruction_amd.synthetic")
         x = syn.superpoint_like(6, 300, 128, seed=5, device=gpu)
-        bank = sfm.DescriptorBank.from_float(x, mode=1)
+        bank = sfm.DescriptorBank.from_float(x, mode=1, exact=False)
         pairs = torch.from_numpy(sfm.all_pairs(6)).to(gpu)
         P = pairs.shape[0]
         ref = bank.match(pairs.cpu().numpy(), ratio=0.75).to(torch.int16)

@@ -42,7 +42,7 @@ def test_match_ragged_pairs_bitexact(sfm, gpu, d, mode):
     for i in range(n_img):
         x[i, nk[i]:] = 0
     pairs = np.array([[0, 1], [1, 0], [0, 2], [2, 3], [3, 0], [4, 0], [0, 4], [1, 1]], np.int32)
-    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=mode)
+    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=mode, exact=False)
     m0, d1, d2 = bank.match(pairs, ratio=0.75, with_dist=True)
     torch.cuda.synchronize()
     q = om.quantize(x, mode)
@@ -78,7 +78,7 @@ def test_match_shifted_operands_identical(sfm, gpu, monkeypatch, lo, hi):
     for shift, exp in (("1", auto), ("0", 0), ("48", 48 if lo >= -48 and hi <= 79 else 0),
                        ("64", 64 if lo >= -64 and hi <= 63 else 0)):
         monkeypatch.setenv("SFMHIP_MATCH_SHIFT", shift)
-        bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=1)
+        bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=1, exact=False)
         assert bank.shift == exp and (bank.qm is not bank.q) == (exp != 0)
         out.append([t.cpu().numpy() for t in bank.match(pairs, ratio=0.8, with_dist=True)])
     q = om.quantize(x, 1)
@@ -107,9 +107,9 @@ def test_match_ties_lowest_index(sfm, gpu):
         dup[i] = j
     qa, qb = qa.astype(np.float32) / 127.0, qb.astype(np.float32) / 127.0
     QA, QB = om.quantize(qa, 1), om.quantize(qb, 1)
-    got = sfm.bf_match(qa, qb, ratio=(1, 1), mode=1)
+    got = sfm.bf_match(qa, qb, ratio=(1, 1), mode=1, exact=False)
     assert np.array_equal(got, om.bf_match_q(QA, QB, (1, 1)))
-    got2 = sfm.bf_match(qa, qb, ratio=(2, 1), mode=1)
+    got2 = sfm.bf_match(qa, qb, ratio=(2, 1), mode=1, exact=False)
     assert np.array_equal(got2, om.bf_match_q(QA, QB, (2, 1)))
     rows = np.array(sorted(dup))
     # the oracle's argmin is the lowest index; the GPU must agree on every tied row
@@ -121,7 +121,7 @@ def test_match_ties_lowest_index(sfm, gpu):
 def test_match_mutual(sfm, gpu):
     x = syn.superpoint_like(3, 512, 128, seed=9).numpy()
     pairs = np.array([[0, 1], [2, 1], [1, 2]], np.int32)
-    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), mode=1)
+    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), mode=1, exact=False)
     m0, m1 = bank.match(pairs, ratio=0.8, mutual=True)
     q = om.quantize(x, 1)
     for p, (a, b) in enumerate(pairs):
@@ -134,7 +134,7 @@ def test_mutual_golden_filter_matches(sfm, gpu):
     """GPU mutual BF == the reference's lightglue filter_matches on the same distances."""
     g = golden("filter_matches_golden.npz")
     qa, qb = g["qa"].astype(np.float32) / 127.0, g["qb"].astype(np.float32) / 127.0
-    bank = sfm.DescriptorBank.from_float([qa, qb], mode=1)
+    bank = sfm.DescriptorBank.from_float([qa, qb], mode=1, exact=False)
     m0, m1 = bank.match(np.array([[0, 1]], np.int32), ratio=(1, 1), mutual=True)
     assert np.array_equal(m0[0, :200].cpu().numpy(), g["m0"])
     assert np.array_equal(m1[0, :180].cpu().numpy(), g["m1"])
@@ -179,7 +179,7 @@ def test_match_c3_full_size_properties(sfm, gpu):
     """C3 geometry at full size (257 x 4096 x 256): 64 pairs spread over the
     pair index space bit-exact vs oracle (every row), plus graph properties."""
     x = syn.superpoint_like(257, 4096, 256, seed=1, device=gpu)
-    bank = sfm.DescriptorBank.from_float(x, mode=1)
+    bank = sfm.DescriptorBank.from_float(x, mode=1, exact=False)
     del x
     pairs = sfm.all_pairs(257)
     m0 = bank.match(pairs)
@@ -239,7 +239,7 @@ def test_match_empty_and_single_keypoint_images(sfm, gpu):
     for i in range(3):
         x[i, nk[i]:] = 0
     pairs = np.array([[0, 2], [2, 0], [1, 2], [2, 1], [0, 1]], np.int32)
-    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=1)
+    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=1, exact=False)
     m0 = bank.match(pairs, ratio=0.75).cpu().numpy()
     q = om.quantize(x, 1)
     ref, _, _ = _oracle_pairs(q, nk, pairs, (3, 4))

@@ -1,5 +1,6 @@
 """GPU: the whole matching stage (BoW graph -> all-pairs mutual BF on MFMA ->
-BFS + tracks) equals the same stage driven by the oracle's matches."""
+BFS + tracks) equals the same stage driven by the oracle's matches (the stage's
+default exact-float semantics: oracle.match.bf_match_exact, bit for bit)."""
 import importlib
 
 import numpy as np
@@ -47,10 +48,8 @@ def test_matching_stage_equals_oracle_driven(sfm, gpu):
     book, _ = ob.codebook(descs, 40, 1, seed=1)
     out = pipe.matching_stage(descs, book, min_matches=200)
     assert len(out["img_pairs"]) >= 3
-    q = [om.quantize(x, 1) for x in descs]
-
-    def oracle_fn(r, i):
-        m0 = om.bf_match_q(q[r], q[i], (3, 4), mutual=True)
+    def oracle_fn(r, i):   # the stage's default: exact-float BF (f32 descriptors, f64 distances)
+        m0 = om.bf_match_exact(descs[r], descs[i], (3, 4), mutual=True)
         idx0 = np.nonzero(m0 >= 0)[0]
         return idx0.astype(np.int64), m0[idx0].astype(np.int64)
 
@@ -73,12 +72,11 @@ def test_matching_stage_with_essential_verification(sfm, gpu):
     book, _ = ob.codebook(descs, 40, 1, seed=1)
     out = pipe.matching_stage(descs, book, min_matches=200, verify="essential", all_points=pts)
     assert len(out["img_pairs"]) >= 3
-    q = [om.quantize(x, 1) for x in descs]
     f = importlib.import_module("3d_reconstruction_amd.synthetic").FOCAL
     K = np.array([[f, 0, 0], [0, f, 0], [0, 0, 1.0]])
 
     def oracle_fn(r, i):
-        m0 = om.bf_match_q(q[r], q[i], (3, 4), mutual=True)
+        m0 = om.bf_match_exact(descs[r], descs[i], (3, 4), mutual=True)
         idx0 = np.nonzero(m0 >= 0)[0]
         return idx0.astype(np.int64), m0[idx0].astype(np.int64)
 

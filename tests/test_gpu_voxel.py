@@ -241,51 +241,58 @@ def _tsdf_case(R=48, F=12, Hd=96, Wd=128, focal=110.0):
     return R, depth.numpy(), poses.numpy(), K.numpy()
 
 
-# "auto": small grids run in latency mode; "0" forces the whole-grid path (refinement
-# pass, per-voxel block test); "heavy*": every sub-tile with a projected frame goes through
-# tsdf_heavy_kernel (frame-split producers + ordered consumer), in either mode, and with a
-# 3-workgroup grid so each workgroup takes several sub-tiles
-LAT_MODES = ["auto", "0", "heavy", "heavy0", "pre0"]
+# "auto": small grids run in latency mode; "0" / "1" force the whole-grid mode (refinement
+# pass, per-voxel block test) / the latency mode; "slots*": a partial-slot capacity of a few
+# slots, so the first split sub-tiles keep their window items and the rest merge into one
+# item each (both forms in one call)
+LAT_MODES = ["auto", "0", "1", "slots", "slots0"]
 
 
-def _set_lat(monkeypatch, lat):
-    if lat in ("auto", "heavy"):
-        pass
-    else:
-        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", "0")
-    if lat == "pre0":   # the pre-pass pipeline: block tables of frame groups on the side stream
-        monkeypatch.setenv("SFMHIP_TSDF_PREPIPE", "3")
-    if lat.startswith("heavy"):
-        monkeypatch.setenv("SFMHIP_TSDF_HEAVY", "1")
-        monkeypatch.setenv("SFMHIP_TSDF_HEAVY_WG", "3")
+def _set_lat(knob, lat):
+    if lat in ("0", "1"):
+        knob("TSDF_LATENCY", lat)
+    elif lat == "slots":
+        knob("TSDF_SLOTS", 5)
+    elif lat == "slots0":
+        knob("TSDF_LATENCY", 0)
+        knob("TSDF_SLOTS", 9)
+
+
+def _close_to_seq(Tg, Wg, Ts, Ws):
+    """The order-free fusion vs the sequential running average (oracle tsdf_integrate_seq):
+    same weights, T within the accumulated roundings (|dT| <= 3e-5 + 1e-4 |T|)."""
+    np.testing.assert_array_equal(Wg, Ws)
+    m = Ws > 0
+    np.testing.assert_allclose(Tg[m], Ts[m], rtol=1e-4, atol=3e-5)
 
 
 @pytest.mark.parametrize("lat", LAT_MODES)
-def test_tsdf_vs_oracle_bitexact(sfm, gpu, monkeypatch, lat):
-    _set_lat(monkeypatch, lat)
+def test_tsdf_vs_oracle_bitexact(sfm, gpu, knob, lat):
+    _set_lat(knob, lat)
     R, depth, poses, K = _tsdf_case()
     T = torch.zeros((R, R, R), dtype=torch.float32, device=gpu)
     W = torch.zeros_like(T)
     sfm.tsdf_integrate(T, W, torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K),
                        (-1, -1, -1), (1, 1, 1), 3 * 2.0 / (R - 1))
-    Tr, Wr = ov.tsdf_integrate(np.zeros((R, R, R), np.float32), np.zeros((R, R, R), np.float32), depth, poses, K,
-                               (-1, -1, -1), (1, 1, 1), np.float32(3 * 2.0 / (R - 1)))
+    args = (depth, poses, K, (-1, -1, -1), (1, 1, 1), np.float32(3 * 2.0 / (R - 1)))
+    Tr, Wr = ov.tsdf_integrate(np.zeros((R, R, R), np.float32), np.zeros((R, R, R), np.float32), *args)
     Tg, Wg = T.cpu().numpy(), W.cpu().numpy()
     np.testing.assert_array_equal(Wg, Wr)
     np.testing.assert_array_equal(Tg, Tr)
     assert (Wg > 0).mean() > 0.2
+    _close_to_seq(Tg, Wg, *ov.tsdf_integrate_seq(np.zeros((R, R, R), np.float32), np.zeros((R, R, R), np.float32),
+                                                 *args))
 
 
 @pytest.mark.parametrize("lat", LAT_MODES)
 @pytest.mark.parametrize("Wd", [96, 97])
-def test_tsdf_edge_cases_bitexact(sfm, gpu, monkeypatch, Wd, lat):
-    """Odd / non-cubic grid (a lane's second voxel off the grid), 30 frames (two
-    frame-chunk launches), prior (T, W) state including values outside the fast
-    division's range, depth holes / negative depth, a camera plane cutting the
-    grid (Zc <= 0), and frames with a NaN pose, an infinite intrinsic and a
-    >= 2^60 translation (skipped as a whole): bit-exact with the oracle."""
-    monkeypatch.setenv("SFMHIP_TSDF_CHUNK", "7")  # several launches; Wd = 97: unaligned depth rows
-    _set_lat(monkeypatch, lat)
+def test_tsdf_edge_cases_bitexact(sfm, gpu, knob, Wd, lat):
+    """Odd / non-cubic grid (a lane's second voxel off the grid), prior (T, W) state
+    including huge, tiny, negative and non-integer values, depth holes / negative
+    depth, a camera plane cutting the grid (Zc <= 0), and frames with a NaN pose, an
+    infinite intrinsic and a >= 2^60 translation (skipped as a whole), unaligned depth
+    rows (Wd = 97): bit-exact with the oracle."""
+    _set_lat(knob, lat)
     D, H, W_ = 20, 33, 45
     F, Hd = 30, 72
     depth, poses, K = syn.tsdf_scene(F, Hd, Wd, focal=80.0, seed=11)
@@ -312,51 +319,74 @@ def test_tsdf_edge_cases_bitexact(sfm, gpu, monkeypatch, Wd, lat):
     assert (Wr > W0).mean() > 0.1
 
 
-def test_tsdf_culling_is_exact(sfm, gpu, monkeypatch):
-    """The (tile, frame) culling pre-pass only drops work and the free-space
-    path only skips gathers: grids with culling off, culling without the
-    free-space path and both on are bit-identical (full-resolution frames,
-    96^3 grid, z-slab), and the free-space path is exercised (probe mode
-    SFMHIP_TSDF_FREE=2 writes tsdf 0.5 there, which must change the grid)."""
+def test_tsdf_multi_step_bitexact(sfm, gpu, knob):
+    """More than 512 frames: the call fuses them in consecutive 512-frame integration
+    steps (each finished before the next), exactly as the oracle defines it; a split
+    call (frames [0, 300) then [300, F)) is a different (also exact) sequence of steps."""
+    knob("TSDF_SLOTS", 4)
+    R, F, Hd, Wd = 20, 530, 24, 32
+    depth, poses, K = syn.tsdf_scene(F, Hd, Wd, focal=30.0, seed=13)
+    depth, poses, K = depth.numpy(), poses.numpy(), K.numpy()
+    rng = np.random.default_rng(7)
+    T0 = rng.uniform(-1, 1, (R, R, R)).astype(np.float32)
+    W0 = rng.integers(0, 3, (R, R, R)).astype(np.float32)
+    bnd = ((-1, -1, -1), (1, 1, 1), np.float32(0.3))
+    T, Wt = torch.from_numpy(T0).to(gpu), torch.from_numpy(W0).to(gpu)
+    sfm.tsdf_integrate(T, Wt, torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K), *bnd)
+    Tr, Wr = ov.tsdf_integrate(T0, W0, depth, poses, K, *bnd)
+    np.testing.assert_array_equal(Wt.cpu().numpy(), Wr)
+    np.testing.assert_array_equal(T.cpu().numpy(), Tr)
+    assert (Wr - W0).max() > 300   # voxels seen by frames of both steps
+    T2, W2 = torch.from_numpy(T0).to(gpu), torch.from_numpy(W0).to(gpu)
+    for a, b in ((0, 300), (300, F)):
+        sfm.tsdf_integrate(T2, W2, torch.from_numpy(depth[a:b]), torch.from_numpy(poses[a:b]),
+                           torch.from_numpy(K[a:b]), *bnd)
+    Ta, Wa = ov.tsdf_integrate(T0, W0, depth[:300], poses[:300], K[:300], *bnd)
+    Ta, Wa = ov.tsdf_integrate(Ta, Wa, depth[300:], poses[300:], K[300:], *bnd)
+    np.testing.assert_array_equal(W2.cpu().numpy(), Wa)
+    np.testing.assert_array_equal(T2.cpu().numpy(), Ta)
+
+
+def test_tsdf_modes_and_splits_identical(sfm, gpu, knob):
+    """Full-resolution frames, 96^3 grid, z-slab: every mode (whole-grid with brick /
+    refinement / per-voxel block test, latency) and every partial-slot capacity (window
+    items vs merged items) gives the same grid bit for bit (integer sums: the split is
+    free), equal to the oracle on sampled slices, with both culling and the free-space
+    path active (cull stats)."""
     depth, poses, K = syn.tsdf_scene(40, seed=3)   # two mask words per sub-tile
+    bnd = ((-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95)
     out = []
-    variants = [dict(CULL="0"), dict(CULL="2", FREE="0"), dict(CULL="2"), dict(CULL="2", FREE="2"),
-                dict(CULL="2", CULLSUB="4"), dict(CULL="2", CHUNK="3"), dict(CULL="2", VOXTEST="0"),
-                dict(CULL="2", CHUNK="512"), dict(CULL="2", REFINE="0"), dict(CULL="2", LATENCY="1"),
-                dict(CULL="2", LATENCY="0"), dict(CULL="2", ORDER="0"), dict(CULL="2", BRICK="0"),
-                dict(CULL="2", BRICK="0", CULLSUB="4"), dict(CULL="2", LATENCY="1", PIPE="0"),
-                dict(CULL="2", LATENCY="1", EASY="0"), dict(CULL="2", EASY="0"),
-                dict(CULL="2", LATENCY="0", REFINE="0"), dict(CULL="2", LATENCY="0", VOXTEST="0"),
-                dict(CULL="2", HEAVY="1"), dict(CULL="2", HEAVY="1", LATENCY="0"),
-                dict(CULL="2", HEAVY="2", HEAVY_WG="5", CHUNK="17"), dict(CULL="2", HEAVY="1", EASY="0"),
-                dict(CULL="2", HEAVY="0", LATENCY="1"),
-                dict(CULL="2", LATENCY="0", PREPIPE="4"), dict(CULL="2", LATENCY="0", PREPIPE="3", CHUNK="17"),
-                dict(CULL="2", LATENCY="0", PREPIPE="8", FREE="0"), dict(CULL="2", LATENCY="0", PREPIPE="2", REFINE="0")]
+    variants = [{}, dict(TSDF_LATENCY=0), dict(TSDF_LATENCY=1), dict(TSDF_SLOTS=1), dict(TSDF_SLOTS=2),
+                dict(TSDF_SLOTS=50, TSDF_LATENCY=0), dict(TSDF_SLOTS=3, TSDF_LATENCY=1), dict(TSDF_SLOTS=1 << 20)]
     for v in variants:
-        for k in ("CULL", "FREE", "CULLSUB", "CHUNK", "VOXTEST", "REFINE", "LATENCY", "ORDER", "BRICK", "PIPE", "EASY",
-                  "HEAVY", "HEAVY_WG", "PREPIPE"):
-            monkeypatch.delenv("SFMHIP_TSDF_" + k, raising=False)
+        knob("TSDF_LATENCY", -1)
+        knob("TSDF_SLOTS", 0)
         for k, x in v.items():
-            monkeypatch.setenv("SFMHIP_TSDF_" + k, x)
+            knob(k, x)
         T = torch.zeros((96, 96, 96), dtype=torch.float32, device=gpu)
         W = torch.zeros_like(T)
-        sfm.tsdf_integrate(T, W, depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95, z0=5, z1=90)
+        sfm.tsdf_integrate(T, W, depth, poses, K, *bnd, z0=5, z1=90)
         out.append((T.cpu(), W.cpu()))
-    for i in [1, 2] + list(range(4, len(variants))):
+    for i in range(1, len(variants)):
         assert torch.equal(out[0][0], out[i][0]) and torch.equal(out[0][1], out[i][1]), variants[i]
     assert (out[0][1] > 0).float().mean() > 0.3
-    assert torch.equal(out[0][1], out[3][1])            # probe: same update pattern ...
-    assert (out[3][0] != out[0][0]).float().mean() > 0.05  # ... and many free-space updates
+    st = sfm.tsdf_cull_stats((96, 96, 96), depth, poses, K, *bnd, z0=5, z1=90)
+    assert st["culled"] > 0.2 * st["tested"] and st["free"] > 0.05 * st["tested"]
+    dc, pc, kc = depth.numpy(), poses.numpy(), K.numpy()
+    zeros = np.zeros((96, 96, 96), np.float32)
+    for z0 in (5, 47, 88):
+        Tr, Wr = ov.tsdf_integrate(zeros, zeros, dc, pc, kc, *bnd[:2], np.float32(bnd[2]), z0, z0 + 2)
+        np.testing.assert_array_equal(out[0][1][z0:z0 + 2].numpy(), Wr[z0:z0 + 2])
+        np.testing.assert_array_equal(out[0][0][z0:z0 + 2].numpy(), Tr[z0:z0 + 2])
 
 
 @pytest.mark.parametrize("lat", LAT_MODES)
 @pytest.mark.parametrize("trunc", [0.1, 0.3, 3 * 2.0 / 31, 0.0625])
-def test_tsdf_free_space_near_trunc_bitexact(sfm, gpu, monkeypatch, trunc, lat):
+def test_tsdf_free_space_near_trunc_bitexact(sfm, gpu, knob, trunc, lat):
     """Frontal planes placed so that whole tiles sit just in front of depth - mu
     (the free-space proof's boundary), several truncation distances, prior
-    (T, W) state: bit-exact with the oracle, with culling + free space forced."""
-    monkeypatch.setenv("SFMHIP_TSDF_CULL", "2")
-    _set_lat(monkeypatch, lat)
+    (T, W) state: bit-exact with the oracle."""
+    _set_lat(knob, lat)
     R, F, Hd, Wd = 32, 6, 64, 80
     rng = np.random.default_rng(int(trunc * 1000))
     zs = (np.float32(-1) + np.arange(R, dtype=np.float32) * (np.float32(2) / np.float32(R - 1)))
@@ -414,10 +444,11 @@ def test_tsdf_with_shared_table_bitexact(sfm, gpu):
     assert (W1 > 0).float().mean() > 0.3
 
 
-def test_tsdf_c5_full_size_slabs_bitexact(sfm, gpu, monkeypatch):
+def test_tsdf_c5_full_size_slabs_bitexact(sfm, gpu, knob):
     """The bench workload itself (C5: 256^3 grid, 257 depth maps 1936x1296, every
-    pre-pass and fast path at its default): three 2-slice z-slabs of the fused
-    grid equal the oracle bit for bit, and culling off gives the same grid."""
+    pre-pass and fast path at its default): three 2-slice z-slabs of the fused grid
+    equal the oracle bit for bit and the sequential running average within 1e-4 rel /
+    3e-5 abs; the latency mode and other partial-slot capacities give the same grid."""
     depth, poses, K = syn.tsdf_scene(257, syn.IMG_H, syn.IMG_W, device=gpu)
     R = 256
     args = (depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / (R - 1))
@@ -427,28 +458,22 @@ def test_tsdf_c5_full_size_slabs_bitexact(sfm, gpu, monkeypatch):
     dc, pc, kc = depth.cpu().numpy(), poses.cpu().numpy(), K.cpu().numpy()
     zeros = np.zeros((R, R, R), np.float32)
     for z0 in (0, 127, 254):
-        Tr, Wr = ov.tsdf_integrate(zeros, zeros, dc, pc, kc, (-1.2,) * 3, (1.2,) * 3, np.float32(3 * 2.4 / (R - 1)),
-                                   z0, z0 + 2)
-        np.testing.assert_array_equal(W[z0:z0 + 2].cpu().numpy(), Wr[z0:z0 + 2])
-        np.testing.assert_array_equal(T[z0:z0 + 2].cpu().numpy(), Tr[z0:z0 + 2])
+        oargs = (dc, pc, kc, (-1.2,) * 3, (1.2,) * 3, np.float32(3 * 2.4 / (R - 1)), z0, z0 + 2)
+        Tr, Wr = ov.tsdf_integrate(zeros, zeros, *oargs)
+        Tg, Wg = T[z0:z0 + 2].cpu().numpy(), W[z0:z0 + 2].cpu().numpy()
+        np.testing.assert_array_equal(Wg, Wr[z0:z0 + 2])
+        np.testing.assert_array_equal(Tg, Tr[z0:z0 + 2])
+        Ts, Ws = ov.tsdf_integrate_seq(zeros, zeros, *oargs)
+        _close_to_seq(Tg, Wg, Ts[z0:z0 + 2], Ws[z0:z0 + 2])
     assert (W > 0).float().mean() > 0.5
     T2, W2 = torch.zeros_like(T), torch.zeros_like(T)
-    monkeypatch.setenv("SFMHIP_TSDF_CULL", "0")
-    sfm.tsdf_integrate(T2, W2, *args)
-    assert torch.equal(T, T2) and torch.equal(W, W2)
-    # the latency mode of thin slabs (no block-table test, no refinement pass; heavy sub-tiles
-    # frame-split) on the full grid, and the whole-grid mode with the heavy path
-    monkeypatch.setenv("SFMHIP_TSDF_CULL", "1")
-    for lat, heavy, pre in (("1", None, None), ("0", "48", None), ("0", "0", "4")):
-        monkeypatch.setenv("SFMHIP_TSDF_LATENCY", lat)
-        if heavy:
-            monkeypatch.setenv("SFMHIP_TSDF_HEAVY", heavy)
-        if pre:
-            monkeypatch.setenv("SFMHIP_TSDF_PREPIPE", pre)
+    for lat, slots in (("1", 0), ("0", 7), ("-1", 20000)):
+        knob("TSDF_LATENCY", lat)
+        knob("TSDF_SLOTS", slots)
         T2.zero_()
         W2.zero_()
         sfm.tsdf_integrate(T2, W2, *args)
-        assert torch.equal(T, T2) and torch.equal(W, W2), (lat, heavy)
+        assert torch.equal(T, T2) and torch.equal(W, W2), (lat, slots)
 
 
 def test_tsdf_zslab_split_equals_whole(sfm, gpu):

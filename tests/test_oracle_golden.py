@@ -174,6 +174,33 @@ def test_tsdf_oracle_planar_known_answer():
     assert (~upd == (exp * 0.2 < -0.2)).all()
 
 
+def test_tsdf_oracle_order_free_vs_sequential():
+    """The order-free fixed-point fusion (the definition the HIP path computes) against
+    the sequential running average: same weights, T within 1e-4 rel / 3e-5 abs, from a
+    prior state; the integration step (512 frames) is the unit of fusion."""
+    import importlib
+    syn = importlib.import_module("3d_reconstruction_amd.synthetic")
+    R, F = 24, 20
+    depth, poses, K = (a.numpy() for a in syn.tsdf_scene(F, 48, 64, focal=60.0, seed=4))
+    rng = np.random.default_rng(2)
+    T0 = rng.uniform(-1, 1, (R, R, R)).astype(np.float32)
+    W0 = rng.integers(0, 5, (R, R, R)).astype(np.float32)
+    args = (depth, poses, K, (-1, -1, -1), (1, 1, 1), np.float32(0.2))
+    Tn, Wn = ov.tsdf_integrate(T0, W0, *args)
+    Ts, Ws = ov.tsdf_integrate_seq(T0, W0, *args)
+    np.testing.assert_array_equal(Wn, Ws)
+    assert (Wn > W0).mean() > 0.2
+    np.testing.assert_allclose(Tn, Ts, rtol=1e-4, atol=3e-5)
+    # slab arrays (grid_depth) give the same slices
+    Tz, Wz = ov.tsdf_integrate(T0[5:11], W0[5:11], *args, z0=5, z1=11, grid_depth=R)
+    assert np.array_equal(Tz, Tn[5:11]) and np.array_equal(Wz, Wn[5:11])
+    # one step vs two calls: a different (but equally close) sequence of steps
+    Ta, Wa = ov.tsdf_integrate(T0, W0, depth[:9], poses[:9], K[:9], *args[3:])
+    Ta, Wa = ov.tsdf_integrate(Ta, Wa, depth[9:], poses[9:], K[9:], *args[3:])
+    np.testing.assert_array_equal(Wa, Ws)
+    np.testing.assert_allclose(Ta, Ts, rtol=1e-4, atol=3e-5)
+
+
 # --- BoW retrieval (§8f row 3) -------------------------------------------------
 def test_bow_oracle_matches_reference():
     from oracle import bow as ob

@@ -33,3 +33,11 @@ for k, c in vals.items():
         print(f"   VALU-active / wave-cycles {avg['SQ_ACTIVE_INST_VALU'] / avg['SQ_WAVE_CYCLES']:.1%}, "
               + (f"wait_any {avg['SQ_WAIT_ANY'] / avg['SQ_WAVE_CYCLES']:.1%}, " if "SQ_WAIT_ANY" in avg else "")
               + (f"wait_inst {avg['SQ_WAIT_INST_ANY'] / avg['SQ_WAVE_CYCLES']:.1%}" if "SQ_WAIT_INST_ANY" in avg else ""))
+    if "GRBM_GUI_ACTIVE" in avg:
+        cyc = avg["GRBM_GUI_ACTIVE"] / 8 * 256   # CU-cycles (8 XCDs x 32 CUs)
+        for n in ("TA_TA_BUSY_sum", "TD_TD_BUSY_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TD_TC_STALL_sum",
+                  "TCP_PENDING_STALL_CYCLES_sum", "TCP_READ_TAGCONFLICT_STALL_CYCLES_sum"):
+            if n in avg:
+                print(f"   {n[:-4]} per CU-cycle {avg[n] / cyc:.1%}")
+        if "SQ_INSTS_VALU" in avg:   # a wave64 VALU op holds its SIMD 4 cycles (4 SIMDs per CU)
+            print(f"   VALU issue per SIMD-cycle ~ {avg['SQ_INSTS_VALU'] * 4 / (cyc * 4):.1%} (x4 cycles per op)")
