@@ -47,7 +47,6 @@ __device__ unsigned long long g_ba_prof[4096 * kProfPhases];
 // scale_inv (3: the column norms, max'ed across Jacobian evaluations); d is stored so that no pass
 // divides (the same IEEE quotient once per Jacobian instead of once per pass)
 constexpr int kRec = 29;
-constexpr int kRecRC = 9;  // RC records: fields 20-28 only (d, X_new, scale_inv)
 
 // sum of K doubles over the workgroup (NW waves); every thread receives the totals in out[]
 template <int NW, int K>
@@ -175,17 +174,13 @@ struct BaState {   // LDS: the iteration's scalars, written by thread 0 or by bl
 };
 
 // A pair's observation records in the scratch block of kRec doubles per
-// observation: AoS (record i at i * kRec) or, SOA, field-major within the pair
-// (field f of record i at f * n + i: a wave's load of one field is 64
-// consecutive doubles).  Passes copy the fields they use into registers.
-template <bool SOA, bool RC = false>
+// observation, field-major within the pair (field f of record i at f * n + i: a
+// wave's load of one field is 64 consecutive doubles; AoS records measured slower,
+// profiles/r3/ba_variants_r3m.txt).  Passes copy the fields they use into registers.
 struct Recs {
     double* base;
     int n;
-    __device__ __forceinline__ double* at(int i, int f) const {
-        if (RC) f -= 20;   // only fields 20-25 are stored
-        return SOA ? base + (size_t)f * n + i : base + (size_t)i * (RC ? kRecRC : kRec) + f;
-    }
+    __device__ __forceinline__ double* at(int i, int f) const { return base + (size_t)f * n + i; }
     template <int LO, int HI>
     __device__ __forceinline__ void load(int i, double* r) const {
 #pragma unroll
@@ -200,8 +195,8 @@ struct Recs {
 
 // for i = tid, tid + NT, ... < n: body(i, r) with r[LO, HI) = record i, the next
 // record's loads issued before the current one's arithmetic (one record ahead)
-template <int NT, int LO, int HI, bool SOA, typename F>
-__device__ __forceinline__ void stream_recs(const Recs<SOA, false>& rec, int n, F&& body) {
+template <int NT, int LO, int HI, typename F>
+__device__ __forceinline__ void stream_recs(const Recs& rec, int n, F&& body) {
     double nx[kRec];
     int i = threadIdx.x;
     if (i < n) rec.template load<LO, HI>(i, nx);
@@ -223,12 +218,7 @@ __device__ __forceinline__ void resid(const double* R, const double* c, const do
     rv = pts[1] - v;
 }
 
-// RC (recompute): the records hold only the point column scales (d and scale_inv, 3 each) and the trial point (3);
-// every pass re-derives the observation's J (18) and f (2) from X, pts and the pair's camera
-// (fd_obs: the same function, the same values as the Jacobian pass) instead of re-reading a
-// 23-double record written by it — ~450 f64 flops per observation and pass against 184 B of
-// record traffic (5.5 GB per launch at 23 % L2 hits).
-template <int NT, bool SOA, bool RC = false>
+template <int NT>
 __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io, const double* __restrict__ Kall,
                                                     double* __restrict__ X, const double* __restrict__ pts2d,
                                                     const int64_t* __restrict__ off, int64_t n_obs, double ftol,
@@ -248,20 +238,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     const double* k = Kall + (size_t)p * 9;
     double* Xp = X + 3 * o0;
     const double* pts = pts2d + 2 * o0;
-    const Recs<SOA, RC> rec{scratch + (size_t)o0 * (RC ? kRecRC : kRec), n};
+    const Recs rec{scratch + (size_t)o0 * kRec, n};
     // the pass view of observation i: r[0..17] J, r[18..19] f, r[20..22] the point column scales d
-    auto pass_rec = [&](int i, double* r) {
-        if constexpr (RC) {
-            const double Xi[3] = {Xp[3 * i], Xp[3 * i + 1], Xp[3 * i + 2]};
-            double f[2];
-            rec.template load<20, 23>(i, r);
-            fd_obs(&S.R[0][0], S.cam, k, Xi, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
-            r[18] = f[0];
-            r[19] = f[1];
-        } else {
-            rec.template load<0, 23>(i, r);
-        }
-    };
+    auto pass_rec = [&](int i, double* r) { rec.template load<0, 23>(i, r); };
     if (tid < 6) S.cam[tid] = cam_io[(size_t)p * 6 + tid];
     __syncthreads();
     if (n == 0) {
@@ -314,8 +293,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 r[26 + c] = si;
                 r[20 + c] = 1.0 / si;
             }
-            if (RC) rec.template store<20, 23>(i, r);
-            else rec.template store<0, 23>(i, r);
+            rec.template store<0, 23>(i, r);
             rec.template store<26, 29>(i, r);
         }
         gmax = block_max<NW>(gmax, S.red);
@@ -697,39 +675,10 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
         set_error("sfmhip_ba_solve: scratch allocation failed");
         return SFMHIP_E_HIP;
     }
-    // SFMHIP_BA_VARIANT (A/B runs): 2 (default) field-major records, 512 threads; 1 field-major, 256 threads;
-    // 0 AoS records, 256 threads; 3 AoS, 512 threads (profiles/r3/ba_variants_r3m.txt)
-    // 4 / 5 / 6: the recompute form (RC) at 512 / 256 / 1024 threads
-    const int variant = [] { const char* e = std::getenv("SFMHIP_BA_VARIANT"); return e ? std::atoi(e) : 2; }();
-    switch (variant) {
-        case 0:
-            hipLaunchKernelGGL((ba_trf_kernel<256, false>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
-                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-            break;
-        case 1:
-            hipLaunchKernelGGL((ba_trf_kernel<256, true>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d, pair_off,
-                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-            break;
-        case 3:
-            hipLaunchKernelGGL((ba_trf_kernel<512, false>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
-                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-            break;
-        case 4:
-            hipLaunchKernelGGL((ba_trf_kernel<512, true, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d,
-                               pair_off, n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-            break;
-        case 5:
-            hipLaunchKernelGGL((ba_trf_kernel<256, true, true>), dim3(n_pairs), dim3(256), 0, st, cam, K, X, pts2d,
-                               pair_off, n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-            break;
-        case 6:
-            hipLaunchKernelGGL((ba_trf_kernel<1024, true, true>), dim3(n_pairs), dim3(1024), 0, st, cam, K, X, pts2d,
-                               pair_off, n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-            break;
-        default:
-            hipLaunchKernelGGL((ba_trf_kernel<512, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off,
-                               n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
-    }
+    // one 512-thread workgroup per pair, field-major records (256 threads, AoS records and the
+    // recompute form measured slower: profiles/r3/ba_variants_r3m.txt, DESIGN.md K3'')
+    hipLaunchKernelGGL((ba_trf_kernel<512>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off, n_obs, ftol,
+                       xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
     const int rc = check_launch("ba_trf_kernel");
     scratch_free(scratch, st);
     return rc;

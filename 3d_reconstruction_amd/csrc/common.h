@@ -58,7 +58,6 @@ void scratch_free(void* p, hipStream_t s);
 // fixed in the code.
 struct Knobs {
     int tsdf_latency;   // SFMHIP_TSDF_LATENCY: -1 auto, 0 whole-grid mode, 1 latency mode
-    int tsdf_slots;     // SFMHIP_TSDF_SLOTS: fusion partial-slot capacity (0: 4 per wave sub-tile)
 };
 const Knobs& knobs();
 

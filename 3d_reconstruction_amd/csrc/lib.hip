@@ -157,7 +157,6 @@ static int env_knob(const char* name, int dflt) {
 static Knobs read_knobs() {
     Knobs k;
     k.tsdf_latency = env_knob("SFMHIP_TSDF_LATENCY", -1);
-    k.tsdf_slots = env_knob("SFMHIP_TSDF_SLOTS", 0);
     return k;
 }
 static Knobs g_knobs;

@@ -431,9 +431,13 @@ __device__ int five_point_group(const double (&q)[5][4], int gl, int gsh, double
             zr -= wr;
             zi -= wi;
             // converged: step at rounding level, or |p(z)| within the rounding noise of Horner
-            // (compared squared: no square roots on the chain)
-            conv = (wr * wr + wi * wi) <= (16 * kDblEps * kDblEps) * (zr * zr + zi * zi) ||
-                   (pr * pr + pim * pim) <= (256 * kDblEps * kDblEps) * (pabs * pabs);
+            // (compared squared: no square roots on the chain).  Magnitudes >= 2^500 are scaled
+            // by 2^-600 first (exact), so no square overflows into a trivially true test.
+            const double sc = (pabs >= 0x1p500 || az >= 0x1p500 || fabs(wr) + fabs(wi) >= 0x1p500) ? 0x1p-600 : 1.0;
+            const double wrs = wr * sc, wis = wi * sc, zrs = zr * sc, zis = zi * sc;
+            const double prs = pr * sc, pis = pim * sc, pas = pabs * sc;
+            conv = (wrs * wrs + wis * wis) <= (16 * kDblEps * kDblEps) * (zrs * zrs + zis * zis) ||
+                   (prs * prs + pis * pis) <= (256 * kDblEps * kDblEps) * (pas * pas);
         }
         wave_sync_lds();
         if ((((unsigned)(__ballot(!conv) >> gsh)) & 0xFFFFu) == 0u) {

@@ -12,9 +12,8 @@
 //     T' = f32( (f64(T) f64(W) + f64(S) 2^-21) / (f64(W) + n) )
 // which telescopes the sequential T <- (T W + tsdf)/(W + 1), W <- W + 1 (within
 // 2^-22 per update of the exact average; tests/test_gpu_voxel.py checks it against
-// the sequential restatement too).  Order freedom is what lets the frames of a
-// surface sub-tile be split over several waves and the frames be fused window by
-// window across the whole grid: no per-voxel update chain, no per-frame division.
+// the sequential restatement too): no per-voxel update chain, no per-frame division,
+// and any split of the frames (tiles, waves, ranks) gives the same bits.
 //
 // Pipeline per step (one launch of each kernel):
 //   tsdf_setup_kernel     validated camera records (f32 for the fusion, f64 CullCam
@@ -24,11 +23,9 @@
 //   coarse_table_kernel + tsdf_brick_kernel   (whole-grid mode) brick pre-pass
 //   tsdf_cull_kernel      exact (tile, frame) culling / free-space proofs -> masks
 //   tsdf_refine_kernel    (whole-grid mode) the projected pairs again per wave sub-tile
-//   tsdf_items_kernel     work items (wave sub-tile, 32-frame window) into per-window lists
-//   tsdf_fuse_kernel      persistent, window-major: one wave per item, integer (S, n) in
-//                         registers; a one-item sub-tile finishes its voxels in place,
-//                         the items of a split sub-tile store partial sums
-//   tsdf_finish_kernel    split sub-tiles: partials summed, T/W finished
+//   tsdf_order_kernel     longest-first workgroup order per XCD class
+//   tsdf_fuse_kernel      one wave per 8x2x8 sub-tile: integer (S, n) in registers over
+//                         the step's frames, then the voxels finished in place
 // All fp32/fp64 with -ffp-contract=off so the op order matches the oracle.
 #include "common.h"
 #include <climits>
@@ -368,14 +365,16 @@ __global__ __launch_bounds__(256) void tsdf_brick_kernel(int H, int W, int z0, i
 // tile are packed through LDS and stored as the low or high half of its mask word in
 // each of the tile's 4 wave slots.  Masks are [wave slot][nw] words, bit j of word w =
 // frame 32 w + j.  With `plist`, every (tile, frame) that is neither culled nor free
-// space is appended to a list for tsdf_refine_kernel.
+// space is appended to a list for tsdf_refine_kernel; `tcost` sums each tile's cost
+// (4 x projected + free-space frames per wave slot, before refinement) for the
+// fusion's longest-first order.
 constexpr int kCullFrames = 16;
 // waves_per_eu(8): two 16-wave workgroups per CU (the f64 frame record lives in SGPRs)
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void tsdf_cull_kernel(
     int H, int W, int z0, int z1, int F, int Hd, int Wd, const CullCam* __restrict__ cams, CullGeom G, float trunc,
     const float2* __restrict__ bmm, int nbu, int nbv, const int4* __restrict__ range, int nw,
     const unsigned char* __restrict__ bdec, unsigned short* __restrict__ cull, unsigned short* __restrict__ freem,
-    unsigned* __restrict__ plist, unsigned* __restrict__ pcount) {
+    unsigned* __restrict__ plist, unsigned* __restrict__ pcount, unsigned* __restrict__ tcost) {
     __shared__ unsigned char bits[kCullFrames][64];
     __shared__ unsigned wcnt[kCullFrames + 1];
     const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
@@ -432,6 +431,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             const unsigned b = bits[q][l];
             cw |= (b & 1u) << q;
             fw |= (b >> 1) << q;
+        }
+        if (tcost) {   // the fusion's workgroup order: 4 x projected + free-space frames per wave sub-tile
+            const int nlive = min(kCullFrames, F - hf * kCullFrames);
+            const unsigned live = nlive >= kCullFrames ? 0xFFFFu : (nlive > 0 ? (1u << nlive) - 1u : 0u);
+            const unsigned c = 4u * __popc(live & ~cw & ~fw) + __popc(live & fw & ~cw);
+            if (c) atomicAdd(tcost + tile, 4u * c);
         }
         for (int q = 0; q < kCullSub; ++q) {
             const int64_t h = ((tile * kCullSub + q) * nw) * 2 + hf;   // half hf of word hf / 2
@@ -494,7 +499,7 @@ __device__ __forceinline__ void tsdf_cam_record(const float* __restrict__ poses,
 // Per-step setup in one launch: per frame the fusion's f32 record, the culling
 // passes' CullCam and the slab's block range (range_mode 1: every block, an external
 // table; 2: the slab's footprint); the workgroups past the frames zero the step's
-// counters (nzero words: the per-tile costs, the refinement-list and share counters).
+// counters (nzero words: the refinement-list counter and the per-tile costs).
 __global__ __launch_bounds__(64) void tsdf_setup_kernel(const float* __restrict__ poses, const float* __restrict__ Kf,
                                                         int F, float* __restrict__ rec, CullCam* __restrict__ ccam,
                                                         int range_mode, int H, int W, int z0, int z1, int Hd, int Wd,
@@ -527,94 +532,98 @@ __global__ __launch_bounds__(64) void tsdf_setup_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Work items.  The fusion runs frame-window-major: item = (wave sub-tile, mask word w,
-// i.e. the window of frames 32 w .. 32 w + 31) for every sub-tile with a projected
-// frame in the window, and the persistent fusion grid walks the windows in order, so
-// at any time the GPU gathers from the depth lines of about one window of frames (a
-// call's distinct gathered lines are ~0.9 GB, 3.5 MB per frame: tools/sim_gather_lines.py)
-// instead of every wave walking all frames on its own schedule (5.5 GB fetched, L2 hit
-// 23 %, TD 95 % busy stalled on the cache: profiles/r5).  Integer sums make the split
-// exact.  Per sub-tile (tsdf_items_kernel, one lane each):
-//   m = number of windows with a projected frame; nitem[sub] = m (1 when merged)
-//   m == 1: its one item also adds the free-space frames and finishes the voxels in place
-//   m >= 2: m consecutive partial slots [pslot, pslot + m) (one atomic per wave); item r
-//           stores (S0, S1, n0 | n1 << 16) in slot pslot + r; the sub-tile is listed for
-//           tsdf_finish_kernel (partials + free space, then T/W)
-//   m == 0 with free-space frames: listed for tsdf_finish_kernel only
-// A reservation past the partial capacity merges the sub-tile into one item over all
-// windows (flag bit 31, in the list of its first window): still exact.
-// list[w][k]: sub | r << 27 | merged << 31;  cnt: [kCntPart] partial slots,
-// [kCntFin] finish list, [kCntList + w] list w.
-constexpr int kCntPl = 0, kCntPart = 1, kCntFin = 2, kCntList = 4, kNCnt = kCntList + kTsdfMaxFrames / 32;
-constexpr unsigned kItemMerged = 1u << 31;
+// Fusion workgroup order.  One 8x8x8 tile per workgroup (4 waves = its 4 wave
+// sub-tiles).  Spatially compact "super-bricks" of SB_X x SB_Y x SB_Z tiles, dealt
+// round-robin over the 8 XCDs (the 1-D grid's slot % 8 is its XCD): workgroups resident
+// on one XCD at the same time project onto one compact image region per frame, so the
+// depth lines they gather meet in that XCD's L2, and the round-robin spreads the uneven
+// culled work (the floor plane, the spheres) over the XCDs (speed only, never
+// correctness).  A y-band per XCD instead (every ray of the nearly horizontal orbit
+// cameras in one XCD) measured 1.97 vs 1.17 ms: the floor's band holds most of the work.
+//   tsdf_slot_tile: (slot) -> tile, false for padding slots
+//   tsdf_order_kernel: longest-first order within each XCD class (the cull pass sums each
+//     tile's cost): the surface tiles, up to ~10x the work of a free-space tile, would
+//     otherwise land in the last round of a short call (a z-slab of an N-way split).
+struct SlotMap { int ntx, nty, ntz, sbx, sby, sbz, nsx, nsy, per; };   // per: slots per XCD class
 
-// wave-aggregated append: returns this lane's index (lanes with !want get garbage)
-__device__ __forceinline__ unsigned wave_append(unsigned* ctr, bool want, unsigned n_each = 1u) {
-    const uint64_t b = __builtin_amdgcn_ballot_w64(want);
-    if (b == 0) return 0u;
-    const int lane = threadIdx.x & 63;
-    const int first = __builtin_ctzll(b);
-    unsigned base = 0u;
-    if (lane == first) base = atomicAdd(ctr, (unsigned)__builtin_popcountll(b) * n_each);
-    base = __shfl(base, first, 64);
-    return base + (unsigned)__builtin_popcountll(b & ((1ull << lane) - 1ull)) * n_each;
+static SlotMap make_slot_map(int ntx, int nty, int ntz) {
+    SlotMap m;
+    m.ntx = ntx;
+    m.nty = nty;
+    m.ntz = ntz;
+    // 3 x 2 x 8 tiles (24 x 16 x 64 voxels): sweeps in tools/bench_tsdf_variants.py (round 2)
+    m.sbx = 3;
+    m.sby = 2;
+    m.sbz = std::min(8, ntz);
+    m.nsx = ceil_div(ntx, m.sbx);
+    m.nsy = ceil_div(nty, m.sby);
+    const int nsb = m.nsx * m.nsy * ceil_div(ntz, m.sbz);
+    m.per = ceil_div(nsb, kNumXcd) * m.sbx * m.sby * m.sbz;   // padding super-bricks exit at once
+    return m;
 }
 
-__global__ __launch_bounds__(256) void tsdf_items_kernel(const unsigned* __restrict__ cull,
-                                                         const unsigned* __restrict__ freem, int nw, int F,
-                                                         int64_t nsub, unsigned pcap,
-                                                         unsigned char* __restrict__ nitem,
-                                                         unsigned* __restrict__ pslot, unsigned* __restrict__ list,
-                                                         unsigned* __restrict__ cnt, unsigned* __restrict__ fin) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    unsigned pw = 0u;   // windows with a projected frame
-    int kfree = 0;
-    if (i < nsub) {
-        for (int w = 0; w < nw; ++w) {
-            const int w0 = w << 5;
-            const unsigned live = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u);
-            const unsigned todo = live & ~cull[i * nw + w];
-            const unsigned fr = todo & freem[i * nw + w];
-            if (todo & ~fr) pw |= 1u << w;
-            kfree += __builtin_popcount(fr);
-        }
-    }
-    const int m = __builtin_popcount(pw);
-    // m >= 2: m partial slots (variable count per lane: wave prefix sum, one atomic)
-    const int want = m >= 2 ? m : 0;
-    int incl = want;
+__device__ __forceinline__ bool tsdf_slot_tile(int slot, const SlotMap& m, int& tx, int& ty, int& tz) {
+    const int j = slot / kNumXcd, sbn = m.sbx * m.sby * m.sbz;
+    const int sb = (j / sbn) * kNumXcd + slot % kNumXcd, in = j % sbn;
+    tx = (sb % m.nsx) * m.sbx + in % m.sbx;
+    ty = ((sb / m.nsx) % m.nsy) * m.sby + (in / m.sbx) % m.sby;
+    tz = (sb / (m.nsx * m.nsy)) * m.sbz + in / (m.sbx * m.sby);
+    return tx < m.ntx && ty < m.nty && tz < m.ntz;
+}
+
+constexpr int kOrderBuckets = 64;
+__device__ __forceinline__ unsigned slot_bucket(int s, const SlotMap& m, int F, const unsigned* __restrict__ tcost) {
+    int tx, ty, tz;
+    const bool ok = tsdf_slot_tile(s, m, tx, ty, tz);
+    const unsigned cost = ok ? tcost[((size_t)tz * m.nty + ty) * m.ntx + tx] : 0u;
+    return min((unsigned)(kOrderBuckets - 1), cost * kOrderBuckets / (16u * F + 1u));
+}
+
+// One workgroup per XCD class, stable counting sort of the class's slots by cost
+// bucket, heaviest first: order[x + 8 k] = k-th slot.  Dynamic LDS: one bucket byte per
+// slot of the class (m <= 30000, host-checked).
+__global__ __launch_bounds__(256) void tsdf_order_kernel(SlotMap SM, int F, const unsigned* __restrict__ tcost,
+                                                         unsigned* __restrict__ order) {
+    __shared__ unsigned short hist[kOrderBuckets][256];
+    __shared__ unsigned wsum[4];
+    extern __shared__ unsigned char bk[];
+    const int x = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int m = SM.per;   // slots x, x+8, ... of this class
+    const int per = (m + 255) / 256, j0 = min(m, t * per), j1 = min(m, j0 + per);
+    for (int b = 0; b < kOrderBuckets; ++b) hist[b][t] = 0;
+    for (int j = t; j < m; j += 256)   // coalesced over the class: every cost load in flight
+        bk[j] = (unsigned char)slot_bucket(x + kNumXcd * j, SM, F, tcost);
+    __syncthreads();
+    for (int j = j0; j < j1; ++j) ++hist[bk[j]][t];
+    __syncthreads();
+    // exclusive scan over (bucket descending, thread): thread u owns entries [64u, 64u + 64)
+    unsigned run = 0;
+    for (int e = 64 * t; e < 64 * t + 64; ++e) run += hist[kOrderBuckets - 1 - e / 256][e % 256];
+    unsigned incl = run;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        const int up = __shfl_up(incl, off, 64);
+        const unsigned up = __shfl_up(incl, off, 64);
         if (lane >= off) incl += up;
     }
-    const int tot = __shfl(incl, 63, 64);
-    unsigned base = 0u;
-    if (tot > 0) {
-        if (lane == 0) base = atomicAdd(cnt + kCntPart, (unsigned)tot);
-        base = __shfl(base, 0, 64);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    unsigned base = 0;
+    for (int w = 0; w < wv; ++w) base += wsum[w];
+    run = base + incl - run;
+    for (int e = 64 * t; e < 64 * t + 64; ++e) {
+        unsigned short& h = hist[kOrderBuckets - 1 - e / 256][e % 256];
+        const unsigned v = h;
+        h = (unsigned short)run;   // positions < m <= 65535
+        run += v;
     }
-    const unsigned pb = base + (unsigned)(incl - want);
-    const bool merged = want > 0 && pb + (unsigned)want > pcap;
-    const int ms = merged ? 1 : m;
-    if (i < nsub) {
-        nitem[i] = (unsigned char)ms;
-        if (ms >= 2) pslot[i] = pb;
-    }
-    const bool need_fin = i < nsub && (ms >= 2 || (m == 0 && kfree > 0));
-    const unsigned fpos = wave_append(cnt + kCntFin, need_fin);
-    if (need_fin) fin[fpos] = (unsigned)i;
-    const unsigned first = pw ? (unsigned)__builtin_ctz(pw) : 0u;
-    for (int w = 0; w < nw; ++w) {   // one atomic per wave and window
-        const bool has = i < nsub && (merged ? w == (int)first : ((pw >> w) & 1u));
-        const unsigned pos = wave_append(cnt + kCntList + w, has);
-        if (has) {
-            const unsigned r = merged ? 0u : (unsigned)__builtin_popcount(pw & ((1u << w) - 1u));
-            list[(size_t)w * nsub + pos] = (unsigned)i | (r << 27) | (merged ? kItemMerged : 0u);
-        }
+    __syncthreads();
+    for (int j = j0; j < j1; ++j) {
+        const unsigned pos = hist[bk[j]][t]++;
+        order[x + kNumXcd * pos] = (unsigned)(x + kNumXcd * j);
     }
 }
+
+constexpr int kCntPl = 0, kNCnt = 4;   // counters: the refinement list
 
 // Voxel of lane l in wave sub-tile q of tile (bx, by, bz): each 16-lane quarter-wave
 // is a 4x4 (x, z) patch at one y (the orbiting cameras map y to image rows: a compact
@@ -645,18 +654,6 @@ struct FrameCtx {
     int nbytes, Wd4, Hd, Wd, nbu, nbv;
     float trunc, inv_trunc;
 };
-
-// the free-space frames of a sub-tile over the step (every window)
-__device__ __forceinline__ int sub_free(const unsigned* __restrict__ cull, const unsigned* __restrict__ freem,
-                                       size_t slot, int nw, int F) {
-    int k = 0;
-    for (int w = 0; w < nw; ++w) {
-        const int w0 = w << 5;
-        const unsigned live = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u);
-        k += __builtin_popcount(live & ~cull[slot + w] & freem[slot + w]);
-    }
-    return __builtin_amdgcn_readfirstlane(k);
-}
 
 // The same evaluation for NF frames at once, in stages, so that every stage's loads
 // of all NF frames are in flight together (one basic block: the boolean logic is
@@ -750,21 +747,41 @@ __device__ __forceinline__ void frames_eval(const FrameCtx& c, const int* f, flo
     }
 }
 
-// One work item (sub-tile, window w; merged: every window): its projected frames,
-// evaluated two at a time, summed in registers; a one-item sub-tile adds its free-space
-// frames and finishes its voxels in place (grid read and written once, only where a
-// voxel updated), else the sums go to the item's partial slot.
+// One wave = one wave sub-tile (8 x 2 x 8 voxels, two per lane): a sub-tile with every
+// frame culled returns before touching the grid.  Walks the sub-tile's mask words
+// (scalar): culled frames are skipped, free-space frames add 2^21 and 1 per voxel, the
+// projected frames are evaluated two at a time (three or four in flight measured the
+// same: 1.13 / 1.16 ms, profiles/r5).  The voxels are finished in place (grid read and
+// written once, only where a voxel updated).
+// Splitting a surface sub-tile's frames over several waves (integer sums make any split
+// exact; partial sums + a finish pass) measured slower in both modes: whole grid 1.19 vs
+// 1.13 ms, an N = 8 slab 0.33 vs 0.28 ms (profiles/r5): the fusion is bound by the gather
+// traffic, not by its longest sub-tiles.  Walking each wave's frames from a wall-clock
+// phase (so that resident waves gather from the same frames at the same time) and
+// frame-window-major work lists (32-frame windows over the whole grid, partial sums)
+// did not raise the L2 hit rate (23 -> 26 %) and measured slower too.
 template <bool VT>
-__device__ __forceinline__ void fuse_item(float* __restrict__ T, float* __restrict__ Wt, int D, int H, int W, int z0,
-                                          int z1, const FrameCtx& c, const GridBox& B, int F,
-                                          const unsigned* __restrict__ cull, const unsigned* __restrict__ freem,
-                                          int nw, const unsigned char* __restrict__ nitem,
-                                          const unsigned* __restrict__ pslot, int4* __restrict__ partial,
-                                          unsigned e, int w, int l) {
-    const int64_t sub = e & ((1u << 27) - 1u);
-    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
+__global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, float* __restrict__ Wt, int D,
+                                                        int H, int W, int z0, int z1, FrameCtx c, GridBox B, int F,
+                                                        SlotMap SM, const unsigned* __restrict__ cull,
+                                                        const unsigned* __restrict__ freem, int nw,
+                                                        const unsigned* __restrict__ order) {
+    const int l = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    int tx, ty, tz;
+    if (!tsdf_slot_tile(order ? (int)order[blockIdx.x] : (int)blockIdx.x, SM, tx, ty, tz)) return;
+    const int64_t sub = (((int64_t)tz * SM.nty + ty) * SM.ntx + tx) * kCullSub + wave;
+    const size_t slot = (size_t)sub * nw;
+    {   // every frame culled for this wave: the grid is not even read
+        unsigned any = 0u;
+        for (int w = 0; w < nw; ++w) {
+            const int w0 = w << 5;
+            any |= ~cull[slot + w] & (F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u));
+        }
+        if (__builtin_amdgcn_readfirstlane((int)any) == 0) return;
+    }
     int x, y, z;
-    sub_voxel(sub, ntx, nty, z0, l, x, y, z);
+    sub_voxel(sub, SM.ntx, SM.nty, z0, l, x, y, z);
     if (y >= H) return;                      // wave-uniform (a ragged last tile row)
     const bool in0 = x < W && z < z1;
     const bool two = in0 && y + 1 < H;
@@ -775,6 +792,7 @@ __device__ __forceinline__ void fuse_item(float* __restrict__ T, float* __restri
     const f2 vy = {B.mn[1] + (float)y * sy, B.mn[1] + (float)(y + 1) * sy};
     const float vz = B.mn[2] + (float)z * sz;
     int S0 = 0, S1 = 0, n0 = 0, n1 = 0;
+    int kfree = 0;                           // free-space frames
     int pend = -1;                           // a projected frame waiting for its pair
     auto add = [&](int q0, int q1, bool g0, bool g1) {
         S0 += g0 ? q0 : 0;
@@ -782,14 +800,13 @@ __device__ __forceinline__ void fuse_item(float* __restrict__ T, float* __restri
         S1 += g1 ? q1 : 0;
         n1 += g1 ? 1 : 0;
     };
-    const size_t slot = (size_t)sub * nw;
-    const bool merged = (e & kItemMerged) != 0u;
-    const int wa = merged ? 0 : w, wb = merged ? nw : w + 1;
-    for (int ww = wa; ww < wb; ++ww) {
-        const int w0 = ww << 5;
+    for (int w = 0; w < nw; ++w) {
+        const int w0 = w << 5;
         const unsigned live = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u);
-        const unsigned todo = (unsigned)__builtin_amdgcn_readfirstlane((int)(live & ~cull[slot + ww]));
-        unsigned proj = todo & ~(unsigned)__builtin_amdgcn_readfirstlane((int)freem[slot + ww]);
+        const unsigned todo = (unsigned)__builtin_amdgcn_readfirstlane((int)(live & ~cull[slot + w]));
+        const unsigned fre = (unsigned)__builtin_amdgcn_readfirstlane((int)freem[slot + w]) & todo;
+        unsigned proj = todo & ~fre;
+        kfree += __builtin_popcount(fre);
         while (proj) {
             const int f = w0 + __builtin_ctz(proj);
             proj &= proj - 1u;
@@ -813,12 +830,7 @@ __device__ __forceinline__ void fuse_item(float* __restrict__ T, float* __restri
         frames_eval<VT, 1>(c, ff, vx, vy, vz, two, qa, qb, ga, gb);
         add(qa[0], qb[0], ga[0], gb[0]);
     }
-    if (nitem[sub] > 1) {   // split: partial sums of every lane (fixed slot)
-        partial[(size_t)(pslot[sub] + ((e >> 27) & 15u)) * 64 + l] = make_int4(S0, S1, n0 | (n1 << 16), 0);
-        return;
-    }
-    const int kfree = sub_free(cull, freem, slot, nw, F);   // free space: tsdf = 1 for every voxel
-    S0 += kfree << kTsdfQBits;
+    S0 += kfree << kTsdfQBits;   // free space: tsdf = 1 for every voxel of the sub-tile
     S1 += kfree << kTsdfQBits;
     n0 += kfree;
     n1 += kfree;
@@ -838,97 +850,12 @@ __device__ __forceinline__ void fuse_item(float* __restrict__ T, float* __restri
     }
 }
 
-// Persistent fusion grid: the windows in order; the items of window w are dealt in 8
-// contiguous chunks, one per XCD (workgroup b runs on XCD b % 8; the list is in sub-tile
-// order, so each XCD works on one compact region of the grid), and the waves of an XCD
-// stride over its chunk.  A wave that finishes window w starts on w + 1 at once.
-template <bool VT>
-__global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, float* __restrict__ Wt, int D,
-                                                        int H, int W, int z0, int z1, FrameCtx c, GridBox B, int F,
-                                                        const unsigned* __restrict__ cull,
-                                                        const unsigned* __restrict__ freem, int nw,
-                                                        const unsigned char* __restrict__ nitem,
-                                                        const unsigned* __restrict__ pslot,
-                                                        const unsigned* __restrict__ list, int64_t nsub,
-                                                        const unsigned* __restrict__ cnt,
-                                                        int4* __restrict__ partial) {
-    const int l = threadIdx.x & 63;
-    const unsigned wave = (unsigned)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const unsigned xcd = blockIdx.x % kNumXcd;
-    const unsigned nwg = (gridDim.x - xcd + kNumXcd - 1) / kNumXcd;   // workgroups on this XCD
-    const unsigned lw = (blockIdx.x / kNumXcd) * 4u + wave, wx = nwg * 4u;
-    for (int w = 0; w < nw; ++w) {
-        const unsigned n = cnt[kCntList + w];
-        const unsigned per = (n + kNumXcd - 1) / kNumXcd;
-        const unsigned k1 = min(n, (xcd + 1) * per);
-        for (unsigned k = xcd * per + lw; k < k1; k += wx)
-            fuse_item<VT>(T, Wt, D, H, W, z0, z1, c, B, F, cull, freem, nw, nitem, pslot, partial,
-                          list[(size_t)w * nsub + k], w, l);
-    }
-}
-
-// Split sub-tiles (and free-space-only ones): one wave each sums its partials in slot
-// order (integers: any order gives the same sums), adds the free-space frames and
-// finishes the voxels.
-__global__ __launch_bounds__(256) void tsdf_finish_kernel(float* __restrict__ T, float* __restrict__ Wt, int H,
-                                                          int W, int z0, int z1, int F, int nw,
-                                                          const unsigned* __restrict__ cull,
-                                                          const unsigned* __restrict__ freem,
-                                                          const unsigned* __restrict__ fin,
-                                                          const unsigned* __restrict__ cnt,
-                                                          const unsigned char* __restrict__ nitem,
-                                                          const unsigned* __restrict__ pslot,
-                                                          const int4* __restrict__ partial) {
-    const int l = threadIdx.x & 63;
-    const unsigned nf = cnt[kCntFin];
-    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
-    for (unsigned k = blockIdx.x * 4u + (threadIdx.x >> 6); k < nf; k += gridDim.x * 4u) {
-        const int64_t sub = fin[k];
-        int x, y, z;
-        sub_voxel(sub, ntx, nty, z0, l, x, y, z);
-        if (y >= H) continue;
-        const int m = nitem[sub];
-        int S0 = 0, n0 = 0, S1 = 0, n1 = 0;
-        if (m > 1) {
-            const int4* p = partial + (size_t)pslot[sub] * 64 + l;
-            for (int j = 0; j < m; ++j) {
-                const int4 v = p[(size_t)j * 64];
-                S0 += v.x;
-                S1 += v.y;
-                n0 += v.z & 0xFFFF;
-                n1 += v.z >> 16;
-            }
-        }
-        const int kfree = sub_free(cull, freem, (size_t)sub * nw, nw, F);
-        S0 += kfree << kTsdfQBits;
-        S1 += kfree << kTsdfQBits;
-        n0 += kfree;
-        n1 += kfree;
-        if (x >= W || z >= z1) continue;
-        const size_t idx = ((size_t)z * H + y) * W + x;
-        if (n0 > 0) {
-            float t = T[idx], wt = Wt[idx];
-            tsdf_finish_voxel(t, wt, S0, n0);
-            T[idx] = t;
-            Wt[idx] = wt;
-        }
-        if (y + 1 < H && n1 > 0) {
-            float t = T[idx + W], wt = Wt[idx + W];
-            tsdf_finish_voxel(t, wt, S1, n1);
-            T[idx + W] = t;
-            Wt[idx + W] = wt;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
-// Host.  Knobs (read once, sfmhip_knobs_reload re-reads them: lib.hip):
+// Host.  Knob (read once, sfmhip_knobs_reload re-reads it: lib.hip):
 //   SFMHIP_TSDF_LATENCY  -1 auto (default), 0 whole-grid mode, 1 latency mode
-//   SFMHIP_TSDF_SLOTS    partial-slot capacity (0: 4 per sub-tile; tests force a few, so
-//                        that most split sub-tiles merge into one item)
-// Latency mode (few resident rounds of fusion waves: a z-slab of an N-way split):
-// no brick pre-pass, no refinement pass, no per-voxel block test (each costs more
-// than it saves when the call is bound by its longest waves).
+// Latency mode (few resident rounds of fusion waves: a z-slab of an N-way split): no
+// brick pre-pass, no refinement pass, no per-voxel block test (each costs more than it
+// saves when the call is bound by its longest waves: N = 8 slab 0.39 vs 0.44 ms, round 3).
 // stats != nullptr: run only the culling pre-passes and count (wave sub-tile, frame)
 // pairs: stats[0] tested, [1] culled, [2] free space (layer_stats: per 8-voxel z layer).
 // ext_table != nullptr: the caller's {min, max} block table of every frame over the
@@ -949,6 +876,9 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const int nbx = ceil_div(W, kTsdfTX), nby = ceil_div(H, kTsdfTY), nbz = ceil_div(z1 - z0, kTsdfTZ);
     const int64_t ntiles = (int64_t)nbx * nby * nbz, nsub = ntiles * kCullSub;
     SFMHIP_REQUIRE(nsub < (1 << 27) && ntiles < (1 << 23), "sfmhip_tsdf_integrate: grid too large");
+    const SlotMap sm = make_slot_map(nbx, nby, nbz);
+    const int64_t main_slots = (int64_t)sm.per * kNumXcd;
+    SFMHIP_REQUIRE(main_slots < INT_MAX / 2, "sfmhip_tsdf_integrate: grid too large");
     const Knobs& kn = knobs();
     int ncu = 256;
     {
@@ -984,12 +914,12 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const int ncbu = ceil_div(nbu, kCoarse), ncbv = ceil_div(nbv, kCoarse);
     // refinement list capacity: one entry per (tile, frame)
     const int64_t plist_cap = ntiles * 32 * nwmax;
-    // partial slots (1 KB of (S, n) sums each): 4 per sub-tile by default
-    const unsigned pcap = (unsigned)std::min<int64_t>(kn.tsdf_slots > 0 ? kn.tsdf_slots : nsub * 4, 1 << 22);
-    // scratch (stream-ordered, one block): counters first (zeroed by the setup kernel)
+    const bool order = !stats && sm.per <= 30000;
+    // scratch (stream-ordered, one block): counters + per-tile costs first (zeroed by the setup kernel)
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_cnt = take(kNCnt * sizeof(unsigned));
+    const int nzero = kNCnt + (order ? (int)ntiles : 0);
+    const size_t o_cnt = take((size_t)nzero * sizeof(unsigned));
     const size_t o_rec = take((size_t)cf * 16 * sizeof(float));
     const size_t o_cam = take((size_t)cf * sizeof(CullCam));
     const size_t o_rng = take((size_t)cf * sizeof(int4));
@@ -999,11 +929,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const size_t o_ctab = brick ? take((size_t)cf * ncbu * ncbv * sizeof(float2)) : 0;
     const size_t o_bdec = brick ? take((size_t)cull_bricks * cf) : 0;
     const size_t o_pl = refine ? take((size_t)plist_cap * sizeof(unsigned)) : 0;
-    const size_t o_ni = take((size_t)nsub);
-    const size_t o_ps = take((size_t)nsub * sizeof(unsigned));
-    const size_t o_fin = take((size_t)nsub * sizeof(unsigned));
-    const size_t o_lst = take((size_t)nwmax * nsub * sizeof(unsigned));
-    const size_t o_par = stats ? 0 : take((size_t)pcap * 64 * sizeof(int4));
+    const size_t o_ord = order ? take((size_t)main_slots * sizeof(unsigned)) : 0;
     char* sc = nullptr;
     if (scratch_alloc((void**)&sc, off, st) != hipSuccess) {
         (void)hipGetLastError();
@@ -1011,6 +937,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         return SFMHIP_E_HIP;
     }
     unsigned* cnt = reinterpret_cast<unsigned*>(sc + o_cnt);
+    unsigned* tcost = order ? cnt + kNCnt : nullptr;
     float* rec = reinterpret_cast<float*>(sc + o_rec);
     CullCam* ccam = reinterpret_cast<CullCam*>(sc + o_cam);
     int4* crange = reinterpret_cast<int4*>(sc + o_rng);
@@ -1020,13 +947,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     float2* ctab = brick ? reinterpret_cast<float2*>(sc + o_ctab) : nullptr;
     unsigned char* bdec = brick ? reinterpret_cast<unsigned char*>(sc + o_bdec) : nullptr;
     unsigned* plist = refine ? reinterpret_cast<unsigned*>(sc + o_pl) : nullptr;
-    unsigned char* nitem = reinterpret_cast<unsigned char*>(sc + o_ni);
-    unsigned* pslot = reinterpret_cast<unsigned*>(sc + o_ps);
-    unsigned* fin = reinterpret_cast<unsigned*>(sc + o_fin);
-    unsigned* list = reinterpret_cast<unsigned*>(sc + o_lst);
-    int4* partial = stats ? nullptr : reinterpret_cast<int4*>(sc + o_par);
-    // persistent fusion grid: 7 four-wave workgroups per CU (the kernel's occupancy)
-    const int fuse_wg = ncu * 7;
+    unsigned* ord = order ? reinterpret_cast<unsigned*>(sc + o_ord) : nullptr;
     int rc = SFMHIP_OK;
     // integration steps of at most kTsdfMaxFrames frames, in order on the stream
     for (int f0 = 0; f0 < F; f0 += kTsdfMaxFrames) {
@@ -1035,8 +956,9 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         const float* dp = depth + (size_t)f0 * Hd * Wd;
         const float* pp = poses + (size_t)f0 * 12;
         const float* kp = Kf + (size_t)f0 * 4;
-        hipLaunchKernelGGL(tsdf_setup_kernel, dim3(ceil_div(nf, 64) + 1), dim3(64), 0, st, pp, kp, nf, rec, ccam,
-                           ext_table ? 1 : 2, H, W, z0, z1, Hd, Wd, cg, nbu, nbv, crange, cnt, kNCnt);
+        hipLaunchKernelGGL(tsdf_setup_kernel, dim3(ceil_div(nf, 64) + std::min(64, ceil_div(nzero, 1024) + 1)),
+                           dim3(64), 0, st, pp, kp, nf, rec, ccam, ext_table ? 1 : 2, H, W, z0, z1, Hd, Wd, cg, nbu,
+                           nbv, crange, cnt, nzero);
         const float2* tab = ext_table ? ext_table + (size_t)f0 * nbv * nbu : cbmm;
         if (!ext_table) {
             if (Wd % 4 == 0)
@@ -1055,7 +977,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         }
         hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nw * 2)), dim3(1024), 0, st, H, W, z0, z1,
                            nf, Hd, Wd, ccam, cg, trunc, tab, nbu, nbv, crange, nw, bdec, (unsigned short*)cmask,
-                           (unsigned short*)cfree, plist, cnt + kCntPl);
+                           (unsigned short*)cfree, plist, cnt + kCntPl, tcost);
         // refinement: grid-stride over the device-side count (atomic ORs: any grid gives the
         // same masks); 8192 x 256 threads fill the 6 waves per SIMD its VGPRs allow
         if (plist)
@@ -1090,8 +1012,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             }
             continue;
         }
-        hipLaunchKernelGGL(tsdf_items_kernel, dim3((unsigned)ceil_div(nsub, (int64_t)256)), dim3(256), 0, st, cmask,
-                           cfree, nw, nf, nsub, pcap, nitem, pslot, list, cnt, fin);
+        if (ord)   // longest-first workgroup order within each XCD class (same results)
+            hipLaunchKernelGGL(tsdf_order_kernel, dim3(kNumXcd), dim3(256), (size_t)sm.per, st, sm, nf, tcost, ord);
         FrameCtx fc;
         fc.rec = rec;
         fc.depth = dp;
@@ -1105,23 +1027,10 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         fc.nbv = nbv;
         fc.trunc = trunc;
         fc.inv_trunc = 1.0f / trunc;
-        hipLaunchKernelGGL(vox_test ? tsdf_fuse_kernel<true> : tsdf_fuse_kernel<false>, dim3(fuse_wg), dim3(256), 0,
-                           st, T, Wt, D, H, W, z0, z1, fc, gb, nf, cmask, cfree, nw, nitem, pslot, list, nsub, cnt,
-                           partial);
-        hipLaunchKernelGGL(tsdf_finish_kernel, dim3(ncu * 8), dim3(256), 0, st, T, Wt, H, W, z0, z1, nf, nw, cmask,
-                           cfree, fin, cnt, nitem, pslot, partial);
+        hipLaunchKernelGGL(vox_test ? tsdf_fuse_kernel<true> : tsdf_fuse_kernel<false>, dim3((unsigned)main_slots),
+                           dim3(256), 0, st, T, Wt, D, H, W, z0, z1, fc, gb, nf, sm, cmask, cfree, nw, ord);
         rc = check_launch("tsdf_fuse_kernel");
         if (rc != SFMHIP_OK) break;
-        static const bool dev_cnt = std::getenv("SFMHIP_TSDF_DEVCNT") != nullptr;   // DEV ONLY (removed)
-        if (dev_cnt) {
-            unsigned h[kNCnt];
-            (void)hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, st);
-            (void)hipStreamSynchronize(st);
-            unsigned items = 0;
-            for (int w = 0; w < nw; ++w) items += h[kCntList + w];
-            fprintf(stderr, "tsdf dev: plist %u partial slots %u (cap %u) finish %u items %u\n", h[kCntPl], h[kCntPart],
-                    pcap, h[kCntFin], items);
-        }
     }
     scratch_free(sc, st);
     return rc;

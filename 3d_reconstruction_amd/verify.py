@@ -36,6 +36,8 @@ def _cam_rows(cam, P: int) -> torch.Tensor:
     for the work queued before it."""
     if isinstance(cam, torch.Tensor):
         t = dev(cam, torch.float64).reshape(-1, 4)
+        if t.shape[0] not in (1, P):
+            raise ValueError(f"camera rows must be 1 or {P}, got {t.shape[0]}")
         return (t.expand(P, 4) if t.shape[0] == 1 else t).contiguous()
     return dev(np.broadcast_to(np.asarray(cam, np.float64).reshape(-1, 4), (P, 4)).copy(), torch.float64)
 

@@ -115,6 +115,21 @@ class VoxelGrid:
         self.mask_mode = int(mask_mode)
         self._vm = None
         self._finite = None
+        self._ver = None
+
+    def invalidate(self) -> None:
+        """Drop the cached voxel-major copy and finiteness flag (they are also dropped
+        automatically when ``self.grid`` is modified in place: its version counter)."""
+        self._vm = None
+        self._finite = None
+        self._ver = None
+
+    def _sync_cache(self) -> None:
+        # self.grid may alias the caller's tensor (dev() does not copy): an in-place update
+        # bumps its version, and the derived copies must follow it
+        if self._ver is not None and self._ver != self.grid._version:
+            self.invalidate()
+        self._ver = self.grid._version
 
     @classmethod
     def plenoxel(cls, voxel_grid: torch.Tensor, scale: float = 1.5) -> "VoxelGrid":
@@ -151,6 +166,7 @@ class VoxelGrid:
         return s[:, 0], s[:, 1:]
 
     def voxel_major(self) -> torch.Tensor:
+        self._sync_cache()
         if self._vm is None:
             if self.C > 32:
                 raise ValueError("voxel-major layout supports C <= 32")
@@ -195,6 +211,7 @@ class VoxelGrid:
     def finite(self) -> bool:
         """Whether every grid value is finite (cached with the voxel-major copy): the render
         may then skip the colour lines of samples with alpha = 0, bit-identically."""
+        self._sync_cache()
         if getattr(self, "_finite", None) is None:
             self._finite = bool(torch.isfinite(self.grid).all().item())
         return self._finite

@@ -52,13 +52,10 @@ def _solve_gpu(sfm, gpu, cams, Ks, Xs, ps, **kw):
     return cam.cpu().numpy(), X.cpu().numpy(), {k: v.cpu().numpy() for k, v in res.items()}, off
 
 
-@pytest.mark.parametrize("variant", ["default", "2", "4", "5"])
 @pytest.mark.parametrize("far", [False, True])
-def test_ba_solve_batched_vs_oracle(sfm, gpu, monkeypatch, far, variant):
-    """Every kernel form (SFMHIP_BA_VARIANT: 2 stored records, 4 / 5 the recompute form at
-    512 / 256 threads) meets the oracle's iteration."""
-    if variant != "default":
-        monkeypatch.setenv("SFMHIP_BA_VARIANT", variant)
+def test_ba_solve_batched_vs_oracle(sfm, gpu, far):
+    """The batched device TRF meets the oracle's iteration (nfev, njev, x, cost) on ragged
+    pairs, including an empty one."""
     sizes = [300, 0, 1000, 37, 700, 2048]
     cams, Ks, Xs, ps = _ragged_problem(sizes, seed=40 + far, far=far)
     cam, X, res, off = _solve_gpu(sfm, gpu, cams, Ks, Xs, ps)

@@ -241,21 +241,14 @@ def _tsdf_case(R=48, F=12, Hd=96, Wd=128, focal=110.0):
     return R, depth.numpy(), poses.numpy(), K.numpy()
 
 
-# "auto": small grids run in latency mode; "0" / "1" force the whole-grid mode (refinement
-# pass, per-voxel block test) / the latency mode; "slots*": a partial-slot capacity of a few
-# slots, so the first split sub-tiles keep their window items and the rest merge into one
-# item each (both forms in one call)
-LAT_MODES = ["auto", "0", "1", "slots", "slots0"]
+# "auto": small grids run in latency mode; "0" / "1" force the whole-grid mode (brick and
+# refinement passes, per-voxel block test) / the latency mode
+LAT_MODES = ["auto", "0", "1"]
 
 
 def _set_lat(knob, lat):
     if lat in ("0", "1"):
         knob("TSDF_LATENCY", lat)
-    elif lat == "slots":
-        knob("TSDF_SLOTS", 5)
-    elif lat == "slots0":
-        knob("TSDF_LATENCY", 0)
-        knob("TSDF_SLOTS", 9)
 
 
 def _close_to_seq(Tg, Wg, Ts, Ws):
@@ -319,11 +312,10 @@ def test_tsdf_edge_cases_bitexact(sfm, gpu, knob, Wd, lat):
     assert (Wr > W0).mean() > 0.1
 
 
-def test_tsdf_multi_step_bitexact(sfm, gpu, knob):
+def test_tsdf_multi_step_bitexact(sfm, gpu):
     """More than 512 frames: the call fuses them in consecutive 512-frame integration
     steps (each finished before the next), exactly as the oracle defines it; a split
     call (frames [0, 300) then [300, F)) is a different (also exact) sequence of steps."""
-    knob("TSDF_SLOTS", 4)
     R, F, Hd, Wd = 20, 530, 24, 32
     depth, poses, K = syn.tsdf_scene(F, Hd, Wd, focal=30.0, seed=13)
     depth, poses, K = depth.numpy(), poses.numpy(), K.numpy()
@@ -348,19 +340,16 @@ def test_tsdf_multi_step_bitexact(sfm, gpu, knob):
 
 
 def test_tsdf_modes_and_splits_identical(sfm, gpu, knob):
-    """Full-resolution frames, 96^3 grid, z-slab: every mode (whole-grid with brick /
-    refinement / per-voxel block test, latency) and every partial-slot capacity (window
-    items vs merged items) gives the same grid bit for bit (integer sums: the split is
-    free), equal to the oracle on sampled slices, with both culling and the free-space
-    path active (cull stats)."""
+    """Full-resolution frames, 96^3 grid, z-slab: both modes (whole-grid with brick /
+    refinement / per-voxel block test, latency) give the same grid bit for bit, equal to
+    the oracle on sampled slices, with both culling and the free-space path active
+    (cull stats)."""
     depth, poses, K = syn.tsdf_scene(40, seed=3)   # two mask words per sub-tile
     bnd = ((-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95)
     out = []
-    variants = [{}, dict(TSDF_LATENCY=0), dict(TSDF_LATENCY=1), dict(TSDF_SLOTS=1), dict(TSDF_SLOTS=2),
-                dict(TSDF_SLOTS=50, TSDF_LATENCY=0), dict(TSDF_SLOTS=3, TSDF_LATENCY=1), dict(TSDF_SLOTS=1 << 20)]
+    variants = [{}, dict(TSDF_LATENCY=0), dict(TSDF_LATENCY=1)]
     for v in variants:
         knob("TSDF_LATENCY", -1)
-        knob("TSDF_SLOTS", 0)
         for k, x in v.items():
             knob(k, x)
         T = torch.zeros((96, 96, 96), dtype=torch.float32, device=gpu)
@@ -448,7 +437,7 @@ def test_tsdf_c5_full_size_slabs_bitexact(sfm, gpu, knob):
     """The bench workload itself (C5: 256^3 grid, 257 depth maps 1936x1296, every
     pre-pass and fast path at its default): three 2-slice z-slabs of the fused grid
     equal the oracle bit for bit and the sequential running average within 1e-4 rel /
-    3e-5 abs; the latency mode and other partial-slot capacities give the same grid."""
+    3e-5 abs; the latency mode gives the same grid."""
     depth, poses, K = syn.tsdf_scene(257, syn.IMG_H, syn.IMG_W, device=gpu)
     R = 256
     args = (depth, poses, K, (-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / (R - 1))
@@ -467,13 +456,11 @@ def test_tsdf_c5_full_size_slabs_bitexact(sfm, gpu, knob):
         _close_to_seq(Tg, Wg, Ts[z0:z0 + 2], Ws[z0:z0 + 2])
     assert (W > 0).float().mean() > 0.5
     T2, W2 = torch.zeros_like(T), torch.zeros_like(T)
-    for lat, slots in (("1", 0), ("0", 7), ("-1", 20000)):
-        knob("TSDF_LATENCY", lat)
-        knob("TSDF_SLOTS", slots)
-        T2.zero_()
-        W2.zero_()
-        sfm.tsdf_integrate(T2, W2, *args)
-        assert torch.equal(T, T2) and torch.equal(W, W2), (lat, slots)
+    knob("TSDF_LATENCY", 1)
+    T2.zero_()
+    W2.zero_()
+    sfm.tsdf_integrate(T2, W2, *args)
+    assert torch.equal(T, T2) and torch.equal(W, W2)
 
 
 def test_tsdf_zslab_split_equals_whole(sfm, gpu):
