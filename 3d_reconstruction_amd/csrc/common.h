@@ -58,6 +58,12 @@ void scratch_free(void* p, hipStream_t s);
 // fixed in the code.
 struct Knobs {
     int tsdf_latency;   // SFMHIP_TSDF_LATENCY: -1 auto, 0 whole-grid mode, 1 latency mode
+    int match_cert;     // SFMHIP_MATCH_CERT: 0 sends every row of the exact float mode to the f64 pass
+    int ess_mono;       // SFMHIP_ESS_MONO: 1 runs the one-workgroup-per-pair essential RANSAC kernel
+    int ess_rece;       // SFMHIP_ESS_RECE: essential models whose E is kept per record (0: all re-solved)
+    int dlt_qr;         // SFMHIP_DLT_QR: 1 runs the QR DLT for every observation (no normal-equation pass)
+    int render_sort;    // SFMHIP_RENDER_SORT: 0 renders rays in input order (no spatial sort)
+    int dda_direct;     // SFMHIP_DDA_DIRECT: fill kernel of the two-pass DDA (-1 auto, 0 staged, 1 direct)
 };
 const Knobs& knobs();
 

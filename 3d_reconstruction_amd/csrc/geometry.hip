@@ -226,7 +226,7 @@ __global__ __launch_bounds__(64) void dlt_list_kernel(const double* __restrict__
                                                       const unsigned* __restrict__ slots,
                                                       const unsigned* __restrict__ counts,
                                                       const double4* __restrict__ recx, const int* __restrict__ recpr,
-                                                      int64_t n_waves, int probe) {
+                                                      int64_t n_waves) {
     __shared__ unsigned items[64 * 64];
     const int lane = threadIdx.x;
     const int64_t w = (int64_t)blockIdx.x * 64 + lane;
@@ -248,18 +248,13 @@ __global__ __launch_bounds__(64) void dlt_list_kernel(const double* __restrict__
         const double4 xr = recx[pos];
         double X[4];
         const double *Pa = P + (size_t)pr * 24, xa = xr.x, ya = xr.y, xb = xr.z, yb = xr.w;
-        if (probe == 1) {   // timing probe (SFMHIP_DLT_LISTPROBE=1): the loads and stores without the solve
-            X[0] = Pa[0] + xa; X[1] = Pa[13] + ya; X[2] = Pa[23] + xb; X[3] = yb;
-        } else if (!dlt_point_qr3(Pa, Pa + 12, xa, ya, xb, yb, X)) {
-            if (probe == 2) X[0] = X[1] = X[2] = X[3] = 0.0;   // timing probe: no dlt_point fallback
-            else dlt_point(Pa, Pa + 12, xa, ya, xb, yb, X);
-        }
+        if (!dlt_point_qr3(Pa, Pa + 12, xa, ya, xb, yb, X)) dlt_point(Pa, Pa + 12, xa, ya, xb, yb, X);
 #pragma unroll
         for (int r = 0; r < 4; ++r) X4[(int64_t)r * n + i] = X[r];
     }
 }
 
-// the QR path for every observation (SFMHIP_DLT_QR=1 A/B runs; scratch failure)
+// the QR path for every observation (SFMHIP_DLT_QR=1, tests; scratch failure)
 __global__ void dlt_kernel(const double* __restrict__ P, const int32_t* __restrict__ pair_of_obs,
                            const double* __restrict__ x0, const double* __restrict__ x1, int64_t n,
                            double* __restrict__ X4) {
@@ -382,8 +377,8 @@ extern "C" int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_ob
     hipStream_t st = as_stream(stream);
     unsigned* slots = nullptr;   // [n_waves][64] listed observations + [n_waves] counts
     const int64_t n_waves = ceil_div(n, 64);
-    const char* qr = std::getenv("SFMHIP_DLT_QR");
-    if (!(qr && std::atoi(qr) != 0) && n < ((int64_t)1 << 31) &&
+    // SFMHIP_DLT_QR=1 (tests): the QR path for every observation, as on a scratch failure
+    if (knobs().dlt_qr == 0 && n < ((int64_t)1 << 31) &&
         scratch_alloc((void**)&slots, (size_t)ceil_div(n_waves * 65, (int64_t)8) * 32 + (size_t)n_waves * 64 * 36, st) ==
             hipSuccess) {
         // [n_waves * 64] indices, [n_waves] counts, then (32-B aligned) the listed observations'
@@ -395,13 +390,8 @@ extern "C" int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_ob
                            X4, slots, counts, recx, recpr);
         int rc = check_launch("dlt_normal_kernel");
         if (rc == SFMHIP_OK) {
-#ifdef SFMHIP_PROBES   // timing probes (tool-only builds: make EXTRA=-DSFMHIP_PROBES); they return fake triangulations
-            static const int probe = [] { const char* e = std::getenv("SFMHIP_DLT_LISTPROBE"); return e ? std::atoi(e) : 0; }();
-#else
-            constexpr int probe = 0;
-#endif
             hipLaunchKernelGGL(dlt_list_kernel, dim3((unsigned)ceil_div(n_waves, 64)), dim3(64), 0, st, P, pair_of_obs,
-                               x0, x1, n, X4, slots, counts, recx, recpr, n_waves, probe);
+                               x0, x1, n, X4, slots, counts, recx, recpr, n_waves);
             rc = check_launch("dlt_list_kernel");
         }
         scratch_free(slots, st);

@@ -157,6 +157,12 @@ static int env_knob(const char* name, int dflt) {
 static Knobs read_knobs() {
     Knobs k;
     k.tsdf_latency = env_knob("SFMHIP_TSDF_LATENCY", -1);
+    k.match_cert = env_knob("SFMHIP_MATCH_CERT", 1);
+    k.ess_mono = env_knob("SFMHIP_ESS_MONO", 0);
+    k.ess_rece = env_knob("SFMHIP_ESS_RECE", 1 << 20);
+    k.dlt_qr = env_knob("SFMHIP_DLT_QR", 0);
+    k.render_sort = env_knob("SFMHIP_RENDER_SORT", 1);
+    k.dda_direct = env_knob("SFMHIP_DDA_DIRECT", -1);
     return k;
 }
 static Knobs g_knobs;

@@ -476,9 +476,9 @@ __global__ __launch_bounds__(256) void vq_kernel(const double* __restrict__ obs,
 // codewords (row stride DP+4 f64, i.e. == 4 mod 32, so the 16 rows x 4 k of an
 // MFMA B fragment hit distinct bank pairs).  Each wave keeps the A fragments
 // of its 32 observations (2 row tiles x DP/4 f64 per lane) in registers for a
-// whole pass; every B fragment read from LDS feeds two MFMAs (PAIR: two code
-// blocks per step, four accumulator chains; measured slower once the
-// difference-form epilogue raised register pressure: 1.37 vs 1.33 ms).  Each lane
+// whole pass; every B fragment read from LDS feeds two MFMAs (two code blocks
+// per step, four accumulator chains, measured slower once the difference-form
+// epilogue raised register pressure: 1.37 vs 1.33 ms).  Each lane
 // tracks the best codeword among j == lane (mod 16) for its 4 C rows, then a
 // 16-lane (d2, index) argmin with lowest-index tie-break; passes merge through
 // the output arrays (strict <: later passes hold higher indices), and the
@@ -490,7 +490,7 @@ constexpr int kVqmWaves = 8;
 constexpr int kVqmObsPerWave = 32;
 constexpr int kVqmTile = kVqmWaves * kVqmObsPerWave;   // 256 observations
 
-template <int DP, bool PAIR, bool FULL>   // FULL: d == DP (no k padding)
+template <int DP, bool FULL>   // FULL: d == DP (no k padding)
 __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
     const double* __restrict__ obs, int64_t n_obs, const double* __restrict__ code, int n_codes, int d,
     int codes_per_pass, int32_t* __restrict__ codes, double* __restrict__ dist) {
@@ -537,7 +537,6 @@ __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
             for (int h = 0; h < 2; ++h)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) { best[h][g] = __builtin_inf(); bj[h][g] = INT_MAX; }
-            // Two code blocks per step when VQ_PAIR: four independent accumulator chains per wave.
             auto epilogue = [&](const v4d& acc0, const v4d& acc1, int j) {
                 const double cn = sn[j];
 #pragma unroll
@@ -548,25 +547,7 @@ __global__ __launch_bounds__(kVqmWaves * 64) void vq_mfma_kernel(
                     if (d1 < best[1][g]) { best[1][g] = d1; bj[1][g] = c0 + j; }
                 }
             };
-            int cb = 0;
-            if (PAIR) {
-                for (; cb + 1 < ncb; cb += 2) {
-                    const int j = cb * 16 + r16;
-                    const double* bp = sc + j * LD + kq;
-                    v4d a00 = {0.0, 0.0, 0.0, 0.0}, a01 = a00, a10 = a00, a11 = a00;
-#pragma unroll
-                    for (int s = 0; s < KS; ++s) {
-                        const double b0 = bp[4 * s], b1 = bp[16 * LD + 4 * s];
-                        a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0][s], b0, a00, 0, 0, 0);
-                        a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1][s], b0, a01, 0, 0, 0);
-                        a10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0][s], b1, a10, 0, 0, 0);
-                        a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1][s], b1, a11, 0, 0, 0);
-                    }
-                    epilogue(a00, a01, j);         // block cb before cb + 1: index order kept
-                    epilogue(a10, a11, j + 16);
-                }
-            }
-            for (; cb < ncb; ++cb) {
+            for (int cb = 0; cb < ncb; ++cb) {
                 const int j = cb * 16 + r16;
                 const double* bp = sc + j * LD + kq;
                 v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
@@ -652,346 +633,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ double vq_eps_abs(int DP, double xn, double cmax) {
     return 0x1p-126 * (2.0 * sqrt((double)DP) * (cmax + xn) + 2.0 * DP + 4.0) * 1.01;
 }
-constexpr int kVqfWaves = 12;
-constexpr int kVqfTile = kVqfWaves * 32;   // observations per tile (32 per wave)
-__global__ __launch_bounds__(kVqfWaves * 64) void vq_f32f_kernel(const double* __restrict__ obs, int64_t n_obs,
-                                                                  const double* __restrict__ code, int n_codes,
-                                                                  int32_t* __restrict__ codes,
-                                                                  double* __restrict__ dist,
-                                                                  unsigned* __restrict__ amb,
-                                                                  unsigned* __restrict__ namb) {
-    constexpr int DP = 128, LD = DP + 4, KS = DP / 4;
-    extern __shared__ float smf[];
-    const int ncb = (n_codes + 15) >> 4;
-    float* sc = smf;                              // [ncb * 16][LD] codebook (f32)
-    float* sn = smf + (size_t)ncb * 16 * LD;      // [ncb * 16] squared norms (f32)
-    __shared__ int s_win[kVqfWaves][32];
-    __shared__ unsigned s_cmax;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int r16 = lane & 15, kq = lane >> 4;
-    if (threadIdx.x == 0) s_cmax = 0u;
-    for (int t = threadIdx.x; t < ncb * 16 * DP; t += blockDim.x) {
-        const int r = t / DP, k = t - r * DP;
-        sc[r * LD + k] = r < n_codes ? (float)code[(size_t)r * DP + k] : 0.f;
-    }
-    __syncthreads();
-    for (int r = threadIdx.x; r < ncb * 16; r += blockDim.x) {
-        double q = 0.0;
-        if (r < n_codes)
-            for (int k = 0; k < DP; ++k) q = __builtin_fma(code[(size_t)r * DP + k], code[(size_t)r * DP + k], q);
-        sn[r] = r < n_codes ? (float)q : __builtin_inff();   // padded codewords never win
-        if (r < n_codes) atomicMax(&s_cmax, __float_as_uint((float)sqrt(q) * 1.001f));   // positive floats
-    }
-    __syncthreads();
-    const double cmax = (double)__uint_as_float(s_cmax);
-    const double u = 0x1p-24;
-    const int64_t n_tiles = (n_obs + kVqfTile - 1) / kVqfTile;
-    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-        const int64_t ob = t * kVqfTile + wave * 32;
-        float a[2][KS];
-        double xn[2] = {0.0, 0.0};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int64_t o = ob + 16 * h + r16;
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const double x = o < n_obs ? __builtin_nontemporal_load(obs + o * DP + 4 * s + kq) : 0.0;
-                a[h][s] = (float)x;
-                xn[h] = __builtin_fma(x, x, xn[h]);
-            }
-            xn[h] += __shfl_xor(xn[h], 16);
-            xn[h] += __shfl_xor(xn[h], 32);   // |x|^2 of row r16, in every lane group
-            __builtin_amdgcn_sched_barrier(0);   // one row tile's f64 loads in flight at a time (VGPRs)
-        }
-        float b1[2][4], b2[2][4];
-        int i1[2][4];
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) { b1[h][g] = b2[h][g] = __builtin_inff(); i1[h][g] = INT_MAX; }
-        for (int cb = 0; cb < ncb; ++cb) {
-            const int j = cb * 16 + r16;
-            const float* bp = sc + j * LD + kq;
-            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const float b = bp[4 * s];
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s], b, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1][s], b, acc1, 0, 0, 0);
-            }
-            const float cn = sn[j];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {   // C row 4 kq + g (observation), column r16 (codeword j)
-                const float d0 = cn - 2.f * acc0[g], d1 = cn - 2.f * acc1[g];
-                if (d0 < b1[0][g]) { b2[0][g] = b1[0][g]; b1[0][g] = d0; i1[0][g] = j; }
-                else if (d0 < b2[0][g]) b2[0][g] = d0;
-                if (d1 < b1[1][g]) { b2[1][g] = b1[1][g]; b1[1][g] = d1; i1[1][g] = j; }
-                else if (d1 < b2[1][g]) b2[1][g] = d1;
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                float v1 = b1[h][g], v2 = b2[h][g];
-                int x1 = i1[h][g];
-#pragma unroll
-                for (int off = 8; off >= 1; off >>= 1) {   // top-2 over the 16 codeword lanes
-                    const float o1 = __shfl_xor(v1, off, 16), o2 = __shfl_xor(v2, off, 16);
-                    const int ox = __shfl_xor(x1, off, 16);
-                    if (o1 < v1 || (o1 == v1 && ox < x1)) { v2 = fminf(v1, o2); v1 = o1; x1 = ox; }
-                    else v2 = fminf(o1, v2);
-                }
-                const int row = 4 * kq + g;
-                const double xr = __shfl(xn[h], row);   // lane `row` (group 0) holds |x|^2 of that row
-                const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax) +
-                                   vq_eps_abs(DP, sqrt(xr), cmax);
-                if (r16 == 0) s_win[wave][16 * h + row] = ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
-            }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // exact distances of the proven winners, difference form, 8 rows' loads in flight at a time
-        for (int r0 = 0; r0 < 32; r0 += 8) {
-            double part[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int64_t o = min(ob + r0 + q, n_obs - 1);
-                const int w = max(s_win[wave][r0 + q], 0);
-                const double* xp = obs + o * DP;
-                const double* cp = code + (size_t)w * DP;
-                const double d0 = xp[lane] - cp[lane], d1 = xp[lane + 64] - cp[lane + 64];
-                part[q] = __builtin_fma(d1, d1, d0 * d0);
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) part[q] += __shfl_xor(part[q], off);
-            if (lane == 0)
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int64_t o = ob + r0 + q;
-                    const int w = s_win[wave][r0 + q];
-                    if (o < n_obs) {
-                        if (w >= 0) {
-                            codes[o] = w;
-                            dist[o] = sqrt(part[q]);
-                        } else {
-                            amb[atomicAdd(namb, 1u)] = (unsigned)o;
-                        }
-                    }
-                }
-        }
-        __builtin_amdgcn_wave_barrier();   // s_win reused by the next tile
-    }
-}
-
-// vq, d = 128, <= 256 codewords, register-resident observations (default).  Same
-// filter and bound as vq_f32f_kernel, re-shaped so that every observation byte is
-// read from HBM once: a wave owns 16 observations, lane (r, q) holds row r's f64
-// values k = 8t + 2q + {0,1} (t < 16) in VGPRs for the whole unit — each load
-// instruction reads 64 contiguous bytes per row, so the texture path handles 16
-// half-lines per instruction, not 64 scattered 16-B pieces — (k-step 2t + e feeds
-// the MFMA with k = 8t + 2q + e; the codebook fragments are laid out to match),
-// and the proven winner's difference-form distance is summed from those registers
-// against the f64 codeword (L2-resident).  The f32 codebook sits in LDS in MFMA
-// B-fragment order ([block][k-quad][lane] float4: one conflict-free ds_read_b128
-// per 4 k-steps), two codeword blocks per pass (two independent MFMA chains).
-// 8 waves per workgroup (2 per SIMD, 256 VGPRs each), units dealt wave by wave;
-// each wave's next unit is loaded while the current one computes.
 typedef double f64x2 __attribute__((ext_vector_type(2)));
-constexpr int kVqrWaves = 8;
-template <int PROBE, int WAVES = kVqrWaves>   // WAVES 16: 4 per SIMD, no prefetch (A/B);  PROBE (timing ablations only, never the product): 1 no HBM loads,
-                       // 3 no codeword loads in the exact tail, 4 cached (not non-temporal) loads
-__global__ __launch_bounds__(WAVES * 64) void vq_f32r_kernel(const double* __restrict__ obs, int64_t n_obs,
-                                                                  const double* __restrict__ code, int n_codes,
-                                                                  int32_t* __restrict__ codes,
-                                                                  double* __restrict__ dist,
-                                                                  unsigned* __restrict__ amb,
-                                                                  unsigned* __restrict__ namb) {
-    constexpr int DP = 128, KS = 32;
-    extern __shared__ f32x4 smv[];
-    const int ncb = (n_codes + 15) >> 4;           // codeword blocks of 16
-    const int ncp = (ncb + 1) & ~1;                // LDS blocks (even count)
-    f32x4* sc = smv;                                // [ncp][8][64] B fragments
-    float* sn = reinterpret_cast<float*>(smv + ncp * 8 * 64);   // [ncp * 16] squared norms
-    __shared__ unsigned s_cmax;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int r16 = lane & 15, kq = lane >> 4;
-    if (threadIdx.x == 0) s_cmax = 0u;
-    for (int t = threadIdx.x; t < ncp * 16 * DP; t += blockDim.x) {
-        const int j = t >> 7, k = t & (DP - 1);
-        const float v = j < n_codes ? (float)code[(size_t)j * DP + k] : 0.f;
-        const int ln = (((k >> 1) & 3) << 4) | (j & 15), s = ((k >> 3) << 1) | (k & 1);
-        reinterpret_cast<float*>(sc)[((((j >> 4) * 8 + (s >> 2)) * 64 + ln) << 2) | (s & 3)] = v;
-    }
-    __syncthreads();
-    for (int r = threadIdx.x; r < ncp * 16; r += blockDim.x) {
-        double q = 0.0;
-        if (r < n_codes)
-            for (int k = 0; k < DP; ++k) q = __builtin_fma(code[(size_t)r * DP + k], code[(size_t)r * DP + k], q);
-        sn[r] = r < n_codes ? (float)q : __builtin_inff();   // padded codewords never win
-        if (r < n_codes) atomicMax(&s_cmax, __float_as_uint((float)sqrt(q) * 1.001f));
-    }
-    __syncthreads();
-    const double cmax = (double)__uint_as_float(s_cmax);
-    const double u = 0x1p-24;
-    const int64_t n_units = (n_obs + 15) >> 4;
-    constexpr bool kPre = WAVES <= 8;   // the prefetch needs the VGPRs of 2 waves per SIMD
-    const int64_t ustep = (int64_t)gridDim.x * WAVES;
-    f64x2 nx[KS / 2];   // the next unit's observations, in flight while this unit computes
-    auto fetch = [&](int64_t un) {
-        const f64x2* xp = reinterpret_cast<const f64x2*>(obs + min(un * 16 + r16, n_obs - 1) * DP) + kq;
-#pragma unroll
-        for (int s2 = 0; s2 < KS / 2; ++s2) {
-            if (PROBE == 1) nx[s2] = f64x2{(double)(lane + un), (double)s2};
-            else if (PROBE == 4) nx[s2] = xp[4 * s2];
-            else nx[s2] = __builtin_nontemporal_load(xp + 4 * s2);
-        }
-    };
-    if (kPre) fetch(min((int64_t)blockIdx.x * WAVES + wave, n_units - 1));
-    for (int64_t un = (int64_t)blockIdx.x * WAVES + wave; un < n_units; un += ustep) {
-        const int64_t o = un * 16 + r16;
-        if (!kPre) fetch(un);
-        double x[KS];
-#pragma unroll
-        for (int s2 = 0; s2 < KS / 2; ++s2) {
-            x[2 * s2] = nx[s2].x;
-            x[2 * s2 + 1] = nx[s2].y;
-        }
-        if (kPre) fetch(min(un + ustep, n_units - 1));
-        double xn = 0.0;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) xn = __builtin_fma(x[s], x[s], xn);
-        xn += __shfl_xor(xn, 16);
-        xn += __shfl_xor(xn, 32);   // |x|^2 of row r16, in every lane group
-        float b1[4], b2[4];
-        int i1[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) { b1[g] = b2[g] = __builtin_inff(); i1[g] = INT_MAX; }
-        auto take = [&](int g, float dd, int j) {   // branch-free top-2 (selects, no exec-mask branches)
-            const bool l = dd < b1[g];
-            b2[g] = l ? b1[g] : fminf(dd, b2[g]);
-            i1[g] = l ? j : i1[g];
-            b1[g] = l ? dd : b1[g];
-        };
-        for (int cb = 0; cb + 1 < ncb; cb += 2) {
-            if (!kPre) {
-#pragma unroll
-                for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(x[s]));   // convert per pass (VGPRs)
-            }
-            const f32x4* bp = sc + cb * 8 * 64 + lane;
-            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-#pragma unroll
-            for (int s4 = 0; s4 < KS / 4; ++s4) {
-                const f32x4 c0 = bp[s4 * 64], c1 = bp[(8 + s4) * 64];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float a = (float)x[4 * s4 + e];
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, c0[e], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, c1[e], acc1, 0, 0, 0);
-                }
-                if (s4 & 1) __builtin_amdgcn_sched_barrier(0);   // LDS fragments two k-quads ahead at most
-            }
-            const int j0 = cb * 16 + r16;
-            const float cn0 = sn[j0], cn1 = sn[j0 + 16];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {   // C row 4 kq + g (observation), columns j0, j0 + 16
-                take(g, cn0 - 2.f * acc0[g], j0);
-                take(g, cn1 - 2.f * acc1[g], j0 + 16);
-            }
-        }
-        if (ncb & 1) {   // odd block count: the last block alone (its padded partner is never computed)
-            const int cb = ncb - 1;
-            const f32x4* bp = sc + cb * 8 * 64 + lane;
-            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;   // even / odd k-steps: two chains
-#pragma unroll
-            for (int s4 = 0; s4 < KS / 4; ++s4) {
-                const f32x4 c0 = bp[s4 * 64];
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x[4 * s4], c0[0], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x[4 * s4 + 1], c0[1], acc1, 0, 0, 0);
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x[4 * s4 + 2], c0[2], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x[4 * s4 + 3], c0[3], acc1, 0, 0, 0);
-            }
-            const int j0 = cb * 16 + r16;
-            const float cn0 = sn[j0];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) take(g, cn0 - 2.f * (acc0[g] + acc1[g]), j0);
-        }
-        int win[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            float v1 = b1[g], v2 = b2[g];
-            int x1 = i1[g];
-#pragma unroll
-            for (int off = 8; off >= 1; off >>= 1) {   // top-2 over the 16 codeword lanes
-                const float o1 = __shfl_xor(v1, off, 16), o2 = __shfl_xor(v2, off, 16);
-                const int ox = __shfl_xor(x1, off, 16);
-                const bool t = o1 < v1 || (o1 == v1 && ox < x1);
-                v2 = t ? fminf(v1, o2) : fminf(o1, v2);
-                v1 = t ? o1 : v1;
-                x1 = t ? ox : x1;
-            }
-            const double xr = __shfl(xn, 4 * kq + g);   // lane 4kq+g holds |x|^2 of that row
-            const double eps = 1.01 * ((2.0 * DP + 5.0) * u * sqrt(xr) * cmax + u * cmax * cmax) +
-                               vq_eps_abs(DP, sqrt(xr), cmax);
-            win[g] = PROBE == 4 || PROBE >= 7 ? (4 * kq + g) % n_codes : ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
-        }
-        int w = -1;   // row r16's verdict: group r16 >> 2, entry r16 & 3
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int t = __shfl(win[g], (r16 >> 2) << 4);
-            if ((r16 & 3) == g) w = t;
-        }
-        const f64x2* cp = reinterpret_cast<const f64x2*>(code + (size_t)max(w, 0) * DP) + kq;
-        double part = 0.0;
-#pragma unroll
-        for (int s2 = 0; s2 < KS / 2; ++s2) {
-            const f64x2 c = PROBE == 3 ? f64x2{x[2 * s2 + 1], x[2 * s2]} : cp[4 * s2];
-            const double d0 = x[2 * s2] - c.x, d1 = x[2 * s2 + 1] - c.y;
-            part = __builtin_fma(d0, d0, part);
-            part = __builtin_fma(d1, d1, part);
-            if ((s2 & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // 4 codeword loads in flight (VGPRs)
-        }
-        part += __shfl_xor(part, 16);
-        part += __shfl_xor(part, 32);
-        if (kq == 0 && o < n_obs) {
-            if (w >= 0) {
-                codes[o] = w;
-                dist[o] = sqrt(part);
-            } else {
-                amb[atomicAdd(namb, 1u)] = (unsigned)o;
-            }
-        }
-    }
-}
-
-// vq, d = 128, <= 256 codewords: the same exact decision with the filter's products on the
-// f16 matrix cores (v_mfma_f32_16x16x32_f16, 16x the f32 matrix rate).  Each input is split
-// v = v_hi + v_lo, v_hi = fl16(v), v_lo = fl16(v - v_hi), and x.c is taken as
-// x_hi.c_hi + (x_hi.c_lo + x_lo.c_hi): the main products in one f32 accumulator, the two
-// correction products (each <= 2^-11 of a main one) in a second, added at the end; f16 x f16
-// products are exact in f32.  Error of the score s_j = fl32(|c_j|^2) - 2 (x.c_j)~ against
-// |c_j|^2 - 2 x.c_j, with u = 2^-24 and |v - v_hi - v_lo| <= 2^-22 |v| + 2^-25 (the two
-// roundings to f16, f64 -> f32 -> f16 rounding twice, 2^-25 the f16 subnormal half-ulp):
-//   dropped x_hi.c_e + x_lo.c_lo + x_lo.c_e + x_e.c (c_e, x_e the split remainders):
-//   <= 2 (3 2^-22 |x| cmax + 2^-25 sqrt(d) (|x| + cmax) + d 2^-48); the main accumulator's d
-//   products in any order, truncating or not: <= 2 d 2u |x| cmax (1 + 2^-10); the correction
-//   accumulator's 2d products of <= 2^-10 |x| cmax in sum: <= 2 2d 2u 2^-10 |x| cmax; their sum:
-//   2u |x| cmax; the norm and the final subtraction: 2u (cmax^2 + 2 |x| cmax);
-// so eps16 = 1.01 (2 |x| cmax (3 2^-22 + 2.02 d u + 4u) + 4u cmax^2 + 2^-24 sqrt(d) (|x| + cmax)
-// + 2 d 2^-48) + the subnormal term of the f32 path (one accumulator for all 3d products would
-// need 6d u: the split cuts the bound, and with it the exact pass's share, ~3x).  Inputs of
-// magnitude >= 2^15 (f16 overflow) decide nothing: such an observation, or every observation
-// when the codebook holds one, goes to the exact pass.
-// Layout: a wave owns 16 observations (rows).  Loads: instruction j (< 16) reads rows
-// (l & 7) + 8 (j >> 3), 128 contiguous bytes of each (lane l takes f64 pair 8 (j & 7) +
-// 2 (l >> 4) + ((l >> 3) & 1)): whole cache lines, where 16 rows x 64 B per instruction ran the
-// stream at half the rate.  One exchange between lanes l and l ^ 8 (DPP row_ror:8) then leaves
-// lane (r = l & 15, q = l >> 4) with row r's pairs 8m + 2q + c in register 8c + m — the MFMA's
-// A-fragment order (fragment b element j = register 4b + j/2, half j%2; the dot product's k
-// order is free), and the codebook sits in LDS in that order ([block][k-block][hi/lo][lane],
-// 8 halves per lane: one ds_read_b128 per operand).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 constexpr int kVqhWaves = 8;
 __device__ __forceinline__ double vq_eps16(int DP, double xn, double cmax) {
@@ -1186,7 +828,7 @@ __global__ __launch_bounds__(kVqhWaves * 64) void vq_f16s_kernel(const double* _
     }
 }
 
-// The observations vq_f32f_kernel / vq_f32r_kernel could not decide: one wave each, every codeword
+// The observations vq_f16s_kernel could not decide: one wave each, every codeword
 // in f64 difference form, lowest index on ties.
 __global__ __launch_bounds__(256) void vq_exact_kernel(const double* __restrict__ obs, const double* __restrict__ code,
                                                        int n_codes, int d, const unsigned* __restrict__ amb,
@@ -1504,14 +1146,9 @@ extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, cons
     SFMHIP_REQUIRE(ratio_num > 0 && ratio_den > 0 && ratio_num <= 65535 && ratio_den <= 65535,
                    "sfmhip_match_pairs: ratio must be a positive fraction");
     if (P == 0) return SFMHIP_OK;
-    // Variant (SFMHIP_MATCH_VARIANT, for A/B runs): {MFMA tile, tiles/wave, waves/WG}
-    //   0: 16x16, 4, 4 (default; fastest measured)   1: 32x32, 2, 4   2: 16x16, 8, 4   3: 32x32, 4, 4   4: 16x16, 4, 8
-    //   5: 16x16, 2, 8 (half the resident query rows per wave: 4 waves/SIMD instead of 2)
-    const char* venv = std::getenv("SFMHIP_MATCH_VARIANT");
-    const int variant = venv ? std::atoi(venv) : 0;
-    static const int kIBv[6] = {256, 256, 512, 512, 512, 256};
-    const int iblk = kIBv[(variant >= 0 && variant < 6) ? variant : 0];
-    const int n_iblk = ceil_div(m_pad, iblk);
+    // 16x16x64 int8 MFMA tiles, 4 per wave, 4 waves per workgroup: 256 query rows per workgroup
+    // (32x32 tiles, 8 tiles per wave and 8-wave workgroups measured slower: DESIGN.md K1)
+    const int n_iblk = ceil_div(m_pad, 256);
     const int64_t nwg64 = (int64_t)P * n_iblk;
     SFMHIP_REQUIRE(nwg64 < INT_MAX, "sfmhip_match_pairs: too many pairs for one launch");
     const int nwg = (int)nwg64;
@@ -1520,15 +1157,7 @@ extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, cons
 #define SFMHIP_LAUNCH_MATCH(DD, MF, NS, WW)                                                              \
     hipLaunchKernelGGL((match_kernel<DD, MF, NS, WW>), dim3(nwg), dim3(64 * WW), 0, s, desc, norms, keys, \
                        n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2, CertArgs{})
-#define SFMHIP_LAUNCH_D(DD)                                        \
-    switch (variant) {                                             \
-        case 1: SFMHIP_LAUNCH_MATCH(DD, 32, 2, 4); break;          \
-        case 2: SFMHIP_LAUNCH_MATCH(DD, 16, 8, 4); break;          \
-        case 3: SFMHIP_LAUNCH_MATCH(DD, 32, 4, 4); break;          \
-        case 4: SFMHIP_LAUNCH_MATCH(DD, 16, 4, 8); break;          \
-        case 5: SFMHIP_LAUNCH_MATCH(DD, 16, 2, 8); break;          \
-        default: SFMHIP_LAUNCH_MATCH(DD, 16, 4, 4); break;         \
-    }
+#define SFMHIP_LAUNCH_D(DD) SFMHIP_LAUNCH_MATCH(DD, 16, 4, 4)
     switch (d) {
         case 64: SFMHIP_LAUNCH_D(64); break;
         case 128: SFMHIP_LAUNCH_D(128); break;
@@ -1558,14 +1187,13 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
     SFMHIP_REQUIRE(obs && code_book && codes && dist, "sfmhip_vq: null pointer");
     SFMHIP_REQUIRE(n_obs >= 0 && n_codes > 0 && d > 0 && d <= 256, "sfmhip_vq: bad shape (d <= 256)");
     if (n_obs == 0) return SFMHIP_OK;
-    const char* venv = std::getenv("SFMHIP_VQ_VARIANT");    // 1: the FMA difference-form kernel (A/B runs)
-    const int variant = venv ? std::atoi(venv) : 6;          // 3: the f64-MFMA GEMM-form kernel (A/B runs)
-    if (d == 128 && n_codes <= 256 && (variant == 0 || variant == 4 || variant == 6)) {   // 6 (default): vq_f16s_kernel
-        const bool reg = variant == 0, half = variant == 6;   // 0: vq_f32r_kernel, 4: vq_f32f_kernel (A/B runs)
-        const int ncb = ceil_div(n_codes, 16), ncp = ceil_div(n_codes, 32) * 2;
-        const size_t shm = half ? (size_t)ncp * 4 * 2 * 64 * 16 + (size_t)ncp * 16 * sizeof(float)
-                           : reg ? (size_t)ncp * 16 * (128 + 1) * sizeof(float)
-                                 : (size_t)ncb * 16 * (128 + 4 + 1) * sizeof(float);
+    // d = 128, <= 256 codewords (matching.py:27's 200-word codebook): the f16-split MFMA
+    // filter + exact f64 decision (vq_f16s_kernel + vq_exact_kernel); other shapes: the
+    // f64-MFMA GEMM-form kernel (d <= 128) or the f64 difference-form kernel.  The f32
+    // filter kernels (LDS-staged and register-resident) measured slower.
+    if (d == 128 && n_codes <= 256) {
+        const int ncp = ceil_div(n_codes, 32) * 2;
+        const size_t shm = (size_t)ncp * 4 * 2 * 64 * 16 + (size_t)ncp * 16 * sizeof(float);
         hipStream_t s = as_stream(stream);
         unsigned* amb = nullptr;
         if (scratch_alloc((void**)&amb, (size_t)(n_obs + 1) * sizeof(unsigned), s) == hipSuccess &&
@@ -1575,49 +1203,12 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
             int dev = 0, n_cu = 256;
             if (hipGetDevice(&dev) == hipSuccess)
                 (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-            int rc;
-            if (half) {
-#ifdef SFMHIP_PROBES   // timing ablations (tool-only builds: make EXTRA=-DSFMHIP_PROBES); they return wrong codes
-                const char* penv = std::getenv("SFMHIP_VQ_PROBE");
-                const int probe = penv ? std::atoi(penv) : 0;
-#else
-                constexpr int probe = 0;
-#endif
-                const int64_t n_wg = ((n_obs + 15) / 16 + kVqhWaves - 1) / kVqhWaves;
-                auto kern = probe == 1   ? vq_f16s_kernel<1>
-                            : probe == 2 ? vq_f16s_kernel<2>
-                            : probe == 4 ? vq_f16s_kernel<4> : vq_f16s_kernel<0>;
-                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-                hipLaunchKernelGGL(kern, dim3((unsigned)std::min<int64_t>(n_wg, n_cu)),
-                                   dim3(kVqhWaves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
-                                   namb);
-                rc = check_launch("vq_f16s_kernel");
-            } else if (reg) {
-#ifdef SFMHIP_PROBES   // timing ablations (tool-only builds: make EXTRA=-DSFMHIP_PROBES); they return wrong codes
-                const char* penv = std::getenv("SFMHIP_VQ_PROBE");
-                const int probe = penv ? std::atoi(penv) : 0;
-#else
-                constexpr int probe = 0;
-#endif
-                const int waves = probe == 5 ? 16 : kVqrWaves;
-                const int64_t n_wg = ((n_obs + 15) / 16 + waves - 1) / waves;
-                auto kern = probe == 1 ? vq_f32r_kernel<1>
-                           : probe == 3 ? vq_f32r_kernel<3> : probe == 4 ? vq_f32r_kernel<4>
-                           : probe == 5 ? vq_f32r_kernel<0, 16> : vq_f32r_kernel<0>;
-                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-                hipLaunchKernelGGL(kern, dim3((unsigned)std::min<int64_t>(n_wg, n_cu)),
-                                   dim3(waves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
-                                   namb);
-                rc = check_launch("vq_f32r_kernel");
-            } else {
-                const int64_t n_tiles = (n_obs + kVqfTile - 1) / kVqfTile;
-                (void)hipFuncSetAttribute((const void*)vq_f32f_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)shm);
-                hipLaunchKernelGGL(vq_f32f_kernel, dim3((unsigned)std::min<int64_t>(n_tiles, n_cu)),
-                                   dim3(kVqfWaves * 64), shm, s, obs, n_obs, code_book, n_codes, codes, dist, amb,
-                                   namb);
-                rc = check_launch("vq_f32f_kernel");
-            }
+            const int64_t n_wg = ((n_obs + 15) / 16 + kVqhWaves - 1) / kVqhWaves;
+            auto kern = vq_f16s_kernel<0>;
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+            hipLaunchKernelGGL(kern, dim3((unsigned)std::min<int64_t>(n_wg, n_cu)), dim3(kVqhWaves * 64), shm, s, obs,
+                               n_obs, code_book, n_codes, codes, dist, amb, namb);
+            int rc = check_launch("vq_f16s_kernel");
             if (rc == SFMHIP_OK) {
                 hipLaunchKernelGGL(vq_exact_kernel, dim3(1024), dim3(256), 0, s, obs, code_book, n_codes, 128, amb,
                                    namb, codes, dist);
@@ -1629,7 +1220,7 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
         (void)hipGetLastError();   // no scratch: the f64 kernels below
     }
     const int dp = d <= 32 ? 32 : d <= 64 ? 64 : d <= 128 ? 128 : 0;
-    if (dp && variant != 1) {
+    if (dp) {
         const int ld = dp + 4;
         const int max_cpp = std::min(144, (int)((150 * 1024 / 8) / (ld + 1)) / 16 * 16);
         const int passes = ceil_div(n_codes, max_cpp);
@@ -1640,19 +1231,17 @@ extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_bo
         const int64_t n_tiles = (n_obs + kVqmTile - 1) / kVqmTile;
         const int grid = (int)std::min<int64_t>(n_tiles, n_cu);
         hipStream_t s = as_stream(stream);
-#define SFMHIP_LAUNCH_VQM(DP, PR, FL)                                                                             \
+#define SFMHIP_LAUNCH_VQM(DP, FL)                                                                             \
     do {                                                                                                  \
-        (void)hipFuncSetAttribute((const void*)vq_mfma_kernel<DP, PR, FL>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+        (void)hipFuncSetAttribute((const void*)vq_mfma_kernel<DP, FL>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)shm);                                                               \
-        hipLaunchKernelGGL((vq_mfma_kernel<DP, PR, FL>), dim3(grid), dim3(kVqmWaves * 64), shm, s, obs, n_obs,      \
+        hipLaunchKernelGGL((vq_mfma_kernel<DP, FL>), dim3(grid), dim3(kVqmWaves * 64), shm, s, obs, n_obs,      \
                            code_book, n_codes, d, cpp, codes, dist);                                       \
     } while (0)
-        const bool pair = variant == 2;   // 2: two code blocks per step (A/B runs)
-        if (dp == 32) SFMHIP_LAUNCH_VQM(32, false, false);
-        else if (dp == 64) SFMHIP_LAUNCH_VQM(64, false, false);
-        else if (d != 128) SFMHIP_LAUNCH_VQM(128, false, false);
-        else if (pair) SFMHIP_LAUNCH_VQM(128, true, true);
-        else SFMHIP_LAUNCH_VQM(128, false, true);
+        if (dp == 32) SFMHIP_LAUNCH_VQM(32, false);
+        else if (dp == 64) SFMHIP_LAUNCH_VQM(64, false);
+        else if (d != 128) SFMHIP_LAUNCH_VQM(128, false);
+        else SFMHIP_LAUNCH_VQM(128, true);
 #undef SFMHIP_LAUNCH_VQM
         return check_launch("vq_mfma_kernel");
     }
@@ -1694,14 +1283,14 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
     SFMHIP_REQUIRE(ratio_num > 0 && ratio_den > 0 && ratio_num <= 65535 && ratio_den <= 65535,
                    "sfmhip_match_pairs_exact: ratio must be a positive fraction");
     if (P == 0) return SFMHIP_OK;
-    constexpr int IB = 256;   // the default variant's query rows per workgroup (16x16 tiles, 4 per wave, 4 waves)
+    constexpr int IB = 256;   // match_kernel's query rows per workgroup (16x16 tiles, 4 per wave, 4 waves)
     const int n_iblk = ceil_div(m_pad, IB);
     const int64_t nwg64 = (int64_t)P * n_iblk;
     SFMHIP_REQUIRE(nwg64 < INT_MAX, "sfmhip_match_pairs_exact: too many pairs for one launch");
     const int nwg = (int)nwg64;
     const long long rn2 = (long long)ratio_num * ratio_num, rd2 = (long long)ratio_den * ratio_den;
-    const char* cenv = std::getenv("SFMHIP_MATCH_CERT");   // 0: every row through the exact pass (tests)
-    const CertArgs ca{resid_row, resid_img, mode == 0 ? 1.0 : 1.0 / 127.0, (cenv && std::atoi(cenv) == 0) ? 1 : 0};
+    // SFMHIP_MATCH_CERT=0 (tests): every row through the exact pass
+    const CertArgs ca{resid_row, resid_img, mode == 0 ? 1.0 : 1.0 / 127.0, knobs().match_cert == 0 ? 1 : 0};
     hipStream_t s = as_stream(stream);
     int dev = 0, n_cu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);

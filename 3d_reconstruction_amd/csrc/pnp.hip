@@ -30,15 +30,9 @@ namespace {
 constexpr int kPnThreads = 256;
 constexpr int kPnGL = 8;                   // lanes per EPnP group
 constexpr int kPnH = kPnThreads / kPnGL;  // hypotheses per chunk
-constexpr int kJcN = 144 / kPnGL;          // convergence-check elements per lane
-constexpr int kJbN = (36 + kPnGL - 1) / kPnGL;  // 2x2 rotation blocks per lane
 static_assert(144 % kPnGL == 0 && kPnGL >= 6, "EPnP group width");
 constexpr int kPnGS = 448;                // LDS doubles per group
 constexpr int kPnStageCap = kPnH * kPnGS * 8 / 21;   // LM points staged in the group scratch (5 floats + a flag)
-#ifndef SFMHIP_PNP_FAST_ROT   // 1: measured 0.705 vs 0.713 ms (noise level, profiles/r4/ab_pnp_verify_heavyprobe_r4j.log)
-#define SFMHIP_PNP_FAST_ROT 0
-#endif
-constexpr bool kPnFastRot = SFMHIP_PNP_FAST_ROT != 0;   // EPnP Jacobi rotations without IEEE div / sqrt
 constexpr double kEps64 = 2.220446049250313e-16;
 constexpr double kDblMin64 = 2.2250738585072014e-308;
 
@@ -343,18 +337,6 @@ __device__ unsigned long long g_wgt[2 * 1024];  // per-workgroup start / end
 #define PPROF_ADD(i, v) do {} while (0)
 #endif
 
-// Round-robin pair schedule of the 12x12 parallel Jacobi: round r pairs (11, r) and
-// ((r + k) mod 11, (r - k) mod 11), k = 1..5, each ordered p < q; entry r * 6 + k = p | q << 8.
-__device__ __forceinline__ void pnp_pair_table(unsigned short* pq, int tid) {
-    if (tid < 66) {
-        const int r = tid / 6, k = tid % 6;
-        int p, q;
-        if (k == 0) { p = 11; q = r; } else { p = (r + k) % 11; q = (r - k + 11) % 11; }
-        if (p > q) { const int t = p; p = q; q = t; }
-        pq[tid] = (unsigned short)(p | (q << 8));
-    }
-}
-
 // EPnP eigen-decomposition of M^T M (12x12, symmetric) by Householder tridiagonalisation and
 // the implicit QL iteration (EISPACK tred2 / tql2 form), on a kPnGL-lane group.  A (G[gA]) is
 // reduced in LDS, each lane owning rows gl and gl + 8; the reflector v and the update vector q
@@ -513,8 +495,7 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
 }
 
 // EPnP on 5 correspondences by a kPnGL-lane group; writes (rvec, tvec) to out[6].
-__device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G, double* out,
-                                           const unsigned short* __restrict__ pq, bool ql) {
+__device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
     PPROF_INIT;
     // M^T M (12x12) into A, V = I
     // (alphas and uc - u, vc - v were staged in G by prepare: a dynamic index into D would put
@@ -539,96 +520,9 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
     }
     lds_fence();
     PPROF(7);
-    // parallel-ordered two-sided Jacobi: 11 rounds of 6 disjoint pairs per sweep
-    // the round's pairs from the workgroup's LDS table (pnp_pair_table: p | q << 8), not two
-    // modulo-11 divisions per block and round
-    auto pair_of = [&](int rnd, int k, int& p, int& q) {
-        const unsigned e = pq[rnd * 6 + k];
-        p = (int)(e & 255u);
-        q = (int)(e >> 8);
-    };
-    double* A = G + gA;
-    double* V = G + gV;
-    if (ql) epnp_eig_ql(gl, G);   // default (SFMHIP_PNP_EIG=0: the Jacobi below)
-    for (int sweep = 0; sweep < (ql ? 0 : 15); ++sweep) {
-        // convergence: off-diagonal vs diagonal mass (group reduction; kJcN (18) elements per lane,
-        // all loads issued before the sums)
-        double av[kJcN];
-#pragma unroll
-        for (int it = 0; it < kJcN; ++it) av[it] = A[gl + kPnGL * it];
-        double off = 0, dg = 0;
-#pragma unroll
-        for (int it = 0; it < kJcN; ++it) {
-            const int e = gl + kPnGL * it;
-            if (e / 12 == e % 12) dg += av[it] * av[it]; else off += av[it] * av[it];
-        }
-        for (int o = kPnGL / 2; o > 0; o >>= 1) { off += __shfl_xor(off, o, kPnGL); dg += __shfl_xor(dg, o, kPnGL); }
-        if (off <= 1e-30 * dg) break;
-        PPROF_ADD(15, 1);
-        for (int rnd = 0; rnd < 11; ++rnd) {
-            PPROF(8);
-            if (gl < 6) {
-                int p, q;
-                pair_of(rnd, gl, p, q);
-                const double apq = A[p * 12 + q], aqq = A[q * 12 + q], app = A[p * 12 + p];
-                const bool rot = apq != 0.0;
-                double t, c;
-                if (kPnFastRot) {   // Newton-refined v_rcp / v_rsq (a few ulps): any rotation this close keeps
-                                    // the sweep convergent, and the chain has no IEEE division / sqrt
-                    const double tau = (aqq - app) * (0.5 * rcp_nr(rot ? apq : 1.0));
-                    t = (tau >= 0 ? 1.0 : -1.0) * rcp_nr(fabs(tau) + sqrt_nr(fma(tau, tau, 1.0)));
-                    c = rsq_nr(fma(t, t, 1.0));
-                } else {
-                    const double tau = (aqq - app) / (2.0 * apq);
-                    t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
-                    c = 1.0 / sqrt(1.0 + t * t);
-                }
-                G[gRot + 2 * gl] = rot ? c : 1.0;
-                G[gRot + 2 * gl + 1] = rot ? t * c : 0.0;
-            }
-            lds_fence();
-            PPROF(13);
-            // A <- J^T A J and V <- V J fused per 2x2 block: block (bi, bj) of A is rows
-            // pair bi x columns pair bj, rotated by rows then by columns (the same operations,
-            // in the same order, as two separate passes); V block = rows 2bi, 2bi+1 x pair bj.
-            // The 36 blocks are disjoint: a lane loads its kJbN blocks, then rotates and stores them.
-            int ia[kJbN][4], iv[kJbN][4];
-            double ld[kJbN][12];
-#pragma unroll
-            for (int it = 0; it < kJbN; ++it) {
-                const int b = min(gl + kPnGL * it, 35);
-                const int bi = b / 6, bj = b - 6 * bi;
-                int pi, qi, pj, qj;
-                pair_of(rnd, bi, pi, qi);
-                pair_of(rnd, bj, pj, qj);
-                ia[it][0] = pi * 12 + pj; ia[it][1] = pi * 12 + qj; ia[it][2] = qi * 12 + pj; ia[it][3] = qi * 12 + qj;
-                iv[it][0] = 24 * bi + pj; iv[it][1] = 24 * bi + qj; iv[it][2] = 24 * bi + 12 + pj; iv[it][3] = 24 * bi + 12 + qj;
-                ld[it][0] = G[gRot + 2 * bi]; ld[it][1] = G[gRot + 2 * bi + 1];
-                ld[it][2] = G[gRot + 2 * bj]; ld[it][3] = G[gRot + 2 * bj + 1];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) { ld[it][4 + k] = A[ia[it][k]]; ld[it][8 + k] = V[iv[it][k]]; }
-            }
-#pragma unroll
-            for (int it = 0; it < kJbN; ++it) {
-                if (gl + kPnGL * it >= 36) break;
-                const double ci = ld[it][0], si = ld[it][1], cj = ld[it][2], sj = ld[it][3];
-                const double a00 = ld[it][4], a01 = ld[it][5], a10 = ld[it][6], a11 = ld[it][7];
-                const double v0p = ld[it][8], v0q = ld[it][9], v1p = ld[it][10], v1q = ld[it][11];
-                const double r00 = ci * a00 - si * a10, r10 = si * a00 + ci * a10;
-                const double r01 = ci * a01 - si * a11, r11 = si * a01 + ci * a11;
-                A[ia[it][0]] = cj * r00 - sj * r01;
-                A[ia[it][1]] = sj * r00 + cj * r01;
-                A[ia[it][2]] = cj * r10 - sj * r11;
-                A[ia[it][3]] = sj * r10 + cj * r11;
-                V[iv[it][0]] = cj * v0p - sj * v0q;
-                V[iv[it][1]] = sj * v0p + cj * v0q;
-                V[iv[it][2]] = cj * v1p - sj * v1q;
-                V[iv[it][3]] = sj * v1p + cj * v1q;
-            }
-            lds_fence();
-            PPROF(14);
-        }
-    }
+    // the 12x12 symmetric eigen-decomposition: Householder tridiagonalisation + implicit QL
+    // (a parallel-ordered two-sided Jacobi measured slower: EPnP 154 vs 98 us of QL, round 4)
+    epnp_eig_ql(gl, G);
     PPROF(8);
     // the 4 smallest eigenvalues (ascending), canonical signs
     int vi[4];
@@ -1013,7 +907,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
     const double* __restrict__ obj, const double* __restrict__ img, const int64_t* __restrict__ offs,
     const double* __restrict__ cam, int max_iters, double reproj, double confidence, float* __restrict__ wf,
     double* __restrict__ rvec_out, double* __restrict__ tvec_out, uint8_t* __restrict__ mask,
-    int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out, int eig_ql) {
+    int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out, int32_t* __restrict__ ok_out) {
     __shared__ double s_grp[kPnH * kPnGS];
     __shared__ double s_models[kPnH][6 + 9];  // rvec, tvec, R
     __shared__ int s_cnt[kPnH];
@@ -1022,7 +916,6 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
     __shared__ double s_red[4 * 28];
     __shared__ double s_lm[6 + 6 + 27 + 9];   // param, prev, dRdr, R
     __shared__ int s_niters, s_maxgood, s_k0, s_last, s_flag;
-    __shared__ unsigned short s_pq[66];
 
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int h = tid / kPnGL, gl = tid % kPnGL;
@@ -1038,7 +931,6 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         mask[off + i] = 0;
     }
     if (tid == 0) { s_niters = max(max_iters, 1); s_maxgood = 0; s_k0 = 0; s_last = -1; }
-    pnp_pair_table(s_pq, tid);
     __syncthreads();
     if (n < 5) {
         if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
@@ -1052,7 +944,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
             EpnpData D;
             load_sample(idx, D);
             prepare(D, s_grp);
-            epnp_group(D, gl, s_grp, s_best, s_pq, eig_ql != 0);
+            epnp_group(D, gl, s_grp, s_best);
         }
         __syncthreads();
         if (tid == 0) {
@@ -1087,7 +979,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
             double* G = s_grp + h * kPnGS;
             prepare(D, G);
             PPROF(6);
-            epnp_group(D, gl, G, s_models[h], s_pq, eig_ql != 0);
+            epnp_group(D, gl, G, s_models[h]);
             if (gl == 0) rodrigues(s_models[h], s_models[h] + 6);
         }
         __syncthreads();
@@ -1144,264 +1036,6 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
 }
 
 
-// ---------------------------------------------------------------------------
-// Phase-split form (SFMHIP_PNP_MONO=0; the default is pnp_ransac_kernel).  With one workgroup per
-// problem the call lasts as long as its slowest problem: one that needs a second 32-hypothesis
-// chunk (33-37 iterations on the bench scene) runs the EPnP solves twice in a row, at one wave per
-// SIMD (the whole kernel's 454 VGPRs), scoring included.  Here the phases are separate kernels:
-//   pnp_init_kernel    float copies, per-problem state, outputs of n < 5, round 0's samples
-//                      (hypotheses up to min(niters, 32): one chunk);
-//   pnp_solve_kernel   persistent workgroups take (problem, chunk) items: the chunk's EPnP solves
-//                      (one workgroup per CU: 454 VGPRs and 115 KB of LDS per 32 hypotheses, so a
-//                      second chunk cannot run beside the first without halving both);
-//   pnp_score_kernel   each item's hypotheses scored on every correspondence (96 VGPRs: full
-//                      occupancy, where the one-workgroup kernel scored at one wave per SIMD);
-//   pnp_replay_kernel  one wave per problem replays the counts in OpenCV's order (a model
-//                      replaces the best iff count > max(best, 4); niters shrinks) and, unless the
-//                      problem is complete, draws round 1's samples up to the niters it left;
-//   pnp_final_kernel   the best model's inlier mask, CvLevMarq and the outputs (pnp_refine).
-// The same samples, solver, counts and replay as pnp_ransac_kernel: the same outputs; a
-// hypothesis past the final niters costs work, never a different result.
-constexpr int kPnSpecHyps = 32;   // round 0: one chunk per problem (the solve kernel holds one workgroup per CU)
-constexpr int kPnRounds = 2;
-constexpr int kPnFive = 1, kPnDone = 2;
-
-struct PnpState {
-    uint64_t rng;
-    int n, flags, niters, maxgood, gen_upto, eval_upto, rk, last, best_k;
-};
-
-struct PnpBufs {
-    PnpState* st;
-    int* samp;        // [P][hcap][5]
-    double* models;   // [P][hcap][15]: rvec, tvec, R
-    int* cnt;         // [P][hcap]
-    int2* list;       // [kPnRounds][P * cmax]: {problem, chunk (-1: the n == 5 call)}
-    int* ctr;         // [2 kPnRounds]: (count, head) per round
-    int cmax, hcap;
-};
-
-// One lane per problem: samples [gen_upto, target) in cv::RNG order, then the chunks covering them.
-__device__ void pnp_gen(PnpState& s, int p, int P, int round, const PnpBufs& B) {
-    const int target = round + 1 < kPnRounds ? min(s.niters, kPnSpecHyps) : s.niters;
-    const unsigned n = (unsigned)s.n;
-    const unsigned mg = (unsigned)((1ULL << 32) / n);   // n > 5
-    int* smp = B.samp + (size_t)p * B.hcap * 5;
-    for (int k = s.gen_upto; k < target; ++k) {
-        int d[5];
-        cv_rng_sample5(s.rng, n, mg, d);
-#pragma unroll
-        for (int i = 0; i < 5; ++i) smp[5 * k + i] = d[i];
-    }
-    s.gen_upto = max(s.gen_upto, target);
-    const int c0 = s.eval_upto / kPnH, c1 = (target + kPnH - 1) / kPnH;
-    if (c1 > c0) {
-        int2* list = B.list + (size_t)round * P * B.cmax;
-        const int base = atomicAdd(B.ctr + 2 * round, c1 - c0);
-        for (int c = c0; c < c1; ++c) list[base + c - c0] = make_int2(p, c);
-        s.eval_upto = c1 * kPnH;
-    }
-}
-
-__global__ __launch_bounds__(kPnThreads) void pnp_init_kernel(const double* __restrict__ obj,
-                                                              const double* __restrict__ img,
-                                                              const int64_t* __restrict__ offs, int max_iters,
-                                                              float* __restrict__ wf, uint8_t* __restrict__ mask,
-                                                              int32_t* __restrict__ ninl_out,
-                                                              int32_t* __restrict__ iters_out,
-                                                              int32_t* __restrict__ ok_out, int P, PnpBufs B) {
-    const int p = blockIdx.x, tid = threadIdx.x;
-    const int64_t off = offs[p];
-    const int n = (int)(offs[p + 1] - off);
-    float* f = wf + off * 5;
-    for (int i = tid; i < n; i += kPnThreads) {
-        for (int k = 0; k < 3; ++k) f[5 * i + k] = (float)obj[3 * (off + i) + k];
-        for (int k = 0; k < 2; ++k) f[5 * i + 3 + k] = (float)img[2 * (off + i) + k];
-        mask[off + i] = 0;
-    }
-    if (tid == 0) {
-        PnpState s;
-        s.rng = ~0ULL;
-        s.n = n;
-        s.flags = n < 5 ? kPnDone : n == 5 ? kPnFive : 0;
-        s.niters = max(max_iters, 1);
-        s.maxgood = 0;
-        s.gen_upto = s.eval_upto = s.rk = 0;
-        s.last = s.best_k = -1;
-        if (n < 5) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
-        if (n == 5) B.list[atomicAdd(B.ctr, 1)] = make_int2(p, -1);
-        if (n > 5) pnp_gen(s, p, P, 0, B);
-        B.st[p] = s;
-    }
-}
-
-__global__ __launch_bounds__(kPnThreads) void pnp_solve_kernel(
-    int P, int round, const int64_t* __restrict__ offs, const double* __restrict__ cam,
-    const float* __restrict__ wf, double* __restrict__ rvec_out, double* __restrict__ tvec_out,
-    uint8_t* __restrict__ mask, int32_t* __restrict__ ninl_out, int32_t* __restrict__ iters_out,
-    int32_t* __restrict__ ok_out, int eig_ql, PnpBufs B) {
-    __shared__ double s_grp[kPnH * kPnGS];
-    __shared__ double s_models[kPnH][6 + 9];
-    __shared__ unsigned short s_pq[66];
-    __shared__ int s_item, s_five[5];
-    const int tid = threadIdx.x, h = tid / kPnGL, gl = tid % kPnGL;
-    pnp_pair_table(s_pq, tid);
-    if (tid < 5) s_five[tid] = tid;
-    const int2* list = B.list + (size_t)round * P * B.cmax;
-    const int count = B.ctr[2 * round];
-    for (;;) {
-        if (tid == 0) s_item = atomicAdd(B.ctr + 2 * round + 1, 1);
-        __syncthreads();
-        const int it = s_item;
-        if (it >= count) break;
-        const int p = list[it].x, c = list[it].y;
-        const int64_t off = offs[p];
-        const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
-        const float* f = wf + off * 5;
-        // c < 0: model_points == npoints, solvePnP(EPnP) on all points (group 0), no refinement.
-        // One call site of the solver for both kinds of item (one inlined copy of it).
-        const bool five = c < 0;
-        const int k = five ? 0 : c * kPnH + h;
-        if (five ? h == 0 : k < B.st[p].gen_upto) {
-            EpnpData D;
-            pnp_load_sample(f, five ? s_five : B.samp + ((size_t)p * B.hcap + k) * 5, fx, fy, cx, cy, D);
-            double* G = s_grp + h * kPnGS;
-            pnp_prepare(D, G, gl);
-            epnp_group(D, gl, G, s_models[h], s_pq, eig_ql != 0);
-            if (gl == 0 && !five) rodrigues(s_models[h], s_models[h] + 6);
-            lds_fence();
-            if (!five) {
-                double* mo = B.models + ((size_t)p * B.hcap + k) * 15;
-                mo[gl] = s_models[h][gl];
-                if (gl + kPnGL < 15) mo[gl + kPnGL] = s_models[h][gl + kPnGL];
-            }
-        }
-        __syncthreads();
-        if (five) {
-            if (tid == 0) {
-                for (int q = 0; q < 3; ++q) { rvec_out[3 * p + q] = s_models[0][q]; tvec_out[3 * p + q] = s_models[0][3 + q]; }
-                ok_out[p] = 1; ninl_out[p] = 5; iters_out[p] = 1;
-            }
-            if (tid < 5) mask[off + tid] = 1;
-            __syncthreads();
-        }
-    }
-}
-
-// One item per workgroup pass: the chunk's models against every correspondence, four per step.
-__global__ __launch_bounds__(kPnThreads) void pnp_score_kernel(int P, int round, const int64_t* __restrict__ offs,
-                                                               const double* __restrict__ cam, double reproj,
-                                                               const float* __restrict__ wf, PnpBufs B) {
-    __shared__ double s_m[kPnH][15];
-    __shared__ int s_cnt[kPnH];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int2* list = B.list + (size_t)round * P * B.cmax;
-    const int count = B.ctr[2 * round];
-    const float thr = (float)(reproj * reproj);
-    for (int it = blockIdx.x; it < count; it += gridDim.x) {
-        const int p = list[it].x, c = list[it].y;
-        if (c < 0) continue;   // uniform
-        const int64_t off = offs[p];
-        const int n = B.st[p].n;
-        const int nh = min(kPnH, B.st[p].gen_upto - c * kPnH);
-        const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
-        const float* f = wf + off * 5;
-        const double* mo = B.models + ((size_t)p * B.hcap + c * kPnH) * 15;
-        for (int e = tid; e < nh * 15; e += kPnThreads) s_m[e / 15][e % 15] = mo[e];
-        if (tid < kPnH) s_cnt[tid] = 0;
-        __syncthreads();
-        for (int i0 = 0; i0 < n; i0 += kPnThreads) {
-            const int i = i0 + tid;
-            const bool valid = i < n;
-            float X = 0, Y = 0, Z = 0, u = 0, v = 0;
-            if (valid) { X = f[5 * i]; Y = f[5 * i + 1]; Z = f[5 * i + 2]; u = f[5 * i + 3]; v = f[5 * i + 4]; }
-            for (int h0 = 0; h0 < nh; h0 += 4) {
-                float e4[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int hh = min(h0 + q, nh - 1);
-                    float pu, pv;
-                    project_f(s_m[hh] + 6, s_m[hh] + 3, fx, fy, cx, cy, X, Y, Z, pu, pv);
-                    const float du = u - pu, dv = v - pv;
-                    e4[q] = du * du + dv * dv;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int cq = __popcll(__ballot(valid && e4[q] <= thr));
-                    if (lane == 0 && cq && h0 + q < nh) atomicAdd(&s_cnt[h0 + q], cq);
-                }
-            }
-        }
-        __syncthreads();
-        if (tid < nh) B.cnt[(size_t)p * B.hcap + c * kPnH + tid] = s_cnt[tid];
-        __syncthreads();
-    }
-}
-
-// One wave per problem: the counts of the listed hypotheses staged in LDS, lane 0 replays them.
-__global__ __launch_bounds__(64) void pnp_replay_kernel(int P, int round, double confidence, PnpBufs B) {
-    __shared__ int s_c[256];
-    const int p = blockIdx.x, lane = threadIdx.x;
-    PnpState s = B.st[p];
-    if (s.flags & (kPnFive | kPnDone)) return;   // uniform
-    int nit = s.niters, k = s.rk;
-    bool done = false;
-    while (k < s.eval_upto && k < nit && !done) {   // windows of 256 hypotheses
-        const int w = min(256, s.eval_upto - k);
-        for (int t = lane; t < w; t += 64) s_c[t] = B.cnt[(size_t)p * B.hcap + k + t];
-        __syncthreads();
-        if (lane == 0) {
-            int t = 0;
-            for (; t < w; ++t) {
-                if (k + t >= nit) { done = true; break; }
-                const int good = s_c[t];
-                if (good > max(s.maxgood, 4)) {
-                    s.best_k = k + t;
-                    s.maxgood = good;
-                    nit = update_num_iters(confidence, (double)(s.n - good) / s.n, 5, nit);
-                }
-                s.last = k + t;
-            }
-            s_c[0] = t | (done ? 1 << 30 : 0);
-        }
-        __syncthreads();
-        const int r = s_c[0];
-        done = (r >> 30) & 1;
-        k += r & ((1 << 30) - 1);
-        nit = __shfl(nit, 0);
-        __syncthreads();
-    }
-    if (lane != 0) return;
-    s.rk = k;
-    s.niters = nit;
-    if (done || k >= nit) s.flags |= kPnDone;
-    else if (round + 1 < kPnRounds) pnp_gen(s, p, P, round + 1, B);
-    B.st[p] = s;
-}
-
-__global__ __launch_bounds__(kPnThreads) void pnp_final_kernel(const int64_t* __restrict__ offs,
-                                                               const double* __restrict__ cam, double reproj,
-                                                               const float* __restrict__ wf,
-                                                               double* __restrict__ rvec_out,
-                                                               double* __restrict__ tvec_out,
-                                                               uint8_t* __restrict__ mask,
-                                                               int32_t* __restrict__ ninl_out,
-                                                               int32_t* __restrict__ iters_out,
-                                                               int32_t* __restrict__ ok_out, PnpBufs B) {
-    __shared__ double s_best[6];
-    __shared__ double s_red[4 * 28];
-    __shared__ double s_lm[6 + 6 + 27 + 9];
-    const int p = blockIdx.x, tid = threadIdx.x;
-    const PnpState s = B.st[p];
-    if (s.n <= 5) return;   // n < 5: ess_init; n == 5: the solve kernel
-    if (s.maxgood > 0 && tid < 6) s_best[tid] = B.models[((size_t)p * B.hcap + s.best_k) * 15 + tid];
-    __syncthreads();
-    const int64_t off = offs[p];
-    const double fx = cam[4 * p], fy = cam[4 * p + 1], cx = cam[4 * p + 2], cy = cam[4 * p + 3];
-    pnp_refine(p, s.n, off, wf + off * 5, fx, fy, cx, cy, (float)(reproj * reproj), s.maxgood, s.last, s_best,
-               s_lm, s_red, mask, rvec_out, tvec_out, ninl_out, iters_out, ok_out);
-}
-
 }  // namespace
 }  // namespace sfmhip
 
@@ -1431,64 +1065,10 @@ extern "C" int sfmhip_pnp_ransac(const double* obj, const double* img, const int
                    "pnp_ransac: null pointer");
     SFMHIP_REQUIRE(reprojection_error > 0 && confidence >= 0 && confidence <= 1,
                    "pnp_ransac: reprojection_error > 0, confidence in [0, 1]");
-    // EPnP's 12x12 eigen-decomposition: tridiagonal QL (default) or the parallel Jacobi (A/B)
-    const char* eg = getenv("SFMHIP_PNP_EIG");
-    const int eig_ql = eg && *eg ? atoi(eg) : 1;
-    hipStream_t st = as_stream(stream);
-    const char* mo = getenv("SFMHIP_PNP_MONO");   // 1 (default): one workgroup per problem; 0: phase-split
-    if (!(mo && *mo && atoi(mo) == 0)) {
-        hipLaunchKernelGGL(pnp_ransac_kernel, dim3(n_problems), dim3(kPnThreads), 0, st, obj, img, offsets, cam,
-                           iterations, reprojection_error, confidence, work, rvec, tvec, inlier_mask, n_inliers, iters,
-                           ok, eig_ql);
-        return check_launch("pnp_ransac_kernel");
-    }
-    const int cmax = ceil_div(std::max(iterations, 1), kPnH), hcap = cmax * kPnH;
-    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t per = sizeof(PnpState) + (size_t)hcap * (5 * sizeof(int) + 15 * sizeof(double) + sizeof(int)) +
-                       kPnRounds * (size_t)cmax * sizeof(int2);
-    const int batch = (int)std::max<int64_t>(1, std::min<int64_t>(n_problems, ((size_t)192 << 20) / per));
-    const size_t bytes = al(batch * sizeof(PnpState)) + al((size_t)batch * hcap * 5 * sizeof(int)) +
-                         al((size_t)batch * hcap * 15 * sizeof(double)) + al((size_t)batch * hcap * sizeof(int)) +
-                         al(kPnRounds * (size_t)batch * cmax * sizeof(int2)) + al(2 * kPnRounds * sizeof(int));
-    char* base = nullptr;
-    if (scratch_alloc((void**)&base, bytes, st) != hipSuccess) {
-        (void)hipGetLastError();
-        set_error("pnp_ransac: scratch allocation of %zu bytes failed", bytes);
-        return SFMHIP_E_HIP;
-    }
-    PnpBufs B;
-    char* cur = base;
-    auto carve = [&](size_t b) { char* r = cur; cur += al(b); return r; };
-    B.st = (PnpState*)carve(batch * sizeof(PnpState));
-    B.samp = (int*)carve((size_t)batch * hcap * 5 * sizeof(int));
-    B.models = (double*)carve((size_t)batch * hcap * 15 * sizeof(double));
-    B.cnt = (int*)carve((size_t)batch * hcap * sizeof(int));
-    B.list = (int2*)carve(kPnRounds * (size_t)batch * cmax * sizeof(int2));
-    B.ctr = (int*)carve(2 * kPnRounds * sizeof(int));
-    B.cmax = cmax;
-    B.hcap = hcap;
-    int rc = SFMHIP_OK;
-    for (int p0 = 0; p0 < n_problems && rc == SFMHIP_OK; p0 += batch) {
-        const int PB = std::min(batch, n_problems - p0);
-        const int64_t* of = offsets + p0;
-        const double* cm = cam + 4 * (size_t)p0;
-        double *rv = rvec + 3 * (size_t)p0, *tv = tvec + 3 * (size_t)p0;
-        int32_t *nib = n_inliers + p0, *itb = iters + p0, *okb = ok + p0;
-        (void)hipMemsetAsync(B.ctr, 0, 2 * kPnRounds * sizeof(int), st);
-        hipLaunchKernelGGL(pnp_init_kernel, dim3(PB), dim3(kPnThreads), 0, st, obj, img, of, iterations, work,
-                           inlier_mask, nib, itb, okb, PB, B);
-        for (int round = 0; round < kPnRounds; ++round) {
-            const int items = (int)std::min<int64_t>((int64_t)PB * (round == 0 ? std::min(cmax, ceil_div(kPnSpecHyps, kPnH)) : cmax), 1 << 30);
-            hipLaunchKernelGGL(pnp_solve_kernel, dim3(std::min(items, 512)), dim3(kPnThreads), 0, st, PB, round, of,
-                               cm, work, rv, tv, inlier_mask, nib, itb, okb, eig_ql, B);
-            hipLaunchKernelGGL(pnp_score_kernel, dim3(std::min(items, 2048)), dim3(kPnThreads), 0, st, PB, round, of,
-                               cm, reprojection_error, work, B);
-            hipLaunchKernelGGL(pnp_replay_kernel, dim3(PB), dim3(64), 0, st, PB, round, confidence, B);
-        }
-        hipLaunchKernelGGL(pnp_final_kernel, dim3(PB), dim3(kPnThreads), 0, st, of, cm, reprojection_error, work, rv,
-                           tv, inlier_mask, nib, itb, okb, B);
-        rc = check_launch("pnp_*_kernel");
-    }
-    scratch_free(base, st);
-    return rc;
+    // one workgroup per problem (a phase-split form -- EPnP solves, scoring and the RANSAC replay as
+    // separate kernels over (problem, chunk) items -- measured slower: 0.694 vs 0.555 ms, round 4)
+    hipLaunchKernelGGL(pnp_ransac_kernel, dim3(n_problems), dim3(kPnThreads), 0, as_stream(stream), obj, img, offsets,
+                       cam, iterations, reprojection_error, confidence, work, rvec, tvec, inlier_mask, n_inliers, iters,
+                       ok);
+    return check_launch("pnp_ransac_kernel");
 }

@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
                                                               int32_t* __restrict__ nmodels_out,
                                                               uint8_t* __restrict__ mask,
                                                               int32_t* __restrict__ ninl_out,
-                                                              int32_t* __restrict__ iters_out, int f32pre, EssBufs B) {
+                                                              int32_t* __restrict__ iters_out, EssBufs B) {
     constexpr int CH = NT / kGL, NW = NT / 64;
     __shared__ double s_grp[CH * kGS];
     __shared__ double s_models[CH * kMaxModels * 9];
@@ -1152,10 +1152,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void es
         const int nlist = s_nlist;
         RPROF(9, tp);
         auto score = [&](const int* lst, int nl, int lo, int hi) {
-            if (f32pre)
-                score_chunk_f32<NT>(q, n, lst, nl, s_models, s_models32, s_cnt, tf, Tmax, tlo, thi, tid, lo, hi);
-            else
-                score_chunk<NT>(q, n, lst, nl, s_models, s_cnt, tf, tlo, thi, tid, lo, hi);
+            score_chunk_f32<NT>(q, n, lst, nl, s_models, s_models32, s_cnt, tf, Tmax, tlo, thi, tid, lo, hi);
         };
         // Rounds >= 1: every model of this chunk is replayed after the previous rounds' replays, so
         // one whose count cannot exceed max(their best, 4) never replaces the best and need not be
@@ -1438,7 +1435,7 @@ __global__ __launch_bounds__(kPThreads) void recover_pose_kernel(
     const double* __restrict__ Ein, int64_t e_stride, const double* __restrict__ pts0,
     const double* __restrict__ pts1, const int64_t* __restrict__ offs, const double* __restrict__ cam,
     const uint8_t* __restrict__ mask_in, double dist, double* __restrict__ R_out, double* __restrict__ t_out,
-    uint8_t* __restrict__ mask_out, int32_t* __restrict__ good_out, int fast) {
+    uint8_t* __restrict__ mask_out, int32_t* __restrict__ good_out) {
     __shared__ double sP[4][12];
     __shared__ double sPP[4][24];   // [P0 | P_k] contiguous, for dlt_point_normal
     __shared__ int s_cnt[4];
@@ -1494,7 +1491,7 @@ __global__ __launch_bounds__(kPThreads) void recover_pose_kernel(
                 // decisions are dlt_point's
                 double Q[4];
                 bool ok = false, sure = false;
-                if (fast && dlt_point_normal(sPP[k], x1, y1, x2, y2, Q) == 0) {
+                if (dlt_point_normal(sPP[k], x1, y1, x2, y2, Q) == 0) {
                     double sc;
                     test(Q, ok, sc);
                     sure = sc > 1.0;
@@ -1582,21 +1579,16 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
                    "find_essential: null pointer");
     SFMHIP_REQUIRE(prob >= 0 && prob <= 1 && threshold > 0, "find_essential: prob in [0,1], threshold > 0");
     hipStream_t st = as_stream(stream);
-    auto env = [](const char* name, int dflt) {
-        const char* v = getenv(name);
-        return v && *v ? atoi(v) : dflt;
-    };
-    const int mono = env("SFMHIP_ESS_MONO", 0);   // A/B: the one-workgroup-per-pair kernel
-    if (mono) {
+    if (knobs().ess_mono) {   // the one-workgroup-per-pair kernel (tests: the balanced form's reference)
         hipLaunchKernelGGL(essential_ransac_kernel, dim3(n_pairs), dim3(kRThreads), 0, st, pts0, pts1, offsets, cam,
                            prob, threshold, max_iters, work, E, n_models, mask, n_inliers, iters);
         return check_launch("essential_ransac_kernel");
     }
     // load-balanced form: per-pair scratch, pairs in batches of at most ~192 MB of it.  Chunk
     // kernel: 256 threads (16 hypotheses per item, two workgroups per CU so one's scoring overlaps
-    // the other's solve) or 512 (SFMHIP_ESS_CT=512: 32 per item, one per CU)
-    const int ct = env("SFMHIP_ESS_CT", 256) == 512 ? 512 : 256;
-    const int f32pre = env("SFMHIP_ESS_F32", 1);   // packed-f32 Sampson pre-test (0: f64 throughout)
+    // the other's solve; 512 threads, 32 per item, measured slower), packed-f32 Sampson pre-test
+    // with certified bounds (f64 throughout measured slower: 1.065 vs 0.98 ms)
+    constexpr int ct = 256;
     const int ch = ct / kGL, recmax = ch * kMaxModels;
     const int cmax = ceil_div(std::max(max_iters, 1), ch), hcap = cmax * ch;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1630,21 +1622,21 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
     B.cmax = cmax;
     B.hcap = hcap;
     B.ch = ch;
-    // samples drawn ahead on a side stream while round 0 runs (SFMHIP_ESS_PREGEN=0: off)
+    // samples drawn ahead on a side stream while round 0 runs
     int dev = -1;
-    EssSide* side = env("SFMHIP_ESS_PREGEN", 1) && hipGetDevice(&dev) == hipSuccess ? ess_side(dev) : nullptr;
+    EssSide* side = hipGetDevice(&dev) == hipSuccess ? ess_side(dev) : nullptr;
     (void)hipGetLastError();
     std::unique_lock<std::mutex> side_lock;
     if (side) side_lock = std::unique_lock<std::mutex>(side->mu);
     else B.spec_upto = nullptr;
-    // records whose E is kept (tests: 0 re-solves every chosen model from its sample)
-    B.rece = std::min(kRecE, std::max(0, env("SFMHIP_ESS_RECE", kRecE)));
-    // speculation caps: round 0 (SFMHIP_ESS_CAP0, default kSpecHyps) and round 1 (SFMHIP_ESS_CAP1, at
-    // least cap0): the pre-drawn samples' reach by default, so round 1 is the last round a pair needs
-    // unless its niters exceeds kPreHyps.  Whole chunks: a listed chunk counts as evaluated, and the
-    // chunk kernel solves only below the listing target, so a target short of niters must end a chunk
-    B.cap0 = ceil_div(std::max(1, env("SFMHIP_ESS_CAP0", kSpecHyps)), ch) * ch;
-    B.cap1 = std::max(B.cap0, ceil_div(std::max(1, env("SFMHIP_ESS_CAP1", kPreHyps)), ch) * ch);
+    // records whose E is kept (SFMHIP_ESS_RECE, tests: 0 re-solves every chosen model from its sample)
+    B.rece = std::min(kRecE, std::max(0, knobs().ess_rece));
+    // speculation caps: round 0 (kSpecHyps; 32/48/96 measured no faster) and round 1 (the pre-drawn
+    // samples' reach), so round 1 is the last round a pair needs unless its niters exceeds kPreHyps.
+    // Whole chunks: a listed chunk counts as evaluated, and the chunk kernel solves only below the
+    // listing target, so a target short of niters must end a chunk
+    B.cap0 = ceil_div(kSpecHyps, ch) * ch;
+    B.cap1 = std::max(B.cap0, ceil_div(kPreHyps, ch) * ch);
     int rc = SFMHIP_OK;
     for (int p0 = 0; p0 < n_pairs && rc == SFMHIP_OK; p0 += batch) {
         const int PB = std::min(batch, n_pairs - p0);
@@ -1663,13 +1655,9 @@ extern "C" int sfmhip_find_essential(const double* pts0, const double* pts1, con
         }
         for (int round = 0; round < kEssRounds; ++round) {
             const int items = round == 0 ? ceil_div(B.cap0, ch) : round + 1 < kEssRounds ? ceil_div(B.cap1, ch) : cmax;
-            const int g = (int)std::min<int64_t>(ct == 512 ? 512 : 1024, (int64_t)PB * std::min(cmax, items));
-            if (ct == 512)
-                hipLaunchKernelGGL(ess_chunk_kernel<512>, dim3(g), dim3(512), 0, st, PB, round, of, cm, threshold,
-                                   work, Eb, nmb, mask, nib, itb, f32pre, B);
-            else
-                hipLaunchKernelGGL(ess_chunk_kernel<256>, dim3(g), dim3(256), 0, st, PB, round, of, cm, threshold,
-                                   work, Eb, nmb, mask, nib, itb, f32pre, B);
+            const int g = (int)std::min<int64_t>(1024, (int64_t)PB * std::min(cmax, items));
+            hipLaunchKernelGGL(ess_chunk_kernel<ct>, dim3(g), dim3(ct), 0, st, PB, round, of, cm, threshold, work, Eb,
+                               nmb, mask, nib, itb, B);
             if (side && round == 0) (void)hipStreamWaitEvent(st, side->join, 0);   // join before round 1's draws
             hipLaunchKernelGGL(ess_replay_kernel, dim3(PB), dim3(64), 0, st, PB, round, prob, B);
         }
@@ -1690,9 +1678,7 @@ extern "C" int sfmhip_recover_pose(const double* E, int64_t e_stride, const doub
     SFMHIP_REQUIRE(E && pts0 && pts1 && offsets && cam && R && t && mask_out && n_good,
                    "recover_pose: null pointer");
     SFMHIP_REQUIRE(e_stride >= 9, "recover_pose: e_stride >= 9");
-    const char* rpf = getenv("SFMHIP_RP_FAST");   // A/B: 0 = dlt_point for every triangulation
-    const int rp_fast = rpf && *rpf ? atoi(rpf) : 1;
     hipLaunchKernelGGL(recover_pose_kernel, dim3(n_pairs), dim3(kPThreads), 0, as_stream(stream), E, e_stride,
-                       pts0, pts1, offsets, cam, mask_in, distance_thresh, R, t, mask_out, n_good, rp_fast);
+                       pts0, pts1, offsets, cam, mask_in, distance_thresh, R, t, mask_out, n_good);
     return check_launch("recover_pose_kernel");
 }

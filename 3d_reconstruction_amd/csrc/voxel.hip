@@ -434,137 +434,18 @@ __device__ __forceinline__ void render_body(const float* __restrict__ gvm, int D
     }
 }
 
-// Two-phase form of render_body<true> (SFMHIP_RENDER_2PH): per group of NCH chunks of 64 samples,
-// phase 1 issues every chunk's depth and sdf-plane gathers together and composites the alphas
-// (the transmittance scan in chunk order), phase 2 fetches the colour lines of the alpha != 0
-// samples chunk by chunk.  Each chunk's scan, weights and sums are the same operations in the same
-// order as render_body's, so the colours are the same bits; the plane gathers of all chunks are in
-// flight at once instead of one chunk's per round trip.
-template <int NCH>
-__device__ __forceinline__ void render_body_2ph(const float* __restrict__ gvm, int D, int H, int W, Bounds B, int mode,
-                                                const float* __restrict__ ro, const float* __restrict__ rd,
-                                                const float* __restrict__ zv, int64_t nrays, int S,
-                                                float* __restrict__ rgb, const unsigned* __restrict__ order,
-                                                const float* __restrict__ sdfp) {
-    const int lane = threadIdx.x & 63;
-    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (w >= nrays) return;  // wave-uniform
-    const int64_t ray = order ? (int64_t)order[w] : w;
-    const float o[3] = {ro[3 * ray], ro[3 * ray + 1], ro[3 * ray + 2]};
-    const float d[3] = {rd[3 * ray], rd[3 * ray + 1], rd[3 * ray + 2]};
-    if (!(isfinite(d[0]) && isfinite(d[1]) && isfinite(d[2]))) {   // the full path (wave-uniform)
-        render_body<true>(gvm, D, H, W, B, mode, ro, rd, zv, nrays, S, rgb, order, sdfp);
-        return;
-    }
-    const float* z = zv + (size_t)ray * S;
-    float carry = 1.f;
-    float cr = 0.f, cg = 0.f, cb = 0.f, ws = 0.f;
-    for (int g0 = 0; g0 < S; g0 += 64 * NCH) {
-        float alpha[NCH], wgt[NCH], zsv[NCH];
-        bool lines[NCH];
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {   // phase 1: depths, plane sdf, alpha
-            const int s = g0 + 64 * c + lane;
-            alpha[c] = 0.f;
-            lines[c] = false;
-            zsv[c] = 0.f;
-            if (s < S) {
-                const float zs = z[s];
-                zsv[c] = zs;
-                const float p[3] = {o[0] + d[0] * zs, o[1] + d[1] * zs, o[2] + d[2] * zs};
-                const float delta = (s + 1 < S) ? (z[s + 1] - zs) : 1e10f;
-                float g[3], sdf = 0.f;
-                if (normalise(p, B, mode, g)) {
-                    Corners cn;
-                    corners(g, D, H, W, cn);
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) {
-                        int x, y, zz;
-                        if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
-                        sdf = sdf + sdfp[((size_t)zz * H + y) * W + x] * cn.w[q];
-                    }
-                }
-                alpha[c] = 1.f - expf((-fmaxf(sdf, 0.f)) * delta);
-                lines[c] = alpha[c] != 0.f;
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {   // transmittance in chunk order (render_body's scan)
-            wgt[c] = 0.f;
-            if (g0 + 64 * c >= S) continue;   // wave-uniform
-            float incl = 1.f - alpha[c];
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const float up = __shfl_up(incl, off, 64);
-                if (lane >= off) incl = incl * up;
-            }
-            float excl = __shfl_up(incl, 1, 64);
-            if (lane == 0) excl = 1.f;
-            wgt[c] = (carry * excl) * alpha[c];
-            carry = carry * __shfl(incl, 63, 64);
-        }
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {   // phase 2: colour lines where alpha != 0, sums in chunk order
-            if (g0 + 64 * c >= S) continue;   // wave-uniform
-            float k[27];
-#pragma unroll
-            for (int q = 0; q < 27; ++q) k[q] = 0.f;
-            if (lines[c]) {
-                const float zs = zsv[c];
-                const float p[3] = {o[0] + d[0] * zs, o[1] + d[1] * zs, o[2] + d[2] * zs};
-                float g[3];
-                normalise(p, B, mode, g);   // true: alpha != 0 needs a sample inside the mask
-                Corners cn;
-                corners(g, D, H, W, cn);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    int x, y, zz;
-                    if (!corner_in(cn, q, D, H, W, x, y, zz)) continue;
-                    const float cw = cn.w[q];
-                    const float4* v = reinterpret_cast<const float4*>(gvm + ((((size_t)zz * H + y) * W + x) << 5));
-                    float vv[28];
-#pragma unroll
-                    for (int t = 0; t < 7; ++t) {
-                        const float4 f = v[t];
-                        vv[4 * t] = f.x; vv[4 * t + 1] = f.y; vv[4 * t + 2] = f.z; vv[4 * t + 3] = f.w;
-                    }
-#pragma unroll
-                    for (int q2 = 0; q2 < 27; ++q2) k[q2] = k[q2] + vv[1 + q2] * cw;
-                }
-            }
-            float col[3];
-            sh_colour(k, d[0], d[1], d[2], col);
-            const float wc = wgt[c];
-            float pr = wc * col[0], pg = wc * col[1], pb = wc * col[2], pw = wc;
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                pr += __shfl_xor(pr, off, 64);
-                pg += __shfl_xor(pg, off, 64);
-                pb += __shfl_xor(pb, off, 64);
-                pw += __shfl_xor(pw, off, 64);
-            }
-            cr += pr; cg += pg; cb += pb; ws += pw;
-        }
-    }
-    if (lane == 0) {
-        rgb[3 * ray] = (cr + 1.f) - ws;
-        rgb[3 * ray + 1] = (cg + 1.f) - ws;
-        rgb[3 * ray + 2] = (cb + 1.f) - ws;
-    }
-}
-
-// OCC: amdgpu_waves_per_eu floor (register budget) for the occupancy A/B (SFMHIP_RENDER_OCC);
-// 0 = the compiler's choice (130 VGPRs: 3 waves per SIMD)
-template <bool SIG, int OCC, int NCH = 0>
+// OCC: amdgpu_waves_per_eu floor (register budget); 0 = the compiler's choice (130 VGPRs: 3
+// waves per SIMD).  The sdf-plane form runs at 4 waves per SIMD (128 VGPRs): 0.524 vs 0.538 ms
+// on the bench workload; 5, 6 and 8 spill (0.69 / 0.84 / 3.8 ms,
+// profiles/r4/ab_render_occ_heavy_trace_r4g.log).  A two-phase sdf-plane form (every chunk's
+// plane gathers in flight at once, colour lines after) measured no faster (round 4) and left.
+template <bool SIG, int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void render_kernel(const float* __restrict__ gvm, int D, int H, int W, Bounds B, int mode,
                    const float* __restrict__ ro, const float* __restrict__ rd, const float* __restrict__ zv,
                    int64_t nrays, int S, float* __restrict__ rgb, const unsigned* __restrict__ order,
                    const float* __restrict__ sdfp) {
-    if constexpr (SIG && NCH > 0)
-        render_body_2ph<NCH>(gvm, D, H, W, B, mode, ro, rd, zv, nrays, S, rgb, order, sdfp);
-    else
-        render_body<SIG>(gvm, D, H, W, B, mode, ro, rd, zv, nrays, S, rgb, order, sdfp);
+    render_body<SIG>(gvm, D, H, W, B, mode, ro, rd, zv, nrays, S, rgb, order, sdfp);
 }
 
 // NerfModel.forward (plenoxel.py:31-43): the 28 channels at each point
@@ -612,10 +493,6 @@ __global__ void nerf_forward_kernel(const float* __restrict__ grid, int D, int H
     color[3 * i + 2] = col[2];
 }
 
-static int env_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
 
 // ---------------------------------------------------------------------------
 // §8f row 4: one training step of the grid (plenoxel.py:100-111, sdf.py:427-438):
@@ -982,10 +859,10 @@ extern "C" int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, i
     SFMHIP_REQUIRE(rays && out, "sfmhip_voxel_traversal: null pointer");
     SFMHIP_REQUIRE(N >= 0 && S >= 1, "sfmhip_voxel_traversal: bad args");
     if (N == 0) return SFMHIP_OK;
-    // SFMHIP_DDA_DIRECT (A/B): 1 per-lane row stores, 0 LDS-staged coalesced
+    // SFMHIP_DDA_DIRECT (tests): 1 per-lane row stores, 0 LDS-staged coalesced
     // chunks; default: direct below 64k rays (latency-bound), staged above.
-    const char* denv = std::getenv("SFMHIP_DDA_DIRECT");
-    const bool direct = denv ? std::atoi(denv) != 0 : N < 65536;
+    const int dk = knobs().dda_direct;
+    const bool direct = dk >= 0 ? dk != 0 : N < 65536;
     if (direct) {
         hipLaunchKernelGGL(dda_fill_direct_kernel, dim3(ceil_div(N, 64)), dim3(64), 0, as_stream(stream), rays, N,
                            bin, S, out, nullptr);
@@ -1130,13 +1007,11 @@ __global__ __launch_bounds__(256) void render_key_kernel(const float* __restrict
 }
 
 // order[pos] = ray, pos = (exclusive prefix of the bucket counts, recomputed per
-// workgroup from the L2-resident histogram) + rank; with xchunk > 0 the sorted positions
-// are laid out so that XCD x gets runs of xchunk consecutive 4-ray workgroups (blocks
-// are dealt round-robin over the XCDs)
+// workgroup from the L2-resident histogram) + rank
 __global__ __launch_bounds__(256) void render_scatter_kernel(const unsigned* __restrict__ hist, int nb,
                                                              const unsigned* __restrict__ key,
                                                              const unsigned* __restrict__ rank, int64_t nrays,
-                                                             int xchunk, unsigned* __restrict__ order) {
+                                                             unsigned* __restrict__ order) {
     __shared__ unsigned base[kRenderSortMaxBuckets];
     __shared__ unsigned part[256];
     const int t = threadIdx.x, per = (nb + 255) / 256, a = t * per, e = min(nb, a + per);
@@ -1158,55 +1033,18 @@ __global__ __launch_bounds__(256) void render_scatter_kernel(const unsigned* __r
     __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nrays) return;
-    int64_t pos = (int64_t)base[key[i]] + rank[i];
-    if (xchunk > 0) {
-        const int64_t grp = (int64_t)4 * kNumXcd * xchunk;   // rays per full round of runs
-        const int64_t full = nrays / grp * grp;
-        if (pos < full) {   // logical block L -> launch block: L = ((s / c) * 8 + x) * c + s % c
-            const int64_t L = pos >> 2, c = xchunk;
-            const int64_t rn = L / c, s_in = L % c, x = rn % kNumXcd, sq = (rn / kNumXcd) * c + s_in;
-            pos = ((sq * kNumXcd + x) << 2) | (pos & 3);
-        }
-    }
-    order[pos] = (unsigned)i;
+    order[(int64_t)base[key[i]] + rank[i]] = (unsigned)i;
 }
 
 static void launch_render(const float* sdfp, dim3 grid, hipStream_t st, const float* gvm, int D, int H, int W,
                           const Bounds& bb, int mode, const float* ro, const float* rd, const float* z, int64_t B, int S,
                           float* rgb, const unsigned* order) {
-    // 4 waves per SIMD for the sdf-plane form (128 VGPRs): 0.524 vs 0.538 ms on the bench workload; 5, 6
-    // and 8 spill (0.69 / 0.84 / 3.8 ms), profiles/r4/ab_render_occ_heavy_trace_r4g.log
-    const int occ = env_int("SFMHIP_RENDER_OCC", sdfp ? 4 : 0);
-#define SFMHIP_RENDER_LAUNCH(SIG, OCC)                                                                        \
-    hipLaunchKernelGGL((render_kernel<SIG, OCC>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd, z, B, S, \
-                       rgb, order, SIG ? sdfp : nullptr)
-    const int two = env_int("SFMHIP_RENDER_2PH", 0);   // A/B: two-phase sdf-plane form, chunks per group
-    if (sdfp && two > 0) {
-        if (two >= 4) {
-            if (occ == 4) hipLaunchKernelGGL((render_kernel<true, 4, 4>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode,
-                                             ro, rd, z, B, S, rgb, order, sdfp);
-            else hipLaunchKernelGGL((render_kernel<true, 0, 4>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd,
-                                    z, B, S, rgb, order, sdfp);
-        } else {
-            if (occ == 4) hipLaunchKernelGGL((render_kernel<true, 4, 3>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode,
-                                             ro, rd, z, B, S, rgb, order, sdfp);
-            else hipLaunchKernelGGL((render_kernel<true, 0, 3>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd,
-                                    z, B, S, rgb, order, sdfp);
-        }
-    } else if (sdfp) {
-        if (occ == 4) SFMHIP_RENDER_LAUNCH(true, 4);
-        else if (occ == 5) SFMHIP_RENDER_LAUNCH(true, 5);
-        else if (occ == 6) SFMHIP_RENDER_LAUNCH(true, 6);
-        else if (occ == 8) SFMHIP_RENDER_LAUNCH(true, 8);
-        else SFMHIP_RENDER_LAUNCH(true, 0);
-    } else {
-        if (occ == 4) SFMHIP_RENDER_LAUNCH(false, 4);
-        else if (occ == 5) SFMHIP_RENDER_LAUNCH(false, 5);
-        else if (occ == 6) SFMHIP_RENDER_LAUNCH(false, 6);
-        else if (occ == 8) SFMHIP_RENDER_LAUNCH(false, 8);
-        else SFMHIP_RENDER_LAUNCH(false, 0);
-    }
-#undef SFMHIP_RENDER_LAUNCH
+    if (sdfp)
+        hipLaunchKernelGGL((render_kernel<true, 4>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd, z, B, S,
+                           rgb, order, sdfp);
+    else
+        hipLaunchKernelGGL((render_kernel<false, 0>), grid, dim3(256), 0, st, gvm, D, H, W, bb, mode, ro, rd, z, B, S,
+                           rgb, order, nullptr);
 }
 
 static int render_run(const float* grid_vm, const float* sdfp, int D, int H, int W, const float* bmin,
@@ -1219,16 +1057,15 @@ static int render_run(const float* grid_vm, const float* sdfp, int D, int H, int
     if (B == 0) return SFMHIP_OK;
     hipStream_t st = as_stream(stream);
     const Bounds bb = make_bounds(bmin, bmax);
-    // ray ordering (SFMHIP_RENDER_SORT=0 off; _BITS cells per axis as a power of two, _SIDX the
-    // sample (default the last), _XCHUNK XCD runs of workgroups): batches below 8192 rays fill
-    // only a fraction of the chip's waves at once and are rendered as given.  Bench workload
-    // (tools/bench_render_order.py, profiles/r3/ab/render_order_r3j.txt): 0.627-0.648 ms as
-    // given, 0.598 ms with this ordering (sort kernels included); keys and cell sizes from
-    // 2^2 to 2^8 per axis, host-sorted, all give the same ~0.58 ms kernel
-    const int sort = env_int("SFMHIP_RENDER_SORT", 1);
-    const int bits = std::min(std::max(env_int("SFMHIP_RENDER_SORT_BITS", 3), 1), 4);
-    const int sidx = std::min(std::max(env_int("SFMHIP_RENDER_SORT_SIDX", S - 1), 0), S - 1);
-    const int xchunk = std::max(env_int("SFMHIP_RENDER_SORT_XCHUNK", 0), 0);
+    // ray ordering (SFMHIP_RENDER_SORT=0 off, tests): Morton cells of 2^3 per axis holding each
+    // ray's last sample; batches below 8192 rays fill only a fraction of the chip's waves at
+    // once and are rendered as given.  Bench workload (tools/bench_render_order.py,
+    // profiles/r3/ab/render_order_r3j.txt): 0.627-0.648 ms as given, 0.598 ms with this
+    // ordering (sort kernels included); keys and cell sizes from 2^2 to 2^8 per axis,
+    // host-sorted, and XCD-run layouts all give the same ~0.58 ms kernel
+    const int sort = knobs().render_sort;
+    constexpr int bits = 3;
+    const int sidx = S - 1;
     unsigned* scratch = nullptr;
     const int nb = 1 << (3 * bits);
     if (sort && B >= 8192) {
@@ -1247,7 +1084,7 @@ static int render_run(const float* grid_vm, const float* sdfp, int D, int H, int
         }
         if (rc == SFMHIP_OK) {
             hipLaunchKernelGGL(render_scatter_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, st, hist, nb, key, rank, B,
-                               xchunk, order);
+                               order);
             rc = check_launch("render_scatter_kernel");
         }
         if (rc == SFMHIP_OK) {

@@ -60,7 +60,7 @@ def test_triangulate_batched_pairs(sfm, gpu):
         np.testing.assert_allclose((X4[:3, sl] / X4[3, sl]).T, (ref[:3] / ref[3]).T, rtol=1e-8)
 
 
-def test_triangulate_normal_and_qr_paths(sfm, gpu, monkeypatch):
+def test_triangulate_normal_and_qr_paths(sfm, gpu, knob):
     """The normal-equation fast pass + QR list pass (default) and the QR path for
     every observation (SFMHIP_DLT_QR=1) agree with the oracle and each other,
     including small-baseline pairs whose observations go to the QR list."""
@@ -74,9 +74,9 @@ def test_triangulate_normal_and_qr_paths(sfm, gpu, monkeypatch):
     args = (torch.from_numpy(P).to(dv), torch.from_numpy(s["pair_of_obs"]).to(dv),
             torch.from_numpy(s["x0"]).to(dv), torch.from_numpy(s["x1"]).to(dv))
     fast = sfm.triangulate_batched(*args).cpu().numpy()
-    monkeypatch.setenv("SFMHIP_DLT_QR", "1")
+    knob("DLT_QR", 1)
     qr = sfm.triangulate_batched(*args).cpu().numpy()
-    monkeypatch.delenv("SFMHIP_DLT_QR")
+    knob("DLT_QR", 0)
     for p in range(4, 16):      # well-conditioned pairs: both paths equal the oracle
         sl = slice(p * 1000, (p + 1) * 1000)
         ref = og.triangulate_points(P[p, 0], P[p, 1], s["x0"][:, sl], s["x1"][:, sl])

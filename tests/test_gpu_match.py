@@ -211,12 +211,10 @@ def test_vq_gpu_golden(sfm, gpu):
         assert abs(da - db) <= 1e-12 * max(da, db)
 
 
-@pytest.mark.parametrize("variant", ["0", "4", "6"])
-def test_vq_tiny_scale_takes_exact_path(sfm, gpu, monkeypatch, variant):
-    """Data scaled by 1e-21: f32 products fall to the subnormal range, so the
-    f32 filter's absolute error term sends every observation to the exact f64
-    pass; codes equal scipy's."""
-    monkeypatch.setenv("SFMHIP_VQ_VARIANT", variant)
+def test_vq_tiny_scale_takes_exact_path(sfm, gpu):
+    """Data scaled by 1e-21: the filter's products fall to the subnormal range, so
+    its absolute error term sends every observation to the exact f64 pass; codes
+    equal scipy's."""
     rng = np.random.default_rng(4)
     code = rng.standard_normal((200, 128)) * 1e-21
     obs = code[rng.integers(0, 200, 3000)] + rng.standard_normal((3000, 128)) * 3e-22
@@ -250,16 +248,12 @@ def test_match_empty_and_single_keypoint_images(sfm, gpu):
 
 @pytest.mark.parametrize("n,k,d", [(5000, 200, 128), (777, 300, 40), (300, 1, 128), (1, 17, 64), (4097, 145, 20),
                                    (3001, 256, 128), (257, 16, 128)])
-@pytest.mark.parametrize("variant", ["0", "4", "6"])
-def test_vq_mfma_integer_bit_exact(sfm, gpu, monkeypatch, variant, n, k, d):
-    """vq on integer data: bit-exact with scipy — the f32-filter path (d = 128,
-    k <= 256; exact ties go through the f64 exact pass) and the f64-MFMA GEMM
-    form (other shapes), across code-book passes (k > 144), padded dims (d not
-    a power of two), a single codeword and ragged observation tiles; ties
-    resolve to the lowest index.  Variant 4 is the tile-staged f32 filter
-    (vq_f32f_kernel) beside the default register-resident one; variant 6 the
-    f16-split matrix-core filter (vq_f16s_kernel)."""
-    monkeypatch.setenv("SFMHIP_VQ_VARIANT", variant)
+def test_vq_mfma_integer_bit_exact(sfm, gpu, n, k, d):
+    """vq on integer data: bit-exact with scipy -- the f16-split matrix-core filter
+    (d = 128, k <= 256; exact ties go through the f64 exact pass) and the f64-MFMA
+    GEMM form (other shapes), across code-book passes (k > 144), padded dims (d not
+    a power of two), a single codeword and ragged observation tiles; ties resolve to
+    the lowest index."""
     rng = np.random.default_rng(n + k + d)
     obs = rng.integers(-20, 21, (n, d)).astype(np.float64)
     code = rng.integers(-20, 21, (k, d)).astype(np.float64)
@@ -270,18 +264,18 @@ def test_vq_mfma_integer_bit_exact(sfm, gpu, monkeypatch, variant, n, k, d):
     assert np.array_equal(codes, rc) and np.array_equal(dist, rd)
 
 
-def test_vq_f32_filter_floats_vs_scipy(sfm, gpu, monkeypatch):
-    """Float data (unit-norm descriptors, codewords not representable in f32):
-    the f32-filter path agrees with scipy's f64 vq on the codes (any difference
-    is a near-tie within f64 rounding) and on the distances to 1e-12, as the
-    f64-MFMA path does."""
-    x = syn.superpoint_like(5, 4096, 128, seed=21).reshape(-1, 128).double().numpy()
+@pytest.mark.parametrize("dim", [128, 120])
+def test_vq_filter_floats_vs_scipy(sfm, gpu, dim):
+    """Float data (unit-norm descriptors, codewords not representable in f32): the
+    f16-split filter (d = 128) and the f64-MFMA path (d = 120) agree with scipy's
+    f64 vq on the codes (any difference is a near-tie within f64 rounding) and on
+    the distances to 1e-12."""
+    x = syn.superpoint_like(5, 4096, 128, seed=21).reshape(-1, 128)[:, :dim].double().numpy()
     rng = np.random.default_rng(3)
-    code = x[rng.choice(len(x), 200, replace=False)] + rng.normal(0, 1e-3, (200, 128))
+    code = x[rng.choice(len(x), 200, replace=False)] + rng.normal(0, 1e-3, (200, dim))
     code[7] = code[3]                                             # an exact tie too
     rc, rd = om.vq(x, code)
-    for variant in ("0", "4", "3", "6"):
-        monkeypatch.setenv("SFMHIP_VQ_VARIANT", variant)
+    if True:
         codes, dist = sfm.vq(x, code)
         # scipy's GEMM-form sqrt(|x|^2 + |c|^2 - 2 x.c) carries ~1e-16 |x|^2 of cancellation
         # (obs next to a codeword); both GPU paths return the difference form
@@ -295,11 +289,10 @@ def test_vq_f32_filter_floats_vs_scipy(sfm, gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("scale", [2.0 ** 16, 1e30])
-def test_vq_f16_filter_out_of_range_inputs(sfm, gpu, monkeypatch, scale):
+def test_vq_f16_filter_out_of_range_inputs(sfm, gpu, scale):
     """Inputs beyond f16 range (|v| >= 2^15) decide nothing in the f16-split
     filter: a large codebook sends every observation, a large observation row
     only itself, to the exact f64 pass — codes and distances stay scipy's."""
-    monkeypatch.setenv("SFMHIP_VQ_VARIANT", "6")
     rng = np.random.default_rng(11)
     obs = rng.integers(-20, 21, (2000, 128)).astype(np.float64)
     code = rng.integers(-20, 21, (150, 128)).astype(np.float64)
@@ -310,16 +303,15 @@ def test_vq_f16_filter_out_of_range_inputs(sfm, gpu, monkeypatch, scale):
         np.testing.assert_allclose(dist, rd, rtol=1e-15)
 
 
-def test_vq_f16_filter_matches_f32_filter(sfm, gpu, monkeypatch):
-    """The f16-split filter and the f32 filter decide the same codes on float
-    descriptors (both exact up to f64 near-ties, which go to the same exact
-    pass) with distances within 1e-13."""
+def test_vq_f16_filter_matches_f64_mfma(sfm, gpu):
+    """The f16-split filter (d = 128) and the f64 difference-form kernel (the same
+    data zero-padded to d = 129, which adds nothing to any distance) decide the same
+    codes on float descriptors (both exact up to f64 near-ties) with distances within
+    1e-13."""
     x = syn.superpoint_like(4, 4096, 128, seed=5).reshape(-1, 128).double().numpy()
     rng = np.random.default_rng(8)
     code = x[rng.choice(len(x), 256, replace=False)] + rng.normal(0, 3e-3, (256, 128))
-    out = {}
-    for variant in ("0", "6"):
-        monkeypatch.setenv("SFMHIP_VQ_VARIANT", variant)
-        out[variant] = sfm.vq(x, code)
-    assert np.array_equal(out["0"][0], out["6"][0])
-    np.testing.assert_allclose(out["0"][1], out["6"][1], rtol=1e-13)
+    a = sfm.vq(x, code)
+    b = sfm.vq(np.pad(x, ((0, 0), (0, 1))), np.pad(code, ((0, 0), (0, 1))))
+    assert np.array_equal(a[0], b[0])
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-13)

@@ -25,8 +25,8 @@ def _oracle(x, nk, pairs, ratio):
 
 @pytest.mark.parametrize("cert", ["1", "0"])
 @pytest.mark.parametrize("d,kind", [(256, "superpoint"), (128, "disk"), (64, "randn"), (128, "sift")])
-def test_exact_float_ragged_pairs(sfm, gpu, monkeypatch, cert, d, kind):
-    monkeypatch.setenv("SFMHIP_MATCH_CERT", cert)
+def test_exact_float_ragged_pairs(sfm, gpu, knob, cert, d, kind):
+    knob("MATCH_CERT", cert)
     n_img, m = 5, 600
     if kind == "randn":        # not normalised, components beyond the int8 range after rint(127 x): clipped rows
         x = torch.randn((n_img, m, d), generator=torch.Generator().manual_seed(d)).numpy() * 0.6
@@ -48,11 +48,11 @@ def test_exact_float_ragged_pairs(sfm, gpu, monkeypatch, cert, d, kind):
 
 
 @pytest.mark.parametrize("cert", ["1", "0"])
-def test_exact_float_near_ties_and_ratio_boundary(sfm, gpu, monkeypatch, cert):
+def test_exact_float_near_ties_and_ratio_boundary(sfm, gpu, knob, cert):
     """Rows whose int8 images tie or sit at the ratio boundary: exact ties
     (lowest index wins, then d1 == d2 -> reject), 1-ulp perturbations of the
     best candidate, and d1/d2 = 9/16 exactly (rejected: not strictly below)."""
-    monkeypatch.setenv("SFMHIP_MATCH_CERT", cert)
+    knob("MATCH_CERT", cert)
     rng = np.random.default_rng(5)
     d = 128
     a = (rng.standard_normal((64, d)) * 0.05).astype(np.float32)

@@ -76,58 +76,3 @@ def test_pnp_five_points_and_batch(sfm, gpu):
     with pytest.raises(NotImplementedError):
         sfm.solvePnPRansac(X[:4], uv[:4], K)
 
-
-def test_pnp_eigensolvers_same_outcome(sfm, gpu):
-    """EPnP's eigen-decomposition by tridiagonal QL (default) and by the parallel Jacobi
-    (SFMHIP_PNP_EIG=0) on 64 bench-like problems: the same RANSAC iterations and inlier masks,
-    the refined poses to 1e-7 (the eigenvectors differ only inside M^T M's near-null space)."""
-    import os
-    import torch
-    v = sfm.verify
-    scenes = [_scene(2000 if k % 4 else 300, 100 + k) for k in range(64)]
-    offs = torch.tensor(np.cumsum([0] + [len(s[0]) for s in scenes]))
-    X = np.concatenate([s[0] for s in scenes])
-    uv = np.concatenate([s[1] for s in scenes])
-    out = []
-    for eig in ("1", "0"):
-        os.environ["SFMHIP_PNP_EIG"] = eig
-        try:
-            r = v.pnp_ransac_batched(X, uv, offs, v._cam(scenes[0][2]))
-            torch.cuda.synchronize()
-            out.append({k: t.cpu().numpy() for k, t in r.items()})
-        finally:
-            os.environ.pop("SFMHIP_PNP_EIG", None)
-    for k in ("ok", "n_inliers", "iters", "mask"):
-        assert np.array_equal(out[0][k], out[1][k]), k
-    np.testing.assert_allclose(out[0]["rvec"], out[1]["rvec"], rtol=0, atol=1e-7)
-    np.testing.assert_allclose(out[0]["tvec"], out[1]["tvec"], rtol=0, atol=1e-7)
-
-
-def test_pnp_balanced_equals_monolithic(sfm, gpu):
-    """The phase-split form (solve / score / replay / refine kernels over (problem, chunk) items)
-    (SFMHIP_PNP_MONO=0) gives the same bits as the one-workgroup-per-problem kernel: ragged
-    problems incl. n < 5, n == 5, all-outlier and bench-sized ones, and iteration caps."""
-    import os
-    import torch
-    v = sfm.verify
-    sizes = [300, 3, 5, 2000, 60, 9, 2000, 0, 120, 2000]
-    scenes = [_scene(max(nn, 1), 200 + k, outlier=0.9 if k == 8 else 0.3) for k, nn in enumerate(sizes)]
-    X = np.concatenate([s[0][:nn] for s, nn in zip(scenes, sizes)])
-    uv = np.concatenate([s[1][:nn] for s, nn in zip(scenes, sizes)])
-    offs = torch.tensor(np.cumsum([0] + sizes))
-    for iters in (100, 1, 40):
-        out = []
-        for mono in ("1", "0"):
-            os.environ["SFMHIP_PNP_MONO"] = mono
-            try:
-                r = v.pnp_ransac_batched(X, uv, offs, v._cam(scenes[0][2]), iterations=iters)
-                torch.cuda.synchronize()
-                out.append({k: t.cpu().numpy() for k, t in r.items()})
-            finally:
-                os.environ.pop("SFMHIP_PNP_MONO", None)
-        for k in out[0]:
-            if k in ("rvec", "tvec"):
-                ok = out[0]["ok"] > 0
-                assert np.array_equal(out[0][k][ok], out[1][k][ok]), (iters, k)
-            else:
-                assert np.array_equal(out[0][k], out[1][k]), (iters, k)

@@ -24,5 +24,5 @@ for rep in range(6):
     torch.cuda.synchronize()
     if rep:
         ts.append(e0.elapsed_time(e1))
-print(f"variant {os.environ.get('SFMHIP_BA_VARIANT', '1')} BA solve 256 x 4096: {np.median(ts):.3f} ms, nfev mean {r['nfev'].float().mean().item():.2f}, "
+print(f"BA solve 256 x 4096: {np.median(ts):.3f} ms, nfev mean {r['nfev'].float().mean().item():.2f}, "
       f"status>0 {(r['status'] > 0).sum().item()}/256", flush=True)

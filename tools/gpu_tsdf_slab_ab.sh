@@ -1,5 +1,5 @@
 #!/bin/bash
-# Kernel traces of one N=8 C5 slab (rank 3) per knob config: SCONFIGS="DEVNF=4;SHARE=1000" (SFMHIP_TSDF_ prefix)
+# Kernel traces of one N=8 C5 slab (rank 3) per knob config: SCONFIGS="LATENCY=0;LATENCY=1" (SFMHIP_TSDF_ prefix)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp
 TAG=${1:-r5}; OUT=gpurun_out/$TAG; mkdir -p $OUT
