@@ -64,6 +64,7 @@ struct Knobs {
     int dlt_qr;         // SFMHIP_DLT_QR: 1 runs the QR DLT for every observation (no normal-equation pass)
     int render_sort;    // SFMHIP_RENDER_SORT: 0 renders rays in input order (no spatial sort)
     int dda_direct;     // SFMHIP_DDA_DIRECT: fill kernel of the two-pass DDA (-1 auto, 0 staged, 1 direct)
+    int ab;             // SFMHIP_AB: A/B selector for a form under measurement (0 = the default form)
 };
 const Knobs& knobs();
 

@@ -163,6 +163,7 @@ static Knobs read_knobs() {
     k.dlt_qr = env_knob("SFMHIP_DLT_QR", 0);
     k.render_sort = env_knob("SFMHIP_RENDER_SORT", 1);
     k.dda_direct = env_knob("SFMHIP_DDA_DIRECT", -1);
+    k.ab = env_knob("SFMHIP_AB", 0);
     return k;
 }
 static Knobs g_knobs;

@@ -24,7 +24,7 @@ IFS=';' read -ra CF <<< "${CONFIGS:--}"
 for c in "${CF[@]}"; do
   i=$((i+1))
   ENVS="REPS=4"
-  if [ "$c" != "-" ]; then IFS=',' read -ra KV <<< "$c"; for kv in "${KV[@]}"; do ENVS="$ENVS SFMHIP_TSDF_$kv"; done; fi
+  if [ "$c" != "-" ]; then IFS=',' read -ra KV <<< "$c"; for kv in "${KV[@]}"; do case $kv in SFMHIP_*) ENVS="$ENVS $kv";; *) ENVS="$ENVS SFMHIP_TSDF_$kv";; esac; done; fi
   env $ENVS timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt$i -o run -- \
       python tools/run_tsdf_once.py > $OUT/kt$i.log 2>&1 || { echo "prof $c failed"; tail -5 $OUT/kt$i.log; exit 1; }
   find $OUT/kt$i -type f ! -name "*stats*" -delete
