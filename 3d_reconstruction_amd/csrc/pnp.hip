@@ -6,13 +6,16 @@
 // cvFindExtrinsicCameraParams2 + CvLevMarq); CPU restatement oracle/pnp.py.
 // Parity with OpenCV is unpinned (cv2 absent).
 //
-// One workgroup (4 waves) per registration problem:
+// One workgroup (8 waves, two per SIMD) per registration problem:
 //   * points are converted to float (solvePnPRansac's CV_32F conversion);
-//   * RANSAC: lane 0 draws 32 five-point samples per chunk from cv::RNG(-1)
-//     (OpenCV's ~25 iterations at 30 % outliers fit one chunk);
-//     each sample is solved by EPnP in an 8-lane group (M^T M eigenvectors by
-//     a parallel-ordered two-sided Jacobi in LDS, the three beta
-//     approximations + Gauss-Newton in lanes 0..2, Procrustes), scored by all
+//   * RANSAC: lane 0 draws 64 five-point samples per chunk from cv::RNG(-1)
+//     (OpenCV's ~25-40 iterations at 30 % outliers fit one chunk: round 4's
+//     32-hypothesis chunks sent the 33-37-iteration problems through a second
+//     chunk, which bounded the call); each sample is solved by EPnP in an
+//     8-lane group (M^T M reduced to tridiagonal form and its eigenvectors by
+//     the implicit QL iteration, the three beta approximations + Gauss-Newton
+//     in lanes 0..2, Procrustes; the sample, alphas, L and V live in the
+//     group's LDS scratch so that the kernel fits 256 VGPRs), scored by all
 //     lanes (float squared reprojection error <= 64, wave ballots) and
 //     replayed in OpenCV's sequential order;
 //   * the RANSAC pose is refined on the inliers by Levenberg-Marquardt with
@@ -27,19 +30,22 @@
 namespace sfmhip {
 namespace {
 
-constexpr int kPnThreads = 256;
+constexpr int kPnThreads = 512;           // 8 waves: two per SIMD (<= 256 VGPRs)
+constexpr int kPnNW = kPnThreads / 64;
 constexpr int kPnGL = 8;                   // lanes per EPnP group
-constexpr int kPnH = kPnThreads / kPnGL;  // hypotheses per chunk
+constexpr int kPnH = kPnThreads / kPnGL;  // hypotheses per chunk: 64 (OpenCV's ~25-40 iterations at 30 % outliers)
 static_assert(144 % kPnGL == 0 && kPnGL >= 6, "EPnP group width");
-constexpr int kPnGS = 448;                // LDS doubles per group
+constexpr int kPnGS = 280;                // LDS doubles per group
 constexpr int kPnStageCap = kPnH * kPnGS * 8 / 21;   // LM points staged in the group scratch (5 floats + a flag)
 constexpr double kEps64 = 2.220446049250313e-16;
 constexpr double kDblMin64 = 2.2250738585072014e-308;
 
-// group scratch map (doubles)
-constexpr int gA = 0, gV = 144, gRot = 288 /* 6 x (c, s) */, gL = 300, gRho = 360, gSol = 366 /* 3 x 13 */,
-              gCws = 405 /* 12 */, gAl = 417 /* 5 x 4 alphas */, gUd = 437 /* 5 x (uc - u, vc - v) */;
-static_assert(gUd + 10 <= kPnGS, "group scratch map");
+// group scratch map (doubles): M^T M, reduced in place, then the eigenvectors (columns of V) over it;
+// the eigenvalues; L_6x10 (the tridiagonalisation's reflector and update vectors before it); rho; the
+// control points; the alphas; the sample's object points and image points
+constexpr int gA = 0, gV = 0, gEv = 144, gL = 156, gRho = 216, gCws = 222 /* 12 */, gAl = 234 /* 5 x 4 */,
+              gPw = 254 /* 5 x 3 */, gUs = 269 /* 5 x 2 */;
+static_assert(gUs + 10 <= kPnGS, "group scratch map");
 
 struct CvRng {
     uint64_t s;
@@ -272,8 +278,7 @@ __device__ void lsq6(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
     }
 }
 
-struct EpnpData {
-    double pw[5][3], us[5][2], al[5][4];
+struct EpnpData {   // the sample's points and alphas live in the group scratch (gPw, gUs, gAl)
     double fu, fv, uc, vc;
 };
 
@@ -289,18 +294,19 @@ __device__ __forceinline__ double epnp_R_t(const EpnpData& D, const double* G, c
     double pcs[5][3];
     for (int p = 0; p < 5; ++p)
         for (int j = 0; j < 3; ++j)
-            pcs[p][j] = D.al[p][0] * ccs[0][j] + D.al[p][1] * ccs[1][j] + D.al[p][2] * ccs[2][j] + D.al[p][3] * ccs[3][j];
+            pcs[p][j] = G[gAl + 4 * p] * ccs[0][j] + G[gAl + 4 * p + 1] * ccs[1][j] + G[gAl + 4 * p + 2] * ccs[2][j] +
+                        G[gAl + 4 * p + 3] * ccs[3][j];
     if (pcs[0][2] < 0)
         for (int p = 0; p < 5; ++p)
             for (int j = 0; j < 3; ++j) pcs[p][j] = -pcs[p][j];
     double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
     for (int p = 0; p < 5; ++p)
-        for (int j = 0; j < 3; ++j) { pc0[j] += pcs[p][j]; pw0[j] += D.pw[p][j]; }
+        for (int j = 0; j < 3; ++j) { pc0[j] += pcs[p][j]; pw0[j] += G[gPw + 3 * p + j]; }
     for (int j = 0; j < 3; ++j) { pc0[j] /= 5; pw0[j] /= 5; }
     double abt[9] = {};
     for (int p = 0; p < 5; ++p)
         for (int j = 0; j < 3; ++j)
-            for (int k = 0; k < 3; ++k) abt[3 * j + k] += (pcs[p][j] - pc0[j]) * (D.pw[p][k] - pw0[k]);
+            for (int k = 0; k < 3; ++k) abt[3 * j + k] += (pcs[p][j] - pc0[j]) * (G[gPw + 3 * p + k] - pw0[k]);
     double U[3][3], s[3], V[3][3];
     svd3(abt, U, s, V);
     for (int i = 0; i < 3; ++i)
@@ -311,12 +317,13 @@ __device__ __forceinline__ double epnp_R_t(const EpnpData& D, const double* G, c
     for (int i = 0; i < 3; ++i) t[i] = pc0[i] - (R[3 * i] * pw0[0] + R[3 * i + 1] * pw0[1] + R[3 * i + 2] * pw0[2]);
     double sum = 0;
     for (int p = 0; p < 5; ++p) {
-        const double* pw = D.pw[p];
+        const double* pw = G + gPw + 3 * p;
         const double Xc = R[0] * pw[0] + R[1] * pw[1] + R[2] * pw[2] + t[0];
         const double Yc = R[3] * pw[0] + R[4] * pw[1] + R[5] * pw[2] + t[1];
         const double iz = 1.0 / (R[6] * pw[0] + R[7] * pw[1] + R[8] * pw[2] + t[2]);
         const double ue = D.uc + D.fu * Xc * iz, ve = D.vc + D.fv * Yc * iz;
-        sum += sqrt((D.us[p][0] - ue) * (D.us[p][0] - ue) + (D.us[p][1] - ve) * (D.us[p][1] - ve));
+        const double u0 = G[gUs + 2 * p], u1 = G[gUs + 2 * p + 1];
+        sum += sqrt((u0 - ue) * (u0 - ue) + (u1 - ve) * (u1 - ve));
     }
     return sum / 5;
 }
@@ -340,14 +347,14 @@ __device__ unsigned long long g_wgt[2 * 1024];  // per-workgroup start / end
 // EPnP eigen-decomposition of M^T M (12x12, symmetric) by Householder tridiagonalisation and
 // the implicit QL iteration (EISPACK tred2 / tql2 form), on a kPnGL-lane group.  A (G[gA]) is
 // reduced in LDS, each lane owning rows gl and gl + 8; the reflector v and the update vector q
-// go through LDS (G[gRot], G[gL]); Q = H_0 ... H_9 is kept in registers (the lane's two rows).
+// go through LDS (G[gL], before L is built); Q = H_0 ... H_9 is kept in registers (the lane's two rows).
 // The QL iteration runs on every lane of the group (d, e in registers, the same operations on
 // the same values) and each lane rotates its own rows of Q, so no rotation is broadcast.
-// Result as the Jacobi's: eigenvalues on A's diagonal, eigenvectors as the columns of V (G[gV]).
+// Result: the eigenvalues in G[gEv], the eigenvectors as the columns of V (G[gV], over A).
 __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
     double* A = G + gA;
-    double* vv = G + gRot;   // 12 doubles
-    double* qv = G + gL;     // 12 doubles
+    double* vv = G + gL;        // 12 doubles (L is built later)
+    double* qv = G + gL + 12;   // 12 doubles
     const int r0 = gl, r1 = gl + kPnGL;
     const bool h1 = r1 < 12;
     double z0[12], z1[12];   // rows r0 and r1 of Q
@@ -448,7 +455,9 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
             for (int i = 10; i >= 0; --i) {
                 if (!(live && i >= l && i < m)) continue;
                 const double f = s * e[i], b = c * e[i];
-                r = sqrt_nr(fma(f, f, g * g));
+                const double x2 = fma(f, f, g * g);
+                const double ir = x2 > 0.0 ? rsq_nr(x2) : 0.0;   // r and 1/r from one reciprocal square root
+                r = x2 * ir;
                 e[i + 1] = r;
                 if (r == 0.0) {   // underflow: deflate and restart this l
                     d[i + 1] -= p;
@@ -458,7 +467,6 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
                     live = false;
                     continue;
                 }
-                const double ir = rcp_nr(r);
                 s = f * ir;
                 c = g * ir;
                 g = d[i + 1] - p;
@@ -481,10 +489,10 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
             }
         }
     }
-    lds_fence();
+    lds_fence();   // (the group is 8 lanes of one wave: every read of A above precedes these writes)
     if (gl == 0) {
 #pragma unroll
-        for (int i = 0; i < 12; ++i) A[i * 13] = d[i];
+        for (int i = 0; i < 12; ++i) G[gEv + i] = d[i];
     }
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
@@ -497,7 +505,7 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
 // EPnP on 5 correspondences by a kPnGL-lane group; writes (rvec, tvec) to out[6].
 __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
     PPROF_INIT;
-    // M^T M (12x12) into A, V = I
+    // M^T M (12x12) into A
     // (alphas and uc - u, vc - v were staged in G by prepare: a dynamic index into D would put
     // it in scratch memory)
     for (int e = gl; e < 144; e += kPnGL) {
@@ -508,7 +516,7 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
             // M rows 2p (u) and 2p+1 (v): col 3c -> a*fu / 0, col 3c+1 -> 0 / a*fv, col 3c+2 -> a*(uc-u) / a*(vc-v)
             const int ci = i / 3, ki = i % 3, cj = j / 3, kj = j % 3;
             const double ai = G[gAl + 4 * p + ci], aj = G[gAl + 4 * p + cj];
-            const double du = G[gUd + 2 * p], dv = G[gUd + 2 * p + 1];
+            const double du = D.uc - G[gUs + 2 * p], dv = D.vc - G[gUs + 2 * p + 1];
             const double mu_i = ki == 0 ? ai * D.fu : ki == 1 ? 0.0 : ai * du;
             const double mu_j = kj == 0 ? aj * D.fu : kj == 1 ? 0.0 : aj * du;
             const double mv_i = ki == 0 ? 0.0 : ki == 1 ? ai * D.fv : ai * dv;
@@ -516,7 +524,6 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
             acc += mu_i * mu_j + mv_i * mv_j;
         }
         G[gA + e] = acc;
-        G[gV + e] = (i == j) ? 1.0 : 0.0;
     }
     lds_fence();
     PPROF(7);
@@ -529,7 +536,7 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
     {
         double ev[12];
 #pragma unroll
-        for (int i = 0; i < 12; ++i) ev[i] = G[gA + i * 13];
+        for (int i = 0; i < 12; ++i) ev[i] = G[gEv + i];
         unsigned used = 0;  // bit mask: no dynamically indexed arrays
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -572,31 +579,30 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
     }
     lds_fence();
     PPROF(9);
-    // three beta approximations (lane 0: B11 B12 B13 B14, 1: B11 B12 B22, 2: B11 B12 B22 B13 B23)
+    // three beta approximations (lane 0: B11 B12 B13 B14, 1: B11 B12 B22, 2: B11 B12 B22 B13 B23);
+    // L and rho are read from the group scratch where they are used (registers for 3 lanes of 8)
+    double R[9], t[3], err = INFINITY;
     if (gl < 3) {
-        double L[6][10], rho[6];
-        for (int r = 0; r < 6; ++r) {
-            for (int c = 0; c < 10; ++c) L[r][c] = G[gL + 10 * r + c];
-            rho[r] = G[gRho + r];
-        }
+        const double* L = G + gL;   // row r: L[10 r + c]
+        const double* rho = G + gRho;
         double be[4] = {0, 0, 0, 0};
         if (gl == 0) {
             double A[6][4], b[6], x[4];
             const int cs[4] = {0, 1, 3, 6};
-            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 4; ++c) A[r][c] = L[r][cs[c]]; b[r] = rho[r]; }
+            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 4; ++c) A[r][c] = L[10 * r + cs[c]]; b[r] = rho[r]; }
             lsq6<4>(A, b, x);
             if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = -x[1] / be[0]; be[2] = -x[2] / be[0]; be[3] = -x[3] / be[0]; }
             else { be[0] = sqrt(x[0]); be[1] = x[1] / be[0]; be[2] = x[2] / be[0]; be[3] = x[3] / be[0]; }
         } else if (gl == 1) {
             double A[6][3], b[6], x[3];
-            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 3; ++c) A[r][c] = L[r][c]; b[r] = rho[r]; }
+            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 3; ++c) A[r][c] = L[10 * r + c]; b[r] = rho[r]; }
             lsq6<3>(A, b, x);
             if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0; }
             else { be[0] = sqrt(x[0]); be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0; }
             if (x[1] < 0) be[0] = -be[0];
         } else {
             double A[6][5], b[6], x[5];
-            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 5; ++c) A[r][c] = L[r][c]; b[r] = rho[r]; }
+            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 5; ++c) A[r][c] = L[10 * r + c]; b[r] = rho[r]; }
             lsq6<5>(A, b, x);
             if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0; }
             else { be[0] = sqrt(x[0]); be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0; }
@@ -604,9 +610,10 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
             be[2] = x[3] / be[0];
         }
         for (int it = 0; it < 5; ++it) {  // gauss_newton
+            __asm__ volatile("" ::: "memory");   // L is re-read from LDS each step, not held in registers
             double A[6][4], b[6], x[4];
             for (int i = 0; i < 6; ++i) {
-                const double* l = L[i];
+                const double* l = L + 10 * i;
                 A[i][0] = 2 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
                 A[i][1] = l[1] * be[0] + 2 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
                 A[i][2] = l[3] * be[0] + l[4] * be[1] + 2 * l[5] * be[2] + l[8] * be[3];
@@ -619,22 +626,17 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
             lsq6<4>(A, b, x);
             for (int i = 0; i < 4; ++i) be[i] += x[i];
         }
-        double R[9], t[3];
-        const double err = epnp_R_t(D, G, vi, be, R, t);
-        double* sol = G + gSol + 13 * gl;
-        for (int k = 0; k < 9; ++k) sol[k] = R[k];
-        for (int k = 0; k < 3; ++k) sol[9 + k] = t[k];
-        sol[12] = err;
+        err = epnp_R_t(D, G, vi, be, R, t);
     }
-    lds_fence();
     PPROF(10);
-    if (gl == 0) {
-        int N = 0;
-        if (G[gSol + 13 + 12] < G[gSol + 12]) N = 1;
-        if (G[gSol + 26 + 12] < G[gSol + 13 * N + 12]) N = 2;
-        const double* sol = G + gSol + 13 * N;
-        rodrigues_inv(sol, out);
-        out[3] = sol[9]; out[4] = sol[10]; out[5] = sol[11];
+    // the solution with the least mean reprojection error (the first on ties), chosen within the group
+    const double e0 = __shfl(err, 0, kPnGL), e1 = __shfl(err, 1, kPnGL), e2 = __shfl(err, 2, kPnGL);
+    int N = 0;
+    if (e1 < e0) N = 1;
+    if (e2 < (N == 1 ? e1 : e0)) N = 2;
+    if (gl == N) {
+        rodrigues_inv(R, out);
+        out[3] = t[0]; out[4] = t[1]; out[5] = t[2];
     }
     lds_fence();
     PPROF(11);
@@ -655,7 +657,7 @@ __device__ __forceinline__ void project_f(const double* R, const double* t, doub
 // K sums at once: the same per-value wave reduction and cross-wave order as block_sum
 // (the same bits), one barrier pair instead of K
 template <int K>
-__device__ __forceinline__ void block_sum_n(double (&v)[K], double* red /* [K * 4] */) {
+__device__ __forceinline__ void block_sum_n(double (&v)[K], double* red /* [K * kPnNW] */) {
 #pragma unroll
     for (int k = 0; k < K; ++k)
         for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
@@ -663,41 +665,47 @@ __device__ __forceinline__ void block_sum_n(double (&v)[K], double* red /* [K * 
     __syncthreads();
     if ((threadIdx.x & 63) == 0)
 #pragma unroll
-        for (int k = 0; k < K; ++k) red[k * 4 + w] = v[k];
+        for (int k = 0; k < K; ++k) red[k * kPnNW + w] = v[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = ((red[k * 4] + red[k * 4 + 1]) + red[k * 4 + 2]) + red[k * 4 + 3];
-}
-
-__device__ __forceinline__ double block_sum(double v, double* red) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    return ((red[0] + red[1]) + red[2]) + red[3];
-}
-
-// One sample's correspondences (the float copies, as solvePnPRansac casts them) and intrinsics.
-__device__ __forceinline__ void pnp_load_sample(const float* __restrict__ f, const int* idx, double fx, double fy,
-                                                double cx, double cy, EpnpData& D) {
-    D.fu = fx; D.fv = fy; D.uc = cx; D.vc = cy;
-    for (int j = 0; j < 5; ++j) {
-        for (int k = 0; k < 3; ++k) D.pw[j][k] = (double)f[5 * idx[j] + k];
-        for (int k = 0; k < 2; ++k) D.us[j][k] = (double)f[5 * idx[j] + 3 + k];
+    for (int k = 0; k < K; ++k) {   // the waves in order
+        double a = red[k * kPnNW];
+#pragma unroll
+        for (int u = 1; u < kPnNW; ++u) a += red[k * kPnNW + u];
+        v[k] = a;
     }
 }
 
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    double a[1] = {v};
+    block_sum_n<1>(a, red);
+    return a[0];
+}
+
+// One sample's correspondences (the float copies, as solvePnPRansac casts them) into the group
+// scratch (lane j < 5: point j), and the intrinsics.
+__device__ __forceinline__ void pnp_load_sample(const float* __restrict__ f, const int* idx, double fx, double fy,
+                                                double cx, double cy, EpnpData& D, double* G, int gl) {
+    D.fu = fx; D.fv = fy; D.uc = cx; D.vc = cy;
+    if (gl < 5) {
+        const int j = idx[gl == 0 ? 0 : gl == 1 ? 1 : gl == 2 ? 2 : gl == 3 ? 3 : 4];
+        for (int k = 0; k < 3; ++k) G[gPw + 3 * gl + k] = (double)f[5 * j + k];
+        for (int k = 0; k < 2; ++k) G[gUs + 2 * gl + k] = (double)f[5 * j + 3 + k];
+    }
+    lds_fence();
+}
+
 // EPnP control points and barycentric alphas (every lane of the group; lane 0 stages them in G).
-__device__ __forceinline__ void pnp_prepare(EpnpData& D, double* G, int gl) {
+__device__ __forceinline__ void pnp_prepare(double* G, int gl) {
+    const double* pw = G + gPw;
     double c0[3] = {0, 0, 0};
     for (int j = 0; j < 5; ++j)
-        for (int k = 0; k < 3; ++k) c0[k] += D.pw[j][k];
+        for (int k = 0; k < 3; ++k) c0[k] += pw[3 * j + k];
     for (int k = 0; k < 3; ++k) c0[k] /= 5;
     double A[3][3] = {}, w[3], E[3][3];
     for (int j = 0; j < 5; ++j)
         for (int a = 0; a < 3; ++a)
-            for (int b = 0; b < 3; ++b) A[a][b] += (D.pw[j][a] - c0[a]) * (D.pw[j][b] - c0[b]);
+            for (int b = 0; b < 3; ++b) A[a][b] += (pw[3 * j + a] - c0[a]) * (pw[3 * j + b] - c0[b]);
     eig3_desc(A, w, E);
     double cws[4][3];
     for (int k = 0; k < 3; ++k) cws[0][k] = c0[k];
@@ -725,16 +733,13 @@ __device__ __forceinline__ void pnp_prepare(EpnpData& D, double* G, int gl) {
     ci[2][0] = (CC[1][0] * CC[2][1] - CC[1][1] * CC[2][0]) * id;
     ci[2][1] = (CC[0][1] * CC[2][0] - CC[0][0] * CC[2][1]) * id;
     ci[2][2] = (CC[0][0] * CC[1][1] - CC[0][1] * CC[1][0]) * id;
-    for (int j = 0; j < 5; ++j) {
-        const double d0 = D.pw[j][0] - cws[0][0], d1 = D.pw[j][1] - cws[0][1], d2 = D.pw[j][2] - cws[0][2];
-        for (int a = 0; a < 3; ++a) D.al[j][1 + a] = ci[a][0] * d0 + ci[a][1] * d1 + ci[a][2] * d2;
-        D.al[j][0] = 1.0 - D.al[j][1] - D.al[j][2] - D.al[j][3];
-    }
     if (gl == 0)
         for (int j = 0; j < 5; ++j) {
-            for (int a = 0; a < 4; ++a) G[gAl + 4 * j + a] = D.al[j][a];
-            G[gUd + 2 * j] = D.uc - D.us[j][0];
-            G[gUd + 2 * j + 1] = D.vc - D.us[j][1];
+            const double d0 = pw[3 * j] - cws[0][0], d1 = pw[3 * j + 1] - cws[0][1], d2 = pw[3 * j + 2] - cws[0][2];
+            double al[4];
+            for (int a = 0; a < 3; ++a) al[1 + a] = ci[a][0] * d0 + ci[a][1] * d1 + ci[a][2] * d2;
+            al[0] = 1.0 - al[1] - al[2] - al[3];
+            for (int a = 0; a < 4; ++a) G[gAl + 4 * j + a] = al[a];
         }
     lds_fence();
 }
@@ -913,7 +918,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
     __shared__ int s_cnt[kPnH];
     __shared__ int s_sub[kPnH * 5];
     __shared__ double s_best[6];
-    __shared__ double s_red[4 * 28];
+    __shared__ double s_red[kPnNW * 28];
     __shared__ double s_lm[6 + 6 + 27 + 9];   // param, prev, dRdr, R
     __shared__ int s_niters, s_maxgood, s_k0, s_last, s_flag;
 
@@ -936,14 +941,13 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         if (tid == 0) { ok_out[p] = 0; ninl_out[p] = 0; iters_out[p] = 0; }
         return;
     }
-    auto load_sample = [&](const int* idx, EpnpData& D) { pnp_load_sample(f, idx, fx, fy, cx, cy, D); };
-    auto prepare = [&](EpnpData& D, double* G) { pnp_prepare(D, G, gl); };
+    auto load_sample = [&](const int* idx, EpnpData& D, double* G) { pnp_load_sample(f, idx, fx, fy, cx, cy, D, G, gl); };
     if (n == 5) {  // model_points == npoints: solvePnP(EPnP) on all points, no refinement
         if (h == 0) {
             const int idx[5] = {0, 1, 2, 3, 4};
             EpnpData D;
-            load_sample(idx, D);
-            prepare(D, s_grp);
+            load_sample(idx, D, s_grp);
+            pnp_prepare(s_grp, gl);
             epnp_group(D, gl, s_grp, s_best);
         }
         __syncthreads();
@@ -975,9 +979,9 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         if (live) {
             EpnpData D;
             PPROF_INIT;
-            load_sample(s_sub + h * 5, D);
             double* G = s_grp + h * kPnGS;
-            prepare(D, G);
+            load_sample(s_sub + h * 5, D, G);
+            pnp_prepare(G, gl);
             PPROF(6);
             epnp_group(D, gl, G, s_models[h]);
             if (gl == 0) rodrigues(s_models[h], s_models[h] + 6);
@@ -1065,8 +1069,9 @@ extern "C" int sfmhip_pnp_ransac(const double* obj, const double* img, const int
                    "pnp_ransac: null pointer");
     SFMHIP_REQUIRE(reprojection_error > 0 && confidence >= 0 && confidence <= 1,
                    "pnp_ransac: reprojection_error > 0, confidence in [0, 1]");
-    // one workgroup per problem (a phase-split form -- EPnP solves, scoring and the RANSAC replay as
-    // separate kernels over (problem, chunk) items -- measured slower: 0.694 vs 0.555 ms, round 4)
+    // one 512-thread workgroup per problem (a phase-split form -- EPnP solves, scoring and the RANSAC
+    // replay as separate kernels over (problem, chunk) items -- measured slower: 0.694 vs 0.555 ms,
+    // round 4; 256 threads with 32-hypothesis chunks and 432 registers: 0.517 vs 0.467 ms, round 5)
     hipLaunchKernelGGL(pnp_ransac_kernel, dim3(n_problems), dim3(kPnThreads), 0, as_stream(stream), obj, img, offsets,
                        cam, iterations, reprojection_error, confidence, work, rvec, tvec, inlier_mask, n_inliers, iters,
                        ok);

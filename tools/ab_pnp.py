@@ -1,5 +1,6 @@
-"""A/B of two library builds (separate processes) on bench.py's PnP workload (256 x 2000, 30 %
-outliers): median time of the batched solvePnPRansac call and a checksum of every output."""
+"""PnP A/B on bench.py's workload (256 x 2000, 30 % outliers): median time of the batched
+solvePnPRansac call and a checksum of every output, interleaved over SFMHIP_AB values in one
+process: python tools/ab_pnp.py [ab values, default 0]."""
 import hashlib
 import importlib
 import os
@@ -32,18 +33,26 @@ Xd = torch.tensor(np.concatenate(Xs), device=dev)
 ud = torch.tensor(np.concatenate(uvs), device=dev)
 of = torch.tensor(np.arange(P + 1, dtype=np.int64) * n, device=dev)
 cam = torch.tensor(v._cam(K), device=dev).expand(P, 4).contiguous()
-r = v.pnp_ransac_batched(Xd, ud, of, cam)
-ts = []
-for _ in range(10):
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    r = v.pnp_ransac_batched(Xd, ud, of, cam)
-    e1.record()
-    torch.cuda.synchronize()
-    ts.append(e0.elapsed_time(e1))
-h = hashlib.sha256()
-for k in sorted(r):
-    if isinstance(r[k], torch.Tensor):
-        h.update(r[k].cpu().numpy().tobytes())
-print(f"pnp {np.median(ts):.3f} ms sha {h.hexdigest()[:16]}", flush=True)
+abs_ = [int(a) for a in sys.argv[1:]] or [0]
+ts = {a: [] for a in abs_}
+sha = {}
+for rnd in range(3):
+    for a in abs_:
+        os.environ["SFMHIP_AB"] = str(a)
+        sfm.knobs_reload()
+        r = v.pnp_ransac_batched(Xd, ud, of, cam)
+        for _ in range(5):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = v.pnp_ransac_batched(Xd, ud, of, cam)
+            e1.record()
+            torch.cuda.synchronize()
+            ts[a].append(e0.elapsed_time(e1))
+        h = hashlib.sha256()
+        for k in sorted(r):
+            if isinstance(r[k], torch.Tensor):
+                h.update(r[k].cpu().numpy().tobytes())
+        sha[a] = h.hexdigest()[:16]
+for a in abs_:
+    print(f"ab {a}: pnp {np.median(ts[a]):.3f} ms (min {min(ts[a]):.3f}) sha {sha[a]}", flush=True)
