@@ -988,47 +988,54 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         }
         __syncthreads();
         PPROF(1);
-        const int nh = min(kPnH, niters - k0);   // uniform
-        for (int i0 = 0; i0 < n; i0 += kPnThreads) {
-            const int i = i0 + tid;
-            const bool valid = i < n;
-            float X = 0, Y = 0, Z = 0, u = 0, v = 0;
-            if (valid) { X = f[5 * i]; Y = f[5 * i + 1]; Z = f[5 * i + 2]; u = f[5 * i + 3]; v = f[5 * i + 4]; }
-            // four models per step: independent projection chains (each with its IEEE division)
-            for (int h0 = 0; h0 < nh; h0 += 4) {
-                float e4[4];
+        // scoring and replay in two halves of the chunk: the replay of the first half usually
+        // lowers niters below the second (OpenCV's ~25 iterations), whose scoring is then skipped
+        for (int hb = 0; hb < kPnH; hb += kPnH / 2) {
+            const int nh = min(hb + kPnH / 2, s_niters - k0);   // uniform: the models [hb, nh) are live
+            if (nh <= hb) break;
+            for (int i0 = 0; i0 < n; i0 += kPnThreads) {
+                const int i = i0 + tid;
+                const bool valid = i < n;
+                float X = 0, Y = 0, Z = 0, u = 0, v = 0;
+                if (valid) { X = f[5 * i]; Y = f[5 * i + 1]; Z = f[5 * i + 2]; u = f[5 * i + 3]; v = f[5 * i + 4]; }
+                // four models per step: independent projection chains (each with its IEEE division)
+                for (int h0 = hb; h0 < nh; h0 += 4) {
+                    float e4[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int hh = min(h0 + q, nh - 1);
-                    float pu, pv;
-                    project_f(s_models[hh] + 6, s_models[hh] + 3, fx, fy, cx, cy, X, Y, Z, pu, pv);
-                    const float du = u - pu, dv = v - pv;
-                    e4[q] = du * du + dv * dv;
-                }
+                    for (int q = 0; q < 4; ++q) {
+                        const int hh = min(h0 + q, nh - 1);
+                        float pu, pv;
+                        project_f(s_models[hh] + 6, s_models[hh] + 3, fx, fy, cx, cy, X, Y, Z, pu, pv);
+                        const float du = u - pu, dv = v - pv;
+                        e4[q] = du * du + dv * dv;
+                    }
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int c = __popcll(__ballot(valid && e4[q] <= thr));
-                    if (lane == 0 && c && h0 + q < nh) atomicAdd(&s_cnt[h0 + q], c);
+                    for (int q = 0; q < 4; ++q) {
+                        const int c = __popcll(__ballot(valid && e4[q] <= thr));
+                        if (lane == 0 && c && h0 + q < nh) atomicAdd(&s_cnt[h0 + q], c);
+                    }
                 }
             }
-        }
-        __syncthreads();
-        PPROF(2);
-        if (tid == 0) {
-            int nit = niters, maxgood = s_maxgood, last = s_last;
-            for (int hh = 0; hh < kPnH; ++hh) {
-                const int k = k0 + hh;
-                if (k >= nit) break;
-                const int good = s_cnt[hh];
-                if (good > max(maxgood, 4)) {
-                    for (int e = 0; e < 6; ++e) s_best[e] = s_models[hh][e];
-                    maxgood = good;
-                    nit = update_num_iters(confidence, (double)(n - good) / n, 5, nit);
+            __syncthreads();
+            PPROF(2);
+            if (tid == 0) {
+                int nit = s_niters, maxgood = s_maxgood, last = s_last;
+                for (int hh = hb; hh < hb + kPnH / 2; ++hh) {
+                    const int k = k0 + hh;
+                    if (k >= nit) break;
+                    const int good = s_cnt[hh];
+                    if (good > max(maxgood, 4)) {
+                        for (int e = 0; e < 6; ++e) s_best[e] = s_models[hh][e];
+                        maxgood = good;
+                        nit = update_num_iters(confidence, (double)(n - good) / n, 5, nit);
+                    }
+                    last = k;
                 }
-                last = k;
+                s_niters = nit; s_maxgood = maxgood; s_last = last;
             }
-            s_niters = nit; s_maxgood = maxgood; s_last = last; s_k0 = k0 + kPnH;
+            __syncthreads();
         }
+        if (tid == 0) s_k0 = k0 + kPnH;
         __syncthreads();
         if (s_k0 >= s_niters) break;
     }
