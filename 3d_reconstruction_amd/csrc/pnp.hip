@@ -353,10 +353,14 @@ __device__ unsigned long long g_wgt[2 * 1024];  // per-workgroup start / end
 // Result: the eigenvalues in G[gEv], the eigenvectors as the columns of V (G[gV], over A).
 __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
     double* A = G + gA;
-    double* vv = G + gL;        // 12 doubles (L is built later)
-    double* qv = G + gL + 12;   // 12 doubles
+    double* vv = G + gL;        // 13 doubles (L is built later)
+    double* qv = G + gL + 13;   // 13 doubles
     const int r0 = gl, r1 = gl + kPnGL;
     const bool h1 = r1 < 12;
+    // lanes without a second row read and write a sink row 12 (A[144..155] = the eigenvalue slots,
+    // written after the QL): every load is unconditional (no branch and wait per element) and the
+    // results of the sink row are masked by selects
+    const int r1s = h1 ? r1 : 12;
     double z0[12], z1[12];   // rows r0 and r1 of Q
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
@@ -367,8 +371,9 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
         // x = A[k+1..11][k]; |x|^2 over the group
-        const double a0 = r0 > k ? A[r0 * 12 + k] : 0.0;
-        const double a1 = h1 && r1 > k ? A[r1 * 12 + k] : 0.0;
+        const double t0 = A[r0 * 12 + k], t1 = A[r1s * 12 + k];
+        const double a0 = r0 > k ? t0 : 0.0;
+        const double a1 = h1 && r1 > k ? t1 : 0.0;
         double n2 = fma(a0, a0, a1 * a1);
 #pragma unroll
         for (int o = kPnGL / 2; o > 0; o >>= 1) n2 += __shfl_xor(n2, o, kPnGL);
@@ -385,7 +390,7 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
         const double v0 = r0 == k + 1 ? vk : a0;   // rows <= k: 0 (a0 = 0 there)
         const double v1 = r1 == k + 1 ? vk : a1;
         vv[r0] = v0;
-        if (h1) vv[r1] = v1;
+        vv[r1s] = v1;
         lds_fence();
         // p = beta A v on the trailing block; K = beta / 2 v.p
         double p0 = 0.0, p1 = 0.0;
@@ -393,7 +398,7 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
         for (int j = k + 1; j < 12; ++j) {
             const double vj = vv[j];
             p0 = fma(A[r0 * 12 + j], vj, p0);
-            if (h1) p1 = fma(A[r1 * 12 + j], vj, p1);
+            p1 = fma(A[r1s * 12 + j], vj, p1);
         }
         p0 = r0 > k ? beta * p0 : 0.0;
         p1 = h1 && r1 > k ? beta * p1 : 0.0;
@@ -403,15 +408,16 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
         kk *= 0.5 * beta;
         const double q0 = fma(-kk, v0, p0), q1 = fma(-kk, v1, p1);
         qv[r0] = q0;
-        if (h1) qv[r1] = q1;
+        qv[r1s] = q1;
         lds_fence();
         // A <- A - v q^T - q v^T on the trailing block (own rows); Q <- Q H (own rows)
         double w0 = 0.0, w1 = 0.0;
 #pragma unroll
         for (int j = k + 1; j < 12; ++j) {
             const double vj = vv[j], qj = qv[j];
-            if (r0 > k) A[r0 * 12 + j] = A[r0 * 12 + j] - fma(v0, qj, q0 * vj);
-            if (h1 && r1 > k) A[r1 * 12 + j] = A[r1 * 12 + j] - fma(v1, qj, q1 * vj);
+            const double x0j = A[r0 * 12 + j], x1j = A[r1s * 12 + j];
+            if (r0 > k) A[r0 * 12 + j] = x0j - fma(v0, qj, q0 * vj);
+            if (r1 > k) A[r1s * 12 + j] = x1j - fma(v1, qj, q1 * vj);
             w0 = fma(z0[j], vj, w0);
             w1 = fma(z1[j], vj, w1);
         }
@@ -508,15 +514,26 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
     // M^T M (12x12) into A
     // (alphas and uc - u, vc - v were staged in G by prepare: a dynamic index into D would put
     // it in scratch memory)
-    for (int e = gl; e < 144; e += kPnGL) {
+    double al[5][4], dup[5], dvp[5];   // the alphas and (uc - u, vc - v) in registers: static indices below
+#pragma unroll
+    for (int p = 0; p < 5; ++p) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) al[p][c] = G[gAl + 4 * p + c];
+        dup[p] = D.uc - G[gUs + 2 * p];
+        dvp[p] = D.vc - G[gUs + 2 * p + 1];
+    }
+#pragma unroll 1
+    for (int t = 0; t < 144 / kPnGL; ++t) {
+        const int e = gl + kPnGL * t;
         const int i = e / 12, j = e % 12;
+        const int ci = i / 3, ki = i % 3, cj = j / 3, kj = j % 3;
         double acc = 0;
 #pragma unroll
         for (int p = 0; p < 5; ++p) {
             // M rows 2p (u) and 2p+1 (v): col 3c -> a*fu / 0, col 3c+1 -> 0 / a*fv, col 3c+2 -> a*(uc-u) / a*(vc-v)
-            const int ci = i / 3, ki = i % 3, cj = j / 3, kj = j % 3;
-            const double ai = G[gAl + 4 * p + ci], aj = G[gAl + 4 * p + cj];
-            const double du = D.uc - G[gUs + 2 * p], dv = D.vc - G[gUs + 2 * p + 1];
+            const double ai = ci == 0 ? al[p][0] : ci == 1 ? al[p][1] : ci == 2 ? al[p][2] : al[p][3];
+            const double aj = cj == 0 ? al[p][0] : cj == 1 ? al[p][1] : cj == 2 ? al[p][2] : al[p][3];
+            const double du = dup[p], dv = dvp[p];
             const double mu_i = ki == 0 ? ai * D.fu : ki == 1 ? 0.0 : ai * du;
             const double mu_j = kj == 0 ? aj * D.fu : kj == 1 ? 0.0 : aj * du;
             const double mv_i = ki == 0 ? 0.0 : ki == 1 ? ai * D.fv : ai * dv;
