@@ -1,4 +1,5 @@
-"""Launch the C3 match kernel a few times (for rocprofv3 --pmc passes)."""
+"""Launch the C3 all-pairs match a few times (for rocprofv3 --pmc passes): the exact float mode
+of the bench headline (int8 MFMA certified filter + f64 re-score); EXACT=0 runs the int8 mode."""
 import importlib
 import os
 import sys
@@ -15,7 +16,8 @@ bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_FLOAT)
 del x
 pairs = torch.from_numpy(sfm.all_pairs(n_img)).to(dev)
 out = torch.empty((pairs.shape[0], bank.m_pad), dtype=torch.int32, device=dev)
+exact = os.environ.get("EXACT", "1") != "0"
 for _ in range(int(os.environ.get("REPS", "2"))):
-    bank._launch(pairs, 3, 4, out, None, None)
+    bank.match(pairs, ratio=0.75, out=out, exact=exact)
 torch.cuda.synchronize()
 print("matches", int((out >= 0).sum().item()))
