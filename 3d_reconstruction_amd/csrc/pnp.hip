@@ -12,8 +12,8 @@
 //     (OpenCV's ~25-40 iterations at 30 % outliers fit one chunk: round 4's
 //     32-hypothesis chunks sent the 33-37-iteration problems through a second
 //     chunk, which bounded the call); each sample is solved by EPnP in an
-//     8-lane group (M^T M reduced to tridiagonal form and its eigenvectors by
-//     the implicit QL iteration, the three beta approximations + Gauss-Newton
+//     8-lane group (M^T M reduced to tridiagonal form, its four smallest
+//     eigenpairs by bisection + inverse iteration, the three beta approximations + Gauss-Newton
 //     in lanes 0..2, Procrustes; the sample, alphas, L and V live in the
 //     group's LDS scratch so that the kernel fits 256 VGPRs), scored by all
 //     lanes (float squared reprojection error <= 64, wave ballots) and
@@ -344,14 +344,173 @@ __device__ unsigned long long g_wgt[2 * 1024];  // per-workgroup start / end
 #define PPROF_ADD(i, v) do {} while (0)
 #endif
 
-// EPnP eigen-decomposition of M^T M (12x12, symmetric) by Householder tridiagonalisation and
-// the implicit QL iteration (EISPACK tred2 / tql2 form), on a kPnGL-lane group.  A (G[gA]) is
-// reduced in LDS, each lane owning rows gl and gl + 8; the reflector v and the update vector q
-// go through LDS (G[gL], before L is built); Q = H_0 ... H_9 is kept in registers (the lane's two rows).
-// The QL iteration runs on every lane of the group (d, e in registers, the same operations on
-// the same values) and each lane rotates its own rows of Q, so no rotation is broadcast.
+// The 4 smallest eigenpairs of the tridiagonal T (d, e: e[i] couples i and i + 1) that the
+// Householder reduction left, back-transformed by Q (rows z0, z1 of this lane): EPnP needs only
+// the four eigenvectors of the smallest eigenvalues of M^T M.  Lane k = gl & 3 bisects the Sturm
+// counts for the k-th smallest eigenvalue (LAPACK dstebz form; lanes k and k + 4 trisect the
+// Gershgorin interval together, 30 steps); then, in order k = 0..3, every lane of the group runs three steps
+// of inverse iteration on T - lambda_k I (Gaussian elimination with partial pivoting, dlagtf /
+// dlagts form, tiny pivots perturbed), each step reorthogonalised against the earlier vectors
+// (the two exact null vectors of M^T M form a cluster).  Output as the QL's: the eigenvalues in
+// G[gEv] (slots 4..11 = +inf, so the selection below takes 0..3 ascending), the eigenvectors in
+// columns 0..3 of V.
+template <int NB, int NI>
+__device__ __forceinline__ void epnp_eig4_tri(int gl, double* G, const double (&d)[12], const double (&e)[12],
+                                              const double (&z0)[12], const double (&z1)[12], int r0, int r1,
+                                              bool h1) {
+    // Q's rows wait in the reduced matrix's slots (A is consumed: d, e are in registers)
+    const int r1s = h1 ? r1 : 12;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        G[gA + r0 * 12 + j] = z0[j];
+        G[gA + r1s * 12 + j] = z1[j];
+    }
+    double lo = d[0], hi = d[0], emax2 = 0.0, tn = 0.0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + fabs(e[i]);
+        lo = fmin(lo, d[i] - r);
+        hi = fmax(hi, d[i] + r);
+        emax2 = fmax(emax2, e[i] * e[i]);
+        tn = fmax(tn, fabs(d[i]) + r);
+    }
+    const double pivmin = 0x1p-1000 * fmax(1.0, emax2);
+    const double margin = 0x1p-50 * fmax(tn, 0x1p-1000) + 2.0 * pivmin;
+    lo -= margin;
+    hi += margin;
+    auto count = [&](double x) -> int {   // eigenvalues < x (Sturm sequence of the LDL^T pivots)
+        double q = d[0] - x;
+        int c = q < 0.0 ? 1 : 0;
+#pragma unroll
+        for (int i = 1; i < 12; ++i) {
+            if (fabs(q) < pivmin) q = -pivmin;
+            double r = __builtin_amdgcn_rcp(q);
+            r = fma(fma(-q, r, 1.0), r, r);
+            q = fma(-e[i - 1] * e[i - 1], r, d[i] - x);
+            c += q < 0.0 ? 1 : 0;
+        }
+        return c;
+    };
+    // lanes k and k + 4 trisect together: counts at a + w and a + 2w, exchanged (3^30 ~ 2^47.5)
+    const int kk = gl & 3;
+    double a = lo, b = hi;
+    for (int it = 0; it < NB; ++it) {
+        const double w = (b - a) * (1.0 / 3.0);
+        const double m1 = a + w, m2 = a + 2.0 * w;
+        const int c = count(gl < 4 ? m1 : m2);
+        const int c1 = __shfl(c, kk, kPnGL), c2 = __shfl(c, kk + 4, kPnGL);
+        if (c1 > kk) {
+            b = m1;
+        } else if (c2 > kk) {
+            a = m1;
+            b = m2;
+        } else {
+            a = m2;
+        }
+    }
+    const double lam_own = 0.5 * (a + b);
+    double lam[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lam[k] = __shfl(lam_own, k, kPnGL);
+    double* Y = G + gL;   // the four vectors of T (the reduction's scratch is free)
+    const double tol = 0x1p-52 * fmax(tn, 0x1p-1000);
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+        const double lk = __shfl(lam_own, k, kPnGL);
+        // T - lambda I = P L U (U: diagonal u0 and two superdiagonals u1, u2)
+        double u0[12], u1[12], u2[12], lm[11];
+        bool sw[11];
+        double pd = d[0] - lk, p1 = e[0], p2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 11; ++i) {
+            const double nd = e[i], n1 = d[i + 1] - lk, n2 = i + 1 < 11 ? e[i + 1] : 0.0;
+            sw[i] = fabs(nd) > fabs(pd);
+            if (!sw[i]) {
+                const double piv = fabs(pd) < tol ? (pd < 0.0 ? -tol : tol) : pd;
+                const double m = nd * rcp_nr(piv);
+                u0[i] = piv; u1[i] = p1; u2[i] = p2; lm[i] = m;
+                pd = n1 - m * p1; p1 = n2 - m * p2; p2 = 0.0;
+            } else {
+                const double m = pd * rcp_nr(nd);
+                u0[i] = nd; u1[i] = n1; u2[i] = n2; lm[i] = m;
+                pd = p1 - m * n1; p1 = p2 - m * n2; p2 = 0.0;
+            }
+        }
+        u0[11] = fabs(pd) < tol ? (pd < 0.0 ? -tol : tol) : pd;
+        u1[11] = 0.0; u2[11] = 0.0; u2[10] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) u0[i] = rcp_nr(u0[i]);   // the solves multiply by 1 / u0
+        double y[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) y[i] = 1.0 / (1.0 + (double)((i * 7 + k * 5) % 12));   // a generic start
+#pragma unroll 1
+        for (int step = 0; step < NI; ++step) {
+            // solve (T - lambda I) x = y: the row operations, then U back-substitution
+#pragma unroll
+            for (int i = 0; i < 11; ++i) {
+                if (sw[i]) { const double t = y[i]; y[i] = y[i + 1]; y[i + 1] = t; }
+                y[i + 1] -= lm[i] * y[i];
+            }
+            y[11] = y[11] * u0[11];
+            y[10] = (y[10] - u1[10] * y[11]) * u0[10];
+#pragma unroll
+            for (int i = 9; i >= 0; --i) y[i] = (y[i] - u1[i] * y[i + 1] - u2[i] * y[i + 2]) * u0[i];
+            // against the earlier vectors (modified Gram-Schmidt), then to unit length
+            for (int j = 0; j < k; ++j) {
+                double dt = 0.0;
+#pragma unroll
+                for (int i = 0; i < 12; ++i) dt = fma(y[i], Y[12 * j + i], dt);
+#pragma unroll
+                for (int i = 0; i < 12; ++i) y[i] = fma(-dt, Y[12 * j + i], y[i]);
+            }
+            double n2 = 0.0;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) n2 = fma(y[i], y[i], n2);
+            const double inv = n2 > 0.0 ? rsq_nr(n2) : 0.0;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) y[i] *= inv;
+        }
+        if (gl == 0)
+#pragma unroll
+            for (int i = 0; i < 12; ++i) Y[12 * k + i] = y[i];
+        lds_fence();
+    }
+    // V[:, k] = Q y_k (this lane's rows: read back, then overwritten by V's), the eigenvalues
+    double q0[12], q1[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        q0[j] = G[gA + r0 * 12 + j];
+        q1[j] = G[gA + r1s * 12 + j];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const double yj = Y[12 * k + j];
+            v0 = fma(q0[j], yj, v0);
+            v1 = fma(q1[j], yj, v1);
+        }
+        G[gV + r0 * 12 + k] = v0;
+        if (h1) G[gV + r1 * 12 + k] = v1;
+    }
+    if (gl == 0) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) G[gEv + i] = i < 4 ? lam[i] : INFINITY;
+    }
+    lds_fence();
+}
+
+// EPnP eigen-decomposition of M^T M (12x12, symmetric): Householder tridiagonalisation (EISPACK
+// tred2 form) on a kPnGL-lane group, then the four smallest eigenpairs of the tridiagonal
+// (epnp_eig4_tri).  A (G[gA]) is reduced in LDS, each lane owning rows gl and gl + 8; the
+// reflector v and the update vector q go through LDS (G[gL], before L is built); Q = H_0 ... H_9
+// is kept in registers (the lane's two rows).  Round 4-5 ran the implicit QL iteration (tql2) for
+// all twelve eigenpairs instead: 96-100 us of a 150 us EPnP; bisection + inverse iteration took
+// the bench's PnP call from 0.414 to 0.353 ms (profiles/r5/ab/pnp_512_ab_r5.txt).
 // Result: the eigenvalues in G[gEv], the eigenvectors as the columns of V (G[gV], over A).
-__device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
+template <int NB, int NI>
+__device__ __forceinline__ void epnp_eig(int gl, double* G) {
     double* A = G + gA;
     double* vv = G + gL;        // 13 doubles (L is built later)
     double* qv = G + gL + 13;   // 13 doubles
@@ -435,80 +594,11 @@ __device__ __forceinline__ void epnp_eig_ql(int gl, double* G) {
     e[11] = 0.0;
 #pragma unroll
     for (int i = 0; i < 12; ++i) d[i] = A[i * 13];
-    // implicit QL (tql2): e[i] couples d[i] and d[i + 1]
-    for (int l = 0; l < 12; ++l) {
-        for (int iter = 0; iter < 40; ++iter) {
-            int m = 11;
-#pragma unroll
-            for (int j = 10; j >= 0; --j) {
-                const double dd = fabs(d[j]) + fabs(d[j + 1]);
-                if (j >= l && fabs(e[j]) + dd == dd) m = j;
-            }
-            if (m <= l) break;
-            double dl = 0.0, dl1 = 0.0, el = 0.0, dm = 0.0;
-#pragma unroll
-            for (int j = 0; j < 12; ++j) {
-                if (j == l) { dl = d[j]; el = e[j]; }
-                if (j == l + 1) dl1 = d[j];
-                if (j == m) dm = d[j];
-            }
-            double g = (dl1 - dl) * (0.5 * rcp_nr(el));
-            double r = sqrt_nr(fma(g, g, 1.0));
-            g = dm - dl + el * rcp_nr(g + (g >= 0.0 ? r : -r));
-            double s = 1.0, c = 1.0, p = 0.0;
-            bool live = true;
-#pragma unroll
-            for (int i = 10; i >= 0; --i) {
-                if (!(live && i >= l && i < m)) continue;
-                const double f = s * e[i], b = c * e[i];
-                const double x2 = fma(f, f, g * g);
-                const double ir = x2 > 0.0 ? rsq_nr(x2) : 0.0;   // r and 1/r from one reciprocal square root
-                r = x2 * ir;
-                e[i + 1] = r;
-                if (r == 0.0) {   // underflow: deflate and restart this l
-                    d[i + 1] -= p;
-#pragma unroll
-                    for (int j = 0; j < 12; ++j)
-                        if (j == m) e[j] = 0.0;
-                    live = false;
-                    continue;
-                }
-                s = f * ir;
-                c = g * ir;
-                g = d[i + 1] - p;
-                r = fma(d[i] - g, s, 2.0 * c * b);
-                p = s * r;
-                d[i + 1] = g + p;
-                g = fma(c, r, -b);
-                const double f0 = z0[i + 1], f1 = z1[i + 1];
-                z0[i + 1] = fma(s, z0[i], c * f0);
-                z0[i] = fma(c, z0[i], -s * f0);
-                z1[i + 1] = fma(s, z1[i], c * f1);
-                z1[i] = fma(c, z1[i], -s * f1);
-            }
-            if (live) {
-#pragma unroll
-                for (int j = 0; j < 12; ++j) {
-                    if (j == l) { d[j] -= p; e[j] = g; }
-                    if (j == m) e[j] = 0.0;
-                }
-            }
-        }
-    }
-    lds_fence();   // (the group is 8 lanes of one wave: every read of A above precedes these writes)
-    if (gl == 0) {
-#pragma unroll
-        for (int i = 0; i < 12; ++i) G[gEv + i] = d[i];
-    }
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {
-        G[gV + r0 * 12 + j] = z0[j];
-        if (h1) G[gV + r1 * 12 + j] = z1[j];
-    }
-    lds_fence();
+    epnp_eig4_tri<NB, NI>(gl, G, d, e, z0, z1, r0, r1, h1);
 }
 
 // EPnP on 5 correspondences by a kPnGL-lane group; writes (rvec, tvec) to out[6].
+template <int NB, int NI>
 __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
     PPROF_INIT;
     // M^T M (12x12) into A
@@ -544,9 +634,10 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
     }
     lds_fence();
     PPROF(7);
-    // the 12x12 symmetric eigen-decomposition: Householder tridiagonalisation + implicit QL
-    // (a parallel-ordered two-sided Jacobi measured slower: EPnP 154 vs 98 us of QL, round 4)
-    epnp_eig_ql(gl, G);
+    // the four smallest eigenpairs of the 12x12 M^T M: Householder tridiagonalisation + bisection +
+    // inverse iteration (the implicit QL for all twelve, round 4-5, and a parallel-ordered two-sided
+    // Jacobi before it measured slower)
+    epnp_eig<NB, NI>(gl, G);
     PPROF(8);
     // the 4 smallest eigenvalues (ascending), canonical signs
     int vi[4];
@@ -675,14 +766,35 @@ __device__ __forceinline__ void project_f(const double* R, const double* t, doub
 // (the same bits), one barrier pair instead of K
 template <int K>
 __device__ __forceinline__ void block_sum_n(double (&v)[K], double* red /* [K * kPnNW] */) {
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0)
+    if constexpr (K == 1) {
+        for (int o = 32; o > 0; o >>= 1) v[0] += __shfl_xor(v[0], o);
+        __syncthreads();
+        if (lane == 0) red[w] = v[0];
+    } else {
+        // reduce-scatter over the wave: at the step with offset o each lane keeps the half of its
+        // values its lane bit selects and adds the partner's copy of that half (the same pairwise
+        // tree per value as the plain xor butterfly, so the same sums): 16 + 8 + 4 + 2 + 1 + 1
+        // shuffles for up to 32 values instead of 6 per value; lane l ends with value (l >> 1) & 31
+        static_assert(K <= 32, "reduce-scatter width");
+        double x[32];
 #pragma unroll
-        for (int k = 0; k < K; ++k) red[k * kPnNW + w] = v[k];
+        for (int k = 0; k < 32; ++k) x[k] = k < K ? v[k] : 0.0;
+#pragma unroll
+        for (int o = 32, half = 16; o >= 2; o >>= 1, half >>= 1) {
+            const bool hi = (lane & o) != 0;
+#pragma unroll
+            for (int j = 0; j < half; ++j) {
+                const double keep = hi ? x[j + half] : x[j], send = hi ? x[j] : x[j + half];
+                x[j] = keep + __shfl_xor(send, o);
+            }
+        }
+        x[0] += __shfl_xor(x[0], 1);
+        __syncthreads();
+        const int idx = (lane >> 1) & 31;
+        if ((lane & 1) == 0 && idx < K) red[idx * kPnNW + w] = x[0];
+    }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < K; ++k) {   // the waves in order
@@ -807,10 +919,8 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
     __syncthreads();
     PPROF(4);
     auto eval = [&](bool with_j, double* jtj, double* jte) -> double {
-        if (tid == 0) {
-            rodrigues(prm, Rm);
-            rodrigues_jac(prm, dR);
-        }
+        if (tid == 0) rodrigues(prm, Rm);
+        if (with_j && tid == 64) rodrigues_jac(prm, dR);   // another wave: the two run side by side
         __syncthreads();
         double acc[28];
         for (int k = 0; k < 28; ++k) acc[k] = 0;
@@ -925,6 +1035,7 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
     }
 }
 
+template <int NB, int NI>
 __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
     const double* __restrict__ obj, const double* __restrict__ img, const int64_t* __restrict__ offs,
     const double* __restrict__ cam, int max_iters, double reproj, double confidence, float* __restrict__ wf,
@@ -965,7 +1076,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
             EpnpData D;
             load_sample(idx, D, s_grp);
             pnp_prepare(s_grp, gl);
-            epnp_group(D, gl, s_grp, s_best);
+            epnp_group<NB, NI>(D, gl, s_grp, s_best);
         }
         __syncthreads();
         if (tid == 0) {
@@ -1000,7 +1111,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
             load_sample(s_sub + h * 5, D, G);
             pnp_prepare(G, gl);
             PPROF(6);
-            epnp_group(D, gl, G, s_models[h]);
+            epnp_group<NB, NI>(D, gl, G, s_models[h]);
             if (gl == 0) rodrigues(s_models[h], s_models[h] + 6);
         }
         __syncthreads();
@@ -1096,7 +1207,8 @@ extern "C" int sfmhip_pnp_ransac(const double* obj, const double* img, const int
     // one 512-thread workgroup per problem (a phase-split form -- EPnP solves, scoring and the RANSAC
     // replay as separate kernels over (problem, chunk) items -- measured slower: 0.694 vs 0.555 ms,
     // round 4; 256 threads with 32-hypothesis chunks and 432 registers: 0.517 vs 0.467 ms, round 5)
-    hipLaunchKernelGGL(pnp_ransac_kernel, dim3(n_problems), dim3(kPnThreads), 0, as_stream(stream), obj, img, offsets,
+    // 30 trisection steps (bisection: 40 / 48 / 56 steps within 2 %), 3 inverse-iteration steps
+    hipLaunchKernelGGL((pnp_ransac_kernel<30, 3>), dim3(n_problems), dim3(kPnThreads), 0, as_stream(stream), obj, img, offsets,
                        cam, iterations, reprojection_error, confidence, work, rvec, tvec, inlier_mask, n_inliers, iters,
                        ok);
     return check_launch("pnp_ransac_kernel");
