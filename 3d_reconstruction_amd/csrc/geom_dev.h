@@ -7,6 +7,37 @@
 
 namespace sfmhip {
 
+// Wave sum of K doubles per lane as a reduce-scatter: at the step with offset o (32, 16, ...)
+// each lane keeps the half of its values that its lane bit o selects and adds the partner's copy
+// of that half, then the last value is summed over the remaining offsets.  Each value is summed
+// by the same pairwise tree as the plain xor butterfly (offset 32 first), so the sums are the same
+// bits, with 2^P - 1 + (6 - P) shuffles (P = ceil(log2 K)) instead of 6 K.  Returns the sum of
+// value `idx` = lane >> (6 - P); the lanes whose low 6 - P bits are zero hold distinct indices.
+template <int K>
+__device__ __forceinline__ double wave_reduce_scatter(const double (&v)[K], int lane, int& idx, bool& writer) {
+    constexpr int P = K <= 1 ? 0 : K <= 2 ? 1 : K <= 4 ? 2 : K <= 8 ? 3 : K <= 16 ? 4 : 5;
+    static_assert(K <= 32, "reduce-scatter width");
+    constexpr int NP = 1 << P;
+    double x[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) x[k] = k < K ? v[k] : 0.0;
+#pragma unroll
+    for (int st = 0; st < P; ++st) {
+        const int o = 32 >> st, half = NP >> (st + 1);
+        const bool hi = (lane & o) != 0;
+#pragma unroll
+        for (int j = 0; j < half; ++j) {
+            const double keep = hi ? x[j + half] : x[j], send = hi ? x[j] : x[j + half];
+            x[j] = keep + __shfl_xor(send, o);
+        }
+    }
+#pragma unroll
+    for (int o = 32 >> P; o >= 1; o >>= 1) x[0] += __shfl_xor(x[0], o);
+    idx = lane >> (6 - P);
+    writer = (lane & ((64 >> P) - 1)) == 0 && idx < K;
+    return x[0];
+}
+
 // OpenCV Rodrigues (vector -> matrix), op order of cv::Rodrigues:
 //   theta = sqrt(rx^2+ry^2+rz^2); theta < DBL_EPSILON -> I;
 //   R = (c*I + c1*r r^T) + s*[r]_x  with r normalised by itheta = 1/theta.

@@ -768,33 +768,11 @@ template <int K>
 __device__ __forceinline__ void block_sum_n(double (&v)[K], double* red /* [K * kPnNW] */) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if constexpr (K == 1) {
-        for (int o = 32; o > 0; o >>= 1) v[0] += __shfl_xor(v[0], o);
-        __syncthreads();
-        if (lane == 0) red[w] = v[0];
-    } else {
-        // reduce-scatter over the wave: at the step with offset o each lane keeps the half of its
-        // values its lane bit selects and adds the partner's copy of that half (the same pairwise
-        // tree per value as the plain xor butterfly, so the same sums): 16 + 8 + 4 + 2 + 1 + 1
-        // shuffles for up to 32 values instead of 6 per value; lane l ends with value (l >> 1) & 31
-        static_assert(K <= 32, "reduce-scatter width");
-        double x[32];
-#pragma unroll
-        for (int k = 0; k < 32; ++k) x[k] = k < K ? v[k] : 0.0;
-#pragma unroll
-        for (int o = 32, half = 16; o >= 2; o >>= 1, half >>= 1) {
-            const bool hi = (lane & o) != 0;
-#pragma unroll
-            for (int j = 0; j < half; ++j) {
-                const double keep = hi ? x[j + half] : x[j], send = hi ? x[j] : x[j + half];
-                x[j] = keep + __shfl_xor(send, o);
-            }
-        }
-        x[0] += __shfl_xor(x[0], 1);
-        __syncthreads();
-        const int idx = (lane >> 1) & 31;
-        if ((lane & 1) == 0 && idx < K) red[idx * kPnNW + w] = x[0];
-    }
+    int idx;
+    bool wr;
+    const double x = wave_reduce_scatter<K>(v, lane, idx, wr);   // geom_dev.h: the same sums, fewer shuffles
+    __syncthreads();
+    if (wr) red[idx * kPnNW + w] = x;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < K; ++k) {   // the waves in order
