@@ -374,26 +374,32 @@ __device__ __forceinline__ void epnp_eig4_tri(int gl, double* G, const double (&
         emax2 = fmax(emax2, e[i] * e[i]);
         tn = fmax(tn, fabs(d[i]) + r);
     }
-    const double pivmin = 0x1p-1000 * fmax(1.0, emax2);
-    const double margin = 0x1p-50 * fmax(tn, 0x1p-1000) + 2.0 * pivmin;
-    lo -= margin;
-    hi += margin;
-    auto count = [&](double x) -> int {   // eigenvalues < x (Sturm sequence of the LDL^T pivots)
-        double q = d[0] - x;
-        int c = q < 0.0 ? 1 : 0;
+    // the counts run on T scaled by a power of two to |T| <= 1 (exact), where the leading minors
+    // p_i of T - x I (three-term recurrence, one FMA per step on the chain) cannot overflow:
+    // |p_i| <= 3^12; a cluster at x (the null pair) leaves |p_12| ~ 1e-32, far from underflow
+    (void)emax2;
+    const double sc = tn > 0.0 ? ldexp(1.0, -ilogb(tn) - 1) : 1.0;
+    double ds[12], es2[11];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) ds[i] = d[i] * sc;
+#pragma unroll
+    for (int i = 0; i < 11; ++i) es2[i] = (e[i] * sc) * (e[i] * sc);
+    const double margin = 0x1p-50;
+    auto count = [&](double x) -> int {   // eigenvalues < x: sign changes of 1, p_1, ..., p_12
+        double p0 = 1.0, p1 = ds[0] - x;
+        int c = p1 < 0.0 ? 1 : 0;
 #pragma unroll
         for (int i = 1; i < 12; ++i) {
-            if (fabs(q) < pivmin) q = -pivmin;
-            double r = __builtin_amdgcn_rcp(q);
-            r = fma(fma(-q, r, 1.0), r, r);
-            q = fma(-e[i - 1] * e[i - 1], r, d[i] - x);
-            c += q < 0.0 ? 1 : 0;
+            const double p2 = fma(ds[i] - x, p1, -es2[i - 1] * p0);
+            c += (p2 < 0.0) != (p1 < 0.0) ? 1 : 0;
+            p0 = p1;
+            p1 = p2;
         }
         return c;
     };
     // lanes k and k + 4 trisect together: counts at a + w and a + 2w, exchanged (3^30 ~ 2^47.5)
     const int kk = gl & 3;
-    double a = lo, b = hi;
+    double a = lo * sc - margin, b = hi * sc + margin;
     for (int it = 0; it < NB; ++it) {
         const double w = (b - a) * (1.0 / 3.0);
         const double m1 = a + w, m2 = a + 2.0 * w;
@@ -408,6 +414,8 @@ __device__ __forceinline__ void epnp_eig4_tri(int gl, double* G, const double (&
             a = m2;
         }
     }
+    a /= sc;
+    b /= sc;
     const double lam_own = 0.5 * (a + b);
     double lam[4];
 #pragma unroll
