@@ -45,6 +45,8 @@ __device__ __forceinline__ int max3i(int a, int b, int c) {
     asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+// (the min/max pattern instead of the asm selects v_med3_i32 too, but the compiler then reorders the
+// C3 loop badly: 434 vs 101 ms, C2 1.32 vs 1.27 ms; profiles/r5/ab/match_med3_ab_r5.txt)
 __device__ __forceinline__ int med3i(int a, int b, int c) {
     int r;
     asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
