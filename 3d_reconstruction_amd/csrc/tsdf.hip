@@ -38,7 +38,7 @@ namespace sfmhip {
 constexpr int kTsdfMaxFrames = 512;   // frames per integration step (host splits longer calls)
 constexpr int kTsdfQBits = 21;        // tsdf fixed point: |S| <= 512 (2^21 + 1) < 2^31
 static_assert(kTsdfMaxFrames * ((1 << kTsdfQBits) + 1) < INT_MAX, "S must fit an int32");
-constexpr double kTsdfLatencyRounds = 4.0;   // below: latency mode (tsdf_run)
+constexpr double kTsdfLatencyRounds = 1.0;   // below: latency mode (tsdf_run)
 constexpr int kTsdfTX = 8, kTsdfTY = 8, kTsdfTZ = 8;    // workgroup tile: 4 waves x (8 x, 2 y, 8 z)
 constexpr int kCullSub = 4;           // wave sub-tiles per tile
 
@@ -853,9 +853,10 @@ __global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, f
 // ---------------------------------------------------------------------------
 // Host.  Knob (read once, sfmhip_knobs_reload re-reads it: lib.hip):
 //   SFMHIP_TSDF_LATENCY  -1 auto (default), 0 whole-grid mode, 1 latency mode
-// Latency mode (few resident rounds of fusion waves: a z-slab of an N-way split): no
-// brick pre-pass, no refinement pass, no per-voxel block test (each costs more than it
-// saves when the call is bound by its longest waves: N = 8 slab 0.39 vs 0.44 ms, round 3).
+// Latency mode (less than one resident round of fusion waves): no brick pre-pass, no
+// refinement pass, no per-voxel block test.  Round 3's sequential fusion put an N = 8 z-slab
+// (two rounds) in it (0.39 vs 0.44 ms); with the order-free fusion the whole-grid mode is
+// faster there: slowest N = 8 slab 0.29-0.30 vs 0.31-0.35 ms (profiles/r5/tsdf_slabs_r5.txt).
 // stats != nullptr: run only the culling pre-passes and count (wave sub-tile, frame)
 // pairs: stats[0] tested, [1] culled, [2] free space (layer_stats: per 8-voxel z layer).
 // ext_table != nullptr: the caller's {min, max} block table of every frame over the
