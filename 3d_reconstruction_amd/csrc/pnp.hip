@@ -702,28 +702,29 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
         const double* L = G + gL;   // row r: L[10 r + c]
         const double* rho = G + gRho;
         double be[4] = {0, 0, 0, 0};
-        if (gl == 0) {
-            double A[6][4], b[6], x[4];
-            const int cs[4] = {0, 1, 3, 6};
-            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 4; ++c) A[r][c] = L[10 * r + cs[c]]; b[r] = rho[r]; }
-            lsq6<4>(A, b, x);
-            if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = -x[1] / be[0]; be[2] = -x[2] / be[0]; be[3] = -x[3] / be[0]; }
-            else { be[0] = sqrt(x[0]); be[1] = x[1] / be[0]; be[2] = x[2] / be[0]; be[3] = x[3] / be[0]; }
-        } else if (gl == 1) {
-            double A[6][3], b[6], x[3];
-            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 3; ++c) A[r][c] = L[10 * r + c]; b[r] = rho[r]; }
-            lsq6<3>(A, b, x);
-            if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0; }
-            else { be[0] = sqrt(x[0]); be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0; }
-            if (x[1] < 0) be[0] = -be[0];
-        } else {
-            double A[6][5], b[6], x[5];
-            for (int r = 0; r < 6; ++r) { for (int c = 0; c < 5; ++c) A[r][c] = L[10 * r + c]; b[r] = rho[r]; }
-            lsq6<5>(A, b, x);
-            if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0; }
-            else { be[0] = sqrt(x[0]); be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0; }
-            if (x[1] < 0) be[0] = -be[0];
-            be[2] = x[3] / be[0];
+        {   // one least-squares solve on all three lanes: each lane's columns of L, zero-padded to
+            // five (a zero column leaves the Householder steps of the others and x unchanged, so
+            // x is lsq6<4> / <3> / <5> of the lane's own system bit for bit)
+            double A[6][5], bb[6], x[5];
+            for (int r = 0; r < 6; ++r) {
+#pragma unroll
+                for (int c = 0; c < 5; ++c) {
+                    const int col = gl == 0 ? (c == 0 ? 0 : c == 1 ? 1 : c == 2 ? 3 : 6) : c;
+                    const bool use = gl == 0 ? c < 4 : gl == 1 ? c < 3 : true;
+                    A[r][c] = use ? L[10 * r + col] : 0.0;
+                }
+                bb[r] = rho[r];
+            }
+            lsq6<5>(A, bb, x);
+            if (gl == 0) {
+                if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = -x[1] / be[0]; be[2] = -x[2] / be[0]; be[3] = -x[3] / be[0]; }
+                else { be[0] = sqrt(x[0]); be[1] = x[1] / be[0]; be[2] = x[2] / be[0]; be[3] = x[3] / be[0]; }
+            } else {
+                if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0; }
+                else { be[0] = sqrt(x[0]); be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0; }
+                if (x[1] < 0) be[0] = -be[0];
+                if (gl == 2) be[2] = x[3] / be[0];
+            }
         }
         for (int it = 0; it < 5; ++it) {  // gauss_newton
             __asm__ volatile("" ::: "memory");   // L is re-read from LDS each step, not held in registers
