@@ -358,6 +358,7 @@ template <int NB, int NI>
 __device__ __forceinline__ void epnp_eig4_tri(int gl, double* G, const double (&d)[12], const double (&e)[12],
                                               const double (&z0)[12], const double (&z1)[12], int r0, int r1,
                                               bool h1) {
+    PPROF_INIT;
     // Q's rows wait in the reduced matrix's slots (A is consumed: d, e are in registers)
     const int r1s = h1 ? r1 : 12;
 #pragma unroll
@@ -417,72 +418,76 @@ __device__ __forceinline__ void epnp_eig4_tri(int gl, double* G, const double (&
     a /= sc;
     b /= sc;
     const double lam_own = 0.5 * (a + b);
-    double lam[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lam[k] = __shfl(lam_own, k, kPnGL);
+    PPROF(13);
     double* Y = G + gL;   // the four vectors of T (the reduction's scratch is free)
     const double tol = 0x1p-52 * fmax(tn, 0x1p-1000);
+    // lane k (and k + 4) iterates eigenvector k; the four run in lockstep and every step ends
+    // with modified Gram-Schmidt in order 0..3 through LDS (lane j publishes its normalised
+    // vector, the lanes after it remove that direction): the null pair of M^T M is a cluster
+    const double lk = lam_own;
+    // T - lambda I = P L U (U: diagonal u0 and two superdiagonals u1, u2)
+    double u0[12], u1[12], u2[12], lm[11];
+    bool sw[11];
+    double pd = d[0] - lk, p1 = e[0], p2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 11; ++i) {
+        const double nd = e[i], n1 = d[i + 1] - lk, n2 = i + 1 < 11 ? e[i + 1] : 0.0;
+        sw[i] = fabs(nd) > fabs(pd);
+        const double piv = sw[i] ? nd : (fabs(pd) < tol ? (pd < 0.0 ? -tol : tol) : pd);
+        const double num = sw[i] ? pd : nd;
+        const double m = num * rcp_nr(piv);
+        const double a1 = sw[i] ? n1 : p1, a2 = sw[i] ? n2 : p2;   // the pivot row's superdiagonals
+        const double b1 = sw[i] ? p1 : n1, b2 = sw[i] ? p2 : n2;   // the other row's
+        u0[i] = piv; u1[i] = a1; u2[i] = a2; lm[i] = m;
+        pd = b1 - m * a1; p1 = b2 - m * a2; p2 = 0.0;
+    }
+    u0[11] = fabs(pd) < tol ? (pd < 0.0 ? -tol : tol) : pd;
+    u1[11] = 0.0; u2[11] = 0.0; u2[10] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) u0[i] = rcp_nr(u0[i]);   // the solves multiply by 1 / u0
+    double y[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) y[i] = 1.0 / (1.0 + (double)((i * 7 + kk * 5) % 12));   // a generic start
 #pragma unroll 1
-    for (int k = 0; k < 4; ++k) {
-        const double lk = __shfl(lam_own, k, kPnGL);
-        // T - lambda I = P L U (U: diagonal u0 and two superdiagonals u1, u2)
-        double u0[12], u1[12], u2[12], lm[11];
-        bool sw[11];
-        double pd = d[0] - lk, p1 = e[0], p2 = 0.0;
+    for (int step = 0; step < NI; ++step) {
+        // solve (T - lambda I) x = y: the row operations, then U back-substitution
 #pragma unroll
         for (int i = 0; i < 11; ++i) {
-            const double nd = e[i], n1 = d[i + 1] - lk, n2 = i + 1 < 11 ? e[i + 1] : 0.0;
-            sw[i] = fabs(nd) > fabs(pd);
-            if (!sw[i]) {
-                const double piv = fabs(pd) < tol ? (pd < 0.0 ? -tol : tol) : pd;
-                const double m = nd * rcp_nr(piv);
-                u0[i] = piv; u1[i] = p1; u2[i] = p2; lm[i] = m;
-                pd = n1 - m * p1; p1 = n2 - m * p2; p2 = 0.0;
-            } else {
-                const double m = pd * rcp_nr(nd);
-                u0[i] = nd; u1[i] = n1; u2[i] = n2; lm[i] = m;
-                pd = p1 - m * n1; p1 = p2 - m * n2; p2 = 0.0;
-            }
+            const double t0 = y[i], t1 = y[i + 1];
+            y[i] = sw[i] ? t1 : t0;
+            y[i + 1] = (sw[i] ? t0 : t1) - lm[i] * y[i];
         }
-        u0[11] = fabs(pd) < tol ? (pd < 0.0 ? -tol : tol) : pd;
-        u1[11] = 0.0; u2[11] = 0.0; u2[10] = 0.0;
+        y[11] = y[11] * u0[11];
+        y[10] = (y[10] - u1[10] * y[11]) * u0[10];
 #pragma unroll
-        for (int i = 0; i < 12; ++i) u0[i] = rcp_nr(u0[i]);   // the solves multiply by 1 / u0
-        double y[12];
+        for (int i = 9; i >= 0; --i) y[i] = (y[i] - u1[i] * y[i + 1] - u2[i] * y[i + 2]) * u0[i];
 #pragma unroll
-        for (int i = 0; i < 12; ++i) y[i] = 1.0 / (1.0 + (double)((i * 7 + k * 5) % 12));   // a generic start
-#pragma unroll 1
-        for (int step = 0; step < NI; ++step) {
-            // solve (T - lambda I) x = y: the row operations, then U back-substitution
+        for (int j = 0; j < 4; ++j) {
+            if (kk == j) {   // publish vector j, normalised
+                double n2 = 0.0;
 #pragma unroll
-            for (int i = 0; i < 11; ++i) {
-                if (sw[i]) { const double t = y[i]; y[i] = y[i + 1]; y[i + 1] = t; }
-                y[i + 1] -= lm[i] * y[i];
+                for (int i = 0; i < 12; ++i) n2 = fma(y[i], y[i], n2);
+                const double inv = n2 > 0.0 ? rsq_nr(n2) : 0.0;
+#pragma unroll
+                for (int i = 0; i < 12; ++i) {
+                    y[i] *= inv;
+                    Y[12 * j + i] = y[i];
+                }
             }
-            y[11] = y[11] * u0[11];
-            y[10] = (y[10] - u1[10] * y[11]) * u0[10];
-#pragma unroll
-            for (int i = 9; i >= 0; --i) y[i] = (y[i] - u1[i] * y[i + 1] - u2[i] * y[i + 2]) * u0[i];
-            // against the earlier vectors (modified Gram-Schmidt), then to unit length
-            for (int j = 0; j < k; ++j) {
+            lds_fence();
+            if (kk > j) {   // remove direction j
                 double dt = 0.0;
 #pragma unroll
                 for (int i = 0; i < 12; ++i) dt = fma(y[i], Y[12 * j + i], dt);
 #pragma unroll
                 for (int i = 0; i < 12; ++i) y[i] = fma(-dt, Y[12 * j + i], y[i]);
             }
-            double n2 = 0.0;
-#pragma unroll
-            for (int i = 0; i < 12; ++i) n2 = fma(y[i], y[i], n2);
-            const double inv = n2 > 0.0 ? rsq_nr(n2) : 0.0;
-#pragma unroll
-            for (int i = 0; i < 12; ++i) y[i] *= inv;
         }
-        if (gl == 0)
-#pragma unroll
-            for (int i = 0; i < 12; ++i) Y[12 * k + i] = y[i];
-        lds_fence();
     }
+    double lam[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lam[k] = __shfl(lam_own, k, kPnGL);
+    PPROF(14);
     // V[:, k] = Q y_k (this lane's rows: read back, then overwritten by V's), the eigenvalues
     double q0[12], q1[12];
 #pragma unroll
@@ -507,6 +512,7 @@ __device__ __forceinline__ void epnp_eig4_tri(int gl, double* G, const double (&
         for (int i = 0; i < 12; ++i) G[gEv + i] = i < 4 ? lam[i] : INFINITY;
     }
     lds_fence();
+    PPROF(15);
 }
 
 // EPnP eigen-decomposition of M^T M (12x12, symmetric): Householder tridiagonalisation (EISPACK
@@ -528,23 +534,32 @@ __device__ __forceinline__ void epnp_eig(int gl, double* G) {
     // written after the QL): every load is unconditional (no branch and wait per element) and the
     // results of the sink row are masked by selects
     const int r1s = h1 ? r1 : 12;
+    PPROF_INIT;
     double z0[12], z1[12];   // rows r0 and r1 of Q
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
         z0[j] = j == r0 ? 1.0 : 0.0;
         z1[j] = j == r1 ? 1.0 : 0.0;
     }
+    // the lane's rows of A in registers (A is symmetric: the trailing block's columns are rows);
+    // only v and q go through LDS
+    double a0[12], a1[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        a0[j] = A[r0 * 12 + j];
+        a1[j] = h1 ? A[r1s * 12 + j] : 0.0;
+    }
     double d[12], e[12];
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
-        // x = A[k+1..11][k]; |x|^2 over the group
-        const double t0 = A[r0 * 12 + k], t1 = A[r1s * 12 + k];
-        const double a0 = r0 > k ? t0 : 0.0;
-        const double a1 = h1 && r1 > k ? t1 : 0.0;
-        double n2 = fma(a0, a0, a1 * a1);
+        // x = A[k+1..11][k]; |x|^2 over the group; x0 = A[k+1][k] from the owner of row k+1
+        const double t0 = a0[k], t1 = a1[k];
+        const double a0k = r0 > k ? t0 : 0.0;
+        const double a1k = h1 && r1 > k ? t1 : 0.0;
+        double n2 = fma(a0k, a0k, a1k * a1k);
+        const double x0 = __shfl(k + 1 < kPnGL ? t0 : t1, (k + 1) % kPnGL, kPnGL);
 #pragma unroll
         for (int o = kPnGL / 2; o > 0; o >>= 1) n2 += __shfl_xor(n2, o, kPnGL);
-        const double x0 = A[(k + 1) * 12 + k];
         const double s2 = n2 - x0 * x0;
         if (!(s2 > 1e-300 * n2) || !(n2 > 0.0)) {   // column already reduced (uniform in the group)
             e[k] = x0;
@@ -554,8 +569,8 @@ __device__ __forceinline__ void epnp_eig(int gl, double* G) {
         const double vk = x0 - alpha;
         const double beta = 2.0 * rcp_nr(fma(vk, vk, s2));
         e[k] = alpha;
-        const double v0 = r0 == k + 1 ? vk : a0;   // rows <= k: 0 (a0 = 0 there)
-        const double v1 = r1 == k + 1 ? vk : a1;
+        const double v0 = r0 == k + 1 ? vk : a0k;   // rows <= k: 0 (a0k = 0 there)
+        const double v1 = r1 == k + 1 ? vk : a1k;
         vv[r0] = v0;
         vv[r1s] = v1;
         lds_fence();
@@ -564,8 +579,8 @@ __device__ __forceinline__ void epnp_eig(int gl, double* G) {
 #pragma unroll
         for (int j = k + 1; j < 12; ++j) {
             const double vj = vv[j];
-            p0 = fma(A[r0 * 12 + j], vj, p0);
-            p1 = fma(A[r1s * 12 + j], vj, p1);
+            p0 = fma(a0[j], vj, p0);
+            p1 = fma(a1[j], vj, p1);
         }
         p0 = r0 > k ? beta * p0 : 0.0;
         p1 = h1 && r1 > k ? beta * p1 : 0.0;
@@ -582,9 +597,8 @@ __device__ __forceinline__ void epnp_eig(int gl, double* G) {
 #pragma unroll
         for (int j = k + 1; j < 12; ++j) {
             const double vj = vv[j], qj = qv[j];
-            const double x0j = A[r0 * 12 + j], x1j = A[r1s * 12 + j];
-            if (r0 > k) A[r0 * 12 + j] = x0j - fma(v0, qj, q0 * vj);
-            if (r1 > k) A[r1s * 12 + j] = x1j - fma(v1, qj, q1 * vj);
+            if (r0 > k) a0[j] = a0[j] - fma(v0, qj, q0 * vj);
+            if (r1 > k) a1[j] = a1[j] - fma(v1, qj, q1 * vj);
             w0 = fma(z0[j], vj, w0);
             w1 = fma(z1[j], vj, w1);
         }
@@ -598,10 +612,21 @@ __device__ __forceinline__ void epnp_eig(int gl, double* G) {
         }
         lds_fence();
     }
-    e[10] = A[11 * 12 + 10];
-    e[11] = 0.0;
+    // the diagonal and the last subdiagonal element through the v slots
+    double dg0 = 0.0, dg1 = 0.0;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) d[i] = A[i * 13];
+    for (int j = 0; j < 12; ++j) {
+        if (j == r0) dg0 = a0[j];
+        if (j == r1) dg1 = a1[j];
+    }
+    e[10] = __shfl(a1[10], 11 - kPnGL, kPnGL);
+    e[11] = 0.0;
+    vv[r0] = dg0;
+    vv[r1s] = dg1;
+    lds_fence();
+#pragma unroll
+    for (int i = 0; i < 12; ++i) d[i] = vv[i];
+    PPROF(12);
     epnp_eig4_tri<NB, NI>(gl, G, d, e, z0, z1, r0, r1, h1);
 }
 
@@ -620,25 +645,39 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
         dup[p] = D.uc - G[gUs + 2 * p];
         dvp[p] = D.vc - G[gUs + 2 * p + 1];
     }
-#pragma unroll 1
-    for (int t = 0; t < 144 / kPnGL; ++t) {
-        const int e = gl + kPnGL * t;
-        const int i = e / 12, j = e % 12;
-        const int ci = i / 3, ki = i % 3, cj = j / 3, kj = j % 3;
-        double acc = 0;
+    // M^T M = sum_p (a_p a_p^T) (x) S_p with S_p = [[fu^2, 0, fu du], [0, fv^2, fv dv],
+    // [fu du, fv dv, du^2 + dv^2]]: block (ci, cj) needs four sums over the points; lane gl forms
+    // blocks gl and gl + 8 of the ten with ci <= cj and writes them and their mirror images
+    double nn[5];
 #pragma unroll
-        for (int p = 0; p < 5; ++p) {
-            // M rows 2p (u) and 2p+1 (v): col 3c -> a*fu / 0, col 3c+1 -> 0 / a*fv, col 3c+2 -> a*(uc-u) / a*(vc-v)
-            const double ai = ci == 0 ? al[p][0] : ci == 1 ? al[p][1] : ci == 2 ? al[p][2] : al[p][3];
-            const double aj = cj == 0 ? al[p][0] : cj == 1 ? al[p][1] : cj == 2 ? al[p][2] : al[p][3];
-            const double du = dup[p], dv = dvp[p];
-            const double mu_i = ki == 0 ? ai * D.fu : ki == 1 ? 0.0 : ai * du;
-            const double mu_j = kj == 0 ? aj * D.fu : kj == 1 ? 0.0 : aj * du;
-            const double mv_i = ki == 0 ? 0.0 : ki == 1 ? ai * D.fv : ai * dv;
-            const double mv_j = kj == 0 ? 0.0 : kj == 1 ? aj * D.fv : aj * dv;
-            acc += mu_i * mu_j + mv_i * mv_j;
+    for (int p = 0; p < 5; ++p) nn[p] = dup[p] * dup[p] + dvp[p] * dvp[p];
+    const double fu2 = D.fu * D.fu, fv2 = D.fv * D.fv;
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+        const int bk = gl + kPnGL * rep;
+        if (bk < 10) {
+            const int ci = bk < 4 ? 0 : bk < 7 ? 1 : bk < 9 ? 2 : 3;
+            const int cj = bk < 4 ? bk : bk < 7 ? bk - 3 : bk < 9 ? bk - 5 : 3;
+            double W = 0.0, Wu = 0.0, Wv = 0.0, Wn = 0.0;
+#pragma unroll
+            for (int p = 0; p < 5; ++p) {
+                const double ai = ci == 0 ? al[p][0] : ci == 1 ? al[p][1] : ci == 2 ? al[p][2] : al[p][3];
+                const double aj = cj == 0 ? al[p][0] : cj == 1 ? al[p][1] : cj == 2 ? al[p][2] : al[p][3];
+                const double w = ai * aj;
+                W += w;
+                Wu += w * dup[p];
+                Wv += w * dvp[p];
+                Wn += w * nn[p];
+            }
+            const double blk[9] = {fu2 * W, 0.0, D.fu * Wu, 0.0, fv2 * W, D.fv * Wv, D.fu * Wu, D.fv * Wv, Wn};
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    G[gA + (3 * ci + r) * 12 + 3 * cj + c] = blk[3 * r + c];
+                    G[gA + (3 * cj + c) * 12 + 3 * ci + r] = blk[3 * r + c];
+                }
         }
-        G[gA + e] = acc;
     }
     lds_fence();
     PPROF(7);

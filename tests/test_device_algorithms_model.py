@@ -6,7 +6,8 @@ bit-for-bit against the oracle:
   are the same floating-point results (the claim behind "the same bits" in pnp.hip / ba.hip).
 * pnp.hip `epnp_eig4_tri`: the four smallest eigenpairs of the Householder tridiagonal by
   Sturm-count trisection (leading-minor recurrence on the power-of-two-scaled matrix) and inverse
-  iteration with partial pivoting and reorthogonalisation, restated step for step in numpy and
+  iteration with partial pivoting (the four vectors in lockstep, modified Gram-Schmidt after
+  every step), restated step for step in numpy and
   checked against LAPACK (numpy.linalg.eigh) on EPnP-like M^T M matrices.
 """
 import math
@@ -115,7 +116,7 @@ def _eig4_tri(d, e):
                 a = m2
         lams.append(0.5 * (a + b) / sc)
     tol = 2.0 ** -52 * max(tn, 2.0 ** -1000)
-    Y = []
+    facts, ys = [], []
     for k in range(4):
         lk = lams[k]
         u0, u1, u2, lm, sw = np.zeros(n), np.zeros(n), np.zeros(n), np.zeros(n - 1), np.zeros(n - 1, bool)
@@ -133,8 +134,14 @@ def _eig4_tri(d, e):
                 u0[i], u1[i], u2[i], lm[i] = nd, n1, n2, m
                 pd, p1, p2 = p1 - m * n1, p2 - m * n2, 0.0
         u0[n - 1] = (-tol if pd < 0 else tol) if abs(pd) < tol else pd
-        y = np.array([1.0 / (1.0 + ((i * 7 + k * 5) % 12)) for i in range(n)])
-        for _ in range(3):
+        facts.append((u0, u1, u2, lm, sw))
+        ys.append(np.array([1.0 / (1.0 + ((i * 7 + k * 5) % 12)) for i in range(n)]))
+    # the four iterations in lockstep (one lane each); every step ends with modified
+    # Gram-Schmidt in order 0..3 against the other lanes' current iterates
+    for _ in range(3):
+        for k in range(4):
+            u0, u1, u2, lm, sw = facts[k]
+            y = ys[k]
             for i in range(n - 1):
                 if sw[i]:
                     y[i], y[i + 1] = y[i + 1], y[i]
@@ -143,10 +150,11 @@ def _eig4_tri(d, e):
             y[n - 2] = (y[n - 2] - u1[n - 2] * y[n - 1]) / u0[n - 2]
             for i in range(n - 3, -1, -1):
                 y[i] = (y[i] - u1[i] * y[i + 1] - u2[i] * y[i + 2]) / u0[i]
-            for yj in Y:
-                y = y - (y @ yj) * yj
-            y = y / math.sqrt(y @ y)
-        Y.append(y)
+        for j in range(4):
+            ys[j] = ys[j] / math.sqrt(ys[j] @ ys[j])
+            for k in range(j + 1, 4):
+                ys[k] = ys[k] - (ys[k] @ ys[j]) * ys[j]
+    Y = ys
     return np.array(lams), np.array(Y).T
 
 

@@ -45,8 +45,8 @@ print("per-problem mean (us, wall clock 100 MHz):", {nm: round(buf[i] / P / 100,
 print("fractions:", {nm: round(buf[i] / max(tot, 1), 3) for i, nm in enumerate(names)})
 sub = ["load+prepare", "MtM", "Jacobi", "signs+L/rho", "betas+GN+R_t", "select+rodrigues_inv"]
 print("EPnP sub-phases of group 0 (us per problem):", {nm: round(buf[6 + i] / P / 100, 1) for i, nm in enumerate(sub)})
-print("Jacobi sweeps per problem (group 0):", buf[15] / P)
-print("Jacobi rounds: rotation / blocks (us per problem, group 0):", round(buf[13] / P / 100, 1), round(buf[14] / P / 100, 1))
+esub = ["householder", "trisection", "inverse iteration", "back-transform"]
+print("eig sub-phases of group 0 (us per problem):", {nm: round(buf[12 + i] / P / 100, 1) for i, nm in enumerate(esub)})
 wg = (ctypes.c_ulonglong * 2048)()
 sfm.lib.sfmhip_debug_pnp_wg(wg)
 w = np.array(wg[:2 * P], dtype=np.int64).reshape(P, 2)
