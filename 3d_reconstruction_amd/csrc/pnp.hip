@@ -76,9 +76,19 @@ __device__ int update_num_iters(double p, double ep, int m, int max_iters) {
 
 __device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
 
+// The Jacobi rotation's tangent t = sign(x) / (|x| + sqrt(1 + x^2)) by the Newton reciprocal and
+// square root; 0 for |x| > 1e150 (|t| < 1e-150, where 1 + x^2 overflows and the Newton forms
+// would give inf * 0) and for a NaN x (0 * rcp of an off-diagonal below the normal range: that
+// rotation is skipped)
+__device__ __forceinline__ double jacobi_tan(double x) {
+    const double t = (x >= 0 ? 1.0 : -1.0) * rcp_nr(fabs(x) + sqrt_nr(1.0 + x * x));
+    return fabs(x) <= 1e150 ? t : 0.0;
+}
+
 // Symmetric 3x3 eigen-decomposition by cyclic Jacobi: eigenvalues descending,
 // rows of E = eigenvectors with the largest-|.| component positive.
 __device__ void eig3_desc(double A[3][3], double w[3], double E[3][3]) {
+#pragma clang fp contract(fast)
     double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
     for (int sweep = 0; sweep < 30; ++sweep) {
         const double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
@@ -87,9 +97,9 @@ __device__ void eig3_desc(double A[3][3], double w[3], double E[3][3]) {
         for (int p = 0; p < 2; ++p)
             for (int q = p + 1; q < 3; ++q) {
                 if (A[p][q] == 0.0) continue;
-                const double tau = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
-                const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
-                const double c = 1.0 / sqrt(1.0 + t * t), s = t * c;
+                const double tau = (A[q][q] - A[p][p]) * rcp_nr(2.0 * A[p][q]);
+                const double t = jacobi_tan(tau);
+                const double c = rsq_nr(1.0 + t * t), s = t * c;
                 for (int k = 0; k < 3; ++k) {  // A <- A J (columns p, q)
                     const double ap = A[k][p], aq = A[k][q];
                     A[k][p] = c * ap - s * aq;
@@ -131,6 +141,7 @@ __device__ void eig3_desc(double A[3][3], double w[3], double E[3][3]) {
 
 // SVD of a 3x3 (row-major A) by one-sided Jacobi: A = U diag(s) V^T, s descending.
 __device__ __forceinline__ void svd3(const double* A, double U[3][3], double s[3], double V[3][3]) {
+#pragma clang fp contract(fast)
     double B[3][3];  // B[col][row]
     double W[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};  // W[col][row]
     for (int c = 0; c < 3; ++c)
@@ -145,11 +156,11 @@ __device__ __forceinline__ void svd3(const double* A, double U[3][3], double s[3
                     be += B[q][r] * B[q][r];
                     ga += B[p][r] * B[q][r];
                 }
-                if (ga == 0.0 || fabs(ga) <= 1e-15 * sqrt(al * be)) continue;
+                if (ga == 0.0 || fabs(ga) <= 1e-15 * sqrt_nr(al * be)) continue;
                 rot = true;
-                const double zeta = (be - al) / (2.0 * ga);
-                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+                const double zeta = (be - al) * rcp_nr(2.0 * ga);
+                const double t = jacobi_tan(zeta);
+                const double c = rsq_nr(1.0 + t * t), sn = c * t;
                 for (int r = 0; r < 3; ++r) {
                     const double bp = B[p][r], bq = B[q][r];
                     B[p][r] = c * bp - sn * bq;
@@ -162,7 +173,7 @@ __device__ __forceinline__ void svd3(const double* A, double U[3][3], double s[3
         if (!rot) break;
     }
     double sg[3];
-    for (int c = 0; c < 3; ++c) sg[c] = sqrt(B[c][0] * B[c][0] + B[c][1] * B[c][1] + B[c][2] * B[c][2]);
+    for (int c = 0; c < 3; ++c) sg[c] = sqrt_nr(B[c][0] * B[c][0] + B[c][1] * B[c][1] + B[c][2] * B[c][2]);
     // bubble sort (descending) of (sigma, B column, W column); static indices only
     auto cswap = [&](int j) {
         if (sg[j] < sg[j + 1]) {
@@ -179,9 +190,10 @@ __device__ __forceinline__ void svd3(const double* A, double U[3][3], double s[3
         for (int r = 0; r < 3; ++r) V[r][i] = W[i][r];
     }
     for (int i = 0; i < 2; ++i)
-        for (int r = 0; r < 3; ++r) U[r][i] = s[i] > 0 ? B[i][r] / s[i] : (r == i ? 1.0 : 0.0);
+        for (int r = 0; r < 3; ++r) U[r][i] = s[i] > 0 ? B[i][r] * rcp_nr(s[i]) : (r == i ? 1.0 : 0.0);
     if (s[2] > 1e-300 * s[0] && s[2] > 0) {
-        for (int r = 0; r < 3; ++r) U[r][2] = B[2][r] / s[2];
+        const double i2 = rcp_nr(s[2]);
+        for (int r = 0; r < 3; ++r) U[r][2] = B[2][r] * i2;
     } else {  // rank-deficient: complete the basis
         U[0][2] = U[1][0] * U[2][1] - U[2][0] * U[1][1];
         U[1][2] = U[2][0] * U[0][1] - U[0][0] * U[2][1];
@@ -192,6 +204,7 @@ __device__ __forceinline__ void svd3(const double* A, double U[3][3], double s[3
 // cv::Rodrigues matrix -> vector (calibration.cpp): R projected on SO(3) by
 // SVD, then the axis-angle with OpenCV's small-s branch.
 __device__ void rodrigues_inv(const double* Rin, double* rv) {
+#pragma clang fp contract(fast)
     double U[3][3], s[3], V[3][3], R[3][3];
     svd3(Rin, U, s, V);
     for (int i = 0; i < 3; ++i)
@@ -243,14 +256,22 @@ __device__ void rodrigues_jac(const double* rvec, double* J) {
     }
 }
 
+// EPnP (the sample solve: control points, M^T M, its eigenpairs, the betas, R and t) and the
+// 3x3 SVD / Rodrigues inverse contract a * b + c into FMAs (#pragma clang fp contract(fast)):
+// the library builds with -ffp-contract=off for the kernels whose operation order follows the
+// oracle bit for bit; EPnP agrees with it to a tolerance (its eigen-solver is its own), and the
+// scoring, the inlier masks and the LM keep the uncontracted order.
+//
 // Least squares min ||A x - b|| for a 6 x nc (nc <= 5) full-column-rank A by
-// Householder QR (row-major A, modified in place).
+// Householder QR (row-major A, modified in place); Newton reciprocals / square roots (the IEEE
+// division and square-root sequences were most of the EPnP beta phase's instructions).
 template <int NC>
 __device__ void lsq6(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
+#pragma clang fp contract(fast)
     for (int k = 0; k < NC; ++k) {
         double nrm = 0;
         for (int r = k; r < 6; ++r) nrm += A[r][k] * A[r][k];
-        nrm = sqrt(nrm);
+        nrm = sqrt_nr(nrm);
         if (nrm == 0.0) continue;
         const double alpha = A[k][k] >= 0 ? -nrm : nrm;
         double v[6];
@@ -259,7 +280,7 @@ __device__ void lsq6(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
         double vn = 0;
         for (int r = k; r < 6; ++r) vn += v[r] * v[r];
         if (vn == 0.0) continue;
-        const double beta = 2.0 / vn;
+        const double beta = 2.0 * rcp_nr(vn);
         for (int c = k; c < NC; ++c) {
             double s = 0;
             for (int r = k; r < 6; ++r) s += v[r] * A[r][c];
@@ -274,7 +295,7 @@ __device__ void lsq6(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
     for (int k = NC - 1; k >= 0; --k) {
         double s = b[k];
         for (int c = k + 1; c < NC; ++c) s -= A[k][c] * x[c];
-        x[k] = A[k][k] != 0.0 ? s / A[k][k] : 0.0;
+        x[k] = A[k][k] != 0.0 ? s * rcp_nr(A[k][k]) : 0.0;
     }
 }
 
@@ -285,6 +306,7 @@ struct EpnpData {   // the sample's points and alphas live in the group scratch 
 // compute_R_and_t for one beta vector (epnp.cpp); returns the mean reprojection error.
 __device__ __forceinline__ double epnp_R_t(const EpnpData& D, const double* G, const int* vi, const double* betas, double* R,
                            double* t) {
+#pragma clang fp contract(fast)
     double ccs[4][3] = {};
     for (int i = 0; i < 4; ++i) {
         const double* v = G + gV;  // eigenvector vi[i] = column vi[i] of V
@@ -320,10 +342,10 @@ __device__ __forceinline__ double epnp_R_t(const EpnpData& D, const double* G, c
         const double* pw = G + gPw + 3 * p;
         const double Xc = R[0] * pw[0] + R[1] * pw[1] + R[2] * pw[2] + t[0];
         const double Yc = R[3] * pw[0] + R[4] * pw[1] + R[5] * pw[2] + t[1];
-        const double iz = 1.0 / (R[6] * pw[0] + R[7] * pw[1] + R[8] * pw[2] + t[2]);
+        const double iz = rcp_nr(R[6] * pw[0] + R[7] * pw[1] + R[8] * pw[2] + t[2]);
         const double ue = D.uc + D.fu * Xc * iz, ve = D.vc + D.fv * Yc * iz;
         const double u0 = G[gUs + 2 * p], u1 = G[gUs + 2 * p + 1];
-        sum += sqrt((u0 - ue) * (u0 - ue) + (u1 - ve) * (u1 - ve));
+        sum += sqrt_nr((u0 - ue) * (u0 - ue) + (u1 - ve) * (u1 - ve));
     }
     return sum / 5;
 }
@@ -358,6 +380,7 @@ template <int NB, int NI>
 __device__ __forceinline__ void epnp_eig4_tri(int gl, double* G, const double (&d)[12], const double (&e)[12],
                                               const double (&z0)[12], const double (&z1)[12], int r0, int r1,
                                               bool h1) {
+#pragma clang fp contract(fast)
     PPROF_INIT;
     // Q's rows wait in the reduced matrix's slots (A is consumed: d, e are in registers)
     const int r1s = h1 ? r1 : 12;
@@ -525,6 +548,7 @@ __device__ __forceinline__ void epnp_eig4_tri(int gl, double* G, const double (&
 // Result: the eigenvalues in G[gEv], the eigenvectors as the columns of V (G[gV], over A).
 template <int NB, int NI>
 __device__ __forceinline__ void epnp_eig(int gl, double* G) {
+#pragma clang fp contract(fast)
     double* A = G + gA;
     double* vv = G + gL;        // 13 doubles (L is built later)
     double* qv = G + gL + 13;   // 13 doubles
@@ -633,6 +657,7 @@ __device__ __forceinline__ void epnp_eig(int gl, double* G) {
 // EPnP on 5 correspondences by a kPnGL-lane group; writes (rvec, tvec) to out[6].
 template <int NB, int NI>
 __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G, double* out) {
+#pragma clang fp contract(fast)
     PPROF_INIT;
     // M^T M (12x12) into A
     // (alphas and uc - u, vc - v were staged in G by prepare: a dynamic index into D would put
@@ -756,13 +781,14 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
             }
             lsq6<5>(A, bb, x);
             if (gl == 0) {
-                if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = -x[1] / be[0]; be[2] = -x[2] / be[0]; be[3] = -x[3] / be[0]; }
-                else { be[0] = sqrt(x[0]); be[1] = x[1] / be[0]; be[2] = x[2] / be[0]; be[3] = x[3] / be[0]; }
+                be[0] = sqrt_nr(fabs(x[0]));
+                const double ib = (x[0] < 0 ? -1.0 : 1.0) * rcp_nr(be[0]);
+                be[1] = x[1] * ib; be[2] = x[2] * ib; be[3] = x[3] * ib;
             } else {
-                if (x[0] < 0) { be[0] = sqrt(-x[0]); be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0; }
-                else { be[0] = sqrt(x[0]); be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0; }
+                be[0] = sqrt_nr(fabs(x[0]));
+                be[1] = (x[0] < 0 ? x[2] < 0 : x[2] > 0) ? sqrt_nr(fabs(x[2])) : 0.0;
                 if (x[1] < 0) be[0] = -be[0];
-                if (gl == 2) be[2] = x[3] / be[0];
+                if (gl == 2) be[2] = x[3] * rcp_nr(be[0]);
             }
         }
         for (int it = 0; it < 5; ++it) {  // gauss_newton
@@ -783,6 +809,7 @@ __device__ __forceinline__ void epnp_group(const EpnpData& D, int gl, double* G,
             for (int i = 0; i < 4; ++i) be[i] += x[i];
         }
         err = epnp_R_t(D, G, vi, be, R, t);
+        if (!(err <= INFINITY)) err = INFINITY;   // a degenerate sample (NaN from the Newton forms) loses
     }
     PPROF(10);
     // the solution with the least mean reprojection error (the first on ties), chosen within the group
@@ -852,6 +879,7 @@ __device__ __forceinline__ void pnp_load_sample(const float* __restrict__ f, con
 
 // EPnP control points and barycentric alphas (every lane of the group; lane 0 stages them in G).
 __device__ __forceinline__ void pnp_prepare(double* G, int gl) {
+#pragma clang fp contract(fast)
     const double* pw = G + gPw;
     double c0[3] = {0, 0, 0};
     for (int j = 0; j < 5; ++j)
