@@ -231,15 +231,41 @@ __device__ void rodrigues_inv(const double* Rin, double* rv) {
     rv[0] = rx * vth; rv[1] = ry * vth; rv[2] = rz * vth;
 }
 
-// cv::Rodrigues vector -> matrix Jacobian, J[i*9+k] = dR_k / dr_i.
+// The LM's R(r) (geom_dev.h rodrigues, the same formula) with one sincos, the Newton reciprocal
+// and FMAs: one thread forms it between two barriers every evaluation, so its instruction count is
+// on the refinement's critical path.  The inlier masks keep the IEEE rodrigues.
+__device__ __forceinline__ void rodrigues_lm(const double* rv, double* R) {
+#pragma clang fp contract(fast)
+    double rx = rv[0], ry = rv[1], rz = rv[2];
+    const double theta = sqrt_nr(rx * rx + ry * ry + rz * rz);
+    if (theta < 2.220446049250313e-16) {
+        R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
+        return;
+    }
+    double s, c;
+    sincos(theta, &s, &c);
+    const double c1 = 1.0 - c;
+    const double itheta = rcp_nr(theta);
+    rx = rx * itheta; ry = ry * itheta; rz = rz * itheta;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double rxm[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = (c * I[k] + c1 * rrt[k]) + s * rxm[k];
+}
+
+// cv::Rodrigues vector -> matrix Jacobian, J[i*9+k] = dR_k / dr_i (one sincos, FMAs).
 __device__ void rodrigues_jac(const double* rvec, double* J) {
+#pragma clang fp contract(fast)
     const double theta = sqrt(rvec[0] * rvec[0] + rvec[1] * rvec[1] + rvec[2] * rvec[2]);
     if (theta < kEps64) {
         for (int k = 0; k < 27; ++k) J[k] = 0;
         J[5] = -1; J[7] = 1; J[9 + 2] = 1; J[9 + 6] = -1; J[18 + 1] = -1; J[18 + 3] = 1;
         return;
     }
-    const double c = cos(theta), s = sin(theta), c1 = 1. - c, it = 1. / theta;
+    double s, c;
+    sincos(theta, &s, &c);
+    const double c1 = 1. - c, it = rcp_nr(theta);
     const double rx = rvec[0] * it, ry = rvec[1] * it, rz = rvec[2] * it;
     const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
     const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
@@ -354,11 +380,11 @@ __device__ __forceinline__ double epnp_R_t(const EpnpData& D, const double* G, c
 // compiled out otherwise.
 #ifdef SFMHIP_PNP_PROF
 __device__ unsigned long long g_pprof[16];
-__device__ unsigned long long g_wgt[2 * 1024];  // per-workgroup start / end
+__device__ unsigned long long g_wgt[4 * 1024];  // per workgroup: start, end, first chunk's EPnP end, RANSAC end
 #define PPROF(i) do { if (threadIdx.x == 0) { const unsigned long long t1_ = wall_clock64(); atomicAdd(&g_pprof[i], t1_ - pp_t); pp_t = t1_; } } while (0)
 #define PPROF_INIT unsigned long long pp_t = wall_clock64()
 #define PPROF_ADD(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_pprof[i], (unsigned long long)(v)); } while (0)
-#define PPROF_WG(k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_wgt[2 * blockIdx.x + (k)] = wall_clock64(); } while (0)
+#define PPROF_WG(k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_wgt[4 * blockIdx.x + (k)] = wall_clock64(); } while (0)
 #else
 #define PPROF(i) do {} while (0)
 #define PPROF_INIT do {} while (0)
@@ -838,8 +864,9 @@ __device__ __forceinline__ void project_f(const double* R, const double* t, doub
 }
 
 // K sums at once: the same per-value wave reduction and cross-wave order as block_sum
-// (the same bits), one barrier pair instead of K
-template <int K>
+// (the same bits), one barrier pair instead of K.  LAST_ONLY: waves other than wave 0 form only
+// the last sum (the LM's cost; J^T J and J^T e go to thread 0 alone)
+template <int K, bool LAST_ONLY = false>
 __device__ __forceinline__ void block_sum_n(double (&v)[K], double* red /* [K * kPnNW] */) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -851,6 +878,7 @@ __device__ __forceinline__ void block_sum_n(double (&v)[K], double* red /* [K * 
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < K; ++k) {   // the waves in order
+        if (LAST_ONLY && k < K - 1 && w != 0) continue;
         double a = red[k * kPnNW];
 #pragma unroll
         for (int u = 1; u < kPnNW; ++u) a += red[k * kPnNW + u];
@@ -927,6 +955,11 @@ __device__ __forceinline__ void pnp_prepare(double* G, int gl) {
     lds_fence();
 }
 
+// 10^k, k = -16..16 (the LM's damping factors)
+__constant__ double kPow10[33] = {1e-16, 1e-15, 1e-14, 1e-13, 1e-12, 1e-11, 1e-10, 1e-9, 1e-8, 1e-7, 1e-6,
+                                  1e-5,  1e-4,  1e-3,  1e-2,  1e-1,  1e0,   1e1,   1e2,  1e3,  1e4,  1e5,
+                                  1e6,   1e7,   1e8,   1e9,   1e10,  1e11,  1e12,  1e13, 1e14, 1e15, 1e16};
+
 // After the RANSAC loop (best model s_best, maxgood inliers, last hypothesis run): the inlier mask
 // of the best model, CvLevMarq on the inliers (cvProjectPoints2's analytic Jacobian, J^T J / J^T e
 // as fixed-order block reductions), the outputs.  Every thread of the kPnThreads workgroup.
@@ -973,7 +1006,7 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
     __syncthreads();
     PPROF(4);
     auto eval = [&](bool with_j, double* jtj, double* jte) -> double {
-        if (tid == 0) rodrigues(prm, Rm);
+        if (tid == 0) rodrigues_lm(prm, Rm);
         if (with_j && tid == 64) rodrigues_jac(prm, dR);   // another wave: the two run side by side
         __syncthreads();
         double acc[28];
@@ -1007,7 +1040,7 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
         }
         double e2 = 0;
         if (with_j) {   // all 28 sums behind one barrier pair
-            block_sum_n<28>(acc, s_red);
+            block_sum_n<28, true>(acc, s_red);
             for (int k = 0; k < 21; ++k) jtj[k] = acc[k];
             for (int k = 21; k < 27; ++k) jte[k - 21] = acc[k];
             e2 = acc[27];
@@ -1017,13 +1050,15 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
         return sqrt(e2);
     };
     // thread 0 solves (JtJ + lambda diag) x = JtErr; param = prev - x
+    // (one thread: FMAs, one Newton reciprocal per pivot, 10^lambda from a table)
     auto step = [&](const double* jtj, const double* jte, int lam) {
+#pragma clang fp contract(fast)
         if (tid == 0) {
             double A[6][7];
             int k = 0;
             for (int a = 0; a < 6; ++a)
                 for (int b = a; b < 6; ++b) { A[a][b] = jtj[k]; A[b][a] = jtj[k]; ++k; }
-            const double l = exp(lam * log(10.0));
+            const double l = kPow10[lam + 16];
             for (int a = 0; a < 6; ++a) { A[a][a] *= 1.0 + l; A[a][6] = jte[a]; }
 #pragma unroll
             for (int c = 0; c < 6; ++c) {  // Gaussian elimination, partial pivoting (static indices)
@@ -1038,9 +1073,10 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
 #pragma unroll
                         for (int j = 0; j < 7; ++j) { const double t = A[c][j]; A[c][j] = A[r][j]; A[r][j] = t; }
                 if (A[c][c] == 0.0) continue;
+                const double ip = rcp_nr(A[c][c]);
 #pragma unroll
                 for (int r = c + 1; r < 6; ++r) {
-                    const double fct = A[r][c] / A[c][c];
+                    const double fct = A[r][c] * ip;
 #pragma unroll
                     for (int j = c; j < 7; ++j) A[r][j] -= fct * A[c][j];
                 }
@@ -1049,7 +1085,7 @@ __device__ __forceinline__ void pnp_refine(int p, int n, int64_t off, const floa
             for (int r = 5; r >= 0; --r) {
                 double s = A[r][6];
                 for (int j = r + 1; j < 6; ++j) s -= A[r][j] * x[j];
-                x[r] = A[r][r] != 0.0 ? s / A[r][r] : 0.0;
+                x[r] = A[r][r] != 0.0 ? s * rcp_nr(A[r][r]) : 0.0;
             }
             for (int a = 0; a < 6; ++a) prm[a] = prev[a] - x[a];
         }
@@ -1170,6 +1206,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         }
         __syncthreads();
         PPROF(1);
+        if (k0 == 0) PPROF_WG(2);
         // scoring and replay in two halves of the chunk: the replay of the first half usually
         // lowers niters below the second (OpenCV's ~25 iterations), whose scoring is then skipped
         for (int hb = 0; hb < kPnH; hb += kPnH / 2) {
@@ -1222,6 +1259,7 @@ __global__ __launch_bounds__(kPnThreads) void pnp_ransac_kernel(
         if (s_k0 >= s_niters) break;
     }
     PPROF(3);
+    PPROF_WG(3);
     // the EPnP group scratch is free now: the LM stages the points there
     pnp_refine(p, n, off, f, fx, fy, cx, cy, thr, s_maxgood, s_last, s_best, s_lm, s_red, mask, rvec_out,
                tvec_out, ninl_out, iters_out, ok_out, reinterpret_cast<float*>(s_grp), kPnStageCap);
@@ -1243,8 +1281,8 @@ extern "C" int sfmhip_debug_pnp_prof(unsigned long long* out) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(sfmhip::g_pprof), z, sizeof(z)) != hipSuccess) return -2;
     return 0;
 }
-extern "C" int sfmhip_debug_pnp_wg(unsigned long long* out /* [2 * 1024] */) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfmhip::g_wgt), sizeof(unsigned long long) * 2048) == hipSuccess ? 0 : -2;
+extern "C" int sfmhip_debug_pnp_wg(unsigned long long* out /* [4 * 1024] */) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfmhip::g_wgt), sizeof(unsigned long long) * 4096) == hipSuccess ? 0 : -2;
 }
 #endif
 

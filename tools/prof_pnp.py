@@ -47,14 +47,21 @@ sub = ["load+prepare", "MtM", "Jacobi", "signs+L/rho", "betas+GN+R_t", "select+r
 print("EPnP sub-phases of group 0 (us per problem):", {nm: round(buf[6 + i] / P / 100, 1) for i, nm in enumerate(sub)})
 esub = ["householder", "trisection", "inverse iteration", "back-transform"]
 print("eig sub-phases of group 0 (us per problem):", {nm: round(buf[12 + i] / P / 100, 1) for i, nm in enumerate(esub)})
-wg = (ctypes.c_ulonglong * 2048)()
+wg = (ctypes.c_ulonglong * 4096)()
 sfm.lib.sfmhip_debug_pnp_wg(wg)
-w = np.array(wg[:2 * P], dtype=np.int64).reshape(P, 2)
+w = np.array(wg[:4 * P], dtype=np.int64).reshape(P, 4)
 st = (w[:, 0] - w[:, 0].min()) / 100.0
 dur = (w[:, 1] - w[:, 0]) / 100.0
 print("workgroup start offsets (us): min/median/max", st.min(), np.median(st), st.max(), " n started > 50 us late:", int((st > 50).sum()))
 print("workgroup durations (us): min/median/mean/max", dur.min(), np.median(dur), dur.mean().round(1), dur.max())
 print("span first start -> last end (us):", (w[:, 1].max() - w[:, 0].min()) / 100.0)
 it = r["iters"].cpu().numpy()
-print("slowest 5 problems (us, iters):", [(round(float(dur[i]), 1), int(it[i])) for i in np.argsort(dur)[-5:]])
+ep = (w[:, 2] - w[:, 0]) / 100.0
+rs = (w[:, 3] - w[:, 2]) / 100.0
+lm = (w[:, 1] - w[:, 3]) / 100.0
+print("per workgroup (us) mean / max: to first EPnP end %.1f / %.1f, rest of RANSAC %.1f / %.1f, LM %.1f / %.1f" % (
+    ep.mean(), ep.max(), rs.mean(), rs.max(), lm.mean(), lm.max()))
+print("slowest 8 problems (total, to EPnP end, RANSAC rest, LM us; iters):")
+for i in np.argsort(dur)[-8:]:
+    print("  %.1f  %.1f  %.1f  %.1f  %d" % (dur[i], ep[i], rs[i], lm[i], it[i]))
 print("mean ransac iters", r["iters"].float().mean().item())
