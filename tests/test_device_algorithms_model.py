@@ -191,3 +191,101 @@ def test_eig4_tridiagonal_matches_lapack():
         for k in (2, 3):
             if w[k + 1] - w[k] > 1e-6 * scale and w[k] - w[k - 1] > 1e-6 * scale:
                 assert min(np.linalg.norm(V[:, k] - U[:, k]), np.linalg.norm(V[:, k] + U[:, k])) <= 1e-6
+
+
+# ---------------------------------------------------------------------------------------------
+# pnp.hip pnp_sample_chunk: cv::RNG's multiply-with-carry step s' = A lo(s) + hi(s) is
+# s' = s b^-1 mod m (b = 2^32, m = A b - 1, b^-1 = A), so the state 5 L draws ahead is
+# s A^(5 L) mod m, formed on the device as mwc_red^3(s C_L) with C_L = A^(5 L - 3) mod m
+# (mwc_red(T) = (T >> 32) + lo32(T) A = T b^-1 mod m).  The wave's 64 lanes each draw one
+# sample from their jumped state; the first lane whose five draws repeat an index redraws one at
+# a time (cv_rng_sample5) and the lanes after it restart from its final state.
+
+_A = 4164903690
+_M = _A * (1 << 32) - 1
+
+
+def _mwc(s):
+    return (s & 0xFFFFFFFF) * _A + (s >> 32)
+
+
+def _rng_mod(x, n):
+    mg = (1 << 32) // n
+    r = x - ((x * mg) >> 32) * n
+    return r - n if r >= n else r
+
+
+def _sample5(s, n):
+    """geom_dev.h cv_rng_sample5 restated: (state after, five indices)"""
+    d = []
+    while len(d) < 5:
+        s = _mwc(s)
+        idx = _rng_mod(s & 0xFFFFFFFF, n)
+        if idx not in d:
+            d.append(idx)
+    return s, d
+
+
+def _mulred3(s, c):
+    t = s * c
+    for _ in range(3):
+        t = (t >> 32) + (t & 0xFFFFFFFF) * _A
+    assert t < 2 * _M
+    return t - _M if t >= _M else t
+
+
+def _jump_table():
+    import re
+    from pathlib import Path
+    src = (Path(__file__).resolve().parent.parent / "3d_reconstruction_amd" / "csrc" / "pnp.hip").read_text()
+    body = src[src.index("kMwcJump5[64] = {"):]
+    body = body[:body.index("};")]
+    return [int(v, 16) for v in re.findall(r"0x([0-9a-f]+)ULL", body)]
+
+
+def _parallel_chunk(rs, n, nh, C):
+    out = [None] * nh
+    base, b0 = rs, 0
+    while True:
+        starts, draws, dups = {}, {}, []
+        for lane in range(b0, nh):
+            L = lane - b0
+            st = base if L == 0 else _mulred3(base, C[L])
+            sv, d = st, []
+            for _ in range(5):
+                sv = _mwc(sv)
+                d.append(_rng_mod(sv & 0xFFFFFFFF, n))
+            starts[lane], draws[lane] = st, (sv, d)
+            if len(set(d)) < 5:
+                dups.append(lane)
+        hs = dups[0] if dups else nh
+        for lane in range(b0, hs):
+            out[lane] = draws[lane][1]
+        if hs >= nh:
+            return draws[nh - 1][0], out
+        s2, d2 = _sample5(starts[hs], n)
+        out[hs] = d2
+        base, b0 = s2, hs + 1
+        if b0 >= nh:
+            return base, out
+
+
+def test_mwc_jump_sampler_matches_serial():
+    C = _jump_table()
+    assert len(C) == 64
+    for L in range(1, 64):
+        assert C[L] == pow(_A, 5 * L - 3, _M)
+    # one step from any state is s * A mod m (the seed ~0 is >= m: its successor is not reduced)
+    rs = (1 << 64) - 1
+    assert _mwc(rs) % _M == rs * _A % _M
+    for n in (6, 7, 9, 40, 300, 2000):
+        s_ser = s_par = (1 << 64) - 1
+        for chunk in range(4):
+            nh = 64 if chunk < 3 else 23
+            ser = []
+            for _ in range(nh):
+                s_ser, d = _sample5(s_ser, n)
+                ser.append(d)
+            s_par, par = _parallel_chunk(s_par, n, nh, C)
+            assert par == ser, (n, chunk)
+            assert s_par == s_ser, (n, chunk)
