@@ -1,14 +1,16 @@
-"""CPU models of two device algorithms whose correctness arguments are numerical, not
-bit-for-bit against the oracle:
+"""CPU models of three device algorithms whose correctness arguments are numerical or
+number-theoretic rather than bit-for-bit against the oracle:
 
 * geom_dev.h `wave_reduce_scatter`: the reduce-scatter form of the wave sums adds every value
   along the same pairwise tree as the plain xor butterfly (offset 32 first), so the per-value sums
   are the same floating-point results (the claim behind "the same bits" in pnp.hip / ba.hip).
 * pnp.hip `epnp_eig4_tri`: the four smallest eigenpairs of the Householder tridiagonal by
-  Sturm-count trisection (leading-minor recurrence on the power-of-two-scaled matrix) and inverse
-  iteration with partial pivoting (the four vectors in lockstep, modified Gram-Schmidt after
-  every step), restated step for step in numpy and
-  checked against LAPACK (numpy.linalg.eigh) on EPnP-like M^T M matrices.
+  Sturm-count trisection (leading-minor recurrence on the power-of-two-scaled
+  matrix) and inverse iteration with partial pivoting (the four vectors in lockstep, modified
+  Gram-Schmidt after every step), restated step for step in numpy and checked against LAPACK
+  (numpy.linalg.eigh) on EPnP-like M^T M matrices.
+* pnp.hip `pnp_sample_chunk`: cv::RNG jump-ahead; the wave-parallel sampler gives the serial
+  cv_rng_sample5 sequence and final state exactly.
 """
 import math
 
