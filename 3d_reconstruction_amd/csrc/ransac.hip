@@ -95,12 +95,14 @@ constexpr int kQL[10][4] = {{0, 2, 4, 5},    {2, 3, 8, 9},     {4, 8, 10, 11},  
                             {3, 1, 6, 7},    {8, 6, 13, 14},   {9, 7, 14, 15},   {10, 13, 16, 17},
                             {11, 14, 17, 18}, {12, 15, 18, 19}};
 __device__ __forceinline__ void mul_ll(const double* a, const double* b, double sgn, double* q) {
+#pragma clang fp contract(fast)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) q[kLL[i][j]] += sgn * (a[i] * b[j]);
 }
 __device__ __forceinline__ void mul_ql(const double* q, const double* l, double sgn, double* c) {
+#pragma clang fp contract(fast)
 #pragma unroll
     for (int i = 0; i < 10; ++i)
 #pragma unroll
@@ -109,6 +111,7 @@ __device__ __forceinline__ void mul_ql(const double* q, const double* l, double 
 
 template <int NA, int NB>
 __device__ __forceinline__ void pmul(const double* a, const double* b, double* o) {
+#pragma clang fp contract(fast)
 #pragma unroll
     for (int i = 0; i < NA + NB - 1; ++i) o[i] = 0.0;
 #pragma unroll
@@ -140,6 +143,7 @@ __device__ unsigned long long g_rprof[16];
 // lane in group, gsh = bit offset of the group in the wave's ballot).  G is
 // the group's LDS area; up to 10 unit-norm E (row-major) go to models.
 __device__ int five_point_group(const double (&q)[5][4], int gl, int gsh, double* G, double* models) {
+#pragma clang fp contract(fast)
     SPROF_INIT;
     // 1. orthonormal null-space basis of the 5x9 system (Householder QR of
     //    Q^T, reflectors stored in place; every lane computes it in registers).
@@ -156,13 +160,13 @@ __device__ int five_point_group(const double (&q)[5][4], int gl, int gsh, double
         double nrm2 = 0;
 #pragma unroll
         for (int r = k; r < 9; ++r) nrm2 += A[r][k] * A[r][k];
-        const double nrm = sqrt(nrm2);
+        const double nrm = sqrt_nr(nrm2);
         const double alpha = (A[k][k] >= 0) ? -nrm : nrm;
         A[k][k] -= alpha;  // column k below the diagonal is now the reflector v_k
         double vn2 = 0;
 #pragma unroll
         for (int r = k; r < 9; ++r) vn2 += A[r][k] * A[r][k];
-        beta[k] = (vn2 > 0) ? 2.0 / vn2 : 0.0;
+        beta[k] = (vn2 > 0) ? 2.0 * rcp_nr(vn2) : 0.0;
 #pragma unroll
         for (int c = k + 1; c < 5; ++c) {
             double s = 0;
@@ -279,7 +283,7 @@ __device__ int five_point_group(const double (&q)[5][4], int gl, int gsh, double
 #pragma unroll
         for (int r = 0; r < 10; ++r) f[r] = __shfl(col[r], k, kGL);
         if (fabs(f[k]) < 100 * kDblEps) return 0;
-        const double inv = 1.0 / f[k];
+        const double inv = rcp_nr(f[k]);
         const double xk = col[k] * inv, xk2 = col2[k] * inv;
 #pragma unroll
         for (int r = 0; r < 10; ++r) {
