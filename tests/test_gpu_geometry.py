@@ -176,3 +176,36 @@ def test_sfm_triangulate_wrapper_vs_reference(sfm, gpu, solver):
     np.testing.assert_allclose(pts[ok], g["points"][ok], rtol=1e-5, atol=1e-6)
     cols = np.array([c if c is not None else np.full(3, -1) for c in all_point3ds[1]]).astype(np.int64)
     assert np.array_equal(cols, g["point_colors"])
+
+
+def test_dlt_residual_jacobian_full_bench_batch(sfm, gpu):
+    """The bench's C3 BA batch itself (syn.ba_scene(256, 4096, seed=4), the inputs bench.py times):
+    every pair's DLT points, residuals and FD Jacobian against the oracle, and the unit null
+    vectors with w >= 0."""
+    P_, N_ = 256, 4096
+    s = syn.ba_scene(P_, N_, seed=4)
+    dv = gpu
+    X4 = sfm.triangulate_batched(torch.from_numpy(s["P"]).to(dv), torch.from_numpy(s["pair_of_obs"]).to(dv),
+                                 torch.from_numpy(s["x0"]).to(dv), torch.from_numpy(s["x1"]).to(dv)).cpu().numpy()
+    assert X4.shape == (4, P_ * N_)
+    np.testing.assert_allclose(np.linalg.norm(X4, axis=0), 1.0, rtol=1e-12)
+    assert (X4[3] >= 0).all()
+    worst = 0.0
+    for p in range(P_):
+        sl = slice(p * N_, (p + 1) * N_)
+        ref = og.triangulate_points(s["P"][p, 0], s["P"][p, 1], s["x0"][:, sl], s["x1"][:, sl])
+        Xg, Xr = (X4[:3, sl] / X4[3, sl]).T, (ref[:3] / ref[3]).T
+        np.testing.assert_allclose(Xg, Xr, rtol=1e-4, atol=0)
+        worst = max(worst, float(np.abs(Xg - Xr).max() / np.abs(Xr).max()))
+    assert worst < 1e-8
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dv) for k, v in s.items()}
+    r, jv = sfm.residual_jacobian_batched(t["cam"], t["K"], t["X"], t["pts2d"], t["pair_of_obs"])
+    r, jv = r.cpu().numpy(), jv.cpu().numpy()
+    assert np.isfinite(r).all() and np.isfinite(jv).all()
+    for p in range(P_):
+        sl = slice(p * N_, (p + 1) * N_)
+        x = _x_of(s, p, N_)
+        np.testing.assert_allclose(r[sl].ravel(), og.reprojection_error(x, s["K"][p], s["pts2d"][sl]), rtol=1e-12,
+                                   atol=1e-9)
+        np.testing.assert_allclose(jv[sl], og.fd_jacobian_direct(x, s["K"][p], s["pts2d"][sl]), rtol=1e-6,
+                                   atol=JAC_ATOL)
