@@ -43,11 +43,13 @@ __device__ unsigned long long g_ba_prof[4096 * kProfPhases];
     } while (0)
 #endif
 
-// per observation: J (18: u row, v row; the point block stored scaled, J_p d), f (2), the point's
-// column scales d = 1 / scale_inv (3), X_new (3), scale_inv (3: the column norms, max'ed across
-// Jacobian evaluations); d is stored so that no pass divides (the same IEEE quotient once per
-// Jacobian instead of once per pass) — only the trial pass reads it alone
-constexpr int kRec = 29;
+// per observation: J (18: u row, v row; the point block stored scaled, J_p d with the point's
+// column scales d = 1 / scale_inv), f (2), X_new (3), scale_inv (3: the column norms, max'ed
+// across Jacobian evaluations).  d itself is not stored: the trial pass, the one pass that needs
+// it alone, forms the same IEEE quotient 1 / scale_inv again (round 5: 29 -> 26 fields, the
+// records of all 256 C3 pairs 243 -> 218 MB)
+constexpr int kRec = 26;
+constexpr int kFX = 20, kFS = 23;   // X_new, scale_inv
 
 // sum of K doubles over the workgroup (NW waves); every thread receives the totals in out[]
 template <int NW, int K>
@@ -240,11 +242,14 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     double* Xp = X + 3 * o0;
     const double* pts = pts2d + 2 * o0;
     const Recs rec{scratch + (size_t)o0 * kRec, n};
-    // the pass view of observation i: r[0..17] J, r[18..19] f, r[20..22] the point column scales d
-    // the records hold the point block of J already scaled, Pp = J_p d (fields 6-8, 15-17): the
-    // passes that do not need d alone read 20 fields instead of 23 (round 5: 1.33 -> 1.27 ms)
+    // the pass view of observation i: r[0..17] J, r[18..19] f; the records hold the point block
+    // of J already scaled, Pp = J_p d (fields 6-8, 15-17), so the passes read 20 fields
+    // (round 5: 1.33 -> 1.27 ms); the trial pass adds scale_inv (its d = 1 / scale_inv)
     auto pass_rec = [&](int i, double* r) { rec.template load<0, 20>(i, r); };
-    auto pass_rec_d = [&](int i, double* r) { rec.template load<0, 23>(i, r); };
+    auto pass_rec_d = [&](int i, double* r) {
+        rec.template load<0, 20>(i, r);
+        rec.template load<kFS, kFS + 3>(i, r);
+    };
     if (tid < 6) S.cam[tid] = cam_io[(size_t)p * 6 + tid];
     __syncthreads();
     if (n == 0) {
@@ -272,12 +277,12 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             double r[kRec];
             double f[2], Xi[3];
             if (moved) {
-                rec.template load<23, 26>(i, r);
-                for (int c = 0; c < 3; ++c) { Xi[c] = r[23 + c]; Xp[3 * i + c] = Xi[c]; }
+                rec.template load<kFX, kFX + 3>(i, r);
+                for (int c = 0; c < 3; ++c) { Xi[c] = r[kFX + c]; Xp[3 * i + c] = Xi[c]; }
             } else {
                 for (int c = 0; c < 3; ++c) Xi[c] = Xp[3 * i + c];
             }
-            if (!first) rec.template load<26, 29>(i, r);
+            if (!first) rec.template load<kFS, kFS + 3>(i, r);
             fd_obs(&S.R[0][0], S.cam, k, Xi, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
             r[18] = f[0];
             r[19] = f[1];
@@ -293,14 +298,14 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 gmax = fmax(gmax, fabs(gp));
                 double si = sqrt(r[6 + c] * r[6 + c] + r[15 + c] * r[15 + c]);
                 if (first) si = si == 0.0 ? 1.0 : si;
-                else si = fmax(si, r[26 + c]);
-                r[26 + c] = si;
-                r[20 + c] = 1.0 / si;
-                r[6 + c] = r[6 + c] * r[20 + c];   // Pp
-                r[15 + c] = r[15 + c] * r[20 + c];
+                else si = fmax(si, r[kFS + c]);
+                r[kFS + c] = si;
+                const double d = 1.0 / si;
+                r[6 + c] = r[6 + c] * d;   // Pp
+                r[15 + c] = r[15 + c] * d;
             }
-            rec.template store<0, 23>(i, r);
-            rec.template store<26, 29>(i, r);
+            rec.template store<0, 20>(i, r);
+            rec.template store<kFS, kFS + 3>(i, r);
         }
         gmax = block_max<NW>(gmax, S.red);
         block_sum<NW, 13>(acc, S.red, S.tot);
@@ -325,8 +330,8 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         double acc[1] = {0.0};
         for (int i = tid; i < n; i += NT) {
             double r[kRec];
-            rec.template load<26, 29>(i, r);
-            for (int c = 0; c < 3; ++c) { const double t = Xp[3 * i + c] * r[26 + c]; acc[0] += t * t; }
+            rec.template load<kFS, kFS + 3>(i, r);
+            for (int c = 0; c < 3; ++c) { const double t = Xp[3 * i + c] * r[kFS + c]; acc[0] += t * t; }
         }
         block_sum<NW, 1>(acc, S.red, S.tot);
         if (tid == 0) {
@@ -576,7 +581,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 for (int c = 0; c < 6; ++c) { ju += r[c] * S.dc[c] * S.shc[c]; jv += r[9 + c] * S.dc[c] * S.shc[c]; }
                 double Xn[3];
                 for (int c = 0; c < 3; ++c) {
-                    const double d = r[20 + c];
+                    const double d = 1.0 / r[kFS + c];   // the Jacobian pass's quotient
                     const double sh = S.pS[0] * s1[c] + S.pS[1] * (s2[c] / s2n);
                     ju += r[6 + c] * sh;
                     jv += r[15 + c] * sh;
@@ -587,9 +592,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                     const double x = Xp[3 * i + c];
                     acc[5] += x * x;
                     Xn[c] = x + st;
-                    r[23 + c] = Xn[c];
+                    r[kFX + c] = Xn[c];
                 }
-                rec.template store<23, 26>(i, r);
+                rec.template store<kFX, kFX + 3>(i, r);
                 acc[0] += ju * ju + jv * jv;
                 double ru, rv;
                 resid(S.Rn, S.cam_new, k, Xn, pts + 2 * i, ru, rv);
