@@ -262,7 +262,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
 #endif
 
     // J, f at the current point; scale_inv (max with the old unless first); gc, cost, |g|_inf.
-    // moved: the point is the accepted trial point, read from the records (fields 23-25)
+    // moved: the point is the accepted trial point, read from the records (X_new fields)
     // and written to X here (no separate pass to move X)
     auto jacobian = [&](bool first, bool moved) {
         if (tid < 4) {   // R(rvec) and the three perturbed rotations of the FD
