@@ -776,6 +776,9 @@ __global__ __launch_bounds__(kVqhWaves * 64) void vq_f16s_kernel(const double* _
                 take(g, cn1 - 2.f * (m1[g] + c1[g]), j0 + 16);
             }
         }
+        // the filter's bound for row r16 (every lane group holds |x|^2 of its row r16): formed once
+        // per lane, then fetched for the lane's four C rows 4 kq + g
+        const double eps_row = vq_eps16(DP, sqrt(xn), cmax);
         int win[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -790,8 +793,7 @@ __global__ __launch_bounds__(kVqhWaves * 64) void vq_f16s_kernel(const double* _
                 v1 = t ? o1 : v1;
                 x1 = t ? ox : x1;
             }
-            const double xr = __shfl(xn, 4 * kq + g);   // lane 4kq+g holds |x|^2 of that row
-            const double eps = vq_eps16(DP, sqrt(xr), cmax);
+            const double eps = __shfl(eps_row, 4 * kq + g);   // lane 4kq+g: row 4kq+g's bound
             win[g] = PROBE == 4 ? (4 * kq + g) % n_codes : ((double)v2 - (double)v1 > 2.0 * eps) ? x1 : -1;
         }
         int w = -1;   // row r16's verdict: group r16 >> 2, entry r16 & 3
