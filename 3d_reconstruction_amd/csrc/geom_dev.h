@@ -581,4 +581,90 @@ __device__ __forceinline__ void cv_rng_sample5(uint64_t& s, unsigned n, unsigned
     s = sv;
 }
 
+// cv::RNG jump-ahead.  The multiply-with-carry step s' = A lo(s) + hi(s) is s' = s b^-1 mod m
+// (b = 2^32, m = A b - 1, b^-1 = A mod m) for every state, so the state 5 L draws ahead of s is
+// s A^(5 L) mod m: mwc_jump5 forms it as red^3(s C_L) with C_L = A^(5 L - 3) mod m and
+// red(T) = (T >> 32) + lo32(T) A = T b^-1 mod m (T < 2^128 -> < 2^96 + 2^64 -> < 2^65 + 2^32 ->
+// < 2^64 + 2^33 < 2 m: one conditional subtraction).  Every state after the first draw is below
+// m (only the seed ~0 is not, and its lane draws from it directly), so the reduced state is the
+// state itself.  C_L: tests/test_device_algorithms_model.py checks the table and the sampler.
+static __constant__ uint64_t kMwcJump5[64] = {
+    0x0000000000000000ULL, 0xf0badf95453cbc64ULL, 0x5ba03b6718928580ULL, 0xd1d2d0db8d934886ULL,
+    0xe69a527185f4f056ULL, 0xc02e3eee453a4663ULL, 0x636eb442dcc2d6eaULL, 0x6cbe3044aad17ec3ULL,
+    0x0b3deacb73698228ULL, 0x4ed646868fe1c5fbULL, 0x67b91866a3348f12ULL, 0xbdfe19229db55884ULL,
+    0x8b1de00fc853e701ULL, 0x964bfc7907213ec9ULL, 0xa18b02d7c6b8c7a8ULL, 0x119ceafee6ad2026ULL,
+    0x851e0ae42a79a01fULL, 0x4d75d441ef06651aULL, 0xca305cd8b6735d9dULL, 0xa0cead46256802d9ULL,
+    0xcc0331836d720255ULL, 0x5293772ecb76750aULL, 0x7f9c531a780ed630ULL, 0x16a4383076ab1eb7ULL,
+    0xb41cae51c1ab3a46ULL, 0x580309f14acbf443ULL, 0xd3c43315504a7b0eULL, 0xd6cd8ebac60bc726ULL,
+    0x21de78f80dc167b5ULL, 0xc16d99fec2c1006fULL, 0x813367d18a1eba79ULL, 0xb9e3b30d5bbc6228ULL,
+    0xce86181c1400891eULL, 0x6c2f5101981cd491ULL, 0x0b755f939d9236b7ULL, 0x2bc5b67e95aa60afULL,
+    0x769dc25a88e6402eULL, 0xf026697513cafd28ULL, 0x8f57614bbe869ac9ULL, 0x2f555dd061a0c749ULL,
+    0x0bb03d0077fce7f4ULL, 0x02694ae2e0277ea6ULL, 0x8f7d57288669d5fdULL, 0x5381a6d920d7393fULL,
+    0xb6f3db5ccd8e3480ULL, 0xde07aa5052fe5699ULL, 0xc0ea448bd283eddeULL, 0xbd0f6b5121d2d374ULL,
+    0xedfc3be01d06cf79ULL, 0xa25415f2113258adULL, 0x9fc0ea9d68d631acULL, 0x022b45e69f54b3d6ULL,
+    0x9c4841ea5e5d86b3ULL, 0x0d0baff2178ada20ULL, 0xb4da0dedd6f4c6e9ULL, 0x6c4cd03af7e06ecdULL,
+    0xe8da77b922d167ffULL, 0x295e9ee377d09aa1ULL, 0x4b01b846854dde13ULL, 0x79e0e2751095f676ULL,
+    0x15befe6ca57026bbULL, 0x2a400035a330630aULL, 0x3db0c72c02ec828eULL, 0xa043e4b51f7bb93dULL
+};
+
+__device__ __forceinline__ uint64_t mwc_jump5(uint64_t s, int L) {
+    constexpr uint64_t A = 4164903690ULL;
+    constexpr unsigned __int128 M = (((unsigned __int128)A) << 32) - 1;
+    unsigned __int128 t = (unsigned __int128)s * kMwcJump5[L];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t = (t >> 32) + (unsigned __int128)(uint32_t)t * A;
+    return (uint64_t)(t >= M ? t - M : t);
+}
+
+// nh <= 64 consecutive samples (5 distinct indices each, cv_rng_sample5's sequence) on the 64
+// lanes of a wave: lane h draws sample h from the state 5 (h - b0) draws past the base; the first
+// lane whose draws repeat an index redraws one at a time and the lanes after it restart from its
+// final state.  rs: the state before the chunk (uniform), the state after it on return; sample h
+// goes to out[5 h .. 5 h + 4].  (pnp.hip: a RANSAC chunk into LDS; ransac.hip: ess_pregen_kernel.)
+__device__ __forceinline__ void cv_rng_sample_wave(uint64_t& rs, unsigned n, unsigned mg, int nh, int* out,
+                                                   int lane) {
+    constexpr uint64_t A = 4164903690ULL;
+    uint64_t base = rs;
+    int b0 = 0;
+    for (;;) {
+        const int L = lane - b0;
+        const bool act = L >= 0 && lane < nh;
+        const uint64_t st = L <= 0 ? base : mwc_jump5(base, min(L, 63));
+        uint64_t sv = st;
+        int d[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            sv = (uint64_t)(unsigned)sv * A + (unsigned)(sv >> 32);
+            d[i] = (int)cv_rng_mod((unsigned)sv, n, mg);
+        }
+        bool dup = false;
+#pragma unroll
+        for (int i = 1; i < 5; ++i)
+#pragma unroll
+            for (int t = 0; t < i; ++t) dup = dup || d[t] == d[i];
+        const uint64_t dm = __ballot(act && dup);
+        const int hs = dm ? __ffsll((unsigned long long)dm) - 1 : nh;
+        if (act && lane < hs) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) out[lane * 5 + i] = d[i];
+        }
+        if (hs >= nh) {
+            rs = __shfl(sv, nh - 1);
+            return;
+        }
+        uint64_t s2 = st;
+        if (lane == hs) {
+            cv_rng_sample5(s2, n, mg, d);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) out[lane * 5 + i] = d[i];
+        }
+        base = __shfl(s2, hs);
+        b0 = hs + 1;
+        if (b0 >= nh) {
+            rs = base;
+            return;
+        }
+    }
+}
+
 }  // namespace sfmhip

@@ -9,7 +9,7 @@ number-theoretic rather than bit-for-bit against the oracle:
   matrix) and inverse iteration with partial pivoting (the four vectors in lockstep, modified
   Gram-Schmidt after every step), restated step for step in numpy and checked against LAPACK
   (numpy.linalg.eigh) on EPnP-like M^T M matrices.
-* pnp.hip `pnp_sample_chunk`: cv::RNG jump-ahead; the wave-parallel sampler gives the serial
+* geom_dev.h `cv_rng_sample_wave`: cv::RNG jump-ahead; the wave-parallel sampler gives the serial
   cv_rng_sample5 sequence and final state exactly.
 """
 import math
@@ -196,7 +196,8 @@ def test_eig4_tridiagonal_matches_lapack():
 
 
 # ---------------------------------------------------------------------------------------------
-# pnp.hip pnp_sample_chunk: cv::RNG's multiply-with-carry step s' = A lo(s) + hi(s) is
+# geom_dev.h cv_rng_sample_wave (pnp.hip's RANSAC chunks, ransac.hip's ess_pregen_kernel):
+# cv::RNG's multiply-with-carry step s' = A lo(s) + hi(s) is
 # s' = s b^-1 mod m (b = 2^32, m = A b - 1, b^-1 = A), so the state 5 L draws ahead is
 # s A^(5 L) mod m, formed on the device as mwc_red^3(s C_L) with C_L = A^(5 L - 3) mod m
 # (mwc_red(T) = (T >> 32) + lo32(T) A = T b^-1 mod m).  The wave's 64 lanes each draw one
@@ -239,7 +240,7 @@ def _mulred3(s, c):
 def _jump_table():
     import re
     from pathlib import Path
-    src = (Path(__file__).resolve().parent.parent / "3d_reconstruction_amd" / "csrc" / "pnp.hip").read_text()
+    src = (Path(__file__).resolve().parent.parent / "3d_reconstruction_amd" / "csrc" / "geom_dev.h").read_text()
     body = src[src.index("kMwcJump5[64] = {"):]
     body = body[:body.index("};")]
     return [int(v, 16) for v in re.findall(r"0x([0-9a-f]+)ULL", body)]
