@@ -940,6 +940,106 @@ __global__ __launch_bounds__(256) void desc_residual_kernel(const float* __restr
 // those (at most kResolveCap, else for every j).  A persistent scan over the
 // match graph finds the marked rows (grid-stride over 64-row chunks).
 constexpr int kResolveCap = 512;
+// One undecided row e (its mark = kUndecidedBase - D2) by one wave; sxa / sqa / scand: the wave's
+// LDS rows.
+template <int D>
+__device__ __forceinline__ void resolve_row(int64_t e, int mark, const int8_t* __restrict__ q,
+                                            const float* __restrict__ x, const int32_t* __restrict__ nk, int m_pad,
+                                            const int32_t* __restrict__ pairs, const double* __restrict__ erow,
+                                            const double* __restrict__ eimg, double s, double rn2, double rd2,
+                                            int32_t* __restrict__ m0, unsigned* __restrict__ n_resolved, float* sxa,
+                                            int* sqa, int* scand, int lane) {
+    constexpr int W4 = D / 4;
+    const int pair = (int)(e / m_pad), i = (int)(e % m_pad);
+    const int a = pairs[2 * pair], b = pairs[2 * pair + 1], nb = nk[b];
+    const int d2q = kUndecidedBase - mark;
+    const size_t arow = (size_t)a * m_pad + i;
+    for (int k = lane; k < D; k += 64) sxa[k] = x[arow * D + k];
+    for (int w = lane; w < W4; w += 64) sqa[w] = reinterpret_cast<const int*>(q + arow * D)[w];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // |q_a|^2
+    int na = 0;
+    for (int w = lane; w < W4; w += 64) na = __builtin_amdgcn_sdot4(sqa[w], sqa[w], na, false);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) na += __shfl_xor(na, off);
+    const double se = (erow[arow] + eimg[b]) * s * (1.0 + 1e-12);
+    const double bq = (se + (sqrt((double)d2q) + se) * (1.0 + 1e-12)) * (1.0 + 1e-12);
+    const double tq = floor(bq * bq) + 1.0;   // every j with D_j <= tq may reach the top two
+    int ncand = 0;
+    for (int j0 = 0; j0 < nb; j0 += 64) {
+        const int j = j0 + lane;
+        bool in = false;
+        if (j < nb) {
+            const int4* qb = reinterpret_cast<const int4*>(q + ((size_t)b * m_pad + j) * D);
+            int dot = 0, nbn = 0;
+#pragma unroll 4
+            for (int w4 = 0; w4 < W4 / 4; ++w4) {
+                const int4 t = qb[w4];
+                const int4 u = reinterpret_cast<const int4*>(sqa)[w4];
+                dot = __builtin_amdgcn_sdot4(t.x, u.x, dot, false);
+                dot = __builtin_amdgcn_sdot4(t.y, u.y, dot, false);
+                dot = __builtin_amdgcn_sdot4(t.z, u.z, dot, false);
+                dot = __builtin_amdgcn_sdot4(t.w, u.w, dot, false);
+                nbn = __builtin_amdgcn_sdot4(t.x, t.x, nbn, false);
+                nbn = __builtin_amdgcn_sdot4(t.y, t.y, nbn, false);
+                nbn = __builtin_amdgcn_sdot4(t.z, t.z, nbn, false);
+                nbn = __builtin_amdgcn_sdot4(t.w, t.w, nbn, false);
+            }
+            in = (double)((long long)na + nbn - 2LL * dot) <= tq;
+        }
+        const unsigned long long cb = __ballot(in);
+        const int pos = ncand + __popcll(cb & ((1ull << lane) - 1ull));
+        if (in && pos < kResolveCap) scand[pos] = j;
+        ncand += __popcll(cb);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool every = ncand > kResolveCap;
+    const int nc = every ? nb : ncand;
+    double v1 = __builtin_inf(), v2 = __builtin_inf();
+    int j1 = INT_MAX;
+    for (int t = lane; t < nc; t += 64) {   // ascending j per lane
+        const int j = every ? t : scand[t];
+        const float4* xb = reinterpret_cast<const float4*>(x + ((size_t)b * m_pad + j) * D);
+        double acc = 0.0;
+        for (int k4 = 0; k4 < D / 4; ++k4) {
+            const float4 xv = xb[k4];
+            double df;
+            df = (double)sxa[4 * k4] - (double)xv.x;
+            acc = acc + df * df;
+            df = (double)sxa[4 * k4 + 1] - (double)xv.y;
+            acc = acc + df * df;
+            df = (double)sxa[4 * k4 + 2] - (double)xv.z;
+            acc = acc + df * df;
+            df = (double)sxa[4 * k4 + 3] - (double)xv.w;
+            acc = acc + df * df;
+        }
+        if (acc < v1) { v2 = v1; v1 = acc; j1 = j; }
+        else if (acc < v2) v2 = acc;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double o1 = __shfl_xor(v1, off), o2 = __shfl_xor(v2, off);
+        const int oj = __shfl_xor(j1, off);
+        const bool mine = v1 < o1 || (v1 == o1 && j1 < oj);
+        const double n2 = mine ? fmin(v2, o1) : fmin(o2, v1);
+        if (!mine) { v1 = o1; j1 = oj; }
+        v2 = n2;
+    }
+    // den^2 d1 < num^2 d2, exactly: (p, e) two-products compare lexicographically (RN is monotone)
+    const double p1 = rd2 * v1, e1 = __builtin_fma(rd2, v1, -p1);
+    const double p2 = rn2 * v2, e2 = __builtin_fma(rn2, v2, -p2);
+    const bool acc_ok = p1 < p2 || (p1 == p2 && e1 < e2);
+    if (lane == 0) {
+        m0[e] = acc_ok ? j1 : -1;
+        if (n_resolved) atomicAdd(n_resolved, 1u);
+    }
+    __builtin_amdgcn_wave_barrier();   // LDS rows reused by the next marked row
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void match_resolve_kernel(const int8_t* __restrict__ q, const float* __restrict__ x,
                                                             const int32_t* __restrict__ nk, int m_pad,
@@ -947,7 +1047,9 @@ __global__ __launch_bounds__(256) void match_resolve_kernel(const int8_t* __rest
                                                             const double* __restrict__ erow,
                                                             const double* __restrict__ eimg, double s, double rn2,
                                                             double rd2, int32_t* __restrict__ m0,
-                                                            unsigned* __restrict__ n_resolved) {
+                                                            unsigned* __restrict__ n_resolved,
+                                                            const unsigned* __restrict__ overflow = nullptr) {
+    if (overflow && *overflow == 0u) return;   // the bucketed pass below settled every row
     constexpr int W4 = D / 4;
     __shared__ float sxa[4][D];
     __shared__ __attribute__((aligned(16))) int sqa[4][W4];
@@ -962,97 +1064,103 @@ __global__ __launch_bounds__(256) void match_resolve_kernel(const int8_t* __rest
         while (bal) {
             const int l = __builtin_ctzll(bal);
             bal &= bal - 1;
-            const int mark = __shfl(v, l);
-            const int64_t e = e0 + l;
-            const int pair = (int)(e / m_pad), i = (int)(e % m_pad);
-            const int a = pairs[2 * pair], b = pairs[2 * pair + 1], nb = nk[b];
-            const int d2q = kUndecidedBase - mark;
-            const size_t arow = (size_t)a * m_pad + i;
-            for (int k = lane; k < D; k += 64) sxa[wave][k] = x[arow * D + k];
-            for (int w = lane; w < W4; w += 64) sqa[wave][w] = reinterpret_cast<const int*>(q + arow * D)[w];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // |q_a|^2
-            int na = 0;
-            for (int w = lane; w < W4; w += 64) na = __builtin_amdgcn_sdot4(sqa[wave][w], sqa[wave][w], na, false);
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) na += __shfl_xor(na, off);
-            const double se = (erow[arow] + eimg[b]) * s * (1.0 + 1e-12);
-            const double bq = (se + (sqrt((double)d2q) + se) * (1.0 + 1e-12)) * (1.0 + 1e-12);
-            const double tq = floor(bq * bq) + 1.0;   // every j with D_j <= tq may reach the top two
-            int ncand = 0;
-            for (int j0 = 0; j0 < nb; j0 += 64) {
-                const int j = j0 + lane;
-                bool in = false;
-                if (j < nb) {
-                    const int4* qb = reinterpret_cast<const int4*>(q + ((size_t)b * m_pad + j) * D);
-                    int dot = 0, nbn = 0;
-#pragma unroll 4
-                    for (int w4 = 0; w4 < W4 / 4; ++w4) {
-                        const int4 t = qb[w4];
-                        const int4 u = reinterpret_cast<const int4*>(sqa[wave])[w4];
-                        dot = __builtin_amdgcn_sdot4(t.x, u.x, dot, false);
-                        dot = __builtin_amdgcn_sdot4(t.y, u.y, dot, false);
-                        dot = __builtin_amdgcn_sdot4(t.z, u.z, dot, false);
-                        dot = __builtin_amdgcn_sdot4(t.w, u.w, dot, false);
-                        nbn = __builtin_amdgcn_sdot4(t.x, t.x, nbn, false);
-                        nbn = __builtin_amdgcn_sdot4(t.y, t.y, nbn, false);
-                        nbn = __builtin_amdgcn_sdot4(t.z, t.z, nbn, false);
-                        nbn = __builtin_amdgcn_sdot4(t.w, t.w, nbn, false);
-                    }
-                    in = (double)((long long)na + nbn - 2LL * dot) <= tq;
-                }
-                const unsigned long long cb = __ballot(in);
-                const int pos = ncand + __popcll(cb & ((1ull << lane) - 1ull));
-                if (in && pos < kResolveCap) scand[wave][pos] = j;
-                ncand += __popcll(cb);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const bool every = ncand > kResolveCap;
-            const int nc = every ? nb : ncand;
-            double v1 = __builtin_inf(), v2 = __builtin_inf();
-            int j1 = INT_MAX;
-            for (int t = lane; t < nc; t += 64) {   // ascending j per lane
-                const int j = every ? t : scand[wave][t];
-                const float4* xb = reinterpret_cast<const float4*>(x + ((size_t)b * m_pad + j) * D);
-                double acc = 0.0;
-                for (int k4 = 0; k4 < D / 4; ++k4) {
-                    const float4 xv = xb[k4];
-                    double df;
-                    df = (double)sxa[wave][4 * k4] - (double)xv.x;
-                    acc = acc + df * df;
-                    df = (double)sxa[wave][4 * k4 + 1] - (double)xv.y;
-                    acc = acc + df * df;
-                    df = (double)sxa[wave][4 * k4 + 2] - (double)xv.z;
-                    acc = acc + df * df;
-                    df = (double)sxa[wave][4 * k4 + 3] - (double)xv.w;
-                    acc = acc + df * df;
-                }
-                if (acc < v1) { v2 = v1; v1 = acc; j1 = j; }
-                else if (acc < v2) v2 = acc;
-            }
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                const double o1 = __shfl_xor(v1, off), o2 = __shfl_xor(v2, off);
-                const int oj = __shfl_xor(j1, off);
-                const bool mine = v1 < o1 || (v1 == o1 && j1 < oj);
-                const double n2 = mine ? fmin(v2, o1) : fmin(o2, v1);
-                if (!mine) { v1 = o1; j1 = oj; }
-                v2 = n2;
-            }
-            // den^2 d1 < num^2 d2, exactly: (p, e) two-products compare lexicographically (RN is monotone)
-            const double p1 = rd2 * v1, e1 = __builtin_fma(rd2, v1, -p1);
-            const double p2 = rn2 * v2, e2 = __builtin_fma(rn2, v2, -p2);
-            const bool acc_ok = p1 < p2 || (p1 == p2 && e1 < e2);
-            if (lane == 0) {
-                m0[e] = acc_ok ? j1 : -1;
-                if (n_resolved) atomicAdd(n_resolved, 1u);
-            }
-            __builtin_amdgcn_wave_barrier();   // LDS rows reused by the next marked row
+            resolve_row<D>(e0 + l, __shfl(v, l), q, x, nk, m_pad, pairs, erow, eimg, s, rn2, rd2, m0, n_resolved,
+                           sxa[wave], sqa[wave], scand[wave], lane);
         }
+    }
+}
+
+// Default order (round 5): the undecided rows are first collected per image b (one scan of the
+// match graph into buckets of up to kResolveBucket rows), then the rows of image b are settled by
+// the waves of XCD b % 8 together, so image b's int8 rows (the candidate prefilter reads all of
+// them, 1 MB per row at C3) are fetched into that XCD's L2 once instead of once per row.  The
+// per-row work is the same; a bucket overflow sets *overflow and match_resolve_kernel's graph
+// scan settles every row instead.
+constexpr int kResolveBucket = 4096;
+__global__ __launch_bounds__(256) void resolve_collect_kernel(const int32_t* __restrict__ m0, int64_t total, int m_pad,
+                                                              const int32_t* __restrict__ pairs,
+                                                              unsigned* __restrict__ cnt, int64_t* __restrict__ list,
+                                                              unsigned* __restrict__ overflow) {
+    auto take = [&](int64_t e) {
+        const int b = pairs[2 * (int)(e / m_pad) + 1];
+        const unsigned slot = atomicAdd(cnt + b, 1u);
+        if (slot < (unsigned)kResolveBucket) list[(size_t)b * kResolveBucket + slot] = e;
+        else atomicOr(overflow, 1u);
+    };
+    const int64_t n4 = total >> 2;   // m_pad is a multiple of 128: the graph is whole int4s
+    const int4* m4 = reinterpret_cast<const int4*>(m0);
+    for (int64_t e4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e4 < n4; e4 += (int64_t)gridDim.x * blockDim.x) {
+        const int4 v = m4[e4];
+        if (min(min(v.x, v.y), min(v.z, v.w)) > kUndecidedBase) continue;
+        if (v.x <= kUndecidedBase) take(4 * e4);
+        if (v.y <= kUndecidedBase) take(4 * e4 + 1);
+        if (v.z <= kUndecidedBase) take(4 * e4 + 2);
+        if (v.w <= kUndecidedBase) take(4 * e4 + 3);
+    }
+}
+
+// The buckets flattened XCD-major (images b = x, x + 8, ... for x = 0..7, each image's rows
+// together), with each XCD's range [xr[x], xr[x] + xr[8 + x]): resolve_offsets_kernel (one
+// thread: the image offsets), then resolve_flatten_kernel (one entry per thread, its image found
+// by a binary search over the offsets in that order).
+__global__ void resolve_offsets_kernel(const unsigned* __restrict__ cnt, int n_img, unsigned* __restrict__ off,
+                                       unsigned* __restrict__ okey /* [n_img + 1]: offsets in XCD-major order */,
+                                       int* __restrict__ oimg, unsigned* __restrict__ xr,
+                                       const unsigned* __restrict__ overflow) {
+    if (*overflow != 0u || threadIdx.x != 0) return;
+    unsigned run = 0;
+    int pos = 0;
+    for (int x = 0; x < 8; ++x) {
+        xr[x] = run;
+        for (int b = x; b < n_img; b += 8) {
+            off[b] = run;
+            okey[pos] = run;
+            oimg[pos] = b;
+            ++pos;
+            run += min(cnt[b], (unsigned)kResolveBucket);
+        }
+        xr[8 + x] = run - xr[x];
+    }
+    okey[pos] = run;
+}
+__global__ __launch_bounds__(256) void resolve_flatten_kernel(const unsigned* __restrict__ okey,
+                                                              const int* __restrict__ oimg, int n_img,
+                                                              const int64_t* __restrict__ list,
+                                                              int64_t* __restrict__ flat,
+                                                              const unsigned* __restrict__ overflow) {
+    if (*overflow != 0u) return;
+    const unsigned total = okey[n_img];
+    for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        int lo = 0, hi = n_img - 1;   // the last position with okey <= t
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (okey[mid] <= t) lo = mid;
+            else hi = mid - 1;
+        }
+        flat[t] = list[(size_t)oimg[lo] * kResolveBucket + (t - okey[lo])];
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void match_resolve_xcd_kernel(
+    const int8_t* __restrict__ q, const float* __restrict__ x, const int32_t* __restrict__ nk, int m_pad,
+    const int32_t* __restrict__ pairs, const double* __restrict__ erow, const double* __restrict__ eimg,
+    double s, double rn2, double rd2, int32_t* __restrict__ m0, unsigned* __restrict__ n_resolved,
+    const int64_t* __restrict__ flat, const unsigned* __restrict__ xr, const unsigned* __restrict__ overflow) {
+    constexpr int W4 = D / 4;
+    __shared__ float sxa[4][D];
+    __shared__ __attribute__((aligned(16))) int sqa[4][W4];
+    __shared__ int scand[4][kResolveCap];
+    if (*overflow != 0u) return;   // match_resolve_kernel takes every row
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int xcd = blockIdx.x % 8, nx = (gridDim.x + 7 - xcd) / 8;   // this XCD's blocks
+    const int wx = (blockIdx.x / 8) * 4 + wave, nw = nx * 4;         // this wave among them
+    const unsigned xb = xr[xcd], xn = xr[8 + xcd];
+    // consecutive rows (the same image b) go to consecutive waves of the XCD: they run together
+    for (unsigned t = wx; t < xn; t += nw) {
+        const int64_t e = flat[xb + t];
+        resolve_row<D>(e, m0[e], q, x, nk, m_pad, pairs, erow, eimg, s, rn2, rd2, m0, n_resolved, sxa[wave],
+                       sqa[wave], scand[wave], lane);
     }
 }
 
@@ -1301,21 +1409,60 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
     const int64_t nchunk = ((int64_t)P * m_pad + 63) / 64;
     const int rgrid = (int)std::min<int64_t>((nchunk + 3) / 4, (int64_t)n_cu * 8);
     if (n_resolved && hipMemsetAsync(n_resolved, 0, sizeof(uint32_t), s) != hipSuccess) return check_launch("memset");
+    // the resolve's buckets: per image a row count and up to kResolveBucket graph entries
+    const int64_t total = (int64_t)P * m_pad;
+    void* rbuf = nullptr;
+    const size_t rlist_bytes = (size_t)n_img * kResolveBucket * sizeof(int64_t);   // buckets, then the flat list
+    const size_t rcnt_bytes = ((size_t)n_img + 1) * sizeof(unsigned);
+    const size_t roff_bytes = (3 * (size_t)n_img + 17) * sizeof(unsigned);   // off, okey (+1), oimg, xr (16)
+    if (scratch_alloc(&rbuf, 2 * rlist_bytes + rcnt_bytes + roff_bytes, s) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("sfmhip_match_pairs_exact: scratch allocation failed");
+        return SFMHIP_E_HIP;
+    }
+    int64_t* rlist = reinterpret_cast<int64_t*>(rbuf);
+    unsigned* rcnt = reinterpret_cast<unsigned*>(static_cast<char*>(rbuf) + rlist_bytes);
+    unsigned* rflag = rcnt + n_img;
+    int64_t* rflat = reinterpret_cast<int64_t*>(static_cast<char*>(rbuf) + rlist_bytes + rcnt_bytes + roff_bytes);
+    unsigned* roff = reinterpret_cast<unsigned*>(static_cast<char*>(rbuf) + rlist_bytes + rcnt_bytes);
+    unsigned* rokey = roff + n_img;
+    int* roimg = reinterpret_cast<int*>(rokey + n_img + 1);
+    unsigned* rxr = reinterpret_cast<unsigned*>(roimg + n_img);
+    if (hipMemsetAsync(rcnt, 0, rcnt_bytes, s) != hipSuccess) {
+        scratch_free(rbuf, s);
+        return check_launch("memset");
+    }
+    const int rxgrid = n_cu * 8;   // a multiple of 8: every XCD gets the same number of blocks
 #define SFMHIP_LAUNCH_EXACT(DD)                                                                                  \
     hipLaunchKernelGGL((match_kernel<DD, 16, 4, 4, true>), dim3(nwg), dim3(256), 0, s, desc, norms, keys, n_kpts, \
                        m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2, ca);                         \
-    if (int rc = check_launch("match_kernel<cert>")) return rc;                                                   \
+    if (int rc = check_launch("match_kernel<cert>")) {                                                          \
+        scratch_free(rbuf, s);                                                                                    \
+        return rc;                                                                                                \
+    }                                                                                                             \
+    hipLaunchKernelGGL(resolve_collect_kernel, dim3(rgrid), dim3(256), 0, s, matches0, total, m_pad, pairs, rcnt,  \
+                       rlist, rflag);                                                                             \
+    hipLaunchKernelGGL(resolve_offsets_kernel, dim3(1), dim3(64), 0, s, rcnt, n_img, roff, rokey, roimg, rxr,      \
+                       rflag);                                                                                    \
+    hipLaunchKernelGGL(resolve_flatten_kernel, dim3(n_cu), dim3(256), 0, s, rokey, roimg, n_img, rlist, rflat,     \
+                       rflag);                                                                                    \
+    hipLaunchKernelGGL((match_resolve_xcd_kernel<DD>), dim3(rxgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts,      \
+                       m_pad, pairs, resid_row, resid_img, mode == 0 ? 1.0 : 127.0, (double)rn2, (double)rd2,     \
+                       matches0, n_resolved, rflat, rxr, rflag);                                                  \
     hipLaunchKernelGGL((match_resolve_kernel<DD>), dim3(rgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts, m_pad,   \
                        pairs, P, resid_row, resid_img, mode == 0 ? 1.0 : 127.0, (double)rn2, (double)rd2,        \
-                       matches0, n_resolved)
+                       matches0, n_resolved, rflag)
     switch (d) {
         case 64: SFMHIP_LAUNCH_EXACT(64); break;
         case 128: SFMHIP_LAUNCH_EXACT(128); break;
         case 256: SFMHIP_LAUNCH_EXACT(256); break;
         default:
             set_error("sfmhip_match_pairs_exact: descriptor dim %d not in {64,128,256}", d);
+            scratch_free(rbuf, s);
             return SFMHIP_E_UNSUPPORTED;
     }
 #undef SFMHIP_LAUNCH_EXACT
-    return check_launch("match_resolve_kernel");
+    const int rc = check_launch("match_resolve_kernel");
+    scratch_free(rbuf, s);
+    return rc;
 }
