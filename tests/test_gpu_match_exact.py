@@ -171,3 +171,23 @@ def test_exact_float_c3_whole_pairs(sfm, gpu):
         j1, d1, d2 = om.top2_f(D)
         ref = np.where(om.ratio_accept_exact(d1, d2, 3, 4), j1, -1)
         assert np.array_equal(m0[p, :4096].cpu().numpy(), ref), p
+
+
+def test_exact_float_resolve_bucket_overflow(sfm, gpu, knob):
+    """More than 4096 undecided rows against one image (the resolve's per-image bucket): the
+    collected pass stands down and the graph-scanning per-row pass settles every row; the graph
+    equals the certified run's and the oracle's on sampled rows."""
+    n_img, m, d = 3, 4096, 64
+    x = syn.superpoint_like(n_img, m, d, seed=9).numpy()
+    pairs = np.array([[0, 1], [2, 1], [1, 0]], np.int32)   # image 1 receives 8192 rows
+    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), mode=1, exact=True)
+    knob("MATCH_CERT", "0")   # every row undecided
+    forced = bank.match(pairs, ratio=0.75).cpu().numpy()
+    assert int(bank.last_resolved.item()) == len(pairs) * m
+    knob("MATCH_CERT", "1")
+    certified = bank.match(pairs, ratio=0.75).cpu().numpy()
+    assert np.array_equal(forced, certified)
+    rows = np.random.default_rng(3).choice(m, 48, replace=False)
+    for p, (a, b) in enumerate(pairs):
+        ref = om.bf_match_exact(x[a, rows], x[b], (3, 4))
+        assert np.array_equal(forced[p, rows], ref)
