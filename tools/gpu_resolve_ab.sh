@@ -1,3 +1,6 @@
+# Exact-mode resolve A/B on a GPU box: the match GPU tests with abl/lib_rx.so, then rocprofv3
+# kernel stats of tools/run_match_once.py (C3, 2 reps) for abl/lib_base.so and abl/lib_rx.so
+# (two library builds copied there beforehand; abl/ is scratch, not part of the tree).
 set -o pipefail
 mkdir -p gpurun_out
 L=3d_reconstruction_amd/libsfmhip.so
