@@ -940,6 +940,11 @@ __global__ __launch_bounds__(256) void desc_residual_kernel(const float* __restr
 // those (at most kResolveCap, else for every j).  A persistent scan over the
 // match graph finds the marked rows (grid-stride over 64-row chunks).
 constexpr int kResolveCap = 512;
+#ifdef SFMHIP_RESOLVE_PROF
+// tool-only build (tools/prof_resolve.py): rows, candidates, rows over the cap, max candidates,
+// a histogram by 64 — of the batched resolve
+__device__ unsigned long long g_rprof[16];
+#endif
 // One undecided row e (its mark = kUndecidedBase - D2) by one wave; sxa / sqa / scand: the wave's
 // LDS rows.
 template <int D>
@@ -1070,12 +1075,11 @@ __global__ __launch_bounds__(256) void match_resolve_kernel(const int8_t* __rest
     }
 }
 
-// Default order (round 5): the undecided rows are first collected per image b (one scan of the
-// match graph into buckets of up to kResolveBucket rows), then the rows of image b are settled by
-// the waves of XCD b % 8 together, so image b's int8 rows (the candidate prefilter reads all of
-// them, 1 MB per row at C3) are fetched into that XCD's L2 once instead of once per row.  The
-// per-row work is the same; a bucket overflow sets *overflow and match_resolve_kernel's graph
-// scan settles every row instead.
+// Default (round 5): the undecided rows are collected per image b (one scan of the match graph
+// into buckets of up to kResolveBucket rows), laid out XCD-major (images b = x, x + 8, ... on XCD x)
+// and settled kResolveRows at a time per workgroup (match_resolve_batched_kernel), so image b's int8
+// rows — the candidate prefilter reads all of them, 1 MB per row at C3 — are read once per batch.
+// A bucket overflow sets *overflow and match_resolve_kernel's graph scan settles every row instead.
 constexpr int kResolveBucket = 4096;
 __global__ __launch_bounds__(256) void resolve_collect_kernel(const int32_t* __restrict__ m0, int64_t total, int m_pad,
                                                               const int32_t* __restrict__ pairs,
@@ -1103,23 +1107,35 @@ __global__ __launch_bounds__(256) void resolve_collect_kernel(const int32_t* __r
 // together), with each XCD's range [xr[x], xr[x] + xr[8 + x]): resolve_offsets_kernel (one
 // thread: the image offsets), then resolve_flatten_kernel (one entry per thread, its image found
 // by a binary search over the offsets in that order).
+constexpr int kResolveRows = 16;   // rows of one image settled together (resolve_batched_kernel)
 __global__ void resolve_offsets_kernel(const unsigned* __restrict__ cnt, int n_img, unsigned* __restrict__ off,
                                        unsigned* __restrict__ okey /* [n_img + 1]: offsets in XCD-major order */,
                                        int* __restrict__ oimg, unsigned* __restrict__ xr,
+                                       int* __restrict__ items /* [3][n_img * (kResolveBucket / kResolveRows + 1)] */,
+                                       unsigned* __restrict__ ir /* [16]: per XCD item start, count */,
                                        const unsigned* __restrict__ overflow) {
     if (*overflow != 0u || threadIdx.x != 0) return;
+    const int cap = n_img * (kResolveBucket / kResolveRows + 1);
     unsigned run = 0;
-    int pos = 0;
+    int pos = 0, k = 0;
     for (int x = 0; x < 8; ++x) {
         xr[x] = run;
+        ir[x] = k;
         for (int b = x; b < n_img; b += 8) {
+            const unsigned cb = min(cnt[b], (unsigned)kResolveBucket);
             off[b] = run;
             okey[pos] = run;
             oimg[pos] = b;
             ++pos;
-            run += min(cnt[b], (unsigned)kResolveBucket);
+            for (unsigned r0 = 0; r0 < cb; r0 += kResolveRows, ++k) {
+                items[k] = (int)(run + r0);                                  // first flat row
+                items[cap + k] = (int)min((unsigned)kResolveRows, cb - r0);  // rows
+                items[2 * cap + k] = b;
+            }
+            run += cb;
         }
         xr[8 + x] = run - xr[x];
+        ir[8 + x] = k - ir[x];
     }
     okey[pos] = run;
 }
@@ -1141,32 +1157,159 @@ __global__ __launch_bounds__(256) void resolve_flatten_kernel(const unsigned* __
     }
 }
 
+// Up to kResolveRows undecided rows of one image b per workgroup (the items of the XCD-major
+// order above, dealt to the XCD's own workgroups): the query rows staged in LDS, image b's int8
+// rows read ONCE for the whole batch by the candidate prefilter (threads over the candidates j,
+// every row tested per j), then the f64 distances of each row's candidates by one wave per row
+// (any order: a tie-aware top two, lowest index on equal distances) — resolve_row's result.
+// At C3 a row keeps ~2 candidates, so the prefilter (4096 int8 rows of image b per row in the
+// per-row form) is nearly all of the work.
 template <int D>
-__global__ __launch_bounds__(256) void match_resolve_xcd_kernel(
+__global__ __launch_bounds__(256) void match_resolve_batched_kernel(
     const int8_t* __restrict__ q, const float* __restrict__ x, const int32_t* __restrict__ nk, int m_pad,
-    const int32_t* __restrict__ pairs, const double* __restrict__ erow, const double* __restrict__ eimg,
+    const int32_t* __restrict__ pairs, int n_img, const double* __restrict__ erow, const double* __restrict__ eimg,
     double s, double rn2, double rd2, int32_t* __restrict__ m0, unsigned* __restrict__ n_resolved,
-    const int64_t* __restrict__ flat, const unsigned* __restrict__ xr, const unsigned* __restrict__ overflow) {
-    constexpr int W4 = D / 4;
-    __shared__ float sxa[4][D];
-    __shared__ __attribute__((aligned(16))) int sqa[4][W4];
-    __shared__ int scand[4][kResolveCap];
+    const int64_t* __restrict__ flat, const int* __restrict__ items, const unsigned* __restrict__ ir,
+    const unsigned* __restrict__ overflow) {
+    constexpr int W4 = D / 4, R = kResolveRows;
+    __shared__ __attribute__((aligned(16))) int sqa[R][W4];
+    __shared__ float sxa[R][D];
+    __shared__ int scand[R][kResolveCap];
+    __shared__ int sncand[R], sna[R];
+    __shared__ double stq[R];
+    __shared__ int64_t se_[R];
     if (*overflow != 0u) return;   // match_resolve_kernel takes every row
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int xcd = blockIdx.x % 8, nx = (gridDim.x + 7 - xcd) / 8;   // this XCD's blocks
-    const int wx = (blockIdx.x / 8) * 4 + wave, nw = nx * 4;         // this wave among them
-    const unsigned xb = xr[xcd], xn = xr[8 + xcd];
-    // consecutive rows (the same image b) go to consecutive waves of the XCD: they run together
-    for (unsigned t = wx; t < xn; t += nw) {
-        const int64_t e = flat[xb + t];
-        resolve_row<D>(e, m0[e], q, x, nk, m_pad, pairs, erow, eimg, s, rn2, rd2, m0, n_resolved, sxa[wave],
-                       sqa[wave], scand[wave], lane);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int cap = n_img * (kResolveBucket / kResolveRows + 1);
+    const int xcd = blockIdx.x % 8, nx = (gridDim.x + 7 - xcd) / 8;
+    const unsigned ib = ir[xcd], in = ir[8 + xcd];
+    for (unsigned k = blockIdx.x / 8; k < in; k += nx) {
+        const int f0 = items[ib + k], nr = items[cap + ib + k], b = items[2 * cap + ib + k];
+        const int nb = nk[b];
+        for (int t = tid; t < nr * W4; t += 256) {
+            const int r = t / W4, w = t % W4;
+            const int64_t e = flat[f0 + r];
+            const size_t arow = (size_t)pairs[2 * (int)(e / m_pad)] * m_pad + (int)(e % m_pad);
+            sqa[r][w] = reinterpret_cast<const int*>(q + arow * D)[w];
+        }
+        for (int t = tid; t < nr * D; t += 256) {
+            const int r = t / D, kk = t % D;
+            const int64_t e = flat[f0 + r];
+            const size_t arow = (size_t)pairs[2 * (int)(e / m_pad)] * m_pad + (int)(e % m_pad);
+            sxa[r][kk] = x[arow * D + kk];
+        }
+        if (tid < R) sncand[tid] = 0;
+        __syncthreads();
+        for (int r = wave; r < nr; r += 4) {
+            int na = 0;
+            for (int w = lane; w < W4; w += 64) na = __builtin_amdgcn_sdot4(sqa[r][w], sqa[r][w], na, false);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) na += __shfl_xor(na, off);
+            if (lane == 0) {
+                const int64_t e = flat[f0 + r];
+                const size_t arow = (size_t)pairs[2 * (int)(e / m_pad)] * m_pad + (int)(e % m_pad);
+                const int d2q = kUndecidedBase - m0[e];
+                const double se = (erow[arow] + eimg[b]) * s * (1.0 + 1e-12);
+                const double bq = (se + (sqrt((double)d2q) + se) * (1.0 + 1e-12)) * (1.0 + 1e-12);
+                stq[r] = floor(bq * bq) + 1.0;   // every j with D_j <= tq may reach the top two
+                sna[r] = na;
+                se_[r] = e;
+            }
+        }
+        __syncthreads();
+        for (int j = tid; j < nb; j += 256) {   // image b's int8 rows, once for the batch
+            const int4* qb = reinterpret_cast<const int4*>(q + ((size_t)b * m_pad + j) * D);
+            int4 t[W4 / 4];
+            int nbn = 0;
+#pragma unroll
+            for (int w4 = 0; w4 < W4 / 4; ++w4) {
+                t[w4] = qb[w4];
+                nbn = __builtin_amdgcn_sdot4(t[w4].x, t[w4].x, nbn, false);
+                nbn = __builtin_amdgcn_sdot4(t[w4].y, t[w4].y, nbn, false);
+                nbn = __builtin_amdgcn_sdot4(t[w4].z, t[w4].z, nbn, false);
+                nbn = __builtin_amdgcn_sdot4(t[w4].w, t[w4].w, nbn, false);
+            }
+            for (int r = 0; r < nr; ++r) {
+                int dot = 0;
+#pragma unroll
+                for (int w4 = 0; w4 < W4 / 4; ++w4) {
+                    const int4 u = reinterpret_cast<const int4*>(sqa[r])[w4];
+                    dot = __builtin_amdgcn_sdot4(t[w4].x, u.x, dot, false);
+                    dot = __builtin_amdgcn_sdot4(t[w4].y, u.y, dot, false);
+                    dot = __builtin_amdgcn_sdot4(t[w4].z, u.z, dot, false);
+                    dot = __builtin_amdgcn_sdot4(t[w4].w, u.w, dot, false);
+                }
+                if ((double)((long long)sna[r] + nbn - 2LL * dot) <= stq[r]) {
+                    const int pos = atomicAdd(&sncand[r], 1);
+                    if (pos < kResolveCap) scand[r][pos] = j;
+                }
+            }
+        }
+        __syncthreads();
+        for (int r = wave; r < nr; r += 4) {   // f64 distances of the row's candidates
+            const int ncand = sncand[r];
+            const bool every = ncand > kResolveCap;
+#ifdef SFMHIP_RESOLVE_PROF
+            if (lane == 0) {
+                atomicAdd(&g_rprof[0], 1ull);
+                atomicAdd(&g_rprof[1], (unsigned long long)ncand);
+                if (every) atomicAdd(&g_rprof[2], 1ull);
+                atomicMax(&g_rprof[3], (unsigned long long)ncand);
+                atomicAdd(&g_rprof[4 + min(ncand / 64, 11)], 1ull);
+            }
+#endif
+            const int nc = every ? nb : ncand;
+            double v1 = __builtin_inf(), v2 = __builtin_inf();
+            int j1 = INT_MAX;
+            for (int t = lane; t < nc; t += 64) {
+                const int j = every ? t : scand[r][t];
+                const float4* xb = reinterpret_cast<const float4*>(x + ((size_t)b * m_pad + j) * D);
+                double acc = 0.0;
+                for (int k4 = 0; k4 < D / 4; ++k4) {
+                    const float4 xv = xb[k4];
+                    double df;
+                    df = (double)sxa[r][4 * k4] - (double)xv.x;
+                    acc = acc + df * df;
+                    df = (double)sxa[r][4 * k4 + 1] - (double)xv.y;
+                    acc = acc + df * df;
+                    df = (double)sxa[r][4 * k4 + 2] - (double)xv.z;
+                    acc = acc + df * df;
+                    df = (double)sxa[r][4 * k4 + 3] - (double)xv.w;
+                    acc = acc + df * df;
+                }
+                if (acc < v1 || (acc == v1 && j < j1)) { v2 = v1; v1 = acc; j1 = j; }
+                else if (acc < v2) v2 = acc;
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                const double o1 = __shfl_xor(v1, off), o2 = __shfl_xor(v2, off);
+                const int oj = __shfl_xor(j1, off);
+                const bool mine = v1 < o1 || (v1 == o1 && j1 < oj);
+                const double n2 = mine ? fmin(v2, o1) : fmin(o2, v1);
+                if (!mine) { v1 = o1; j1 = oj; }
+                v2 = n2;
+            }
+            const double p1 = rd2 * v1, e1 = __builtin_fma(rd2, v1, -p1);
+            const double p2 = rn2 * v2, e2 = __builtin_fma(rn2, v2, -p2);
+            const bool acc_ok = p1 < p2 || (p1 == p2 && e1 < e2);
+            if (lane == 0) {
+                m0[se_[r]] = acc_ok ? j1 : -1;
+                if (n_resolved) atomicAdd(n_resolved, 1u);
+            }
+        }
+        __syncthreads();   // the batch's LDS is reused by the next item
     }
 }
 
 }  // namespace sfmhip
 
 using namespace sfmhip;
+
+#ifdef SFMHIP_RESOLVE_PROF
+extern "C" int sfmhip_debug_resolve_prof(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfmhip::g_rprof), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
+}
+#endif
 
 extern "C" int sfmhip_desc_quantize(const float* in, int n_img, int m_pad, int d,
                                     const int32_t* n_kpts, int mode, int8_t* out, void* stream) {
@@ -1414,8 +1557,9 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
     void* rbuf = nullptr;
     const size_t rlist_bytes = (size_t)n_img * kResolveBucket * sizeof(int64_t);   // buckets, then the flat list
     const size_t rcnt_bytes = ((size_t)n_img + 1) * sizeof(unsigned);
-    const size_t roff_bytes = (3 * (size_t)n_img + 17) * sizeof(unsigned);   // off, okey (+1), oimg, xr (16)
-    if (scratch_alloc(&rbuf, 2 * rlist_bytes + rcnt_bytes + roff_bytes, s) != hipSuccess) {
+    const size_t roff_bytes = (3 * (size_t)n_img + 33) * sizeof(unsigned);   // off, okey (+1), oimg, xr, ir
+    const size_t ritem_bytes = 3 * (size_t)n_img * (kResolveBucket / kResolveRows + 1) * sizeof(int);
+    if (scratch_alloc(&rbuf, 2 * rlist_bytes + rcnt_bytes + roff_bytes + ritem_bytes, s) != hipSuccess) {
         (void)hipGetLastError();
         set_error("sfmhip_match_pairs_exact: scratch allocation failed");
         return SFMHIP_E_HIP;
@@ -1428,11 +1572,13 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
     unsigned* rokey = roff + n_img;
     int* roimg = reinterpret_cast<int*>(rokey + n_img + 1);
     unsigned* rxr = reinterpret_cast<unsigned*>(roimg + n_img);
+    unsigned* rir = rxr + 16;
+    int* ritems = reinterpret_cast<int*>(static_cast<char*>(rbuf) + 2 * rlist_bytes + rcnt_bytes + roff_bytes);
     if (hipMemsetAsync(rcnt, 0, rcnt_bytes, s) != hipSuccess) {
         scratch_free(rbuf, s);
         return check_launch("memset");
     }
-    const int rxgrid = n_cu * 8;   // a multiple of 8: every XCD gets the same number of blocks
+    const int rxgrid = n_cu * 2;   // a multiple of 8: every XCD gets the same number of blocks
 #define SFMHIP_LAUNCH_EXACT(DD)                                                                                  \
     hipLaunchKernelGGL((match_kernel<DD, 16, 4, 4, true>), dim3(nwg), dim3(256), 0, s, desc, norms, keys, n_kpts, \
                        m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2, ca);                         \
@@ -1443,12 +1589,12 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
     hipLaunchKernelGGL(resolve_collect_kernel, dim3(rgrid), dim3(256), 0, s, matches0, total, m_pad, pairs, rcnt,  \
                        rlist, rflag);                                                                             \
     hipLaunchKernelGGL(resolve_offsets_kernel, dim3(1), dim3(64), 0, s, rcnt, n_img, roff, rokey, roimg, rxr,      \
-                       rflag);                                                                                    \
+                       ritems, rir, rflag);                                                                       \
     hipLaunchKernelGGL(resolve_flatten_kernel, dim3(n_cu), dim3(256), 0, s, rokey, roimg, n_img, rlist, rflat,     \
                        rflag);                                                                                    \
-    hipLaunchKernelGGL((match_resolve_xcd_kernel<DD>), dim3(rxgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts,      \
-                       m_pad, pairs, resid_row, resid_img, mode == 0 ? 1.0 : 127.0, (double)rn2, (double)rd2,     \
-                       matches0, n_resolved, rflat, rxr, rflag);                                                  \
+    hipLaunchKernelGGL((match_resolve_batched_kernel<DD>), dim3(rxgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts,  \
+                       m_pad, pairs, n_img, resid_row, resid_img, mode == 0 ? 1.0 : 127.0, (double)rn2,          \
+                       (double)rd2, matches0, n_resolved, rflat, ritems, rir, rflag);                              \
     hipLaunchKernelGGL((match_resolve_kernel<DD>), dim3(rgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts, m_pad,   \
                        pairs, P, resid_row, resid_img, mode == 0 ? 1.0 : 127.0, (double)rn2, (double)rd2,        \
                        matches0, n_resolved, rflag)
