@@ -1325,8 +1325,8 @@ def main():
                      "frac": achieved_tops / PEAK_INT8_TOPS,
                      "traffic": pmc_traffic("match", pairs_per_launch / P) if n_img == N_IMG else None,
                      "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r5/traffic.json: match_kernel "
-                                     "(certifying epilogue) + match_resolve_kernel)",
-                     "kernel": "match_kernel<256> (exact mode) + match_resolve_kernel", "kernel_ms": kern_ms,
+                                     "(certifying epilogue) + the resolve kernels: collect, batched f64 re-score)",
+                     "kernel": "match_kernel<256> (exact mode) + resolve kernels", "kernel_ms": kern_ms,
                      "algorithmic": "2*M*N*d int8 ops per pair x pairs per launch (the f64 re-score of the "
                                     "uncertified rows is overhead, not work)"},
     }
