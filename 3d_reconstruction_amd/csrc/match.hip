@@ -1105,39 +1105,82 @@ __global__ __launch_bounds__(256) void resolve_collect_kernel(const int32_t* __r
 
 // The buckets flattened XCD-major (images b = x, x + 8, ... for x = 0..7, each image's rows
 // together), with each XCD's range [xr[x], xr[x] + xr[8 + x]): resolve_offsets_kernel (one
-// thread: the image offsets), then resolve_flatten_kernel (one entry per thread, its image found
-// by a binary search over the offsets in that order).
+// workgroup: position p of that order holds image b(p); an LDS scan over the positions, 1024 at a
+// time, gives each image's first flat row and first item), then resolve_flatten_kernel (one entry
+// per thread, its image found by a binary search over the offsets in that order).
 constexpr int kResolveRows = 16;   // rows of one image settled together (resolve_batched_kernel)
-__global__ void resolve_offsets_kernel(const unsigned* __restrict__ cnt, int n_img, unsigned* __restrict__ off,
-                                       unsigned* __restrict__ okey /* [n_img + 1]: offsets in XCD-major order */,
-                                       int* __restrict__ oimg, unsigned* __restrict__ xr,
-                                       int* __restrict__ items /* [3][n_img * (kResolveBucket / kResolveRows + 1)] */,
-                                       unsigned* __restrict__ ir /* [16]: per XCD item start, count */,
-                                       const unsigned* __restrict__ overflow) {
-    if (*overflow != 0u || threadIdx.x != 0) return;
+__global__ __launch_bounds__(1024) void resolve_offsets_kernel(
+    const unsigned* __restrict__ cnt, int n_img, unsigned* __restrict__ off,
+    unsigned* __restrict__ okey /* [n_img + 1]: offsets in XCD-major order */, int* __restrict__ oimg,
+    unsigned* __restrict__ xr, int* __restrict__ items /* [3][n_img * (kResolveBucket / kResolveRows + 1)] */,
+    unsigned* __restrict__ ir /* [16]: per XCD item start, count */, const unsigned* __restrict__ overflow) {
+    __shared__ unsigned sr[1024], sk[1024];
+    __shared__ unsigned sxs[9], sks[9];
+    if (*overflow != 0u) return;
+    const int tid = threadIdx.x;
     const int cap = n_img * (kResolveBucket / kResolveRows + 1);
-    unsigned run = 0;
-    int pos = 0, k = 0;
-    for (int x = 0; x < 8; ++x) {
-        xr[x] = run;
-        ir[x] = k;
-        for (int b = x; b < n_img; b += 8) {
-            const unsigned cb = min(cnt[b], (unsigned)kResolveBucket);
-            off[b] = run;
-            okey[pos] = run;
-            oimg[pos] = b;
-            ++pos;
-            for (unsigned r0 = 0; r0 < cb; r0 += kResolveRows, ++k) {
-                items[k] = (int)(run + r0);                                  // first flat row
-                items[cap + k] = (int)min((unsigned)kResolveRows, cb - r0);  // rows
-                items[2 * cap + k] = b;
-            }
-            run += cb;
+    int ps[9];   // first position of XCD x (ps[8] = n_img)
+    ps[0] = 0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) ps[x + 1] = ps[x] + (x < n_img ? (n_img - x + 7) / 8 : 0);
+    unsigned carry_r = 0, carry_k = 0;
+    for (int base = 0; base < n_img; base += 1024) {
+        const int p = base + tid;
+        int b = -1;
+        unsigned cb = 0, ni = 0;
+        if (p < n_img) {
+            int x = 0;
+#pragma unroll
+            for (int y = 1; y < 8; ++y) x += (p >= ps[y]) ? 1 : 0;
+            b = x + 8 * (p - ps[x]);
+            cb = min(cnt[b], (unsigned)kResolveBucket);
+            ni = (cb + kResolveRows - 1) / kResolveRows;
         }
-        xr[8 + x] = run - xr[x];
-        ir[8 + x] = k - ir[x];
+        sr[tid] = cb;
+        sk[tid] = ni;
+        __syncthreads();
+        for (int d = 1; d < 1024; d <<= 1) {   // inclusive scan
+            const unsigned vr = tid >= d ? sr[tid - d] : 0u, vk = tid >= d ? sk[tid - d] : 0u;
+            __syncthreads();
+            sr[tid] += vr;
+            sk[tid] += vk;
+            __syncthreads();
+        }
+        const unsigned run = carry_r + sr[tid] - cb, k0 = carry_k + sk[tid] - ni;
+        if (b >= 0) {
+            off[b] = run;
+            okey[p] = run;
+            oimg[p] = b;
+#pragma unroll
+            for (int x = 0; x < 8; ++x)
+                if (p == ps[x]) {
+                    sxs[x] = run;
+                    sks[x] = k0;
+                }
+            for (unsigned i = 0; i < ni; ++i) {
+                items[k0 + i] = (int)(run + i * kResolveRows);                          // first flat row
+                items[cap + k0 + i] = (int)min((unsigned)kResolveRows, cb - i * kResolveRows);   // rows
+                items[2 * cap + k0 + i] = b;
+            }
+        }
+        carry_r += sr[1023];
+        carry_k += sk[1023];
+        __syncthreads();
     }
-    okey[pos] = run;
+    if (tid < 9) {   // XCDs without images (n_img < 8) start at the end
+        if (tid == 8 || ps[tid] >= n_img) {
+            sxs[tid] = carry_r;
+            sks[tid] = carry_k;
+        }
+    }
+    __syncthreads();
+    if (tid < 8) {
+        xr[tid] = sxs[tid];
+        xr[8 + tid] = sxs[tid + 1] - sxs[tid];
+        ir[tid] = sks[tid];
+        ir[8 + tid] = sks[tid + 1] - sks[tid];
+    }
+    if (tid == 0) okey[n_img] = carry_r;
 }
 __global__ __launch_bounds__(256) void resolve_flatten_kernel(const unsigned* __restrict__ okey,
                                                               const int* __restrict__ oimg, int n_img,
@@ -1588,7 +1631,7 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
     }                                                                                                             \
     hipLaunchKernelGGL(resolve_collect_kernel, dim3(rgrid), dim3(256), 0, s, matches0, total, m_pad, pairs, rcnt,  \
                        rlist, rflag);                                                                             \
-    hipLaunchKernelGGL(resolve_offsets_kernel, dim3(1), dim3(64), 0, s, rcnt, n_img, roff, rokey, roimg, rxr,      \
+    hipLaunchKernelGGL(resolve_offsets_kernel, dim3(1), dim3(1024), 0, s, rcnt, n_img, roff, rokey, roimg, rxr,      \
                        ritems, rir, rflag);                                                                       \
     hipLaunchKernelGGL(resolve_flatten_kernel, dim3(n_cu), dim3(256), 0, s, rokey, roimg, n_img, rlist, rflat,     \
                        rflag);                                                                                    \

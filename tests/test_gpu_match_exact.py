@@ -191,3 +191,23 @@ def test_exact_float_resolve_bucket_overflow(sfm, gpu, knob):
     for p, (a, b) in enumerate(pairs):
         ref = om.bf_match_exact(x[a, rows], x[b], (3, 4))
         assert np.array_equal(forced[p, rows], ref)
+
+
+@pytest.mark.parametrize("cert", ["1", "0"])
+def test_exact_float_resolve_many_images(sfm, gpu, knob, cert):
+    """More images than the resolve's offset scan takes at once (1024 positions of the XCD-major
+    order per pass): the image offsets and per-XCD ranges carried across passes, with pairs whose
+    image b sits before and after position 1024 on every XCD."""
+    knob("MATCH_CERT", cert)
+    n_img, m, d = 1100, 128, 64
+    x = syn.superpoint_like(n_img, m, d, seed=21).numpy()
+    nk = np.full(n_img, m, np.int32)
+    nk[1093] = 77
+    rng = np.random.default_rng(8)
+    bs = np.concatenate([np.arange(8), np.arange(1088, 1100), [512, 1023, 1024, 1025]])
+    pairs = np.array([[int(rng.integers(n_img)), int(b)] for b in bs], np.int32)
+    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=1, exact=True)
+    m0 = bank.match(pairs, ratio=0.75).cpu().numpy()[:, :m]
+    assert np.array_equal(m0, _oracle(x, nk, pairs, (3, 4)))
+    if cert == "0":
+        assert int(bank.last_resolved.item()) == sum(int(nk[a]) for a, b in pairs)
