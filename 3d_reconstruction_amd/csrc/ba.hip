@@ -259,6 +259,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     const int max_nfev = max_nfev_arg > 0 ? max_nfev_arg : (int)min((int64_t)INT_MAX, 100 * (6 + 3 * (int64_t)n));
 #ifdef SFMHIP_BA_PROF
     unsigned long long prof_acc[kProfPhases] = {}, prof_t = wall_clock64();
+    const unsigned long long prof_t0 = prof_t;   // slots 8, 9: the pair's start and end
 #endif
 
     // J, f at the current point; scale_inv (max with the old unless first); gc, cost, |g|_inf.
@@ -650,6 +651,8 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         if (S.done) break;
     }
 #ifdef SFMHIP_BA_PROF
+    prof_acc[8] = prof_t0;
+    prof_acc[9] = wall_clock64();
     if (tid == 0 && p < 4096)
         for (int kk = 0; kk < kProfPhases; ++kk) g_ba_prof[p * kProfPhases + kk] = prof_acc[kk];
 #endif

@@ -25,7 +25,7 @@ buf = (ctypes.c_ulonglong * (P * 10))()
 assert sfm.lib.sfmhip_ba_prof_read(buf, P) == 0
 t = np.array(buf[:], dtype=np.float64).reshape(P, 10) / 100.0   # us
 names = ["jacobian", "regularize", "ridge", "gauss-newton", "subspace", "2-D subproblem", "trial", "accept"]
-tot = t.sum(1)
+tot = t[:, :8].sum(1)
 nfev = r["nfev"].cpu().numpy()
 njev = r["njev"].cpu().numpy()
 print("per pair (us) mean / max total:", round(tot.mean(), 1), round(tot.max(), 1))
@@ -36,5 +36,9 @@ print("jacobian pass per evaluation (us): mean %.1f" % per_j.mean())
 print("slowest 8 pairs: total, nfev, njev, phases")
 for i in np.argsort(tot)[-8:]:
     print("  %.1f  %d  %d  %s" % (tot[i], nfev[i], njev[i], " ".join("%.1f" % v for v in t[i, :8])))
+t0, t1 = t[:, 8] - t[:, 8].min(), t[:, 9] - t[:, 8].min()
+print("pair start spread (us): max %.1f; end: min %.1f median %.1f max %.1f" % (t0.max(), t1.min(), np.median(t1), t1.max()))
+alive = [(int(((t0 <= x) & (t1 > x)).sum())) for x in np.arange(0, t1.max(), 50.0)]
+print("pairs alive every 50 us:", alive)
 hist = np.bincount(nfev.astype(int))
 print("nfev histogram:", {k: int(v) for k, v in enumerate(hist) if v})
