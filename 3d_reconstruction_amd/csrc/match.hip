@@ -1202,14 +1202,16 @@ __global__ __launch_bounds__(256) void resolve_flatten_kernel(const unsigned* __
 
 // Up to kResolveRows undecided rows of one image b per workgroup (the items of the XCD-major
 // order above, dealt to the XCD's own workgroups): the query rows staged in LDS, image b's int8
-// rows read ONCE for the whole batch by the candidate prefilter (threads over the candidates j,
-// every row tested per j), then the f64 distances of each row's candidates by one wave per row
-// (any order: a tie-aware top two, lowest index on equal distances) — resolve_row's result.
-// At C3 a row keeps ~2 candidates, so the prefilter (4096 int8 rows of image b per row in the
-// per-row form) is nearly all of the work.
+// rows read ONCE for the whole batch by the candidate prefilter (16 candidates x the batch's 16
+// rows per MFMA chain, four tiles' loads in flight per wave: 0.41 -> 0.30 ms per C3 call against
+// v_dot4 over the candidates, profiles/r5/ab/resolve_mfma_prefilter_ab_r5.txt), then the f64
+// distances of each row's candidates by one wave per row (any order: a tie-aware top two, lowest
+// index on equal distances) — resolve_row's result.  At C3 a row keeps ~2 candidates, so the
+// prefilter (4096 int8 rows of image b per row in the per-row form) is most of the work.
 template <int D>
 __global__ __launch_bounds__(256) void match_resolve_batched_kernel(
-    const int8_t* __restrict__ q, const float* __restrict__ x, const int32_t* __restrict__ nk, int m_pad,
+    const int8_t* __restrict__ q /* the matcher's (shifted) int8 operands */, const int32_t* __restrict__ norms,
+    const float* __restrict__ x, const int32_t* __restrict__ nk, int m_pad,
     const int32_t* __restrict__ pairs, int n_img, const double* __restrict__ erow, const double* __restrict__ eimg,
     double s, double rn2, double rd2, int32_t* __restrict__ m0, unsigned* __restrict__ n_resolved,
     const int64_t* __restrict__ flat, const int* __restrict__ items, const unsigned* __restrict__ ir,
@@ -1218,7 +1220,7 @@ __global__ __launch_bounds__(256) void match_resolve_batched_kernel(
     __shared__ __attribute__((aligned(16))) int sqa[R][W4];
     __shared__ float sxa[R][D];
     __shared__ int scand[R][kResolveCap];
-    __shared__ int sncand[R], sna[R];
+    __shared__ int sncand[R], sna[R], sccd[R];
     __shared__ double stq[R];
     __shared__ int64_t se_[R];
     if (*overflow != 0u) return;   // match_resolve_kernel takes every row
@@ -1256,35 +1258,50 @@ __global__ __launch_bounds__(256) void match_resolve_batched_kernel(
                 const double bq = (se + (sqrt((double)d2q) + se) * (1.0 + 1e-12)) * (1.0 + 1e-12);
                 stq[r] = floor(bq * bq) + 1.0;   // every j with D_j <= tq may reach the top two
                 sna[r] = na;
+                sccd[r] = norms[arow] - na;   // the matcher's norms carry c^2 d of its operand shift c
                 se_[r] = e;
             }
         }
         __syncthreads();
-        for (int j = tid; j < nb; j += 256) {   // image b's int8 rows, once for the batch
-            const int4* qb = reinterpret_cast<const int4*>(q + ((size_t)b * m_pad + j) * D);
-            int4 t[W4 / 4];
-            int nbn = 0;
+        {   // the prefilter on the matrix cores: <q_j, q_r> for 16 candidates j x the batch's 16 rows r
+            // per v_mfma_i32_16x16x64_i8 chain (the matcher's operands, shifted by c: D_j is
+            // shift-invariant, |q_j|^2 = norms_j - c^2 d, and the int32 dots are exact, so the
+            // candidate set is the one the per-row form tests)
+            using M16 = Mfma<16>;
+            constexpr int KK = D / M16::KB;
+            const int lr = lane & 15, grp = lane >> 4;   // lane: row lr of the batch, candidates 4 grp + e
+            i32x4 bqv[KK];
 #pragma unroll
-            for (int w4 = 0; w4 < W4 / 4; ++w4) {
-                t[w4] = qb[w4];
-                nbn = __builtin_amdgcn_sdot4(t[w4].x, t[w4].x, nbn, false);
-                nbn = __builtin_amdgcn_sdot4(t[w4].y, t[w4].y, nbn, false);
-                nbn = __builtin_amdgcn_sdot4(t[w4].z, t[w4].z, nbn, false);
-                nbn = __builtin_amdgcn_sdot4(t[w4].w, t[w4].w, nbn, false);
-            }
-            for (int r = 0; r < nr; ++r) {
-                int dot = 0;
+            for (int kk = 0; kk < KK; ++kk) bqv[kk] = *reinterpret_cast<const i32x4*>(&sqa[lr][kk * 16 + grp * 4]);
+            const bool live = lr < nr;
+            const long long na_r = live ? (long long)sna[lr] - sccd[lr] : 0;   // |q_r|^2 - c^2 d
+            const double tq_r = live ? stq[lr] : -1.0;
+            const size_t bbase = (size_t)b * m_pad;
+            constexpr int TG = 4;   // 16-candidate tiles per wave step, their loads issued together
+            for (int jg = wave * 16; jg < nb; jg += 64 * TG) {
+                i32x4 av[TG][KK], nv[TG];
 #pragma unroll
-                for (int w4 = 0; w4 < W4 / 4; ++w4) {
-                    const int4 u = reinterpret_cast<const int4*>(sqa[r])[w4];
-                    dot = __builtin_amdgcn_sdot4(t[w4].x, u.x, dot, false);
-                    dot = __builtin_amdgcn_sdot4(t[w4].y, u.y, dot, false);
-                    dot = __builtin_amdgcn_sdot4(t[w4].z, u.z, dot, false);
-                    dot = __builtin_amdgcn_sdot4(t[w4].w, u.w, dot, false);
+                for (int t = 0; t < TG; ++t) {
+                    const int j0 = min(jg + 64 * t, m_pad - 16);   // whole rows (m_pad % 128 == 0)
+                    const int8_t* rp = q + (bbase + j0 + lr) * D + grp * 16;
+#pragma unroll
+                    for (int kk = 0; kk < KK; ++kk) av[t][kk] = *reinterpret_cast<const i32x4*>(rp + kk * M16::KB);
+                    nv[t] = *reinterpret_cast<const i32x4*>(norms + bbase + j0 + 4 * grp);   // norms of the 4 candidates
                 }
-                if ((double)((long long)sna[r] + nbn - 2LL * dot) <= stq[r]) {
-                    const int pos = atomicAdd(&sncand[r], 1);
-                    if (pos < kResolveCap) scand[r][pos] = j;
+#pragma unroll
+                for (int t = 0; t < TG; ++t) {
+                    const int j0 = jg + 64 * t;
+                    i32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+                    for (int kk = 0; kk < KK; ++kk) acc = M16::run(av[t][kk], bqv[kk], acc);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int j = j0 + 4 * grp + e;
+                        if (live && j < nb && (double)(na_r + nv[t][e] - 2LL * acc[e]) <= tq_r) {
+                            const int pos = atomicAdd(&sncand[lr], 1);
+                            if (pos < kResolveCap) scand[lr][pos] = j;
+                        }
+                    }
                 }
             }
         }
@@ -1635,7 +1652,7 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
                        ritems, rir, rflag);                                                                       \
     hipLaunchKernelGGL(resolve_flatten_kernel, dim3(n_cu), dim3(256), 0, s, rokey, roimg, n_img, rlist, rflat,     \
                        rflag);                                                                                    \
-    hipLaunchKernelGGL((match_resolve_batched_kernel<DD>), dim3(rxgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts,  \
+    hipLaunchKernelGGL((match_resolve_batched_kernel<DD>), dim3(rxgrid), dim3(256), 0, s, desc, norms, desc_f, n_kpts,  \
                        m_pad, pairs, n_img, resid_row, resid_img, mode == 0 ? 1.0 : 127.0, (double)rn2,          \
                        (double)rd2, matches0, n_resolved, rflat, ritems, rir, rflag);                              \
     hipLaunchKernelGGL((match_resolve_kernel<DD>), dim3(rgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts, m_pad,   \
