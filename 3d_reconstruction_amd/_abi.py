@@ -60,10 +60,13 @@ SIGNATURES = {
     "sfmhip_desc_prepare": [_p, _i32, _i32, _i32, _p, _p, _p, _p],
     "sfmhip_desc_prepare_shifted": [_p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _p],
     "sfmhip_match_pairs": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p],
+    "sfmhip_match_pairs_i16": [_p, _p, _p, _p, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p],
     "sfmhip_mutual_filter": [_p, _p, _i32, _i32, _p],
     "sfmhip_desc_residual": [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p],
     "sfmhip_match_pairs_exact": [_p, _p, _p, _p, _p, _p, _p, _i32, _p, _i32, _i32, _i32, _p, _i32, _i32, _i32,
                                  _p, _p, _p, _p, _p],
+    "sfmhip_match_pairs_exact_i16": [_p, _p, _p, _p, _p, _p, _p, _i32, _p, _i32, _i32, _i32, _p, _i32, _i32,
+                                     _i32, _p, _p, _p],
     "sfmhip_vq": [_p, _i64, _p, _i32, _i32, _p, _p, _p],
     "sfmhip_word_histogram": [_p, _p, _i32, _i32, _p, _p],
     "sfmhip_kmeans_update": [_p, _i64, _i32, _p, _i32, _p, _p, _p],

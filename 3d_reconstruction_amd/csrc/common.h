@@ -55,7 +55,7 @@ void scratch_free(void* p, hipStream_t s);
 
 // Runtime knobs (INTEGRATION.md "Runtime knobs"): read from the environment once, at
 // the first call; sfmhip_knobs_reload() re-reads them (tests).  Every other choice is
-// fixed in the code.
+// fixed in the code.  knobs() returns a copy of the current snapshot (thread-safe).
 struct Knobs {
     int tsdf_latency;   // SFMHIP_TSDF_LATENCY: -1 auto, 0 whole-grid mode, 1 latency mode
     int match_cert;     // SFMHIP_MATCH_CERT: 0 sends every row of the exact float mode to the f64 pass
@@ -66,7 +66,7 @@ struct Knobs {
     int dda_direct;     // SFMHIP_DDA_DIRECT: fill kernel of the two-pass DDA (-1 auto, 0 staged, 1 direct)
     int ab;             // SFMHIP_AB: A/B selector for a form under measurement (0 = the default form)
 };
-const Knobs& knobs();
+Knobs knobs();
 
 }  // namespace sfmhip
 

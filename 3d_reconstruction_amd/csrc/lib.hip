@@ -166,21 +166,24 @@ static Knobs read_knobs() {
     k.ab = env_knob("SFMHIP_AB", 0);
     return k;
 }
-static Knobs g_knobs;
-static std::once_flag g_knobs_once;
+// Immutable snapshots: knobs() copies the current one out under the lock, so a reload while
+// another thread is inside a library call never hands that call a torn mix of old and new
+// values (superseded snapshots are kept: a reload is a test-time event, a few dozen bytes each).
 static std::mutex g_knobs_mu;
-const Knobs& knobs() {
-    std::call_once(g_knobs_once, [] { g_knobs = read_knobs(); });
-    return g_knobs;
+static const Knobs* g_knobs = nullptr;
+Knobs knobs() {
+    std::lock_guard<std::mutex> lk(g_knobs_mu);
+    if (!g_knobs) g_knobs = new Knobs(read_knobs());
+    return *g_knobs;
 }
 }  // namespace sfmhip
 
 // Re-read the runtime knobs from the environment (tests that switch a knob between
-// calls; not thread-safe against concurrent library calls).
+// calls); calls already running keep the snapshot they took.
 extern "C" int sfmhip_knobs_reload(void) {
-    (void)sfmhip::knobs();
+    const sfmhip::Knobs* k = new sfmhip::Knobs(sfmhip::read_knobs());
     std::lock_guard<std::mutex> lk(sfmhip::g_knobs_mu);
-    sfmhip::g_knobs = sfmhip::read_knobs();
+    sfmhip::g_knobs = k;
     return SFMHIP_OK;
 }
 
@@ -215,7 +218,9 @@ extern "C" int sfmhip_scratch_trim(uint64_t keep) {
 extern "C" int sfmhip_device_arch(char* buf, int len) {
     SFMHIP_REQUIRE(buf != nullptr && len > 0, "sfmhip_device_arch: null buffer");
     hipDeviceProp_t prop;
-    hipError_t e = hipGetDeviceProperties(&prop, 0);
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipGetDeviceProperties(&prop, dev);
     if (e != hipSuccess) {
         sfmhip::set_error("hipGetDeviceProperties: %s", hipGetErrorString(e));
         return SFMHIP_E_HIP;

@@ -199,6 +199,27 @@ struct CertArgs {
     int force;            // 1: no row is certified (every row takes the exact path; tests)
 };
 constexpr int kUndecidedBase = -3;   // matches0 = kUndecidedBase - D2 marks an undecided row
+// int16 graphs (m_pad <= 32767: dist.graph_dtype) carry an upper bound of sqrt(D2) instead:
+// mark = kUndecidedBase - u, u = ceil(8 sqrt(D2)) <= 32640 for d <= 256 (D2 <= 256 * 255^2),
+// so the mark stays above -32768 and the resolve's candidate radius only grows (by < 1/8).
+__device__ __forceinline__ int sqrt8_ceil(int d2) {
+    const long long t = 64LL * d2;
+    int u = (int)ceil(sqrt((double)t));
+    while (u > 0 && (long long)(u - 1) * (u - 1) >= t) --u;
+    while ((long long)u * u < t) ++u;
+    return u;
+}
+template <typename OutT>
+__device__ __forceinline__ int undecided_mark(int d2) {
+    if constexpr (sizeof(OutT) == 2) return kUndecidedBase - sqrt8_ceil(d2);
+    else return kUndecidedBase - d2;
+}
+// an upper bound of sqrt(D2) from a mark (the resolve widens it by 1e-12 relative)
+template <typename OutT>
+__device__ __forceinline__ double mark_sqrt_d2(int mark) {
+    if constexpr (sizeof(OutT) == 2) return (double)(kUndecidedBase - mark) * 0.125;
+    else return sqrt((double)(kUndecidedBase - mark));
+}
 
 // 1 accept, 0 reject, -1 undecided
 __device__ __forceinline__ int certify(int d1, int d2, double E, double inv_s, double rn2, double rd2) {
@@ -216,12 +237,12 @@ __device__ __forceinline__ int certify(int d1, int d2, double E, double inv_s, d
 // One workgroup = one pair x (WAVES * NS * MF) query rows of image a.  Each
 // wave owns NS column tiles of MF query rows as resident B-operand fragments
 // and streams image b's 128-row blocks from the LDS ring (LDS-DMA filled).
-template <int D, int MF, int NS, int WAVES, bool CERT = false>
+template <int D, int MF, int NS, int WAVES, bool CERT = false, typename OutT = int32_t>
 __global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
     const int8_t* __restrict__ desc, const int32_t* __restrict__ norms,
     const int32_t* __restrict__ keys, const int32_t* __restrict__ nk, int m_pad,
     const int32_t* __restrict__ pairs, int n_iblk, int nwg, long long rn2, long long rd2,
-    int32_t* __restrict__ m0, int32_t* __restrict__ dist1, int32_t* __restrict__ dist2, CertArgs ca) {
+    OutT* __restrict__ m0, int32_t* __restrict__ dist1, int32_t* __restrict__ dist2, CertArgs ca) {
     using S = Stager<D, WAVES>;
     using M = Mfma<MF>;
     using acc_t = typename M::acc_t;
@@ -245,7 +266,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the LDS-DMA M0 addresses stay scalar
     const int grp = lane / MF, lr = lane % MF;
     const int ibase = ib * IB + wave * IW;
-    int32_t* out_m = m0 + (size_t)pair * m_pad;
+    OutT* out_m = m0 + (size_t)pair * m_pad;
 
     if (ib * IB >= na_rows || nb_rows < 2) {  // block-uniform: nothing to match
         const int iend = min(ib * IB + IB, m_pad);
@@ -374,12 +395,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void match_kernel(
                 const int v = ca.force ? -1
                                        : certify(d1, d2, ca.erow[(size_t)a * m_pad + i] + ca.eimg[b], ca.inv_s,
                                                  (double)rn2, (double)rd2);
-                res = v > 0 ? g1i[s] : (v == 0 ? -1 : kUndecidedBase - d2);
+                res = v > 0 ? g1i[s] : (v == 0 ? -1 : undecided_mark<OutT>(d2));
             } else if (rd2 * (long long)d1 < rn2 * (long long)d2) {
                 res = g1i[s];
             }
         }
-        out_m[i] = res;
+        out_m[i] = (OutT)res;
         if (dist1) dist1[(size_t)pair * m_pad + i] = d1;
         if (dist2) dist2[(size_t)pair * m_pad + i] = d2;
     }
@@ -947,17 +968,16 @@ __device__ unsigned long long g_rprof[16];
 #endif
 // One undecided row e (its mark = kUndecidedBase - D2) by one wave; sxa / sqa / scand: the wave's
 // LDS rows.
-template <int D>
+template <int D, typename OutT>
 __device__ __forceinline__ void resolve_row(int64_t e, int mark, const int8_t* __restrict__ q,
                                             const float* __restrict__ x, const int32_t* __restrict__ nk, int m_pad,
                                             const int32_t* __restrict__ pairs, const double* __restrict__ erow,
                                             const double* __restrict__ eimg, double s, double rn2, double rd2,
-                                            int32_t* __restrict__ m0, unsigned* __restrict__ n_resolved, float* sxa,
+                                            OutT* __restrict__ m0, unsigned* __restrict__ n_resolved, float* sxa,
                                             int* sqa, int* scand, int lane) {
     constexpr int W4 = D / 4;
     const int pair = (int)(e / m_pad), i = (int)(e % m_pad);
     const int a = pairs[2 * pair], b = pairs[2 * pair + 1], nb = nk[b];
-    const int d2q = kUndecidedBase - mark;
     const size_t arow = (size_t)a * m_pad + i;
     for (int k = lane; k < D; k += 64) sxa[k] = x[arow * D + k];
     for (int w = lane; w < W4; w += 64) sqa[w] = reinterpret_cast<const int*>(q + arow * D)[w];
@@ -970,7 +990,7 @@ __device__ __forceinline__ void resolve_row(int64_t e, int mark, const int8_t* _
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) na += __shfl_xor(na, off);
     const double se = (erow[arow] + eimg[b]) * s * (1.0 + 1e-12);
-    const double bq = (se + (sqrt((double)d2q) + se) * (1.0 + 1e-12)) * (1.0 + 1e-12);
+    const double bq = (se + (mark_sqrt_d2<OutT>(mark) + se) * (1.0 + 1e-12)) * (1.0 + 1e-12);
     const double tq = floor(bq * bq) + 1.0;   // every j with D_j <= tq may reach the top two
     int ncand = 0;
     for (int j0 = 0; j0 < nb; j0 += 64) {
@@ -1039,19 +1059,19 @@ __device__ __forceinline__ void resolve_row(int64_t e, int mark, const int8_t* _
     const double p2 = rn2 * v2, e2 = __builtin_fma(rn2, v2, -p2);
     const bool acc_ok = p1 < p2 || (p1 == p2 && e1 < e2);
     if (lane == 0) {
-        m0[e] = acc_ok ? j1 : -1;
+        m0[e] = (OutT)(acc_ok ? j1 : -1);
         if (n_resolved) atomicAdd(n_resolved, 1u);
     }
     __builtin_amdgcn_wave_barrier();   // LDS rows reused by the next marked row
 }
 
-template <int D>
+template <int D, typename OutT>
 __global__ __launch_bounds__(256) void match_resolve_kernel(const int8_t* __restrict__ q, const float* __restrict__ x,
                                                             const int32_t* __restrict__ nk, int m_pad,
                                                             const int32_t* __restrict__ pairs, int P,
                                                             const double* __restrict__ erow,
                                                             const double* __restrict__ eimg, double s, double rn2,
-                                                            double rd2, int32_t* __restrict__ m0,
+                                                            double rd2, OutT* __restrict__ m0,
                                                             unsigned* __restrict__ n_resolved,
                                                             const unsigned* __restrict__ overflow = nullptr) {
     if (overflow && *overflow == 0u) return;   // the bucketed pass below settled every row
@@ -1064,12 +1084,12 @@ __global__ __launch_bounds__(256) void match_resolve_kernel(const int8_t* __rest
     const int64_t nchunk = (total + 63) >> 6;
     for (int64_t c = (int64_t)blockIdx.x * 4 + wave; c < nchunk; c += (int64_t)gridDim.x * 4) {
         const int64_t e0 = c << 6;
-        const int v = (e0 + lane < total) ? m0[e0 + lane] : -1;
+        const int v = (e0 + lane < total) ? (int)m0[e0 + lane] : -1;
         unsigned long long bal = __ballot(v <= kUndecidedBase);
         while (bal) {
             const int l = __builtin_ctzll(bal);
             bal &= bal - 1;
-            resolve_row<D>(e0 + l, __shfl(v, l), q, x, nk, m_pad, pairs, erow, eimg, s, rn2, rd2, m0, n_resolved,
+            resolve_row<D, OutT>(e0 + l, __shfl(v, l), q, x, nk, m_pad, pairs, erow, eimg, s, rn2, rd2, m0, n_resolved,
                            sxa[wave], sqa[wave], scand[wave], lane);
         }
     }
@@ -1081,7 +1101,8 @@ __global__ __launch_bounds__(256) void match_resolve_kernel(const int8_t* __rest
 // rows — the candidate prefilter reads all of them, 1 MB per row at C3 — are read once per batch.
 // A bucket overflow sets *overflow and match_resolve_kernel's graph scan settles every row instead.
 constexpr int kResolveBucket = 4096;
-__global__ __launch_bounds__(256) void resolve_collect_kernel(const int32_t* __restrict__ m0, int64_t total, int m_pad,
+template <typename OutT>
+__global__ __launch_bounds__(256) void resolve_collect_kernel(const OutT* __restrict__ m0, int64_t total, int m_pad,
                                                               const int32_t* __restrict__ pairs,
                                                               unsigned* __restrict__ cnt, int64_t* __restrict__ list,
                                                               unsigned* __restrict__ overflow) {
@@ -1091,15 +1112,33 @@ __global__ __launch_bounds__(256) void resolve_collect_kernel(const int32_t* __r
         if (slot < (unsigned)kResolveBucket) list[(size_t)b * kResolveBucket + slot] = e;
         else atomicOr(overflow, 1u);
     };
-    const int64_t n4 = total >> 2;   // m_pad is a multiple of 128: the graph is whole int4s
+    constexpr int PER = 16 / sizeof(OutT);   // entries per 16-B load (m_pad % 128 == 0: whole loads)
+    const int64_t n4 = total / PER;
     const int4* m4 = reinterpret_cast<const int4*>(m0);
     for (int64_t e4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e4 < n4; e4 += (int64_t)gridDim.x * blockDim.x) {
         const int4 v = m4[e4];
-        if (min(min(v.x, v.y), min(v.z, v.w)) > kUndecidedBase) continue;
-        if (v.x <= kUndecidedBase) take(4 * e4);
-        if (v.y <= kUndecidedBase) take(4 * e4 + 1);
-        if (v.z <= kUndecidedBase) take(4 * e4 + 2);
-        if (v.w <= kUndecidedBase) take(4 * e4 + 3);
+        if constexpr (sizeof(OutT) == 2) {
+            // 8 int16 entries: a mark is <= -3, i.e. in 0x8000..0xFFFD as an unsigned half
+            const unsigned w[4] = {(unsigned)v.x, (unsigned)v.y, (unsigned)v.z, (unsigned)v.w};
+            bool any = false;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                any |= (short)(w[h] & 0xFFFFu) <= kUndecidedBase;
+                any |= (short)(w[h] >> 16) <= kUndecidedBase;
+            }
+            if (!any) continue;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                if ((short)(w[h] & 0xFFFFu) <= kUndecidedBase) take(PER * e4 + 2 * h);
+                if ((short)(w[h] >> 16) <= kUndecidedBase) take(PER * e4 + 2 * h + 1);
+            }
+        } else {
+            if (min(min(v.x, v.y), min(v.z, v.w)) > kUndecidedBase) continue;
+            if (v.x <= kUndecidedBase) take(4 * e4);
+            if (v.y <= kUndecidedBase) take(4 * e4 + 1);
+            if (v.z <= kUndecidedBase) take(4 * e4 + 2);
+            if (v.w <= kUndecidedBase) take(4 * e4 + 3);
+        }
     }
 }
 
@@ -1208,12 +1247,12 @@ __global__ __launch_bounds__(256) void resolve_flatten_kernel(const unsigned* __
 // distances of each row's candidates by one wave per row (any order: a tie-aware top two, lowest
 // index on equal distances) — resolve_row's result.  At C3 a row keeps ~2 candidates, so the
 // prefilter (4096 int8 rows of image b per row in the per-row form) is most of the work.
-template <int D>
+template <int D, typename OutT>
 __global__ __launch_bounds__(256) void match_resolve_batched_kernel(
     const int8_t* __restrict__ q /* the matcher's (shifted) int8 operands */, const int32_t* __restrict__ norms,
     const float* __restrict__ x, const int32_t* __restrict__ nk, int m_pad,
     const int32_t* __restrict__ pairs, int n_img, const double* __restrict__ erow, const double* __restrict__ eimg,
-    double s, double rn2, double rd2, int32_t* __restrict__ m0, unsigned* __restrict__ n_resolved,
+    double s, double rn2, double rd2, OutT* __restrict__ m0, unsigned* __restrict__ n_resolved,
     const int64_t* __restrict__ flat, const int* __restrict__ items, const unsigned* __restrict__ ir,
     const unsigned* __restrict__ overflow) {
     constexpr int W4 = D / 4, R = kResolveRows;
@@ -1253,9 +1292,8 @@ __global__ __launch_bounds__(256) void match_resolve_batched_kernel(
             if (lane == 0) {
                 const int64_t e = flat[f0 + r];
                 const size_t arow = (size_t)pairs[2 * (int)(e / m_pad)] * m_pad + (int)(e % m_pad);
-                const int d2q = kUndecidedBase - m0[e];
                 const double se = (erow[arow] + eimg[b]) * s * (1.0 + 1e-12);
-                const double bq = (se + (sqrt((double)d2q) + se) * (1.0 + 1e-12)) * (1.0 + 1e-12);
+                const double bq = (se + (mark_sqrt_d2<OutT>((int)m0[e]) + se) * (1.0 + 1e-12)) * (1.0 + 1e-12);
                 stq[r] = floor(bq * bq) + 1.0;   // every j with D_j <= tq may reach the top two
                 sna[r] = na;
                 sccd[r] = norms[arow] - na;   // the matcher's norms carry c^2 d of its operand shift c
@@ -1353,7 +1391,7 @@ __global__ __launch_bounds__(256) void match_resolve_batched_kernel(
             const double p2 = rn2 * v2, e2 = __builtin_fma(rn2, v2, -p2);
             const bool acc_ok = p1 < p2 || (p1 == p2 && e1 < e2);
             if (lane == 0) {
-                m0[se_[r]] = acc_ok ? j1 : -1;
+                m0[se_[r]] = (OutT)(acc_ok ? j1 : -1);
                 if (n_resolved) atomicAdd(n_resolved, 1u);
             }
         }
@@ -1450,10 +1488,11 @@ extern "C" int sfmhip_desc_prepare_shifted(const int8_t* desc, int n_img, int m_
     return check_launch("prepare_shifted_kernel");
 }
 
-extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, const int32_t* keys,
-                                  const int32_t* n_kpts, int n_img, int m_pad, int d,
-                                  const int32_t* pairs, int P, int ratio_num, int ratio_den,
-                                  int32_t* matches0, int32_t* dist1, int32_t* dist2, void* stream) {
+template <typename OutT>
+static int match_pairs_impl(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                            const int32_t* n_kpts, int n_img, int m_pad, int d,
+                            const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                            OutT* matches0, int32_t* dist1, int32_t* dist2, void* stream) {
     SFMHIP_REQUIRE(desc && norms && keys && n_kpts && pairs && matches0,
                    "sfmhip_match_pairs: null pointer");
     SFMHIP_REQUIRE(n_img > 0 && P >= 0, "sfmhip_match_pairs: bad counts");
@@ -1469,8 +1508,10 @@ extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, cons
     const int nwg = (int)nwg64;
     const long long rn2 = (long long)ratio_num * ratio_num, rd2 = (long long)ratio_den * ratio_den;
     hipStream_t s = as_stream(stream);
+    if constexpr (sizeof(OutT) == 2)
+        SFMHIP_REQUIRE(m_pad <= 32767, "sfmhip_match_pairs_i16: m_pad must be <= 32767 for an int16 graph");
 #define SFMHIP_LAUNCH_MATCH(DD, MF, NS, WW)                                                              \
-    hipLaunchKernelGGL((match_kernel<DD, MF, NS, WW>), dim3(nwg), dim3(64 * WW), 0, s, desc, norms, keys, \
+    hipLaunchKernelGGL((match_kernel<DD, MF, NS, WW, false, OutT>), dim3(nwg), dim3(64 * WW), 0, s, desc, norms, keys, \
                        n_kpts, m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2, CertArgs{})
 #define SFMHIP_LAUNCH_D(DD) SFMHIP_LAUNCH_MATCH(DD, 16, 4, 4)
     switch (d) {
@@ -1484,6 +1525,22 @@ extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, cons
 #undef SFMHIP_LAUNCH_D
 #undef SFMHIP_LAUNCH_MATCH
     return check_launch("match_kernel");
+}
+
+extern "C" int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                                  const int32_t* n_kpts, int n_img, int m_pad, int d,
+                                  const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                                  int32_t* matches0, int32_t* dist1, int32_t* dist2, void* stream) {
+    return match_pairs_impl(desc, norms, keys, n_kpts, n_img, m_pad, d, pairs, P, ratio_num, ratio_den, matches0,
+                            dist1, dist2, stream);
+}
+
+extern "C" int sfmhip_match_pairs_i16(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                                      const int32_t* n_kpts, int n_img, int m_pad, int d,
+                                      const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                                      int16_t* matches0, void* stream) {
+    return match_pairs_impl(desc, norms, keys, n_kpts, n_img, m_pad, d, pairs, P, ratio_num, ratio_den, matches0,
+                            (int32_t*)nullptr, (int32_t*)nullptr, stream);
 }
 
 extern "C" int sfmhip_mutual_filter(int32_t* matches0, int32_t* matches1, int P, int m_pad, void* stream) {
@@ -1584,12 +1641,13 @@ extern "C" int sfmhip_desc_residual(const float* desc_f, const int8_t* desc_q, i
     return check_launch("desc_residual_kernel");
 }
 
-extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms, const int32_t* keys,
-                                        const int8_t* desc_q, const float* desc_f, const double* resid_row,
-                                        const double* resid_img, int mode, const int32_t* n_kpts, int n_img,
-                                        int m_pad, int d, const int32_t* pairs, int P, int ratio_num, int ratio_den,
-                                        int32_t* matches0, int32_t* dist1, int32_t* dist2, uint32_t* n_resolved,
-                                        void* stream) {
+template <typename OutT>
+static int match_exact_impl(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                            const int8_t* desc_q, const float* desc_f, const double* resid_row,
+                            const double* resid_img, int mode, const int32_t* n_kpts, int n_img,
+                            int m_pad, int d, const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                            OutT* matches0, int32_t* dist1, int32_t* dist2, uint32_t* n_resolved,
+                            void* stream) {
     SFMHIP_REQUIRE(desc && norms && keys && desc_q && desc_f && resid_row && resid_img && n_kpts && pairs && matches0,
                    "sfmhip_match_pairs_exact: null pointer");
     SFMHIP_REQUIRE(n_img > 0 && P >= 0, "sfmhip_match_pairs_exact: bad counts");
@@ -1597,6 +1655,8 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
     SFMHIP_REQUIRE(mode == 0 || mode == 1, "sfmhip_match_pairs_exact: mode must be 0 or 1");
     SFMHIP_REQUIRE(ratio_num > 0 && ratio_den > 0 && ratio_num <= 65535 && ratio_den <= 65535,
                    "sfmhip_match_pairs_exact: ratio must be a positive fraction");
+    if constexpr (sizeof(OutT) == 2)
+        SFMHIP_REQUIRE(m_pad <= 32767, "sfmhip_match_pairs_exact_i16: m_pad must be <= 32767 for an int16 graph");
     if (P == 0) return SFMHIP_OK;
     constexpr int IB = 256;   // match_kernel's query rows per workgroup (16x16 tiles, 4 per wave, 4 waves)
     const int n_iblk = ceil_div(m_pad, IB);
@@ -1640,22 +1700,22 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
     }
     const int rxgrid = n_cu * 2;   // a multiple of 8: every XCD gets the same number of blocks
 #define SFMHIP_LAUNCH_EXACT(DD)                                                                                  \
-    hipLaunchKernelGGL((match_kernel<DD, 16, 4, 4, true>), dim3(nwg), dim3(256), 0, s, desc, norms, keys, n_kpts, \
+    hipLaunchKernelGGL((match_kernel<DD, 16, 4, 4, true, OutT>), dim3(nwg), dim3(256), 0, s, desc, norms, keys, n_kpts, \
                        m_pad, pairs, n_iblk, nwg, rn2, rd2, matches0, dist1, dist2, ca);                         \
     if (int rc = check_launch("match_kernel<cert>")) {                                                          \
         scratch_free(rbuf, s);                                                                                    \
         return rc;                                                                                                \
     }                                                                                                             \
-    hipLaunchKernelGGL(resolve_collect_kernel, dim3(rgrid), dim3(256), 0, s, matches0, total, m_pad, pairs, rcnt,  \
+    hipLaunchKernelGGL(resolve_collect_kernel<OutT>, dim3(rgrid), dim3(256), 0, s, matches0, total, m_pad, pairs, rcnt,  \
                        rlist, rflag);                                                                             \
     hipLaunchKernelGGL(resolve_offsets_kernel, dim3(1), dim3(1024), 0, s, rcnt, n_img, roff, rokey, roimg, rxr,      \
                        ritems, rir, rflag);                                                                       \
     hipLaunchKernelGGL(resolve_flatten_kernel, dim3(n_cu), dim3(256), 0, s, rokey, roimg, n_img, rlist, rflat,     \
                        rflag);                                                                                    \
-    hipLaunchKernelGGL((match_resolve_batched_kernel<DD>), dim3(rxgrid), dim3(256), 0, s, desc, norms, desc_f, n_kpts,  \
+    hipLaunchKernelGGL((match_resolve_batched_kernel<DD, OutT>), dim3(rxgrid), dim3(256), 0, s, desc, norms, desc_f, n_kpts,  \
                        m_pad, pairs, n_img, resid_row, resid_img, mode == 0 ? 1.0 : 127.0, (double)rn2,          \
                        (double)rd2, matches0, n_resolved, rflat, ritems, rir, rflag);                              \
-    hipLaunchKernelGGL((match_resolve_kernel<DD>), dim3(rgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts, m_pad,   \
+    hipLaunchKernelGGL((match_resolve_kernel<DD, OutT>), dim3(rgrid), dim3(256), 0, s, desc_q, desc_f, n_kpts, m_pad,   \
                        pairs, P, resid_row, resid_img, mode == 0 ? 1.0 : 127.0, (double)rn2, (double)rd2,        \
                        matches0, n_resolved, rflag)
     switch (d) {
@@ -1671,4 +1731,24 @@ extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms
     const int rc = check_launch("match_resolve_kernel");
     scratch_free(rbuf, s);
     return rc;
+}
+
+extern "C" int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                                        const int8_t* desc_q, const float* desc_f, const double* resid_row,
+                                        const double* resid_img, int mode, const int32_t* n_kpts, int n_img,
+                                        int m_pad, int d, const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                                        int32_t* matches0, int32_t* dist1, int32_t* dist2, uint32_t* n_resolved,
+                                        void* stream) {
+    return match_exact_impl(desc, norms, keys, desc_q, desc_f, resid_row, resid_img, mode, n_kpts, n_img, m_pad, d,
+                            pairs, P, ratio_num, ratio_den, matches0, dist1, dist2, n_resolved, stream);
+}
+
+extern "C" int sfmhip_match_pairs_exact_i16(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                                            const int8_t* desc_q, const float* desc_f, const double* resid_row,
+                                            const double* resid_img, int mode, const int32_t* n_kpts, int n_img,
+                                            int m_pad, int d, const int32_t* pairs, int P, int ratio_num,
+                                            int ratio_den, int16_t* matches0, uint32_t* n_resolved, void* stream) {
+    return match_exact_impl(desc, norms, keys, desc_q, desc_f, resid_row, resid_img, mode, n_kpts, n_img, m_pad, d,
+                            pairs, P, ratio_num, ratio_den, matches0, (int32_t*)nullptr, (int32_t*)nullptr,
+                            n_resolved, stream);
 }

@@ -121,7 +121,7 @@ __device__ __forceinline__ int box_footprint(const CullCam& cc, const CullGeom& 
     const double cyw = G.mn[1] + 0.5 * (ya + yb) * G.s[1], hy = 0.5 * (yb - ya) * G.as[1];
     const double czw = G.mn[2] + 0.5 * (za + zb) * G.s[2], hz = 0.5 * (zb - za) * G.as[2];
     const double mxw = fabs(cxw) + hx, myw = fabs(cyw) + hy, mzw = fabs(czw) + hz;   // |coord| bounds
-    double c[3], e[3], mag[3];
+    double c[3], e[3], mag[3], magm[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const double* p = cc.P + 4 * r;
@@ -129,17 +129,24 @@ __device__ __forceinline__ int box_footprint(const CullCam& cc, const CullGeom& 
         c[r] = p[0] * cxw + p[1] * cyw + p[2] * czw + p[3];
         e[r] = a[0] * hx + a[1] * hy + a[2] * hz;
         mag[r] = a[0] * mxw + a[1] * myw + a[2] * mzw + a[3];
+        magm[r] = a[0] * fabs(G.mn[0]) + a[1] * fabs(G.mn[1]) + a[2] * fabs(G.mn[2]);
     }
-    // f32 error of the kernel's Zc / Xc / Yc (unit roundoff 2^-24, generous op counts)
+    // f32 error of the kernel's Zc / Xc / Yc (unit roundoff u = 2^-24).  The kernel's voxel
+    // coordinate v' = fl(mn + fl(i fl(fl(mx - mn) / (R - 1)))) is within u (4.01 |v| + 3.01 |mn|)
+    // of this f64 model's v — a term in |mn| that does not shrink with |v| (a camera inside a
+    // grid with a large |bmin|) — and the row's four products and three sums add at most
+    // 4 u (sum |P_rj| |v_j| + |P_r3|): so 10 u mag + 4 u sum_j |P_rj| |mn_j| covers both.
     const double eps = 0x1p-24;
-    const double dz = 8 * eps * mag[2];
-    zlo = c[2] - e[2] - dz;
-    zhi = c[2] + e[2] + dz;
+    double dr[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) dr[r] = 10 * eps * mag[r] + 4 * eps * magm[r];
+    zlo = c[2] - e[2] - dr[2];
+    zhi = c[2] + e[2] + dr[2];
     inside = false;
     if (!(zlo > 1e-3 && zhi < 1e30 && c[0] == c[0] && c[1] == c[1])) return 0;
     const double izl = cull_rcp(zlo), izh = cull_rcp(zhi);
-    const double xl = c[0] - e[0] - 8 * eps * mag[0], xh = c[0] + e[0] + 8 * eps * mag[0];
-    const double yl = c[1] - e[1] - 8 * eps * mag[1], yh = c[1] + e[1] + 8 * eps * mag[1];
+    const double xl = c[0] - e[0] - dr[0], xh = c[0] + e[0] + dr[0];
+    const double yl = c[1] - e[1] - dr[1], yh = c[1] + e[1] + dr[1];
     const double qx0 = fmin(fmin(xl * izl, xl * izh), fmin(xh * izl, xh * izh));
     const double qx1 = fmax(fmax(xl * izl, xl * izh), fmax(xh * izl, xh * izh));
     const double qy0 = fmin(fmin(yl * izl, yl * izh), fmin(yh * izl, yh * izh));
@@ -880,7 +887,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const SlotMap sm = make_slot_map(nbx, nby, nbz);
     const int64_t main_slots = (int64_t)sm.per * kNumXcd;
     SFMHIP_REQUIRE(main_slots < INT_MAX / 2, "sfmhip_tsdf_integrate: grid too large");
-    const Knobs& kn = knobs();
+    const Knobs kn = knobs();
     int ncu = 256;
     {
         int dev = 0;

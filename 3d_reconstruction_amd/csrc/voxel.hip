@@ -1211,17 +1211,3 @@ extern "C" int sfmhip_stratified_samples(const float* t_near, const float* t_far
                        t_rand, B, S, perturb, z);
     return check_launch("stratified_kernel");
 }
-
-#ifdef SFMHIP_TSDF_PROF
-extern "C" int sfmhip_tsdf_prof_read(unsigned long long* host, int n_waves, int clear) {
-    const int n = std::min(n_waves, kTsdfProfWaves) * 3;
-    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tsdf_prof), (size_t)n * sizeof(unsigned long long)) != hipSuccess)
-        return -1;
-    if (clear) {
-        static std::vector<unsigned long long> z((size_t)kTsdfProfWaves * 3, 0ull);
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tsdf_prof), z.data(), z.size() * sizeof(unsigned long long)) != hipSuccess)
-            return -1;
-    }
-    return 0;
-}
-#endif

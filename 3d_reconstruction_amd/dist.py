@@ -252,11 +252,9 @@ def match_all_pairs_sharded(bank, pairs, ratio=0.75, exact=None, comm: RcclComm 
     if chunks is None:
         chunks = 4 if world > 1 else 1
     per = -(-P // (world * chunks)) if P else 0
-    buf = torch.empty((max(per, 1), m_pad), dtype=torch.int32, device=dvc)
 
-    def compute(lo, hi, out):
-        m = bank.match(pr[lo:hi], ratio=ratio, out=buf[: hi - lo], exact=exact)
-        out.copy_(m)
+    def compute(lo, hi, out):   # the kernels write the graph dtype (int16 / int32) in place
+        bank.match(pr[lo:hi], ratio=ratio, out=out, exact=exact)
 
     if world == 1 and comm is None:
         full = torch.empty((P, m_pad), dtype=dt, device=dvc)

@@ -171,7 +171,10 @@ class DescriptorBank:
         ``with_dist`` also int32 squared distances ``dist1``, ``dist2`` (of the
         int8 quantisation); with ``mutual`` also the backward ``matches1``
         after the mutual filter.  ``exact`` (default: the bank's mode) selects
-        the exact float distance (module docstring).
+        the exact float distance (module docstring).  ``out``: a caller-owned
+        contiguous [P, m_pad] int32 or int16 tensor (int16: m_pad <= 32767, the
+        kernels write the int16 graph directly — dist.match_all_pairs_sharded's
+        all-gathered form — without distances or the mutual filter).
         """
         exact = self.exact if exact is None else bool(exact)
         if exact and self.x is None:
@@ -182,6 +185,15 @@ class DescriptorBank:
         P = pr.shape[0]
         dv = self.q.device
         m0 = out if out is not None else torch.empty((P, self.m_pad), dtype=torch.int32, device=dv)
+        if m0.dtype == torch.int16:
+            if with_dist or mutual:
+                raise ValueError("an int16 graph has no distance outputs or mutual filter: use an int32 out")
+            if self.m_pad > 32767:
+                raise ValueError(f"an int16 graph needs m_pad <= 32767, got {self.m_pad}")
+        elif m0.dtype != torch.int32:
+            raise ValueError(f"out must be int32 or int16, got {m0.dtype}")
+        if tuple(m0.shape) != (P, self.m_pad) or not m0.is_contiguous() or m0.device != dv:
+            raise ValueError(f"out must be a contiguous ({P}, {self.m_pad}) tensor on {dv}")
         d1 = torch.empty_like(m0) if with_dist else None
         d2 = torch.empty_like(m0) if with_dist else None
         self._launch(pr, num, den, m0, d1, d2)
@@ -196,6 +208,17 @@ class DescriptorBank:
 
     def _launch(self, pr, num, den, m0, d1, d2, exact: bool | None = None):
         exact = getattr(self, "_exact_now", False) if exact is None else exact
+        i16 = m0.dtype == torch.int16
+        if exact and i16:
+            call("sfmhip_match_pairs_exact_i16", ptr(self.qm), ptr(self.norms), ptr(self.keys), ptr(self.q),
+                 ptr(self.x), ptr(self.erow), ptr(self.eimg), self.mode, ptr(self.n_kpts), self.n_img, self.m_pad,
+                 self.d, ptr(pr), int(pr.shape[0]), num, den, ptr(m0), ptr(self._nres), stream_ptr())
+            self.last_resolved = self._nres
+            return
+        if i16:
+            call("sfmhip_match_pairs_i16", ptr(self.qm), ptr(self.norms), ptr(self.keys), ptr(self.n_kpts),
+                 self.n_img, self.m_pad, self.d, ptr(pr), int(pr.shape[0]), num, den, ptr(m0), stream_ptr())
+            return
         if exact:
             call("sfmhip_match_pairs_exact", ptr(self.qm), ptr(self.norms), ptr(self.keys), ptr(self.q), ptr(self.x),
                  ptr(self.erow), ptr(self.eimg), self.mode, ptr(self.n_kpts), self.n_img, self.m_pad, self.d,

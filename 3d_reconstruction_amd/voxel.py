@@ -226,7 +226,19 @@ def tsdf_integrate(T: torch.Tensor, Wt: torch.Tensor, depth: torch.Tensor, poses
     K (F,4) [fx, fy, cx, cy] f32, bounds in world units, trunc = mu.
     block_table: optional (F, ceil(Hd/16), ceil(Wd/16), 2) f32 device table from
     tsdf_block_table (e.g. assembled across ranks by dist.shared_block_table);
-    the result is bit-identical, the call's own pass over the depth maps skipped."""
+    the result is bit-identical, the call's own pass over the depth maps skipped.
+
+    Batching: the frames of ONE call are fused order-free in integration steps of
+    at most 512 frames (integer fixed-point sums S = sum rint(tsdf 2^21), n = #updates,
+    then one finish per voxel and step: T' = (T W + S 2^-21) / (W + n); include/sfmhip.h
+    V5 block).  The result therefore depends on how frames are grouped into calls:
+    one call with F <= 512 frames gives different low bits than F calls of one frame
+    (each a step of its own), and both differ from a sequential running average
+    T <- (T W + tsdf)/(W + 1) by at most ~2^-22 per update.  Any z-slab / rank split
+    of one call is bit-identical to the whole call.  A caller that streams frames and
+    needs batching-independent bits integrates them one frame per call (each frame
+    its own step, which IS the sequential running average up to the 2^-21 quantum).
+    There is no TSDF in the reference (build-defined)."""
     gpu = require_gpu()
     if T.dtype != torch.float32 or Wt.dtype != torch.float32 or not T.is_contiguous() or not Wt.is_contiguous():
         raise ValueError("T and Wt must be contiguous float32 device tensors")

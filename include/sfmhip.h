@@ -106,6 +106,14 @@ int sfmhip_match_pairs(const int8_t* desc, const int32_t* norms, const int32_t* 
                        int32_t* matches0 /* [P][m_pad] */,
                        int32_t* dist1, int32_t* dist2, void* stream);
 
+/* The same graph written as int16 (the all-gathered match graph of SURVEY.md §8e,
+ * replacing the matching.py:122-128 per-pair LightGlue call over every pair):
+ * matches0 entries are identical values; m_pad <= 32767; no distance outputs.  */
+int sfmhip_match_pairs_i16(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                           const int32_t* n_kpts, int n_img, int m_pad, int d,
+                           const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                           int16_t* matches0 /* [P][m_pad] */, void* stream);
+
 /* LightGlue-style mutual filter (lightglue/lightglue.py:235-254 semantics):
  * given forward matches0 (a->b) and backward matches1 (b->a), both [P][m_pad],
  * clear every match that is not mutual, in place.                           */
@@ -137,6 +145,17 @@ int sfmhip_match_pairs_exact(const int8_t* desc, const int32_t* norms, const int
                              const int32_t* pairs, int P, int ratio_num, int ratio_den,
                              int32_t* matches0, int32_t* dist1, int32_t* dist2, uint32_t* n_resolved,
                              void* stream);
+
+/* sfmhip_match_pairs_exact writing the int16 graph directly (the bench's and
+ * dist.match_all_pairs_sharded's graph dtype while m_pad <= 32767; matching.py:122-128
+ * over every pair): the same matches0 values, no distance outputs.  Undecided rows
+ * carry ceil(8 sqrt(D2)) in their transient mark instead of D2 (a wider candidate
+ * radius for the exact pass, never a different result).                      */
+int sfmhip_match_pairs_exact_i16(const int8_t* desc, const int32_t* norms, const int32_t* keys,
+                                 const int8_t* desc_q, const float* desc_f, const double* resid_row,
+                                 const double* resid_img, int mode, const int32_t* n_kpts, int n_img, int m_pad,
+                                 int d, const int32_t* pairs, int P, int ratio_num, int ratio_den,
+                                 int16_t* matches0, uint32_t* n_resolved, void* stream);
 
 /* ---- M2: scipy.cluster.vq.vq (matching.py:27, bow.py:23) ---------------
  * codes[i] = argmin_c sum_k (obs[i,k]-code[c,k])^2 (lowest index on ties),

@@ -161,6 +161,30 @@ def bf_match_exact(xa, xb, ratio=(3, 4), mutual: bool = False, return_dist: bool
     return (m0, d1, d2) if return_dist else m0
 
 
+def bf_match_gemm_f32(xa, xb, ratio=(3, 4)):
+    """The host path a numpy user would run at the matching.py:122 call site
+    ("numpy oracle GEMM-form", the survey's 192 ms/pair probe):
+    f32 d = |a|^2 + |b|^2 - 2 A @ B.T, top two by argpartition, ratio test on
+    the f32 values.  bench.py's CPU baseline for the float headline times THIS
+    form; it is not the parity oracle (its f32 rounding can reorder near-ties,
+    which bf_match_exact decides exactly)."""
+    num, den = ratio
+    A = np.asarray(xa, np.float32)
+    B = np.asarray(xb, np.float32)
+    M, N = A.shape[0], B.shape[0]
+    if M == 0 or N < 2:
+        return np.full(M, -1, np.int64)
+    D = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - np.float32(2) * (A @ B.T)
+    p = np.argpartition(D, 1, axis=1)[:, :2]
+    r = np.arange(M)
+    da, db = D[r, p[:, 0]], D[r, p[:, 1]]
+    first = (da < db) | ((da == db) & (p[:, 0] < p[:, 1]))
+    j1 = np.where(first, p[:, 0], p[:, 1])
+    d1, d2 = np.minimum(da, db), np.maximum(da, db)
+    ok = np.float32(den * den) * d1 < np.float32(num * num) * d2
+    return np.where(ok, j1, -1).astype(np.int64)
+
+
 def bf_match_exact_mutual_pair(xa, xb, ratio=(3, 4)):
     """(matches0, matches1) of the exact float mode after the mutual filter."""
     return bf_match_exact(xa, xb, ratio, mutual=True), bf_match_exact(xb, xa, ratio, mutual=True)

@@ -37,6 +37,22 @@ def test_cpu_leg_reports_both_thread_counts():
     assert "median of 3" in leg["timing"]
 
 
+def test_gemm_form_baseline_matches_exact_oracle_away_from_ties():
+    """The headline's CPU baseline (numpy f32 GEMM form) does the
+    same matching as the exact oracle: identical matches0 on C3-like descriptors
+    except rows whose ratio test sits within f32 rounding of the threshold."""
+    from oracle import match as om
+    x = syn.superpoint_like(2, 512, 256, seed=5).numpy()
+    a, b = x[0], x[1]
+    g = om.bf_match_gemm_f32(a, b, (3, 4))
+    m, d1, d2 = om.bf_match_exact(a, b, (3, 4), return_dist=True)
+    near = np.abs(16 * d1 - 9 * d2) <= 1e-4 * d2
+    assert (m >= 0).sum() > 20
+    np.testing.assert_array_equal(g[~near], m[~near])
+    assert om.bf_match_gemm_f32(a[:0], b).shape == (0,)
+    assert (om.bf_match_gemm_f32(a[:3], b[:1]) == -1).all()
+
+
 def test_pool_map_keeps_order():
     assert bench.pool_map(lambda i: i * i, range(10), 4) == [i * i for i in range(10)]
     assert bench.pool_map(lambda i: i + 1, [3, 1], 1) == [4, 2]

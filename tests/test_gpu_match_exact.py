@@ -211,3 +211,69 @@ def test_exact_float_resolve_many_images(sfm, gpu, knob, cert):
     assert np.array_equal(m0, _oracle(x, nk, pairs, (3, 4)))
     if cert == "0":
         assert int(bank.last_resolved.item()) == sum(int(nk[a]) for a, b in pairs)
+
+
+def _i16(bank, pairs, **kw):
+    out = torch.empty((len(pairs), bank.m_pad), dtype=torch.int16, device=bank.device)
+    bank.match(pairs, out=out, **kw)
+    return out.cpu().numpy().astype(np.int64)
+
+
+@pytest.mark.parametrize("cert", ["1", "0"])
+@pytest.mark.parametrize("d,kind", [(256, "superpoint"), (128, "sift"), (64, "randn")])
+def test_int16_graph_equals_int32_graph(sfm, gpu, knob, cert, d, kind):
+    """The kernels writing the int16 graph directly (dist.match_all_pairs_sharded's form:
+    sfmhip_match_pairs_exact_i16 / sfmhip_match_pairs_i16) give the int32 graph's values in
+    both modes; with every row undecided (MATCH_CERT=0) each row's transient mark carries
+    ceil(8 sqrt(D2)) instead of D2 and the resolve still settles every row to the oracle's
+    answer (the widest distances: SIFT-range values, clipped randn rows)."""
+    knob("MATCH_CERT", cert)
+    n_img, m = 4, 520
+    if kind == "randn":
+        x = torch.randn((n_img, m, d), generator=torch.Generator().manual_seed(d)).numpy() * 0.6
+    elif kind == "sift":
+        x = syn.sift_like(n_img, m, d, seed=d).numpy() + np.float32(0.37)
+    else:
+        x = syn.superpoint_like(n_img, m, d, seed=d + 1).numpy()
+    nk = np.array([520, 300, 129, 2], np.int32)
+    for i in range(n_img):
+        x[i, nk[i]:] = 0
+    mode = 0 if kind == "sift" else 1
+    pairs = np.array([[0, 1], [1, 0], [0, 2], [2, 0], [3, 0], [0, 3], [1, 1]], np.int32)
+    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=mode, exact=True)
+    for exact in (True, False):
+        g32 = bank.match(pairs, ratio=0.75, exact=exact).cpu().numpy().astype(np.int64)
+        g16 = _i16(bank, pairs, ratio=0.75, exact=exact)
+        assert np.array_equal(g16, g32), exact
+        if exact and cert == "0":
+            assert int(bank.last_resolved.item()) == sum(int(nk[a]) for a, b in pairs if nk[b] >= 2)
+    assert np.array_equal(_i16(bank, pairs, ratio=0.75)[:, :m], _oracle(x, nk, pairs, (3, 4)))
+
+
+def test_int16_graph_resolve_bucket_overflow(sfm, gpu, knob):
+    """int16 graph, more than 4096 undecided rows against one image: the graph-scanning
+    per-row pass reads the int16 marks (the same graph as the int32 run)."""
+    n_img, m, d = 3, 4096, 64
+    x = syn.superpoint_like(n_img, m, d, seed=9).numpy()
+    pairs = np.array([[0, 1], [2, 1], [1, 0]], np.int32)
+    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), mode=1, exact=True)
+    knob("MATCH_CERT", "0")
+    g16 = _i16(bank, pairs, ratio=0.75)
+    assert int(bank.last_resolved.item()) == len(pairs) * m
+    g32 = bank.match(pairs, ratio=0.75).cpu().numpy()
+    assert np.array_equal(g16, g32)
+
+
+def test_int16_graph_sharded_product_api(sfm, gpu):
+    """dist.match_all_pairs_sharded on one rank returns the int16 graph straight from the
+    kernels, equal to the int32 graph of bank.match."""
+    sdist = importlib.import_module("3d_reconstruction_amd.dist")
+    x = syn.superpoint_like(6, 640, 256, seed=4).to(gpu)
+    bank = sfm.DescriptorBank.from_float(x, mode=1, exact=True)
+    pairs = sfm.all_pairs(6)
+    g = sdist.match_all_pairs_sharded(bank, torch.from_numpy(pairs).to(gpu), exact=True)
+    assert g.dtype == torch.int16 and tuple(g.shape) == (len(pairs), bank.m_pad)
+    ref = bank.match(pairs)
+    assert torch.equal(g.long(), ref.long())
+    with pytest.raises(ValueError):
+        bank.match(pairs, out=torch.empty((len(pairs), bank.m_pad), dtype=torch.int16, device=gpu), mutual=True)

@@ -395,6 +395,47 @@ def test_tsdf_free_space_near_trunc_bitexact(sfm, gpu, knob, trunc, lat):
     np.testing.assert_array_equal(T.cpu().numpy(), Tr)
 
 
+@pytest.mark.parametrize("lat", LAT_MODES)
+def test_tsdf_camera_inside_large_grid_near_trunc_bitexact(sfm, gpu, knob, lat):
+    """Cameras at the centre of a grid with a large |bmin| (translation ~0, voxels near
+    the origin: the f32 voxel coordinate's error is set by |bmin|, not |v|), slightly
+    rotated, with planes a few ulps either side of the f32 Zc of a voxel layer + mu (the
+    free-space proof's boundary) and of Zc - mu (the skip boundary): bit-exact."""
+    _set_lat(knob, lat)
+    R, F, Hd, Wd = 48, 8, 64, 80
+    lo, hi = np.float32(-100.0), np.float32(100.0)
+    trunc = np.float32(3.0) * (hi - lo) / np.float32(R - 1)
+    s = (hi - lo) / np.float32(R - 1)
+    zs = lo + np.arange(R, dtype=np.float32) * s            # the kernel's f32 voxel coordinates
+    rng = np.random.default_rng(21)
+    depth = np.empty((F, Hd, Wd), np.float32)
+    poses = np.zeros((F, 3, 4), np.float32)
+    for f in range(F):
+        a = np.float32(0.02 * (f - F / 2))
+        c, sn = np.cos(a), np.sin(a)
+        poses[f, :3, :3] = np.array([[c, 0, sn], [0, 1, 0], [-sn, 0, c]], np.float32)
+        poses[f, :, 3] = rng.uniform(-1e-3, 1e-3, 3).astype(np.float32)
+        zl = zs[R // 2 + 2 + f % 4]
+        edge = zl + trunc if f % 2 == 0 else zl - trunc
+        k = int(rng.integers(-3, 4))
+        depth[f] = edge
+        for _ in range(abs(k)):
+            depth[f] = np.nextafter(depth[f], np.float32(np.inf if k > 0 else -np.inf))
+        depth[f, :, : Wd // 4] = np.nextafter(edge, np.float32(np.inf))
+    K = np.tile(np.array([[40.0, 40.0, Wd / 2, Hd / 2]], np.float32), (F, 1))
+    T0 = rng.uniform(-1, 1, (R, R, R)).astype(np.float32)
+    W0 = rng.integers(0, 3, (R, R, R)).astype(np.float32)
+    T = torch.from_numpy(T0).to(gpu)
+    Wt = torch.from_numpy(W0).to(gpu)
+    bnd = ((lo,) * 3, (hi,) * 3)
+    sfm.tsdf_integrate(T, Wt, torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K), *bnd,
+                       float(trunc))
+    Tr, Wr = ov.tsdf_integrate(T0, W0, depth, poses, K, *bnd, trunc)
+    np.testing.assert_array_equal(Wt.cpu().numpy(), Wr)
+    np.testing.assert_array_equal(T.cpu().numpy(), Tr)
+    assert (Wr > W0).mean() > 0.005
+
+
 @pytest.mark.parametrize("Wd", [96, 97])
 def test_tsdf_block_table_vs_oracle(sfm, gpu, Wd):
     """The pre-pass table ({min, max} per 16x16 block, NaN rules) built in two

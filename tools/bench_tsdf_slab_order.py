@@ -45,6 +45,7 @@ if os.environ.get("NO_TABLE"):   # the single-GPU call: the block pass inside ts
 for name, env in VARIANTS:
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
+    sfm.knobs_reload()   # knobs are read once per process: re-read after every change
     t = timed()
     out = (T[z0:z1].clone(), W[z0:z1].clone())
     same = ref is None or (torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1]))
@@ -55,3 +56,4 @@ for name, env in VARIANTS:
             os.environ.pop(k)
         else:
             os.environ[k] = v
+    sfm.knobs_reload()
