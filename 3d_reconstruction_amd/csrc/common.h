@@ -7,7 +7,6 @@
 #include <stdint.h>
 #include <cstdio>
 #include <cstdarg>
-#include <mutex>
 
 #include "../../include/sfmhip.h"
 
@@ -53,17 +52,6 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 // Return scratch from scratch_alloc (stream-ordered: the next call on the same stream may
 // reuse it at once, its kernels run after this call's).
 void scratch_free(void* p, hipStream_t s);
-
-// Per-device side stream for fork/join inside one call (lib.hip): a lease holds the device's
-// side context locked while the call enqueues (host side only) and hands out kSideEvents
-// events.  The side stream is non-blocking; every hand-off is an explicit event wait.
-constexpr int kSideEvents = 16;
-struct SideLease {
-    hipStream_t s = nullptr;
-    hipEvent_t* ev = nullptr;
-    std::unique_lock<std::mutex> lk;
-};
-bool side_lease(SideLease& L);   // false: no side stream (then run everything on the caller's)
 
 // Runtime knobs (INTEGRATION.md "Runtime knobs"): read from the environment once, at
 // the first call; sfmhip_knobs_reload() re-reads them (tests).  Every other choice is

@@ -150,36 +150,6 @@ void scratch_free(void* p, hipStream_t s) {
     (void)hipFreeAsync(p, s);
 }
 
-struct SideCtx {
-    hipStream_t s = nullptr;
-    hipEvent_t ev[kSideEvents] = {};
-    bool ok = false;
-    std::mutex mu;
-};
-static SideCtx g_side[kMaxDev];
-static std::once_flag g_side_once[kMaxDev];
-
-bool side_lease(SideLease& L) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) {
-        (void)hipGetLastError();
-        return false;
-    }
-    SideCtx& c = g_side[dev];
-    std::call_once(g_side_once[dev], [&c] {
-        bool ok = hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking) == hipSuccess;
-        for (int i = 0; ok && i < kSideEvents; ++i)
-            ok = hipEventCreateWithFlags(&c.ev[i], hipEventDisableTiming) == hipSuccess;
-        c.ok = ok;
-        (void)hipGetLastError();
-    });
-    if (!c.ok) return false;
-    L.lk = std::unique_lock<std::mutex>(c.mu);
-    L.s = c.s;
-    L.ev = c.ev;
-    return true;
-}
-
 static int env_knob(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return e && *e ? std::atoi(e) : dflt;

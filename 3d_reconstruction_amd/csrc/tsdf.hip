@@ -36,7 +36,6 @@
 namespace sfmhip {
 
 constexpr int kTsdfMaxFrames = 512;   // frames per integration step (host splits longer calls)
-constexpr int kTsdfChunk = 64;        // frames per block-pass chunk of a pipelined step (a multiple of 32)
 constexpr int kTsdfQBits = 21;        // tsdf fixed point: |S| <= 512 (2^21 + 1) < 2^31
 static_assert(kTsdfMaxFrames * ((1 << kTsdfQBits) + 1) < INT_MAX, "S must fit an int32");
 constexpr double kTsdfLatencyRounds = 1.0;   // below: latency mode (tsdf_run)
@@ -380,17 +379,16 @@ constexpr int kCullFrames = 16;
 // waves_per_eu(8): two 16-wave workgroups per CU (the f64 frame record lives in SGPRs)
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void tsdf_cull_kernel(
     int H, int W, int z0, int z1, int F, int Hd, int Wd, const CullCam* __restrict__ cams, CullGeom G, float trunc,
-    const float2* __restrict__ bmm, int nbu, int nbv, const int4* __restrict__ range, int nw, int hf0, int nh,
-    int nbricks, const unsigned char* __restrict__ bdec, unsigned short* __restrict__ cull,
-    unsigned short* __restrict__ freem, unsigned* __restrict__ plist, unsigned* __restrict__ pcount,
-    unsigned* __restrict__ tcost) {
+    const float2* __restrict__ bmm, int nbu, int nbv, const int4* __restrict__ range, int nw,
+    const unsigned char* __restrict__ bdec, unsigned short* __restrict__ cull, unsigned short* __restrict__ freem,
+    unsigned* __restrict__ plist, unsigned* __restrict__ pcount, unsigned* __restrict__ tcost) {
     __shared__ unsigned char bits[kCullFrames][64];
     __shared__ unsigned wcnt[kCullFrames + 1];
     const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
     const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
     const int nqx = (ntx + 3) >> 2, nqy = (nty + 3) >> 2;  // 4x4x4 bricks of tiles
-    // this launch: 16-frame halves [hf0, hf0 + nh) of the step's 2 nw (a frame chunk), all bricks
-    const int hf = hf0 + (int)(blockIdx.x % nh), brick = (int)(blockIdx.x / nh);
+    const int nh = 2 * nw;                                  // 16-frame halves
+    const int hf = (int)(blockIdx.x % nh), brick = (int)(blockIdx.x / nh);
     const int l = threadIdx.x & 63, j = threadIdx.x >> 6;
     const int f = hf * kCullFrames + j;
     const int tx = (brick % nqx) * 4 + (l & 3);
@@ -400,7 +398,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const int64_t tile = ((int64_t)tz * nty + ty) * ntx + tx;
     bool skip = false, fre = false;
     // the brick pre-pass's decision for (brick, frame f): wave-uniform
-    const int dec = bdec && f < F ? bdec[(size_t)__builtin_amdgcn_readfirstlane(f) * nbricks + brick] : 0;
+    const int dec = bdec && f < F ? bdec[(size_t)__builtin_amdgcn_readfirstlane(f) * (gridDim.x / nh) + brick] : 0;
     if (tile_ok && f < F && dec) {
         skip = dec == 1;
         fre = dec == 2;
@@ -632,7 +630,7 @@ __global__ __launch_bounds__(256) void tsdf_order_kernel(SlotMap SM, int F, cons
     }
 }
 
-constexpr int kCntPl = 0, kNCnt = 16;  // counters: the refinement list of each frame chunk
+constexpr int kCntPl = 0, kNCnt = 4;   // counters: the refinement list
 
 // Voxel of lane l in wave sub-tile q of tile (bx, by, bz): each 16-lane quarter-wave
 // is a 4x4 (x, z) patch at one y (the orbiting cameras map y to image rows: a compact
@@ -769,36 +767,26 @@ __device__ __forceinline__ void frames_eval(const FrameCtx& c, const int* f, flo
 // phase (so that resident waves gather from the same frames at the same time) and
 // frame-window-major work lists (32-frame windows over the whole grid, partial sums)
 // did not raise the L2 hit rate (23 -> 26 %) and measured slower too.
-// MODE (the frames of one step fused in parts, the order-free sums carried between them):
-//   0  the whole step: mask words [0, nw), voxels finished in place
-//   1  a first part: words [w_lo, w_hi) (w_lo = 0), the lane's (S0, n0, S1, n1) stored to SN
-//      (only by waves with a live frame in the part)
-//   2  the last part: words [w_lo, nw) plus SN where the earlier words [0, w_lo) had a live
-//      frame (the same test the first part made), voxels finished in place
-template <bool VT, int MODE = 0>
+template <bool VT>
 __global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, float* __restrict__ Wt, int D,
                                                         int H, int W, int z0, int z1, FrameCtx c, GridBox B, int F,
                                                         SlotMap SM, const unsigned* __restrict__ cull,
-                                                        const unsigned* __restrict__ freem, int nw, int w_lo,
-                                                        int w_hi, const unsigned* __restrict__ order,
-                                                        int4* __restrict__ SN) {
+                                                        const unsigned* __restrict__ freem, int nw,
+                                                        const unsigned* __restrict__ order) {
     const int l = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int tx, ty, tz;
     if (!tsdf_slot_tile(order ? (int)order[blockIdx.x] : (int)blockIdx.x, SM, tx, ty, tz)) return;
     const int64_t sub = (((int64_t)tz * SM.nty + ty) * SM.ntx + tx) * kCullSub + wave;
     const size_t slot = (size_t)sub * nw;
-    auto live_in = [&](int wa, int wb) {   // any frame of words [wa, wb) not culled for this wave
+    {   // every frame culled for this wave: the grid is not even read
         unsigned any = 0u;
-        for (int w = wa; w < wb; ++w) {
+        for (int w = 0; w < nw; ++w) {
             const int w0 = w << 5;
             any |= ~cull[slot + w] & (F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u));
         }
-        return __builtin_amdgcn_readfirstlane((int)any) != 0;
-    };
-    const bool prior = MODE == 2 && live_in(0, w_lo);   // the first part stored this wave's sums
-    // every frame culled for this wave (in this part, and before it): the grid is not even read
-    if (!live_in(w_lo, w_hi) && !prior) return;
+        if (__builtin_amdgcn_readfirstlane((int)any) == 0) return;
+    }
     int x, y, z;
     sub_voxel(sub, SM.ntx, SM.nty, z0, l, x, y, z);
     if (y >= H) return;                      // wave-uniform (a ragged last tile row)
@@ -819,7 +807,7 @@ __global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, f
         S1 += g1 ? q1 : 0;
         n1 += g1 ? 1 : 0;
     };
-    for (int w = w_lo; w < w_hi; ++w) {
+    for (int w = 0; w < nw; ++w) {
         const int w0 = w << 5;
         const unsigned live = F - w0 >= 32 ? ~0u : ((1u << (F - w0)) - 1u);
         const unsigned todo = (unsigned)__builtin_amdgcn_readfirstlane((int)(live & ~cull[slot + w]));
@@ -853,17 +841,6 @@ __global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, f
     S1 += kfree << kTsdfQBits;
     n0 += kfree;
     n1 += kfree;
-    if constexpr (MODE == 1) {       // integer sums: any split of the frames gives the same bits
-        SN[sub * 64 + l] = make_int4(S0, n0, S1, n1);
-        return;
-    }
-    if (MODE == 2 && prior) {
-        const int4 p = SN[sub * 64 + l];
-        S0 += p.x;
-        n0 += p.y;
-        S1 += p.z;
-        n1 += p.w;
-    }
     if (!in0) return;
     const size_t idx = ((size_t)z * H + y) * W + x;
     if (n0 > 0) {
@@ -946,22 +923,10 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     // refinement list capacity: one entry per (tile, frame)
     const int64_t plist_cap = ntiles * 32 * nwmax;
     const bool order = !stats && sm.per <= 30000;
-    // Pipelined steps (whole-grid mode, own block pass, >= 2 chunks of frames): the block pass runs
-    // on the library's side stream in 64-frame chunks, and each chunk's culling passes follow it on
-    // the caller's stream while the next chunk's depth maps stream in; the fusion runs in two parts
-    // (frames of the first and second half of the chunks) whose integer (S, n) sums are carried in
-    // scratch (MODE 1 / 2 of tsdf_fuse_kernel), so the second half's block pass and culling run
-    // under the first half's fusion.  Same sums, same bits as the one-launch step.
-    //   SFMHIP_AB (A/B runs only): 1 the serial step, 2 pipelined culling with one fusion launch
-    const int ab = kn.ab;
-    SideLease side;
-    const bool can_pipe = !ext_table && !stats && !latency_mode && ab != 1 && cf >= 2 * kTsdfChunk &&
-                          side_lease(side);
-    const bool two_parts = can_pipe && ab != 2;
     // scratch (stream-ordered, one block): counters + per-tile costs first (zeroed by the setup kernel)
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const int nzero = kNCnt + (order ? (two_parts ? 2 : 1) * (int)ntiles : 0);
+    const int nzero = kNCnt + (order ? (int)ntiles : 0);
     const size_t o_cnt = take((size_t)nzero * sizeof(unsigned));
     const size_t o_rec = take((size_t)cf * 16 * sizeof(float));
     const size_t o_cam = take((size_t)cf * sizeof(CullCam));
@@ -972,8 +937,7 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const size_t o_ctab = brick ? take((size_t)cf * ncbu * ncbv * sizeof(float2)) : 0;
     const size_t o_bdec = brick ? take((size_t)cull_bricks * cf) : 0;
     const size_t o_pl = refine ? take((size_t)plist_cap * sizeof(unsigned)) : 0;
-    const size_t o_ord = order ? take((size_t)main_slots * sizeof(unsigned) * (two_parts ? 2 : 1)) : 0;
-    const size_t o_sn = two_parts ? take((size_t)nsub * 64 * sizeof(int4)) : 0;
+    const size_t o_ord = order ? take((size_t)main_slots * sizeof(unsigned)) : 0;
     char* sc = nullptr;
     if (scratch_alloc((void**)&sc, off, st) != hipSuccess) {
         (void)hipGetLastError();
@@ -982,7 +946,6 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     }
     unsigned* cnt = reinterpret_cast<unsigned*>(sc + o_cnt);
     unsigned* tcost = order ? cnt + kNCnt : nullptr;
-    unsigned* tcost2 = order && two_parts ? tcost + ntiles : nullptr;
     float* rec = reinterpret_cast<float*>(sc + o_rec);
     CullCam* ccam = reinterpret_cast<CullCam*>(sc + o_cam);
     int4* crange = reinterpret_cast<int4*>(sc + o_rng);
@@ -993,8 +956,6 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     unsigned char* bdec = brick ? reinterpret_cast<unsigned char*>(sc + o_bdec) : nullptr;
     unsigned* plist = refine ? reinterpret_cast<unsigned*>(sc + o_pl) : nullptr;
     unsigned* ord = order ? reinterpret_cast<unsigned*>(sc + o_ord) : nullptr;
-    unsigned* ord2 = order && two_parts ? ord + main_slots : nullptr;
-    int4* sn = two_parts ? reinterpret_cast<int4*>(sc + o_sn) : nullptr;
     int rc = SFMHIP_OK;
     // integration steps of at most kTsdfMaxFrames frames, in order on the stream
     for (int f0 = 0; f0 < F; f0 += kTsdfMaxFrames) {
@@ -1007,66 +968,29 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                            dim3(64), 0, st, pp, kp, nf, rec, ccam, ext_table ? 1 : 2, H, W, z0, z1, Hd, Wd, cg, nbu,
                            nbv, crange, cnt, nzero);
         const float2* tab = ext_table ? ext_table + (size_t)f0 * nbv * nbu : cbmm;
-        // frame chunks [ch[k], ch[k + 1]): 64 frames (the last takes the remainder), one when serial
-        const bool pipe = can_pipe && nf >= 2 * kTsdfChunk;
-        const bool parts2 = pipe && two_parts;
-        int ch[kTsdfMaxFrames / kTsdfChunk + 1], nch = 0;
-        ch[0] = 0;
-        if (pipe) {
-            for (int a = kTsdfChunk; a + kTsdfChunk / 2 <= nf; a += kTsdfChunk) ch[++nch] = a;
-            ch[++nch] = nf;
-        } else {
-            ch[nch = 1] = nf;
-        }
-        const int nchA = parts2 ? nch / 2 : nch;   // chunks of the first fusion part
-        hipStream_t bq = pipe ? side.s : st;       // the block pass's stream
-        if (pipe) {
-            (void)hipEventRecord(side.ev[0], st);
-            (void)hipStreamWaitEvent(side.s, side.ev[0], 0);
-        }
         if (!ext_table) {
-            for (int k = 0; k < nch; ++k) {
-                const int fa = ch[k], nfk = ch[k + 1] - ch[k];
-                const float* dk = dp + (size_t)fa * Hd * Wd;
-                if (Wd % 4 == 0)
-                    hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nfk), dim3(256), 0,
-                                       bq, dk, nfk, Hd, Wd, nbu, nbv, crange + fa, cbmm + (size_t)fa * nbv * nbu);
-                else
-                    hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nfk), dim3(256), 0,
-                                       bq, dk, nfk, Hd, Wd, nbu, nbv, crange + fa, cbmm + (size_t)fa * nbv * nbu);
-                if (pipe) (void)hipEventRecord(side.ev[1 + k], bq);
-            }
+            if (Wd % 4 == 0)
+                hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st,
+                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
+            else
+                hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st,
+                                   dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
         }
-        // culling of chunk k on stream q: brick pre-pass, the (tile, frame) masks, refinement
-        auto prep = [&](hipStream_t q, int k, unsigned* tc) {
-            const int fa = ch[k], nfk = ch[k + 1] - ch[k];
-            if (brick) {
-                const int64_t nc = (int64_t)nfk * ncbu * ncbv, nd = (cull_bricks + 63) / 64 * 64 * nfk;
-                float2* ct = ctab + (size_t)fa * ncbu * ncbv;
-                hipLaunchKernelGGL(coarse_table_kernel, dim3((unsigned)ceil_div(nc, (int64_t)256)), dim3(256), 0, q,
-                                   tab + (size_t)fa * nbv * nbu, nfk, nbu, nbv, ncbu, ncbv,
-                                   ext_table ? nullptr : crange + fa, ct);
-                hipLaunchKernelGGL(tsdf_brick_kernel, dim3((unsigned)ceil_div(nd, (int64_t)256)), dim3(256), 0, q, H,
-                                   W, z0, z1, nfk, Hd, Wd, ccam + fa, cg, trunc, ct, ncbu, ncbv, (int)cull_bricks,
-                                   bdec + (size_t)fa * cull_bricks);
-            }
-            const int nh = ceil_div(nfk, kCullFrames);
-            unsigned* pl = plist ? plist + (size_t)ntiles * fa : nullptr;
-            hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nh)), dim3(1024), 0, q, H, W, z0, z1,
-                               nf, Hd, Wd, ccam, cg, trunc, tab, nbu, nbv, crange, nw, fa / kCullFrames, nh,
-                               (int)cull_bricks, bdec, (unsigned short*)cmask, (unsigned short*)cfree, pl,
-                               cnt + kCntPl + k, tc);
-            // refinement: grid-stride over the device-side count (atomic ORs: any grid gives the
-            // same masks); 8192 x 256 threads fill the 6 waves per SIMD its VGPRs allow
-            if (pl)
-                hipLaunchKernelGGL(tsdf_refine_kernel, dim3(pipe ? 4096 : 8192), dim3(256), 0, q, H, W, z0, z1, nf,
-                                   Hd, Wd, pp, kp, cg, trunc, tab, nbu, nbv, crange, nw, cmask, cfree, pl,
-                                   cnt + kCntPl + k);
-        };
-        for (int k = 0; k < nchA; ++k) {
-            if (pipe && !ext_table) (void)hipStreamWaitEvent(st, side.ev[1 + k], 0);
-            prep(st, k, tcost);
+        if (brick) {
+            const int64_t nc = (int64_t)nf * ncbu * ncbv, nd = (cull_bricks + 63) / 64 * 64 * nf;
+            hipLaunchKernelGGL(coarse_table_kernel, dim3((unsigned)ceil_div(nc, (int64_t)256)), dim3(256), 0, st, tab,
+                               nf, nbu, nbv, ncbu, ncbv, ext_table ? nullptr : crange, ctab);
+            hipLaunchKernelGGL(tsdf_brick_kernel, dim3((unsigned)ceil_div(nd, (int64_t)256)), dim3(256), 0, st, H, W,
+                               z0, z1, nf, Hd, Wd, ccam, cg, trunc, ctab, ncbu, ncbv, (int)cull_bricks, bdec);
         }
+        hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nw * 2)), dim3(1024), 0, st, H, W, z0, z1,
+                           nf, Hd, Wd, ccam, cg, trunc, tab, nbu, nbv, crange, nw, bdec, (unsigned short*)cmask,
+                           (unsigned short*)cfree, plist, cnt + kCntPl, tcost);
+        // refinement: grid-stride over the device-side count (atomic ORs: any grid gives the
+        // same masks); 8192 x 256 threads fill the 6 waves per SIMD its VGPRs allow
+        if (plist)
+            hipLaunchKernelGGL(tsdf_refine_kernel, dim3(8192), dim3(256), 0, st, H, W, z0, z1, nf, Hd, Wd, pp, kp, cg,
+                               trunc, tab, nbu, nbv, crange, nw, cmask, cfree, plist, cnt + kCntPl);
         if (stats) {
             std::vector<unsigned> mc((size_t)nsub * nw), mf((size_t)nsub * nw);
             hipError_t e = hipMemcpyAsync(mc.data(), cmask, mc.size() * sizeof(unsigned), hipMemcpyDeviceToHost, st);
@@ -1096,6 +1020,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
             }
             continue;
         }
+        if (ord)   // longest-first workgroup order within each XCD class (same results)
+            hipLaunchKernelGGL(tsdf_order_kernel, dim3(kNumXcd), dim3(256), (size_t)sm.per, st, sm, nf, tcost, ord);
         FrameCtx fc;
         fc.rec = rec;
         fc.depth = dp;
@@ -1109,28 +1035,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         fc.nbv = nbv;
         fc.trunc = trunc;
         fc.inv_trunc = 1.0f / trunc;
-        // longest-first workgroup order within each XCD class (same results), from a part's costs
-        auto order_launch = [&](hipStream_t q, const unsigned* tc, int frames, unsigned* o) {
-            if (o) hipLaunchKernelGGL(tsdf_order_kernel, dim3(kNumXcd), dim3(256), (size_t)sm.per, q, sm, frames, tc, o);
-        };
-        order_launch(st, tcost, ch[nchA], ord);
-        if (!parts2) {
-            hipLaunchKernelGGL((vox_test ? tsdf_fuse_kernel<true, 0> : tsdf_fuse_kernel<false, 0>),
-                               dim3((unsigned)main_slots), dim3(256), 0, st, T, Wt, D, H, W, z0, z1, fc, gb, nf, sm,
-                               cmask, cfree, nw, 0, nw, ord, (int4*)nullptr);
-        } else {
-            const int wA = ch[nchA] / 32;   // chunk boundaries are multiples of 64 frames
-            hipLaunchKernelGGL((vox_test ? tsdf_fuse_kernel<true, 1> : tsdf_fuse_kernel<false, 1>),
-                               dim3((unsigned)main_slots), dim3(256), 0, st, T, Wt, D, H, W, z0, z1, fc, gb, nf, sm,
-                               cmask, cfree, nw, 0, wA, ord, sn);
-            for (int k = nchA; k < nch; ++k) prep(side.s, k, tcost2);   // under the first part's fusion
-            order_launch(side.s, tcost2, nf - ch[nchA], ord2);
-            (void)hipEventRecord(side.ev[kSideEvents - 1], side.s);
-            (void)hipStreamWaitEvent(st, side.ev[kSideEvents - 1], 0);
-            hipLaunchKernelGGL((vox_test ? tsdf_fuse_kernel<true, 2> : tsdf_fuse_kernel<false, 2>),
-                               dim3((unsigned)main_slots), dim3(256), 0, st, T, Wt, D, H, W, z0, z1, fc, gb, nf, sm,
-                               cmask, cfree, nw, wA, nw, ord2, sn);
-        }
+        hipLaunchKernelGGL(vox_test ? tsdf_fuse_kernel<true> : tsdf_fuse_kernel<false>, dim3((unsigned)main_slots),
+                           dim3(256), 0, st, T, Wt, D, H, W, z0, z1, fc, gb, nf, sm, cmask, cfree, nw, ord);
         rc = check_launch("tsdf_fuse_kernel");
         if (rc != SFMHIP_OK) break;
     }

@@ -395,37 +395,6 @@ def test_tsdf_free_space_near_trunc_bitexact(sfm, gpu, knob, trunc, lat):
     np.testing.assert_array_equal(T.cpu().numpy(), Tr)
 
 
-@pytest.mark.parametrize("F", [130, 257, 600])
-def test_tsdf_pipelined_step_forms_bitexact(sfm, gpu, knob, F):
-    """The pipelined step (block pass in 64-frame chunks on the side stream, each chunk's
-    culling on the caller's stream; the fusion in two parts whose integer sums are carried
-    in scratch) against the serial step (SFMHIP_AB=1) and the pipelined culling with one
-    fusion launch (SFMHIP_AB=2): the same bits, with prior (T, W) state; 130 frames (two
-    chunks, one per part), 257 (four) and 600 (a 512-frame pipelined step, then an
-    88-frame serial one); oracle-exact on z-slices."""
-    depth, poses, K = syn.tsdf_scene(F, 96, 128, focal=110.0, seed=17)
-    R = 128
-    bnd = ((-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / (R - 1))
-    rng = np.random.default_rng(F)
-    T0 = rng.uniform(-1, 1, (R, R, R)).astype(np.float32)
-    W0 = rng.integers(0, 3, (R, R, R)).astype(np.float32)
-    outs = []
-    for ab in ("1", "2", "0"):
-        knob("AB", ab)
-        T, Wt = torch.from_numpy(T0).to(gpu), torch.from_numpy(W0).to(gpu)
-        sfm.tsdf_integrate(T, Wt, depth, poses, K, *bnd)
-        outs.append((T.cpu().numpy(), Wt.cpu().numpy()))
-    for i in (1, 2):
-        np.testing.assert_array_equal(outs[i][1], outs[0][1])
-        np.testing.assert_array_equal(outs[i][0], outs[0][0])
-    assert (outs[0][1] > W0).mean() > 0.3
-    dc, pc, kc = depth.numpy(), poses.numpy(), K.numpy()
-    for z0 in (3, 64, 125):
-        Tr, Wr = ov.tsdf_integrate(T0, W0, dc, pc, kc, *bnd[:2], np.float32(bnd[2]), z0, z0 + 2)
-        np.testing.assert_array_equal(outs[2][1][z0:z0 + 2], Wr[z0:z0 + 2])
-        np.testing.assert_array_equal(outs[2][0][z0:z0 + 2], Tr[z0:z0 + 2])
-
-
 @pytest.mark.parametrize("lat", LAT_MODES)
 def test_tsdf_camera_inside_large_grid_near_trunc_bitexact(sfm, gpu, knob, lat):
     """Cameras at the centre of a grid with a large |bmin| (translation ~0, voxels near
