@@ -43,6 +43,35 @@ __device__ unsigned long long g_ba_prof[4096 * kProfPhases];
     } while (0)
 #endif
 
+// Tool-only audit builds (tools/ba_audit.sh; never the product library): SFMHIP_BA_AUDIT puts a full
+// wait + workgroup barrier at every phase boundary and around every pass over the records (a missing
+// barrier or an LDS / global ordering race in the shipped kernel would change its bits); SFMHIP_BA_PRINTF
+// adds an inert printf inside every pass (never executed: p < 0), which changes register allocation,
+// spills and scheduling — the symptom round 5's fused prototype showed.  Both must give the product
+// build's bits on the bench batch.
+#if defined(SFMHIP_BA_AUDIT)
+#define BA_AUDIT()                          \
+    do {                                    \
+        __builtin_amdgcn_s_waitcnt(0);      \
+        __threadfence_block();              \
+        __syncthreads();                    \
+    } while (0)
+#else
+#define BA_AUDIT() \
+    do {           \
+    } while (0)
+#endif
+#if defined(SFMHIP_BA_PRINTF)
+#define BA_PRINTF(i)                                                         \
+    do {                                                                     \
+        if (p < 0) printf("ba pair %d obs %d nfev %d\n", p, (int)(i), S.nfev); \
+    } while (0)
+#else
+#define BA_PRINTF(i) \
+    do {             \
+    } while (0)
+#endif
+
 // per observation: J (18: u row, v row; the point block stored scaled, J_p d with the point's
 // column scales d = 1 / scale_inv), f (2), X_new (3), scale_inv (3: the column norms, max'ed
 // across Jacobian evaluations).  d itself is not stored: the trial pass, the one pass that needs
@@ -274,7 +303,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         __syncthreads();
         double acc[13] = {0};   // gc (6), column sums of squares (6), cost
         double gmax = 0.0;
+        BA_AUDIT();
         for (int i = tid; i < n; i += NT) {
+            BA_PRINTF(i);
             double r[kRec];
             double f[2], Xi[3];
             if (moved) {
@@ -309,7 +340,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             rec.template store<kFS, kFS + 3>(i, r);
         }
         gmax = block_max<NW>(gmax, S.red);
+        BA_AUDIT();
         block_sum<NW, 13>(acc, S.red, S.tot);
+        BA_AUDIT();
         if (tid == 0) {
             double gm = gmax;
             for (int c = 0; c < 6; ++c) {
@@ -329,12 +362,15 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     // Delta = |x0 * scale_inv|
     {
         double acc[1] = {0.0};
+        BA_AUDIT();
         for (int i = tid; i < n; i += NT) {
+            BA_PRINTF(i);
             double r[kRec];
             rec.template load<kFS, kFS + 3>(i, r);
             for (int c = 0; c < 3; ++c) { const double t = Xp[3 * i + c] * r[kFS + c]; acc[0] += t * t; }
         }
         block_sum<NW, 1>(acc, S.red, S.tot);
+        BA_AUDIT();
         if (tid == 0) {
             double d2 = S.tot[0];
             for (int c = 0; c < 6; ++c) d2 += (S.cam[c] * S.sic[c]) * (S.cam[c] * S.sic[c]);
@@ -357,7 +393,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         // regularize: a = 0.5 |J_h (-g_h)|^2, |g_h|^2 (build_quadratic_1d along -g_h)
         {
             double acc[2] = {0.0, 0.0};
+            BA_AUDIT();
             for (int i = tid; i < n; i += NT) {
+                BA_PRINTF(i);
                 double r[kRec];
                 pass_rec(i, r);
                 double vu = 0.0, vv = 0.0;
@@ -371,6 +409,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 acc[0] += vu * vu + vv * vv;
             }
             block_sum<NW, 2>(acc, S.red, S.tot);
+            BA_AUDIT();
             if (tid == 0) {
                 double gh2 = S.tot[1];
                 for (int c = 0; c < 6; ++c) gh2 += S.ghc[c] * S.ghc[c];
@@ -393,7 +432,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             double acc[27];
 #pragma unroll
             for (int e = 0; e < 27; ++e) acc[e] = 0.0;
+            BA_AUDIT();
             for (int i = tid; i < n; i += NT) {
+                BA_PRINTF(i);
                 double r[kRec];
                 pass_rec(i, r);
                 double C[2][6], Pp[2][3];
@@ -416,6 +457,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 for (int a = 0; a < 6; ++a) acc[21 + a] += C[0][a] * u0 + C[1][a] * u1;
             }
             block_sum<NW, 27>(acc, S.red, S.tot);
+            BA_AUDIT();
             if (tid == 0) {
                 double G[6][6], h[6];
                 int e = 0;
@@ -431,7 +473,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         // gn_h = J_h^T y, y = B^-1 f - B^-1 C z; g_h . gn_h and |gn_h|^2 (Gram-Schmidt of [g_h, gn_h])
         {
             double acc[7] = {0};   // gnc (6), point part of g_h . gn_h
+            BA_AUDIT();
             for (int i = tid; i < n; i += NT) {
+                BA_PRINTF(i);
                 double r[kRec];
                 pass_rec(i, r);
                 double C[2][6], Pp[2][3];
@@ -456,6 +500,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 }
             }
             block_sum<NW, 7>(acc, S.red, S.tot);
+            BA_AUDIT();
             if (tid == 0) {
                 const double ghn = sqrt(S.gh2);
                 double dot = S.tot[6];
@@ -500,7 +545,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         // divided by |s2| (or |s2|^2) once afterwards
         {
             double acc[6] = {0};   // JS1.JS1, JS1.JS2u, JS2u.JS2u, s2u . g_h and s1 . g_h (point parts), |s2u pts|^2
+            BA_AUDIT();
             for (int i = tid; i < n; i += NT) {
+                BA_PRINTF(i);
                 double r[kRec];
                 pass_rec(i, r);
                 double s1[3], s2[3];
@@ -528,6 +575,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 acc[2] += b0 * b0 + b1 * b1;
             }
             block_sum<NW, 6>(acc, S.red, S.tot);
+            BA_AUDIT();
             if (tid == 0) {
                 double n2 = S.tot[5];
                 for (int c = 0; c < 6; ++c) n2 += S.s2c[c] * S.s2c[c];
@@ -573,7 +621,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             if (S.done) break;
             // step, J_h step, f(x_new): predicted reduction, cost_new, |step_h|, |step|, |x|, finiteness
             double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
+            BA_AUDIT();
             for (int i = tid; i < n; i += NT) {
+                BA_PRINTF(i);
                 double r[kRec];
                 pass_rec_d(i, r);
                 double s1[3], s2[3];
@@ -603,6 +653,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
             }
             block_sum<NW, 7>(acc, S.red, S.tot);
+            BA_AUDIT();
             BA_MARK(6);
             if (tid == 0) {
                 double sg = S.tot[1], sh2 = S.tot[3], st2 = S.tot[4], x2 = S.tot[5];
