@@ -39,6 +39,7 @@ constexpr int kTsdfMaxFrames = 512;   // frames per integration step (host split
 constexpr int kTsdfQBits = 21;        // tsdf fixed point: |S| <= 512 (2^21 + 1) < 2^31
 static_assert(kTsdfMaxFrames * ((1 << kTsdfQBits) + 1) < INT_MAX, "S must fit an int32");
 constexpr double kTsdfLatencyRounds = 1.0;   // below: latency mode (tsdf_run)
+constexpr double kTsdfDeepRounds = 6.0;      // below: four projected frames per fusion stage
 constexpr int kTsdfTX = 8, kTsdfTY = 8, kTsdfTZ = 8;    // workgroup tile: 4 waves x (8 x, 2 y, 8 z)
 constexpr int kCullSub = 4;           // wave sub-tiles per tile
 
@@ -767,7 +768,10 @@ __device__ __forceinline__ void frames_eval(const FrameCtx& c, const int* f, flo
 // phase (so that resident waves gather from the same frames at the same time) and
 // frame-window-major work lists (32-frame windows over the whole grid, partial sums)
 // did not raise the L2 hit rate (23 -> 26 %) and measured slower too.
-template <bool VT>
+// NFS: projected frames evaluated per stage (their loads in flight together): 2 when the grid
+// is many rounds of resident waves (throughput: three or four measured no faster), 4 for a thin
+// z-slab (an N-way split: a couple of rounds, the call is its heaviest waves' frame chains).
+template <bool VT, int NFS = 2>
 __global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, float* __restrict__ Wt, int D,
                                                         int H, int W, int z0, int z1, FrameCtx c, GridBox B, int F,
                                                         SlotMap SM, const unsigned* __restrict__ cull,
@@ -800,7 +804,7 @@ __global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, f
     const float vz = B.mn[2] + (float)z * sz;
     int S0 = 0, S1 = 0, n0 = 0, n1 = 0;
     int kfree = 0;                           // free-space frames
-    int pend = -1;                           // a projected frame waiting for its pair
+    int pend[NFS], np = 0;                   // projected frames waiting for a full stage
     auto add = [&](int q0, int q1, bool g0, bool g1) {
         S0 += g0 ? q0 : 0;
         n0 += g0 ? 1 : 0;
@@ -815,26 +819,21 @@ __global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, f
         unsigned proj = todo & ~fre;
         kfree += __builtin_popcount(fre);
         while (proj) {
-            const int f = w0 + __builtin_ctz(proj);
+            pend[np++] = w0 + __builtin_ctz(proj);
             proj &= proj - 1u;
-            if (pend < 0) {
-                pend = f;
-                continue;
-            }
-            const int ff[2] = {pend, f};
-            int qa[2], qb[2];
-            bool ga[2], gb[2];
-            frames_eval<VT, 2>(c, ff, vx, vy, vz, two, qa, qb, ga, gb);
-            add(qa[0], qb[0], ga[0], gb[0]);
-            add(qa[1], qb[1], ga[1], gb[1]);
-            pend = -1;
+            if (np < NFS) continue;
+            int qa[NFS], qb[NFS];
+            bool ga[NFS], gb[NFS];
+            frames_eval<VT, NFS>(c, pend, vx, vy, vz, two, qa, qb, ga, gb);
+#pragma unroll
+            for (int k = 0; k < NFS; ++k) add(qa[k], qb[k], ga[k], gb[k]);
+            np = 0;
         }
     }
-    if (pend >= 0) {
-        const int ff[1] = {pend};
+    for (int k = 0; k < np; ++k) {   // the last stage's remainder, one frame at a time
         int qa[1], qb[1];
         bool ga[1], gb[1];
-        frames_eval<VT, 1>(c, ff, vx, vy, vz, two, qa, qb, ga, gb);
+        frames_eval<VT, 1>(c, pend + k, vx, vy, vz, two, qa, qb, ga, gb);
         add(qa[0], qb[0], ga[0], gb[0]);
     }
     S0 += kfree << kTsdfQBits;   // free space: tsdf = 1 for every voxel of the sub-tile
@@ -898,8 +897,12 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     }
     const double rounds = (double)nsub / (ncu * 32.0);   // 8 waves per SIMD
     const bool latency_mode = kn.tsdf_latency >= 0 ? kn.tsdf_latency != 0 : rounds < kTsdfLatencyRounds;
-    const bool refine = !latency_mode;
-    const bool brick = !latency_mode;
+    // a thin slab (fewer than kTsdfDeepRounds rounds of resident fusion waves: a z-slab of an N >= 4
+    // split): four projected frames per fusion stage and no brick / refinement pre-passes (their
+    // fixed cost outweighs the fusion work they save there); SFMHIP_AB=1 keeps the whole-grid form
+    const bool deep = rounds < kTsdfDeepRounds && kn.ab != 1;
+    const bool refine = !latency_mode && !deep;
+    const bool brick = !latency_mode && !deep;
     const bool vox_test = !latency_mode;
     GridBox gb;
     CullGeom cg;
@@ -1035,8 +1038,14 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         fc.nbv = nbv;
         fc.trunc = trunc;
         fc.inv_trunc = 1.0f / trunc;
-        hipLaunchKernelGGL(vox_test ? tsdf_fuse_kernel<true> : tsdf_fuse_kernel<false>, dim3((unsigned)main_slots),
-                           dim3(256), 0, st, T, Wt, D, H, W, z0, z1, fc, gb, nf, sm, cmask, cfree, nw, ord);
+        if (deep)
+            hipLaunchKernelGGL((vox_test ? tsdf_fuse_kernel<true, 4> : tsdf_fuse_kernel<false, 4>),
+                               dim3((unsigned)main_slots), dim3(256), 0, st, T, Wt, D, H, W, z0, z1, fc, gb, nf, sm,
+                               cmask, cfree, nw, ord);
+        else
+            hipLaunchKernelGGL((vox_test ? tsdf_fuse_kernel<true, 2> : tsdf_fuse_kernel<false, 2>),
+                               dim3((unsigned)main_slots), dim3(256), 0, st, T, Wt, D, H, W, z0, z1, fc, gb, nf, sm,
+                               cmask, cfree, nw, ord);
         rc = check_launch("tsdf_fuse_kernel");
         if (rc != SFMHIP_OK) break;
     }

@@ -336,15 +336,19 @@ def test_tsdf_multi_step_bitexact(sfm, gpu):
 
 def test_tsdf_modes_and_splits_identical(sfm, gpu, knob):
     """Full-resolution frames, 96^3 grid, z-slab: both modes (whole-grid with brick /
-    refinement / per-voxel block test, latency) give the same grid bit for bit, equal to
+    refinement / per-voxel block test, latency) and both thin-grid forms (the default: four
+    projected frames per fusion stage, no brick / refinement passes; SFMHIP_AB=1: the
+    whole-grid form) give the same grid bit for bit, equal to
     the oracle on sampled slices, with both culling and the free-space path active
     (cull stats)."""
     depth, poses, K = syn.tsdf_scene(40, seed=3)   # two mask words per sub-tile
     bnd = ((-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95)
     out = []
-    variants = [{}, dict(TSDF_LATENCY=0), dict(TSDF_LATENCY=1)]
+    # AB=1: the whole-grid form (brick + refinement, two frames per stage) where the thin default differs
+    variants = [{}, dict(TSDF_LATENCY=0), dict(TSDF_LATENCY=1), dict(AB=1), dict(AB=1, TSDF_LATENCY=0)]
     for v in variants:
         knob("TSDF_LATENCY", -1)
+        knob("AB", 0)
         for k, x in v.items():
             knob(k, x)
         T = torch.zeros((96, 96, 96), dtype=torch.float32, device=gpu)
