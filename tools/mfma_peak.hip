@@ -112,8 +112,12 @@ int main(int argc, char** argv) {
     int h[4096];
     // operand byte distributions: 0 uniform random bytes, 1 zero, then C3-like small
     // signed values round(N(0, 8)) (two's complement) shifted by 0, 64, 88, 100
-    const char* names[6] = {"random", "zero", "N(0,8)+0", "N(0,8)+64", "N(0,8)+88", "N(0,8)+100"};
-    const int shifts[6] = {0, 0, 0, 64, 88, 100};
+    // (round 6) N(0,6): the C3 descriptors quantised at 95 instead of 127 (|q| <= 30, the same
+    // certified decisions in tools/sim_mx_certify-style models); +48 the matcher's shift
+    const char* names[8] = {"random", "zero", "N(0,8)+0", "N(0,8)+64", "N(0,8)+88", "N(0,8)+100", "N(0,8)+48",
+                            "N(0,6)+48"};
+    const int shifts[8] = {0, 0, 0, 64, 88, 100, 48, 48};
+    const float sigmas[8] = {8.f, 8.f, 8.f, 8.f, 8.f, 8.f, 8.f, 6.f};
     const int modes = argc > 2 ? atoi(argv[2]) : 2;
     for (int zero = 0; zero < modes; ++zero) {
         unsigned x = 12345;
@@ -125,7 +129,7 @@ int main(int argc, char** argv) {
                 // Irwin-Hall(12) - 6 ~ N(0, 1), times 8, rounded, clamped to [-40, 39]
                 float g = -6.f;
                 for (int t = 0; t < 12; ++t) { x = x * 1664525u + 1013904223u; g += (float)(x >> 8) / 16777216.f; }
-                int v = (int)lrintf(8.f * g);
+                int v = (int)lrintf(sigmas[zero] * g);
                 v = v < -40 ? -40 : (v > 39 ? 39 : v);
                 v += shifts[zero];
                 w |= (unsigned)(v & 255) << (8 * b);
