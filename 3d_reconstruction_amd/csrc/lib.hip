@@ -187,8 +187,9 @@ extern "C" int sfmhip_knobs_reload(void) {
     return SFMHIP_OK;
 }
 
+// 0.3.0: sfmhip_match_pairs_i16 / sfmhip_match_pairs_exact_i16 (the int16 graph written by the kernels)
 // 0.2.0: sfmhip_ba_solve takes n_obs (between n_pairs and ftol); sfmhip_scratch_release_stream
-extern "C" int sfmhip_version(void) { return (0 << 16) | (2 << 8) | 0; }
+extern "C" int sfmhip_version(void) { return (0 << 16) | (3 << 8) | 0; }
 
 extern "C" const char* sfmhip_last_error(void) { return sfmhip::g_err; }
 

@@ -40,7 +40,7 @@ def test_ctypes_signatures_match_header(sfm):
 
 
 def test_version_and_error_channel(sfm):
-    assert sfm.lib.sfmhip_version() == 0x000200   # 0.2.0: sfmhip_ba_solve n_obs, release_stream
+    assert sfm.lib.sfmhip_version() == 0x000300   # 0.3.0: the int16-graph match entry points
     # an argument error is reported without touching the GPU
     rc = sfm.lib.sfmhip_match_pairs(None, None, None, None, 1, 128, 128, None, 1, 3, 4, None, None, None, None)
     assert rc == -1
