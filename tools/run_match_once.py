@@ -15,7 +15,9 @@ x = syn.superpoint_like(n_img, 4096, 256, seed=1, device=dev)
 bank = sfm.DescriptorBank.from_float(x, mode=sfm.MODE_FLOAT)
 del x
 pairs = torch.from_numpy(sfm.all_pairs(n_img)).to(dev)
-out = torch.empty((pairs.shape[0], bank.m_pad), dtype=torch.int32, device=dev)
+# the bench's graph: int16 written by the kernels (GRAPH=int32: the int32 entry points)
+gdt = torch.int32 if os.environ.get("GRAPH", "int16") == "int32" else torch.int16
+out = torch.empty((pairs.shape[0], bank.m_pad), dtype=gdt, device=dev)
 exact = os.environ.get("EXACT", "1") != "0"
 for _ in range(int(os.environ.get("REPS", "2"))):
     bank.match(pairs, ratio=0.75, out=out, exact=exact)

@@ -15,7 +15,7 @@ src, dst = os.path.join(ROOT, "gpurun_out"), os.path.join(ROOT, "profiles", rnd)
 os.makedirs(dst, exist_ok=True)
 old = os.path.join(dst, "traffic.json")
 traffic = json.load(open(old)) if os.path.exists(old) else {}   # kinds without a run here keep their entry
-for kind in ("match", "tsdf", "render", "ba", "vq"):
+for kind in ("match", "match_int8", "tsdf", "render", "ba", "vq"):
     if not glob.glob(os.path.join(src, f"pmc_{kind}_{tag}", "p*")):
         continue
     per = {}
