@@ -54,8 +54,7 @@ PEAK_FP64_TFLOPS = 78.6       # fp64 (vector and v_mfma_f64 matrix peaks are the
 DLT_FLOP_PER_OBS = 1200.0     # 6x4 f64 DLT null vector, ~1.2 kflop per observation
 FDJ_BYTES_PER_OBS = 200.0     # 40 B in + 16 B residual + 144 B Jacobian values
 DLT_BYTES_PER_OBS = 64.0      # 2 x 2 f64 pixels in, 4 f64 out
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r5", "traffic.json")
-TRAFFIC_FILE_INT8 = os.path.join(ROOT, "profiles", "r4", "traffic.json")   # the int8-mode match launch
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r6", "traffic.json")
 VERIFY_WORK_FILE = os.path.join(ROOT, "profiles", "r3", "verify_work.json")
 # Algorithmic fp64 flop counts of the secondary lines (DESIGN.md §5 derives each):
 F_5PT = 18_000.0        # one 5-point solve: 5x9 null space, 10x20 constraint matrix, 10x10 solve, degree-10 roots
@@ -291,7 +290,7 @@ def c2_line(sfm, syn, device, args, barrier, cpu=True):
             "roofline": {"bound": "mfma", "kernel": "match_kernel<128>", "kernel_ms": k_ms, "unit": "TOPS",
                          "achieved": ops / (k_ms * 1e-3) / 1e12, "peak": PEAK_INT8_TOPS,
                          "frac": ops / (k_ms * 1e-3) / 1e12 / PEAK_INT8_TOPS,
-                         "note": "kernel_ms spans the match launch and the int16 graph copy"}}
+                         "note": "kernel_ms spans the match launch, which writes the int16 graph itself"}}
     if cpu:
         sample = spread(P, 16)
         qcpu = {int(k): bank.q[int(k)].cpu().numpy() for i in sample for k in pairs[i]}
@@ -333,9 +332,9 @@ def int8_line(sfm, syn, device, args, barrier, cpu=True, exact_ms=None):
             "roofline": {"bound": "mfma", "kernel": "match_kernel<256>", "kernel_ms": k_ms, "unit": "TOPS",
                          "achieved": ops / (k_ms * 1e-3) / 1e12, "peak": PEAK_INT8_TOPS,
                          "frac": ops / (k_ms * 1e-3) / 1e12 / PEAK_INT8_TOPS,
-                         "traffic": pmc_traffic("match", src=TRAFFIC_FILE_INT8),
-                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r4/traffic.json: "
-                                         "the int8-mode launch)",
+                         "traffic": pmc_traffic("match_int8"),
+                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r6/traffic.json: "
+                                         "the int8-mode launch writing the int16 graph)",
                          "algorithmic": "2*M*N*d int8 ops per pair"},
             "speed_vs_exact": (exact_ms / ms) if exact_ms else None}
     if cpu:
@@ -456,7 +455,7 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
                          "achieved": comp / (k_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                          "frac": comp / (k_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                          "traffic": pmc_traffic("render"),
-                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r5/traffic.json): "
+                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r6/traffic.json): "
                                          "voxel lines re-fetched, see DESIGN K5",
                          "note": "compulsory = distinct 128-B voxel lines under the in-bounds samples' trilinear "
                                  "corners (exact count) + rays/z read + colours written; the 8-corner x 28-channel "
@@ -509,7 +508,7 @@ def voxel_and_vq_lines(sfm, syn, device, args, barrier, cpu=True):
                          "achieved": obs.shape[0] * (128 * 8 + 12) / (np.mean(kms) * 1e-3) / 1e9,
                          "peak": PEAK_HBM_GBS, "frac": obs.shape[0] * (128 * 8 + 12) / (np.mean(kms) * 1e-3) / 1e9
                          / PEAK_HBM_GBS, "gemm_tflops_2nkd": fl, "traffic": pmc_traffic("vq"),
-                         "traffic_unit": "bytes per call (FETCH_SIZE*2 + WRITE_SIZE, profiles/r5/traffic.json)"}}
+                         "traffic_unit": "bytes per call (FETCH_SIZE*2 + WRITE_SIZE, profiles/r6/traffic.json)"}}
     if cpu:
         from scipy.cluster.vq import vq as scipy_vq
         oo, bb = obs[:65536].cpu().numpy(), book.cpu().numpy()
@@ -1019,7 +1018,7 @@ def ba_solve_line(sfm, syn, device, args, barrier, cpu=True):
                          # per solve: measured L2-miss traffic, the rate the kernel actually moves
                          "traffic": pmc_traffic("ba"),
                          "traffic_gbs": (pmc_traffic("ba") or 0.0) / (k_ms * 1e-3) / 1e9,
-                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r5/traffic.json, "
+                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r6/traffic.json, "
                                          "pmc_ba.txt)"}}
     # sfm.py:37-38 left exactly as written (scipy least_squares, jac_sparsity=ba_sparse, 2-point FD) with
     # only `import sfmhip as cv2`: every residual evaluation is one sfmhip.projectPoints call (host <->
@@ -1345,8 +1344,9 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved_tops, "peak": PEAK_INT8_TOPS, "unit": "TOPS",
                      "frac": achieved_tops / PEAK_INT8_TOPS,
                      "traffic": pmc_traffic("match", pairs_per_launch / P) if n_img == N_IMG else None,
-                     "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r5/traffic.json: match_kernel "
-                                     "(certifying epilogue) + the resolve kernels: collect, batched f64 re-score)",
+                     "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE, profiles/r6/traffic.json: match_kernel "
+                                     "(certifying epilogue, int16 graph) + the resolve kernels: collect, batched f64 "
+                                     "re-score)",
                      "kernel": "match_kernel<256> (exact mode) + resolve kernels", "kernel_ms": kern_ms,
                      "algorithmic": "2*M*N*d int8 ops per pair x pairs per launch (the f64 re-score of the "
                                     "uncertified rows is overhead, not work)"},
@@ -1421,7 +1421,7 @@ def main():
                          "frac": (32.0 * local_upd / (tk_ms * 1e-3) / 1e12) / PEAK_FP32_TFLOPS,
                          "achieved_hbm_gbs": comp_bytes / (tk_ms * 1e-3) / 1e9, "peak_hbm_gbs": PEAK_HBM_GBS,
                          "traffic": pmc_traffic("tsdf", (z1 - z0) / R),
-                         "traffic_unit": "bytes per step (every pre-pass + the fusion, profiles/r5/traffic.json)"},
+                         "traffic_unit": "bytes per step (every pre-pass + the fusion, profiles/r6/traffic.json)"},
             "updated_voxel_frac": float((Wt[z0:z1] > 0).float().mean().item()),
         }
         del depth, T, Wt
