@@ -250,7 +250,12 @@ __device__ __forceinline__ void resid(const double* R, const double* c, const do
     rv = pts[1] - v;
 }
 
-template <int NT>
+// FUSED: the Jacobian at the trial point is formed inside the trial pass into a second record set
+// (taken, with the trial's sums, when the step is accepted: nfev ~ njev on the bench scenes), so an
+// accepted step costs no separate Jacobian sweep; the records then carry the point of their
+// Jacobian (fields kFX) and X is written once at the end.  The same arithmetic in the same order
+// as the two-pass form (the trial's residual IS fd_obs's base residual), so the same bits.
+template <int NT, bool FUSED = false>
 __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io, const double* __restrict__ Kall,
                                                     double* __restrict__ X, const double* __restrict__ pts2d,
                                                     const int64_t* __restrict__ off, int64_t n_obs, double ftol,
@@ -270,14 +275,16 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     const double* k = Kall + (size_t)p * 9;
     double* Xp = X + 3 * o0;
     const double* pts = pts2d + 2 * o0;
-    const Recs rec{scratch + (size_t)o0 * kRec, n};
+    // FUSED: two record sets (the current one and the trial point's), scratch holds 2 n_obs records
+    const Recs recs[2] = {{scratch + (size_t)o0 * kRec, n}, {scratch + (size_t)(n_obs + o0) * kRec, n}};
+    int cur = 0;   // every thread flips it at the same point (after a barrier): uniform
     // the pass view of observation i: r[0..17] J, r[18..19] f; the records hold the point block
     // of J already scaled, Pp = J_p d (fields 6-8, 15-17), so the passes read 20 fields
     // (round 5: 1.33 -> 1.27 ms); the trial pass adds scale_inv (its d = 1 / scale_inv)
-    auto pass_rec = [&](int i, double* r) { rec.template load<0, 20>(i, r); };
+    auto pass_rec = [&](int i, double* r) { recs[cur].template load<0, 20>(i, r); };
     auto pass_rec_d = [&](int i, double* r) {
-        rec.template load<0, 20>(i, r);
-        rec.template load<kFS, kFS + 3>(i, r);
+        recs[cur].template load<0, 20>(i, r);
+        recs[cur].template load<kFS, kFS + 3>(i, r);
     };
     if (tid < 6) S.cam[tid] = cam_io[(size_t)p * 6 + tid];
     __syncthreads();
@@ -309,12 +316,12 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             double r[kRec];
             double f[2], Xi[3];
             if (moved) {
-                rec.template load<kFX, kFX + 3>(i, r);
+                recs[cur].template load<kFX, kFX + 3>(i, r);
                 for (int c = 0; c < 3; ++c) { Xi[c] = r[kFX + c]; Xp[3 * i + c] = Xi[c]; }
             } else {
                 for (int c = 0; c < 3; ++c) Xi[c] = Xp[3 * i + c];
             }
-            if (!first) rec.template load<kFS, kFS + 3>(i, r);
+            if (!first) recs[cur].template load<kFS, kFS + 3>(i, r);
             fd_obs(&S.R[0][0], S.cam, k, Xi, pts[2 * i], pts[2 * i + 1], nullptr, f, r);
             r[18] = f[0];
             r[19] = f[1];
@@ -336,8 +343,12 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                 r[6 + c] = r[6 + c] * d;   // Pp
                 r[15 + c] = r[15 + c] * d;
             }
-            rec.template store<0, 20>(i, r);
-            rec.template store<kFS, kFS + 3>(i, r);
+            recs[cur].template store<0, 20>(i, r);
+            recs[cur].template store<kFS, kFS + 3>(i, r);
+            if (FUSED) {   // the point of this Jacobian (X is read from the records from now on)
+                for (int c = 0; c < 3; ++c) r[kFX + c] = Xi[c];
+                recs[cur].template store<kFX, kFX + 3>(i, r);
+            }
         }
         gmax = block_max<NW>(gmax, S.red);
         BA_AUDIT();
@@ -366,7 +377,7 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         for (int i = tid; i < n; i += NT) {
             BA_PRINTF(i);
             double r[kRec];
-            rec.template load<kFS, kFS + 3>(i, r);
+            recs[cur].template load<kFS, kFS + 3>(i, r);
             for (int c = 0; c < 3; ++c) { const double t = Xp[3 * i + c] * r[kFS + c]; acc[0] += t * t; }
         }
         block_sum<NW, 1>(acc, S.red, S.tot);
@@ -619,42 +630,112 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
             __syncthreads();
             BA_MARK(5);
             if (S.done) break;
-            // step, J_h step, f(x_new): predicted reduction, cost_new, |step_h|, |step|, |x|, finiteness
-            double acc[7] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
-            BA_AUDIT();
-            for (int i = tid; i < n; i += NT) {
-                BA_PRINTF(i);
-                double r[kRec];
-                pass_rec_d(i, r);
-                double s1[3], s2[3];
-                point_vecs(r, s1, s2);
-                double ju = 0, jv = 0;
-                for (int c = 0; c < 6; ++c) { ju += r[c] * S.dc[c] * S.shc[c]; jv += r[9 + c] * S.dc[c] * S.shc[c]; }
-                double Xn[3];
-                for (int c = 0; c < 3; ++c) {
-                    const double d = 1.0 / r[kFS + c];   // the Jacobian pass's quotient
-                    const double sh = S.pS[0] * s1[c] + S.pS[1] * (s2[c] / s2n);
-                    ju += r[6 + c] * sh;
-                    jv += r[15 + c] * sh;
-                    acc[1] += sh * (r[6 + c] * r[18] + r[15 + c] * r[19]);
-                    acc[3] += sh * sh;
-                    const double st = d * sh;
-                    acc[4] += st * st;
-                    const double x = Xp[3 * i + c];
-                    acc[5] += x * x;
-                    Xn[c] = x + st;
-                    r[kFX + c] = Xn[c];
+            if (FUSED) {   // R(rvec_new) and the three perturbed rotations of the FD at the trial point
+                if (tid < 4) {
+                    double q[3] = {S.cam_new[0], S.cam_new[1], S.cam_new[2]};
+                    if (tid > 0) q[tid - 1] = q[tid - 1] + fd_step(q[tid - 1]);
+                    rodrigues(q, S.R[tid]);
                 }
-                rec.template store<kFX, kFX + 3>(i, r);
-                acc[0] += ju * ju + jv * jv;
-                double ru, rv;
-                resid(S.Rn, S.cam_new, k, Xn, pts + 2 * i, ru, rv);
-                acc[2] += ru * ru + rv * rv;
-                if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
+                __syncthreads();
             }
-            block_sum<NW, 7>(acc, S.red, S.tot);
-            BA_AUDIT();
-            BA_MARK(6);
+            // step, J_h step, f(x_new): predicted reduction, cost_new, |step_h|, |step|, |x|, finiteness
+            // (FUSED also: J at x_new into the other record set, gc (6), column sums of squares (6), |g|_inf)
+            constexpr int KT = FUSED ? 19 : 7;
+            double acc[KT] = {0};   // |J_h s|^2, s.g_h (points), cost_new*2, |step_h|^2 pts, |step|^2 pts, |x|^2 pts, nonfinite
+            double gmax_n = 0.0;
+            if constexpr (FUSED) {
+                BA_AUDIT();
+                for (int i = tid; i < n; i += NT) {
+                    BA_PRINTF(i);
+                    double r[kRec];
+                    pass_rec_d(i, r);
+                    recs[cur].template load<kFX, kFX + 3>(i, r);   // the current point
+                    double s1[3], s2[3];
+                    point_vecs(r, s1, s2);
+                    double ju = 0, jv = 0;
+                    for (int c = 0; c < 6; ++c) { ju += r[c] * S.dc[c] * S.shc[c]; jv += r[9 + c] * S.dc[c] * S.shc[c]; }
+                    double Xn[3];
+                    for (int c = 0; c < 3; ++c) {
+                        const double d = 1.0 / r[kFS + c];   // the Jacobian pass's quotient
+                        const double sh = S.pS[0] * s1[c] + S.pS[1] * (s2[c] / s2n);
+                        ju += r[6 + c] * sh;
+                        jv += r[15 + c] * sh;
+                        acc[1] += sh * (r[6 + c] * r[18] + r[15 + c] * r[19]);
+                        acc[3] += sh * sh;
+                        const double st = d * sh;
+                        acc[4] += st * st;
+                        const double x = r[kFX + c];
+                        acc[5] += x * x;
+                        Xn[c] = x + st;
+                    }
+                    acc[0] += ju * ju + jv * jv;
+                    // J at x_new (jacobian(false, true)'s record: the base residual is the trial's)
+                    double o[kRec], f[2];
+                    for (int c = 0; c < 3; ++c) o[kFS + c] = r[kFS + c];
+                    fd_obs(&S.R[0][0], S.cam_new, k, Xn, pts[2 * i], pts[2 * i + 1], nullptr, f, o);
+                    acc[2] += f[0] * f[0] + f[1] * f[1];
+                    if (!isfinite(f[0]) || !isfinite(f[1])) acc[6] += 1.0;
+                    o[18] = f[0];
+                    o[19] = f[1];
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) {
+                        acc[7 + c] += o[c] * f[0] + o[9 + c] * f[1];
+                        acc[13 + c] += o[c] * o[c] + o[9 + c] * o[9 + c];
+                    }
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const double gp = o[6 + c] * f[0] + o[15 + c] * f[1];
+                        gmax_n = fmax(gmax_n, fabs(gp));
+                        const double si = fmax(sqrt(o[6 + c] * o[6 + c] + o[15 + c] * o[15 + c]), o[kFS + c]);
+                        o[kFS + c] = si;
+                        const double d = 1.0 / si;
+                        o[6 + c] = o[6 + c] * d;   // Pp
+                        o[15 + c] = o[15 + c] * d;
+                        o[kFX + c] = Xn[c];
+                    }
+                    recs[cur ^ 1].template store<0, 20>(i, o);
+                    recs[cur ^ 1].template store<kFX, kRec>(i, o);
+                }
+                gmax_n = block_max<NW>(gmax_n, S.red);
+                BA_AUDIT();
+                block_sum<NW, KT>(acc, S.red, S.tot);
+                BA_AUDIT();
+                BA_MARK(6);
+            } else {
+                for (int i = tid; i < n; i += NT) {
+                    BA_PRINTF(i);
+                    double r[kRec];
+                    pass_rec_d(i, r);
+                    double s1[3], s2[3];
+                    point_vecs(r, s1, s2);
+                    double ju = 0, jv = 0;
+                    for (int c = 0; c < 6; ++c) { ju += r[c] * S.dc[c] * S.shc[c]; jv += r[9 + c] * S.dc[c] * S.shc[c]; }
+                    double Xn[3];
+                    for (int c = 0; c < 3; ++c) {
+                        const double d = 1.0 / r[kFS + c];   // the Jacobian pass's quotient
+                        const double sh = S.pS[0] * s1[c] + S.pS[1] * (s2[c] / s2n);
+                        ju += r[6 + c] * sh;
+                        jv += r[15 + c] * sh;
+                        acc[1] += sh * (r[6 + c] * r[18] + r[15 + c] * r[19]);
+                        acc[3] += sh * sh;
+                        const double st = d * sh;
+                        acc[4] += st * st;
+                        const double x = Xp[3 * i + c];
+                        acc[5] += x * x;
+                        Xn[c] = x + st;
+                        r[kFX + c] = Xn[c];
+                    }
+                    recs[cur].template store<kFX, kFX + 3>(i, r);
+                    acc[0] += ju * ju + jv * jv;
+                    double ru, rv;
+                    resid(S.Rn, S.cam_new, k, Xn, pts + 2 * i, ru, rv);
+                    acc[2] += ru * ru + rv * rv;
+                    if (!isfinite(ru) || !isfinite(rv)) acc[6] += 1.0;
+                }
+                block_sum<NW, 7>(acc, S.red, S.tot);
+                BA_AUDIT();
+                BA_MARK(6);
+            }
             if (tid == 0) {
                 double sg = S.tot[1], sh2 = S.tot[3], st2 = S.tot[4], x2 = S.tot[5];
                 for (int c = 0; c < 6; ++c) {
@@ -685,6 +766,16 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                     S.status = (fok && xok) ? 4 : fok ? 2 : xok ? 3 : -1;
                     S.accept = actual > 0.0 ? 1 : 0;
                     if (S.status < 0) S.Delta = Dn;
+                    if (FUSED && S.accept == 1) {   // jacobian(false, true)'s scalars, from the same sums
+                        double gm = gmax_n;
+                        for (int c = 0; c < 6; ++c) {
+                            S.gc[c] = S.tot[7 + c];
+                            gm = fmax(gm, fabs(S.gc[c]));
+                            S.sic[c] = fmax(sqrt(S.tot[13 + c]), S.sic[c]);
+                        }
+                        S.gmax = gm;
+                        S.cost = 0.5 * S.tot[2];
+                    }
                 }
             }
             __syncthreads();
@@ -694,7 +785,8 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
         if (S.accept == 1) {   // x = x_new (moved by the Jacobian pass); J at the new point
             if (tid < 6) S.cam[tid] = S.cam_new[tid];
             __syncthreads();
-            jacobian(false, true);
+            if (FUSED) cur ^= 1;   // the trial pass formed J at x_new already
+            else jacobian(false, true);
             if (tid == 0) { S.njev += 1; }
             __syncthreads();
             BA_MARK(0);
@@ -707,6 +799,9 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     if (tid == 0 && p < 4096)
         for (int kk = 0; kk < kProfPhases; ++kk) g_ba_prof[p * kProfPhases + kk] = prof_acc[kk];
 #endif
+    if (FUSED)   // X = the current records' point
+        for (int i = tid; i < n; i += NT)
+            for (int c = 0; c < 3; ++c) Xp[3 * i + c] = *recs[cur].at(i, kFX + c);
     if (tid < 6) cam_io[(size_t)p * 6 + tid] = S.cam[tid];
     if (tid == 0) {
         cost_out[p] = S.cost;
@@ -731,15 +826,21 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
     if (n_pairs == 0) return SFMHIP_OK;
     hipStream_t st = as_stream(stream);
     double* scratch = nullptr;
-    if (scratch_alloc((void**)&scratch, (size_t)std::max<int64_t>(n_obs, 1) * kRec * sizeof(double), st) != hipSuccess) {
+    const bool fused = knobs().ab == 9;   // A/B (temporary): the fused trial + Jacobian form
+    if (scratch_alloc((void**)&scratch, (size_t)std::max<int64_t>(n_obs, 1) * kRec * sizeof(double) * (fused ? 2 : 1),
+                      st) != hipSuccess) {
         (void)hipGetLastError();
         set_error("sfmhip_ba_solve: scratch allocation failed");
         return SFMHIP_E_HIP;
     }
     // one 512-thread workgroup per pair, field-major records (256 threads, AoS records and the
     // recompute form measured slower: profiles/r3/ba_variants_r3m.txt, DESIGN.md K3'')
-    hipLaunchKernelGGL((ba_trf_kernel<512>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off, n_obs, ftol,
-                       xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+    if (fused)
+        hipLaunchKernelGGL((ba_trf_kernel<512, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off, n_obs,
+                           ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+    else
+        hipLaunchKernelGGL((ba_trf_kernel<512>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off, n_obs, ftol,
+                           xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
     const int rc = check_launch("ba_trf_kernel");
     scratch_free(scratch, st);
     return rc;

@@ -73,6 +73,36 @@ def test_ba_solve_batched_vs_oracle(sfm, gpu, far):
         assert abs(res["cost"][p] - o["cost"]) <= 1e-6 * o["cost"] + 1e-12, p
 
 
+@pytest.mark.parametrize("far", [0, 1])
+def test_ba_fused_trial_jacobian_form_bit_identical(sfm, gpu, knob, far):
+    """The fused form (SFMHIP_AB=9: the Jacobian at the trial point formed inside the trial
+    pass into a second record set, taken on acceptance — VERDICT r5 item 3) against the shipped
+    two-pass form: the same cam, X, cost, nfev, njev and status bits on ragged pairs with
+    rejected steps (far starts), an empty pair, and the bench scene's first 32 pairs."""
+    sizes = [300, 0, 1000, 37, 700, 2048]
+    cams, Ks, Xs, ps = _ragged_problem(sizes, seed=60 + far, far=far)
+    out = []
+    for ab in (0, 9):
+        knob("AB", ab)
+        out.append(_solve_gpu(sfm, gpu, cams, Ks, Xs, ps))
+    (c0, x0, r0, _), (c1, x1, r1, _) = out
+    assert np.array_equal(c0, c1) and np.array_equal(x0, x1)
+    for key in ("cost", "nfev", "njev", "status"):
+        assert np.array_equal(r0[key], r1[key]), key
+    s = syn.ba_scene(32, 4096, seed=4)
+    tt = {k: torch.from_numpy(np.ascontiguousarray(v)).to(gpu) for k, v in s.items()}
+    off = torch.arange(33, dtype=torch.int64, device=gpu) * 4096
+    res = []
+    for ab in (0, 9):
+        knob("AB", ab)
+        cam, X = tt["cam"].clone(), tt["X"].clone()
+        r = sfm.ba_solve_batched(cam, tt["K"], X, tt["pts2d"], off, validate=False)
+        res.append((cam.cpu(), X.cpu(), {k: v.cpu() for k, v in r.items() if isinstance(v, torch.Tensor)}))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for key in res[0][2]:
+        assert torch.equal(res[0][2][key], res[1][2][key]), key
+
+
 def test_least_squares_ba_drop_in_vs_scipy(sfm, gpu):
     """sfm.py:38 with the on-device solve: scipy's nfev and solution."""
     cams, Ks, Xs, ps = _ragged_problem([500], seed=50, far=True)
