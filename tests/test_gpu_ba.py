@@ -77,8 +77,9 @@ def test_ba_solve_batched_vs_oracle(sfm, gpu, far):
 def test_ba_fused_trial_jacobian_form_bit_identical(sfm, gpu, knob, far):
     """The fused form (SFMHIP_AB=9: the Jacobian at the trial point formed inside the trial
     pass into a second record set, taken on acceptance — VERDICT r5 item 3) against the shipped
-    two-pass form: the same cam, X, cost, nfev, njev and status bits on ragged pairs with
-    rejected steps (far starts), an empty pair, and the bench scene's first 32 pairs."""
+    two-pass form: the same cam, X, cost, nfev, njev and status bits on ragged pairs (near and
+    far starts), an empty pair, and the bench scene's first 32 pairs (the digest over all 256
+    bench pairs, rejected steps included, matched too: DESIGN §6f item 3)."""
     sizes = [300, 0, 1000, 37, 700, 2048]
     cams, Ks, Xs, ps = _ragged_problem(sizes, seed=60 + far, far=far)
     out = []
