@@ -277,3 +277,22 @@ def test_int16_graph_sharded_product_api(sfm, gpu):
     assert torch.equal(g.long(), ref.long())
     with pytest.raises(ValueError):
         bank.match(pairs, out=torch.empty((len(pairs), bank.m_pad), dtype=torch.int16, device=gpu), mutual=True)
+
+
+def test_int16_graph_c3_full_size_equals_int32(sfm, gpu):
+    """The bench headline's graph (C3 at full size: 257 x 4096 x 256 float descriptors, all
+    32,896 pairs, exact float mode, dist.match_all_pairs_sharded -> int16 written by the
+    kernels) equals the int32 graph of bank.match entry for entry; sampled rows of both against
+    the oracle are covered by test_exact_float_c3_full_size_sampled_rows."""
+    sdist = importlib.import_module("3d_reconstruction_amd.dist")
+    x = syn.superpoint_like(257, 4096, 256, seed=1, device=gpu)
+    bank = sfm.DescriptorBank.from_float(x, mode=1, exact=True)
+    del x
+    pairs = torch.from_numpy(sfm.all_pairs(257)).to(gpu)
+    g16 = sdist.match_all_pairs_sharded(bank, pairs, exact=True)
+    assert g16.dtype == torch.int16
+    n16 = int(bank.last_resolved.item())
+    g32 = bank.match(pairs)
+    assert int(bank.last_resolved.item()) == n16 > 0          # the same rows went to the exact pass
+    for lo in range(0, pairs.shape[0], 4096):                 # compare in slices (the int32 graph is 539 MB)
+        assert torch.equal(g16[lo:lo + 4096].to(torch.int32), g32[lo:lo + 4096]), lo
