@@ -21,6 +21,8 @@
 //   depth_blockmax_kernel {min, max} per 16x16 depth block: the step's one
 //                         compulsory streaming read of the depth maps
 //   coarse_table_kernel + tsdf_brick_kernel   (whole-grid mode) brick pre-pass
+//   (SFMHIP_AB=3: the block pass and the culling in one persistent tsdf_prepass_kernel +
+//   tsdf_pack_kernel instead; measured slower)
 //   tsdf_cull_kernel      exact (tile, frame) culling / free-space proofs -> masks
 //   tsdf_refine_kernel    (whole-grid mode) the projected pairs again per wave sub-tile
 //   tsdf_order_kernel     longest-first workgroup order per XCD class
@@ -237,6 +239,21 @@ __global__ __launch_bounds__(256) void depth_blockmax_kernel(const float* __rest
     }
 }
 
+// The decision from a box's footprint (box_footprint == 2) and the {min, max} depth
+// over the table blocks that cover it.
+__device__ __forceinline__ void cull_decide(const CullCam& cc, float trunc, float m, float mn, double zlo, double zhi,
+                                            bool inside, bool& skip, bool& fre) {
+    // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for the
+    // rounding of (depth - Zc), so the kernel's !(sdf < -trunc) test fails everywhere
+    skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * 0x1p-24) + 1e-30 < zlo);
+    // free space: for every voxel fl(depth - Zc) >= mu (1 + 2^-21) and
+    // fl(fl(depth - Zc) fl(1/mu)) >= 1, i.e. tsdf = 1 exactly (mu in [2^-100, 2^100]);
+    // needs a frame record the fusion kernel fuses (every parameter < 2^60)
+    fre = false;
+    if (!skip && inside && zlo >= 0x1p-59 && zhi <= 0x1p59 && cc.good != 0.0)
+        fre = (double)mn - zhi >= (double)trunc * (1 + 0x1p-20);
+}
+
 // The (box, frame) test: skip = provably no voxel of the box updates; fre = every
 // voxel of the box updates with tsdf = 1 (free space).
 // BLK: pixel edge of the table's blocks; CAP: larger footprints are kept; range null:
@@ -281,14 +298,7 @@ __device__ __forceinline__ void cull_test(const CullCam& cc, const CullGeom& G, 
                     }
                 }
             }
-            // every depth <= m and every f32 Zc >= zlo: sdf < -trunc with room for the
-            // rounding of (depth - Zc), so the kernel's !(sdf < -trunc) test fails everywhere
-            skip = m <= 0.f || ((double)m + (double)trunc * (1 + 4 * 0x1p-24) + 1e-30 < zlo);
-            // free space: for every voxel fl(depth - Zc) >= mu (1 + 2^-21) and
-            // fl(fl(depth - Zc) fl(1/mu)) >= 1, i.e. tsdf = 1 exactly (mu in [2^-100, 2^100]);
-            // needs a frame record the fusion kernel fuses (every parameter < 2^60)
-            if (!skip && inside && zlo >= 0x1p-59 && zhi <= 0x1p59 && cc.good != 0.0)
-                fre = (double)mn - zhi >= (double)trunc * (1 + 0x1p-20);
+            cull_decide(cc, trunc, m, mn, zlo, zhi, inside, skip, fre);
         }
     }
 }
@@ -485,6 +495,294 @@ __global__ __launch_bounds__(256) void tsdf_refine_kernel(int H, int W, int z0, 
         if (skip) atomicOr(cull + word, 1u << (f & 31));
         else if (fre) atomicOr(freem + word, 1u << (f & 31));
     }
+}
+
+// ---------------------------------------------------------------------------
+// Whole-grid pre-pass in ONE persistent launch (round 6): the block pass streams the
+// depth maps (HBM-bound, ~0.4 ms for C5) while the culling of frames whose table is
+// complete runs beside it in the same workgroups, instead of after it (as separate
+// brick / cull / refine launches the culling added ~0.3 ms of latency-bound work behind
+// the stream; on separate streams the kernels starved each other: profiles/r6).
+//   Tasks: per frame, ceil(nbv / kPreRows) stream tasks (kPreRows block rows of the
+//   table each) and ceil(bricks / (8 kPreBpw)) culling tasks (kPreBpw 4x4x4 bricks of
+//   tiles per wave).  Frames are dealt to 8 shards (f % 8, with the workgroups
+//   blockIdx % 8); each shard hands its tasks out in ticket order, the culling tasks of
+//   a frame kPreLag shard frames behind its stream tasks, so a culling task normally
+//   finds its table complete.  A task's frame and the waits are shard-local, and a ticket
+//   is only taken by a running workgroup, so the waits cannot cycle.
+//   Hand-off (cdna_hip_programming.md §6 Guideline 16, R1): the table entries are stored
+//   write-through (8-B agent-scope atomic stores), every storing wave drains, a barrier,
+//   one lane adds to the frame's counter; the culling task's wave 0 polls that counter
+//   relaxed (bounded, s_sleep), ONE agent acquire, a barrier, then plain vector loads.
+//   A poll that gives up leaves the frame undecided (byte 0: every pair projected),
+//   which the fusion evaluates in full: slower, never wrong.
+//   The culling per (frame, brick), one wave: the brick's box against the full-resolution
+//   table, its footprint's blocks read by all 64 lanes (culled / free space decides the
+//   brick's 64 tiles); otherwise one tile per lane (cull_test), and the projected tiles'
+//   4 wave sub-tiles again, 4 per projected tile spread over the wave's lanes.  One byte
+//   per (frame, tile): bit 2q culled, bit 2q + 1 free space, for wave sub-tile q.
+//   tsdf_pack_kernel turns the bytes into the fusion's mask words and per-tile costs.
+// Every decision is the same proof as the separate passes' (cull_decide on a box that
+// contains the voxels); the masks may differ from theirs, the fused grids do not.
+// Measured (C5, profiles/r6/tsdf_fused_prepass_r6.txt): 0.71-0.73 ms for the launch vs 0.75 ms
+// for the separate passes, but the call is 2 % slower (1.75 vs 1.71 ms): the stream tasks
+// alone take 0.48 ms here (vs 0.40 in depth_blockmax_kernel, which runs at twice the waves per
+// SIMD), the culling tasks alone 0.42 (vs 0.33: 4 vs 8 waves per SIMD for latency-bound tests),
+// and the fusion after it runs ~25 us slower.  Selected by SFMHIP_AB=3 (tests keep it exact).
+// The ticket loop's branches are on readfirstlane'd values: with the task index left in a VGPR
+// the compiler restructured the loop per lane and the barriers deadlocked (first build, r6).
+constexpr int kPreThreads = 512, kPreWaves = kPreThreads / 64;
+constexpr int kPreRows = 4;            // table block rows per stream task
+constexpr int kPreHalf = 8;            // depth rows per load batch of a stream task
+constexpr int kPreBpw = 4;             // bricks per culling task per wave (dealt to the waves one by one)
+constexpr int kPreLag = 4;             // shard frames between a frame's stream and culling tasks
+constexpr int kPreShards = kNumXcd;
+constexpr int kPreTicketStride = 32;   // words between the shards' tickets (own 128-B lines)
+constexpr int kPreBrickLoads = 64;     // brick footprints of up to 64 x 64 table blocks
+constexpr unsigned kPreSpinMax = 1u << 16;   // x (sc1 load + s_sleep) ~ 0.1 s
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// LDS written by some lanes of a wave, then read by other lanes of the same wave
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ unsigned long long f2bits(float lo, float hi) {
+    return (unsigned long long)__float_as_uint(lo) | ((unsigned long long)__float_as_uint(hi) << 32);
+}
+
+// One wave: the brick box's decision from the full-resolution table (0 undecided, 1
+// culled, 2 free space); every lane computes the same footprint.
+__device__ __forceinline__ int brick_decide_wave(const CullCam& cc, const CullGeom& G, int xa, int xb, int ya, int yb,
+                                                 int za, int zb, int Hd, int Wd, float trunc, int f,
+                                                 const float2* __restrict__ bmm, int nbu, int nbv, int4 rg, int lane) {
+    int u0, u1, v0, v1;
+    double zlo, zhi;
+    bool inside = false;
+    const int st = box_footprint(cc, G, xa, xb, ya, yb, za, zb, Hd, Wd, u0, u1, v0, v1, zlo, zhi, inside);
+    if (st == 1) return 1;
+    if (st != 2) return 0;
+    const int bu0 = u0 / kCullBlock, bu1 = u1 / kCullBlock, bv0 = v0 / kCullBlock, bv1 = v1 / kCullBlock;
+    const int nu = bu1 - bu0 + 1, nb = nu * (bv1 - bv0 + 1);
+    if (nb > 64 * kPreBrickLoads || bu0 < rg.x || bu1 > rg.y || bv0 < rg.z || bv1 > rg.w) return 0;
+    const float2* bp = bmm + ((size_t)f * nbv + bv0) * nbu + bu0;
+    float m = -__builtin_inff(), mn = __builtin_inff();
+    for (int k = lane; k < nb; k += 64) {
+        const int r = k / nu;
+        const float2 e = bp[(size_t)r * nbu + (k - r * nu)];
+        m = fmaxf(m, e.y);
+        mn = fminf(mn, e.x);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        m = fmaxf(m, __shfl_xor(m, off, 64));
+        mn = fminf(mn, __shfl_xor(mn, off, 64));
+    }
+    bool skip, fre;
+    cull_decide(cc, trunc, m, mn, zlo, zhi, inside, skip, fre);
+    return skip ? 1 : fre ? 2 : 0;
+}
+
+__global__ __launch_bounds__(kPreThreads, 4) void tsdf_prepass_kernel(
+    const float* __restrict__ depth, int F, int Hd, int Wd, int nbu, int nbv, const int4* __restrict__ range,
+    float2* bmm, int H, int W, int z0, int z1, const CullCam* __restrict__ cams, CullGeom G, float trunc,
+    unsigned* tickets, unsigned* fdone, unsigned char* __restrict__ dec, unsigned* gaveup) {
+    __shared__ int s_task, s_ok, s_next;
+    __shared__ int plist[kPreWaves][64];
+    __shared__ unsigned char sub[kPreWaves][64][kCullSub];
+    // every branch around a barrier is on a readfirstlane'd (scalar) value: the compiler must see
+    // the control flow as uniform, or it may restructure the ticket loop per lane
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int shard = (int)(blockIdx.x % kPreShards);
+    const int ntx = (W + kTsdfTX - 1) / kTsdfTX, nty = (H + kTsdfTY - 1) / kTsdfTY;
+    const int ntz = (z1 - z0 + kTsdfTZ - 1) / kTsdfTZ;
+    const int nqx = (ntx + 3) >> 2, nqy = (nty + 3) >> 2, nqz = (ntz + 3) >> 2;
+    const int nbricks = nqx * nqy * nqz;
+    const int64_t ntiles = (int64_t)ntx * nty * ntz;
+    const int rows = kPreRows, bpw = kPreBpw, lag = kPreLag;
+    const int ns = (nbv + rows - 1) / rows;
+    const int nc = (nbricks + kPreWaves * bpw - 1) / (kPreWaves * bpw);
+    const int nfs = F > shard ? (F - shard + kPreShards - 1) / kPreShards : 0;   // this shard's frames
+    const int per = ns + nc;
+    const int total = nfs ? (nfs + lag) * per : 0;
+    gu32* tk = (gu32*)(tickets + shard * kPreTicketStride);
+    for (;;) {
+        if (tid == 0) s_task = (int)__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int t = __builtin_amdgcn_readfirstlane(s_task);
+        __syncthreads();
+        if (t >= total) break;
+        const int blk = t / per, j = t - blk * per;
+        if (j < ns && blk < nfs) {
+            // ---- stream task: block rows [rows j, rows (j + 1)) of frame shard + 8 blk
+            const int f = shard + kPreShards * blk;
+            const int4 rg = range[f];
+            const float* dp = depth + (size_t)f * Hd * Wd;
+            for (int bv = j * rows; bv < min(nbv, (j + 1) * rows); ++bv) {
+                if (bv < rg.z || bv > rg.w) continue;
+                const int r0 = bv * kCullBlock, nr = min(kCullBlock, Hd - r0);
+                for (int c0 = 0; c0 < Wd; c0 += 4 * kPreThreads) {
+                    const int u = c0 + 4 * tid, bu = u / kCullBlock;
+                    const bool act = u < Wd && bu >= rg.x && bu <= rg.y;
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    float m = -__builtin_inff(), mn = __builtin_inff();
+                    for (int h = 0; h < kCullBlock; h += kPreHalf) {   // kPreHalf rows' loads in flight
+                        f4v q[kPreHalf];
+#pragma unroll
+                        for (int r = 0; r < kPreHalf; ++r) {   // streamed once here: non-temporal
+                            q[r] = f4v{-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+                            if (act && h + r < nr)
+                                q[r] = __builtin_nontemporal_load(
+                                    reinterpret_cast<const f4v*>(dp + (size_t)(r0 + h + r) * Wd + u));
+                        }
+#pragma unroll
+                        for (int r = 0; r < kPreHalf; ++r)
+                            m = fmaxf(m, fmaxf(fmaxf(q[r].x, q[r].y), fmaxf(q[r].z, q[r].w)));
+#pragma unroll
+                        for (int r = 0; r < kPreHalf; ++r)
+                            if (h + r < nr)
+                                mn = fminf(mn, fminf(fminf(nan_low(q[r].x), nan_low(q[r].y)),
+                                                     fminf(nan_low(q[r].z), nan_low(q[r].w))));
+                    }
+                    m = fmaxf(m, __shfl_xor(m, 1, 4));
+                    m = fmaxf(m, __shfl_xor(m, 2, 4));
+                    mn = fminf(mn, __shfl_xor(mn, 1, 4));
+                    mn = fminf(mn, __shfl_xor(mn, 2, 4));
+                    if ((tid & 3) == 0 && act && bu < nbu)   // write-through: the culling tasks read it in this launch
+                        __hip_atomic_store((gu64*)(bmm + ((size_t)f * nbv + bv) * nbu + bu), f2bits(mn, m),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+            __syncthreads();
+            if (tid == 0) __hip_atomic_fetch_add((gu32*)(fdone + f), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (j < ns || blk < lag) continue;   // (scalar branch)
+        // ---- culling task: bricks of part j - ns of frame shard + 8 (blk - lag)
+        const int f = shard + kPreShards * (blk - lag), part = j - ns;
+        if (tid == 0) {
+            int ok = 1;
+            unsigned spins = 0;
+            while (__hip_atomic_load((gu32*)(fdone + f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ns) {
+                if (++spins > kPreSpinMax) { ok = 0; break; }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            if (!ok) atomicAdd(gaveup, 1u);
+            s_ok = ok;
+            s_next = 0;
+        }
+        if (wv == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        const bool ok = __builtin_amdgcn_readfirstlane(s_ok) != 0;
+        CullCam cc;
+        load_cull_cam(cams, f, cc);
+        const int4 rg = range[f];
+        // the task's bricks, dealt to its waves one at a time (bricks differ in cost)
+        const int b0 = part * kPreWaves * bpw, nbt = min(kPreWaves * bpw, nbricks - b0);
+        for (;;) {
+            int bi = 0;
+            if (lane == 0) bi = atomicAdd(&s_next, 1);
+            bi = __builtin_amdgcn_readfirstlane(bi);
+            if (bi >= nbt) break;
+            const int brick = b0 + bi;
+            const bool bok = true;
+            const int qx = brick % nqx, qy = (brick / nqx) % nqy, qz = brick / (nqx * nqy);
+            const int tx = qx * 4 + (lane & 3), ty = qy * 4 + ((lane >> 2) & 3), tz = qz * 4 + (lane >> 4);
+            const bool tile_ok = bok && tx < ntx && ty < nty && tz < ntz;
+            const int64_t tile = ((int64_t)tz * nty + ty) * ntx + tx;
+            int bd = 0;
+            if (bok && ok) {
+                const int xa = qx * 4 * kTsdfTX, xb = min(W, (qx * 4 + 4) * kTsdfTX) - 1;
+                const int ya = qy * 4 * kTsdfTY, yb = min(H, (qy * 4 + 4) * kTsdfTY) - 1;
+                const int za = z0 + qz * 4 * kTsdfTZ, zb = min(z1, z0 + min(ntz, qz * 4 + 4) * kTsdfTZ) - 1;
+                bd = brick_decide_wave(cc, G, xa, xb, ya, yb, za, zb, Hd, Wd, trunc, f, bmm, nbu, nbv, rg, lane);
+            }
+            // one cull_test call site (register pressure): the lane's tile, then the projected
+            // tiles' wave sub-tiles, 64 per round over the wave's lanes
+            bool skip = bd == 1, fre = bd == 2, proj = false;
+            int n = -1;   // -1: the tile round; then the number of projected tiles
+            for (int base = 0;;) {
+                int sx = tx, sy = ty, sz = tz, q = 0, l = lane, yh = kTsdfTY;
+                bool valid;
+                if (n < 0) {
+                    valid = tile_ok && ok && bd == 0;
+                } else {
+                    const int it = base + lane;
+                    valid = it < kCullSub * n;
+                    l = plist[wv][valid ? it / kCullSub : 0];
+                    q = it % kCullSub;
+                    sx = qx * 4 + (l & 3), sy = qy * 4 + ((l >> 2) & 3), sz = qz * 4 + (l >> 4);
+                    yh = kTsdfTY / kCullSub;
+                }
+                const int xa = sx * kTsdfTX, xb = min(W, xa + kTsdfTX) - 1;
+                const int ya = sy * kTsdfTY + yh * q, yb = min(H, ya + yh) - 1;
+                const int za = z0 + sz * kTsdfTZ, zb = min(z1, za + kTsdfTZ) - 1;
+                bool s2 = false, f2v = false;
+                if (valid) cull_test(cc, G, xa, xb, ya, yb, za, zb, Hd, Wd, trunc, f, bmm, nbu, nbv, range, s2, f2v);
+                if (n < 0) {
+                    if (valid) {
+                        skip = s2;
+                        fre = f2v;
+                    }
+                    proj = tile_ok && ok && !skip && !fre;
+                    const unsigned long long bal = __ballot(proj);
+                    if (proj) plist[wv][__popcll(bal & ((1ull << lane) - 1ull))] = lane;
+                    wave_lds_sync();   // the lists are per wave: no workgroup barrier (bricks differ in cost)
+                    n = __popcll(bal);
+                } else {
+                    if (valid) sub[wv][l][q] = (unsigned char)(s2 ? 1 : f2v ? 2 : 0);
+                    base += 64;
+                }
+                if (n >= 0 && base >= kCullSub * n) break;
+            }
+            wave_lds_sync();
+            if (tile_ok) {
+                unsigned b = skip ? 0x55u : fre ? 0xAAu : 0u;
+                if (proj)
+                    for (int q = 0; q < kCullSub; ++q) b |= (unsigned)sub[wv][lane][q] << (2 * q);
+                dec[(size_t)f * ntiles + tile] = (unsigned char)b;
+            }
+        }
+    }
+}
+
+// Mask words and per-tile costs from the pre-pass bytes: one thread per (tile, word).
+__global__ __launch_bounds__(256) void tsdf_pack_kernel(int F, int64_t ntiles, int nw,
+                                                        const unsigned char* __restrict__ dec,
+                                                        unsigned* __restrict__ cull, unsigned* __restrict__ freem,
+                                                        unsigned* __restrict__ tcost) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntiles * nw) return;
+    const int64_t tile = i % ntiles;
+    const int w = (int)(i / ntiles);
+    const int nb = min(32, F - 32 * w);
+    unsigned cw[kCullSub] = {0u, 0u, 0u, 0u}, fw[kCullSub] = {0u, 0u, 0u, 0u};
+    const unsigned char* dp = dec + (size_t)32 * w * ntiles + tile;
+#pragma unroll 8
+    for (int j = 0; j < nb; ++j) {
+        const unsigned b = dp[(size_t)j * ntiles];
+#pragma unroll
+        for (int q = 0; q < kCullSub; ++q) {
+            cw[q] |= ((b >> (2 * q)) & 1u) << j;
+            fw[q] |= ((b >> (2 * q + 1)) & 1u) << j;
+        }
+    }
+    const unsigned live = nb >= 32 ? ~0u : (1u << nb) - 1u;
+    unsigned c = 0u;
+#pragma unroll
+    for (int q = 0; q < kCullSub; ++q) {
+        const int64_t word = (tile * kCullSub + q) * nw + w;
+        cull[word] = cw[q];
+        freem[word] = fw[q];
+        c += 4u * __popc(live & ~cw[q] & ~fw[q]) + __popc(live & fw[q] & ~cw[q]);
+    }
+    if (tcost && c) atomicAdd(tcost + tile, c);
 }
 
 // Validated camera records, 16 floats per frame (non-finite or >= 2^60 anywhere:
@@ -899,11 +1197,16 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const bool latency_mode = kn.tsdf_latency >= 0 ? kn.tsdf_latency != 0 : rounds < kTsdfLatencyRounds;
     // a thin slab (fewer than kTsdfDeepRounds rounds of resident fusion waves: a z-slab of an N >= 4
     // split): four projected frames per fusion stage and no brick / refinement pre-passes (their
-    // fixed cost outweighs the fusion work they save there); SFMHIP_AB=1 keeps the whole-grid form
-    const bool deep = rounds < kTsdfDeepRounds && kn.ab != 1;
+    // fixed cost outweighs the fusion work they save there); SFMHIP_AB=1 (2) keeps the whole-grid
+    // form with the separate (fused) pre-passes
+    const bool deep = rounds < kTsdfDeepRounds && kn.ab != 1 && kn.ab != 3;
     const bool refine = !latency_mode && !deep;
     const bool brick = !latency_mode && !deep;
     const bool vox_test = !latency_mode;
+    // SFMHIP_AB=3: the whole-grid pre-passes as one persistent launch (tsdf_prepass_kernel) instead
+    // of the separate block / brick / cull / refine launches: bit-identical grids, measured 2 %
+    // slower on C5 (1.75 vs 1.71 ms: profiles/r6/tsdf_fused_prepass_r6.txt), so not the default
+    const bool fusedpre = brick && !ext_table && !stats && Wd % 4 == 0 && kn.ab == 3;
     GridBox gb;
     CullGeom cg;
     {
@@ -929,7 +1232,9 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     // scratch (stream-ordered, one block): counters + per-tile costs first (zeroed by the setup kernel)
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const int nzero = kNCnt + (order ? (int)ntiles : 0);
+    // zeroed words: [pre-pass tickets, one 128-B line per shard] [counters] [per-tile costs] [frame counters]
+    const int n_tk = fusedpre ? kPreShards * kPreTicketStride : 0;
+    const int nzero = n_tk + kNCnt + (order ? (int)ntiles : 0) + (fusedpre ? cf : 0);
     const size_t o_cnt = take((size_t)nzero * sizeof(unsigned));
     const size_t o_rec = take((size_t)cf * 16 * sizeof(float));
     const size_t o_cam = take((size_t)cf * sizeof(CullCam));
@@ -937,9 +1242,11 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     const size_t o_bmm = ext_table ? 0 : take((size_t)cf * nbu * nbv * sizeof(float2));
     const size_t o_msk = take((size_t)nsub * nwmax * sizeof(unsigned));
     const size_t o_fre = take((size_t)nsub * nwmax * sizeof(unsigned));
-    const size_t o_ctab = brick ? take((size_t)cf * ncbu * ncbv * sizeof(float2)) : 0;
-    const size_t o_bdec = brick ? take((size_t)cull_bricks * cf) : 0;
-    const size_t o_pl = refine ? take((size_t)plist_cap * sizeof(unsigned)) : 0;
+    const bool sep = brick && !fusedpre;
+    const size_t o_ctab = sep ? take((size_t)cf * ncbu * ncbv * sizeof(float2)) : 0;
+    const size_t o_bdec = sep ? take((size_t)cull_bricks * cf) : 0;
+    const size_t o_pl = refine && !fusedpre ? take((size_t)plist_cap * sizeof(unsigned)) : 0;
+    const size_t o_dec = fusedpre ? take((size_t)cf * ntiles) : 0;
     const size_t o_ord = order ? take((size_t)main_slots * sizeof(unsigned)) : 0;
     char* sc = nullptr;
     if (scratch_alloc((void**)&sc, off, st) != hipSuccess) {
@@ -947,17 +1254,30 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         set_error("sfmhip_tsdf_integrate: scratch allocation of %zu bytes failed", off);
         return SFMHIP_E_HIP;
     }
-    unsigned* cnt = reinterpret_cast<unsigned*>(sc + o_cnt);
+    unsigned* zbase = reinterpret_cast<unsigned*>(sc + o_cnt);
+    unsigned* tickets = zbase;
+    unsigned* cnt = zbase + n_tk;
     unsigned* tcost = order ? cnt + kNCnt : nullptr;
+    unsigned* fdone = cnt + kNCnt + (order ? ntiles : 0);
+    unsigned char* pdec = fusedpre ? reinterpret_cast<unsigned char*>(sc + o_dec) : nullptr;
     float* rec = reinterpret_cast<float*>(sc + o_rec);
     CullCam* ccam = reinterpret_cast<CullCam*>(sc + o_cam);
     int4* crange = reinterpret_cast<int4*>(sc + o_rng);
     float2* cbmm = ext_table ? nullptr : reinterpret_cast<float2*>(sc + o_bmm);
     unsigned* cmask = reinterpret_cast<unsigned*>(sc + o_msk);
     unsigned* cfree = reinterpret_cast<unsigned*>(sc + o_fre);
-    float2* ctab = brick ? reinterpret_cast<float2*>(sc + o_ctab) : nullptr;
-    unsigned char* bdec = brick ? reinterpret_cast<unsigned char*>(sc + o_bdec) : nullptr;
-    unsigned* plist = refine ? reinterpret_cast<unsigned*>(sc + o_pl) : nullptr;
+    float2* ctab = sep ? reinterpret_cast<float2*>(sc + o_ctab) : nullptr;
+    unsigned char* bdec = sep ? reinterpret_cast<unsigned char*>(sc + o_bdec) : nullptr;
+    unsigned* plist = refine && !fusedpre ? reinterpret_cast<unsigned*>(sc + o_pl) : nullptr;
+    int pre_grid = 0;
+    if (fusedpre) {   // the persistent grid: every resident workgroup, a multiple of the shard count
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tsdf_prepass_kernel, kPreThreads, 0) != hipSuccess ||
+            nb <= 0)
+            nb = 1;
+        (void)hipGetLastError();
+        pre_grid = std::max(kPreShards, nb * ncu / kPreShards * kPreShards);
+    }
     unsigned* ord = order ? reinterpret_cast<unsigned*>(sc + o_ord) : nullptr;
     int rc = SFMHIP_OK;
     // integration steps of at most kTsdfMaxFrames frames, in order on the stream
@@ -969,9 +1289,14 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         const float* kp = Kf + (size_t)f0 * 4;
         hipLaunchKernelGGL(tsdf_setup_kernel, dim3(ceil_div(nf, 64) + std::min(64, ceil_div(nzero, 1024) + 1)),
                            dim3(64), 0, st, pp, kp, nf, rec, ccam, ext_table ? 1 : 2, H, W, z0, z1, Hd, Wd, cg, nbu,
-                           nbv, crange, cnt, nzero);
+                           nbv, crange, zbase, nzero);
         const float2* tab = ext_table ? ext_table + (size_t)f0 * nbv * nbu : cbmm;
-        if (!ext_table) {
+        if (fusedpre) {
+            hipLaunchKernelGGL(tsdf_prepass_kernel, dim3(pre_grid), dim3(kPreThreads), 0, st, dp, nf, Hd, Wd, nbu, nbv,
+                               crange, cbmm, H, W, z0, z1, ccam, cg, trunc, tickets, fdone, pdec, cnt + 1);
+            hipLaunchKernelGGL(tsdf_pack_kernel, dim3((unsigned)ceil_div(ntiles * nw, (int64_t)256)), dim3(256), 0, st,
+                               nf, ntiles, nw, pdec, cmask, cfree, tcost);
+        } else if (!ext_table) {
             if (Wd % 4 == 0)
                 hipLaunchKernelGGL(depth_blockmax_kernel<true>, dim3(ceil_div(Wd, 1024), nbv, nf), dim3(256), 0, st,
                                    dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
@@ -979,16 +1304,17 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
                 hipLaunchKernelGGL(depth_blockmax_kernel<false>, dim3(ceil_div(Wd, 256), nbv, nf), dim3(256), 0, st,
                                    dp, nf, Hd, Wd, nbu, nbv, crange, cbmm);
         }
-        if (brick) {
+        if (sep) {
             const int64_t nc = (int64_t)nf * ncbu * ncbv, nd = (cull_bricks + 63) / 64 * 64 * nf;
             hipLaunchKernelGGL(coarse_table_kernel, dim3((unsigned)ceil_div(nc, (int64_t)256)), dim3(256), 0, st, tab,
                                nf, nbu, nbv, ncbu, ncbv, ext_table ? nullptr : crange, ctab);
             hipLaunchKernelGGL(tsdf_brick_kernel, dim3((unsigned)ceil_div(nd, (int64_t)256)), dim3(256), 0, st, H, W,
                                z0, z1, nf, Hd, Wd, ccam, cg, trunc, ctab, ncbu, ncbv, (int)cull_bricks, bdec);
         }
-        hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nw * 2)), dim3(1024), 0, st, H, W, z0, z1,
-                           nf, Hd, Wd, ccam, cg, trunc, tab, nbu, nbv, crange, nw, bdec, (unsigned short*)cmask,
-                           (unsigned short*)cfree, plist, cnt + kCntPl, tcost);
+        if (!fusedpre)
+            hipLaunchKernelGGL(tsdf_cull_kernel, dim3((unsigned)(cull_bricks * nw * 2)), dim3(1024), 0, st, H, W, z0,
+                               z1, nf, Hd, Wd, ccam, cg, trunc, tab, nbu, nbv, crange, nw, bdec,
+                               (unsigned short*)cmask, (unsigned short*)cfree, plist, cnt + kCntPl, tcost);
         // refinement: grid-stride over the device-side count (atomic ORs: any grid gives the
         // same masks); 8192 x 256 threads fill the 6 waves per SIMD its VGPRs allow
         if (plist)

@@ -236,14 +236,18 @@ def _tsdf_case(R=48, F=12, Hd=96, Wd=128, focal=110.0):
     return R, depth.numpy(), poses.numpy(), K.numpy()
 
 
-# "auto": small grids run in latency mode; "0" / "1" force the whole-grid mode (brick and
-# refinement passes, per-voxel block test) / the latency mode
-LAT_MODES = ["auto", "0", "1"]
+# "auto": the library's choice; "0" / "1": whole-grid / latency mode; "w1" / "w3": the whole-grid
+# form even on thin grids, with separate block / brick / cull / refine launches (SFMHIP_AB=1) or
+# with those pre-passes fused in one persistent launch (SFMHIP_AB=3)
+LAT_MODES = ["auto", "0", "1", "w1", "w3"]
 
 
 def _set_lat(knob, lat):
     if lat in ("0", "1"):
         knob("TSDF_LATENCY", lat)
+    elif lat in ("w1", "w3"):
+        knob("TSDF_LATENCY", 0)
+        knob("AB", lat[1])
 
 
 def _close_to_seq(Tg, Wg, Ts, Ws):
@@ -337,15 +341,17 @@ def test_tsdf_multi_step_bitexact(sfm, gpu):
 def test_tsdf_modes_and_splits_identical(sfm, gpu, knob):
     """Full-resolution frames, 96^3 grid, z-slab: both modes (whole-grid with brick /
     refinement / per-voxel block test, latency) and both thin-grid forms (the default: four
-    projected frames per fusion stage, no brick / refinement passes; SFMHIP_AB=1: the
-    whole-grid form) give the same grid bit for bit, equal to
+    projected frames per fusion stage, no brick / refinement passes; SFMHIP_AB=1 / 3: the
+    whole-grid form with separate / fused pre-passes) give the same grid bit for bit, equal to
     the oracle on sampled slices, with both culling and the free-space path active
     (cull stats)."""
     depth, poses, K = syn.tsdf_scene(40, seed=3)   # two mask words per sub-tile
     bnd = ((-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 95)
     out = []
-    # AB=1: the whole-grid form (brick + refinement, two frames per stage) where the thin default differs
-    variants = [{}, dict(TSDF_LATENCY=0), dict(TSDF_LATENCY=1), dict(AB=1), dict(AB=1, TSDF_LATENCY=0)]
+    # AB=1 / 3: the whole-grid form (separate / fused pre-passes, two frames per stage) where the thin
+    # default differs
+    variants = [{}, dict(TSDF_LATENCY=0), dict(TSDF_LATENCY=1), dict(AB=1), dict(AB=1, TSDF_LATENCY=0),
+                dict(AB=3, TSDF_LATENCY=0)]
     for v in variants:
         knob("TSDF_LATENCY", -1)
         knob("AB", 0)
@@ -366,6 +372,31 @@ def test_tsdf_modes_and_splits_identical(sfm, gpu, knob):
         Tr, Wr = ov.tsdf_integrate(zeros, zeros, dc, pc, kc, *bnd[:2], np.float32(bnd[2]), z0, z0 + 2)
         np.testing.assert_array_equal(out[0][1][z0:z0 + 2].numpy(), Wr[z0:z0 + 2])
         np.testing.assert_array_equal(out[0][0][z0:z0 + 2].numpy(), Tr[z0:z0 + 2])
+
+
+def test_tsdf_fused_prepass_hand_off_repeated_scenes(sfm, gpu, knob):
+    """The fused whole-grid pre-pass (SFMHIP_AB=3: the block pass and the culling in one
+    persistent launch, the table handed from stream tasks to culling tasks inside the launch)
+    against the separate launches (SFMHIP_AB=1), call after call on different scenes and
+    carried grid state, so a culling task that read a stale table line (left by the previous
+    call's scene at the same scratch address) would cull differently: the grids must match
+    bit for bit every call.  Full-resolution depth maps, a 160^3 grid, uneven frame costs."""
+    bnd = ((-1.2,) * 3, (1.2,) * 3, 3 * 2.4 / 159)
+    grids = {}
+    for ab in (1, 3):
+        knob("AB", ab)
+        knob("TSDF_LATENCY", 0)
+        T = torch.zeros((160, 160, 160), dtype=torch.float32, device=gpu)
+        W = torch.zeros_like(T)
+        outs = []
+        for seed in (3, 11, 3, 29):
+            depth, poses, K = syn.tsdf_scene(24 + seed, seed=seed, device=gpu)
+            sfm.tsdf_integrate(T, W, depth, poses, K, *bnd)
+            outs.append((T.cpu(), W.cpu()))
+        grids[ab] = outs
+    for i, ((t1, w1), (t3, w3)) in enumerate(zip(grids[1], grids[3])):
+        assert torch.equal(w1, w3) and torch.equal(t1, t3), i
+    assert (grids[3][-1][1] > 0).float().mean() > 0.3
 
 
 @pytest.mark.parametrize("lat", LAT_MODES)
