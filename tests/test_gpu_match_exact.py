@@ -296,3 +296,26 @@ def test_int16_graph_c3_full_size_equals_int32(sfm, gpu):
     assert int(bank.last_resolved.item()) == n16 > 0          # the same rows went to the exact pass
     for lo in range(0, pairs.shape[0], 4096):                 # compare in slices (the int32 graph is 539 MB)
         assert torch.equal(g16[lo:lo + 4096].to(torch.int32), g32[lo:lo + 4096]), lo
+
+
+@pytest.mark.parametrize("cert", ["1", "0"])
+def test_exact_float_empty_and_single_keypoint_images(sfm, gpu, knob, cert):
+    """Exact float mode, int32 and int16 graphs: a query image with 0 keypoints yields only
+    padding rows, a candidate image with 0 or 1 keypoints (no second-best) gives -1 for every
+    query row, padding rows never match; the rest equals the oracle, and an image against itself
+    matches nearly every row to its own index."""
+    knob("MATCH_CERT", cert)
+    x = syn.superpoint_like(3, 300, 128, seed=77).numpy()
+    nk = np.array([0, 1, 300], np.int32)
+    for i in range(3):
+        x[i, nk[i]:] = 0
+    pairs = np.array([[0, 2], [2, 0], [1, 2], [2, 1], [0, 1], [2, 2]], np.int32)
+    bank = sfm.DescriptorBank.from_float(torch.from_numpy(x), n_kpts=nk, mode=1, exact=True)
+    g32 = bank.match(pairs, ratio=0.75).cpu().numpy().astype(np.int64)
+    g16 = _i16(bank, pairs, ratio=0.75)
+    assert np.array_equal(g16, g32)
+    assert np.array_equal(g32[:, :300], _oracle(x, nk, pairs, (3, 4))[:, :300])
+    assert (g32[1] == -1).all() and (g32[3] == -1).all()       # candidate image empty / single keypoint
+    assert (g32[0] == -1).all() and (g32[4] == -1).all()       # query image empty: padding rows only
+    assert (g32[:, 300:] == -1).all()
+    assert (g32[5, :300] == np.arange(300)).mean() > 0.9      # self-match: nearly every row its own index

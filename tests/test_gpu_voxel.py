@@ -625,3 +625,30 @@ def test_tsdf_planned_uneven_slabs_bitexact(sfm, gpu):
     for z0, z1 in slabs:
         sfm.tsdf_integrate(T1, W1, depth, poses, K, *args, z0, z1, block_table=tab)
     assert torch.equal(T0, T1) and torch.equal(W0, W1)
+
+
+@pytest.mark.parametrize("lat", LAT_MODES)
+def test_tsdf_degenerate_calls(sfm, gpu, knob, lat):
+    """Valid but degenerate calls: zero frames and an empty z-slab leave the grids untouched;
+    one frame into the smallest grid (2^3) and into a 1-voxel-thick slab equal the oracle."""
+    _set_lat(knob, lat)
+    R, depth, poses, K = _tsdf_case(R=16, F=4)
+    dt, pt, kt = torch.from_numpy(depth), torch.from_numpy(poses), torch.from_numpy(K)
+    rng = np.random.default_rng(5)
+    T0 = rng.uniform(-1, 1, (R, R, R)).astype(np.float32)
+    W0 = rng.integers(0, 3, (R, R, R)).astype(np.float32)
+    args = ((-1, -1, -1), (1, 1, 1), 0.3)
+    T, W = torch.from_numpy(T0).to(gpu), torch.from_numpy(W0).to(gpu)
+    sfm.tsdf_integrate(T, W, dt[:0], pt[:0], kt[:0], *args)                   # no frames
+    sfm.tsdf_integrate(T, W, dt, pt, kt, *args, 7, 7)                        # empty slab
+    assert np.array_equal(T.cpu().numpy(), T0) and np.array_equal(W.cpu().numpy(), W0)
+    sfm.tsdf_integrate(T, W, dt[:1], pt[:1], kt[:1], *args, 7, 8)            # one frame, one z layer
+    Tr, Wr = ov.tsdf_integrate(T0, W0, depth[:1], poses[:1], K[:1], *args[:2], np.float32(args[2]), 7, 8)
+    np.testing.assert_array_equal(W.cpu().numpy(), Wr)
+    np.testing.assert_array_equal(T.cpu().numpy(), Tr)
+    t2, w2 = torch.zeros((2, 2, 2), device=gpu), torch.zeros((2, 2, 2), device=gpu)   # the smallest grid
+    sfm.tsdf_integrate(t2, w2, dt, pt, kt, (-0.5,) * 3, (0.5,) * 3, 0.3)
+    Tr2, Wr2 = ov.tsdf_integrate(np.zeros((2, 2, 2), np.float32), np.zeros((2, 2, 2), np.float32), depth, poses, K,
+                                 (-0.5,) * 3, (0.5,) * 3, np.float32(0.3))
+    np.testing.assert_array_equal(w2.cpu().numpy(), Wr2)
+    np.testing.assert_array_equal(t2.cpu().numpy(), Tr2)
