@@ -819,11 +819,11 @@ using namespace sfmhip;
 extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const double* pts2d, const int64_t* pair_off,
                                int n_pairs, int64_t n_obs, double ftol, double xtol, double gtol, int max_nfev,
                                double* cost, int32_t* nfev, int32_t* njev, int32_t* status, void* stream) {
-    SFMHIP_REQUIRE(cam && K && X && pts2d && pair_off && cost && nfev && njev && status,
-                   "sfmhip_ba_solve: null pointer");
     SFMHIP_REQUIRE(n_pairs >= 0, "sfmhip_ba_solve: negative n_pairs");
     SFMHIP_REQUIRE(n_obs >= 0, "sfmhip_ba_solve: negative n_obs");
     if (n_pairs == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(cam && K && X && pts2d && pair_off && cost && nfev && njev && status,
+                   "sfmhip_ba_solve: null pointer");
     hipStream_t st = as_stream(stream);
     double* scratch = nullptr;
     const bool fused = knobs().ab == 9;   // A/B (temporary): the fused trial + Jacobian form

@@ -83,9 +83,9 @@ using namespace sfmhip;
 
 extern "C" int sfmhip_word_histogram(const int32_t* codes, const int64_t* offsets, int n_img, int k,
                                      int32_t* hist, void* stream) {
-    SFMHIP_REQUIRE(codes && offsets && hist, "sfmhip_word_histogram: null pointer");
     SFMHIP_REQUIRE(n_img >= 0 && k > 0 && k <= 16384, "sfmhip_word_histogram: bad shape");
     if (n_img == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(codes && offsets && hist, "sfmhip_word_histogram: null pointer");
     hipLaunchKernelGGL(histogram_kernel, dim3(n_img), dim3(256), k * sizeof(int32_t), as_stream(stream), codes,
                        offsets, k, hist);
     return check_launch("histogram_kernel");

@@ -371,9 +371,9 @@ using namespace sfmhip;
 
 extern "C" int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_obs, const double* x0,
                                       const double* x1, int64_t n, double* X4, void* stream) {
-    SFMHIP_REQUIRE(P && x0 && x1 && X4, "sfmhip_triangulate_dlt: null pointer");
     SFMHIP_REQUIRE(n >= 0, "sfmhip_triangulate_dlt: negative n");
     if (n == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(P && x0 && x1 && X4, "sfmhip_triangulate_dlt: null pointer");
     hipStream_t st = as_stream(stream);
     unsigned* slots = nullptr;   // [n_waves][64] listed observations + [n_waves] counts
     const int64_t n_waves = ceil_div(n, 64);
@@ -405,9 +405,9 @@ extern "C" int sfmhip_triangulate_dlt(const double* P, const int32_t* pair_of_ob
 extern "C" int sfmhip_reproj_residual(const double* cam, const double* K, const double* X,
                                       const double* pts2d, const int32_t* pair_of_obs, int64_t n,
                                       double* r, void* stream) {
-    SFMHIP_REQUIRE(cam && K && X && pts2d && r, "sfmhip_reproj_residual: null pointer");
     SFMHIP_REQUIRE(n >= 0, "sfmhip_reproj_residual: negative n");
     if (n == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(cam && K && X && pts2d && r, "sfmhip_reproj_residual: null pointer");
     hipLaunchKernelGGL(residual_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), cam,
                        K, X, pts2d, pair_of_obs, n, r);
     return check_launch("residual_kernel");
@@ -429,9 +429,9 @@ HostStage g_stage[64];
 
 extern "C" int sfmhip_reproj_residual_host(const double* cam, const double* K, const double* X,
                                            const double* pts2d, int64_t n, double* r, void* stream) {
-    SFMHIP_REQUIRE(cam && K && X && r, "sfmhip_reproj_residual_host: null pointer");
     SFMHIP_REQUIRE(n >= 0 && n < ((int64_t)1 << 40), "sfmhip_reproj_residual_host: bad n");
     if (n == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(cam && K && X && r, "sfmhip_reproj_residual_host: null pointer");
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
         (void)hipGetLastError();
@@ -483,9 +483,9 @@ extern "C" int sfmhip_reproj_fd_jacobian(const double* cam, const double* K, con
                                          const double* pts2d, const int32_t* pair_of_obs, int n_pairs,
                                          int64_t n, const double* f0, double* r, double* jvals,
                                          void* stream) {
-    SFMHIP_REQUIRE(cam && K && X && pts2d && jvals, "sfmhip_reproj_fd_jacobian: null pointer");
     SFMHIP_REQUIRE(n >= 0 && n_pairs >= 1, "sfmhip_reproj_fd_jacobian: bad counts");
     if (n == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(cam && K && X && pts2d && jvals, "sfmhip_reproj_fd_jacobian: null pointer");
     hipStream_t st = as_stream(stream);
     double* Rt = nullptr;
     if (scratch_alloc((void**)&Rt, (size_t)n_pairs * 36 * sizeof(double), st) != hipSuccess) {

@@ -1493,13 +1493,13 @@ static int match_pairs_impl(const int8_t* desc, const int32_t* norms, const int3
                             const int32_t* n_kpts, int n_img, int m_pad, int d,
                             const int32_t* pairs, int P, int ratio_num, int ratio_den,
                             OutT* matches0, int32_t* dist1, int32_t* dist2, void* stream) {
-    SFMHIP_REQUIRE(desc && norms && keys && n_kpts && pairs && matches0,
-                   "sfmhip_match_pairs: null pointer");
     SFMHIP_REQUIRE(n_img > 0 && P >= 0, "sfmhip_match_pairs: bad counts");
     SFMHIP_REQUIRE(m_pad > 0 && m_pad % kJB == 0, "sfmhip_match_pairs: m_pad must be a positive multiple of 128");
     SFMHIP_REQUIRE(ratio_num > 0 && ratio_den > 0 && ratio_num <= 65535 && ratio_den <= 65535,
                    "sfmhip_match_pairs: ratio must be a positive fraction");
     if (P == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(desc && norms && keys && n_kpts && pairs && matches0,
+                   "sfmhip_match_pairs: null pointer");
     // 16x16x64 int8 MFMA tiles, 4 per wave, 4 waves per workgroup: 256 query rows per workgroup
     // (32x32 tiles, 8 tiles per wave and 8-wave workgroups measured slower: DESIGN.md K1)
     const int n_iblk = ceil_div(m_pad, 256);
@@ -1544,9 +1544,9 @@ extern "C" int sfmhip_match_pairs_i16(const int8_t* desc, const int32_t* norms, 
 }
 
 extern "C" int sfmhip_mutual_filter(int32_t* matches0, int32_t* matches1, int P, int m_pad, void* stream) {
-    SFMHIP_REQUIRE(matches0 && matches1, "sfmhip_mutual_filter: null pointer");
     SFMHIP_REQUIRE(P >= 0 && m_pad > 0, "sfmhip_mutual_filter: bad shape");
     if (P == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(matches0 && matches1, "sfmhip_mutual_filter: null pointer");
     const int64_t total = (int64_t)P * m_pad;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
     hipLaunchKernelGGL(mutual_kernel, dim3(grid), dim3(256), 0, as_stream(stream), matches0, matches1, P,
@@ -1556,9 +1556,9 @@ extern "C" int sfmhip_mutual_filter(int32_t* matches0, int32_t* matches1, int P,
 
 extern "C" int sfmhip_vq(const double* obs, int64_t n_obs, const double* code_book, int n_codes, int d,
                          int32_t* codes, double* dist, void* stream) {
-    SFMHIP_REQUIRE(obs && code_book && codes && dist, "sfmhip_vq: null pointer");
     SFMHIP_REQUIRE(n_obs >= 0 && n_codes > 0 && d > 0 && d <= 256, "sfmhip_vq: bad shape (d <= 256)");
     if (n_obs == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(obs && code_book && codes && dist, "sfmhip_vq: null pointer");
     // d = 128, <= 256 codewords (matching.py:27's 200-word codebook): the f16-split MFMA
     // filter + exact f64 decision (vq_f16s_kernel + vq_exact_kernel); other shapes: the
     // f64-MFMA GEMM-form kernel (d <= 128) or the f64 difference-form kernel.  The f32
@@ -1648,8 +1648,6 @@ static int match_exact_impl(const int8_t* desc, const int32_t* norms, const int3
                             int m_pad, int d, const int32_t* pairs, int P, int ratio_num, int ratio_den,
                             OutT* matches0, int32_t* dist1, int32_t* dist2, uint32_t* n_resolved,
                             void* stream) {
-    SFMHIP_REQUIRE(desc && norms && keys && desc_q && desc_f && resid_row && resid_img && n_kpts && pairs && matches0,
-                   "sfmhip_match_pairs_exact: null pointer");
     SFMHIP_REQUIRE(n_img > 0 && P >= 0, "sfmhip_match_pairs_exact: bad counts");
     SFMHIP_REQUIRE(m_pad > 0 && m_pad % kJB == 0, "sfmhip_match_pairs_exact: m_pad must be a positive multiple of 128");
     SFMHIP_REQUIRE(mode == 0 || mode == 1, "sfmhip_match_pairs_exact: mode must be 0 or 1");
@@ -1658,6 +1656,8 @@ static int match_exact_impl(const int8_t* desc, const int32_t* norms, const int3
     if constexpr (sizeof(OutT) == 2)
         SFMHIP_REQUIRE(m_pad <= 32767, "sfmhip_match_pairs_exact_i16: m_pad must be <= 32767 for an int16 graph");
     if (P == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(desc && norms && keys && desc_q && desc_f && resid_row && resid_img && n_kpts && pairs && matches0,
+                   "sfmhip_match_pairs_exact: null pointer");
     constexpr int IB = 256;   // match_kernel's query rows per workgroup (16x16 tiles, 4 per wave, 4 waves)
     const int n_iblk = ceil_div(m_pad, IB);
     const int64_t nwg64 = (int64_t)P * n_iblk;

@@ -1168,11 +1168,12 @@ __global__ __launch_bounds__(256) void tsdf_fuse_kernel(float* __restrict__ T, f
 static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, const float* depth, int F, int Hd,
                     int Wd, const float* poses, const float* Kf, const float* bmin, const float* bmax, float trunc,
                     void* stream, int64_t* stats, const float2* ext_table, int64_t* layer_stats = nullptr) {
-    SFMHIP_REQUIRE(T && Wt && depth && poses && Kf && bmin && bmax, "sfmhip_tsdf_integrate: null pointer");
+    // F = 0: nothing to fuse, the frame arrays may be null (an empty tensor's pointer)
     SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && F >= 0 && Hd > 0 && Wd > 0, "sfmhip_tsdf_integrate: bad shape");
     SFMHIP_REQUIRE(0 <= z0 && z0 <= z1 && z1 <= D, "sfmhip_tsdf_integrate: bad z range");
     SFMHIP_REQUIRE(trunc > 0.f, "sfmhip_tsdf_integrate: trunc must be > 0");
     if (F == 0 || z0 == z1) return SFMHIP_OK;
+    SFMHIP_REQUIRE(T && Wt && bmin && bmax && (F == 0 || (depth && poses && Kf)), "sfmhip_tsdf_integrate: null pointer");
     SFMHIP_REQUIRE((int64_t)Hd * Wd * 4 < (int64_t)INT_MAX && Wd < (1 << 22) && Hd < (1 << 22),
                    "sfmhip_tsdf_integrate: depth map too large (4*Hd*Wd must be < 2^31)");
     for (int a = 0; a < 3; ++a)
@@ -1395,17 +1396,17 @@ extern "C" int sfmhip_tsdf_integrate_tab(float* T, float* Wt, int D, int H, int 
                                          const float* depth, int F, int Hd, int Wd, const float* poses,
                                          const float* Kf, const float* bmin, const float* bmax, float trunc,
                                          const float* table, void* stream) {
-    SFMHIP_REQUIRE(table, "sfmhip_tsdf_integrate_tab: null pointer");
+    SFMHIP_REQUIRE(table || F == 0, "sfmhip_tsdf_integrate_tab: null pointer");
     return tsdf_run(T, Wt, D, H, W, z0, z1, depth, F, Hd, Wd, poses, Kf, bmin, bmax, trunc, stream, nullptr,
                     reinterpret_cast<const float2*>(table));
 }
 
 extern "C" int sfmhip_tsdf_block_table(const float* depth, int F, int Hd, int Wd, int f0, int f1, float* table,
                                        void* stream) {
-    SFMHIP_REQUIRE(depth && table, "sfmhip_tsdf_block_table: null pointer");
     SFMHIP_REQUIRE(F >= 0 && Hd > 0 && Wd > 0 && 0 <= f0 && f0 <= f1 && f1 <= F,
                    "sfmhip_tsdf_block_table: bad shape or frame range");
     if (f0 == f1) return SFMHIP_OK;
+    SFMHIP_REQUIRE(depth && table, "sfmhip_tsdf_block_table: null pointer");
     SFMHIP_REQUIRE((int64_t)Hd * Wd * 4 < (int64_t)INT_MAX, "sfmhip_tsdf_block_table: depth map too large");
     const int nbu = ceil_div(Wd, kCullBlock), nbv = ceil_div(Hd, kCullBlock), nf = f1 - f0;
     hipStream_t st = as_stream(stream);

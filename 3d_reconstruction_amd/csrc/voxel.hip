@@ -846,9 +846,9 @@ using namespace sfmhip;
 
 extern "C" int sfmhip_voxel_traversal_count(const float* rays, int64_t N, float bin, int32_t max_steps,
                                             int32_t* n_steps, void* stream) {
-    SFMHIP_REQUIRE(rays && n_steps, "sfmhip_voxel_traversal_count: null pointer");
     SFMHIP_REQUIRE(N >= 0 && max_steps > 0 && max_steps < INT_MAX, "sfmhip_voxel_traversal_count: bad args");
     if (N == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(rays && n_steps, "sfmhip_voxel_traversal_count: null pointer");
     hipLaunchKernelGGL(dda_count_kernel, dim3(ceil_div(N, 64)), dim3(64), 0, as_stream(stream), rays, N, bin,
                        max_steps, n_steps);   // one wave per workgroup: the waves spread over the CUs
     return check_launch("dda_count_kernel");
@@ -856,9 +856,9 @@ extern "C" int sfmhip_voxel_traversal_count(const float* rays, int64_t N, float 
 
 extern "C" int sfmhip_voxel_traversal(const float* rays, int64_t N, float bin, int32_t S, float* out,
                                       void* stream) {
-    SFMHIP_REQUIRE(rays && out, "sfmhip_voxel_traversal: null pointer");
     SFMHIP_REQUIRE(N >= 0 && S >= 1, "sfmhip_voxel_traversal: bad args");
     if (N == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(rays && out, "sfmhip_voxel_traversal: null pointer");
     // SFMHIP_DDA_DIRECT (tests): 1 per-lane row stores, 0 LDS-staged coalesced
     // chunks; default: direct below 64k rays (latency-bound), staged above.
     const int dk = knobs().dda_direct;
@@ -889,9 +889,9 @@ __global__ __launch_bounds__(256) void dda_rows_kernel(const float* __restrict__
 
 extern "C" int sfmhip_voxel_traversal_rows(const float* buf, int32_t cap, const int32_t* n_steps, int64_t N,
                                            int32_t S, float* out, void* stream) {
-    SFMHIP_REQUIRE(buf && n_steps && out, "sfmhip_voxel_traversal_rows: null pointer");
     SFMHIP_REQUIRE(N >= 0 && S >= 1 && S <= cap, "sfmhip_voxel_traversal_rows: bad args (1 <= S <= cap)");
     if (N == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(buf && n_steps && out, "sfmhip_voxel_traversal_rows: null pointer");
     const int64_t total = N * (int64_t)S * 3;
     hipLaunchKernelGGL(dda_rows_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(total, 256), 8192)), dim3(256), 0,
                        as_stream(stream), buf, cap, n_steps, N, S, out);
@@ -900,9 +900,9 @@ extern "C" int sfmhip_voxel_traversal_rows(const float* buf, int32_t cap, const 
 
 extern "C" int sfmhip_voxel_traversal_capped(const float* rays, int64_t N, float bin, int32_t cap, float* out,
                                              int32_t* n_steps, void* stream) {
-    SFMHIP_REQUIRE(rays && out && n_steps, "sfmhip_voxel_traversal_capped: null pointer");
     SFMHIP_REQUIRE(N >= 0 && cap >= 2, "sfmhip_voxel_traversal_capped: bad args (cap >= 2)");
     if (N == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(rays && out && n_steps, "sfmhip_voxel_traversal_capped: null pointer");
     hipLaunchKernelGGL(dda_fill_direct_kernel, dim3(ceil_div(N, 64)), dim3(64), 0, as_stream(stream), rays, N, bin,
                        cap, out, n_steps);
     return check_launch("dda_fill_direct_kernel");
@@ -917,10 +917,10 @@ static Bounds make_bounds(const float* bmin, const float* bmax) {
 extern "C" int sfmhip_grid_sample(const float* grid, int C, int D, int H, int W, const float* bmin,
                                   const float* bmax, int mask_mode, const float* pts, int64_t P, float* out,
                                   void* stream) {
-    SFMHIP_REQUIRE(grid && bmin && bmax && pts && out, "sfmhip_grid_sample: null pointer");
     SFMHIP_REQUIRE(C > 0 && D > 1 && H > 1 && W > 1 && P >= 0, "sfmhip_grid_sample: bad shape");
     SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_grid_sample: mask_mode must be 0 or 1");
     if (P == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(grid && bmin && bmax && pts && out, "sfmhip_grid_sample: null pointer");
     hipLaunchKernelGGL(grid_sample_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, as_stream(stream), grid, C, D,
                        H, W, make_bounds(bmin, bmax), mask_mode, pts, P, out);
     return check_launch("grid_sample_kernel");
@@ -929,10 +929,10 @@ extern "C" int sfmhip_grid_sample(const float* grid, int C, int D, int H, int W,
 extern "C" int sfmhip_nerf_forward(const float* grid, int D, int H, int W, const float* bmin, const float* bmax,
                                    int mask_mode, const float* pts, const float* dirs, int64_t P, float* color,
                                    float* sigma, void* stream) {
-    SFMHIP_REQUIRE(grid && bmin && bmax && pts && dirs && color && sigma, "sfmhip_nerf_forward: null pointer");
     SFMHIP_REQUIRE(D > 0 && H > 0 && W > 0 && P >= 0, "sfmhip_nerf_forward: bad shape");
     SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_nerf_forward: mask_mode must be 0 or 1");
     if (P == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(grid && bmin && bmax && pts && dirs && color && sigma, "sfmhip_nerf_forward: null pointer");
     const Bounds bb = make_bounds(bmin, bmax);
     hipLaunchKernelGGL(nerf_forward_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, as_stream(stream), grid, D, H, W, bb,
                        mask_mode, pts, dirs, P, color, sigma);
@@ -1050,11 +1050,11 @@ static void launch_render(const float* sdfp, dim3 grid, hipStream_t st, const fl
 static int render_run(const float* grid_vm, const float* sdfp, int D, int H, int W, const float* bmin,
                       const float* bmax, int mask_mode, const float* rays_o, const float* rays_d, const float* z,
                       int64_t B, int S, float* rgb, void* stream) {
-    SFMHIP_REQUIRE(grid_vm && bmin && bmax && rays_o && rays_d && z && rgb, "sfmhip_render_rays: null pointer");
     SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && B >= 0 && S >= 1, "sfmhip_render_rays: bad shape");
     SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_render_rays: mask_mode must be 0 or 1");
     SFMHIP_REQUIRE(B < ((int64_t)1 << 32), "sfmhip_render_rays: more than 2^32 rays");
     if (B == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(grid_vm && bmin && bmax && rays_o && rays_d && z && rgb, "sfmhip_render_rays: null pointer");
     hipStream_t st = as_stream(stream);
     const Bounds bb = make_bounds(bmin, bmax);
     // ray ordering (SFMHIP_RENDER_SORT=0 off, tests): Morton cells of 2^3 per axis holding each
@@ -1131,12 +1131,12 @@ extern "C" int sfmhip_render_train(const float* grid_vm, int D, int H, int W, co
                                    int mask_mode, const float* rays_o, const float* rays_d, const float* z,
                                    const float* gt, int64_t B, int S, float* rgb, float* sqerr, float* grad_vm,
                                    uint8_t* touched, void* stream) {
-    SFMHIP_REQUIRE(grid_vm && bmin && bmax && rays_o && rays_d && z && gt && rgb && sqerr && grad_vm,
-                   "sfmhip_render_train: null pointer");
     SFMHIP_REQUIRE(D > 1 && H > 1 && W > 1 && B >= 0 && S >= 1, "sfmhip_render_train: bad shape");
     SFMHIP_REQUIRE(S <= 64 * kTrainChunks, "sfmhip_render_train: S must be <= %d", 64 * kTrainChunks);
     SFMHIP_REQUIRE(mask_mode == 0 || mask_mode == 1, "sfmhip_render_train: mask_mode must be 0 or 1");
     if (B == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(grid_vm && bmin && bmax && rays_o && rays_d && z && gt && rgb && sqerr && grad_vm,
+                   "sfmhip_render_train: null pointer");
     const float gscale = (float)(2.0 / (3.0 * (double)B));  // mse_loss mean over B x 3
     hipLaunchKernelGGL(render_train_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, as_stream(stream), grid_vm, D, H,
                        W, make_bounds(bmin, bmax), mask_mode, rays_o, rays_d, z, gt, B, S, gscale, rgb, sqerr,
@@ -1147,10 +1147,10 @@ extern "C" int sfmhip_render_train(const float* grid_vm, int D, int H, int W, co
 extern "C" int sfmhip_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                                 double lr, double beta1, double beta2, double eps, int64_t step, int zero_grad,
                                 void* stream) {
-    SFMHIP_REQUIRE(param && grad && exp_avg && exp_avg_sq, "sfmhip_adam_step: null pointer");
     SFMHIP_REQUIRE(n >= 0 && n % 4 == 0, "sfmhip_adam_step: n must be a multiple of 4");
     SFMHIP_REQUIRE(step >= 1, "sfmhip_adam_step: step counts from 1");
     if (n == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(param && grad && exp_avg && exp_avg_sq, "sfmhip_adam_step: null pointer");
     // torch computes these in Python floats (double) and casts to the tensor dtype
     const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, s2 = (float)(1.0 - beta2);
     const float bc2s = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
@@ -1166,11 +1166,11 @@ extern "C" int sfmhip_adam_step(float* param, float* grad, float* exp_avg, float
 extern "C" int sfmhip_adam_step_flagged(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                                         double lr, double beta1, double beta2, double eps, int64_t step,
                                         int zero_grad, uint8_t* flags, int flag_shift, void* stream) {
-    SFMHIP_REQUIRE(param && grad && exp_avg && exp_avg_sq && flags, "sfmhip_adam_step_flagged: null pointer");
     SFMHIP_REQUIRE(n >= 0 && n % 4 == 0, "sfmhip_adam_step_flagged: n must be a multiple of 4");
     SFMHIP_REQUIRE(flag_shift >= 2 && flag_shift <= 30, "sfmhip_adam_step_flagged: flag_shift must be in [2, 30]");
     SFMHIP_REQUIRE(step >= 1, "sfmhip_adam_step_flagged: step counts from 1");
     if (n == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(param && grad && exp_avg && exp_avg_sq && flags, "sfmhip_adam_step_flagged: null pointer");
     const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, s2 = (float)(1.0 - beta2);
     const float bc2s = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
     const float stp = (float)(-lr / (1.0 - std::pow(beta1, (double)step)));
@@ -1194,9 +1194,9 @@ extern "C" int sfmhip_adam_step_flagged(float* param, float* grad, float* exp_av
 
 extern "C" int sfmhip_ray_aabb(const float* rays_o, const float* rays_d, int64_t B, const float* bmin,
                                const float* bmax, float* t_near, float* t_far, uint8_t* valid, void* stream) {
-    SFMHIP_REQUIRE(rays_o && rays_d && bmin && bmax && t_near && t_far && valid, "sfmhip_ray_aabb: null pointer");
     SFMHIP_REQUIRE(B >= 0, "sfmhip_ray_aabb: B < 0");
     if (B == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(rays_o && rays_d && bmin && bmax && t_near && t_far && valid, "sfmhip_ray_aabb: null pointer");
     hipLaunchKernelGGL(ray_aabb_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, as_stream(stream), rays_o, rays_d, B,
                        make_bounds(bmin, bmax), t_near, t_far, valid);
     return check_launch("ray_aabb_kernel");
@@ -1204,9 +1204,9 @@ extern "C" int sfmhip_ray_aabb(const float* rays_o, const float* rays_d, int64_t
 
 extern "C" int sfmhip_stratified_samples(const float* t_near, const float* t_far, const float* t_rand, int64_t B,
                                          int S, int perturb, float* z, void* stream) {
-    SFMHIP_REQUIRE(t_near && t_far && z && (t_rand || !perturb), "sfmhip_stratified_samples: null pointer");
     SFMHIP_REQUIRE(B >= 0 && S >= 2, "sfmhip_stratified_samples: bad shape");
     if (B == 0) return SFMHIP_OK;
+    SFMHIP_REQUIRE(t_near && t_far && z && (t_rand || !perturb), "sfmhip_stratified_samples: null pointer");
     hipLaunchKernelGGL(stratified_kernel, dim3(ceil_div(B * S, 256)), dim3(256), 0, as_stream(stream), t_near, t_far,
                        t_rand, B, S, perturb, z);
     return check_launch("stratified_kernel");

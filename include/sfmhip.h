@@ -13,6 +13,9 @@
  *   - Return value: 0 on success, a negative SFMHIP_E_* code on failure; the
  *     message for the calling thread is in sfmhip_last_error().
  *   - Row-major, densely packed arrays unless a stride is given.
+ *   - An empty call (zero observations / pairs / rays / points / frames) is a no-op
+ *     returning 0, and the arrays of that count may then be null (an empty torch
+ *     tensor's data_ptr() is 0); shapes and counts are still validated first.
  *
  * Each entry point cites the reference interface it replaces (file:line in
  * /root/reference).  See INTEGRATION.md for the ctypes binding.
@@ -307,7 +310,8 @@ int sfmhip_render_rays_sdf(const float* grid_vm, const float* sdf_plane, int D, 
  * trunc = truncation distance mu (world units).  The frames of one integration
  * step (the call, in steps of at most 512 frames) are fused order-free: per
  * voxel S = sum rint(tsdf * 2^21) and n updates, then W' = W + n,
- * T' = f32((f64 T * W + S 2^-21) / (W + n))  (oracle/voxel.py tsdf_integrate).  */
+ * T' = f32((f64 T * W + S 2^-21) / (W + n))  (oracle/voxel.py tsdf_integrate).
+ * F = 0 or z0 = z1: a no-op (with F = 0 the frame arrays may be null).        */
 int sfmhip_tsdf_integrate(float* T, float* Wt, int D, int H, int W, int z0, int z1,
                           const float* depth, int F, int Hd, int Wd,
                           const float* poses, const float* Kf,
