@@ -17,6 +17,7 @@
 // the iteration reduced across the workgroup and held in LDS; thread 0 does the
 // 6x6 and 2x2 algebra.
 #include "common.h"
+#include <mutex>
 #include "geom_dev.h"
 #include <climits>
 #include <cstdlib>
@@ -79,6 +80,7 @@ __device__ unsigned long long g_ba_prof[4096 * kProfPhases];
 // records of all 256 C3 pairs 243 -> 218 MB)
 constexpr int kRec = 26;
 constexpr int kFX = 20, kFS = 23;   // X_new, scale_inv
+constexpr int kBaLdsObs = 768;       // observations per pair whose records stay in LDS (156 KB)
 
 // sum of K doubles over the workgroup (NW waves); every thread receives the totals in out[]
 template <int NW, int K>
@@ -209,26 +211,52 @@ struct BaState {   // LDS: the iteration's scalars, written by thread 0 or by bl
 // observation, field-major within the pair (field f of record i at f * n + i: a
 // wave's load of one field is 64 consecutive doubles; AoS records measured slower,
 // profiles/r3/ba_variants_r3m.txt).  Passes copy the fields they use into registers.
-struct Recs {
+// The records of the first L observations live in LDS instead (field f of record i < L at
+// lds[f L + i]); i = tid + k NT with L a multiple of the wave size keeps the choice uniform per
+// wave.  kLdsF < kRec would keep only the pass fields there (more observations per byte): it
+// spilled 76 VGPRs instead of 36 and measured slower (1.26 vs 1.15 ms).
+constexpr int kLdsF = kRec;
+template <bool USE_LDS>
+struct RecsT {
     double* base;
     int n;
-    __device__ __forceinline__ double* at(int i, int f) const { return base + (size_t)f * n + i; }
+    __attribute__((address_space(3))) double* lds;   // dynamic LDS, L * kLdsF doubles (L = 0: none)
+    int L;
+    __device__ __forceinline__ double* at(int i, int f) const {   // (scratch fields only)
+        return base + (size_t)f * n + i;
+    }
     template <int LO, int HI>
     __device__ __forceinline__ void load(int i, double* r) const {
+        constexpr int M = HI < kLdsF ? HI : kLdsF, G0 = LO > kLdsF ? LO : kLdsF;
+        if (USE_LDS && LO < kLdsF && i < L) {
 #pragma unroll
-        for (int f = LO; f < HI; ++f) r[f] = *at(i, f);
+            for (int f = LO; f < M; ++f) r[f] = lds[f * L + i];
+#pragma unroll
+            for (int f = G0; f < HI; ++f) r[f] = base[(size_t)f * n + i];
+        } else {
+#pragma unroll
+            for (int f = LO; f < HI; ++f) r[f] = base[(size_t)f * n + i];
+        }
     }
     template <int LO, int HI>
     __device__ __forceinline__ void store(int i, const double* r) const {
+        constexpr int M = HI < kLdsF ? HI : kLdsF, G0 = LO > kLdsF ? LO : kLdsF;
+        if (USE_LDS && LO < kLdsF && i < L) {
 #pragma unroll
-        for (int f = LO; f < HI; ++f) *at(i, f) = r[f];
+            for (int f = LO; f < M; ++f) lds[f * L + i] = r[f];
+#pragma unroll
+            for (int f = G0; f < HI; ++f) base[(size_t)f * n + i] = r[f];
+        } else {
+#pragma unroll
+            for (int f = LO; f < HI; ++f) base[(size_t)f * n + i] = r[f];
+        }
     }
 };
 
 // for i = tid, tid + NT, ... < n: body(i, r) with r[LO, HI) = record i, the next
 // record's loads issued before the current one's arithmetic (one record ahead)
-template <int NT, int LO, int HI, typename F>
-__device__ __forceinline__ void stream_recs(const Recs& rec, int n, F&& body) {
+template <int NT, int LO, int HI, typename R, typename F>
+__device__ __forceinline__ void stream_recs(const R& rec, int n, F&& body) {
     double nx[kRec];
     int i = threadIdx.x;
     if (i < n) rec.template load<LO, HI>(i, nx);
@@ -262,9 +290,10 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
                                                     double xtol, double gtol, int max_nfev_arg,
                                                     double* __restrict__ scratch, double* __restrict__ cost_out,
                                                     int32_t* __restrict__ nfev_out, int32_t* __restrict__ njev_out,
-                                                    int32_t* __restrict__ status_out) {
+                                                    int32_t* __restrict__ status_out, int lds_obs) {
     constexpr int NW = NT / 64;
     __shared__ BaState<NW> S;
+    extern __shared__ __attribute__((aligned(16))) double lrec[];   // lds_obs * kLdsF (not FUSED)
     const int p = blockIdx.x, tid = threadIdx.x;
     const int64_t o0 = off[p], o1 = off[p + 1];
     if (!(0 <= o0 && o0 <= o1 && o1 <= n_obs && o1 - o0 <= INT_MAX)) {   // malformed offsets: touch nothing
@@ -276,7 +305,10 @@ __global__ __launch_bounds__(NT) void ba_trf_kernel(double* __restrict__ cam_io,
     double* Xp = X + 3 * o0;
     const double* pts = pts2d + 2 * o0;
     // FUSED: two record sets (the current one and the trial point's), scratch holds 2 n_obs records
-    const Recs recs[2] = {{scratch + (size_t)o0 * kRec, n}, {scratch + (size_t)(n_obs + o0) * kRec, n}};
+    const int L = FUSED ? 0 : min(lds_obs, n);
+    using Recs = RecsT<!FUSED>;
+    auto* lr = (__attribute__((address_space(3))) double*)lrec;
+    const Recs recs[2] = {{scratch + (size_t)o0 * kRec, n, lr, L}, {scratch + (size_t)(n_obs + o0) * kRec, n, lr, 0}};
     int cur = 0;   // every thread flips it at the same point (after a barrier): uniform
     // the pass view of observation i: r[0..17] J, r[18..19] f; the records hold the point block
     // of J already scaled, Pp = J_p d (fields 6-8, 15-17), so the passes read 20 fields
@@ -835,12 +867,35 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
     }
     // one 512-thread workgroup per pair, field-major records (256 threads, AoS records and the
     // recompute form measured slower: profiles/r3/ba_variants_r3m.txt, DESIGN.md K3'')
+    // the first 768 observations' records of each pair in LDS (156 KB) when every pair has a CU
+    // of its own (at most one workgroup per CU is resident anyway); else none, so that two
+    // workgroups still fit a CU
+    int ncu = 256, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    (void)hipGetLastError();
+    const int lds_obs = (!fused && n_pairs <= ncu && knobs().ab != 7) ? kBaLdsObs : 0;
+    const size_t lds_bytes = (size_t)lds_obs * kLdsF * sizeof(double);
+    if (lds_bytes > 0) {
+        static std::once_flag attr_once;
+        static hipError_t attr_rc = hipSuccess;
+        std::call_once(attr_once, [&] {
+            attr_rc = hipFuncSetAttribute(reinterpret_cast<const void*>(&ba_trf_kernel<512>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsF * kBaLdsObs * 8));
+        });
+        if (attr_rc != hipSuccess) {
+            scratch_free(scratch, st);
+            set_error("sfmhip_ba_solve: LDS attribute: %s", hipGetErrorString(attr_rc));
+            return SFMHIP_E_HIP;
+        }
+    }
     if (fused)
         hipLaunchKernelGGL((ba_trf_kernel<512, true>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off, n_obs,
-                           ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+                           ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status, 0);
     else
-        hipLaunchKernelGGL((ba_trf_kernel<512>), dim3(n_pairs), dim3(512), 0, st, cam, K, X, pts2d, pair_off, n_obs, ftol,
-                           xtol, gtol, max_nfev, scratch, cost, nfev, njev, status);
+        hipLaunchKernelGGL((ba_trf_kernel<512>), dim3(n_pairs), dim3(512), lds_bytes, st, cam, K, X, pts2d, pair_off,
+                           n_obs, ftol, xtol, gtol, max_nfev, scratch, cost, nfev, njev, status, lds_obs);
     const int rc = check_launch("ba_trf_kernel");
     scratch_free(scratch, st);
     return rc;
