@@ -867,15 +867,9 @@ extern "C" int sfmhip_ba_solve(double* cam, const double* K, double* X, const do
     }
     // one 512-thread workgroup per pair, field-major records (256 threads, AoS records and the
     // recompute form measured slower: profiles/r3/ba_variants_r3m.txt, DESIGN.md K3'')
-    // the first 768 observations' records of each pair in LDS (156 KB) when every pair has a CU
-    // of its own (at most one workgroup per CU is resident anyway); else none, so that two
-    // workgroups still fit a CU
-    int ncu = 256, dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-        ncu = 256;
-    (void)hipGetLastError();
-    const int lds_obs = (!fused && n_pairs <= ncu && knobs().ab != 7) ? kBaLdsObs : 0;
+    // the first 768 observations' records of each pair in LDS (156 KB): the kernel's 256 VGPRs per
+    // lane already hold a CU to one workgroup, so the LDS costs no residency
+    const int lds_obs = (!fused && knobs().ab != 7) ? kBaLdsObs : 0;
     const size_t lds_bytes = (size_t)lds_obs * kLdsF * sizeof(double);
     if (lds_bytes > 0) {
         static std::once_flag attr_once;
