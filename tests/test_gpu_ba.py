@@ -104,6 +104,34 @@ def test_ba_fused_trial_jacobian_form_bit_identical(sfm, gpu, knob, far):
         assert torch.equal(res[0][2][key], res[1][2][key]), key
 
 
+@pytest.mark.parametrize("far", [0, 1])
+def test_ba_lds_records_bit_identical(sfm, gpu, knob, far):
+    """The records of each pair's first 768 observations kept in LDS (the default) against all
+    records in scratch (SFMHIP_AB=7): the same bits on pairs wholly in LDS (<= 768 observations),
+    split across LDS and scratch (769, 1500, 2048), an empty pair, and a batch of 300 pairs
+    (more workgroups than CUs: the launch runs in rounds)."""
+    sizes = [300, 0, 768, 769, 37, 1500, 2048]
+    cams, Ks, Xs, ps = _ragged_problem(sizes, seed=70 + far, far=far)
+    out = []
+    for ab in (0, 7):
+        knob("AB", ab)
+        out.append(_solve_gpu(sfm, gpu, cams, Ks, Xs, ps))
+    (c0, x0, r0, _), (c1, x1, r1, _) = out
+    assert np.array_equal(c0, c1) and np.array_equal(x0, x1)
+    for key in ("cost", "nfev", "njev", "status"):
+        assert np.array_equal(r0[key], r1[key]), key
+    sizes = [int(v) for v in np.random.default_rng(far).integers(20, 120, 300)]
+    cams, Ks, Xs, ps = _ragged_problem(sizes, seed=80 + far, far=far)
+    out = []
+    for ab in (0, 7):
+        knob("AB", ab)
+        out.append(_solve_gpu(sfm, gpu, cams, Ks, Xs, ps))
+    (c0, x0, r0, _), (c1, x1, r1, _) = out
+    assert np.array_equal(c0, c1) and np.array_equal(x0, x1)
+    for key in ("cost", "nfev", "njev", "status"):
+        assert np.array_equal(r0[key], r1[key]), key
+
+
 def test_least_squares_ba_drop_in_vs_scipy(sfm, gpu):
     """sfm.py:38 with the on-device solve: scipy's nfev and solution."""
     cams, Ks, Xs, ps = _ragged_problem([500], seed=50, far=True)
