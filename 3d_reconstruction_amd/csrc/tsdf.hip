@@ -691,13 +691,12 @@ __global__ __launch_bounds__(kPreThreads, 4) void tsdf_prepass_kernel(
             bi = __builtin_amdgcn_readfirstlane(bi);
             if (bi >= nbt) break;
             const int brick = b0 + bi;
-            const bool bok = true;
             const int qx = brick % nqx, qy = (brick / nqx) % nqy, qz = brick / (nqx * nqy);
             const int tx = qx * 4 + (lane & 3), ty = qy * 4 + ((lane >> 2) & 3), tz = qz * 4 + (lane >> 4);
-            const bool tile_ok = bok && tx < ntx && ty < nty && tz < ntz;
+            const bool tile_ok = tx < ntx && ty < nty && tz < ntz;
             const int64_t tile = ((int64_t)tz * nty + ty) * ntx + tx;
             int bd = 0;
-            if (bok && ok) {
+            if (ok) {
                 const int xa = qx * 4 * kTsdfTX, xb = min(W, (qx * 4 + 4) * kTsdfTX) - 1;
                 const int ya = qy * 4 * kTsdfTY, yb = min(H, (qy * 4 + 4) * kTsdfTY) - 1;
                 const int za = z0 + qz * 4 * kTsdfTZ, zb = min(z1, z0 + min(ntz, qz * 4 + 4) * kTsdfTZ) - 1;
