@@ -589,7 +589,8 @@ __device__ __forceinline__ int brick_decide_wave(const CullCam& cc, const CullGe
 __global__ __launch_bounds__(kPreThreads, 4) void tsdf_prepass_kernel(
     const float* __restrict__ depth, int F, int Hd, int Wd, int nbu, int nbv, const int4* __restrict__ range,
     float2* bmm, int H, int W, int z0, int z1, const CullCam* __restrict__ cams, CullGeom G, float trunc,
-    unsigned* tickets, unsigned* fdone, unsigned char* __restrict__ dec, unsigned* gaveup) {
+    unsigned* tickets, unsigned* fdone, unsigned char* __restrict__ dec, unsigned* gaveup, int lag,
+    unsigned spin_max) {
     __shared__ int s_task, s_ok, s_next;
     __shared__ int plist[kPreWaves][64];
     __shared__ unsigned char sub[kPreWaves][64][kCullSub];
@@ -602,7 +603,7 @@ __global__ __launch_bounds__(kPreThreads, 4) void tsdf_prepass_kernel(
     const int nqx = (ntx + 3) >> 2, nqy = (nty + 3) >> 2, nqz = (ntz + 3) >> 2;
     const int nbricks = nqx * nqy * nqz;
     const int64_t ntiles = (int64_t)ntx * nty * ntz;
-    const int rows = kPreRows, bpw = kPreBpw, lag = kPreLag;
+    const int rows = kPreRows, bpw = kPreBpw;
     const int ns = (nbv + rows - 1) / rows;
     const int nc = (nbricks + kPreWaves * bpw - 1) / (kPreWaves * bpw);
     const int nfs = F > shard ? (F - shard + kPreShards - 1) / kPreShards : 0;   // this shard's frames
@@ -667,7 +668,7 @@ __global__ __launch_bounds__(kPreThreads, 4) void tsdf_prepass_kernel(
             int ok = 1;
             unsigned spins = 0;
             while (__hip_atomic_load((gu32*)(fdone + f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ns) {
-                if (++spins > kPreSpinMax) { ok = 0; break; }
+                if (++spins > spin_max) { ok = 0; break; }
                 __builtin_amdgcn_s_sleep(4);
             }
             if (!ok) atomicAdd(gaveup, 1u);
@@ -1199,14 +1200,17 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
     // split): four projected frames per fusion stage and no brick / refinement pre-passes (their
     // fixed cost outweighs the fusion work they save there); SFMHIP_AB=1 (2) keeps the whole-grid
     // form with the separate (fused) pre-passes
-    const bool deep = rounds < kTsdfDeepRounds && kn.ab != 1 && kn.ab != 3;
+    const bool deep = rounds < kTsdfDeepRounds && kn.ab != 1 && kn.ab != 3 && kn.ab != 31;
     const bool refine = !latency_mode && !deep;
     const bool brick = !latency_mode && !deep;
     const bool vox_test = !latency_mode;
     // SFMHIP_AB=3: the whole-grid pre-passes as one persistent launch (tsdf_prepass_kernel) instead
     // of the separate block / brick / cull / refine launches: bit-identical grids, measured 2 %
     // slower on C5 (1.75 vs 1.71 ms: profiles/r6/tsdf_fused_prepass_r6.txt), so not the default
-    const bool fusedpre = brick && !ext_table && !stats && Wd % 4 == 0 && kn.ab == 3;
+    const bool fusedpre = brick && !ext_table && !stats && Wd % 4 == 0 && (kn.ab == 3 || kn.ab == 31);
+    // SFMHIP_AB=31 (tests): the fused pre-pass with no lag and no patience, so culling tasks give up
+    // on frames whose table is not complete yet: the undecided fallback must give the same grid
+    const bool pre_stress = kn.ab == 31;
     GridBox gb;
     CullGeom cg;
     {
@@ -1293,7 +1297,8 @@ static int tsdf_run(float* T, float* Wt, int D, int H, int W, int z0, int z1, co
         const float2* tab = ext_table ? ext_table + (size_t)f0 * nbv * nbu : cbmm;
         if (fusedpre) {
             hipLaunchKernelGGL(tsdf_prepass_kernel, dim3(pre_grid), dim3(kPreThreads), 0, st, dp, nf, Hd, Wd, nbu, nbv,
-                               crange, cbmm, H, W, z0, z1, ccam, cg, trunc, tickets, fdone, pdec, cnt + 1);
+                               crange, cbmm, H, W, z0, z1, ccam, cg, trunc, tickets, fdone, pdec, cnt + 1,
+                               pre_stress ? 0 : kPreLag, pre_stress ? 0u : kPreSpinMax);
             hipLaunchKernelGGL(tsdf_pack_kernel, dim3((unsigned)ceil_div(ntiles * nw, (int64_t)256)), dim3(256), 0, st,
                                nf, ntiles, nw, pdec, cmask, cfree, tcost);
         } else if (!ext_table) {

@@ -238,16 +238,18 @@ def _tsdf_case(R=48, F=12, Hd=96, Wd=128, focal=110.0):
 
 # "auto": the library's choice; "0" / "1": whole-grid / latency mode; "w1" / "w3": the whole-grid
 # form even on thin grids, with separate block / brick / cull / refine launches (SFMHIP_AB=1) or
-# with those pre-passes fused in one persistent launch (SFMHIP_AB=3)
-LAT_MODES = ["auto", "0", "1", "w1", "w3"]
+# with those pre-passes fused in one persistent launch (SFMHIP_AB=3); "w31": the fused form with no
+# lag and no patience (SFMHIP_AB=31), so culling tasks give up on incomplete tables and leave those
+# frames undecided (the fallback: every pair projected, fused in full)
+LAT_MODES = ["auto", "0", "1", "w1", "w3", "w31"]
 
 
 def _set_lat(knob, lat):
     if lat in ("0", "1"):
         knob("TSDF_LATENCY", lat)
-    elif lat in ("w1", "w3"):
+    elif lat.startswith("w"):
         knob("TSDF_LATENCY", 0)
-        knob("AB", lat[1])
+        knob("AB", lat[1:])
 
 
 def _close_to_seq(Tg, Wg, Ts, Ws):
@@ -311,10 +313,13 @@ def test_tsdf_edge_cases_bitexact(sfm, gpu, knob, Wd, lat):
     assert (Wr > W0).mean() > 0.1
 
 
-def test_tsdf_multi_step_bitexact(sfm, gpu):
+@pytest.mark.parametrize("lat", ["auto", "w1", "w3", "w31"])
+def test_tsdf_multi_step_bitexact(sfm, gpu, knob, lat):
     """More than 512 frames: the call fuses them in consecutive 512-frame integration
     steps (each finished before the next), exactly as the oracle defines it; a split
-    call (frames [0, 300) then [300, F)) is a different (also exact) sequence of steps."""
+    call (frames [0, 300) then [300, F)) is a different (also exact) sequence of steps.
+    w3: the fused pre-pass, its tickets and frame counters re-zeroed for every step."""
+    _set_lat(knob, lat)
     R, F, Hd, Wd = 20, 530, 24, 32
     depth, poses, K = syn.tsdf_scene(F, Hd, Wd, focal=30.0, seed=13)
     depth, poses, K = depth.numpy(), poses.numpy(), K.numpy()
