@@ -533,7 +533,7 @@ __global__ __launch_bounds__(256) void tsdf_refine_kernel(int H, int W, int z0, 
 // the compiler restructured the loop per lane and the barriers deadlocked (first build, r6).
 constexpr int kPreThreads = 512, kPreWaves = kPreThreads / 64;
 constexpr int kPreRows = 4;            // table block rows per stream task
-constexpr int kPreHalf = 8;            // depth rows per load batch of a stream task
+constexpr int kPreHalf = 16;           // depth rows per load batch of a stream task
 constexpr int kPreBpw = 4;             // bricks per culling task per wave (dealt to the waves one by one)
 constexpr int kPreLag = 4;             // shard frames between a frame's stream and culling tasks
 constexpr int kPreShards = kNumXcd;
