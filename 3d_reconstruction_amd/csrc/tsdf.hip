@@ -857,8 +857,11 @@ static SlotMap make_slot_map(int ntx, int nty, int ntz) {
     m.ntx = ntx;
     m.nty = nty;
     m.ntz = ntz;
-    // 3 x 2 x 8 tiles (24 x 16 x 64 voxels): sweeps in tools/bench_tsdf_variants.py (round 2)
-    m.sbx = 3;
+    // 1 x 2 x 8 tiles (8 x 16 x 64 voxels): round-6 sweep of the shipped fusion over 23 shapes
+    // (profiles/r6/tsdf_superbrick_sweep_r6.txt): C5 call 1.68 vs 1.73 ms for round 2's 3 x 2 x 8,
+    // the N = 8 slabs 3-4 % faster; the small super-bricks deal the costly surface columns over the
+    // XCDs more evenly
+    m.sbx = 1;
     m.sby = 2;
     m.sbz = std::min(8, ntz);
     m.nsx = ceil_div(ntx, m.sbx);
